@@ -1,0 +1,19 @@
+// gemm.h -- internal launchers shared across translation units.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+
+enum { EPI_STORE = 0, EPI_SUMSQ = 1 };
+
+// acc = A(M x K) B(N x K)^T; see gemm.hip.  For EPI_SUMSQ, C is the partial
+// buffer (ceil(M/64) x ldc) and row tile t writes row t.
+hipError_t launch_gemm_nt(hipStream_t s, int epi, int M, int N, int K, const double *A,
+                          int64_t lda, const double *B, int64_t ldb, double *C, int64_t ldc,
+                          double alpha, double beta, int tri_a, int lower_c, int batch,
+                          int64_t sA, int64_t sB, int64_t sC);
+
+hipError_t launch_trsm_lower_ex(hipStream_t s, int n, int nrhs, const double *L, int64_t ldl,
+                                double *X, int64_t ldx, int trans, int rhs_lower,
+                                double *Linv_blocks);
+
+inline int gemm_row_tiles(int M) { return (M + 63) / 64; }

@@ -1,0 +1,588 @@
+// gp.hip -- exact GP and FITC sparse GP on the device.
+//
+// Exact GP (MultiOutputExactGP.fit -> ExactGP.fit, exact_gp.py:118-204, 476-499):
+// the n_out outputs share one kernel and one X, so a single Gram, a single
+// Cholesky (with the exact_gp.py:163-175 jitter ladder) and a single
+// W = L^-1 serve every output.  alpha = cho_solve(L, y_c) for all
+// outputs at once (n x n_out right-hand sides).
+//
+// Posterior (ExactGP.predict, exact_gp.py:213-268):
+//   K*   = k(X*, X)                          (gram kernel, P x n)
+//   mean = K* alpha * y_std + y_mean          (NT GEMM, alpha^T as A)
+//   var  = max(sigma2 - colsum((W K*^T)^2), 1e-10) * y_std^2
+// where the sum of squares is fused into the GEMM epilogue (gemm.hip).
+#include "internal.h"
+#include "gemm.h"
+#include <cmath>
+#include <vector>
+
+struct GpCore {
+  int kind = 0, n = 0, d = 0, n_out = 0;
+  double sigma2 = 1.0, iso_scale = 0.0;
+  DevBuf ls, Xs, Xn;   // scaled training rows, squared norms
+  DevBuf W;            // n x n, L^-1 (lower)
+  DevBuf alphaT;       // n_out x n
+  DevBuf ymean, ystd;  // n_out
+  std::vector<double> h_ymean, h_ystd;
+};
+
+struct gpmpc_gp {
+  GpCore core;
+  DevBuf L;  // n x n lower Cholesky factor
+  double noise = 1e-4;
+};
+
+struct gpmpc_fitc {
+  GpCore core;  // core.Xs = scaled inducing rows (m), W = L_uu^-1, alphaT, ...
+  DevBuf WB;    // m x m, L_B^-1
+  int m = 0;
+};
+
+// ---------------------------------------------------------------------------
+__global__ void k_eye(int n, double *A) {
+  int j = blockIdx.x * blockDim.x + threadIdx.x, i = blockIdx.y;
+  if (j < n) A[(int64_t)i * n + j] = (i == j) ? 1.0 : 0.0;
+}
+
+// finish the posterior: var (P x n_out), mean (P x n_out) from partials
+__global__ void k_post_finish(int P, int n_out, int nrt, const double *__restrict__ part,
+                              int64_t ldp, const double *__restrict__ meanT, int64_t ldm,
+                              const double *__restrict__ ymean, const double *__restrict__ ystd,
+                              double sigma2, double *__restrict__ mean, double *__restrict__ var) {
+  int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= P) return;
+  double ss = 0.0;
+  for (int t = 0; t < nrt; ++t) ss += part[(int64_t)t * ldp + j];
+  double lat = sigma2 - ss;
+  lat = lat > 1e-10 ? lat : 1e-10;
+  for (int c = 0; c < n_out; ++c) {
+    if (mean) mean[(int64_t)j * n_out + c] = meanT[(int64_t)c * ldm + j] * ystd[c] + ymean[c];
+    if (var) var[(int64_t)j * n_out + c] = lat * ystd[c] * ystd[c];
+  }
+}
+
+// FITC: part2 holds colsums for v = Luu^-1 Ku* (rows tiles) and w = LB^-1 v.
+__global__ void k_fitc_finish(int P, int n_out, int nrt, const double *__restrict__ pv,
+                              const double *__restrict__ pw, int64_t ldp,
+                              const double *__restrict__ meanT, int64_t ldm,
+                              const double *__restrict__ ymean, const double *__restrict__ ystd,
+                              double sigma2, double *__restrict__ mean, double *__restrict__ var) {
+  int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= P) return;
+  double sv = 0.0, sw = 0.0;
+  for (int t = 0; t < nrt; ++t) {
+    sv += pv[(int64_t)t * ldp + j];
+    sw += pw[(int64_t)t * ldp + j];
+  }
+  double lat = sigma2 - sv + sw;
+  lat = lat > 1e-10 ? lat : 1e-10;
+  for (int c = 0; c < n_out; ++c) {
+    mean[(int64_t)j * n_out + c] = meanT[(int64_t)c * ldm + j] * ystd[c] + ymean[c];
+    var[(int64_t)j * n_out + c] = lat * ystd[c] * ystd[c];
+  }
+}
+
+// column scaling: A[i][j] *= s[j]
+__global__ void k_scale_cols(int rows, int cols, double *A, int64_t lda, const double *s) {
+  int j = blockIdx.x * blockDim.x + threadIdx.x, i = blockIdx.y;
+  if (j < cols) A[(int64_t)i * lda + j] *= s[j];
+}
+
+// ---------------------------------------------------------------------------
+// small device reductions (all GP arithmetic stays on the device)
+__device__ double block_sum(double v, double *red) {
+  const int tid = threadIdx.x;
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  __syncthreads();
+  if ((tid & 63) == 0) red[tid >> 6] = v;
+  __syncthreads();
+  double t = 0.0;
+  for (int w = 0; w < (int)(blockDim.x >> 6); ++w) t += red[w];
+  return t;
+}
+
+// exact_gp.py:141-150: per output column, mean / population std (std < 1e-10 -> 1)
+__global__ __launch_bounds__(256) void k_normalise(int n, int n_out, const double *Y, double *yn,
+                                                   double *ymean, double *ystd) {
+  __shared__ double red[4];
+  const int c = blockIdx.x;
+  double s = 0.0;
+  for (int i = threadIdx.x; i < n; i += 256) s += Y[(int64_t)i * n_out + c];
+  const double m = block_sum(s, red) / n;
+  double q = 0.0;
+  for (int i = threadIdx.x; i < n; i += 256) {
+    double t = Y[(int64_t)i * n_out + c] - m;
+    q += t * t;
+  }
+  double sd = sqrt(block_sum(q, red) / n);
+  if (sd < 1e-10) sd = 1.0;
+  for (int i = threadIdx.x; i < n; i += 256) yn[(int64_t)i * n_out + c] = (Y[(int64_t)i * n_out + c] - m) / sd;
+  if (threadIdx.x == 0) { ymean[c] = m; ystd[c] = sd; }
+}
+
+// exact_gp.py:186-204: lml_c = -1/2 y_c.alpha_c - sum log L_ii - n/2 log 2 pi; also alpha^T
+__global__ __launch_bounds__(256) void k_lml_exact(int n, int n_out, const double *L,
+                                                   const double *yn, const double *alpha,
+                                                   double *alphaT, double *lml) {
+  __shared__ double red[4];
+  const int c = blockIdx.x;
+  double ld = 0.0, fit = 0.0;
+  for (int i = threadIdx.x; i < n; i += 256) {
+    ld += log(L[(int64_t)i * n + i]);
+    const double a = alpha[(int64_t)i * n_out + c];
+    fit += yn[(int64_t)i * n_out + c] * a;
+    alphaT[(int64_t)c * n + i] = a;
+  }
+  ld = block_sum(ld, red);
+  fit = block_sum(fit, red);
+  if (threadIdx.x == 0) lml[c] = -0.5 * fit - ld - 0.5 * n * log(2.0 * M_PI);
+}
+
+// FITC Lambda (sparse_gp.py:193-199): lam_j = max(sigma2 - sum_i A_ij^2 + noise, 1e-10)
+__global__ void k_fitc_lambda(int m, int n, const double *A, double sigma2, double noise,
+                              double *lam, double *isq) {
+  int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= n) return;
+  double q = 0.0;
+  for (int i = 0; i < m; ++i) q += A[(int64_t)i * n + j] * A[(int64_t)i * n + j];
+  double v = sigma2 - q + noise;
+  v = v > 1e-10 ? v : 1e-10;
+  lam[j] = v;
+  isq[j] = 1.0 / sqrt(v);
+}
+
+// yl[c][j] = yn[j][c] / lam[j]
+__global__ void k_fitc_yl(int n, int n_out, const double *yn, const double *lam, double *yl) {
+  int j = blockIdx.x * blockDim.x + threadIdx.x, c = blockIdx.y;
+  if (j < n) yl[(int64_t)c * n + j] = yn[(int64_t)j * n_out + c] / lam[j];
+}
+
+// FITC lml (sparse_gp.py:212-218) and alpha^T
+__global__ __launch_bounds__(256) void k_lml_fitc(int m, int n, int n_out, const double *LB,
+                                                  const double *yn, const double *lam,
+                                                  const double *cvec, const double *alpha,
+                                                  double *alphaT, double *lml) {
+  __shared__ double red[4];
+  const int c = blockIdx.x;
+  double ldb = 0.0, ca = 0.0, yly = 0.0, ll = 0.0;
+  for (int i = threadIdx.x; i < m; i += 256) {
+    ldb += log(LB[(int64_t)i * m + i]);
+    const double a = alpha[(int64_t)i * n_out + c];
+    ca += cvec[(int64_t)i * n_out + c] * a;
+    alphaT[(int64_t)c * m + i] = a;
+  }
+  for (int j = threadIdx.x; j < n; j += 256) {
+    const double y = yn[(int64_t)j * n_out + c];
+    yly += y * y / lam[j];
+    ll += log(lam[j]);
+  }
+  ldb = block_sum(ldb, red);
+  ca = block_sum(ca, red);
+  yly = block_sum(yly, red);
+  ll = block_sum(ll, red);
+  if (threadIdx.x == 0) lml[c] = -0.5 * (yly - ca) - ldb - 0.5 * ll - 0.5 * n * log(2.0 * M_PI);
+}
+
+static int core_setup(gpmpc_ctx *ctx, GpCore &g, int kind, const double *X, int n, int d,
+                      const double *ls, double sigma2) {
+  hipStream_t s = ctx->stream;
+  g.kind = kind;
+  g.n = n;
+  g.d = d;
+  g.sigma2 = sigma2;
+  const int iso = (kind == GPMPC_SE_ISO);
+  g.iso_scale = iso ? 1.0 / (2.0 * ls[0] * ls[0]) : 0.0;
+  DevBuf dX;
+  GPMPC_HIP(dX.alloc(sizeof(double) * n * d));
+  GPMPC_HIP(g.ls.alloc(sizeof(double) * d));
+  GPMPC_HIP(g.Xs.alloc(sizeof(double) * n * d));
+  GPMPC_HIP(g.Xn.alloc(sizeof(double) * n));
+  GPMPC_HIP(hipMemcpyAsync(dX.p, X, sizeof(double) * n * d, hipMemcpyHostToDevice, s));
+  GPMPC_HIP(hipMemcpyAsync(g.ls.p, ls, sizeof(double) * d, hipMemcpyHostToDevice, s));
+  GPMPC_HIP(launch_scale_rows(s, dX.as<double>(), n, d, g.ls.as<double>(), iso, g.Xs.as<double>(),
+                              g.Xn.as<double>()));
+  GPMPC_HIP(hipStreamSynchronize(s));
+  return 0;
+}
+
+// K* = k(Xq, X_core) (p x n) on device from host queries; returns scaled queries too
+static int core_cross(gpmpc_ctx *ctx, const GpCore &g, const double *dXq_raw, int p, DevBuf &Ks,
+                      DevBuf *qs = nullptr, DevBuf *qn = nullptr) {
+  hipStream_t s = ctx->stream;
+  DevBuf a, na;
+  DevBuf &A = qs ? *qs : a;
+  DevBuf &NA = qn ? *qn : na;
+  GPMPC_HIP(A.alloc(sizeof(double) * p * g.d));
+  GPMPC_HIP(NA.alloc(sizeof(double) * p));
+  GPMPC_HIP(launch_scale_rows(s, dXq_raw, p, g.d, g.ls.as<double>(), g.kind == GPMPC_SE_ISO,
+                              A.as<double>(), NA.as<double>()));
+  GPMPC_HIP(Ks.alloc(sizeof(double) * (size_t)p * g.n));
+  GPMPC_HIP(launch_gram(s, g.kind, A.as<double>(), NA.as<double>(), p, g.Xs.as<double>(),
+                        g.Xn.as<double>(), g.n, g.d, g.sigma2, g.iso_scale, Ks.as<double>(), g.n,
+                        0));
+  return 0;
+}
+
+// ---------------------------------------------------------------------------
+extern "C" int gpmpc_gp_fit_exact(gpmpc_ctx *ctx, int kind, const double *X, int n, int d,
+                                  const double *Y, int n_out, const double *ls, double sigma2,
+                                  double noise, gpmpc_gp **out, double *y_mean, double *y_std,
+                                  double *lml, int *jitter_steps) {
+  GPMPC_CHECK_ARG(ctx && X && Y && ls && out && n >= 1 && d >= 1 && d <= 32);
+  GPMPC_CHECK_ARG(n_out >= 1 && n_out <= 16 && kind >= 0 && kind <= 3);
+  GPMPC_HIP(hipSetDevice(ctx->device));
+  hipStream_t s = ctx->stream;
+  auto *gp = new gpmpc_gp();
+  GpCore &g = gp->core;
+  gp->noise = noise;
+  int rc = core_setup(ctx, g, kind, X, n, d, ls, sigma2);
+  if (rc) { delete gp; return rc; }
+  DevBuf Kn, dinfo;
+  auto fail = [&](int code) { delete gp; return code; };
+  if (Kn.alloc(sizeof(double) * (size_t)n * n) != hipSuccess ||
+      gp->L.alloc(sizeof(double) * (size_t)n * n) != hipSuccess ||
+      dinfo.alloc(sizeof(int)) != hipSuccess) {
+    gpmpc_set_error("gp_fit_exact: out of device memory");
+    return fail(-1);
+  }
+  // K + noise I   (exact_gp.py:156-160)
+  if (launch_gram(s, kind, g.Xs.as<double>(), g.Xn.as<double>(), n, g.Xs.as<double>(),
+                  g.Xn.as<double>(), n, d, sigma2, g.iso_scale, Kn.as<double>(), n, 0) !=
+          hipSuccess ||
+      launch_add_diag(s, n, Kn.as<double>(), n, noise, 1, 0) != hipSuccess) {
+    gpmpc_set_error("gp_fit_exact: gram launch failed");
+    return fail(-1);
+  }
+  // Cholesky with the jitter ladder (exact_gp.py:163-175): first no jitter,
+  // then j = 1e-6 and j *= 10 while j < 1.
+  int info = 0, steps = 0;
+  double jit = 0.0;
+  for (;;) {
+    if (hipMemcpyAsync(gp->L.p, Kn.p, sizeof(double) * (size_t)n * n, hipMemcpyDeviceToDevice,
+                       s) != hipSuccess)
+      return fail(-1);
+    if (steps > 0 && launch_add_diag(s, n, gp->L.as<double>(), n, jit, 1, 0) != hipSuccess)
+      return fail(-1);
+    if (launch_potrf_batched(s, n, 1, gp->L.as<double>(), n, 0, dinfo.as<int>()) != hipSuccess ||
+        hipMemcpyAsync(&info, dinfo.p, sizeof(int), hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipStreamSynchronize(s) != hipSuccess) {
+      gpmpc_set_error("gp_fit_exact: potrf failed: %s", hipGetErrorString(hipGetLastError()));
+      return fail(-1);
+    }
+    if (info == 0) break;
+    jit = (steps == 0) ? 1e-6 : jit * 10;
+    if (!(jit < 1.0)) {
+      gpmpc_set_error("Kernel matrix is not positive definite even with jitter");
+      return fail(GPMPC_ERR_NOT_PD);
+    }
+    ++steps;
+  }
+  if (jitter_steps) *jitter_steps = steps;
+  // normalised targets, alpha = L^-T L^-1 y for all outputs (exact_gp.py:141-150, 179)
+  DevBuf dYraw, dY, dyn, dlml;
+  if (dYraw.alloc(sizeof(double) * n * n_out) || dY.alloc(sizeof(double) * n * n_out) ||
+      dyn.alloc(sizeof(double) * n * n_out) || dlml.alloc(sizeof(double) * n_out) ||
+      g.ymean.alloc(sizeof(double) * n_out) || g.ystd.alloc(sizeof(double) * n_out) ||
+      g.alphaT.alloc(sizeof(double) * n_out * n) || g.W.alloc(sizeof(double) * (size_t)n * n))
+    return fail(-1);
+  g.n_out = n_out;
+  hipMemcpyAsync(dYraw.p, Y, sizeof(double) * n * n_out, hipMemcpyHostToDevice, s);
+  hipLaunchKernelGGL(k_normalise, dim3(n_out), dim3(256), 0, s, n, n_out, dYraw.as<double>(),
+                     dyn.as<double>(), g.ymean.as<double>(), g.ystd.as<double>());
+  hipMemcpyAsync(dY.p, dyn.p, sizeof(double) * n * n_out, hipMemcpyDeviceToDevice, s);
+  launch_trsm_lower_ex(s, n, n_out, gp->L.as<double>(), n, dY.as<double>(), n_out, 0, 0, nullptr);
+  launch_trsm_lower_ex(s, n, n_out, gp->L.as<double>(), n, dY.as<double>(), n_out, 1, 0, nullptr);
+  // log marginal likelihood per output + alpha^T for the posterior GEMM (exact_gp.py:186-204)
+  hipLaunchKernelGGL(k_lml_exact, dim3(n_out), dim3(256), 0, s, n, n_out, gp->L.as<double>(),
+                     dyn.as<double>(), dY.as<double>(), g.alphaT.as<double>(), dlml.as<double>());
+  // W = L^-1 (identity right-hand side, lower-triangular result)
+  hipLaunchKernelGGL(k_eye, dim3((n + 255) / 256, n), dim3(256), 0, s, n, g.W.as<double>());
+  launch_trsm_lower_ex(s, n, n, gp->L.as<double>(), n, g.W.as<double>(), n, 0, 1, nullptr);
+  g.h_ymean.resize(n_out);
+  g.h_ystd.resize(n_out);
+  hipMemcpyAsync(g.h_ymean.data(), g.ymean.p, sizeof(double) * n_out, hipMemcpyDeviceToHost, s);
+  hipMemcpyAsync(g.h_ystd.data(), g.ystd.p, sizeof(double) * n_out, hipMemcpyDeviceToHost, s);
+  std::vector<double> hl(n_out);
+  hipMemcpyAsync(hl.data(), dlml.p, sizeof(double) * n_out, hipMemcpyDeviceToHost, s);
+  if (hipStreamSynchronize(s) != hipSuccess) {
+    gpmpc_set_error("gp_fit_exact: %s", hipGetErrorString(hipGetLastError()));
+    return fail(-1);
+  }
+  for (int c = 0; c < n_out; ++c) {
+    if (lml) lml[c] = hl[c];
+    if (y_mean) y_mean[c] = g.h_ymean[c];
+    if (y_std) y_std[c] = g.h_ystd[c];
+  }
+  *out = gp;
+  return 0;
+}
+
+// device-side posterior for p queries given K* (p x n): mean/var (p x n_out) device
+static int core_posterior(gpmpc_ctx *ctx, const GpCore &g, const double *Ks, int p, double *dmean,
+                          double *dvar) {
+  hipStream_t s = ctx->stream;
+  const int nrt = gemm_row_tiles(g.n);
+  DevBuf part, meanT;
+  GPMPC_HIP(part.alloc(sizeof(double) * (size_t)nrt * p));
+  GPMPC_HIP(meanT.alloc(sizeof(double) * (size_t)g.n_out * p));
+  // sum_i (W K*^T)_ij^2 per query j
+  GPMPC_HIP(launch_gemm_nt(s, EPI_SUMSQ, g.n, p, g.n, g.W.as<double>(), g.n, Ks, g.n,
+                           part.as<double>(), p, 1.0, 0.0, 1, 0, 1, 0, 0, 0));
+  // K* alpha  -> (n_out x p)
+  GPMPC_HIP(launch_gemm_nt(s, EPI_STORE, g.n_out, p, g.n, g.alphaT.as<double>(), g.n, Ks, g.n,
+                           meanT.as<double>(), p, 1.0, 0.0, 0, 0, 1, 0, 0, 0));
+  hipLaunchKernelGGL(k_post_finish, dim3((p + 255) / 256), dim3(256), 0, s, p, g.n_out, nrt,
+                     part.as<double>(), (int64_t)p, meanT.as<double>(), (int64_t)p,
+                     g.ymean.as<double>(), g.ystd.as<double>(), g.sigma2, dmean, dvar);
+  GPMPC_HIP(hipGetLastError());
+  GPMPC_HIP(hipStreamSynchronize(s));
+  return 0;
+}
+
+extern "C" int gpmpc_gp_predict(gpmpc_ctx *ctx, gpmpc_gp *gp, const double *Xq, int p,
+                                double *mean, double *var) {
+  GPMPC_CHECK_ARG(ctx && gp && Xq && mean && var && p >= 0);
+  if (p == 0) return 0;
+  GPMPC_HIP(hipSetDevice(ctx->device));
+  hipStream_t s = ctx->stream;
+  const GpCore &g = gp->core;
+  DevBuf dq, Ks, dmean, dvar;
+  GPMPC_HIP(dq.alloc(sizeof(double) * p * g.d));
+  GPMPC_HIP(hipMemcpyAsync(dq.p, Xq, sizeof(double) * p * g.d, hipMemcpyHostToDevice, s));
+  int rc = core_cross(ctx, g, dq.as<double>(), p, Ks);
+  if (rc) return rc;
+  GPMPC_HIP(dmean.alloc(sizeof(double) * p * g.n_out));
+  GPMPC_HIP(dvar.alloc(sizeof(double) * p * g.n_out));
+  rc = core_posterior(ctx, g, Ks.as<double>(), p, dmean.as<double>(), dvar.as<double>());
+  if (rc) return rc;
+  GPMPC_HIP(hipMemcpyAsync(mean, dmean.p, sizeof(double) * p * g.n_out, hipMemcpyDeviceToHost, s));
+  GPMPC_HIP(hipMemcpyAsync(var, dvar.p, sizeof(double) * p * g.n_out, hipMemcpyDeviceToHost, s));
+  GPMPC_HIP(hipStreamSynchronize(s));
+  return 0;
+}
+
+extern "C" int gpmpc_gp_predict_cov(gpmpc_ctx *ctx, gpmpc_gp *gp, const double *Xq, int p,
+                                    double *mean, double *cov) {
+  GPMPC_CHECK_ARG(ctx && gp && Xq && mean && cov && p >= 0);
+  if (p == 0) return 0;
+  GPMPC_HIP(hipSetDevice(ctx->device));
+  hipStream_t s = ctx->stream;
+  const GpCore &g = gp->core;
+  DevBuf dq, Ks, qs, qn, V, C, dmean, dvar;
+  GPMPC_HIP(dq.alloc(sizeof(double) * p * g.d));
+  GPMPC_HIP(hipMemcpyAsync(dq.p, Xq, sizeof(double) * p * g.d, hipMemcpyHostToDevice, s));
+  int rc = core_cross(ctx, g, dq.as<double>(), p, Ks, &qs, &qn);
+  if (rc) return rc;
+  // V^T = K* W^T  (p x n):  (V^T)_{jm} = sum_i K*_{ji} W_{mi}
+  GPMPC_HIP(V.alloc(sizeof(double) * (size_t)p * g.n));
+  GPMPC_HIP(launch_gemm_nt(s, EPI_STORE, p, g.n, g.n, Ks.as<double>(), g.n, g.W.as<double>(), g.n,
+                           V.as<double>(), g.n, 1.0, 0.0, 0, 0, 1, 0, 0, 0));
+  // C = K** - V^T V   (exact_gp.py:250-252), in normalised units
+  GPMPC_HIP(C.alloc(sizeof(double) * (size_t)p * p));
+  GPMPC_HIP(launch_gram(s, g.kind, qs.as<double>(), qn.as<double>(), p, qs.as<double>(),
+                        qn.as<double>(), p, g.d, g.sigma2, g.iso_scale, C.as<double>(), p, 0));
+  GPMPC_HIP(launch_gemm_nt(s, EPI_STORE, p, p, g.n, V.as<double>(), g.n, V.as<double>(), g.n,
+                           C.as<double>(), p, -1.0, 1.0, 0, 0, 1, 0, 0, 0));
+  GPMPC_HIP(dmean.alloc(sizeof(double) * p * g.n_out));
+  GPMPC_HIP(dvar.alloc(sizeof(double) * p * g.n_out));
+  rc = core_posterior(ctx, g, Ks.as<double>(), p, dmean.as<double>(), dvar.as<double>());
+  if (rc) return rc;
+  GPMPC_HIP(hipMemcpyAsync(mean, dmean.p, sizeof(double) * p * g.n_out, hipMemcpyDeviceToHost, s));
+  GPMPC_HIP(hipMemcpyAsync(cov, C.p, sizeof(double) * p * p, hipMemcpyDeviceToHost, s));
+  GPMPC_HIP(hipStreamSynchronize(s));
+  return 0;
+}
+
+extern "C" int gpmpc_gp_get_state(gpmpc_ctx *ctx, gpmpc_gp *gp, double *L, double *alpha) {
+  GPMPC_CHECK_ARG(ctx && gp);
+  GPMPC_HIP(hipSetDevice(ctx->device));
+  hipStream_t s = ctx->stream;
+  const int n = gp->core.n, no = gp->core.n_out;
+  if (L) {
+    DevBuf t;
+    GPMPC_HIP(t.alloc(sizeof(double) * (size_t)n * n));
+    GPMPC_HIP(launch_copy_lower(s, n, gp->L.as<double>(), n, t.as<double>(), n));
+    GPMPC_HIP(hipMemcpyAsync(L, t.p, sizeof(double) * (size_t)n * n, hipMemcpyDeviceToHost, s));
+    GPMPC_HIP(hipStreamSynchronize(s));
+  }
+  if (alpha) {
+    std::vector<double> aT((size_t)no * n);
+    GPMPC_HIP(hipMemcpyAsync(aT.data(), gp->core.alphaT.p, sizeof(double) * no * n,
+                             hipMemcpyDeviceToHost, s));
+    GPMPC_HIP(hipStreamSynchronize(s));
+    for (int i = 0; i < n; ++i)
+      for (int c = 0; c < no; ++c) alpha[(size_t)i * no + c] = aT[(size_t)c * n + i];
+  }
+  return 0;
+}
+
+extern "C" int gpmpc_gp_destroy(gpmpc_gp *gp) {
+  delete gp;
+  return 0;
+}
+
+// ---- internal accessors for the fleet ---------------------------------------
+struct GpView {
+  int kind, n, d, n_out;
+  double sigma2, iso_scale;
+  const double *ls, *Xs, *Xn, *W, *alphaT, *ymean, *ystd;
+};
+GpView gp_view(const gpmpc_gp *gp) {
+  const GpCore &g = gp->core;
+  return GpView{g.kind, g.n, g.d, g.n_out, g.sigma2, g.iso_scale, g.ls.as<double>(),
+                g.Xs.as<double>(), g.Xn.as<double>(), g.W.as<double>(), g.alphaT.as<double>(),
+                g.ymean.as<double>(), g.ystd.as<double>()};
+}
+
+// ---------------------------------------------------------------------------
+// FITC (sparse_gp.py:150-219 fit, :255-305 predict)
+extern "C" int gpmpc_fitc_fit(gpmpc_ctx *ctx, const double *Z, int m, const double *X, int n,
+                              int d, const double *Y, int n_out, const double *ls, double sigma2,
+                              double noise, double jitter, gpmpc_fitc **out, double *y_mean,
+                              double *y_std, double *lml, double *lambda_diag) {
+  GPMPC_CHECK_ARG(ctx && Z && X && Y && ls && out && m >= 1 && n >= 1 && d >= 1 && d <= 32);
+  GPMPC_CHECK_ARG(n_out >= 1 && n_out <= 16);
+  GPMPC_HIP(hipSetDevice(ctx->device));
+  hipStream_t s = ctx->stream;
+  auto *gp = new gpmpc_fitc();
+  GpCore &g = gp->core;
+  gp->m = m;
+  int rc = core_setup(ctx, g, GPMPC_SE_ARD, Z, m, d, ls, sigma2);
+  if (rc) { delete gp; return rc; }
+  auto fail = [&](int code) { delete gp; return code; };
+  DevBuf dX, Kuf, Luu, B, dinfo, lam, Xs, Xn, part;
+  if (dX.alloc(sizeof(double) * n * d) || Kuf.alloc(sizeof(double) * (size_t)m * n) ||
+      Luu.alloc(sizeof(double) * (size_t)m * m) || B.alloc(sizeof(double) * (size_t)m * m) ||
+      dinfo.alloc(sizeof(int)) || lam.alloc(sizeof(double) * n) ||
+      Xs.alloc(sizeof(double) * n * d) || Xn.alloc(sizeof(double) * n) ||
+      g.W.alloc(sizeof(double) * (size_t)m * m) || gp->WB.alloc(sizeof(double) * (size_t)m * m)) {
+    gpmpc_set_error("fitc_fit: out of device memory");
+    return fail(-1);
+  }
+  hipMemcpyAsync(dX.p, X, sizeof(double) * n * d, hipMemcpyHostToDevice, s);
+  launch_scale_rows(s, dX.as<double>(), n, d, g.ls.as<double>(), 0, Xs.as<double>(),
+                    Xn.as<double>());
+  // K_uu + jitter I -> L_uu   (sparse_gp.py:181-187; no jitter ladder in the reference)
+  launch_gram(s, GPMPC_SE_ARD, g.Xs.as<double>(), g.Xn.as<double>(), m, g.Xs.as<double>(),
+              g.Xn.as<double>(), m, d, sigma2, 0.0, Luu.as<double>(), m, 0);
+  launch_add_diag(s, m, Luu.as<double>(), m, jitter, 1, 0);
+  int info = 0;
+  launch_potrf_batched(s, m, 1, Luu.as<double>(), m, 0, dinfo.as<int>());
+  hipMemcpyAsync(&info, dinfo.p, sizeof(int), hipMemcpyDeviceToHost, s);
+  GPMPC_HIP(hipStreamSynchronize(s));
+  if (info) {
+    gpmpc_set_error("Matrix is not positive definite (K_uu, column %d)", info);
+    return fail(info);
+  }
+  // A = L_uu^-1 K_uf  (m x n)
+  launch_gram(s, GPMPC_SE_ARD, g.Xs.as<double>(), g.Xn.as<double>(), m, Xs.as<double>(),
+              Xn.as<double>(), n, d, sigma2, 0.0, Kuf.as<double>(), n, 0);
+  launch_trsm_lower_ex(s, m, n, Luu.as<double>(), m, Kuf.as<double>(), n, 0, 0, nullptr);
+  hipLaunchKernelGGL(k_eye, dim3((m + 255) / 256, m), dim3(256), 0, s, m, g.W.as<double>());
+  launch_trsm_lower_ex(s, m, m, Luu.as<double>(), m, g.W.as<double>(), m, 0, 1, nullptr);
+  // normalised targets; c = A (y / Lambda) before A is rescaled  (sparse_gp.py:160-166, 204)
+  DevBuf isq, dYraw, dyn, yl, cvec, alpha, dlml;
+  if (isq.alloc(sizeof(double) * n) || dYraw.alloc(sizeof(double) * n * n_out) ||
+      dyn.alloc(sizeof(double) * n * n_out) || yl.alloc(sizeof(double) * n * n_out) ||
+      cvec.alloc(sizeof(double) * m * n_out) || alpha.alloc(sizeof(double) * m * n_out) ||
+      dlml.alloc(sizeof(double) * n_out) || g.ymean.alloc(sizeof(double) * n_out) ||
+      g.ystd.alloc(sizeof(double) * n_out) || g.alphaT.alloc(sizeof(double) * n_out * m))
+    return fail(-1);
+  g.n_out = n_out;
+  // Lambda = max(sigma2 - colsum(A^2) + noise, 1e-10)   (sparse_gp.py:193-199)
+  hipLaunchKernelGGL(k_fitc_lambda, dim3((n + 255) / 256), dim3(256), 0, s, m, n, Kuf.as<double>(),
+                     sigma2, noise, lam.as<double>(), isq.as<double>());
+  hipMemcpyAsync(dYraw.p, Y, sizeof(double) * n * n_out, hipMemcpyHostToDevice, s);
+  hipLaunchKernelGGL(k_normalise, dim3(n_out), dim3(256), 0, s, n, n_out, dYraw.as<double>(),
+                     dyn.as<double>(), g.ymean.as<double>(), g.ystd.as<double>());
+  hipLaunchKernelGGL(k_fitc_yl, dim3((n + 255) / 256, n_out), dim3(256), 0, s, n, n_out,
+                     dyn.as<double>(), lam.as<double>(), yl.as<double>());
+  launch_gemm_nt(s, EPI_STORE, m, n_out, n, Kuf.as<double>(), n, yl.as<double>(), n,
+                 cvec.as<double>(), n_out, 1.0, 0.0, 0, 0, 1, 0, 0, 0);
+  // B = I + A_s A_s^T, A_s = A Lambda^-1/2  (SYRK on MFMA, K = n)
+  hipLaunchKernelGGL(k_scale_cols, dim3((n + 255) / 256, m), dim3(256), 0, s, m, n,
+                     Kuf.as<double>(), (int64_t)n, isq.as<double>());
+  hipLaunchKernelGGL(k_eye, dim3((m + 255) / 256, m), dim3(256), 0, s, m, B.as<double>());
+  launch_gemm_nt(s, EPI_STORE, m, m, n, Kuf.as<double>(), n, Kuf.as<double>(), n, B.as<double>(), m,
+                 1.0, 1.0, 0, 0, 1, 0, 0, 0);
+  launch_potrf_batched(s, m, 1, B.as<double>(), m, 0, dinfo.as<int>());
+  hipMemcpyAsync(&info, dinfo.p, sizeof(int), hipMemcpyDeviceToHost, s);
+  GPMPC_HIP(hipStreamSynchronize(s));
+  if (info) {
+    gpmpc_set_error("Matrix is not positive definite (B, column %d)", info);
+    return fail(info);
+  }
+  hipLaunchKernelGGL(k_eye, dim3((m + 255) / 256, m), dim3(256), 0, s, m, gp->WB.as<double>());
+  launch_trsm_lower_ex(s, m, m, B.as<double>(), m, gp->WB.as<double>(), m, 0, 1, nullptr);
+  // alpha = B^-1 c  and the FITC lml  (sparse_gp.py:207-218)
+  hipMemcpyAsync(alpha.p, cvec.p, sizeof(double) * m * n_out, hipMemcpyDeviceToDevice, s);
+  launch_trsm_lower_ex(s, m, n_out, B.as<double>(), m, alpha.as<double>(), n_out, 0, 0, nullptr);
+  launch_trsm_lower_ex(s, m, n_out, B.as<double>(), m, alpha.as<double>(), n_out, 1, 0, nullptr);
+  hipLaunchKernelGGL(k_lml_fitc, dim3(n_out), dim3(256), 0, s, m, n, n_out, B.as<double>(),
+                     dyn.as<double>(), lam.as<double>(), cvec.as<double>(), alpha.as<double>(),
+                     g.alphaT.as<double>(), dlml.as<double>());
+  g.h_ymean.resize(n_out);
+  g.h_ystd.resize(n_out);
+  std::vector<double> hl(n_out);
+  hipMemcpyAsync(g.h_ymean.data(), g.ymean.p, sizeof(double) * n_out, hipMemcpyDeviceToHost, s);
+  hipMemcpyAsync(g.h_ystd.data(), g.ystd.p, sizeof(double) * n_out, hipMemcpyDeviceToHost, s);
+  hipMemcpyAsync(hl.data(), dlml.p, sizeof(double) * n_out, hipMemcpyDeviceToHost, s);
+  if (lambda_diag)
+    hipMemcpyAsync(lambda_diag, lam.p, sizeof(double) * n, hipMemcpyDeviceToHost, s);
+  if (hipStreamSynchronize(s) != hipSuccess) {
+    gpmpc_set_error("fitc_fit: %s", hipGetErrorString(hipGetLastError()));
+    return fail(-1);
+  }
+  for (int c = 0; c < n_out; ++c) {
+    if (lml) lml[c] = hl[c];
+    if (y_mean) y_mean[c] = g.h_ymean[c];
+    if (y_std) y_std[c] = g.h_ystd[c];
+  }
+  *out = gp;
+  return 0;
+}
+
+extern "C" int gpmpc_fitc_predict(gpmpc_ctx *ctx, gpmpc_fitc *gp, const double *Xq, int p,
+                                  double *mean, double *var) {
+  GPMPC_CHECK_ARG(ctx && gp && Xq && mean && var && p >= 0);
+  if (p == 0) return 0;
+  GPMPC_HIP(hipSetDevice(ctx->device));
+  hipStream_t s = ctx->stream;
+  const GpCore &g = gp->core;
+  const int m = gp->m;
+  DevBuf dq, Ks, V, pv, pw, meanT, dmean, dvar;
+  GPMPC_HIP(dq.alloc(sizeof(double) * p * g.d));
+  GPMPC_HIP(hipMemcpyAsync(dq.p, Xq, sizeof(double) * p * g.d, hipMemcpyHostToDevice, s));
+  int rc = core_cross(ctx, g, dq.as<double>(), p, Ks);  // K*u (p x m)
+  if (rc) return rc;
+  const int nrt = gemm_row_tiles(m);
+  GPMPC_HIP(V.alloc(sizeof(double) * (size_t)p * m));
+  GPMPC_HIP(pv.alloc(sizeof(double) * (size_t)nrt * p));
+  GPMPC_HIP(pw.alloc(sizeof(double) * (size_t)nrt * p));
+  GPMPC_HIP(meanT.alloc(sizeof(double) * (size_t)g.n_out * p));
+  // v^T = K*u Luu^-T  (p x m); |v|^2 via the SUMSQ epilogue of W_uu K*u^T
+  GPMPC_HIP(launch_gemm_nt(s, EPI_STORE, p, m, m, Ks.as<double>(), m, g.W.as<double>(), m,
+                           V.as<double>(), m, 1.0, 0.0, 0, 0, 1, 0, 0, 0));
+  GPMPC_HIP(launch_gemm_nt(s, EPI_SUMSQ, m, p, m, g.W.as<double>(), m, Ks.as<double>(), m,
+                           pv.as<double>(), p, 1.0, 0.0, 1, 0, 1, 0, 0, 0));
+  GPMPC_HIP(launch_gemm_nt(s, EPI_SUMSQ, m, p, m, gp->WB.as<double>(), m, V.as<double>(), m,
+                           pw.as<double>(), p, 1.0, 0.0, 1, 0, 1, 0, 0, 0));
+  GPMPC_HIP(launch_gemm_nt(s, EPI_STORE, g.n_out, p, m, g.alphaT.as<double>(), m, Ks.as<double>(),
+                           m, meanT.as<double>(), p, 1.0, 0.0, 0, 0, 1, 0, 0, 0));
+  GPMPC_HIP(dmean.alloc(sizeof(double) * p * g.n_out));
+  GPMPC_HIP(dvar.alloc(sizeof(double) * p * g.n_out));
+  hipLaunchKernelGGL(k_fitc_finish, dim3((p + 255) / 256), dim3(256), 0, s, p, g.n_out, nrt,
+                     pv.as<double>(), pw.as<double>(), (int64_t)p, meanT.as<double>(), (int64_t)p,
+                     g.ymean.as<double>(), g.ystd.as<double>(), g.sigma2, dmean.as<double>(),
+                     dvar.as<double>());
+  GPMPC_HIP(hipGetLastError());
+  GPMPC_HIP(hipMemcpyAsync(mean, dmean.p, sizeof(double) * p * g.n_out, hipMemcpyDeviceToHost, s));
+  GPMPC_HIP(hipMemcpyAsync(var, dvar.p, sizeof(double) * p * g.n_out, hipMemcpyDeviceToHost, s));
+  GPMPC_HIP(hipStreamSynchronize(s));
+  return 0;
+}
+
+extern "C" int gpmpc_fitc_destroy(gpmpc_fitc *gp) {
+  delete gp;
+  return 0;
+}

@@ -1,0 +1,69 @@
+// internal.h -- shared helpers for libgpmpc_hip.so (gfx950 only).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+#include <cstdio>
+#include <string>
+#include "../../include/gpmpc.h"
+
+struct gpmpc_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  // scratch that grows on demand (device)
+  void *scratch = nullptr;
+  size_t scratch_bytes = 0;
+};
+
+void gpmpc_set_error(const char *fmt, ...);
+
+#define GPMPC_HIP(call)                                                               \
+  do {                                                                                \
+    hipError_t e_ = (call);                                                           \
+    if (e_ != hipSuccess) {                                                           \
+      gpmpc_set_error("%s:%d %s -> %s", __FILE__, __LINE__, #call, hipGetErrorString(e_)); \
+      return -1;                                                                      \
+    }                                                                                 \
+  } while (0)
+
+#define GPMPC_CHECK_ARG(cond)                                    \
+  do {                                                           \
+    if (!(cond)) {                                               \
+      gpmpc_set_error("%s:%d bad argument: %s", __FILE__, __LINE__, #cond); \
+      return -2;                                                 \
+    }                                                            \
+  } while (0)
+
+// RAII device buffer (host-side bookkeeping only)
+struct DevBuf {
+  void *p = nullptr;
+  size_t bytes = 0;
+  ~DevBuf() { if (p) (void)hipFree(p); }
+  hipError_t alloc(size_t b) {
+    if (p) { (void)hipFree(p); p = nullptr; }
+    bytes = b;
+    return b ? hipMalloc(&p, b) : hipSuccess;
+  }
+  template <class T> T *as() const { return static_cast<T *>(p); }
+};
+
+// ---- internal device entry points shared across translation units ----------
+// Gram: K (n1 x n2, ldk) from pre-scaled rows (a = X1/ls, b = X2/ls) and their
+// squared norms; kind selects the epilogue.
+hipError_t launch_gram(hipStream_t s, int kind, const double *a, const double *na, int n1,
+                       const double *b, const double *nb, int n2, int d, double sigma2,
+                       double iso_scale, double *K, int64_t ldk, int transpose_out);
+// rows / lengthscales -> scaled rows + squared norms
+hipError_t launch_scale_rows(hipStream_t s, const double *X, int n, int d, const double *ls,
+                             int iso, double *out, double *norms);
+// blocked Cholesky of batch matrices; info (device int[batch]), 1-based pivot
+hipError_t launch_potrf_batched(hipStream_t s, int n, int batch, double *A, int64_t lda,
+                                int64_t stride, int *info);
+// X <- L^-1 X (L lower n x n, X n x nrhs row-major ld ldx), batch via strides
+hipError_t launch_trsm_lower(hipStream_t s, int n, int nrhs, const double *L, int64_t ldl,
+                             double *X, int64_t ldx, int transpose_L);
+// add value to the diagonal of A
+hipError_t launch_add_diag(hipStream_t s, int n, double *A, int64_t lda, double v, int batch,
+                           int64_t stride);
+// copy lower triangle of src into dst and zero the strict upper part of dst
+hipError_t launch_copy_lower(hipStream_t s, int n, const double *src, int64_t lds, double *dst,
+                             int64_t ldd);

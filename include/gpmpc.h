@@ -1,0 +1,173 @@
+/*
+ * gpmpc.h -- C-ABI of libgpmpc_hip.so, the MI355X (gfx950) GP + QP hot path.
+ *
+ * The reference (shiivashaakeri/gp-mpc-rocket-landing) is pure Python: its
+ * "boundary" for this path is a set of duck-typed classes whose heavy lifting
+ * is numpy/LAPACK and the third-party OSQP C solver.  Each entry point below
+ * replaces one of those native calls; the Python mirror in
+ * gp_mpc_rocket_landing_amd/ binds them with ctypes.
+ *
+ * Conventions
+ *   - every function returns int: 0 = ok, >0 = LAPACK-style info (e.g. the
+ *     1-based column of the first non-positive pivot), <0 = argument / HIP
+ *     error (gpmpc_last_error() has the message).  Nothing throws.
+ *   - all arithmetic is fp64; host buffers are caller-owned, row-major, with
+ *     explicit leading dimensions.  Functions suffixed _dev take device
+ *     pointers that must stay resident for the call.
+ *   - one gpmpc_ctx per process/rank owns one HIP stream; a ctx is not
+ *     thread-safe.
+ */
+#ifndef GPMPC_H
+#define GPMPC_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GPMPC_ABI_VERSION 1
+
+typedef struct gpmpc_ctx gpmpc_ctx;
+typedef struct gpmpc_gp gpmpc_gp;
+typedef struct gpmpc_fitc gpmpc_fitc;
+typedef struct gpmpc_fleet gpmpc_fleet;
+
+/* kernel kinds: kernels.py:130 (SE-ARD), :392 (isotropic SE), :482 (Matern32), :579 (Matern52) */
+enum { GPMPC_SE_ARD = 0, GPMPC_SE_ISO = 1, GPMPC_MATERN32 = 2, GPMPC_MATERN52 = 3 };
+
+/* OSQP-style status values (OSQP 0.6 constants.h), reported by the ADMM. */
+enum {
+  GPMPC_QP_SOLVED = 1, GPMPC_QP_SOLVED_INACCURATE = 2, GPMPC_QP_MAX_ITER_REACHED = -2,
+  GPMPC_QP_PRIMAL_INFEASIBLE = -3, GPMPC_QP_PRIMAL_INFEASIBLE_INACCURATE = 3,
+  GPMPC_QP_DUAL_INFEASIBLE = -4, GPMPC_QP_DUAL_INFEASIBLE_INACCURATE = 4,
+  GPMPC_QP_NON_CVX = -7, GPMPC_QP_UNSOLVED = -10
+};
+
+int gpmpc_abi_version(void);
+const char *gpmpc_last_error(void);
+
+/* ---- context ---------------------------------------------------------- */
+int gpmpc_ctx_create(int device, gpmpc_ctx **out);
+int gpmpc_ctx_destroy(gpmpc_ctx *ctx);
+int gpmpc_ctx_sync(gpmpc_ctx *ctx);
+/* the HIP stream the context launches on (hipStream_t as void*) */
+void *gpmpc_ctx_stream(gpmpc_ctx *ctx);
+
+/* ---- a2/a3: kernel Gram matrix -----------------------------------------
+ * Replaces SquaredExponentialARD.__call__ / Matern32/52.__call__ /
+ * SquaredExponential.__call__ (kernels.py:238-262, :532-545, :625-637,
+ * :417-432): K[i,j] = k(X1[i], X2[j]).  X2 == NULL means X2 = X1.
+ * ls: d lengthscales (SE_ISO reads ls[0]). */
+int gpmpc_gram(gpmpc_ctx *ctx, int kind, const double *X1, int n1, const double *X2, int n2,
+               int d, const double *ls, double sigma2, double *K, int ldk);
+
+/* ---- Cholesky factor / solve -------------------------------------------
+ * Replaces np.linalg.cholesky (exact_gp.py:164,170; sparse_gp.py:187,205).
+ * In place on the lower triangle; info = 1-based first non-positive pivot. */
+int gpmpc_potrf(gpmpc_ctx *ctx, int n, double *A, int lda, int *info);
+/* batch x (n x n) SPD matrices, device-resident, stride elements apart;
+ * dinfo: device int[batch]. */
+int gpmpc_potrf_batched_dev(gpmpc_ctx *ctx, int n, int batch, double *dA, int lda, int64_t stride,
+                            int *dinfo);
+/* Replaces scipy.linalg.solve_triangular(L, B, lower=True) (exact_gp.py:251,260;
+ * sparse_gp.py:190,293,296): B (n x nrhs) overwritten by L^-1 B. */
+int gpmpc_trsm_lower(gpmpc_ctx *ctx, int n, int nrhs, const double *L, int ldl, double *B, int ldb);
+/* Replaces scipy.linalg.cho_solve((L, True), B) (exact_gp.py:179; sparse_gp.py:210,214). */
+int gpmpc_potrs(gpmpc_ctx *ctx, int n, int nrhs, const double *L, int ldl, double *B, int ldb);
+
+/* ---- a4-a6: exact GP ------------------------------------------------------
+ * MultiOutputExactGP.fit (exact_gp.py:476-499 -> ExactGP.fit :118-184) for
+ * n_out outputs sharing one kernel (one Gram + one Cholesky).
+ * Y is (n x n_out) row-major.  Reproduces the jitter ladder of
+ * exact_gp.py:163-175; jitter_steps = 0 (none) .. 6, and the function returns
+ * GPMPC_ERR_NOT_PD (-100) when the ladder is exhausted (the reference raises
+ * ValueError).  Outputs per output: y_mean, y_std, lml. */
+#define GPMPC_ERR_NOT_PD (-100)
+int gpmpc_gp_fit_exact(gpmpc_ctx *ctx, int kind, const double *X, int n, int d, const double *Y,
+                       int n_out, const double *ls, double sigma2, double noise, gpmpc_gp **out,
+                       double *y_mean, double *y_std, double *lml, int *jitter_steps);
+/* ExactGP.predict (exact_gp.py:213-268) for all outputs: mean/var (p x n_out). */
+int gpmpc_gp_predict(gpmpc_ctx *ctx, gpmpc_gp *gp, const double *Xq, int p, double *mean,
+                     double *var);
+/* ExactGP.predict(return_cov=True) (exact_gp.py:247-254): cov (p x p) of the
+ * latent posterior in normalised units (caller multiplies by y_std^2). */
+int gpmpc_gp_predict_cov(gpmpc_ctx *ctx, gpmpc_gp *gp, const double *Xq, int p, double *mean,
+                         double *cov);
+/* Copies of the device state (L lower, n x n; alpha n x n_out). Either may be NULL. */
+int gpmpc_gp_get_state(gpmpc_ctx *ctx, gpmpc_gp *gp, double *L, double *alpha);
+int gpmpc_gp_destroy(gpmpc_gp *gp);
+
+/* ---- a8-a10: FITC sparse GP ----------------------------------------------
+ * MultiOutputSparseGP.fit (sparse_gp.py:430-456 -> SparseGP.fit FITC :150-219)
+ * with caller-supplied inducing points Z (m x d) shared by all outputs.
+ * Outputs per output: y_mean, y_std, lml.  Lambda (n) optional. */
+int gpmpc_fitc_fit(gpmpc_ctx *ctx, const double *Z, int m, const double *X, int n, int d,
+                   const double *Y, int n_out, const double *ls, double sigma2, double noise,
+                   double jitter, gpmpc_fitc **out, double *y_mean, double *y_std, double *lml,
+                   double *lambda_diag);
+/* SparseGP.predict (sparse_gp.py:255-305), mean as written. */
+int gpmpc_fitc_predict(gpmpc_ctx *ctx, gpmpc_fitc *gp, const double *Xq, int p, double *mean,
+                       double *var);
+int gpmpc_fitc_destroy(gpmpc_fitc *gp);
+
+/* ---- a15: batched OSQP-style ADMM ------------------------------------------
+ * Replaces osqp.OSQP().setup / update / warm_start / solve
+ * (osqp_rti.py:464-478, 496, 517, 524, 527) for a batch of QPs
+ *     min 1/2 x'Px + q'x  s.t.  l <= Ax <= u
+ * sharing one sparsity pattern of A (CSR: rowptr m+1, colidx nnz) and a
+ * diagonal P.  Per problem: Aval (nnz), Pdiag (n), q (n), l/u (m).  The
+ * reduced KKT matrix P + sigma I + A' diag(rho) A must be banded (the MPC
+ * stage structure gives half-bandwidth 2*nx+nu-1); bandwidth <= 24.
+ * State carried between solves (OSQP keeps it in its workspace):
+ *   rho (batch), y_scaled (batch x m).  x_ws: warm-start primal (unscaled).
+ * Outputs: x (batch x n), y (batch x m) unscaled, iters, status, obj. */
+typedef struct {
+  double rho, sigma, alpha;
+  double eps_abs, eps_rel, eps_prim_inf, eps_dual_inf;
+  int max_iter, check_termination, adaptive_rho, adaptive_rho_interval;
+  double adaptive_rho_tolerance;
+  int scaling, warm_start;
+} gpmpc_qp_settings;
+void gpmpc_qp_default_settings(gpmpc_qp_settings *s); /* osqp_rti.py:54-60 + OSQP 0.6 defaults */
+int gpmpc_qp_solve_batched(gpmpc_ctx *ctx, int batch, int n, int m, int nnz, const int *rowptr,
+                           const int *colidx, const double *Aval, const double *Pdiag,
+                           const double *q, const double *l, const double *u,
+                           const gpmpc_qp_settings *s, const double *x_ws, double *rho,
+                           double *y_scaled, double *x, double *y, int *iters, int *status,
+                           double *obj);
+
+/* ---- the control step: a fleet of closed-loop 3-DoF GP-MPC landings -------
+ * One "step" = for every landing: GP posterior (mean + variance) at the N
+ * horizon points of its linearisation trajectory, RTI QP assembly with the GP
+ * mean on the velocity rows (gp_mpc.py:303-320, correct sign), batched ADMM
+ * (osqp_rti.py:501-567 protocol), plant step and Monte-Carlo termination
+ * (monte_carlo.py:455-537).  Everything stays device-resident. */
+typedef struct {
+  int horizon;           /* N (osqp_rti.py OSQPRTIConfig.N / MPCConfig.N) */
+  double dt;             /* control period */
+  int target_mode;       /* 0: fixed x_target (controller.step protocol);
+                            1: incremental target of monte_carlo.py:497-500 (solve protocol) */
+  int use_gp;            /* add GP mean to c_k */
+  int residual_model;    /* 1: plant gets the aero-drag residual (dispersion.py:349-360) */
+  int max_steps;         /* max_time / dt */
+  gpmpc_qp_settings qp;
+} gpmpc_fleet_config;
+void gpmpc_fleet_default_config(gpmpc_fleet_config *c);
+int gpmpc_fleet_create(gpmpc_ctx *ctx, gpmpc_gp *gp, const gpmpc_fleet_config *cfg, int batch,
+                       gpmpc_fleet **out);
+/* (re)initialise landings [first, first+count) from x0 (count x 7) */
+int gpmpc_fleet_reset(gpmpc_fleet *f, int first, int count, const double *x0);
+/* advance every active landing by nsteps control steps (async on the ctx stream) */
+int gpmpc_fleet_step(gpmpc_fleet *f, int nsteps);
+/* records (batch x GPMPC_REC_LEN doubles), see gpmpc_fleet_record layout */
+#define GPMPC_REC_LEN 16
+int gpmpc_fleet_read(gpmpc_fleet *f, double *records, double *x /* batch x 7, may be NULL */);
+/* device pointer of the record array (for collectives) */
+double *gpmpc_fleet_records_dev(gpmpc_fleet *f);
+int gpmpc_fleet_destroy(gpmpc_fleet *f);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GPMPC_H */

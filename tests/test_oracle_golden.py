@@ -1,0 +1,178 @@
+"""The CPU oracle against the reference's own outputs (golden fixtures F1-F8).
+
+These pin the oracle before it is trusted as the parity checker for the HIP path.
+"""
+import numpy as np
+import pytest
+import scipy.sparse as sp
+
+from conftest import close, golden
+from oracle import admm_oracle, admm_ref, gp_oracle, mc_oracle, qp_oracle
+
+
+def test_f3_kernels():
+    f = golden("f3_kernels.npz")
+    X1, X2, ls, s2 = f["X1"], f["X2"], f["ls"], float(f["sigma2"])
+    np.testing.assert_allclose(gp_oracle.gram("se_ard", X1, X2, s2, ls), f["se_ard"], rtol=1e-13, atol=1e-15)
+    np.testing.assert_allclose(gp_oracle.gram("se_ard", X1, None, s2, ls), f["se_ard_self"], rtol=1e-13, atol=1e-15)
+    np.testing.assert_allclose(gp_oracle.gram("matern32", X1, X2, s2, ls), f["matern32"], rtol=1e-13, atol=1e-15)
+    np.testing.assert_allclose(gp_oracle.gram("matern52", X1, X2, s2, ls), f["matern52"], rtol=1e-13, atol=1e-15)
+    np.testing.assert_allclose(gp_oracle.gram("se_iso", X1, X2, s2, [float(f["iso_l"])]), f["se_iso"], rtol=1e-13, atol=1e-15)
+    s = gp_oracle.gram("se_ard", X1, X2, s2, ls) + gp_oracle.gram("matern32", X1, X2, 0.3, ls)
+    np.testing.assert_allclose(s, f["sum_se_m32"], rtol=1e-13, atol=1e-15)
+    p = gp_oracle.gram("se_ard", X1, X2, s2, ls) * gp_oracle.gram("matern52", X1, X2, 0.5, ls)
+    np.testing.assert_allclose(p, f["prod_se_m52"], rtol=1e-13, atol=1e-15)
+
+
+def test_f1_features_and_exact_gp():
+    f = golden("f1_exact_simple3dof.npz")
+    Z = gp_oracle.features_3dof(f["X"], f["U"])
+    np.testing.assert_allclose(Z, f["Z"], rtol=1e-14, atol=1e-15)
+    st = gp_oracle.exact_fit(Z, f["D"])
+    assert st["jitter_steps"] == 0
+    np.testing.assert_allclose(np.diag(st["L"]), f["diagL"], rtol=1e-10)
+    np.testing.assert_allclose(st["y_mean"], f["y_mean"], rtol=1e-14)
+    np.testing.assert_allclose(st["y_std"], f["y_std"], rtol=1e-14)
+    np.testing.assert_allclose(st["lml"], f["lml"], rtol=1e-8)
+    mean, var = gp_oracle.exact_predict(st, gp_oracle.features_3dof(f["Xq"], f["Uq"]))
+    ok, e = close(mean, f["mean"], f["y_std"]); assert ok, e
+    ok, e = close(var, f["var"], f["y_std"] ** 2); assert ok, e
+    m1, v1 = gp_oracle.exact_predict(st, gp_oracle.features_3dof(f["Xq"][:1], f["Uq"][:1]))
+    ok, e = close(m1[0], f["single_mean"], f["y_std"]); assert ok, e
+    ok, e = close(v1[0], f["single_var"], f["y_std"] ** 2); assert ok, e
+
+
+def test_f2_small_exact_jitter_and_cov():
+    f = golden("f2_exact_small.npz")
+    st = gp_oracle.exact_fit(f["X"], f["Y"], noise=1e-3)
+    np.testing.assert_allclose(st["L"], f["L"], rtol=1e-11, atol=1e-13)
+    np.testing.assert_allclose(st["alpha"], f["alpha"], rtol=1e-8, atol=1e-10)
+    np.testing.assert_allclose(st["lml"], f["lml"], rtol=1e-10)
+    mean, var = gp_oracle.exact_predict(st, f["Xq"])
+    np.testing.assert_allclose(mean, f["mean"], rtol=1e-9, atol=1e-12)
+    np.testing.assert_allclose(var, f["var"], rtol=1e-9, atol=1e-12)
+    mc, cov = gp_oracle.exact_predict_cov(st, f["Xq"], out=1)
+    np.testing.assert_allclose(mc, f["cov_mean"], rtol=1e-9, atol=1e-12)
+    np.testing.assert_allclose(cov, f["cov"], rtol=1e-8, atol=1e-12)
+    # jitter ladder (exact_gp.py:163-175)
+    sd = gp_oracle.exact_fit(f["Xdup"], f["ydup"], noise=-1e-7)
+    assert gp_oracle.jitter_ladder()[sd["jitter_steps"] - 1] == float(f["dup_jitter"])
+    np.testing.assert_allclose(sd["L"], f["dup_L"], rtol=1e-9, atol=1e-12)
+    with pytest.raises(ValueError, match="not positive definite"):
+        gp_oracle.exact_fit(f["X"], f["Y"][:, 0], noise=-5.0)
+    assert int(f["neg_noise_raises"]) == 1
+
+
+def test_jitter_ladder_values():
+    lad = gp_oracle.jitter_ladder()
+    assert lad[0] == 1e-6 and len(lad) == 6 and lad[-1] < 1.0
+    assert lad[1] == 9.999999999999999e-06  # repeated multiplication, not 10**k
+
+
+def test_f4_fitc():
+    f = golden("f4_fitc_simple3dof.npz")
+    X = gp_oracle.features_3dof(f["X"], f["U"])
+    st = gp_oracle.fitc_fit(f["Zi"], X, f["D"])
+    np.testing.assert_allclose(st["lam"], f["lam"], rtol=1e-9, atol=1e-15)
+    np.testing.assert_allclose(np.diag(st["Luu"]), f["diagLuu"], rtol=1e-12)
+    np.testing.assert_allclose(st["alpha"], f["alpha"], rtol=1e-7, atol=1e-9)
+    np.testing.assert_allclose(st["lml"], f["lml"], rtol=1e-8)
+    mean, var = gp_oracle.fitc_predict(st, f["Zq"])
+    ok, e = close(mean, f["mean"], f["y_std"]); assert ok, e
+    ok, e = close(var, f["var"], f["y_std"] ** 2); assert ok, e
+
+
+def test_f5_structured_features():
+    f = golden("f5_structured_6dof.npz")
+    np.testing.assert_allclose(gp_oracle.features_translational(f["X"], f["U"]), f["Zv"], rtol=1e-13, atol=1e-14)
+    np.testing.assert_allclose(gp_oracle.features_rotational(f["X"], f["U"]), f["Zw"], rtol=1e-13, atol=1e-14)
+    Zv = gp_oracle.features_translational(f["X"], f["U"])
+    Zw = gp_oracle.features_rotational(f["X"], f["U"])
+    sv = gp_oracle.exact_fit(Zv, f["Dv"]); sw = gp_oracle.exact_fit(Zw, f["Dw"])
+    mv, vv = gp_oracle.exact_predict(sv, gp_oracle.features_translational(f["Xq"], f["Uq"]))
+    mw, vw = gp_oracle.exact_predict(sw, gp_oracle.features_rotational(f["Xq"], f["Uq"]))
+    for a, b, s in ((mv, f["exact_dv_mean"], sv["y_std"]), (mw, f["exact_dw_mean"], sw["y_std"]),
+                    (vv, f["exact_dv_var"], sv["y_std"] ** 2), (vw, f["exact_dw_var"], sw["y_std"] ** 2)):
+        ok, e = close(a, b, s); assert ok, e
+    fv = gp_oracle.fitc_fit(f["fitc_Zv"], Zv, f["Dv"]); fw = gp_oracle.fitc_fit(f["fitc_Zw"], Zw, f["Dw"])
+    mv, vv = gp_oracle.fitc_predict(fv, gp_oracle.features_translational(f["Xq"], f["Uq"]))
+    mw, vw = gp_oracle.fitc_predict(fw, gp_oracle.features_rotational(f["Xq"], f["Uq"]))
+    for a, b, s in ((mv, f["fitc_dv_mean"], fv["y_std"]), (mw, f["fitc_dw_mean"], fw["y_std"]),
+                    (vv, f["fitc_dv_var"], fv["y_std"] ** 2), (vw, f["fitc_dw_var"], fw["y_std"] ** 2)):
+        ok, e = close(a, b, s); assert ok, e
+
+
+def test_f6_qp_assembly():
+    f = golden("f6_qp_assembly.npz")
+    for i in range(int(f["ncases"])):
+        X, U, x0, xt = f[f"c{i}_X"], f[f"c{i}_U"], f[f"c{i}_x0"], f[f"c{i}_xt"]
+        P, q = qp_oracle.cost(20, np.tile(xt, (21, 1)))
+        A, l, u = qp_oracle.constraints(X, U, x0, 0.1, sign=+1.0)
+        Pr = sp.csc_matrix((f[f"c{i}_P_data"], f[f"c{i}_P_indices"], f[f"c{i}_P_indptr"]), shape=P.shape)
+        Ar = sp.csc_matrix((f[f"c{i}_A_data"], f[f"c{i}_A_indices"], f[f"c{i}_A_indptr"]), shape=A.shape)
+        assert (P != Pr).nnz == 0
+        np.testing.assert_array_equal(A.indptr, Ar.indptr)
+        np.testing.assert_array_equal(A.indices, Ar.indices)
+        np.testing.assert_allclose(A.data, Ar.data, rtol=1e-15, atol=0)
+        np.testing.assert_allclose(q, f[f"c{i}_q"], rtol=0, atol=0)
+        np.testing.assert_allclose(l, f[f"c{i}_l"], rtol=1e-14, atol=1e-14)
+        np.testing.assert_allclose(u, f[f"c{i}_u"], rtol=1e-14, atol=1e-14)
+        Ak, Bk = qp_oracle.linearize(X[0], U[0], 0.1)
+        np.testing.assert_allclose(Ak, f[f"c{i}_A0"], rtol=1e-15)
+        np.testing.assert_allclose(Bk, f[f"c{i}_B0"], rtol=1e-15)
+        np.testing.assert_array_equal(qp_oracle.to_vector(X, U), f[f"c{i}_zvec"])
+    # pattern depends on values
+    assert len(f["c0_A_data"]) == 654 and len(f["c1_A_data"]) == 734
+
+
+def test_f7_initial_conditions():
+    f = golden("f7_mc_initial_conditions.npz")
+    x0 = np.array([mc_oracle.sample_initial_condition(42 + i) for i in range(1024)])
+    np.testing.assert_array_equal(x0, f["x0_run_experiments"])
+    x0d = np.array([mc_oracle.sample_initial_condition(42 + i, mc_oracle.DEFAULT_CFG) for i in range(16)])
+    np.testing.assert_array_equal(x0d, f["x0_default"])
+
+
+def test_f8_check_landing():
+    f = golden("f8_check_landing.npz")
+    for k, cfg in enumerate((mc_oracle.DEFAULT_CFG, mc_oracle.RUN_EXPERIMENTS_CFG)):
+        for s, m, ok, reason in zip(f["states"], f["m0"], f["ok"][k], f["reason"][k]):
+            r = mc_oracle.check_landing(s, m, cfg)
+            assert int(r[0]) == int(ok) and r[1] == str(reason)
+
+
+def _qp_case(seed, N=20):
+    rs = np.random.RandomState(seed)
+    x0 = np.array([2.0, 30, 1, -1, -3, 0.2, 0.1]) + rs.randn(7) * [0.1, 3, 1, 1, 0.5, 0.2, 0.2]
+    xt = mc_oracle.incremental_target(x0)
+    X, U = qp_oracle.initial_guess(x0, xt, N)
+    P, q = qp_oracle.cost(N, np.tile(xt, (N + 1, 1)))
+    A, l, u = qp_oracle.constraints(X, U, x0, 0.1, gp_dv=rs.randn(N, 3) * 0.01, sign=-1.0)
+    return P, q, A, l, u, qp_oracle.to_vector(X, U)
+
+
+@pytest.mark.parametrize("seed", [0, 1, 2, 3, 4, 5])
+def test_admm_c_port_matches_numpy_kkt_oracle(seed):
+    """The fast C restatement (reduced banded KKT) vs the numpy KKT-LU restatement:
+    identical status / iteration counts / adaptive-rho decisions, x within 1e-6 rel."""
+    P, q, A, l, u, xw = _qp_case(seed)
+    a = admm_oracle.OSQPOracle(P, q, A, l, u); a.warm_start_x(xw)
+    b = admm_ref.RefQP(A.shape[0])
+    for rep in range(2):
+        ra = a.solve(); rb = b.solve(P.diagonal(), q, A, l, u, xw)
+        assert ra["status"] == rb["status"] and ra["iter"] == rb["iter"]
+        assert abs(ra["rho"] - rb["rho"]) <= 1e-6 * ra["rho"]
+        ok, e = close(rb["x"], ra["x"], np.max(np.abs(ra["x"]))); assert ok, e
+        a.update(P, q, A, l, u); a.warm_start_x(ra["x"]); xw = rb["x"]
+
+
+def test_admm_kkt_optimality():
+    """Solved QPs satisfy the OSQP termination criteria in unscaled terms."""
+    P, q, A, l, u, xw = _qp_case(11)
+    r = admm_ref.RefQP(A.shape[0])
+    for _ in range(3):
+        res = r.solve(P.diagonal(), q, A, l, u, xw)
+        xw = res["x"]
+    assert res["status"] in (1, 2)
+    Ax = A @ res["x"]
+    assert np.all(Ax >= l - 1e-2) and np.all(Ax <= u + 1e-2)
