@@ -1,0 +1,312 @@
+"""ctypes binding of libgpmpc_hip.so (include/gpmpc.h).
+
+The product path has no CPU fallback: importing this module without the built
+HIP library raises, and every call goes through the C-ABI.  Build with
+``python -c "import __graft_entry__ as g; g.build()"`` (hipcc, gfx950).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libgpmpc_hip.so")
+
+SE_ARD, SE_ISO, MATERN32, MATERN52 = 0, 1, 2, 3
+ERR_NOT_PD = -100
+REC_LEN = 16
+
+QP_STATUS = {1: "solved", 2: "solved inaccurate", -2: "maximum iterations reached",
+             -3: "primal infeasible", 3: "primal infeasible inaccurate", -4: "dual infeasible",
+             4: "dual infeasible inaccurate", -7: "problem non convex", -10: "unsolved"}
+
+if not os.path.exists(LIB_PATH):
+    raise ImportError(f"HIP library missing: {LIB_PATH} (build it with __graft_entry__.build(); "
+                      "there is no CPU fallback)")
+
+_L = ctypes.CDLL(LIB_PATH)
+_dp = ctypes.POINTER(ctypes.c_double)
+_ip = ctypes.POINTER(ctypes.c_int)
+_vp = ctypes.c_void_p
+
+
+class QPSettings(ctypes.Structure):
+    _fields_ = [("rho", ctypes.c_double), ("sigma", ctypes.c_double), ("alpha", ctypes.c_double),
+                ("eps_abs", ctypes.c_double), ("eps_rel", ctypes.c_double),
+                ("eps_prim_inf", ctypes.c_double), ("eps_dual_inf", ctypes.c_double),
+                ("max_iter", ctypes.c_int), ("check_termination", ctypes.c_int),
+                ("adaptive_rho", ctypes.c_int), ("adaptive_rho_interval", ctypes.c_int),
+                ("adaptive_rho_tolerance", ctypes.c_double), ("scaling", ctypes.c_int),
+                ("warm_start", ctypes.c_int)]
+
+
+class FleetConfig(ctypes.Structure):
+    _fields_ = [("horizon", ctypes.c_int), ("dt", ctypes.c_double), ("target_mode", ctypes.c_int),
+                ("use_gp", ctypes.c_int), ("residual_model", ctypes.c_int),
+                ("max_steps", ctypes.c_int), ("qp", QPSettings)]
+
+
+def _sig(name, res, *args):
+    f = getattr(_L, name)
+    f.restype = res
+    f.argtypes = list(args)
+    return f
+
+
+_c = ctypes.c_int
+_sig("gpmpc_abi_version", _c)
+_sig("gpmpc_last_error", ctypes.c_char_p)
+_sig("gpmpc_ctx_create", _c, _c, ctypes.POINTER(_vp))
+_sig("gpmpc_ctx_destroy", _c, _vp)
+_sig("gpmpc_ctx_sync", _c, _vp)
+_sig("gpmpc_ctx_stream", _vp, _vp)
+_sig("gpmpc_gram", _c, _vp, _c, _dp, _c, _dp, _c, _c, _dp, ctypes.c_double, _dp, _c)
+_sig("gpmpc_potrf", _c, _vp, _c, _dp, _c, _ip)
+_sig("gpmpc_potrf_batched_dev", _c, _vp, _c, _c, _vp, _c, ctypes.c_int64, _vp)
+_sig("gpmpc_trsm_lower", _c, _vp, _c, _c, _dp, _c, _dp, _c)
+_sig("gpmpc_potrs", _c, _vp, _c, _c, _dp, _c, _dp, _c)
+_sig("gpmpc_gp_fit_exact", _c, _vp, _c, _dp, _c, _c, _dp, _c, _dp, ctypes.c_double,
+     ctypes.c_double, ctypes.POINTER(_vp), _dp, _dp, _dp, _ip)
+_sig("gpmpc_gp_predict", _c, _vp, _vp, _dp, _c, _dp, _dp)
+_sig("gpmpc_gp_predict_cov", _c, _vp, _vp, _dp, _c, _dp, _dp)
+_sig("gpmpc_gp_get_state", _c, _vp, _vp, _dp, _dp)
+_sig("gpmpc_gp_destroy", _c, _vp)
+_sig("gpmpc_fitc_fit", _c, _vp, _dp, _c, _dp, _c, _c, _dp, _c, _dp, ctypes.c_double,
+     ctypes.c_double, ctypes.c_double, ctypes.POINTER(_vp), _dp, _dp, _dp, _dp)
+_sig("gpmpc_fitc_predict", _c, _vp, _vp, _dp, _c, _dp, _dp)
+_sig("gpmpc_fitc_destroy", _c, _vp)
+_sig("gpmpc_qp_default_settings", None, ctypes.POINTER(QPSettings))
+_sig("gpmpc_qp_solve_batched", _c, _vp, _c, _c, _c, _c, _ip, _ip, _dp, _dp, _dp, _dp, _dp,
+     ctypes.POINTER(QPSettings), _dp, _dp, _dp, _dp, _dp, _ip, _ip, _dp)
+_sig("gpmpc_fleet_default_config", None, ctypes.POINTER(FleetConfig))
+_sig("gpmpc_fleet_create", _c, _vp, _vp, ctypes.POINTER(FleetConfig), _c, ctypes.POINTER(_vp))
+_sig("gpmpc_fleet_reset", _c, _vp, _c, _c, _dp)
+_sig("gpmpc_fleet_step", _c, _vp, _c)
+_sig("gpmpc_fleet_read", _c, _vp, _dp, _dp)
+_sig("gpmpc_fleet_records_dev", _vp, _vp)
+_sig("gpmpc_fleet_destroy", _c, _vp)
+
+EXPORTED = ["gpmpc_abi_version", "gpmpc_last_error", "gpmpc_ctx_create", "gpmpc_ctx_destroy",
+            "gpmpc_ctx_sync", "gpmpc_ctx_stream", "gpmpc_gram", "gpmpc_potrf",
+            "gpmpc_potrf_batched_dev", "gpmpc_trsm_lower", "gpmpc_potrs", "gpmpc_gp_fit_exact",
+            "gpmpc_gp_predict", "gpmpc_gp_predict_cov", "gpmpc_gp_get_state", "gpmpc_gp_destroy",
+            "gpmpc_fitc_fit", "gpmpc_fitc_predict", "gpmpc_fitc_destroy",
+            "gpmpc_qp_default_settings", "gpmpc_qp_solve_batched", "gpmpc_fleet_default_config",
+            "gpmpc_fleet_create", "gpmpc_fleet_reset", "gpmpc_fleet_step", "gpmpc_fleet_read",
+            "gpmpc_fleet_records_dev", "gpmpc_fleet_destroy"]
+
+
+class HIPError(RuntimeError):
+    pass
+
+
+def _err(rc, what):
+    msg = _L.gpmpc_last_error().decode(errors="replace")
+    raise HIPError(f"{what} failed ({rc}): {msg}")
+
+
+def _chk(rc, what):
+    if rc != 0:
+        _err(rc, what)
+
+
+def _d(a):
+    return a.ctypes.data_as(_dp)
+
+
+def _i(a):
+    return a.ctypes.data_as(_ip)
+
+
+def f64(a):
+    return np.ascontiguousarray(a, dtype=np.float64)
+
+
+def abi_version():
+    return _L.gpmpc_abi_version()
+
+
+class Context:
+    """One HIP device + stream (gpmpc_ctx)."""
+
+    def __init__(self, device=0):
+        h = _vp()
+        _chk(_L.gpmpc_ctx_create(int(device), ctypes.byref(h)), "gpmpc_ctx_create")
+        self.h = h
+        self.device = device
+
+    @property
+    def stream(self):
+        return _L.gpmpc_ctx_stream(self.h)
+
+    def sync(self):
+        _chk(_L.gpmpc_ctx_sync(self.h), "gpmpc_ctx_sync")
+
+    def close(self):
+        if self.h:
+            _L.gpmpc_ctx_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+_default_ctx = None
+
+
+def default_context():
+    global _default_ctx
+    if _default_ctx is None:
+        _default_ctx = Context(int(os.environ.get("GPMPC_DEVICE", "0")))
+    return _default_ctx
+
+
+# ---- thin wrappers -----------------------------------------------------------
+def gram(ctx, kind, X1, X2, ls, sigma2):
+    X1 = f64(np.atleast_2d(X1)); n1, d = X1.shape
+    ls = f64(np.atleast_1d(ls))
+    if ls.size == 1 and kind != SE_ISO:
+        ls = np.full(d, float(ls[0]))
+    if X2 is None:
+        K = np.empty((n1, n1))
+        _chk(_L.gpmpc_gram(ctx.h, kind, _d(X1), n1, None, n1, d, _d(ls), float(sigma2), _d(K), n1), "gram")
+        return K
+    X2 = f64(np.atleast_2d(X2)); n2 = X2.shape[0]
+    K = np.empty((n1, n2))
+    _chk(_L.gpmpc_gram(ctx.h, kind, _d(X1), n1, _d(X2), n2, d, _d(ls), float(sigma2), _d(K), n2), "gram")
+    return K
+
+
+def potrf(ctx, A):
+    """Lower Cholesky of A (returns L with a zero upper triangle) and LAPACK info."""
+    A = f64(A).copy(); n = A.shape[0]
+    info = np.zeros(1, np.int32)
+    rc = _L.gpmpc_potrf(ctx.h, n, _d(A), n, _i(info))
+    if rc < 0:
+        _err(rc, "potrf")
+    return np.tril(A), int(info[0])
+
+
+def trsm_lower(ctx, L, B):
+    L = f64(L); B = f64(B).copy()
+    vec = B.ndim == 1
+    if vec:
+        B = B[:, None].copy()
+    _chk(_L.gpmpc_trsm_lower(ctx.h, L.shape[0], B.shape[1], _d(L), L.shape[0], _d(B), B.shape[1]), "trsm")
+    return B[:, 0] if vec else B
+
+
+def potrs(ctx, L, B):
+    L = f64(L); B = f64(B).copy()
+    vec = B.ndim == 1
+    if vec:
+        B = B[:, None].copy()
+    _chk(_L.gpmpc_potrs(ctx.h, L.shape[0], B.shape[1], _d(L), L.shape[0], _d(B), B.shape[1]), "potrs")
+    return B[:, 0] if vec else B
+
+
+class ExactGPHandle:
+    """Device-resident exact GP (shared factor across outputs)."""
+
+    def __init__(self, ctx, kind, X, Y, ls, sigma2, noise):
+        X = f64(np.atleast_2d(X)); Y = f64(Y)
+        if Y.ndim == 1:
+            Y = Y[:, None]
+        n, d = X.shape; no = Y.shape[1]
+        ls = f64(np.atleast_1d(ls))
+        if ls.size == 1 and kind != SE_ISO:
+            ls = np.full(d, float(ls[0]))
+        self.ctx = ctx; self.n = n; self.d = d; self.n_out = no
+        self.y_mean = np.empty(no); self.y_std = np.empty(no); self.lml = np.empty(no)
+        js = np.zeros(1, np.int32)
+        h = _vp()
+        rc = _L.gpmpc_gp_fit_exact(ctx.h, kind, _d(X), n, d, _d(Y), no, _d(ls), float(sigma2),
+                                   float(noise), ctypes.byref(h), _d(self.y_mean), _d(self.y_std),
+                                   _d(self.lml), _i(js))
+        if rc == ERR_NOT_PD:
+            raise ValueError("Kernel matrix is not positive definite even with jitter")
+        _chk(rc, "gp_fit_exact")
+        self.h = h
+        self.jitter_steps = int(js[0])
+
+    def predict(self, Xq):
+        Xq = f64(np.atleast_2d(Xq)); p = Xq.shape[0]
+        mean = np.empty((p, self.n_out)); var = np.empty((p, self.n_out))
+        _chk(_L.gpmpc_gp_predict(self.ctx.h, self.h, _d(Xq), p, _d(mean), _d(var)), "gp_predict")
+        return mean, var
+
+    def predict_cov(self, Xq):
+        Xq = f64(np.atleast_2d(Xq)); p = Xq.shape[0]
+        mean = np.empty((p, self.n_out)); cov = np.empty((p, p))
+        _chk(_L.gpmpc_gp_predict_cov(self.ctx.h, self.h, _d(Xq), p, _d(mean), _d(cov)), "gp_predict_cov")
+        return mean, cov
+
+    def state(self):
+        L = np.empty((self.n, self.n)); a = np.empty((self.n, self.n_out))
+        _chk(_L.gpmpc_gp_get_state(self.ctx.h, self.h, _d(L), _d(a)), "gp_get_state")
+        return L, a
+
+    def __del__(self):
+        try:
+            if getattr(self, "h", None):
+                _L.gpmpc_gp_destroy(self.h)
+                self.h = None
+        except Exception:
+            pass
+
+
+class FITCHandle:
+    def __init__(self, ctx, Z, X, Y, ls, sigma2, noise, jitter=1e-6):
+        Z = f64(np.atleast_2d(Z)); X = f64(np.atleast_2d(X)); Y = f64(Y)
+        if Y.ndim == 1:
+            Y = Y[:, None]
+        m, d = Z.shape; n = X.shape[0]; no = Y.shape[1]
+        ls = f64(np.atleast_1d(ls))
+        if ls.size == 1:
+            ls = np.full(d, float(ls[0]))
+        self.ctx = ctx; self.n_out = no; self.m = m
+        self.y_mean = np.empty(no); self.y_std = np.empty(no); self.lml = np.empty(no)
+        self.lam = np.empty(n)
+        h = _vp()
+        rc = _L.gpmpc_fitc_fit(ctx.h, _d(Z), m, _d(X), n, d, _d(Y), no, _d(ls), float(sigma2),
+                               float(noise), float(jitter), ctypes.byref(h), _d(self.y_mean),
+                               _d(self.y_std), _d(self.lml), _d(self.lam))
+        if rc > 0:
+            raise np.linalg.LinAlgError(_L.gpmpc_last_error().decode())
+        _chk(rc, "fitc_fit")
+        self.h = h
+
+    def predict(self, Xq):
+        Xq = f64(np.atleast_2d(Xq)); p = Xq.shape[0]
+        mean = np.empty((p, self.n_out)); var = np.empty((p, self.n_out))
+        _chk(_L.gpmpc_fitc_predict(self.ctx.h, self.h, _d(Xq), p, _d(mean), _d(var)), "fitc_predict")
+        return mean, var
+
+    def __del__(self):
+        try:
+            if getattr(self, "h", None):
+                _L.gpmpc_fitc_destroy(self.h)
+                self.h = None
+        except Exception:
+            pass
+
+
+def qp_default_settings(**kw):
+    s = QPSettings()
+    _L.gpmpc_qp_default_settings(ctypes.byref(s))
+    for k, v in kw.items():
+        setattr(s, k, v)
+    return s
+
+
+def fleet_default_config(**kw):
+    c = FleetConfig()
+    _L.gpmpc_fleet_default_config(ctypes.byref(c))
+    for k, v in kw.items():
+        setattr(c, k, v)
+    return c

@@ -193,12 +193,9 @@ hipError_t launch_potrf_batched(hipStream_t s, int n, int batch, double *A, int6
 
 hipError_t launch_potrf_batched(hipStream_t s, int n, int batch, double *A, int64_t lda,
                                 int64_t stride, int *info) {
-  double *Linv = nullptr;
-  hipError_t e = hipMallocAsync((void **)&Linv, sizeof(double) * NB * NB * batch, s);
-  if (e != hipSuccess) return e;
-  e = launch_potrf_batched(s, n, batch, A, lda, stride, info, Linv);
-  hipError_t e2 = hipFreeAsync(Linv, s);
-  return e != hipSuccess ? e : e2;
+  double *Linv = (double *)gpmpc_scratch(1, sizeof(double) * NB * NB * (size_t)batch);
+  if (!Linv) return hipErrorOutOfMemory;
+  return launch_potrf_batched(s, n, batch, A, lda, stride, info, Linv);
 }
 
 // ---------------------------------------------------------------------------
@@ -233,6 +230,15 @@ __global__ __launch_bounds__(64) void k_tri_inv_blocks(int n, const double *L, i
   for (int e = tid; e < NB * NB; e += 64) Linv[(int64_t)ib * NB * NB + e] = inv[e / NB][e % NB];
 }
 
+// Solved row blocks of X are stored to global memory and re-read by other waves
+// of the same workgroup in later steps.  The vector L1 is not refreshed by those
+// stores (a line cached by the step's first read would be served stale), so every
+// X read goes round L1 (agent-scope relaxed load = global_load sc1) and every
+// step drains its stores (s_waitcnt vmcnt(0)) before the barrier.
+__device__ __forceinline__ double ld_l2(const double *p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // X (n x nrhs, ld ldx) <- op(L)^-1 X ; op = L (trans=0) or L^T (trans=1)
 // rhs_lower: X is known lower-triangular (X[r][c] = 0 for r < c, e.g. identity):
 // the forward walk starts at the panel's first column.
@@ -255,7 +261,7 @@ __global__ __launch_bounds__(256) void k_trsm_panel(int n, int nrhs, const doubl
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
       int c = c0 + cc + q;
-      acc[q] = (rr < nbi && c < nrhs) ? X[(int64_t)(r0 + rr) * ldx + c] : 0.0;
+      acc[q] = (rr < nbi && c < nrhs) ? ld_l2(X + (int64_t)(r0 + rr) * ldx + c) : 0.0;
     }
     // subtract contributions of already-solved blocks
     const int kb_lo = trans ? ib + 1 : ((rhs_lower) ? (c0 / NB) : 0);
@@ -277,7 +283,7 @@ __global__ __launch_bounds__(256) void k_trsm_panel(int n, int nrhs, const doubl
       for (int e = tid; e < NB * 64; e += 256) {
         int i = e / 64, j = e % 64;
         int c = c0 + j;
-        sX[i][j] = (i < nbk && c < nrhs) ? X[(int64_t)(k0 + i) * ldx + c] : 0.0;
+        sX[i][j] = (i < nbk && c < nrhs) ? ld_l2(X + (int64_t)(k0 + i) * ldx + c) : 0.0;
       }
       __syncthreads();
       for (int j = 0; j < NB; ++j) {
@@ -309,6 +315,7 @@ __global__ __launch_bounds__(256) void k_trsm_panel(int n, int nrhs, const doubl
       int c = c0 + cc + q;
       if (rr < nbi && c < nrhs) X[(int64_t)(r0 + rr) * ldx + c] = out[q];
     }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   }
 }
@@ -318,20 +325,12 @@ hipError_t launch_trsm_lower_ex(hipStream_t s, int n, int nrhs, const double *L,
                                 double *Linv_blocks /* may be null */) {
   const int nblk = (n + NB - 1) / NB;
   double *Linv = Linv_blocks;
-  hipError_t e = hipSuccess;
-  if (!Linv) {
-    e = hipMallocAsync((void **)&Linv, sizeof(double) * NB * NB * nblk, s);
-    if (e != hipSuccess) return e;
-  }
+  if (!Linv) Linv = (double *)gpmpc_scratch(0, sizeof(double) * NB * NB * (size_t)nblk);
+  if (!Linv) return hipErrorOutOfMemory;
   hipLaunchKernelGGL(k_tri_inv_blocks, dim3(nblk), dim3(64), 0, s, n, L, ldl, Linv);
   hipLaunchKernelGGL(k_trsm_panel, dim3((nrhs + 63) / 64), dim3(256), 0, s, n, nrhs, L, ldl, Linv,
                      X, ldx, trans, rhs_lower);
-  e = hipGetLastError();
-  if (!Linv_blocks) {
-    hipError_t e2 = hipFreeAsync(Linv, s);
-    if (e == hipSuccess) e = e2;
-  }
-  return e;
+  return hipGetLastError();
 }
 
 hipError_t launch_trsm_lower(hipStream_t s, int n, int nrhs, const double *L, int64_t ldl,

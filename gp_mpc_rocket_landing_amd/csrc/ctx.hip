@@ -12,6 +12,29 @@ void gpmpc_set_error(const char *fmt, ...) {
   va_end(ap);
 }
 
+// Persistent device scratch per (device, slot), grown with hipMalloc after a full
+// device sync.  (Stream-ordered hipMallocAsync scratch returned buffers the next
+// kernel on the same stream did not see written on ROCm 7.2 -- see DESIGN.md.)
+static std::mutex g_scratch_mu;
+static void *g_scratch[64][4];
+static size_t g_scratch_bytes[64][4];
+
+void *gpmpc_scratch(int slot, size_t bytes) {
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  std::lock_guard<std::mutex> lk(g_scratch_mu);
+  if (dev < 0 || dev >= 64 || slot < 0 || slot >= 4) return nullptr;
+  if (g_scratch_bytes[dev][slot] < bytes) {
+    (void)hipDeviceSynchronize();
+    if (g_scratch[dev][slot]) (void)hipFree(g_scratch[dev][slot]);
+    g_scratch[dev][slot] = nullptr;
+    g_scratch_bytes[dev][slot] = 0;
+    if (hipMalloc(&g_scratch[dev][slot], bytes) != hipSuccess) return nullptr;
+    g_scratch_bytes[dev][slot] = bytes;
+  }
+  return g_scratch[dev][slot];
+}
+
 extern "C" int gpmpc_abi_version(void) { return GPMPC_ABI_VERSION; }
 extern "C" const char *gpmpc_last_error(void) { return g_err; }
 

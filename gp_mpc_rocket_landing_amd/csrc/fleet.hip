@@ -1,0 +1,505 @@
+// fleet.hip -- a batch of closed-loop 3-DoF GP-MPC landings, device-resident.
+//
+// One control step for every landing b:
+//   1. k_fleet_queries   Simple3DoF features (features.py:403-444) of the N
+//                        horizon points of b's linearisation trajectory
+//                        (X_lin, U_lin = shifted previous solution: RTI), scaled
+//                        by the kernel lengthscales;
+//   2. GP posterior      K* = k(Z*, X) (gram kernel), mean = K* alpha and
+//                        var = sigma2 - |L^-1 K*^T|^2 on the FP64-MFMA GEMM with
+//                        fused sum-of-squares epilogue (gemm.hip) -- all B*N
+//                        queries in one batched pass over one shared factor;
+//   3. k_fleet_control   one workgroup per landing: Monte-Carlo termination
+//                        checks (monte_carlo.py:455-488), target (monte_carlo.py
+//                        :497-500 or fixed), RTI QP assembly with analytic
+//                        Jacobians (osqp_rti.py:656-710) and the GP mean on the
+//                        velocity rows of c_k with the correct sign (gp_mpc.py
+//                        :309-314, 410-411), the OSQP-style ADMM of
+//                        qp_device.h, the plant step (nominal Euler + the aero
+//                        residual the GP learns) and the warm-start shift.
+#include "internal.h"
+#include "gemm.h"
+#include "qp.h"
+#include <vector>
+
+#define NX 7
+#define NU 3
+#define NFEAT 11
+#define DYN_NNZ 26
+
+struct gpmpc_fleet {
+  gpmpc_ctx *ctx = nullptr;
+  gpmpc_gp *gp = nullptr;
+  gpmpc_fleet_config cfg{};
+  int B = 0, N = 0, n = 0, m = 0;
+  QPPatternHost pat;
+  DevBuf x, Xw, Uw, ysc, rho, rec, xt;      // landing state
+  DevBuf Q, Qn, Ks, part, meanT, mean, var;  // GP scratch
+};
+
+extern "C" void gpmpc_fleet_default_config(gpmpc_fleet_config *c) {
+  c->horizon = 20;           // BASELINE config: N = 20
+  c->dt = 0.1;               // MPCConfig.dt / SimulationConfig.dt
+  c->target_mode = 1;        // solve protocol of MonteCarloSimulator (GPMPC surface)
+  c->use_gp = 1;
+  c->residual_model = 1;
+  c->max_steps = 300;        // run_experiments.py SimulationConfig max_time 30 s / dt
+  gpmpc_qp_default_settings(&c->qp);
+}
+
+// ---------------------------------------------------------------------------
+// structural CSR of the 3-DoF MPC QP (unfiltered: SURVEY D3 zeros kept)
+static void mpc_pattern(int N, std::vector<int> &rp, std::vector<int> &ci) {
+  const int n = (N + 1) * NX + N * NU, m = NX * (N + 1) + n;
+  rp.assign(1, 0);
+  ci.clear();
+  auto row = [&](std::initializer_list<int> cols) {
+    for (int c : cols) ci.push_back(c);
+    rp.push_back((int)ci.size());
+  };
+  for (int i = 0; i < NX; ++i) row({i});
+  for (int k = 0; k < N; ++k) {
+    const int o = k * (NX + NU), on = (k + 1) * (NX + NU);
+    row({o + 0, o + 7, o + 8, o + 9, on + 0});  // mass: A00, B0j, -1
+    row({o + 1, o + 4, on + 1});                // r: A_ii, dt, -1
+    row({o + 2, o + 5, on + 2});
+    row({o + 3, o + 6, on + 3});
+    row({o + 0, o + 4, o + 7, on + 4});         // v: A_i0, A_ii, B, -1
+    row({o + 0, o + 5, o + 8, on + 5});
+    row({o + 0, o + 6, o + 9, on + 6});
+  }
+  for (int j = 0; j < n; ++j) row({j});
+  (void)m;
+}
+
+__device__ __forceinline__ void features3(const double *x, const double *u, double *z) {
+  // Simple3DoFFeatureExtractor.extract (features.py:403-444)
+  const double vx = x[4], vy = x[5], vz = x[6], alt = x[1];
+  const double speed = sqrt(vx * vx + vy * vy + vz * vz);
+  const double rho = 1.225 * exp(-alt / 8500.0);
+  const double qd = 0.5 * rho * speed * speed;
+  const double tm = sqrt(u[0] * u[0] + u[1] * u[1] + u[2] * u[2]);
+  z[0] = vx / 10.0; z[1] = vy / 10.0; z[2] = vz / 10.0; z[3] = speed / 10.0;
+  z[4] = qd / (0.5 * 1.225 * 100.0);
+  z[5] = u[0] / 10.0; z[6] = u[1] / 10.0; z[7] = u[2] / 10.0; z[8] = tm / 10.0;
+  z[9] = alt / 100.0; z[10] = rho / 1.225;
+}
+
+__global__ void k_fleet_queries(int B, int N, const double *__restrict__ Xw,
+                                const double *__restrict__ Uw, const double *__restrict__ ls,
+                                int iso, double *__restrict__ Q, double *__restrict__ Qn) {
+  const int g = blockIdx.x * blockDim.x + threadIdx.x;  // = b*N + k
+  if (g >= B * N) return;
+  const int b = g / N, k = g - b * N;
+  double z[NFEAT];
+  features3(Xw + ((int64_t)b * (N + 1) + k) * NX, Uw + ((int64_t)b * N + k) * NU, z);
+  double s = 0.0;
+#pragma unroll
+  for (int f = 0; f < NFEAT; ++f) {
+    const double v = iso ? z[f] : z[f] / ls[f];
+    Q[(int64_t)g * NFEAT + f] = v;
+    s += v * v;
+  }
+  Qn[g] = s;
+}
+
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void plant_euler(const double *x, const double *u, double dt,
+                                            double *o) {
+  // nominal_mpc.py:585-605 (alpha = 1/(I_sp g0) = 1/30, g = [-1, 0, 0])
+  const double tm = sqrt(u[0] * u[0] + u[1] * u[1] + u[2] * u[2]);
+  o[0] = x[0] - dt * (1.0 / 30.0) * tm;
+  o[1] = x[1] + dt * x[4];
+  o[2] = x[2] + dt * x[5];
+  o[3] = x[3] + dt * x[6];
+  o[4] = x[4] + dt * (u[0] / x[0] + -1.0);
+  o[5] = x[5] + dt * (u[1] / x[0] + 0.0);
+  o[6] = x[6] + dt * (u[2] / x[0] + 0.0);
+}
+
+__device__ __forceinline__ void drag_residual(const double *x, double *d) {
+  // experiments/dispersion.py:349-360: rho 0.02, Cd = A = 1, |v| > 1
+  const double vx = x[4], vy = x[5], vz = x[6];
+  const double sp = sqrt(vx * vx + vy * vy + vz * vz);
+  if (sp > 1.0) {
+    const double a = (0.5 * 0.02 * 1.0 * 1.0 * sp * sp) / x[0];
+    d[0] = -a * (vx / sp); d[1] = -a * (vy / sp); d[2] = -a * (vz / sp);
+  } else {
+    d[0] = d[1] = d[2] = 0.0;
+  }
+}
+
+__device__ __forceinline__ bool landing_ok(const double *x, double m0) {
+  // LandingConstraints.check_landing (monte_carlo.py:54-104), run_experiments.py tolerances
+  if (fabs(x[1]) > 1.0) return false;
+  if (fabs(x[2]) > 5.0 || fabs(x[3]) > 5.0) return false;
+  if (fabs(x[4]) > 3.0) return false;
+  if (fabs(x[5]) > 1.0 || fabs(x[6]) > 1.0) return false;
+  if (1.0 - x[0] / m0 > 1.0 - 0.05) return false;
+  return true;
+}
+
+struct FleetArgs {
+  QPPattern pt;
+  QPSettingsDev st;
+  int N, target_mode, use_gp, residual_model, max_steps;
+  double dt;
+  double *x, *Xw, *Uw, *ysc, *rho, *rec, *xt;
+  const double *gmean;  // (B*N) x 3
+};
+
+__global__ __launch_bounds__(256) void k_fleet_control(FleetArgs a) {
+  __shared__ QPSmemStd s;
+  __shared__ double sx[NX], st_tgt[NX];
+  __shared__ int s_out;
+  const int b = blockIdx.x, tid = threadIdx.x, nt = blockDim.x;
+  const int N = a.N, n = a.pt.n, m = a.pt.m;
+  const double dt = a.dt;
+  double *rec = a.rec + (int64_t)b * GPMPC_REC_LEN;
+  if (rec[0] != 0.0) return;  // terminated landing
+  double *x = a.x + (int64_t)b * NX;
+  double *Xw = a.Xw + (int64_t)b * (N + 1) * NX;
+  double *Uw = a.Uw + (int64_t)b * N * NU;
+  if (tid < NX) sx[tid] = x[tid];
+  __syncthreads();
+  // ---- termination checks at the top of the step (monte_carlo.py:458-488)
+  if (tid == 0) {
+    int out = 0;
+    const double m0 = rec[13];
+    bool div = false;
+    for (int i = 0; i < NX; ++i) div = div || !(fabs(sx[i]) <= 1e6);
+    if ((int)rec[1] >= a.max_steps) out = 5;                    // TIMEOUT
+    else if (sx[1] < 0.0) out = 2;                              // CRASH
+    else if (sx[0] <= 1.0 + 0.01) out = 3;                      // FUEL_EXHAUSTED
+    else if (div) out = 6;                                      // DIVERGENCE
+    else if (sx[1] < 1.0 && fabs(sx[4]) < 5.0) out = landing_ok(sx, m0) ? 1 : 4;
+    s_out = out;
+    // target: incremental (monte_carlo.py:497-500) or fixed
+    for (int i = 0; i < NX; ++i) st_tgt[i] = a.target_mode ? sx[i] : a.xt[(int64_t)b * NX + i];
+    if (a.target_mode) {
+      st_tgt[4] = st_tgt[5] = st_tgt[6] = 0.0;
+      st_tgt[1] = fmax(0.5, sx[1] - 2.0);
+    }
+  }
+  __syncthreads();
+  if (s_out) {
+    if (tid == 0) {
+      rec[0] = s_out;
+      rec[2] = rec[13] - sx[0];
+      for (int i = 0; i < NX; ++i) rec[4 + i] = sx[i];
+    }
+    return;
+  }
+  // ---- QP data (osqp_rti.py:203-372 with the GPMPC sign), straight into LDS
+  const int Nv = N * (NX + NU);
+  for (int j = tid; j < n; j += nt) {
+    double p, qq;
+    if (j >= Nv) {               // x_N block: Q_f = 10 Q
+      const int i = j - Nv;
+      const double qd = (i == 0) ? 0.0 : (i < 4 ? 100.0 : 10.0);
+      p = qd; qq = -qd * st_tgt[i];
+    } else {
+      const int k = j / (NX + NU), i = j - k * (NX + NU);
+      if (i < NX) {
+        const double qd = (i == 0) ? 0.0 : (i < 4 ? 10.0 : 1.0);
+        p = qd; qq = -qd * st_tgt[i];
+      } else {
+        p = 0.01; qq = 0.0;
+      }
+      (void)k;
+    }
+    s.P[j] = p;
+    s.q[j] = qq;
+    // warm start / linearisation point vector
+    if (j >= Nv) s.x[j] = Xw[N * NX + (j - Nv)];
+    else {
+      const int k = j / (NX + NU), i = j - k * (NX + NU);
+      s.x[j] = (i < NX) ? Xw[k * NX + i] : Uw[k * NU + (i - NX)];
+    }
+  }
+  // x0 rows and bound rows
+  for (int r = tid; r < m; r += nt) {
+    if (r < NX) {
+      s.A[r] = 1.0;
+      s.l[r] = sx[r];
+      s.u[r] = sx[r];
+    } else if (r >= NX * (N + 1)) {
+      const int j = r - NX * (N + 1);
+      s.A[NX + N * DYN_NNZ + j] = 1.0;
+      double lo, hi;
+      const int i = (j >= Nv) ? j - Nv : j % (NX + NU);
+      if (i < NX) {
+        const double xmin[NX] = {-INFINITY, -100, -100, -100, -50, -50, -50};
+        const double xmax[NX] = {INFINITY, 500, 100, 100, 50, 50, 50};
+        lo = xmin[i]; hi = xmax[i];
+      } else {
+        const double umin[NU] = {0.3, -5, -5}, umax[NU] = {5, 5, 5};
+        lo = umin[i - NX]; hi = umax[i - NX];
+      }
+      s.l[r] = lo;
+      s.u[r] = hi;
+    }
+  }
+  // dynamics blocks: one thread per stage k
+  for (int k = tid; k < N; k += nt) {
+    const double *xk = Xw + k * NX;
+    const double *uk = Uw + k * NU;
+    const double mk = xk[0], tx = uk[0], ty = uk[1], tz = uk[2];
+    const double tm = sqrt(tx * tx + ty * ty + tz * tz) + 1e-10;
+    const double al = 1.0 / 30.0;
+    // FastRTI3DoF._linearize (osqp_rti.py:656-710)
+    const double a40 = -tx / (mk * mk) * dt, a50 = -ty / (mk * mk) * dt, a60 = -tz / (mk * mk) * dt;
+    const double b00 = -al * tx / tm * dt, b01 = -al * ty / tm * dt, b02 = -al * tz / tm * dt;
+    const double bv = dt / mk;
+    double *Ak = s.A + NX + k * DYN_NNZ;
+    Ak[0] = 1.0; Ak[1] = b00; Ak[2] = b01; Ak[3] = b02; Ak[4] = -1.0;
+    Ak[5] = 1.0; Ak[6] = dt; Ak[7] = -1.0;
+    Ak[8] = 1.0; Ak[9] = dt; Ak[10] = -1.0;
+    Ak[11] = 1.0; Ak[12] = dt; Ak[13] = -1.0;
+    Ak[14] = a40; Ak[15] = 1.0; Ak[16] = bv; Ak[17] = -1.0;
+    Ak[18] = a50; Ak[19] = 1.0; Ak[20] = bv; Ak[21] = -1.0;
+    Ak[22] = a60; Ak[23] = 1.0; Ak[24] = bv; Ak[25] = -1.0;
+    // c_k = f(x,u) - A x - B u (+ dt * GP mean on the velocity rows)
+    double f[NX];
+    plant_euler(xk, uk, dt, f);
+    // (f - A x) - B u, as osqp_rti.py:340-341 evaluates it
+    double ax[NX], bu[NX];
+    ax[0] = xk[0];
+    ax[1] = xk[1] + dt * xk[4];
+    ax[2] = xk[2] + dt * xk[5];
+    ax[3] = xk[3] + dt * xk[6];
+    ax[4] = a40 * xk[0] + xk[4];
+    ax[5] = a50 * xk[0] + xk[5];
+    ax[6] = a60 * xk[0] + xk[6];
+    bu[0] = b00 * tx + b01 * ty + b02 * tz;
+    bu[1] = bu[2] = bu[3] = 0.0;
+    bu[4] = bv * tx; bu[5] = bv * ty; bu[6] = bv * tz;
+    const double *gm = a.gmean + ((int64_t)b * N + k) * 3;
+    for (int i = 0; i < NX; ++i) {
+      double c = (f[i] - ax[i]) - bu[i];
+      if (a.use_gp && i >= 4) c += gm[i - 4] * dt;
+      const int r = NX * (k + 1) + i;
+      s.l[r] = -c;   // A x + B u - x+ = -c   <=>   x+ = A x + B u + c
+      s.u[r] = -c;
+    }
+  }
+  for (int r = tid; r < m; r += nt) s.y[r] = a.ysc[(int64_t)b * m + r];
+  if (tid == 0) s.rho_s = a.rho[b];
+  __syncthreads();
+  // ---- ADMM (qp_device.h)
+  QPResult res = qp_solve(a.pt, s, a.st);
+  const bool has = !res.factor_fail && (res.status == 1 || res.status == 2 || res.status == -2);
+  // ---- solution, plant step, warm-start shift
+  if (has) {
+    for (int j = tid; j < n; j += nt) s.x[j] = s.D[j] * s.x[j];  // unscale
+  }
+  __syncthreads();
+  if (!has && a.target_mode == 1) {  // solve protocol: failed solve -> DIVERGENCE
+    if (tid == 0) {
+      rec[0] = 6;
+      rec[14] = res.factor_fail ? -100 : res.status;
+      for (int i = 0; i < NX; ++i) rec[4 + i] = sx[i];
+      rec[2] = rec[13] - sx[0];
+    }
+    return;
+  }
+  if (has) {
+    // shifted solution -> next linearisation point (X[1:], X[-1]), (U[1:], U[-1])
+    for (int e = tid; e < (N + 1) * NX; e += nt) {
+      const int k = e / NX, i = e - k * NX;
+      const int ks = (k + 1 <= N) ? k + 1 : N;
+      const int src = (ks == N) ? Nv + i : ks * (NX + NU) + i;
+      Xw[e] = s.x[src];
+    }
+    for (int e = tid; e < N * NU; e += nt) {
+      const int k = e / NU, i = e - k * NU;
+      const int ks = (k + 1 < N) ? k + 1 : N - 1;
+      Uw[e] = s.x[ks * (NX + NU) + NX + i];
+    }
+    for (int r = tid; r < m; r += nt) a.ysc[(int64_t)b * m + r] = s.y[r];
+  }
+  if (tid == 0) {
+    double u0[NU];
+    if (has) {
+      u0[0] = s.x[NX]; u0[1] = s.x[NX + 1]; u0[2] = s.x[NX + 2];
+    } else {  // step protocol fallback: shifted previous plan (osqp_rti.py:546-552)
+      u0[0] = Uw[0]; u0[1] = Uw[1]; u0[2] = Uw[2];
+    }
+    double xn[NX], dr[3];
+    plant_euler(sx, u0, dt, xn);
+    if (a.residual_model) {
+      drag_residual(sx, dr);
+      xn[4] += dr[0] * dt; xn[5] += dr[1] * dt; xn[6] += dr[2] * dt;
+    }
+    for (int i = 0; i < NX; ++i) x[i] = xn[i];
+    a.rho[b] = s.rho_s;
+    rec[1] += 1.0;
+    rec[3] = rec[1] * dt;
+    rec[2] = rec[13] - xn[0];
+    for (int i = 0; i < NX; ++i) rec[4 + i] = xn[i];
+    rec[11] += res.iter;
+    rec[12] += (res.status == 1) ? 1.0 : 0.0;
+    rec[14] = res.factor_fail ? -100 : res.status;
+    rec[15] = s.rho_s;
+  }
+}
+
+// initial linearisation point: X linear to the target, U hover (osqp_rti.py:425-446)
+__global__ void k_fleet_reset(int first, int count, int N, int target_mode,
+                              const double *__restrict__ x0, double *x, double *Xw, double *Uw,
+                              double *ysc, int m, double *rho, double rho0, double *rec,
+                              double *xt) {
+  const int i = blockIdx.x;
+  if (i >= count) return;
+  const int b = first + i;
+  const double *xi = x0 + (int64_t)i * NX;
+  double tg[NX];
+  for (int c = 0; c < NX; ++c) tg[c] = 0.0;
+  tg[0] = xi[0];                       // x_target = [m0, 0, ...] (monte_carlo.py:428-430)
+  if (target_mode) {
+    for (int c = 0; c < NX; ++c) tg[c] = xi[c];
+    tg[4] = tg[5] = tg[6] = 0.0;
+    tg[1] = fmax(0.5, xi[1] - 2.0);
+  }
+  for (int e = threadIdx.x; e < (N + 1) * NX; e += blockDim.x) {
+    const int k = e / NX, c = e - k * NX;
+    const double al = (double)k / N;
+    Xw[(int64_t)b * (N + 1) * NX + e] = (1.0 - al) * xi[c] + al * tg[c];
+  }
+  for (int e = threadIdx.x; e < N * NU; e += blockDim.x)
+    Uw[(int64_t)b * N * NU + e] = (e % NU == 0) ? xi[0] * 1.0 : 0.0;
+  for (int r = threadIdx.x; r < m; r += blockDim.x) ysc[(int64_t)b * m + r] = 0.0;
+  if (threadIdx.x < GPMPC_REC_LEN) rec[(int64_t)b * GPMPC_REC_LEN + threadIdx.x] = 0.0;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int c = 0; c < NX; ++c) {
+      x[(int64_t)b * NX + c] = xi[c];
+      xt[(int64_t)b * NX + c] = tg[c];
+      rec[(int64_t)b * GPMPC_REC_LEN + 4 + c] = xi[c];
+    }
+    rec[(int64_t)b * GPMPC_REC_LEN + 13] = xi[0];
+    rho[b] = rho0;
+  }
+}
+
+// ---------------------------------------------------------------------------
+extern "C" int gpmpc_fleet_create(gpmpc_ctx *ctx, gpmpc_gp *gp, const gpmpc_fleet_config *cfg,
+                                  int batch, gpmpc_fleet **out) {
+  GPMPC_CHECK_ARG(ctx && gp && cfg && out && batch > 0);
+  const GpView g = gp_view(gp);
+  GPMPC_CHECK_ARG(g.d == NFEAT && g.n_out == 3);
+  const int N = cfg->horizon;
+  const int n = (N + 1) * NX + N * NU, m = NX * (N + 1) + n;
+  GPMPC_CHECK_ARG(N >= 1 && n <= QP_NMAX && m <= QP_MMAX && NX + N * DYN_NNZ + n <= QP_NNZMAX);
+  GPMPC_HIP(hipSetDevice(ctx->device));
+  auto *f = new gpmpc_fleet();
+  f->ctx = ctx; f->gp = gp; f->cfg = *cfg; f->B = batch; f->N = N; f->n = n; f->m = m;
+  std::vector<int> rp, ci;
+  mpc_pattern(N, rp, ci);
+  if (f->pat.build(n, m, rp.data(), ci.data(), ctx->stream) || f->pat.w > QP_W) {
+    delete f;
+    gpmpc_set_error("fleet: QP pattern setup failed");
+    return -1;
+  }
+  const size_t B = batch, P = (size_t)batch * N;
+  const int nrt = gemm_row_tiles(g.n);
+  if (f->x.alloc(sizeof(double) * B * NX) || f->Xw.alloc(sizeof(double) * B * (N + 1) * NX) ||
+      f->Uw.alloc(sizeof(double) * B * N * NU) || f->ysc.alloc(sizeof(double) * B * m) ||
+      f->rho.alloc(sizeof(double) * B) || f->rec.alloc(sizeof(double) * B * GPMPC_REC_LEN) ||
+      f->xt.alloc(sizeof(double) * B * NX) || f->Q.alloc(sizeof(double) * P * NFEAT) ||
+      f->Qn.alloc(sizeof(double) * P) || f->Ks.alloc(sizeof(double) * P * g.n) ||
+      f->part.alloc(sizeof(double) * nrt * P) || f->meanT.alloc(sizeof(double) * 3 * P) ||
+      f->mean.alloc(sizeof(double) * P * 3) || f->var.alloc(sizeof(double) * P * 3)) {
+    delete f;
+    gpmpc_set_error("fleet: out of device memory");
+    return -1;
+  }
+  // every landing starts terminated until reset
+  std::vector<double> r(B * GPMPC_REC_LEN, 0.0);
+  for (size_t b = 0; b < B; ++b) r[b * GPMPC_REC_LEN] = -1.0;
+  hipMemcpyAsync(f->rec.p, r.data(), sizeof(double) * r.size(), hipMemcpyHostToDevice, ctx->stream);
+  GPMPC_HIP(hipStreamSynchronize(ctx->stream));
+  *out = f;
+  return 0;
+}
+
+extern "C" int gpmpc_fleet_reset(gpmpc_fleet *f, int first, int count, const double *x0) {
+  GPMPC_CHECK_ARG(f && x0 && first >= 0 && count >= 0 && first + count <= f->B);
+  if (count == 0) return 0;
+  hipStream_t s = f->ctx->stream;
+  DevBuf d;
+  GPMPC_HIP(d.alloc(sizeof(double) * count * NX));
+  GPMPC_HIP(hipMemcpyAsync(d.p, x0, sizeof(double) * count * NX, hipMemcpyHostToDevice, s));
+  hipLaunchKernelGGL(k_fleet_reset, dim3(count), dim3(256), 0, s, first, count, f->N,
+                     f->cfg.target_mode, d.as<double>(), f->x.as<double>(), f->Xw.as<double>(),
+                     f->Uw.as<double>(), f->ysc.as<double>(), f->m, f->rho.as<double>(),
+                     f->cfg.qp.rho, f->rec.as<double>(), f->xt.as<double>());
+  GPMPC_HIP(hipGetLastError());
+  GPMPC_HIP(hipStreamSynchronize(s));
+  return 0;
+}
+
+static hipError_t fleet_gp_posterior(gpmpc_fleet *f) {
+  hipStream_t s = f->ctx->stream;
+  const GpView g = gp_view(f->gp);
+  const int P = f->B * f->N;
+  const int nrt = gemm_row_tiles(g.n);
+  hipLaunchKernelGGL(k_fleet_queries, dim3((P + 255) / 256), dim3(256), 0, s, f->B, f->N,
+                     f->Xw.as<double>(), f->Uw.as<double>(), g.ls, g.kind == GPMPC_SE_ISO,
+                     f->Q.as<double>(), f->Qn.as<double>());
+  hipError_t e = launch_gram(s, g.kind, f->Q.as<double>(), f->Qn.as<double>(), P, g.Xs, g.Xn, g.n,
+                             g.d, g.sigma2, g.iso_scale, f->Ks.as<double>(), g.n, 0);
+  if (e != hipSuccess) return e;
+  e = launch_gemm_nt(s, EPI_SUMSQ, g.n, P, g.n, g.W, g.n, f->Ks.as<double>(), g.n,
+                     f->part.as<double>(), P, 1.0, 0.0, 1, 0, 1, 0, 0, 0);
+  if (e != hipSuccess) return e;
+  e = launch_gemm_nt(s, EPI_STORE, 3, P, g.n, g.alphaT, g.n, f->Ks.as<double>(), g.n,
+                     f->meanT.as<double>(), P, 1.0, 0.0, 0, 0, 1, 0, 0, 0);
+  if (e != hipSuccess) return e;
+  return launch_post_finish(s, P, 3, nrt, f->part.as<double>(), P, f->meanT.as<double>(), P,
+                            g.ymean, g.ystd, g.sigma2, f->mean.as<double>(), f->var.as<double>());
+}
+
+extern "C" int gpmpc_fleet_step(gpmpc_fleet *f, int nsteps) {
+  GPMPC_CHECK_ARG(f && nsteps >= 0);
+  GPMPC_HIP(hipSetDevice(f->ctx->device));
+  hipStream_t s = f->ctx->stream;
+  FleetArgs a;
+  a.pt = f->pat.dev;
+  a.st = to_dev(f->cfg.qp);
+  a.N = f->N;
+  a.target_mode = f->cfg.target_mode;
+  a.use_gp = f->cfg.use_gp;
+  a.residual_model = f->cfg.residual_model;
+  a.max_steps = f->cfg.max_steps;
+  a.dt = f->cfg.dt;
+  a.x = f->x.as<double>(); a.Xw = f->Xw.as<double>(); a.Uw = f->Uw.as<double>();
+  a.ysc = f->ysc.as<double>(); a.rho = f->rho.as<double>(); a.rec = f->rec.as<double>();
+  a.xt = f->xt.as<double>();
+  a.gmean = f->mean.as<double>();
+  for (int it = 0; it < nsteps; ++it) {
+    if (f->cfg.use_gp) GPMPC_HIP(fleet_gp_posterior(f));
+    hipLaunchKernelGGL(k_fleet_control, dim3(f->B), dim3(256), 0, s, a);
+    GPMPC_HIP(hipGetLastError());
+  }
+  return 0;
+}
+
+extern "C" int gpmpc_fleet_read(gpmpc_fleet *f, double *records, double *x) {
+  GPMPC_CHECK_ARG(f);
+  hipStream_t s = f->ctx->stream;
+  if (records)
+    GPMPC_HIP(hipMemcpyAsync(records, f->rec.p, sizeof(double) * f->B * GPMPC_REC_LEN,
+                             hipMemcpyDeviceToHost, s));
+  if (x) GPMPC_HIP(hipMemcpyAsync(x, f->x.p, sizeof(double) * f->B * NX, hipMemcpyDeviceToHost, s));
+  GPMPC_HIP(hipStreamSynchronize(s));
+  return 0;
+}
+
+extern "C" double *gpmpc_fleet_records_dev(gpmpc_fleet *f) { return f ? f->rec.as<double>() : nullptr; }
+
+extern "C" int gpmpc_fleet_destroy(gpmpc_fleet *f) {
+  if (f && f->ctx) (void)hipStreamSynchronize(f->ctx->stream);
+  delete f;
+  return 0;
+}

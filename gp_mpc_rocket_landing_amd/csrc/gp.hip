@@ -61,6 +61,14 @@ __global__ void k_post_finish(int P, int n_out, int nrt, const double *__restric
   }
 }
 
+hipError_t launch_post_finish(hipStream_t s, int P, int n_out, int nrt, const double *part,
+                              int64_t ldp, const double *meanT, int64_t ldm, const double *ymean,
+                              const double *ystd, double sigma2, double *mean, double *var) {
+  hipLaunchKernelGGL(k_post_finish, dim3((P + 255) / 256), dim3(256), 0, s, P, n_out, nrt, part,
+                     ldp, meanT, ldm, ymean, ystd, sigma2, mean, var);
+  return hipGetLastError();
+}
+
 // FITC: part2 holds colsums for v = Luu^-1 Ku* (rows tiles) and w = LB^-1 v.
 __global__ void k_fitc_finish(int P, int n_out, int nrt, const double *__restrict__ pv,
                               const double *__restrict__ pw, int64_t ldp,
@@ -421,12 +429,7 @@ extern "C" int gpmpc_gp_destroy(gpmpc_gp *gp) {
   return 0;
 }
 
-// ---- internal accessors for the fleet ---------------------------------------
-struct GpView {
-  int kind, n, d, n_out;
-  double sigma2, iso_scale;
-  const double *ls, *Xs, *Xn, *W, *alphaT, *ymean, *ystd;
-};
+// ---- internal accessor for the fleet ----------------------------------------
 GpView gp_view(const gpmpc_gp *gp) {
   const GpCore &g = gp->core;
   return GpView{g.kind, g.n, g.d, g.n_out, g.sigma2, g.iso_scale, g.ls.as<double>(),

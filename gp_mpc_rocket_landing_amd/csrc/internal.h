@@ -15,6 +15,8 @@ struct gpmpc_ctx {
 };
 
 void gpmpc_set_error(const char *fmt, ...);
+// persistent per-device scratch (slots: 0 trsm block inverses, 1 potrf block inverses)
+void *gpmpc_scratch(int slot, size_t bytes);
 
 #define GPMPC_HIP(call)                                                               \
   do {                                                                                \
@@ -67,3 +69,15 @@ hipError_t launch_add_diag(hipStream_t s, int n, double *A, int64_t lda, double 
 // copy lower triangle of src into dst and zero the strict upper part of dst
 hipError_t launch_copy_lower(hipStream_t s, int n, const double *src, int64_t lds, double *dst,
                              int64_t ldd);
+
+// read-only view of a fitted exact GP (gp.hip) for the fleet
+struct GpView {
+  int kind, n, d, n_out;
+  double sigma2, iso_scale;
+  const double *ls, *Xs, *Xn, *W, *alphaT, *ymean, *ystd;
+};
+GpView gp_view(const gpmpc_gp *gp);
+// posterior finish: var/mean (P x n_out) from SUMSQ partials and K* alpha (gp.hip)
+hipError_t launch_post_finish(hipStream_t s, int P, int n_out, int nrt, const double *part,
+                              int64_t ldp, const double *meanT, int64_t ldm, const double *ymean,
+                              const double *ystd, double sigma2, double *mean, double *var);

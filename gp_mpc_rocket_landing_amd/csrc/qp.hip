@@ -1,0 +1,228 @@
+// qp.hip -- batched OSQP-style ADMM: one workgroup (256 threads) per QP.
+//
+// Replaces the osqp.OSQP() setup / update(q) / update(l, u, Ax) / warm_start(x)
+// / solve() sequence of OSQPRTIMPC (osqp_rti.py:454-567) for a whole batch of
+// QPs that share one sparsity pattern.  The pattern is pre-processed once on
+// the host (CSR -> CSC map, banded-KKT product terms) and shared by every
+// workgroup; the numeric data of each problem is staged into LDS.
+#include "internal.h"
+#include "qp.h"
+#include <algorithm>
+#include <vector>
+
+extern "C" void gpmpc_qp_default_settings(gpmpc_qp_settings *s) {
+  // osqp_rti.py:54-60 (max_iter 50, eps 1e-4, polish off, warm start, scaling 3)
+  // + OSQP 0.6 defaults pinned, adaptive-rho interval fixed at 25.
+  s->rho = 0.1;
+  s->sigma = 1e-6;
+  s->alpha = 1.6;
+  s->eps_abs = 1e-4;
+  s->eps_rel = 1e-4;
+  s->eps_prim_inf = 1e-4;
+  s->eps_dual_inf = 1e-4;
+  s->max_iter = 50;
+  s->check_termination = 25;
+  s->adaptive_rho = 1;
+  s->adaptive_rho_interval = 25;
+  s->adaptive_rho_tolerance = 5.0;
+  s->scaling = 3;
+  s->warm_start = 1;
+}
+
+QPSettingsDev to_dev(const gpmpc_qp_settings &s) {
+  QPSettingsDev d;
+  d.rho = s.rho; d.sigma = s.sigma; d.alpha = s.alpha; d.eps_abs = s.eps_abs;
+  d.eps_rel = s.eps_rel; d.eps_prim_inf = s.eps_prim_inf; d.eps_dual_inf = s.eps_dual_inf;
+  d.max_iter = s.max_iter; d.check_termination = s.check_termination;
+  d.adaptive_rho = s.adaptive_rho; d.adaptive_rho_interval = s.adaptive_rho_interval;
+  d.adaptive_rho_tolerance = s.adaptive_rho_tolerance; d.scaling = s.scaling;
+  d.warm_start = s.warm_start;
+  return d;
+}
+
+int QPPatternHost::build(int n_, int m_, const int *rowptr, const int *colidx, hipStream_t s) {
+  n = n_;
+  m = m_;
+  nnz = rowptr[m];
+  w = 0;
+  for (int r = 0; r < m; ++r)
+    for (int a = rowptr[r]; a < rowptr[r + 1]; ++a)
+      for (int b = rowptr[r]; b < rowptr[r + 1]; ++b) w = std::max(w, colidx[a] - colidx[b]);
+  const int nb = w + 1;
+  // CSC map
+  std::vector<int> colptr(n + 1, 0), csc2csr(nnz), cscrow(nnz);
+  for (int k = 0; k < nnz; ++k) colptr[colidx[k] + 1]++;
+  for (int j = 0; j < n; ++j) colptr[j + 1] += colptr[j];
+  std::vector<int> fill(colptr.begin(), colptr.end() - 1);
+  for (int r = 0; r < m; ++r)
+    for (int k = rowptr[r]; k < rowptr[r + 1]; ++k) {
+      const int p = fill[colidx[k]]++;
+      csc2csr[p] = k;
+      cscrow[p] = r;
+    }
+  // band product terms, generated in (row, a, b) order like the C oracle's factor()
+  struct T { int e, r, a, b; };
+  std::vector<T> terms;
+  for (int r = 0; r < m; ++r)
+    for (int a = rowptr[r]; a < rowptr[r + 1]; ++a)
+      for (int b = rowptr[r]; b < rowptr[r + 1]; ++b) {
+        const int i = colidx[a], j = colidx[b];
+        if (j > i) continue;
+        terms.push_back(T{j * nb + (i - j), r, a, b});
+      }
+  std::stable_sort(terms.begin(), terms.end(), [](const T &x, const T &y) { return x.e < y.e; });
+  std::vector<int> bandptr(n * nb + 1, 0), tv(3 * terms.size());
+  for (size_t k = 0; k < terms.size(); ++k) {
+    bandptr[terms[k].e + 1]++;
+    tv[3 * k] = terms[k].r;
+    tv[3 * k + 1] = terms[k].a;
+    tv[3 * k + 2] = terms[k].b;
+  }
+  for (int e = 0; e < n * nb; ++e) bandptr[e + 1] += bandptr[e];
+  // one device block: rowptr | colidx | colptr | csc2csr | cscrow | bandptr | terms
+  std::vector<int> all;
+  auto app = [&](const int *p, size_t k) { all.insert(all.end(), p, p + k); };
+  const size_t o_rp = 0;
+  app(rowptr, m + 1);
+  const size_t o_ci = all.size();
+  app(colidx, nnz);
+  const size_t o_cp = all.size();
+  app(colptr.data(), n + 1);
+  const size_t o_cm = all.size();
+  app(csc2csr.data(), nnz);
+  const size_t o_cr = all.size();
+  app(cscrow.data(), nnz);
+  const size_t o_bp = all.size();
+  app(bandptr.data(), bandptr.size());
+  const size_t o_tv = all.size();
+  app(tv.data(), tv.size());
+  if (buf.alloc(sizeof(int) * all.size()) != hipSuccess) return -1;
+  if (hipMemcpyAsync(buf.p, all.data(), sizeof(int) * all.size(), hipMemcpyHostToDevice, s) !=
+          hipSuccess ||
+      hipStreamSynchronize(s) != hipSuccess)
+    return -1;
+  const int *d = buf.as<int>();
+  dev.n = n; dev.m = m; dev.nnz = nnz; dev.w = w;
+  dev.rowptr = d + o_rp; dev.colidx = d + o_ci; dev.colptr = d + o_cp; dev.csc2csr = d + o_cm;
+  dev.cscrow = d + o_cr; dev.bandptr = d + o_bp; dev.terms = d + o_tv;
+  return 0;
+}
+
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_qp_batched(QPPattern pt, QPSettingsDev st,
+                                                    const double *__restrict__ Aval,
+                                                    const double *__restrict__ Pd,
+                                                    const double *__restrict__ q,
+                                                    const double *__restrict__ l,
+                                                    const double *__restrict__ u,
+                                                    const double *__restrict__ xws, double *rho,
+                                                    double *yst, double *xo, double *yo,
+                                                    int *iters, int *status, double *obj) {
+  __shared__ QPSmemStd s;
+  const int b = blockIdx.x, tid = threadIdx.x, nt = blockDim.x;
+  const int n = pt.n, m = pt.m, nnz = pt.nnz;
+  for (int k = tid; k < nnz; k += nt) s.A[k] = Aval[(int64_t)b * nnz + k];
+  for (int j = tid; j < n; j += nt) {
+    s.P[j] = Pd[(int64_t)b * n + j];
+    s.q[j] = q[(int64_t)b * n + j];
+    s.x[j] = xws ? xws[(int64_t)b * n + j] : 0.0;
+  }
+  for (int r = tid; r < m; r += nt) {
+    s.l[r] = l[(int64_t)b * m + r];
+    s.u[r] = u[(int64_t)b * m + r];
+    s.y[r] = yst[(int64_t)b * m + r];
+  }
+  if (tid == 0) s.rho_s = rho[b];
+  __syncthreads();
+  QPResult res = qp_solve(pt, s, st);
+  if (res.factor_fail) {
+    if (tid == 0) { status[b] = -100; iters[b] = 0; obj[b] = nan(""); }
+    return;
+  }
+  const bool has = (res.status == 1 || res.status == 2 || res.status == -2);
+  for (int j = tid; j < n; j += nt) xo[(int64_t)b * n + j] = has ? s.D[j] * s.x[j] : nan("");
+  for (int r = tid; r < m; r += nt) {
+    yo[(int64_t)b * m + r] = has ? s.E[r] * s.y[r] / s.c : nan("");
+    yst[(int64_t)b * m + r] = s.y[r];
+  }
+  if (tid == 0) {
+    rho[b] = s.rho_s;
+    iters[b] = res.iter;
+    status[b] = res.status;
+    obj[b] = has ? res.obj : nan("");
+  }
+}
+
+hipError_t launch_qp_batched(hipStream_t s, const QPPattern &pt, const QPSettingsDev &st,
+                             int batch, const double *Aval, const double *Pd, const double *q,
+                             const double *l, const double *u, const double *xws, double *rho,
+                             double *yst, double *xo, double *yo, int *iters, int *status,
+                             double *obj) {
+  hipLaunchKernelGGL(k_qp_batched, dim3(batch), dim3(256), 0, s, pt, st, Aval, Pd, q, l, u, xws,
+                     rho, yst, xo, yo, iters, status, obj);
+  return hipGetLastError();
+}
+
+extern "C" int gpmpc_qp_solve_batched(gpmpc_ctx *ctx, int batch, int n, int m, int nnz,
+                                      const int *rowptr, const int *colidx, const double *Aval,
+                                      const double *Pdiag, const double *q, const double *l,
+                                      const double *u, const gpmpc_qp_settings *st,
+                                      const double *x_ws, double *rho, double *y_scaled,
+                                      double *x, double *y, int *iters, int *status,
+                                      double *obj) {
+  GPMPC_CHECK_ARG(ctx && rowptr && colidx && Aval && Pdiag && q && l && u && st && rho &&
+                  y_scaled && x && y && iters && status && obj);
+  GPMPC_CHECK_ARG(batch >= 0 && n > 0 && m > 0 && nnz == rowptr[m]);
+  GPMPC_CHECK_ARG(n <= QP_NMAX && m <= QP_MMAX && nnz <= QP_NNZMAX);
+  if (batch == 0) return 0;
+  GPMPC_HIP(hipSetDevice(ctx->device));
+  hipStream_t s = ctx->stream;
+  QPPatternHost pat;
+  if (pat.build(n, m, rowptr, colidx, s)) {
+    gpmpc_set_error("qp: pattern upload failed");
+    return -1;
+  }
+  if (pat.w > QP_W) {
+    gpmpc_set_error("qp: reduced KKT half-bandwidth %d exceeds %d", pat.w, QP_W);
+    return -2;
+  }
+  DevBuf dA, dP, dq, dl, du, dx0, drho, dy0, dxo, dyo, dit, dst, dob;
+  const size_t B = batch;
+  GPMPC_HIP(dA.alloc(sizeof(double) * B * nnz));
+  GPMPC_HIP(dP.alloc(sizeof(double) * B * n));
+  GPMPC_HIP(dq.alloc(sizeof(double) * B * n));
+  GPMPC_HIP(dl.alloc(sizeof(double) * B * m));
+  GPMPC_HIP(du.alloc(sizeof(double) * B * m));
+  GPMPC_HIP(drho.alloc(sizeof(double) * B));
+  GPMPC_HIP(dy0.alloc(sizeof(double) * B * m));
+  GPMPC_HIP(dxo.alloc(sizeof(double) * B * n));
+  GPMPC_HIP(dyo.alloc(sizeof(double) * B * m));
+  GPMPC_HIP(dit.alloc(sizeof(int) * B));
+  GPMPC_HIP(dst.alloc(sizeof(int) * B));
+  GPMPC_HIP(dob.alloc(sizeof(double) * B));
+  GPMPC_HIP(hipMemcpyAsync(dA.p, Aval, sizeof(double) * B * nnz, hipMemcpyHostToDevice, s));
+  GPMPC_HIP(hipMemcpyAsync(dP.p, Pdiag, sizeof(double) * B * n, hipMemcpyHostToDevice, s));
+  GPMPC_HIP(hipMemcpyAsync(dq.p, q, sizeof(double) * B * n, hipMemcpyHostToDevice, s));
+  GPMPC_HIP(hipMemcpyAsync(dl.p, l, sizeof(double) * B * m, hipMemcpyHostToDevice, s));
+  GPMPC_HIP(hipMemcpyAsync(du.p, u, sizeof(double) * B * m, hipMemcpyHostToDevice, s));
+  GPMPC_HIP(hipMemcpyAsync(drho.p, rho, sizeof(double) * B, hipMemcpyHostToDevice, s));
+  GPMPC_HIP(hipMemcpyAsync(dy0.p, y_scaled, sizeof(double) * B * m, hipMemcpyHostToDevice, s));
+  if (x_ws) {
+    GPMPC_HIP(dx0.alloc(sizeof(double) * B * n));
+    GPMPC_HIP(hipMemcpyAsync(dx0.p, x_ws, sizeof(double) * B * n, hipMemcpyHostToDevice, s));
+  }
+  GPMPC_HIP(launch_qp_batched(s, pat.dev, to_dev(*st), batch, dA.as<double>(), dP.as<double>(),
+                              dq.as<double>(), dl.as<double>(), du.as<double>(),
+                              x_ws ? dx0.as<double>() : nullptr, drho.as<double>(),
+                              dy0.as<double>(), dxo.as<double>(), dyo.as<double>(), dit.as<int>(),
+                              dst.as<int>(), dob.as<double>()));
+  GPMPC_HIP(hipMemcpyAsync(x, dxo.p, sizeof(double) * B * n, hipMemcpyDeviceToHost, s));
+  GPMPC_HIP(hipMemcpyAsync(y, dyo.p, sizeof(double) * B * m, hipMemcpyDeviceToHost, s));
+  GPMPC_HIP(hipMemcpyAsync(y_scaled, dy0.p, sizeof(double) * B * m, hipMemcpyDeviceToHost, s));
+  GPMPC_HIP(hipMemcpyAsync(rho, drho.p, sizeof(double) * B, hipMemcpyDeviceToHost, s));
+  GPMPC_HIP(hipMemcpyAsync(iters, dit.p, sizeof(int) * B, hipMemcpyDeviceToHost, s));
+  GPMPC_HIP(hipMemcpyAsync(status, dst.p, sizeof(int) * B, hipMemcpyDeviceToHost, s));
+  GPMPC_HIP(hipMemcpyAsync(obj, dob.p, sizeof(double) * B, hipMemcpyDeviceToHost, s));
+  GPMPC_HIP(hipStreamSynchronize(s));
+  return 0;
+}

@@ -1,0 +1,91 @@
+"""Device-resident batch ("fleet") of closed-loop 3-DoF GP-MPC landings.
+
+The fleet is the batched form of ``MonteCarloSimulator.run_single``
+(monte_carlo.py:401-583) driving the 3-DoF ``GPMPC`` surface: every control
+step runs the GP posterior at the N horizon points of every landing, the RTI
+QP assembly with the GP mean, the batched OSQP-style ADMM, the plant step and
+the termination rules -- all on the GPU (libgpmpc_hip.so, csrc/fleet.hip).
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+
+from . import _lib
+from .data import synthetic_training_data
+from .gp.features import Simple3DoFFeatureExtractor
+
+# record layout (GPMPC_REC_LEN = 16 doubles per landing)
+REC_OUTCOME, REC_STEPS, REC_FUEL, REC_TIME = 0, 1, 2, 3
+REC_STATE = slice(4, 11)
+REC_ADMM_ITERS, REC_SOLVED, REC_M0, REC_LAST_STATUS, REC_RHO = 11, 12, 13, 14, 15
+OUTCOMES = {0: "RUNNING", 1: "SUCCESS", 2: "CRASH", 3: "FUEL_EXHAUSTED",
+            4: "CONSTRAINT_VIOLATION", 5: "TIMEOUT", 6: "DIVERGENCE"}
+
+
+def fit_gp(ctx, n_train=1000, seed=0, noise=1e-4):
+    """Exact Simple3DoF GP on generator G -- the GP every landing shares."""
+    X, U, D = synthetic_training_data(n_train, seed=seed)
+    Z = Simple3DoFFeatureExtractor().extract_batch(X, U)
+    return _lib.ExactGPHandle(ctx, _lib.SE_ARD, Z, D, np.ones(Z.shape[1]), 1.0, noise)
+
+
+class Fleet:
+    def __init__(self, ctx, gp, batch, **config):
+        self.ctx = ctx
+        self.gp = gp  # keep the GP alive: the fleet reads its device factor
+        self.cfg = _lib.fleet_default_config()
+        for k, v in config.items():
+            if hasattr(self.cfg, k):
+                setattr(self.cfg, k, v)
+            else:
+                setattr(self.cfg.qp, k, v)
+        self.batch = int(batch)
+        h = ctypes.c_void_p()
+        _lib._chk(_lib._L.gpmpc_fleet_create(ctx.h, gp.h, ctypes.byref(self.cfg), self.batch,
+                                             ctypes.byref(h)), "fleet_create")
+        self.h = h
+
+    def reset(self, x0, first=0):
+        x0 = _lib.f64(np.atleast_2d(x0))
+        _lib._chk(_lib._L.gpmpc_fleet_reset(self.h, int(first), x0.shape[0], _lib._d(x0)), "fleet_reset")
+
+    def step(self, nsteps=1):
+        _lib._chk(_lib._L.gpmpc_fleet_step(self.h, int(nsteps)), "fleet_step")
+
+    def read(self):
+        rec = np.empty((self.batch, _lib.REC_LEN)); x = np.empty((self.batch, 7))
+        _lib._chk(_lib._L.gpmpc_fleet_read(self.h, _lib._d(rec), _lib._d(x)), "fleet_read")
+        return rec, x
+
+    @property
+    def records_dev(self):
+        return _lib._L.gpmpc_fleet_records_dev(self.h)
+
+    def close(self):
+        if getattr(self, "h", None):
+            _lib._L.gpmpc_fleet_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def initial_conditions(count, seed0=42, first=0):
+    from .experiments.monte_carlo import SimulationConfig, sample_initial_condition
+    cfg = SimulationConfig.run_experiments()
+    return np.array([sample_initial_condition(seed0 + first + i, cfg) for i in range(count)])
+
+
+def run_fleet(ctx, batch, steps, seed0=42, gp=None, **config):
+    gp = gp or fit_gp(ctx)
+    f = Fleet(ctx, gp, batch, **config)
+    f.reset(initial_conditions(batch, seed0))
+    f.step(steps)
+    rec, x = f.read()
+    f.close()
+    return dict(records=rec, x=x)

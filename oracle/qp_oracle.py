@@ -78,6 +78,15 @@ def cost(N, x_ref):
     return P, q
 
 
+# structural non-zeros of the analytic 3-DoF Jacobians (osqp_rti.py:682-708)
+A_STRUCT = np.eye(7, dtype=bool)
+A_STRUCT[1, 4] = A_STRUCT[2, 5] = A_STRUCT[3, 6] = True
+A_STRUCT[4:7, 0] = True
+B_STRUCT = np.zeros((7, 3), dtype=bool)
+B_STRUCT[0, :] = True
+B_STRUCT[4, 0] = B_STRUCT[5, 1] = B_STRUCT[6, 2] = True
+
+
 def constraints(X_lin, U_lin, x_init, dt, gp_dv=None, sign=+1.0, filter_small=True):
     """_build_constraint_matrix (osqp_rti.py:260-372).
 
@@ -85,7 +94,9 @@ def constraints(X_lin, U_lin, x_init, dt, gp_dv=None, sign=+1.0, filter_small=Tr
     l = u = [x_init; sign*c_k; ...].  The reference sets +c_k (sign=+1, SURVEY D2);
     the GP-MPC adapter uses sign=-1 (x+ = A x + B u + c) and adds the GP mean
     dt*d_v on the velocity rows of c_k (gp_mpc.py:309-314, 410-411).
-    ``filter_small`` keeps the |a| > 1e-10 value filter.
+    ``filter_small`` keeps the |a| > 1e-10 value filter; False keeps
+    the structural pattern of the analytic Jacobians (zeros stored explicitly), the
+    fixed pattern the batched HIP solver shares across landings.
     """
     N = U_lin.shape[0]; n = n_vars(N)
     rows, cols, vals = [], [], []
@@ -99,10 +110,10 @@ def constraints(X_lin, U_lin, x_init, dt, gp_dv=None, sign=+1.0, filter_small=Tr
         Ak, Bk = linearize(X_lin[k], U_lin[k], dt)
         for i in range(N_X):
             for j in range(N_X):
-                if (not filter_small) or abs(Ak[i, j]) > 1e-10:
+                if (A_STRUCT[i, j] if not filter_small else abs(Ak[i, j]) > 1e-10):
                     rows.append(r0 + i); cols.append(c0 + j); vals.append(Ak[i, j])
             for j in range(N_U):
-                if (not filter_small) or abs(Bk[i, j]) > 1e-10:
+                if (B_STRUCT[i, j] if not filter_small else abs(Bk[i, j]) > 1e-10):
                     rows.append(r0 + i); cols.append(c0 + N_X + j); vals.append(Bk[i, j])
             rows.append(r0 + i); cols.append(c0 + N_X + N_U + i); vals.append(-1.0)
         xn = plant_step(X_lin[k], U_lin[k], dt)

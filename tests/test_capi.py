@@ -1,0 +1,37 @@
+"""The C-ABI library loads and exports every symbol include/gpmpc.h declares
+(no compute call: runs without a GPU)."""
+import ctypes
+import os
+import re
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def header_symbols():
+    src = open(os.path.join(REPO, "include", "gpmpc.h")).read()
+    return sorted(set(re.findall(r"\b(gpmpc_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_library_exports_every_declared_symbol():
+    from gp_mpc_rocket_landing_amd import _lib
+    lib = ctypes.CDLL(_lib.LIB_PATH)
+    missing = [s for s in header_symbols() if not hasattr(lib, s)]
+    assert not missing, missing
+    assert set(header_symbols()) <= set(_lib.EXPORTED) | {"gpmpc_abi_version"}
+
+
+def test_abi_version_and_error_string():
+    from gp_mpc_rocket_landing_amd import _lib
+    assert _lib.abi_version() == 1
+    assert isinstance(_lib._L.gpmpc_last_error(), bytes)
+
+
+def test_default_settings_pin_reference_osqp_config():
+    """osqp_rti.py:54-60 + OSQP 0.6 defaults."""
+    from gp_mpc_rocket_landing_amd import _lib
+    s = _lib.qp_default_settings()
+    assert (s.max_iter, s.check_termination, s.scaling, s.warm_start) == (50, 25, 3, 1)
+    assert (s.rho, s.sigma, s.alpha, s.eps_abs, s.eps_rel) == (0.1, 1e-6, 1.6, 1e-4, 1e-4)
+    assert (s.adaptive_rho, s.adaptive_rho_interval, s.adaptive_rho_tolerance) == (1, 25, 5.0)
+    c = _lib.fleet_default_config()
+    assert (c.horizon, c.dt, c.max_steps) == (20, 0.1, 300)
