@@ -1,0 +1,270 @@
+#!/usr/bin/env python
+"""bench.py -- GP-MPC control steps/s on MI355X (BASELINE.json metric).
+
+Workload (BASELINE configs[3], the run_monte_carlo.py shapes of SURVEY 8d C4):
+per GPU a fleet of ``--landings`` closed-loop 3-DoF GP-MPC landings (initial
+conditions of scripts/run_experiments.py, seeds 42 + global index), horizon
+N = 20, one exact GP on 1000 synthetic training points (generator G) shared by
+every landing.  One "step" = one control step of every active landing: GP
+posterior (mean + variance) at the 20 horizon points, RTI QP assembly with the
+GP mean, OSQP-style ADMM (<= 50 iterations), plant step -- all device-resident.
+
+N > 1: one process per GPU (torch.distributed.run), landings sharded (weak
+scaling: a fixed fleet per GPU), no collective on the data path; the fleet
+records are gathered to rank 0 with one RCCL gather after the timed region.
+
+Prints ONE JSON line on rank 0.  ``value`` = landing control steps executed by
+all ranks / max-over-ranks wall time of the timed region.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+FP64_PEAK_TFLOPS = 78.6   # MI355X FP64 matrix (= vector) peak, spec
+HBM_PEAK_GBS = 8000.0     # MI355X HBM3E spec (MI355X_MICROARCH.md)
+
+
+def admm_flops(n=207, m=354, nnz=734, w=16):
+    """Algorithmic flops of one ADMM iteration and of one (re)factorisation of
+    the reduced KKT band (DESIGN.md 'ADMM kernel')."""
+    it = (2 * nnz + m) + 2 * (2 * n * w + n) + 2 * nnz + 12 * n + 14 * m
+    fac = n * (w * (w + 1)) + 3 * (nnz + 200)
+    return it, fac
+
+
+def cpu_baseline(seconds, n_train=1000, horizon=20):
+    """The reference CPU path restated (oracle): numpy/scipy GP posterior at the N
+    horizon points (same LAPACK calls as exact_gp.py), numpy QP assembly
+    (osqp_rti.py semantics) and the C restatement of the OSQP ADMM, one landing
+    closed loop, BLAS limited to one thread."""
+    from threadpoolctl import threadpool_limits
+    from oracle import admm_ref, gp_oracle, mc_oracle, qp_oracle
+    from gp_mpc_rocket_landing_amd.data import synthetic_training_data
+
+    X, U, D = synthetic_training_data(n_train, seed=0)
+    with threadpool_limits(1):
+        st = gp_oracle.exact_fit(gp_oracle.features_3dof(X, U), D)
+        x = mc_oracle.sample_initial_condition(42)
+        tgt = mc_oracle.incremental_target(x)
+        Xw, Uw = qp_oracle.initial_guess(x, tgt, horizon)
+        P0, _ = qp_oracle.cost(horizon, np.tile(tgt, (horizon + 1, 1)))
+        qp = admm_ref.RefQP(qp_oracle.N_X * (horizon + 1) + qp_oracle.n_vars(horizon))
+        steps = 0
+        t0 = time.perf_counter()
+        deadline = t0 + seconds
+        while time.perf_counter() < deadline:
+            if mc_oracle.pre_step_outcome(x, 2.0):
+                x = mc_oracle.sample_initial_condition(43 + steps)
+                qp = admm_ref.RefQP(qp.y.size)
+            tgt = mc_oracle.incremental_target(x)
+            mean, var = gp_oracle.exact_predict(st, gp_oracle.features_3dof(Xw[:-1], Uw))
+            _, q = qp_oracle.cost(horizon, np.tile(tgt, (horizon + 1, 1)))
+            A, l, u = qp_oracle.constraints(Xw, Uw, x, 0.1, gp_dv=mean, sign=-1.0,
+                                            filter_small=False)
+            r = qp.solve(P0.diagonal(), q, A, l, u, qp_oracle.to_vector(Xw, Uw))
+            Xo, Uo = qp_oracle.from_vector(r["x"], horizon)
+            x = qp_oracle.plant_step(x, Uo[0], 0.1)
+            x[4:7] += qp_oracle.drag_residual(x) * 0.1
+            Xw = np.vstack([Xo[1:], Xo[-1:]]); Uw = np.vstack([Uo[1:], Uo[-1:]])
+            steps += 1
+        el = time.perf_counter() - t0
+    return dict(value=steps / el, unit="control steps/s", cores=1, kind="port",
+                sample=f"1 landing closed loop, {steps} control steps in {el:.1f} s "
+                       f"(numpy/scipy GP N={n_train}, P={horizon}; numpy QP assembly; "
+                       f"C OSQP-0.6 ADMM restatement; OPENBLAS 1 thread)")
+
+
+def cholesky_bench(ctx, torch, n=1000, batch=64, reps=3):
+    """Batched fp64 potrf throughput (BASELINE metric: Cholesky %MFMA peak)."""
+    from gp_mpc_rocket_landing_amd import _lib
+    dev = torch.device("cuda", torch.cuda.current_device())
+    g = torch.Generator(device=dev).manual_seed(0)
+    G = torch.randn(batch, n, n, dtype=torch.float64, device=dev, generator=g) / n ** 0.5
+    base = G @ G.transpose(1, 2) + torch.eye(n, dtype=torch.float64, device=dev)
+    info = torch.zeros(batch, dtype=torch.int32, device=dev)
+    A = base.clone()
+    torch.cuda.synchronize()
+    stream = torch.cuda.ExternalStream(ctx.stream)
+    times = []
+    for _ in range(reps):
+        A.copy_(base)
+        torch.cuda.synchronize()
+        e0 = torch.cuda.Event(enable_timing=True); e1 = torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        rc = _lib._L.gpmpc_potrf_batched_dev(ctx.h, n, batch, A.data_ptr(), n, n * n, info.data_ptr())
+        e1.record(stream)
+        _lib._chk(rc, "potrf_batched_dev")
+        ctx.sync()
+        times.append(e0.elapsed_time(e1) * 1e-3)
+    assert int(info.abs().sum().item()) == 0
+    t = min(times)
+    flops = batch * (n ** 3 / 3.0 + n ** 2 / 2.0 + n / 6.0)
+    tf = flops / t / 1e12
+    # SYRK share: sum_k r_k^2 nb (lower, FMA = 2) with r_k = n - (k+1) nb, nb = 32
+    syrk = batch * sum(max(0, n - (k + 1) * 32) ** 2 * 32 for k in range(n // 32 + 1))
+    return dict(n=n, batch=batch, ms=round(t * 1e3, 3), tflops=round(tf, 3),
+                frac_fp64_peak=round(tf / FP64_PEAK_TFLOPS, 4),
+                syrk_gflop=round(syrk / 1e9, 2))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=40)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--landings", type=int, default=1024, help="landings per GPU")
+    ap.add_argument("--horizon", type=int, default=20)
+    ap.add_argument("--train", type=int, default=1000)
+    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-chol", action="store_true")
+    args = ap.parse_args()
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+    import torch.distributed as dist
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    from gp_mpc_rocket_landing_amd import _lib
+    from gp_mpc_rocket_landing_amd.fleet import Fleet, fit_gp, initial_conditions
+
+    ctx = _lib.Context(local)
+    gp = fit_gp(ctx, n_train=args.train)
+    B = args.landings
+    fl = Fleet(ctx, gp, B, horizon=args.horizon)
+    fl.reset(initial_conditions(B, seed0=42, first=rank * B))
+    for _ in range(args.warmup):
+        fl.step(1)
+    ctx.sync()
+    rec0, _ = fl.read()
+
+    stream = torch.cuda.ExternalStream(ctx.stream)
+    K = args.steps
+    ev = [[torch.cuda.Event(enable_timing=True) for _ in range(5)] for _ in range(K)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(); ctx.sync()
+    t0 = time.perf_counter()
+    for k in range(K):
+        e = ev[k]
+        e[0].record(stream); fl.phases(1)   # features + K* gram
+        e[1].record(stream); fl.phases(4)   # variance GEMM (MFMA)
+        e[2].record(stream); fl.phases(8)   # mean GEMM + finish
+        e[3].record(stream); fl.phases(2)   # QP assembly + ADMM + plant
+        e[4].record(stream)
+    ctx.sync(); torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    rec1, _ = fl.read()
+    steps_done = float(np.sum(rec1[:, 1] - rec0[:, 1]))
+    admm_iters = float(np.sum(rec1[:, 11] - rec0[:, 11]))
+    ph = np.array([[ev[k][i].elapsed_time(ev[k][i + 1]) for i in range(4)] for k in range(K)]) * 1e-3
+    ph_mean = ph.mean(axis=0)
+
+    # ---- aggregate over ranks (max time, summed work); one RCCL gather of records
+    t = torch.tensor([el, steps_done, admm_iters], dtype=torch.float64, device="cuda")
+    if world > 1:
+        tmax = t.clone(); dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+        tsum = t.clone(); dist.all_reduce(tsum, op=dist.ReduceOp.SUM)
+        el_max, steps_all, iters_all = float(tmax[0]), float(tsum[1]), float(tsum[2])
+        recs = torch.from_numpy(rec1).to("cuda")
+        gl = [torch.empty_like(recs) for _ in range(world)] if rank == 0 else None
+        dist.gather(recs, gl, dst=0)
+        all_rec = torch.cat(gl).cpu().numpy() if rank == 0 else None
+    else:
+        el_max, steps_all, iters_all = el, steps_done, admm_iters
+        all_rec = rec1
+
+    if rank == 0:
+        P = B * args.horizon
+        n = args.train
+        # per-launch algorithmic work: variance GEMM n^2 P flop
+        # (lower-triangular L^-1 times K*^T), K* gram 8 n P bytes written
+        var_flops = float(n) * n * P
+        gram_bytes = 8.0 * n * P + 8.0 * (P * 12 + n * 12)
+        mean_bytes = 8.0 * n * P
+        it_f, fac_f = admm_flops()
+        steps_rank0 = steps_done / K
+        admm_flop = (admm_iters / K) * it_f + steps_rank0 * 1.5 * fac_f
+        kern = {
+            "gram_Kstar": dict(ms=ph_mean[0] * 1e3, bound="hbm",
+                               achieved=gram_bytes / ph_mean[0] / 1e9, peak=HBM_PEAK_GBS, unit="GB/s"),
+            "var_gemm_mfma": dict(ms=ph_mean[1] * 1e3, bound="mfma",
+                                  achieved=var_flops / ph_mean[1] / 1e12, peak=FP64_PEAK_TFLOPS,
+                                  unit="TFLOP/s"),
+            "mean_gemm_finish": dict(ms=ph_mean[2] * 1e3, bound="hbm",
+                                     achieved=mean_bytes / ph_mean[2] / 1e9, peak=HBM_PEAK_GBS,
+                                     unit="GB/s"),
+            "qp_admm_plant": dict(ms=ph_mean[3] * 1e3, bound="latency",
+                                  achieved=admm_flop / ph_mean[3] / 1e12, peak=FP64_PEAK_TFLOPS,
+                                  unit="TFLOP/s"),
+        }
+        for v in kern.values():
+            v["frac"] = v["achieved"] / v["peak"]
+            for kk in ("ms", "achieved", "frac"):
+                v[kk] = round(v[kk], 5)
+        # roofline object: the dominant MFMA/HBM kernel by measured time
+        cand = {k: v for k, v in kern.items() if v["bound"] in ("hbm", "mfma")}
+        dom = max(cand, key=lambda k: cand[k]["ms"])
+        d = kern[dom]
+        roof = dict(kernel=dom, bound=d["bound"], achieved=d["achieved"], peak=d["peak"],
+                    unit=d["unit"], frac=d["frac"], traffic=None,
+                    per_launch=("n^2 P flop" if d["bound"] == "mfma" else "bytes"),
+                    launches_per_step=1)
+        out = {
+            "metric": "GP-MPC control steps/sec (N=20, 1000 GP pts)",
+            "value": round(steps_all / el_max, 2),
+            "unit": "control steps/s",
+            "n_gpus": world,
+            "steps": K,
+            "warmup": args.warmup,
+            "ms_per_step": round(el_max / K * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic (generator G training set; run_experiments.py initial conditions)",
+            "config": {"workload": "fleet of closed-loop 3-DoF GP-MPC landings (BASELINE configs[3] "
+                                   "shapes), RTI QP per step",
+                       "landings_per_gpu": B, "horizon": args.horizon, "gp_train_points": n,
+                       "qp": "n=207 m=354, OSQP settings of osqp_rti.py", "parallelism": f"dp{world}"},
+            "roofline": roof,
+            "kernels": kern,
+            "admm_iters_per_solve": round(iters_all / max(steps_all, 1.0), 2),
+            "landing_steps_per_gpu_step": round(steps_done / K, 1),
+        }
+        if all_rec is not None:
+            oc = all_rec[:, 0]
+            out["outcomes"] = {str(int(c)): int(np.sum(oc == c)) for c in np.unique(oc)}
+        if not args.no_chol:
+            try:
+                out["cholesky"] = cholesky_bench(ctx, torch)
+            except Exception as e:  # noqa: BLE001
+                out["cholesky"] = {"error": str(e)[:200]}
+        if not args.no_cpu:
+            cb = cpu_baseline(args.cpu_seconds, n_train=n, horizon=args.horizon)
+            cb["value"] = round(cb["value"], 3)
+            out["cpu_baseline"] = cb
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    fl.close()
+
+
+if __name__ == "__main__":
+    main()

@@ -439,31 +439,39 @@ extern "C" int gpmpc_fleet_reset(gpmpc_fleet *f, int first, int count, const dou
   return 0;
 }
 
-static hipError_t fleet_gp_posterior(gpmpc_fleet *f) {
+// GP posterior of every landing's horizon, in three timed sub-phases:
+//   bit 0: features + K* gram;  bit 2: variance GEMM (W K*^T, SUMSQ epilogue);
+//   bit 3: mean GEMM (alpha^T K*^T) + finish
+static hipError_t fleet_gp_posterior(gpmpc_fleet *f, int mask) {
   hipStream_t s = f->ctx->stream;
   const GpView g = gp_view(f->gp);
   const int P = f->B * f->N;
   const int nrt = gemm_row_tiles(g.n);
-  hipLaunchKernelGGL(k_fleet_queries, dim3((P + 255) / 256), dim3(256), 0, s, f->B, f->N,
-                     f->Xw.as<double>(), f->Uw.as<double>(), g.ls, g.kind == GPMPC_SE_ISO,
-                     f->Q.as<double>(), f->Qn.as<double>());
-  hipError_t e = launch_gram(s, g.kind, f->Q.as<double>(), f->Qn.as<double>(), P, g.Xs, g.Xn, g.n,
-                             g.d, g.sigma2, g.iso_scale, f->Ks.as<double>(), g.n, 0);
-  if (e != hipSuccess) return e;
-  e = launch_gemm_nt(s, EPI_SUMSQ, g.n, P, g.n, g.W, g.n, f->Ks.as<double>(), g.n,
-                     f->part.as<double>(), P, 1.0, 0.0, 1, 0, 1, 0, 0, 0);
-  if (e != hipSuccess) return e;
-  e = launch_gemm_nt(s, EPI_STORE, 3, P, g.n, g.alphaT, g.n, f->Ks.as<double>(), g.n,
-                     f->meanT.as<double>(), P, 1.0, 0.0, 0, 0, 1, 0, 0, 0);
-  if (e != hipSuccess) return e;
-  return launch_post_finish(s, P, 3, nrt, f->part.as<double>(), P, f->meanT.as<double>(), P,
-                            g.ymean, g.ystd, g.sigma2, f->mean.as<double>(), f->var.as<double>());
+  hipError_t e = hipSuccess;
+  if (mask & 1) {
+    hipLaunchKernelGGL(k_fleet_queries, dim3((P + 255) / 256), dim3(256), 0, s, f->B, f->N,
+                       f->Xw.as<double>(), f->Uw.as<double>(), g.ls, g.kind == GPMPC_SE_ISO,
+                       f->Q.as<double>(), f->Qn.as<double>());
+    e = launch_gram(s, g.kind, f->Q.as<double>(), f->Qn.as<double>(), P, g.Xs, g.Xn, g.n, g.d,
+                    g.sigma2, g.iso_scale, f->Ks.as<double>(), g.n, 0);
+    if (e != hipSuccess) return e;
+  }
+  if (mask & 4) {
+    e = launch_gemm_nt(s, EPI_SUMSQ, g.n, P, g.n, g.W, g.n, f->Ks.as<double>(), g.n,
+                       f->part.as<double>(), P, 1.0, 0.0, 1, 0, 1, 0, 0, 0);
+    if (e != hipSuccess) return e;
+  }
+  if (mask & 8) {
+    e = launch_gemm_nt(s, EPI_STORE, 3, P, g.n, g.alphaT, g.n, f->Ks.as<double>(), g.n,
+                       f->meanT.as<double>(), P, 1.0, 0.0, 0, 0, 1, 0, 0, 0);
+    if (e != hipSuccess) return e;
+    e = launch_post_finish(s, P, 3, nrt, f->part.as<double>(), P, f->meanT.as<double>(), P,
+                           g.ymean, g.ystd, g.sigma2, f->mean.as<double>(), f->var.as<double>());
+  }
+  return e;
 }
 
-extern "C" int gpmpc_fleet_step(gpmpc_fleet *f, int nsteps) {
-  GPMPC_CHECK_ARG(f && nsteps >= 0);
-  GPMPC_HIP(hipSetDevice(f->ctx->device));
-  hipStream_t s = f->ctx->stream;
+static FleetArgs fleet_args(gpmpc_fleet *f) {
   FleetArgs a;
   a.pt = f->pat.dev;
   a.st = to_dev(f->cfg.qp);
@@ -477,10 +485,25 @@ extern "C" int gpmpc_fleet_step(gpmpc_fleet *f, int nsteps) {
   a.ysc = f->ysc.as<double>(); a.rho = f->rho.as<double>(); a.rec = f->rec.as<double>();
   a.xt = f->xt.as<double>();
   a.gmean = f->mean.as<double>();
-  for (int it = 0; it < nsteps; ++it) {
-    if (f->cfg.use_gp) GPMPC_HIP(fleet_gp_posterior(f));
-    hipLaunchKernelGGL(k_fleet_control, dim3(f->B), dim3(256), 0, s, a);
+  return a;
+}
+
+extern "C" int gpmpc_fleet_step_phases(gpmpc_fleet *f, int phase_mask) {
+  GPMPC_CHECK_ARG(f);
+  GPMPC_HIP(hipSetDevice(f->ctx->device));
+  if ((phase_mask & 13) && f->cfg.use_gp) GPMPC_HIP(fleet_gp_posterior(f, phase_mask));
+  if (phase_mask & 2) {
+    hipLaunchKernelGGL(k_fleet_control, dim3(f->B), dim3(256), 0, f->ctx->stream, fleet_args(f));
     GPMPC_HIP(hipGetLastError());
+  }
+  return 0;
+}
+
+extern "C" int gpmpc_fleet_step(gpmpc_fleet *f, int nsteps) {
+  GPMPC_CHECK_ARG(f && nsteps >= 0);
+  for (int it = 0; it < nsteps; ++it) {
+    const int rc = gpmpc_fleet_step_phases(f, 15);
+    if (rc) return rc;
   }
   return 0;
 }

@@ -54,6 +54,9 @@ class Fleet:
     def step(self, nsteps=1):
         _lib._chk(_lib._L.gpmpc_fleet_step(self.h, int(nsteps)), "fleet_step")
 
+    def phases(self, mask):
+        _lib._chk(_lib._L.gpmpc_fleet_step_phases(self.h, int(mask)), "fleet_step_phases")
+
     def read(self):
         rec = np.empty((self.batch, _lib.REC_LEN)); x = np.empty((self.batch, 7))
         _lib._chk(_lib._L.gpmpc_fleet_read(self.h, _lib._d(rec), _lib._d(x)), "fleet_read")

@@ -160,7 +160,15 @@ int gpmpc_fleet_create(gpmpc_ctx *ctx, gpmpc_gp *gp, const gpmpc_fleet_config *c
 int gpmpc_fleet_reset(gpmpc_fleet *f, int first, int count, const double *x0);
 /* advance every active landing by nsteps control steps (async on the ctx stream) */
 int gpmpc_fleet_step(gpmpc_fleet *f, int nsteps);
-/* records (batch x GPMPC_REC_LEN doubles), see gpmpc_fleet_record layout */
+/* one step split in its phases, launched in the order 0, 2, 3, 1:
+ * bit 0: horizon features + K* = k(Z*, X) Gram; bit 2: variance GEMM
+ * (|L^-1 K*^T|^2 on FP64 MFMA); bit 3: mean GEMM + posterior finish;
+ * bit 1: QP assembly + ADMM + plant step.  A full step = phases(15). */
+int gpmpc_fleet_step_phases(gpmpc_fleet *f, int phase_mask);
+/* records (batch x GPMPC_REC_LEN doubles): 0 outcome (0 running, 1..6 =
+ * LandingOutcome of monte_carlo.py:25-33), 1 steps, 2 fuel used, 3 flight time,
+ * 4..10 state, 11 total ADMM iterations, 12 solves with status "solved",
+ * 13 initial mass, 14 last QP status, 15 last rho */
 #define GPMPC_REC_LEN 16
 int gpmpc_fleet_read(gpmpc_fleet *f, double *records, double *x /* batch x 7, may be NULL */);
 /* device pointer of the record array (for collectives) */
