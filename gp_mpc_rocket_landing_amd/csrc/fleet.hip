@@ -35,7 +35,14 @@ struct gpmpc_fleet {
   QPPatternHost pat;
   DevBuf x, Xw, Uw, ysc, rho, rec, xt;      // landing state
   DevBuf Q, Qn, Ks, part, meanT, mean, var;  // GP scratch
+  unsigned long long *stamps = nullptr;      // diagnostic (gpmpc_fleet_set_stamps)
 };
+
+extern "C" int gpmpc_fleet_set_stamps(gpmpc_fleet *f, void *dev_u64x8) {
+  GPMPC_CHECK_ARG(f);
+  f->stamps = (unsigned long long *)dev_u64x8;
+  return 0;
+}
 
 extern "C" void gpmpc_fleet_default_config(gpmpc_fleet_config *c) {
   c->horizon = 20;           // BASELINE config: N = 20
@@ -146,6 +153,7 @@ struct FleetArgs {
   double dt;
   double *x, *Xw, *Uw, *ysc, *rho, *rec, *xt;
   const double *gmean;  // (B*N) x 3
+  unsigned long long *stamps;  // diagnostic phase cycles of block 0 (or null)
 };
 
 __global__ __launch_bounds__(256) void k_fleet_control(FleetArgs a) {
@@ -157,6 +165,9 @@ __global__ __launch_bounds__(256) void k_fleet_control(FleetArgs a) {
   const double dt = a.dt;
   double *rec = a.rec + (int64_t)b * GPMPC_REC_LEN;
   if (rec[0] != 0.0) return;  // terminated landing
+  QPStamps T;
+  T.out = (b == 0) ? a.stamps : nullptr;
+  T.start();
   double *x = a.x + (int64_t)b * NX;
   double *Xw = a.Xw + (int64_t)b * (N + 1) * NX;
   double *Uw = a.Uw + (int64_t)b * N * NU;
@@ -286,8 +297,10 @@ __global__ __launch_bounds__(256) void k_fleet_control(FleetArgs a) {
   for (int r = tid; r < m; r += nt) s.y[r] = a.ysc[(int64_t)b * m + r];
   if (tid == 0) s.rho_s = a.rho[b];
   __syncthreads();
+  T.mark(0);
   // ---- ADMM (qp_device.h)
-  QPResult res = qp_solve(a.pt, s, a.st);
+  QPResult res = qp_solve(a.pt, s, a.st, &T);
+  T.mark(7);
   const bool has = !res.factor_fail && (res.status == 1 || res.status == 2 || res.status == -2);
   // ---- solution, plant step, warm-start shift
   if (has) {
@@ -342,6 +355,8 @@ __global__ __launch_bounds__(256) void k_fleet_control(FleetArgs a) {
     rec[14] = res.factor_fail ? -100 : res.status;
     rec[15] = s.rho_s;
   }
+  T.mark(7);
+  T.flush();
 }
 
 // initial linearisation point: X linear to the target, U hover (osqp_rti.py:425-446)
@@ -396,7 +411,7 @@ extern "C" int gpmpc_fleet_create(gpmpc_ctx *ctx, gpmpc_gp *gp, const gpmpc_flee
   f->ctx = ctx; f->gp = gp; f->cfg = *cfg; f->B = batch; f->N = N; f->n = n; f->m = m;
   std::vector<int> rp, ci;
   mpc_pattern(N, rp, ci);
-  if (f->pat.build(n, m, rp.data(), ci.data(), ctx->stream) || f->pat.w > QP_W) {
+  if (f->pat.build(n, m, rp.data(), ci.data(), ctx->stream) || !f->pat.fits()) {
     delete f;
     gpmpc_set_error("fleet: QP pattern setup failed");
     return -1;
@@ -485,6 +500,7 @@ static FleetArgs fleet_args(gpmpc_fleet *f) {
   a.ysc = f->ysc.as<double>(); a.rho = f->rho.as<double>(); a.rec = f->rec.as<double>();
   a.xt = f->xt.as<double>();
   a.gmean = f->mean.as<double>();
+  a.stamps = f->stamps;
   return a;
 }
 

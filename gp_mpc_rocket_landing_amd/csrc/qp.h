@@ -3,15 +3,18 @@
 #include "internal.h"
 #include "qp_device.h"
 
-// LDS caps of the single compiled instantiation (3-DoF MPC up to N = 21)
-#define QP_NMAX 224
-#define QP_MMAX 384
-#define QP_NNZMAX 800
+// LDS caps of the single compiled instantiation: 3-DoF MPC up to N = 20
+// (n = 10N + 7, m = 17N + 14, nnz = 36N + 14), sized so that the fleet's
+// control kernel stays under 80 KB and two workgroups share a CU
+#define QP_NMAX 208
+#define QP_MMAX 360
+#define QP_NNZMAX 736
 #define QP_W 16
 typedef QPSmem<QP_NMAX, QP_MMAX, QP_NNZMAX, QP_W> QPSmemStd;
 
 struct QPPatternHost {
-  int n = 0, m = 0, nnz = 0, w = 0;
+  int n = 0, m = 0, nnz = 0, w = 0, maxrow = 0, maxcol = 0;
+  bool fits() const { return n <= QP_NMAX && m <= QP_MMAX && nnz <= QP_NNZMAX && w <= QP_W && maxrow <= QP_RMAX && maxcol <= QP_CMAX; }
   DevBuf buf;
   QPPattern dev{};
   int build(int n, int m, const int *rowptr, const int *colidx, hipStream_t s);

@@ -49,10 +49,14 @@ int QPPatternHost::build(int n_, int m_, const int *rowptr, const int *colidx, h
     for (int a = rowptr[r]; a < rowptr[r + 1]; ++a)
       for (int b = rowptr[r]; b < rowptr[r + 1]; ++b) w = std::max(w, colidx[a] - colidx[b]);
   const int nb = w + 1;
+  maxrow = 0;
+  for (int r = 0; r < m; ++r) maxrow = std::max(maxrow, rowptr[r + 1] - rowptr[r]);
   // CSC map
   std::vector<int> colptr(n + 1, 0), csc2csr(nnz), cscrow(nnz);
   for (int k = 0; k < nnz; ++k) colptr[colidx[k] + 1]++;
   for (int j = 0; j < n; ++j) colptr[j + 1] += colptr[j];
+  maxcol = 0;
+  for (int j = 0; j < n; ++j) maxcol = std::max(maxcol, colptr[j + 1] - colptr[j]);
   std::vector<int> fill(colptr.begin(), colptr.end() - 1);
   for (int r = 0; r < m; ++r)
     for (int k = rowptr[r]; k < rowptr[r + 1]; ++k) {
@@ -182,8 +186,10 @@ extern "C" int gpmpc_qp_solve_batched(gpmpc_ctx *ctx, int batch, int n, int m, i
     gpmpc_set_error("qp: pattern upload failed");
     return -1;
   }
-  if (pat.w > QP_W) {
-    gpmpc_set_error("qp: reduced KKT half-bandwidth %d exceeds %d", pat.w, QP_W);
+  if (!pat.fits()) {
+    gpmpc_set_error("qp: pattern outside the compiled caps (n %d<=256, m %d<=512, half-bandwidth "
+                    "%d<=%d, row nnz %d<=%d, col nnz %d<=%d)", pat.n, pat.m, pat.w, QP_W,
+                    pat.maxrow, QP_RMAX, pat.maxcol, QP_CMAX);
     return -2;
   }
   DevBuf dA, dP, dq, dl, du, dx0, drho, dy0, dxo, dyo, dit, dst, dob;

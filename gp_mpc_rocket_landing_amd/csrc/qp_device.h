@@ -26,6 +26,8 @@
 #define QP_RHO_TOL 1e-4
 #define QP_RHO_EQ 1e3
 #define QP_DIV_TOL 1e-30
+#define QP_RMAX 8   // max entries per row of A (register-hoisted pattern)
+#define QP_CMAX 12  // max entries per column of A
 
 struct QPSettingsDev {
   double rho, sigma, alpha, eps_abs, eps_rel, eps_prim_inf, eps_dual_inf;
@@ -48,10 +50,15 @@ struct QPPattern {
 
 template <int NMAX, int MMAX, int NNZMAX, int W>
 struct QPSmem {
+  static constexpr int BAND_FRONT = (W + 1) * (W + 2);
+  __device__ double *band() { return band_store + BAND_FRONT; }
   double A[NNZMAX];
-  double P[NMAX], q[NMAX], D[NMAX], x[NMAX], rhs[NMAX], dx[NMAX], aux[NMAX], invd[NMAX], tmpn[NMAX];
+  double P[NMAX], q[NMAX], D[NMAX], x[NMAX], rhs[NMAX], dx[NMAX], aux[NMAX], tmpn[NMAX];
   double E[MMAX], l[MMAX], u[MMAX], rho[MMAX], y[MMAX], z[MMAX], zt[MMAX], dy[MMAX], tmpm[MMAX];
-  double band[NMAX * (W + 1)];
+  // column band, stride W+2: slot 0 holds 1/D_j after factoring, slots 1..W
+  // the multipliers, slot W+1 is always zero; W+1 zero columns in front so
+  // clamped backward-sweep addresses land on a zero slot
+  double band_store[(W + 1) * (W + 2) + NMAX * (W + 2) + 4 * (W + 2)];
   double red[4][8];
   double c, rho_s;
   int flag;
@@ -195,38 +202,44 @@ __device__ void qp_set_rho(const QPPattern &pt, S &s) {
   __syncthreads();
 }
 
-// assemble M = P + sigma I + A' R A into the column band and factor it.
-// band[j*(w+1)+t] = M[j+t][j] -> L[j+t][j]; invd[j] = 1/L[j][j].  Returns 0 or
-// a 1-based failing column.
+// assemble M = P + sigma I + A' R A into the column band and factor it as
+// M = L^ D L^T (L^ unit lower).  band[j*(w+2)+t] = M[j+t][j] -> L^[j+t][j]
+// (1 <= t <= w), band[j*(w+2)] = 1/D[j], band[j*(w+2)+w+1] = 0.  The sweeps
+// then need no division and no lane masks on their critical path.  Returns 0 or a 1-based failing column.
 template <class S>
 __device__ int qp_factor(const QPPattern &pt, S &s, double sigma) {
-  const int n = pt.n, w = pt.w, nb = w + 1, tid = threadIdx.x, nt = blockDim.x;
-  for (int e = tid; e < n * nb; e += nt) {
+  const int n = pt.n, w = pt.w, nb = w + 2, tid = threadIdx.x, nt = blockDim.x;
+  double *band = s.band();
+  for (int e = tid; e < S::BAND_FRONT; e += nt) s.band_store[e] = 0.0;
+  for (int e = tid; e < (n + 4) * nb; e += nt) {
     const int j = e / nb, t = e - j * nb;
-    double v = (t == 0) ? s.P[j] + sigma : 0.0;
-    for (int k = pt.bandptr[e]; k < pt.bandptr[e + 1]; ++k) {
-      const int r = pt.terms[3 * k], a = pt.terms[3 * k + 1], b = pt.terms[3 * k + 2];
-      v += s.rho[r] * s.A[a] * s.A[b];
+    double v = 0.0;
+    if (j < n && t <= w) {
+      const int eb = j * (w + 1) + t;  // pattern's (w+1)-stride band index
+      v = (t == 0) ? s.P[j] + sigma : 0.0;
+      for (int k = pt.bandptr[eb]; k < pt.bandptr[eb + 1]; ++k) {
+        const int r = pt.terms[3 * k], a = pt.terms[3 * k + 1], b = pt.terms[3 * k + 2];
+        v += s.rho[r] * s.A[a] * s.A[b];
+      }
     }
-    s.band[e] = v;
+    band[e] = v;
   }
   if (tid == 0) s.flag = 0;
-  __syncthreads();
+  // (t, u) pair of this thread for the trailing update, 1 <= u <= t <= w
   const int nup = w * (w + 1) / 2;
+  const bool upd = tid < nup;
+  int t = 0, u = 0;
+  if (upd) {
+    t = (int)((sqrt(8.0 * tid + 1.0) + 1.0) * 0.5);
+    while (t * (t - 1) / 2 > tid) --t;
+    while ((t + 1) * t / 2 <= tid) ++t;
+    u = tid - t * (t - 1) / 2 + 1;
+  }
+  __syncthreads();
   for (int j = 0; j < n; ++j) {
-    double *col = s.band + j * nb;
+    double *col = band + j * nb;
     const double dj = col[0];
-    double ct = 0.0, cs = 0.0;
-    int t = 0, u = 0;
-    const bool upd = tid < nup;
-    if (upd) {  // map tid -> (t, u) with 1 <= u <= t <= w
-      t = (int)((sqrt(8.0 * tid + 1.0) + 1.0) * 0.5);
-      while (t * (t - 1) / 2 > tid) --t;
-      while ((t + 1) * t / 2 <= tid) ++t;
-      u = tid - t * (t - 1) / 2 + 1;
-      ct = col[t];
-      cs = col[u];
-    }
+    const double ct = upd ? col[t] : 0.0, cu = upd ? col[u] : 0.0;
     const double cw = (tid >= 1 && tid <= w) ? col[tid] : 0.0;
     __syncthreads();
     if (!(dj > 0.0)) {
@@ -234,89 +247,158 @@ __device__ int qp_factor(const QPPattern &pt, S &s, double sigma) {
       __syncthreads();
       return s.flag;
     }
-    const double d = sqrt(dj);
-    if (tid == 0) {
-      col[0] = d;
-      s.invd[j] = 1.0 / d;
-    }
-    if (tid >= 1 && tid <= w && j + tid < n) col[tid] = cw / d;
-    if (upd && j + t < n) {
-      // M[j+t][j+u] -= L[j+t][j] L[j+u][j]   (stored at band[(j+u)*nb + (t-u)])
-      s.band[(j + u) * nb + (t - u)] -= (ct / d) * (cs / d);
-    }
+    const double inv = 1.0 / dj;
+    if (tid == 0) col[0] = inv;  // the pivot lane's own update is discarded
+    if (tid >= 1 && tid <= w && j + tid < n) col[tid] = cw * inv;
+    // M[j+t][j+u] -= l_t d_j l_u = (c_t / d_j) c_u   (stored at band[(j+u)*nb + (t-u)])
+    if (upd && j + t < n) band[(j + u) * nb + (t - u)] -= (ct * inv) * cu;
     __syncthreads();
   }
   return 0;
 }
 
-// b <- M^-1 b with M = L L' in the column band (wave 0 only; others idle)
+// b <- M^-1 b with M = L^ D L^T in the column band (wave 0 only; others idle).
+// Row i of the right-hand side lives in lane i mod 64 ("modular window").  At
+// step j the lane at offset t = (row - j) mod 64 multiplies band slot min(t,
+// w+1) of column j: slot 0 and slot w+1 hold zeros, so lanes outside the band
+// need no mask.  The pivot value is read with readlane and captured with
+// writelane; lanes that pivoted are refilled from the prefetched next window
+// in bulk every 16 steps (a refilled row is first updated >= 48 steps after
+// its lane pivots).  Band multipliers are prefetched 4 steps ahead.  A step is
+// 2 readlane + 1 FMA + 2 writelane + the prefetch.
+__device__ __forceinline__ void writelane_d(double &dst, double v, int l) {
+  // v is wave-uniform (a readlane result), l an SGPR lane index
+  int lo = __double2loint(dst), hi = __double2hiint(dst);
+  // gfx9 constant bus: one SGPR operand per VOP3, so the lane index goes in m0
+  asm("v_writelane_b32 %0, %2, m0\n\tv_writelane_b32 %1, %3, m0"
+      : "+v"(lo), "+v"(hi)
+      : "s"(__double2loint(v)), "s"(__double2hiint(v)), "{m0}"(l));
+  dst = __hiloint2double(hi, lo);
+}
+
 template <class S>
 __device__ void qp_band_solve(const QPPattern &pt, S &s, double *b) {
   if (threadIdx.x >= 64) return;
-  const int n = pt.n, w = pt.w, nb = w + 1;
+  const int n = pt.n, w = pt.w, nb = w + 2, wz = w + 1;
   const int lane = threadIdx.x;
-  // forward: L y = b
-  double win = (lane < n) ? b[lane] : 0.0;
-#pragma unroll 2
-  for (int j = 0; j < n; ++j) {
-    const int pl = j & 63;
-    const double yj = readlane_d(win, pl) * s.invd[j];
-    const int t = 1 + ((lane - j - 1) & 63);  // row j + t owned by this lane
-    const double lv = (t <= w && j + t < n) ? s.band[j * nb + t] : 0.0;
-    if (lane == pl) {
-      b[j] = yj;
-      win = (j + 64 < n) ? b[j + 64] : 0.0;
-    } else {
-      win = fma(-lv, yj, win);
+  const double *band = s.band();
+  // ---- forward: L^ z = b ; stores w = z / D in b.  L^[j+t][j] = band[j*nb + t]
+  {
+    double win = (lane < n) ? b[lane] : 0.0;
+    for (int j0 = 0; j0 < n; j0 += 64) {
+      const int rn = j0 + 64 + lane;
+      const double nxt = (rn < n) ? b[rn] : 0.0;
+      const int jend = min(n, j0 + 64);
+      double mine = 0.0;
+#define QP_LDF(jj) band[(jj) * nb + min((lane - (jj)) & 63, wz)]
+#define QP_FSTEP(jj, lv)                          \
+  {                                               \
+    const int pl = (jj) & 63;                     \
+    const double zj = readlane_d(win, pl);        \
+    win = fma(-(lv), zj, win);                    \
+    writelane_d(mine, zj, pl);                    \
+  }
+      for (int g = j0; g < jend; g += 16) {
+        const int gend = min(jend, g + 16);
+        if (gend - g == 16) {
+          double l0 = QP_LDF(g), l1 = QP_LDF(g + 1), l2 = QP_LDF(g + 2), l3 = QP_LDF(g + 3);
+#pragma unroll
+          for (int q = 0; q < 16; q += 4) {
+            const int j = g + q;
+            const double n0 = QP_LDF(j + 4), n1 = QP_LDF(j + 5), n2 = QP_LDF(j + 6), n3 = QP_LDF(j + 7);
+            QP_FSTEP(j, l0);
+            QP_FSTEP(j + 1, l1);
+            QP_FSTEP(j + 2, l2);
+            QP_FSTEP(j + 3, l3);
+            l0 = n0; l1 = n1; l2 = n2; l3 = n3;
+          }
+        } else {
+          for (int j = g; j < gend; ++j) {
+            const double l0 = QP_LDF(j);
+            QP_FSTEP(j, l0);
+          }
+        }
+        // lanes that pivoted in [g, gend) take their row of the next window
+        win = ((unsigned)(lane - (g - j0)) < (unsigned)(gend - g)) ? nxt : win;
+      }
+#undef QP_FSTEP
+#undef QP_LDF
+      if (j0 + lane < jend) b[j0 + lane] = mine * band[(j0 + lane) * nb];
     }
   }
   __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-  // backward: L' x = y
+  // ---- backward: L^T x = w.  lane's row r = i - t;  L^[i][r] = band[r*nb + t]
+  //      with t clamped to w+1: band[i*nb - (nb-1)*min(t, w+1)]
   {
-    const int base = n - 64;
-    const int i0 = base + ((lane - base) & 63);
-    win = (i0 >= 0 && i0 < n) ? b[i0] : 0.0;
+    // lanes past the (partial) top window start on their row of the block below,
+    // as if they had already pivoted in the top window
+    const int top = ((n - 1) >> 6) << 6;
+    double win = (top + lane < n) ? b[top + lane] : ((top - 64 + lane >= 0) ? b[top - 64 + lane] : 0.0);
+    for (int i0 = top; i0 >= 0; i0 -= 64) {
+      const int rp = i0 - 64 + lane;
+      const double nxt = (rp >= 0) ? b[rp] : 0.0;
+      const int ihi = min(n, i0 + 64) - 1;
+      double mine = 0.0;
+#define QP_LDB(ii) band[(ii) * nb - (nb - 1) * min(((ii) - lane) & 63, wz)]
+#define QP_BSTEP(ii, lv)                          \
+  {                                               \
+    const int pl = (ii) & 63;                     \
+    const double xi = readlane_d(win, pl);        \
+    win = fma(-(lv), xi, win);                    \
+    writelane_d(mine, xi, pl);                    \
   }
-#pragma unroll 2
-  for (int i = n - 1; i >= 0; --i) {
-    const int pl = i & 63;
-    const double xi = readlane_d(win, pl) * s.invd[i];
-    const int t = 1 + ((i - 1 - lane) & 63);  // row r = i - t owned by this lane
-    const int r = i - t;
-    const double lv = (t <= w && r >= 0) ? s.band[r * nb + t] : 0.0;
-    if (lane == pl) {
-      b[i] = xi;
-      win = (i - 64 >= 0) ? b[i - 64] : 0.0;
-    } else {
-      win = fma(-lv, xi, win);
+      for (int g = ihi; g >= i0; g -= 16) {
+        const int gend = max(i0 - 1, g - 16);  // exclusive
+        if (g - gend == 16) {
+          double l0 = QP_LDB(g), l1 = QP_LDB(g - 1), l2 = QP_LDB(g - 2), l3 = QP_LDB(g - 3);
+#pragma unroll
+          for (int q = 0; q < 16; q += 4) {
+            const int i = g - q;
+            const double n0 = QP_LDB(i - 4), n1 = QP_LDB(i - 5), n2 = QP_LDB(i - 6), n3 = QP_LDB(i - 7);
+            QP_BSTEP(i, l0);
+            QP_BSTEP(i - 1, l1);
+            QP_BSTEP(i - 2, l2);
+            QP_BSTEP(i - 3, l3);
+            l0 = n0; l1 = n1; l2 = n2; l3 = n3;
+          }
+        } else {
+          for (int i = g; i > gend; --i) {
+            const double l0 = QP_LDB(i);
+            QP_BSTEP(i, l0);
+          }
+        }
+        // lanes that pivoted in (gend, g] take their row of the window below
+        win = ((unsigned)(lane - (gend + 1 - i0)) < (unsigned)(g - gend)) ? nxt : win;
+      }
+#undef QP_BSTEP
+#undef QP_LDB
+      if (i0 + lane <= ihi) b[i0 + lane] = mine;
     }
   }
   __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
 }
 
-// residuals (auxil.c update_info) into s.zt = A x, s.aux = P x, s.dx-safe scratch
-// returns pri, dua and the tolerance norms; scratch: zt <- Ax, aux <- Px, rhs <- A'y
+// residuals (auxil.c update_info): tmpm <- A x, aux <- P x, tmpn <- A' y.
+// o: 0 pri (unscaled)  1 |z/E|  2 |Ax/E|  3 dua*c  4 |q/D|  5 |A'y/D|  6 |Px/D|
 template <class S>
 __device__ void qp_update_info(const QPPattern &pt, S &s, double (&o)[8]) {
   const int n = pt.n, m = pt.m, tid = threadIdx.x, nt = blockDim.x;
-  qp_spmv(pt, s, s.x, s.zt);
-  qp_spmv_t(pt, s, s.y, s.rhs);
+  qp_spmv(pt, s, s.x, s.tmpm);
+  qp_spmv_t(pt, s, s.y, s.tmpn);
   for (int j = tid; j < n; j += nt) s.aux[j] = s.P[j] * s.x[j];
   __syncthreads();
-  // o: 0 pri (unscaled)  1 |z/E|  2 |Ax/E|  3 dua*c  4 |q/D|  5 |A'y/D|  6 |Px/D|
-  //    7 unused
   double v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   for (int r = tid; r < m; r += nt) {
     const double e = s.E[r];
-    v[0] = fmax(v[0], fabs((s.zt[r] - s.z[r]) / e));
+    v[0] = fmax(v[0], fabs((s.tmpm[r] - s.z[r]) / e));
     v[1] = fmax(v[1], fabs(s.z[r] / e));
-    v[2] = fmax(v[2], fabs(s.zt[r] / e));
+    v[2] = fmax(v[2], fabs(s.tmpm[r] / e));
   }
   for (int j = tid; j < n; j += nt) {
     const double d = s.D[j];
-    v[3] = fmax(v[3], fabs((s.q[j] + s.aux[j] + s.rhs[j]) / d));
+    v[3] = fmax(v[3], fabs((s.q[j] + s.aux[j] + s.tmpn[j]) / d));
     v[4] = fmax(v[4], fabs(s.q[j] / d));
-    v[5] = fmax(v[5], fabs(s.rhs[j] / d));
+    v[5] = fmax(v[5], fabs(s.tmpn[j] / d));
     v[6] = fmax(v[6], fabs(s.aux[j] / d));
   }
   block_max<8>(v, s.red);
@@ -348,10 +430,10 @@ __device__ bool qp_primal_infeasible(const QPPattern &pt, S &s, double eps) {
     sm[0] += s.u[r] * fmax(s.dy[r], 0.0) + s.l[r] * fmin(s.dy[r], 0.0);
   block_sum<1>(sm, s.red);
   if (!(sm[0] < -eps * nrm)) return false;
-  qp_spmv_t(pt, s, s.dy, s.tmpn);
+  qp_spmv_t(pt, s, s.dy, s.rhs);  // rhs is free at check time
   __syncthreads();
   double mx[1] = {0.0};
-  for (int j = tid; j < n; j += nt) mx[0] = fmax(mx[0], fabs(s.tmpn[j] / s.D[j]));
+  for (int j = tid; j < n; j += nt) mx[0] = fmax(mx[0], fabs(s.rhs[j] / s.D[j]));
   block_max<1>(mx, s.red);
   return mx[0] < eps * nrm;
 }
@@ -372,11 +454,11 @@ __device__ bool qp_dual_infeasible(const QPPattern &pt, S &s, double eps) {
   block_max<1>(pm, s.red);
   if (!(a[0] < s.c * eps * nrm)) return false;
   if (!(pm[0] < s.c * eps * nrm)) return false;
-  qp_spmv(pt, s, s.dx, s.tmpm);
+  qp_spmv(pt, s, s.dx, s.zt);  // zt is rebuilt after every check
   __syncthreads();
   double bad[1] = {0.0};
   for (int r = tid; r < m; r += nt) {
-    const double vv = s.tmpm[r] / s.E[r];
+    const double vv = s.zt[r] / s.E[r];
     if ((s.u[r] < QP_OSQP_INFTY * QP_MIN_SCALING && vv > eps * nrm) ||
         (s.l[r] > -QP_OSQP_INFTY * QP_MIN_SCALING && vv < -eps * nrm))
       bad[0] = 1.0;
@@ -407,19 +489,19 @@ __device__ bool qp_check(const QPPattern &pt, S &s, const QPSettingsDev &st, con
   return false;
 }
 
-// compute_rho_estimate in the scaled space; scratch from qp_update_info still valid:
-// zt = A x, aux = P x, rhs = A' y
+// compute_rho_estimate in the scaled space, from qp_update_info's scratch
+// (tmpm = A x, aux = P x, tmpn = A' y)
 template <class S>
 __device__ double qp_rho_estimate(const QPPattern &pt, S &s) {
   const int n = pt.n, m = pt.m, tid = threadIdx.x, nt = blockDim.x;
   double v[6] = {0, 0, 0, 0, 0, 0};
   for (int r = tid; r < m; r += nt) {
-    v[0] = fmax(v[0], fabs(s.zt[r] - s.z[r]));
-    v[1] = fmax(v[1], fmax(fabs(s.z[r]), fabs(s.zt[r])));
+    v[0] = fmax(v[0], fabs(s.tmpm[r] - s.z[r]));
+    v[1] = fmax(v[1], fmax(fabs(s.z[r]), fabs(s.tmpm[r])));
   }
   for (int j = tid; j < n; j += nt) {
-    v[2] = fmax(v[2], fabs(s.q[j] + s.aux[j] + s.rhs[j]));
-    v[3] = fmax(v[3], fmax(fmax(fabs(s.q[j]), fabs(s.rhs[j])), fabs(s.aux[j])));
+    v[2] = fmax(v[2], fabs(s.q[j] + s.aux[j] + s.tmpn[j]));
+    v[3] = fmax(v[3], fmax(fmax(fabs(s.q[j]), fabs(s.tmpn[j])), fabs(s.aux[j])));
   }
   block_max<6>(v, s.red);
   const double pr = v[0] / (v[1] + 1e-10);
@@ -427,6 +509,27 @@ __device__ double qp_rho_estimate(const QPPattern &pt, S &s) {
   double est = s.rho_s * sqrt(pr / (du + 1e-10));
   return fmin(fmax(est, QP_RHO_MIN), QP_RHO_MAX);
 }
+
+// diagnostic phase stamps (s_memtime), thread 0 only, enabled by a non-null pointer
+struct QPStamps {
+  unsigned long long *out = nullptr;
+  unsigned long long acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  unsigned long long last = 0;
+  __device__ void start() {
+    if (out && threadIdx.x == 0) last = __builtin_amdgcn_s_memtime();
+  }
+  __device__ void mark(int k) {
+    if (out && threadIdx.x == 0) {
+      const unsigned long long t = __builtin_amdgcn_s_memtime();
+      acc[k] += t - last;
+      last = t;
+    }
+  }
+  __device__ void flush() {
+    if (out && threadIdx.x == 0)
+      for (int k = 0; k < 8; ++k) out[k] += acc[k];
+  }
+};
 
 struct QPResult {
   int status, iter;
@@ -438,9 +541,12 @@ struct QPResult {
 // persistent rho, s.y the persistent scaled dual, s.x the unscaled warm start.
 // On exit s.x/s.y hold the scaled iterates (caller unscales), s.D/E/c the scaling.
 template <class S>
-__device__ QPResult qp_solve(const QPPattern &pt, S &s, const QPSettingsDev &st) {
+__device__ QPResult qp_solve(const QPPattern &pt, S &s, const QPSettingsDev &st,
+                             QPStamps *ts = nullptr) {
   const int n = pt.n, m = pt.m, tid = threadIdx.x, nt = blockDim.x;
   QPResult res{-10, 0, 0.0, 0};
+  QPStamps dummy;
+  QPStamps &T = ts ? *ts : dummy;
   for (int r = tid; r < m; r += nt) {
     s.l[r] = fmax(s.l[r], -QP_OSQP_INFTY);
     s.u[r] = fmin(s.u[r], QP_OSQP_INFTY);
@@ -455,8 +561,10 @@ __device__ QPResult qp_solve(const QPPattern &pt, S &s, const QPSettingsDev &st)
   }
   if (tid == 0) s.rho_s = fmin(fmax(s.rho_s, QP_RHO_MIN), QP_RHO_MAX);
   __syncthreads();
+  T.mark(1);
   qp_set_rho(pt, s);
   int f = qp_factor(pt, s, st.sigma);
+  T.mark(2);
   if (f) { res.factor_fail = f; return res; }
   if (st.warm_start) {
     for (int j = tid; j < n; j += nt) s.x[j] = s.x[j] / s.D[j];
@@ -468,43 +576,82 @@ __device__ QPResult qp_solve(const QPPattern &pt, S &s, const QPSettingsDev &st)
   }
   __syncthreads();
   const double sig = st.sigma, al = st.alpha;
+  // sparsity pattern of this thread's column (A' products) and rows (A
+  // products) hoisted into registers for the whole solve
+  int cn = 0, cidx[QP_CMAX], crow[QP_CMAX];
+  if (tid < n) {
+    const int k0 = pt.colptr[tid];
+    cn = pt.colptr[tid + 1] - k0;
+#pragma unroll
+    for (int e = 0; e < QP_CMAX; ++e) {
+      cidx[e] = (e < cn) ? pt.csc2csr[k0 + e] : 0;
+      crow[e] = (e < cn) ? pt.cscrow[k0 + e] : 0;
+    }
+  }
+  int rb[2], rn[2], rc[2][QP_RMAX];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int r = tid + h * 256;
+    rb[h] = (r < m) ? pt.rowptr[r] : 0;
+    rn[h] = (r < m) ? pt.rowptr[r + 1] - rb[h] : 0;
+#pragma unroll
+    for (int e = 0; e < QP_RMAX; ++e) rc[h][e] = (e < rn[h]) ? pt.colidx[rb[h] + e] : 0;
+  }
+  for (int r = tid; r < m; r += nt) s.zt[r] = s.rho[r] * s.z[r] - s.y[r];
+  __syncthreads();
   bool can_check = false;
   int it;
   double o[8];
   for (it = 1; it <= st.max_iter; ++it) {
     // rhs = sigma x - q + A'(rho z - y)
-    for (int r = tid; r < m; r += nt) s.zt[r] = s.rho[r] * s.z[r] - s.y[r];
-    __syncthreads();
-    qp_spmv_t(pt, s, s.zt, s.rhs);
-    __syncthreads();
-    for (int j = tid; j < n; j += nt) s.rhs[j] = sig * s.x[j] - s.q[j] + s.rhs[j];
-    __syncthreads();
-    qp_band_solve(pt, s, s.rhs);
-    __syncthreads();
-    qp_spmv(pt, s, s.rhs, s.zt);  // z~ = A x~
-    for (int j = tid; j < n; j += nt) {
-      const double xn = al * s.rhs[j] + (1.0 - al) * s.x[j];
-      s.dx[j] = xn - s.x[j];
-      s.x[j] = xn;
+    if (tid < n) {
+      double acc = 0.0;
+#pragma unroll
+      for (int e = 0; e < QP_CMAX; ++e)
+        if (e < cn) acc += s.A[cidx[e]] * s.zt[crow[e]];
+      s.rhs[tid] = sig * s.x[tid] - s.q[tid] + acc;
     }
     __syncthreads();
-    for (int r = tid; r < m; r += nt) {
-      const double zr = al * s.zt[r] + (1.0 - al) * s.z[r];
-      double zn = zr + s.y[r] / s.rho[r];
-      zn = fmin(fmax(zn, s.l[r]), s.u[r]);
-      const double d = s.rho[r] * (zr - zn);
-      s.dy[r] = d;
-      s.y[r] += d;
-      s.z[r] = zn;
+    T.mark(3);
+    qp_band_solve(pt, s, s.rhs);  // x~
+    __syncthreads();
+    T.mark(4);
+    if (tid < n) {
+      const double xo = s.x[tid];
+      const double xn = al * s.rhs[tid] + (1.0 - al) * xo;
+      s.dx[tid] = xn - xo;
+      s.x[tid] = xn;
+    }
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int r = tid + h * 256;
+      if (r < m) {
+        double zt = 0.0;  // z~ = A x~
+#pragma unroll
+        for (int e = 0; e < QP_RMAX; ++e)
+          if (e < rn[h]) zt += s.A[rb[h] + e] * s.rhs[rc[h][e]];
+        const double rho = s.rho[r], zo = s.z[r], yo = s.y[r];
+        const double zr = al * zt + (1.0 - al) * zo;
+        double zn = zr + yo / rho;
+        zn = fmin(fmax(zn, s.l[r]), s.u[r]);
+        const double d = rho * (zr - zn);
+        const double yn = yo + d;
+        s.dy[r] = d;
+        s.y[r] = yn;
+        s.z[r] = zn;
+        s.zt[r] = rho * zn - yn;  // next iteration's A' operand
+      }
     }
     __syncthreads();
+    T.mark(5);
     can_check = st.check_termination && (it % st.check_termination == 0);
+    const bool adapt = st.adaptive_rho && st.adaptive_rho_interval && (it % st.adaptive_rho_interval == 0);
     if (can_check) {
       res.iter = it;
       qp_update_info(pt, s, o);
       if (qp_check(pt, s, st, o, false, res.status)) break;
     }
-    if (st.adaptive_rho && st.adaptive_rho_interval && (it % st.adaptive_rho_interval == 0)) {
+    if (adapt) {
       if (!can_check) {
         res.iter = it;
         qp_update_info(pt, s, o);
@@ -519,6 +666,11 @@ __device__ QPResult qp_solve(const QPPattern &pt, S &s, const QPSettingsDev &st)
         if (f) { res.factor_fail = f; return res; }
       }
     }
+    if (can_check || adapt) {  // rebuild rho z - y (scratch reused / rho changed)
+      for (int r = tid; r < m; r += nt) s.zt[r] = s.rho[r] * s.z[r] - s.y[r];
+      __syncthreads();
+    }
+    T.mark(6);
   }
   if (!can_check) {
     res.iter = it - 1;

@@ -171,6 +171,11 @@ int gpmpc_fleet_step_phases(gpmpc_fleet *f, int phase_mask);
  * 13 initial mass, 14 last QP status, 15 last rho */
 #define GPMPC_REC_LEN 16
 int gpmpc_fleet_read(gpmpc_fleet *f, double *records, double *x /* batch x 7, may be NULL */);
+/* diagnostic: accumulate s_memtime cycles of landing 0's control kernel per
+ * phase into dev_u64x8 (8 x uint64 device buffer; NULL disables):
+ * 0 assembly, 1 scaling, 2 factor, 3 A' rhs, 4 band sweeps, 5 fused z/y update,
+ * 6 checks + adaptive rho, 7 tail (plant step, records) */
+int gpmpc_fleet_set_stamps(gpmpc_fleet *f, void *dev_u64x8);
 /* device pointer of the record array (for collectives) */
 double *gpmpc_fleet_records_dev(gpmpc_fleet *f);
 int gpmpc_fleet_destroy(gpmpc_fleet *f);
