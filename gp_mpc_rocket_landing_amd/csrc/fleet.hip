@@ -36,11 +36,18 @@ struct gpmpc_fleet {
   DevBuf x, Xw, Uw, ysc, rho, rec, xt;      // landing state
   DevBuf Q, Qn, Ks, part, meanT, mean, var;  // GP scratch
   unsigned long long *stamps = nullptr;      // diagnostic (gpmpc_fleet_set_stamps)
+  unsigned long long *trace = nullptr;       // diagnostic (gpmpc_fleet_set_trace)
 };
 
-extern "C" int gpmpc_fleet_set_stamps(gpmpc_fleet *f, void *dev_u64x8) {
+extern "C" int gpmpc_fleet_set_stamps(gpmpc_fleet *f, void *dev_u64x10) {
   GPMPC_CHECK_ARG(f);
-  f->stamps = (unsigned long long *)dev_u64x8;
+  f->stamps = (unsigned long long *)dev_u64x10;
+  return 0;
+}
+
+extern "C" int gpmpc_fleet_set_trace(gpmpc_fleet *f, void *dev_u64xbx4) {
+  GPMPC_CHECK_ARG(f);
+  f->trace = (unsigned long long *)dev_u64xbx4;
   return 0;
 }
 
@@ -154,6 +161,7 @@ struct FleetArgs {
   double *x, *Xw, *Uw, *ysc, *rho, *rec, *xt;
   const double *gmean;  // (B*N) x 3
   unsigned long long *stamps;  // diagnostic phase cycles of block 0 (or null)
+  unsigned long long *trace;   // diagnostic per-landing placement/timing (or null)
 };
 
 __global__ __launch_bounds__(256) void k_fleet_control(FleetArgs a) {
@@ -168,6 +176,12 @@ __global__ __launch_bounds__(256) void k_fleet_control(FleetArgs a) {
   QPStamps T;
   T.out = (b == 0) ? a.stamps : nullptr;
   T.start();
+  if (a.trace && tid == 0) {
+    unsigned long long *tr = a.trace + (int64_t)b * 4;
+    tr[0] = __builtin_amdgcn_s_memrealtime();
+    tr[2] = (unsigned)__builtin_amdgcn_s_getreg(4 | (31 << 11));   // HW_ID: wave, simd, cu, sh, se
+    tr[3] = (unsigned)__builtin_amdgcn_s_getreg(20 | (31 << 11));  // XCC_ID
+  }
   double *x = a.x + (int64_t)b * NX;
   double *Xw = a.Xw + (int64_t)b * (N + 1) * NX;
   double *Uw = a.Uw + (int64_t)b * N * NU;
@@ -357,6 +371,7 @@ __global__ __launch_bounds__(256) void k_fleet_control(FleetArgs a) {
   }
   T.mark(7);
   T.flush();
+  if (a.trace && tid == 0) a.trace[(int64_t)b * 4 + 1] = __builtin_amdgcn_s_memrealtime();
 }
 
 // initial linearisation point: X linear to the target, U hover (osqp_rti.py:425-446)
@@ -501,6 +516,7 @@ static FleetArgs fleet_args(gpmpc_fleet *f) {
   a.xt = f->xt.as<double>();
   a.gmean = f->mean.as<double>();
   a.stamps = f->stamps;
+  a.trace = f->trace;
   return a;
 }
 

@@ -11,10 +11,16 @@
 #define QP_NNZMAX 736
 #define QP_W 16
 typedef QPSmem<QP_NMAX, QP_MMAX, QP_NNZMAX, QP_W> QPSmemStd;
+// factor slots available in QPSmem (its factor area minus the 4 zero columns)
+#define QP_FAC_CAP (QP_NMAX * (QP_W + 1) + 64)
 
 struct QPPatternHost {
   int n = 0, m = 0, nnz = 0, w = 0, maxrow = 0, maxcol = 0;
-  bool fits() const { return n <= QP_NMAX && m <= QP_MMAX && nnz <= QP_NNZMAX && w <= QP_W && maxrow <= QP_RMAX && maxcol <= QP_CMAX; }
+  int mode = 0, fac_len = 0, nblk = 0;
+  bool fits() const {
+    return n <= QP_NMAX && m <= QP_MMAX && nnz <= QP_NNZMAX && maxrow <= QP_RMAX &&
+           maxcol <= QP_CMAX && (mode == 1 || (w <= QP_W && fac_len <= QP_FAC_CAP));
+  }
   DevBuf buf;
   QPPattern dev{};
   int build(int n, int m, const int *rowptr, const int *colidx, hipStream_t s);

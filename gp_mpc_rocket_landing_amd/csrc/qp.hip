@@ -64,26 +64,64 @@ int QPPatternHost::build(int n_, int m_, const int *rowptr, const int *colidx, h
       csc2csr[p] = k;
       cscrow[p] = r;
     }
-  // band product terms, generated in (row, a, b) order like the C oracle's factor()
+  // Factor layout.  Mode 1 (block tridiagonal, qp_block.h) when every coupled
+  // pair (i >= j) of M = P + A'RA lies in one block of QP_BLK_SZ variables or
+  // in neighbouring blocks with i among the first QP_BLK_CM rows of its block
+  // (the MPC stage structure); otherwise mode 0, the banded LDL^T with column
+  // stride QP_W+1.  Either way every LDS slot gets its list of rho_r A[a] A[b]
+  // terms, generated in (row, a, b) order like the C oracle's factor().
+  constexpr int NB = QP_W + 1, SZ = QP_BLK_SZ, CM = QP_BLK_CM, BS = SZ * SZ + SZ * CM;
+  nblk = (n + SZ - 1) / SZ;
+  bool blk = true;
+  for (int r = 0; r < m && blk; ++r)
+    for (int a = rowptr[r]; a < rowptr[r + 1]; ++a)
+      for (int b = rowptr[r]; b < rowptr[r + 1]; ++b) {
+        const int i = colidx[a], j = colidx[b];
+        if (j > i) continue;
+        const int bi = i / SZ, bj = j / SZ;
+        if (!(bi == bj || (bi == bj + 1 && i - bi * SZ < CM))) blk = false;
+      }
+  if (blk && nblk * BS - SZ * CM > QP_FAC_CAP) blk = false;
+  mode = blk ? 1 : 0;
+  fac_len = blk ? nblk * BS - SZ * CM : n * NB;
   struct T { int e, r, a, b; };
   std::vector<T> terms;
+  std::vector<int> facdiag(fac_len, -1);
   for (int r = 0; r < m; ++r)
     for (int a = rowptr[r]; a < rowptr[r + 1]; ++a)
       for (int b = rowptr[r]; b < rowptr[r + 1]; ++b) {
         const int i = colidx[a], j = colidx[b];
         if (j > i) continue;
-        terms.push_back(T{j * nb + (i - j), r, a, b});
+        if (!blk) {
+          terms.push_back(T{j * NB + (i - j), r, a, b});
+          continue;
+        }
+        const int bi = i / SZ, bj = j / SZ, ri = i - bi * SZ, rj = j - bj * SZ;
+        if (bi == bj) {
+          terms.push_back(T{bi * BS + rj * SZ + ri, r, a, b});
+          if (i != j) terms.push_back(T{bi * BS + ri * SZ + rj, r, a, b});
+        } else {
+          terms.push_back(T{bj * BS + SZ * SZ + rj * CM + ri, r, a, b});
+        }
       }
+  if (blk) {
+    for (int v = 0; v < nblk * SZ; ++v) {
+      const int k = v / SZ, rv = v - k * SZ;
+      facdiag[k * BS + rv * SZ + rv] = (v < n) ? v : -2;  // identity rows pad the last block
+    }
+  } else {
+    for (int j = 0; j < n; ++j) facdiag[j * NB] = j;
+  }
   std::stable_sort(terms.begin(), terms.end(), [](const T &x, const T &y) { return x.e < y.e; });
-  std::vector<int> bandptr(n * nb + 1, 0), tv(3 * terms.size());
+  std::vector<int> facptr(fac_len + 1, 0), tv(3 * terms.size());
   for (size_t k = 0; k < terms.size(); ++k) {
-    bandptr[terms[k].e + 1]++;
+    facptr[terms[k].e + 1]++;
     tv[3 * k] = terms[k].r;
     tv[3 * k + 1] = terms[k].a;
     tv[3 * k + 2] = terms[k].b;
   }
-  for (int e = 0; e < n * nb; ++e) bandptr[e + 1] += bandptr[e];
-  // one device block: rowptr | colidx | colptr | csc2csr | cscrow | bandptr | terms
+  for (int e = 0; e < fac_len; ++e) facptr[e + 1] += facptr[e];
+  // one device block: rowptr | colidx | colptr | csc2csr | cscrow | facptr | facdiag | terms
   std::vector<int> all;
   auto app = [&](const int *p, size_t k) { all.insert(all.end(), p, p + k); };
   const size_t o_rp = 0;
@@ -97,7 +135,9 @@ int QPPatternHost::build(int n_, int m_, const int *rowptr, const int *colidx, h
   const size_t o_cr = all.size();
   app(cscrow.data(), nnz);
   const size_t o_bp = all.size();
-  app(bandptr.data(), bandptr.size());
+  app(facptr.data(), facptr.size());
+  const size_t o_fd = all.size();
+  app(facdiag.data(), facdiag.size());
   const size_t o_tv = all.size();
   app(tv.data(), tv.size());
   if (buf.alloc(sizeof(int) * all.size()) != hipSuccess) return -1;
@@ -108,7 +148,8 @@ int QPPatternHost::build(int n_, int m_, const int *rowptr, const int *colidx, h
   const int *d = buf.as<int>();
   dev.n = n; dev.m = m; dev.nnz = nnz; dev.w = w;
   dev.rowptr = d + o_rp; dev.colidx = d + o_ci; dev.colptr = d + o_cp; dev.csc2csr = d + o_cm;
-  dev.cscrow = d + o_cr; dev.bandptr = d + o_bp; dev.terms = d + o_tv;
+  dev.cscrow = d + o_cr; dev.facptr = d + o_bp; dev.facdiag = d + o_fd; dev.terms = d + o_tv;
+  dev.mode = mode; dev.fac_len = fac_len; dev.nblk = nblk; dev.bsz = SZ; dev.bcm = CM;
   return 0;
 }
 

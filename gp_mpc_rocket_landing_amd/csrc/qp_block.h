@@ -1,0 +1,250 @@
+// qp_block.h -- block-tridiagonal factor/solve of the reduced KKT matrix
+//     M = P + sigma I + A' R A
+// for QPs whose variables split into uniform blocks of SZ (the MPC stages
+// [x_k, u_k]) such that M couples only neighbouring blocks, and block k+1
+// couples to block k only through its first CM rows (x_{k+1}).  Included by
+// qp_device.h; used when the host pattern analysis selects mode 1.
+//
+//   S_0 = M_00,  S_{k+1} = M_{k+1,k+1} - G_k C_k^T,   G_k = C_k S_k^-1,
+//   C_k = M[block k+1 (first CM rows)][block k]
+// solve  M x = b :
+//   forward   y_0 = b_0,  y_{k+1} = b_{k+1} - G_k y_k         (chain, SZ FMAs/block)
+//   diagonal  u_k = S_k^-1 y_k                                 (independent blocks)
+//   backward  x_K = u_K,  x_k = u_k - G_k^T x_{k+1}            (chain, CM FMAs/block)
+//
+// Everything runs in wave 0 with one block row per lane of a 16-lane DPP row
+// (the four rows of the wave replicate the chain, or work on four blocks at
+// once in the diagonal step).  The vector operand of every block product is
+// broadcast with DPP row_newbcast straight into v_fmac_f64, so the chains
+// need no readlane, no LDS round trip and no barrier: a forward block is 10
+// dependent-free FMAs + one add.
+//
+// Storage (doubles, in the factor area of QPSmem), block stride
+// BS = SZ*SZ + SZ*CM:
+//   [k*BS, +SZ*SZ)       S_k^-1  column-major (symmetric)   slot j*SZ + r = S^-1[r][j]
+//   [k*BS + SZ*SZ, +SZ*CM) G_k   column-major               slot j*CM + r = G_k[r][j]
+// (before factoring the same slots hold M_kk and C_k; a last block shorter
+// than SZ is padded with identity rows by the host).
+#pragma once
+
+// value of lane J of each 16-lane row, in every lane of that row
+template <int J>
+__device__ __forceinline__ double bc16(double v) {
+  return __builtin_amdgcn_mov_dpp(v, 0x150 + J, 0xf, 0xf, true);
+}
+__device__ __forceinline__ double bc16_rt(double v, int j) {
+  switch (j) {  // j is a constant after unrolling
+    case 0: return bc16<0>(v);
+    case 1: return bc16<1>(v);
+    case 2: return bc16<2>(v);
+    case 3: return bc16<3>(v);
+    case 4: return bc16<4>(v);
+    case 5: return bc16<5>(v);
+    case 6: return bc16<6>(v);
+    case 7: return bc16<7>(v);
+    case 8: return bc16<8>(v);
+    case 9: return bc16<9>(v);
+    case 10: return bc16<10>(v);
+    case 11: return bc16<11>(v);
+    case 12: return bc16<12>(v);
+    case 13: return bc16<13>(v);
+    case 14: return bc16<14>(v);
+    default: return bc16<15>(v);
+  }
+}
+
+// acc += bcast_J(src) * mul as ONE v_fmac_f64_dpp.  The compiler does not see
+// the DPP read of src inside the asm, so the first FMA of a chain carries the
+// two wait states a DPP read of a just-written VGPR needs.
+template <int J, bool NOP>
+__device__ __forceinline__ void fmac_bc(double &acc, double src, double mul) {
+  if (NOP)
+    asm volatile("s_nop 1\n\tv_fmac_f64_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf"
+                 : "+v"(acc) : "v"(src), "v"(mul), "i"(J));
+  else
+    asm volatile("v_fmac_f64_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf"
+                 : "+v"(acc) : "v"(src), "v"(mul), "i"(J));
+}
+// returns sum_j mul[j] * bcast_j(src), two interleaved accumulators
+template <int... J>
+__device__ __forceinline__ double dot_bc(double src, const double *mul, std::integer_sequence<int, J...>) {
+  double a0 = 0.0, a1 = 0.0;
+  ((J % 2 == 0 ? fmac_bc<J, J == 0>(a0, src, mul[J]) : fmac_bc<J, false>(a1, src, mul[J])), ...);
+  return a0 + a1;
+}
+// same with compiler-visible DPP moves (2 VALU per term, exact waitcnts)
+template <int... J>
+__device__ __forceinline__ double dot_bcv(double src, const double *mul, std::integer_sequence<int, J...>) {
+  double a0 = 0.0, a1 = 0.0;
+  ((J % 2 == 0 ? (void)(a0 = fma(bc16<J>(src), mul[J], a0)) : (void)(a1 = fma(bc16<J>(src), mul[J], a1))), ...);
+  return a0 + a1;
+}
+#ifndef QP_DOT_ASM
+#define QP_DOT_ASM 0
+#endif
+template <int K>
+__device__ __forceinline__ double dot_bc(double src, const double *mul) {
+  if (QP_DOT_ASM) return dot_bc(src, mul, std::make_integer_sequence<int, K>{});
+  return dot_bcv(src, mul, std::make_integer_sequence<int, K>{});
+}
+
+// factor: returns 0 or the 1-based failing (non-positive pivot) variable.
+// Wave 0 only, all 64 lanes (rows replicate).
+template <int SZ, int CM, class S>
+__device__ int blk_factor(const QPPattern &pt, S &s) {
+  constexpr int BS = SZ * SZ + SZ * CM;
+  const int lane = threadIdx.x, rr = lane & 15;
+  const bool wr = lane < 16;
+  const int rs = rr < SZ ? rr : SZ - 1, rc = rr < CM ? rr : CM - 1;
+  double *F = s.band();
+  const int nblk = pt.nblk;
+  double u[CM];  // Schur update of the next block's CM x CM corner, row rr
+#pragma unroll
+  for (int i = 0; i < CM; ++i) u[i] = 0.0;
+  for (int k = 0; k < nblk; ++k) {
+    double *Sk = F + k * BS;
+    double a[SZ];
+#pragma unroll
+    for (int j = 0; j < SZ; ++j) a[j] = Sk[j * SZ + rs];
+    if (rr < CM) {
+#pragma unroll
+      for (int j = 0; j < CM; ++j) a[j] -= u[j];
+    }
+    // in-place Gauss-Jordan inverse (SPD: no pivoting); pivot row by DPP
+#pragma unroll
+    for (int p = 0; p < SZ; ++p) {
+      const double piv = bc16_rt(a[p], p);
+      if (!(piv > 0.0)) return k * SZ + p + 1;
+      const double inv = 1.0 / piv;
+      // lane p: row *= inv  (= row + row*(inv-1));  other lanes: row -= a[p]/piv * row_p
+      const double f = (rr == p) ? inv - 1.0 : -a[p] * inv;
+#pragma unroll
+      for (int c = 0; c < SZ; ++c)
+        if (c != p) a[c] = fma(bc16_rt(a[c], p), f, a[c]);
+      a[p] = (rr == p) ? inv : f;
+    }
+    if (wr && rr < SZ) {
+#pragma unroll
+      for (int j = 0; j < SZ; ++j) Sk[j * SZ + rr] = a[j];
+    }
+    if (k + 1 < nblk) {
+      double *Ck = Sk + SZ * SZ;
+      double c[SZ], g[SZ];
+#pragma unroll
+      for (int j = 0; j < SZ; ++j) {
+        c[j] = Ck[j * CM + rc];
+        g[j] = 0.0;
+      }
+      // G[rr][j] = sum_l C[rr][l] S^-1[l][j]
+#pragma unroll
+      for (int l = 0; l < SZ; ++l) {
+#pragma unroll
+        for (int j = 0; j < SZ; ++j) g[j] = fma(c[l], bc16_rt(a[j], l), g[j]);
+      }
+      if (wr && rr < CM) {
+#pragma unroll
+        for (int j = 0; j < SZ; ++j) Ck[j * CM + rr] = g[j];
+      }
+      // u[rr][i] = sum_j G[rr][j] C[i][j]
+#pragma unroll
+      for (int i = 0; i < CM; ++i) {
+        double t = 0.0;
+#pragma unroll
+        for (int j = 0; j < SZ; ++j) t = fma(g[j], bc16_rt(c[j], i), t);
+        u[i] = t;
+      }
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+  return 0;
+}
+
+// b <- M^-1 b.  Wave 0 only.
+template <int SZ, int CM, class S>
+__device__ void blk_solve(const QPPattern &pt, S &s, double *b) {
+  if (threadIdx.x >= 64) return;
+  constexpr int BS = SZ * SZ + SZ * CM;
+  const int lane = threadIdx.x, rr = lane & 15, row = lane >> 4;
+  const bool wr = lane < 16;
+  const int rs = rr < SZ ? rr : SZ - 1, rc = rr < CM ? rr : CM - 1;
+  const int n = pt.n, nblk = pt.nblk;
+  const double *F = s.band();
+  // ---- forward: y_{k+1} = b_{k+1} - G_k y_k on the first CM rows of block k+1
+  {
+    double y = (rr < SZ && rr < n) ? b[rr] : 0.0;
+    double g[SZ];
+#pragma unroll
+    for (int j = 0; j < SZ; ++j) g[j] = F[SZ * SZ + j * CM + rc];
+    for (int k = 0; k + 1 < nblk; ++k) {
+      const int s1 = (k + 1) * SZ;
+      const double bn = (rr < SZ && s1 + rr < n) ? b[s1 + rr] : 0.0;
+      double gn[SZ];
+      if (k + 2 < nblk) {
+        const double *Gn = F + (k + 1) * BS + SZ * SZ;
+#pragma unroll
+        for (int j = 0; j < SZ; ++j) gn[j] = Gn[j * CM + rc];
+      }
+      const double acc = dot_bc<SZ>(y, g);
+      if (wr && rr < SZ) b[k * SZ + rr] = y;
+      y = (rr < CM) ? bn - acc : bn;
+#pragma unroll
+      for (int j = 0; j < SZ; ++j) g[j] = gn[j];
+    }
+    const int sl = (nblk - 1) * SZ;
+    if (wr && rr < SZ && sl + rr < n) b[sl + rr] = y;
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+  // ---- diagonal blocks, four at a time (one per DPP row): u_k = S_k^-1 y_k
+  for (int k = row; k < nblk; k += 4) {
+    const int s0 = k * SZ;
+    const bool live = rr < SZ && s0 + rr < n;
+    const double yv = live ? b[s0 + rr] : 0.0;
+    double sv[SZ];
+#pragma unroll
+    for (int j = 0; j < SZ; ++j) sv[j] = F[k * BS + j * SZ + rs];
+    const double uv = dot_bc<SZ>(yv, sv);
+    if (live) b[s0 + rr] = uv;
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+  // ---- backward: x_k = u_k - G_k^T x_{k+1}
+  {
+    const int sl = (nblk - 1) * SZ;
+    double x = (rr < SZ && sl + rr < n) ? b[sl + rr] : 0.0;
+    double gt[CM];
+    if (nblk >= 2) {
+      const double *G = F + (nblk - 2) * BS + SZ * SZ;
+#pragma unroll
+      for (int i = 0; i < CM; ++i) gt[i] = G[rs * CM + i];
+    }
+    for (int k = nblk - 2; k >= 0; --k) {
+      const double un = (rr < SZ) ? b[k * SZ + rr] : 0.0;
+      double gtn[CM];
+      if (k > 0) {
+        const double *G = F + (k - 1) * BS + SZ * SZ;
+#pragma unroll
+        for (int i = 0; i < CM; ++i) gtn[i] = G[rs * CM + i];
+      }
+      const double acc = dot_bc<CM>(x, gt);
+      const int s1 = (k + 1) * SZ;
+      if (wr && rr < SZ && s1 + rr < n) b[s1 + rr] = x;
+      x = un - acc;
+#pragma unroll
+      for (int i = 0; i < CM; ++i) gt[i] = gtn[i];
+    }
+    if (wr && rr < SZ && rr < n) b[rr] = x;
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+}
+
+// the compiled (SZ, CM) instantiations; the host only selects mode 1 for these
+#define QP_BLK_SZ 10  // 3-DoF MPC stage [x_k (7), u_k (3)]
+#define QP_BLK_CM 7   // coupled through x_{k+1}
+
+template <class S>
+__device__ int blk_factor_dispatch(const QPPattern &pt, S &s) {
+  return blk_factor<QP_BLK_SZ, QP_BLK_CM>(pt, s);
+}
+template <class S>
+__device__ void blk_solve_dispatch(const QPPattern &pt, S &s, double *b) {
+  blk_solve<QP_BLK_SZ, QP_BLK_CM>(pt, s, b);
+}

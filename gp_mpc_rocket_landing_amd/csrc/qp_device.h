@@ -17,6 +17,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <cstdint>
+#include <utility>
 
 #define QP_OSQP_INFTY 1e30
 #define QP_MIN_SCALING 1e-4
@@ -44,21 +45,26 @@ struct QPPattern {
   const int *colptr;   // n+1   (CSC)
   const int *csc2csr;  // nnz   CSC entry -> CSR value index
   const int *cscrow;   // nnz   CSC entry -> row
-  const int *bandptr;  // n*(w+1)+1  band entry (j,t) -> term range
+  // factor storage: fac_len LDS slots assembled as  [P_d + sigma] + sum rho_r A[a] A[b]
+  int mode;            // 0: banded LDL^T (slot j*(W+1)+t);  1: block tridiagonal (qp_block.h)
+  int fac_len;
+  int nblk, bsz, bcm;  // mode 1: nblk blocks of bsz variables, coupling prefix bcm
+  const int *facptr;   // fac_len+1  slot -> term range
+  const int *facdiag;  // fac_len    variable d whose P_d + sigma lands in the slot, -1 none, -2 one
   const int *terms;    // 3*nterms: (row, a, b) value pairs with rho_row*A[a]*A[b]
 };
 
 template <int NMAX, int MMAX, int NNZMAX, int W>
 struct QPSmem {
-  static constexpr int BAND_FRONT = (W + 1) * (W + 2);
-  __device__ double *band() { return band_store + BAND_FRONT; }
+  static constexpr int NB = W + 1;  // band column stride
+  __device__ double *band() { return band_store; }
   double A[NNZMAX];
   double P[NMAX], q[NMAX], D[NMAX], x[NMAX], rhs[NMAX], dx[NMAX], aux[NMAX], tmpn[NMAX];
   double E[MMAX], l[MMAX], u[MMAX], rho[MMAX], y[MMAX], z[MMAX], zt[MMAX], dy[MMAX], tmpm[MMAX];
-  // column band, stride W+2: slot 0 holds 1/D_j after factoring, slots 1..W
-  // the multipliers, slot W+1 is always zero; W+1 zero columns in front so
-  // clamped backward-sweep addresses land on a zero slot
-  double band_store[(W + 1) * (W + 2) + NMAX * (W + 2) + 4 * (W + 2)];
+  // column band, stride W+1: slot 0 of column j holds 1/D_j after factoring,
+  // slots 1..W the multipliers L^[j+t][j] (zero beyond the pattern's w);
+  // 64 doubles of tail padding for the sweeps' masked-lane loads
+  double band_store[NMAX * (W + 1) + 4 * (W + 1) + 64];
   double red[4][8];
   double c, rho_s;
   int flag;
@@ -203,26 +209,36 @@ __device__ void qp_set_rho(const QPPattern &pt, S &s) {
 }
 
 // assemble M = P + sigma I + A' R A into the column band and factor it as
-// M = L^ D L^T (L^ unit lower).  band[j*(w+2)+t] = M[j+t][j] -> L^[j+t][j]
-// (1 <= t <= w), band[j*(w+2)] = 1/D[j], band[j*(w+2)+w+1] = 0.  The sweeps
-// then need no division and no lane masks on their critical path.  Returns 0 or a 1-based failing column.
+// M = L^ D L^T (L^ unit lower).  band[j*NB+t] = M[j+t][j] -> L^[j+t][j]
+// (1 <= t <= w), band[j*NB] = 1/D[j].  The sweeps then need no division on
+// their critical path.  Returns 0 or a 1-based failing column.
+template <class S>
+__device__ int blk_factor_dispatch(const QPPattern &pt, S &s);
+
 template <class S>
 __device__ int qp_factor(const QPPattern &pt, S &s, double sigma) {
-  const int n = pt.n, w = pt.w, nb = w + 2, tid = threadIdx.x, nt = blockDim.x;
+  constexpr int nb = S::NB;
+  const int n = pt.n, w = pt.w, tid = threadIdx.x, nt = blockDim.x;
   double *band = s.band();
-  for (int e = tid; e < S::BAND_FRONT; e += nt) s.band_store[e] = 0.0;
-  for (int e = tid; e < (n + 4) * nb; e += nt) {
-    const int j = e / nb, t = e - j * nb;
+  for (int e = tid; e < pt.fac_len + 4 * nb; e += nt) {
     double v = 0.0;
-    if (j < n && t <= w) {
-      const int eb = j * (w + 1) + t;  // pattern's (w+1)-stride band index
-      v = (t == 0) ? s.P[j] + sigma : 0.0;
-      for (int k = pt.bandptr[eb]; k < pt.bandptr[eb + 1]; ++k) {
+    if (e < pt.fac_len) {
+      const int d = pt.facdiag[e];
+      v = (d >= 0) ? s.P[d] + sigma : (d == -2 ? 1.0 : 0.0);
+      for (int k = pt.facptr[e]; k < pt.facptr[e + 1]; ++k) {
         const int r = pt.terms[3 * k], a = pt.terms[3 * k + 1], b = pt.terms[3 * k + 2];
         v += s.rho[r] * s.A[a] * s.A[b];
       }
     }
     band[e] = v;
+  }
+  if (pt.mode == 1) {
+    __syncthreads();
+    int f = 0;
+    if (tid < 64) f = blk_factor_dispatch(pt, s);
+    if (tid == 0) s.flag = f;
+    __syncthreads();
+    return s.flag;
   }
   if (tid == 0) s.flag = 0;
   // (t, u) pair of this thread for the trailing update, 1 <= u <= t <= w
@@ -248,7 +264,7 @@ __device__ int qp_factor(const QPPattern &pt, S &s, double sigma) {
       return s.flag;
     }
     const double inv = 1.0 / dj;
-    if (tid == 0) col[0] = inv;  // the pivot lane's own update is discarded
+    if (tid == 0) col[0] = inv;
     if (tid >= 1 && tid <= w && j + tid < n) col[tid] = cw * inv;
     // M[j+t][j+u] -= l_t d_j l_u = (c_t / d_j) c_u   (stored at band[(j+u)*nb + (t-u)])
     if (upd && j + t < n) band[(j + u) * nb + (t - u)] -= (ct * inv) * cu;
@@ -259,124 +275,128 @@ __device__ int qp_factor(const QPPattern &pt, S &s, double sigma) {
 
 // b <- M^-1 b with M = L^ D L^T in the column band (wave 0 only; others idle).
 // Row i of the right-hand side lives in lane i mod 64 ("modular window").  At
-// step j the lane at offset t = (row - j) mod 64 multiplies band slot min(t,
-// w+1) of column j: slot 0 and slot w+1 hold zeros, so lanes outside the band
-// need no mask.  The pivot value is read with readlane and captured with
-// writelane; lanes that pivoted are refilled from the prefetched next window
-// in bulk every 16 steps (a refilled row is first updated >= 48 steps after
-// its lane pivots).  Band multipliers are prefetched 4 steps ahead.  A step is
-// 2 readlane + 1 FMA + 2 writelane + the prefetch.
-__device__ __forceinline__ void writelane_d(double &dst, double v, int l) {
-  // v is wave-uniform (a readlane result), l an SGPR lane index
-  int lo = __double2loint(dst), hi = __double2hiint(dst);
-  // gfx9 constant bus: one SGPR operand per VOP3, so the lane index goes in m0
-  asm("v_writelane_b32 %0, %2, m0\n\tv_writelane_b32 %1, %3, m0"
-      : "+v"(lo), "+v"(hi)
-      : "s"(__double2loint(v)), "s"(__double2hiint(v)), "{m0}"(l));
-  dst = __hiloint2double(hi, lo);
+// forward step j the pivot z_j is read from lane j mod 64 and the lanes of rows
+// j+1..j+w take  win -= L^[row][j] z_j  under an exec mask (a 64-bit rotating
+// SGPR pair), so no lane needs a zero multiplier and every lane's multiplier
+// address is linear in the step: band + row*W + j*W (forward), band + row*W + i
+// (backward).  All 16 loads of a 16-step group issue up front with immediate
+// offsets.  The pivot lane keeps z_j; lanes that pivoted are captured and
+// refilled from the next window in bulk at the end of the group (a refilled
+// row is first updated >= 48 steps after its lane pivots).  A step is 2
+// readlane + 1 masked FMA + 3 scalar ops.
+__device__ __forceinline__ void fma_exec(double &acc, double l, double z, unsigned long long m) {
+  unsigned long long sv;
+  asm volatile(
+      "s_mov_b64 %1, exec\n\t"
+      "s_mov_b64 exec, %4\n\t"
+      "v_fma_f64 %0, -%2, %3, %0\n\t"
+      "s_mov_b64 exec, %1"
+      : "+v"(acc), "=&s"(sv)
+      : "v"(l), "s"(z), "s"(m));
+}
+__device__ __forceinline__ unsigned long long rotl64(unsigned long long x, int k) {
+  k &= 63;
+  return k ? (x << k) | (x >> (64 - k)) : x;
 }
 
 template <class S>
 __device__ void qp_band_solve(const QPPattern &pt, S &s, double *b) {
   if (threadIdx.x >= 64) return;
-  const int n = pt.n, w = pt.w, nb = w + 2, wz = w + 1;
+  constexpr int W = S::NB - 1;
+  const int n = pt.n, w = pt.w;
   const int lane = threadIdx.x;
   const double *band = s.band();
-  // ---- forward: L^ z = b ; stores w = z / D in b.  L^[j+t][j] = band[j*nb + t]
+  const unsigned long long m0 = (1ull << w) - 1;  // w <= 16
+  // ---- forward: L^ z = b ; stores w = z / D in b.  L^[row][j] = band[row*W + j*W + ... ]
+  //      (band[j*NB + (row - j)] = band[j*W + row])
   {
     double win = (lane < n) ? b[lane] : 0.0;
+    int row = lane;
     for (int j0 = 0; j0 < n; j0 += 64) {
       const int rn = j0 + 64 + lane;
       const double nxt = (rn < n) ? b[rn] : 0.0;
       const int jend = min(n, j0 + 64);
       double mine = 0.0;
-#define QP_LDF(jj) band[(jj) * nb + min((lane - (jj)) & 63, wz)]
-#define QP_FSTEP(jj, lv)                          \
-  {                                               \
-    const int pl = (jj) & 63;                     \
-    const double zj = readlane_d(win, pl);        \
-    win = fma(-(lv), zj, win);                    \
-    writelane_d(mine, zj, pl);                    \
-  }
+      unsigned long long msk = rotl64(m0, j0 + 1);  // lanes (j+1 .. j+w) mod 64
       for (int g = j0; g < jend; g += 16) {
-        const int gend = min(jend, g + 16);
-        if (gend - g == 16) {
-          double l0 = QP_LDF(g), l1 = QP_LDF(g + 1), l2 = QP_LDF(g + 2), l3 = QP_LDF(g + 3);
+        const int cnt = min(16, jend - g);
+        const double *p = band + g * W + row;
+        if (cnt == 16) {
+          double lv[16];
 #pragma unroll
-          for (int q = 0; q < 16; q += 4) {
-            const int j = g + q;
-            const double n0 = QP_LDF(j + 4), n1 = QP_LDF(j + 5), n2 = QP_LDF(j + 6), n3 = QP_LDF(j + 7);
-            QP_FSTEP(j, l0);
-            QP_FSTEP(j + 1, l1);
-            QP_FSTEP(j + 2, l2);
-            QP_FSTEP(j + 3, l3);
-            l0 = n0; l1 = n1; l2 = n2; l3 = n3;
+          for (int q = 0; q < 16; ++q) lv[q] = p[q * W];
+#pragma unroll
+          for (int q = 0; q < 16; ++q) {
+            const double zj = readlane_d(win, (g + q) & 63);
+            fma_exec(win, lv[q], zj, msk);
+            msk = (msk << 1) | (msk >> 63);
           }
         } else {
-          for (int j = g; j < gend; ++j) {
-            const double l0 = QP_LDF(j);
-            QP_FSTEP(j, l0);
+          for (int q = 0; q < cnt; ++q) {
+            const double lq = p[q * W];
+            const double zj = readlane_d(win, (g + q) & 63);
+            fma_exec(win, lq, zj, msk);
+            msk = (msk << 1) | (msk >> 63);
           }
         }
-        // lanes that pivoted in [g, gend) take their row of the next window
-        win = ((unsigned)(lane - (g - j0)) < (unsigned)(gend - g)) ? nxt : win;
+        // lanes that pivoted in [g, g+cnt): capture z, take the next window's row
+        const bool piv = (unsigned)(lane - (g - j0)) < (unsigned)cnt;
+        mine = piv ? win : mine;
+        win = piv ? nxt : win;
+        row = piv ? row + 64 : row;
       }
-#undef QP_FSTEP
-#undef QP_LDF
-      if (j0 + lane < jend) b[j0 + lane] = mine * band[(j0 + lane) * nb];
+      if (j0 + lane < jend) b[j0 + lane] = mine * band[(j0 + lane) * S::NB];
     }
   }
   __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-  // ---- backward: L^T x = w.  lane's row r = i - t;  L^[i][r] = band[r*nb + t]
-  //      with t clamped to w+1: band[i*nb - (nb-1)*min(t, w+1)]
+  // ---- backward: L^T x = w.  L^[i][row] = band[row*NB + (i - row)] = band[row*W + i]
   {
     // lanes past the (partial) top window start on their row of the block below,
     // as if they had already pivoted in the top window
     const int top = ((n - 1) >> 6) << 6;
-    double win = (top + lane < n) ? b[top + lane] : ((top - 64 + lane >= 0) ? b[top - 64 + lane] : 0.0);
+    int row = (top + lane < n) ? top + lane : top - 64 + lane;
+    double win = (row >= 0) ? b[row] : 0.0;
     for (int i0 = top; i0 >= 0; i0 -= 64) {
       const int rp = i0 - 64 + lane;
       const double nxt = (rp >= 0) ? b[rp] : 0.0;
       const int ihi = min(n, i0 + 64) - 1;
       double mine = 0.0;
-#define QP_LDB(ii) band[(ii) * nb - (nb - 1) * min(((ii) - lane) & 63, wz)]
-#define QP_BSTEP(ii, lv)                          \
-  {                                               \
-    const int pl = (ii) & 63;                     \
-    const double xi = readlane_d(win, pl);        \
-    win = fma(-(lv), xi, win);                    \
-    writelane_d(mine, xi, pl);                    \
-  }
+      unsigned long long msk = rotl64(m0, ihi - w);  // lanes (i-w .. i-1) mod 64
       for (int g = ihi; g >= i0; g -= 16) {
-        const int gend = max(i0 - 1, g - 16);  // exclusive
-        if (g - gend == 16) {
-          double l0 = QP_LDB(g), l1 = QP_LDB(g - 1), l2 = QP_LDB(g - 2), l3 = QP_LDB(g - 3);
+        const int cnt = min(16, g - i0 + 1);
+        const double *p = band + max(row, 0) * W + g;  // step i = g - q at p[-q]
+        if (cnt == 16) {
+          double lv[16];
+          const double *pb = p - 15;
 #pragma unroll
-          for (int q = 0; q < 16; q += 4) {
-            const int i = g - q;
-            const double n0 = QP_LDB(i - 4), n1 = QP_LDB(i - 5), n2 = QP_LDB(i - 6), n3 = QP_LDB(i - 7);
-            QP_BSTEP(i, l0);
-            QP_BSTEP(i - 1, l1);
-            QP_BSTEP(i - 2, l2);
-            QP_BSTEP(i - 3, l3);
-            l0 = n0; l1 = n1; l2 = n2; l3 = n3;
+          for (int q = 0; q < 16; ++q) lv[q] = pb[15 - q];
+#pragma unroll
+          for (int q = 0; q < 16; ++q) {
+            const double xi = readlane_d(win, (g - q) & 63);
+            fma_exec(win, lv[q], xi, msk);
+            msk = (msk >> 1) | (msk << 63);
           }
         } else {
-          for (int i = g; i > gend; --i) {
-            const double l0 = QP_LDB(i);
-            QP_BSTEP(i, l0);
+          for (int q = 0; q < cnt; ++q) {
+            const double lq = p[-q];
+            const double xi = readlane_d(win, (g - q) & 63);
+            fma_exec(win, lq, xi, msk);
+            msk = (msk >> 1) | (msk << 63);
           }
         }
-        // lanes that pivoted in (gend, g] take their row of the window below
-        win = ((unsigned)(lane - (gend + 1 - i0)) < (unsigned)(g - gend)) ? nxt : win;
+        // lanes that pivoted in (g-cnt, g]: capture x, take the row of the window below
+        const bool piv = (unsigned)(lane - (g - cnt + 1 - i0)) < (unsigned)cnt;
+        mine = piv ? win : mine;
+        win = piv ? nxt : win;
+        row = piv ? row - 64 : row;
       }
-#undef QP_BSTEP
-#undef QP_LDB
       if (i0 + lane <= ihi) b[i0 + lane] = mine;
     }
   }
   __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
 }
+
+#include "qp_block.h"
 
 // residuals (auxil.c update_info): tmpm <- A x, aux <- P x, tmpn <- A' y.
 // o: 0 pri (unscaled)  1 |z/E|  2 |Ax/E|  3 dua*c  4 |q/D|  5 |A'y/D|  6 |Px/D|
@@ -514,9 +534,12 @@ __device__ double qp_rho_estimate(const QPPattern &pt, S &s) {
 struct QPStamps {
   unsigned long long *out = nullptr;
   unsigned long long acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  unsigned long long last = 0;
+  unsigned long long last = 0, first = 0, rt0 = 0;
   __device__ void start() {
-    if (out && threadIdx.x == 0) last = __builtin_amdgcn_s_memtime();
+    if (out && threadIdx.x == 0) {
+      last = first = __builtin_amdgcn_s_memtime();
+      rt0 = __builtin_amdgcn_s_memrealtime();
+    }
   }
   __device__ void mark(int k) {
     if (out && threadIdx.x == 0) {
@@ -526,8 +549,11 @@ struct QPStamps {
     }
   }
   __device__ void flush() {
-    if (out && threadIdx.x == 0)
+    if (out && threadIdx.x == 0) {
       for (int k = 0; k < 8; ++k) out[k] += acc[k];
+      out[8] += __builtin_amdgcn_s_memrealtime() - rt0;  // 100 MHz constant clock
+      out[9] += last - first;                           // shader clock
+    }
   }
 };
 
@@ -613,7 +639,8 @@ __device__ QPResult qp_solve(const QPPattern &pt, S &s, const QPSettingsDev &st,
     }
     __syncthreads();
     T.mark(3);
-    qp_band_solve(pt, s, s.rhs);  // x~
+    if (pt.mode == 1) blk_solve_dispatch(pt, s, s.rhs);  // x~
+    else qp_band_solve(pt, s, s.rhs);
     __syncthreads();
     T.mark(4);
     if (tid < n) {

@@ -172,10 +172,15 @@ int gpmpc_fleet_step_phases(gpmpc_fleet *f, int phase_mask);
 #define GPMPC_REC_LEN 16
 int gpmpc_fleet_read(gpmpc_fleet *f, double *records, double *x /* batch x 7, may be NULL */);
 /* diagnostic: accumulate s_memtime cycles of landing 0's control kernel per
- * phase into dev_u64x8 (8 x uint64 device buffer; NULL disables):
+ * phase into dev_u64x10 (10 x uint64 device buffer; NULL disables):
  * 0 assembly, 1 scaling, 2 factor, 3 A' rhs, 4 band sweeps, 5 fused z/y update,
- * 6 checks + adaptive rho, 7 tail (plant step, records) */
-int gpmpc_fleet_set_stamps(gpmpc_fleet *f, void *dev_u64x8);
+ * 6 checks + adaptive rho, 7 tail (plant step, records); 8 s_memrealtime
+ * ticks (100 MHz) and 9 shader-clock ticks over the same solves */
+int gpmpc_fleet_set_stamps(gpmpc_fleet *f, void *dev_u64x10);
+/* diagnostic: per-landing control-kernel trace into dev_u64xbx4 (batch x 4
+ * uint64 device buffer; NULL disables): start and end s_memrealtime (100 MHz),
+ * HW_ID and XCC_ID of the landing's first wave */
+int gpmpc_fleet_set_trace(gpmpc_fleet *f, void *dev_u64xbx4);
 /* device pointer of the record array (for collectives) */
 double *gpmpc_fleet_records_dev(gpmpc_fleet *f);
 int gpmpc_fleet_destroy(gpmpc_fleet *f);
