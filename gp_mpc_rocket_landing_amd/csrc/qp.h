@@ -4,9 +4,10 @@
 #include "qp_device.h"
 
 // LDS caps of the single compiled instantiation: 3-DoF MPC up to N = 20
-// (n = 10N + 7, m = 17N + 14, nnz = 36N + 14), sized so that the fleet's
-// control kernel stays under 80 KB and two workgroups share a CU
-#define QP_NMAX 208
+// (n = 10N + 7, m = 17N + 14, nnz = 36N + 14; NMAX also holds n rounded up to
+// whole stage blocks), sized so that the fleet's control kernel stays under
+// 80 KB and two workgroups share a CU
+#define QP_NMAX 216
 #define QP_MMAX 360
 #define QP_NNZMAX 736
 #define QP_W 16
@@ -19,7 +20,8 @@ struct QPPatternHost {
   int mode = 0, fac_len = 0, nblk = 0;
   bool fits() const {
     return n <= QP_NMAX && m <= QP_MMAX && nnz <= QP_NNZMAX && maxrow <= QP_RMAX &&
-           maxcol <= QP_CMAX && (mode == 1 || (w <= QP_W && fac_len <= QP_FAC_CAP));
+           maxcol <= QP_CMAX &&
+           (mode == 1 ? nblk * QP_BLK_SZ <= QP_NMAX : (w <= QP_W && fac_len <= QP_FAC_CAP));
   }
   DevBuf buf;
   QPPattern dev{};

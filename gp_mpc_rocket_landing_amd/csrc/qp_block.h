@@ -80,7 +80,7 @@ __device__ __forceinline__ double dot_bcv(double src, const double *mul, std::in
   return a0 + a1;
 }
 #ifndef QP_DOT_ASM
-#define QP_DOT_ASM 0
+#define QP_DOT_ASM 1
 #endif
 template <int K>
 __device__ __forceinline__ double dot_bc(double src, const double *mul) {
@@ -159,79 +159,134 @@ __device__ int blk_factor(const QPPattern &pt, S &s) {
   return 0;
 }
 
-// b <- M^-1 b.  Wave 0 only.
+// b <- M^-1 b.  Wave 0 only.  The block loops are unrolled by two with
+// ping-pong operand registers, so the next block's operands load under the
+// current block's FMA chain without register copies.  b is zero-padded to
+// nblk*SZ entries (qp_solve), so lanes read it without bounds selects; lanes
+// rr >= SZ (never a broadcast source) read clamped addresses and only the
+// stores are masked.  Per-lane pointers advance by constants; operands sit at
+// immediate offsets.
 template <int SZ, int CM, class S>
 __device__ void blk_solve(const QPPattern &pt, S &s, double *b) {
   if (threadIdx.x >= 64) return;
   constexpr int BS = SZ * SZ + SZ * CM;
   const int lane = threadIdx.x, rr = lane & 15, row = lane >> 4;
-  const bool wr = lane < 16;
   const int rs = rr < SZ ? rr : SZ - 1, rc = rr < CM ? rr : CM - 1;
-  const int n = pt.n, nblk = pt.nblk;
+  const bool wr = rr < SZ;
+  const int nblk = pt.nblk;
   const double *F = s.band();
+  if (nblk == 1) {
+    double sv[SZ];
+#pragma unroll
+    for (int j = 0; j < SZ; ++j) sv[j] = F[j * SZ + rs];
+    const double uv = dot_bc<SZ>(b[rs], sv);
+    if (wr) b[rr] = uv;
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    return;
+  }
   // ---- forward: y_{k+1} = b_{k+1} - G_k y_k on the first CM rows of block k+1
   {
-    double y = (rr < SZ && rr < n) ? b[rr] : 0.0;
-    double g[SZ];
+    double *pb = b + rs;                          // block k of b
+    const double *pg = F + SZ * SZ + rc;          // G_k row rc
+    double y = pb[0];
+    double gA[SZ], gB[SZ];
 #pragma unroll
-    for (int j = 0; j < SZ; ++j) g[j] = F[SZ * SZ + j * CM + rc];
-    for (int k = 0; k + 1 < nblk; ++k) {
-      const int s1 = (k + 1) * SZ;
-      const double bn = (rr < SZ && s1 + rr < n) ? b[s1 + rr] : 0.0;
-      double gn[SZ];
-      if (k + 2 < nblk) {
-        const double *Gn = F + (k + 1) * BS + SZ * SZ;
+    for (int j = 0; j < SZ; ++j) gA[j] = pg[j * CM];
+    for (int k = 0;;) {
+      {
+        const double bn = pb[SZ];
 #pragma unroll
-        for (int j = 0; j < SZ; ++j) gn[j] = Gn[j * CM + rc];
+        for (int j = 0; j < SZ; ++j) gB[j] = pg[BS + j * CM];  // G_{k+1} (past the end: unused)
+        const double acc = dot_bc<SZ>(y, gA);
+        if (wr) pb[0] = y;
+        y = (rr < CM) ? bn - acc : bn;
+        pb += SZ;
+        pg += BS;
+        if (++k >= nblk - 1) break;
       }
-      const double acc = dot_bc<SZ>(y, g);
-      if (wr && rr < SZ) b[k * SZ + rr] = y;
-      y = (rr < CM) ? bn - acc : bn;
+      {
+        const double bn = pb[SZ];
 #pragma unroll
-      for (int j = 0; j < SZ; ++j) g[j] = gn[j];
+        for (int j = 0; j < SZ; ++j) gA[j] = pg[BS + j * CM];
+        const double acc = dot_bc<SZ>(y, gB);
+        if (wr) pb[0] = y;
+        y = (rr < CM) ? bn - acc : bn;
+        pb += SZ;
+        pg += BS;
+        if (++k >= nblk - 1) break;
+      }
     }
-    const int sl = (nblk - 1) * SZ;
-    if (wr && rr < SZ && sl + rr < n) b[sl + rr] = y;
+    if (wr) pb[0] = y;
   }
   __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
   // ---- diagonal blocks, four at a time (one per DPP row): u_k = S_k^-1 y_k
-  for (int k = row; k < nblk; k += 4) {
-    const int s0 = k * SZ;
-    const bool live = rr < SZ && s0 + rr < n;
-    const double yv = live ? b[s0 + rr] : 0.0;
-    double sv[SZ];
+  {
+    const int nr = (nblk + 3) >> 2;
+    double *pb = b + row * SZ + rs;
+    const double *ps = F + row * BS + rs;
+    double sA[SZ], sB[SZ];
 #pragma unroll
-    for (int j = 0; j < SZ; ++j) sv[j] = F[k * BS + j * SZ + rs];
-    const double uv = dot_bc<SZ>(yv, sv);
-    if (live) b[s0 + rr] = uv;
+    for (int j = 0; j < SZ; ++j) sA[j] = ps[j * SZ];
+    double yA = pb[0];
+    for (int t = 0;;) {
+      {
+#pragma unroll
+        for (int j = 0; j < SZ; ++j) sB[j] = ps[4 * BS + j * SZ];  // next round (past the end: unused)
+        const double yB = pb[4 * SZ];
+        const double uv = dot_bc<SZ>(yA, sA);
+        if (wr && t * 4 + row < nblk) pb[0] = uv;
+        yA = yB;
+        pb += 4 * SZ;
+        ps += 4 * BS;
+        if (++t >= nr) break;
+      }
+      {
+#pragma unroll
+        for (int j = 0; j < SZ; ++j) sA[j] = ps[4 * BS + j * SZ];
+        const double yB = pb[4 * SZ];
+        const double uv = dot_bc<SZ>(yA, sB);
+        if (wr && t * 4 + row < nblk) pb[0] = uv;
+        yA = yB;
+        pb += 4 * SZ;
+        ps += 4 * BS;
+        if (++t >= nr) break;
+      }
+    }
   }
   __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
   // ---- backward: x_k = u_k - G_k^T x_{k+1}
   {
-    const int sl = (nblk - 1) * SZ;
-    double x = (rr < SZ && sl + rr < n) ? b[sl + rr] : 0.0;
-    double gt[CM];
-    if (nblk >= 2) {
-      const double *G = F + (nblk - 2) * BS + SZ * SZ;
+    double *pb = b + (nblk - 1) * SZ + rs;        // block k+1 of b
+    const double *pg = F + (nblk - 2) * BS + SZ * SZ + rs * CM;  // G_k column rs
+    double x = pb[0];
+    double gA[CM], gB[CM];
 #pragma unroll
-      for (int i = 0; i < CM; ++i) gt[i] = G[rs * CM + i];
-    }
-    for (int k = nblk - 2; k >= 0; --k) {
-      const double un = (rr < SZ) ? b[k * SZ + rr] : 0.0;
-      double gtn[CM];
-      if (k > 0) {
-        const double *G = F + (k - 1) * BS + SZ * SZ;
+    for (int i = 0; i < CM; ++i) gA[i] = pg[i];
+    for (int k = nblk - 2;;) {
+      {
+        const double un = pb[-SZ];
 #pragma unroll
-        for (int i = 0; i < CM; ++i) gtn[i] = G[rs * CM + i];
+        for (int i = 0; i < CM; ++i) gB[i] = pg[i - BS];  // G_{k-1} (before the start: unused)
+        const double acc = dot_bc<CM>(x, gA);
+        if (wr) pb[0] = x;
+        x = un - acc;
+        pb -= SZ;
+        pg -= BS;
+        if (--k < 0) break;
       }
-      const double acc = dot_bc<CM>(x, gt);
-      const int s1 = (k + 1) * SZ;
-      if (wr && rr < SZ && s1 + rr < n) b[s1 + rr] = x;
-      x = un - acc;
+      {
+        const double un = pb[-SZ];
 #pragma unroll
-      for (int i = 0; i < CM; ++i) gt[i] = gtn[i];
+        for (int i = 0; i < CM; ++i) gA[i] = pg[i - BS];
+        const double acc = dot_bc<CM>(x, gB);
+        if (wr) pb[0] = x;
+        x = un - acc;
+        pb -= SZ;
+        pg -= BS;
+        if (--k < 0) break;
+      }
     }
-    if (wr && rr < SZ && rr < n) b[rr] = x;
+    if (wr) pb[0] = x;
   }
   __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
 }

@@ -66,6 +66,7 @@ struct QPSmem {
   // 64 doubles of tail padding for the sweeps' masked-lane loads
   double band_store[NMAX * (W + 1) + 4 * (W + 1) + 64];
   double red[4][8];
+  double zslot, sink;  // block solve: a 0.0 source and a write sink for idle lanes
   double c, rho_s;
   int flag;
 };
@@ -233,6 +234,7 @@ __device__ int qp_factor(const QPPattern &pt, S &s, double sigma) {
     band[e] = v;
   }
   if (pt.mode == 1) {
+    if (tid == 0) s.zslot = 0.0;
     __syncthreads();
     int f = 0;
     if (tid < 64) f = blk_factor_dispatch(pt, s);
@@ -577,6 +579,8 @@ __device__ QPResult qp_solve(const QPPattern &pt, S &s, const QPSettingsDev &st,
     s.l[r] = fmax(s.l[r], -QP_OSQP_INFTY);
     s.u[r] = fmin(s.u[r], QP_OSQP_INFTY);
   }
+  // the block solve reads the right-hand side in whole blocks: zero the tail
+  for (int j = n + tid; j < (int)(sizeof(s.rhs) / sizeof(double)); j += nt) s.rhs[j] = 0.0;
   __syncthreads();
   if (st.scaling) qp_scale(pt, s, st.scaling);
   else {
