@@ -72,8 +72,9 @@ def cpu_baseline(seconds, n_train=1000, horizon=20):
                                             filter_small=False)
             r = qp.solve(P0.diagonal(), q, A, l, u, qp_oracle.to_vector(Xw, Uw))
             Xo, Uo = qp_oracle.from_vector(r["x"], horizon)
+            dr = qp_oracle.drag_residual(x)  # residual at the pre-step state
             x = qp_oracle.plant_step(x, Uo[0], 0.1)
-            x[4:7] += qp_oracle.drag_residual(x) * 0.1
+            x[4:7] += dr * 0.1
             Xw = np.vstack([Xo[1:], Xo[-1:]]); Uw = np.vstack([Uo[1:], Uo[-1:]])
             steps += 1
         el = time.perf_counter() - t0

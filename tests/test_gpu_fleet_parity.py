@@ -1,0 +1,78 @@
+"""Closed-loop parity of the device-resident fleet against the CPU restatement.
+
+Each control step of a landing: GP posterior mean at the N
+horizon points of the shifted linearisation trajectory (exact_gp.py:213-268 via
+gp_oracle), RTI QP assembly with the GP mean on the velocity rows
+(osqp_rti.py:203-372 with the gp_mpc.py:309-314/411 sign, qp_oracle), the
+OSQP-0.6 ADMM (C restatement, persistent rho and scaled y across steps), the
+plant step with the drag residual, and the incremental target
+(monte_carlo.py:497-500).  The fleet must reproduce the oracle's state
+trajectory within the tolerance spec and its ADMM iteration counts and
+statuses exactly.
+"""
+import numpy as np
+import pytest
+
+from conftest import close
+
+pytestmark = pytest.mark.gpu
+
+B, STEPS, N = 16, 40, 20
+
+
+def _oracle_landing(st, x0, steps):
+    from oracle import admm_ref, gp_oracle, mc_oracle, qp_oracle
+
+    x = x0.copy()
+    tgt = mc_oracle.incremental_target(x)
+    Xw, Uw = qp_oracle.initial_guess(x, tgt, N)
+    P0, _ = qp_oracle.cost(N, np.tile(tgt, (N + 1, 1)))
+    qp = admm_ref.RefQP(qp_oracle.N_X * (N + 1) + qp_oracle.n_vars(N))
+    out = []
+    for _ in range(steps):
+        tgt = mc_oracle.incremental_target(x)
+        mean, _var = gp_oracle.exact_predict(st, gp_oracle.features_3dof(Xw[:-1], Uw))
+        _, q = qp_oracle.cost(N, np.tile(tgt, (N + 1, 1)))
+        A, l, u = qp_oracle.constraints(Xw, Uw, x, 0.1, gp_dv=mean, sign=-1.0, filter_small=False)
+        r = qp.solve(P0.diagonal(), q, A, l, u, qp_oracle.to_vector(Xw, Uw))
+        Xo, Uo = qp_oracle.from_vector(r["x"], N)
+        dr = qp_oracle.drag_residual(x)  # residual at the pre-step state (explicit Euler)
+        x = qp_oracle.plant_step(x, Uo[0], 0.1)
+        x[4:7] += dr * 0.1
+        Xw = np.vstack([Xo[1:], Xo[-1:]])
+        Uw = np.vstack([Uo[1:], Uo[-1:]])
+        out.append((x.copy(), r["iter"], r["status"]))
+    return out
+
+
+def test_fleet_closed_loop_matches_oracle(gpu_ctx):
+    from gp_mpc_rocket_landing_amd.data import synthetic_training_data
+    from gp_mpc_rocket_landing_amd.fleet import (REC_ADMM_ITERS, REC_LAST_STATUS, REC_OUTCOME,
+                                                 Fleet, fit_gp, initial_conditions)
+    from oracle import gp_oracle
+
+    X, U, D = synthetic_training_data(1000, seed=0)
+    st = gp_oracle.exact_fit(gp_oracle.features_3dof(X, U), D)
+    x0 = initial_conditions(B)
+    ref = [_oracle_landing(st, x0[b], STEPS) for b in range(B)]
+
+    gp = fit_gp(gpu_ctx, n_train=1000)
+    fl = Fleet(gpu_ctx, gp, B, horizon=N)
+    try:
+        fl.reset(x0)
+        prev_iters = np.zeros(B)
+        for k in range(STEPS):
+            fl.step(1)
+            rec, xs = fl.read()
+            assert np.all(rec[:, REC_OUTCOME] == 0), "no landing terminates this early"
+            iters = rec[:, REC_ADMM_ITERS] - prev_iters
+            prev_iters = rec[:, REC_ADMM_ITERS].copy()
+            for b in range(B):
+                xr, itr, str_ = ref[b][k]
+                assert int(iters[b]) == itr, (k, b, int(iters[b]), itr)
+                assert int(rec[b, REC_LAST_STATUS]) == str_, (k, b)
+                # state tolerance: 1e-6 relative with a unit floor (SURVEY 8c spec, s = 1)
+                ok, worst = close(xs[b], xr, 1.0, rtol=1e-6)
+                assert ok, (k, b, worst)
+    finally:
+        fl.close()
