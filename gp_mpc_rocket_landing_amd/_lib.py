@@ -314,3 +314,43 @@ def fleet_default_config(**kw):
     for k, v in kw.items():
         setattr(c, k, v)
     return c
+
+
+class QPWorkspace:
+    """OSQP-workspace equivalent over gpmpc_qp_solve_batched: a fixed CSR
+    pattern of A shared by ``batch`` problems, diagonal P, and the state OSQP
+    keeps between solves (rho, scaled y).  Mirrors osqp.OSQP().setup/update/
+    warm_start/solve as osqp_rti.py:454-567 drives it."""
+
+    def __init__(self, ctx, n, m, rowptr, colidx, batch=1, settings=None):
+        self.ctx = ctx; self.n = int(n); self.m = int(m); self.batch = int(batch)
+        self.rowptr = np.ascontiguousarray(rowptr, np.int32)
+        self.colidx = np.ascontiguousarray(colidx, np.int32)
+        self.nnz = int(self.rowptr[-1])
+        self.settings = settings if settings is not None else qp_default_settings()
+        self.reset()
+
+    def reset(self):
+        """Fresh workspace: rho back to settings.rho, y = 0 (osqp.OSQP().setup)."""
+        self.rho = np.full(self.batch, float(self.settings.rho))
+        self.y_scaled = np.zeros((self.batch, self.m))
+
+    def solve(self, Aval, Pdiag, q, l, u, x_ws=None):
+        B, n, m = self.batch, self.n, self.m
+        Av = f64(np.reshape(Aval, (B, self.nnz))); Pd = f64(np.reshape(Pdiag, (B, n)))
+        qv = f64(np.reshape(q, (B, n))); lv = f64(np.reshape(l, (B, m))); uv = f64(np.reshape(u, (B, m)))
+        xw = None if x_ws is None else f64(np.reshape(x_ws, (B, n)))
+        x = np.empty((B, n)); y = np.empty((B, m)); obj = np.empty(B)
+        it = np.zeros(B, np.int32); st = np.zeros(B, np.int32)
+        rc = _L.gpmpc_qp_solve_batched(self.ctx.h, B, n, m, self.nnz, _i(self.rowptr), _i(self.colidx),
+                                       _d(Av), _d(Pd), _d(qv), _d(lv), _d(uv), ctypes.byref(self.settings),
+                                       None if xw is None else _d(xw), _d(self.rho), _d(self.y_scaled),
+                                       _d(x), _d(y), _i(it), _i(st), _d(obj))
+        _chk(rc, "qp_solve_batched")
+        return dict(x=x, y=y, iter=it, status=st, obj_val=obj, rho=self.rho.copy())
+
+
+QP_STATUS_TEXT = {1: "solved", 2: "solved_inaccurate", -2: "maximum iterations reached",
+                  -3: "primal infeasible", 3: "primal infeasible inaccurate",
+                  -4: "dual infeasible", 4: "dual infeasible inaccurate", -7: "problem non convex",
+                  -10: "unsolved", -100: "kkt factorisation failed"}

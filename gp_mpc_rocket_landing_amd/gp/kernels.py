@@ -1,0 +1,277 @@
+"""Kernel surfaces of reference src/gp/kernels.py; Gram matrices on the GPU.
+
+Every Gram matrix of SE-ARD / isotropic SE / Matern-3/2 / Matern-5/2 runs
+through gpmpc_gram (csrc/gram.hip: expansion-form scaled distance, clamped at
+0, kernels.py:205-236).  Hyperparameters are exposed in log space exactly as
+get_params/set_params/n_params/param_names define them (kernels.py:320-371).
+Sum/product kernels combine device Grams elementwise; WhiteNoise is diagonal.
+Gradient methods (hyperparameter fitting) are not part of this
+path.
+"""
+from __future__ import annotations
+
+from abc import ABC, abstractmethod
+from typing import List, Optional
+
+import numpy as np
+
+from .. import _lib
+
+
+def _ctx():
+    return _lib.default_context()
+
+
+class Kernel(ABC):
+    """kernels.py:33-127."""
+
+    @abstractmethod
+    def __call__(self, X1, X2=None) -> np.ndarray: ...
+
+    @abstractmethod
+    def diagonal(self, X) -> np.ndarray: ...
+
+    @property
+    @abstractmethod
+    def n_params(self) -> int: ...
+
+    @property
+    @abstractmethod
+    def param_names(self) -> List[str]: ...
+
+    @abstractmethod
+    def get_params(self) -> np.ndarray: ...
+
+    @abstractmethod
+    def set_params(self, params) -> None: ...
+
+    # device-gram description: (kind, lengthscales, sigma2) or None
+    def _device_spec(self):
+        return None
+
+    def __add__(self, other):
+        return SumKernel(self, other)
+
+    def __mul__(self, other):
+        return ProductKernel(self, other)
+
+
+class _StationaryARD(Kernel):
+    KIND = _lib.SE_ARD
+
+    def __init__(self, input_dim: int, signal_variance: float = 1.0,
+                 lengthscales: Optional[np.ndarray] = None,
+                 learn_signal_variance: bool = True, learn_lengthscales: bool = True):
+        self.input_dim = int(input_dim)
+        self._signal_variance = float(signal_variance)
+        if lengthscales is None:
+            self._lengthscales = np.ones(self.input_dim)
+        else:
+            self._lengthscales = np.asarray(lengthscales, float).flatten()
+            assert len(self._lengthscales) == self.input_dim
+        self.learn_signal_variance = learn_signal_variance
+        self.learn_lengthscales = learn_lengthscales
+
+    @property
+    def signal_variance(self) -> float:
+        return self._signal_variance
+
+    @signal_variance.setter
+    def signal_variance(self, value: float) -> None:
+        assert value > 0, "Signal variance must be positive"
+        self._signal_variance = float(value)
+
+    @property
+    def lengthscales(self) -> np.ndarray:
+        return self._lengthscales
+
+    @lengthscales.setter
+    def lengthscales(self, value) -> None:
+        value = np.asarray(value, float).flatten()
+        assert len(value) == self.input_dim
+        assert np.all(value > 0), "Lengthscales must be positive"
+        self._lengthscales = value
+
+    def _device_spec(self):
+        return self.KIND, self._lengthscales, self._signal_variance
+
+    def __call__(self, X1, X2=None) -> np.ndarray:
+        return _lib.gram(_ctx(), self.KIND, X1, X2, self._lengthscales, self._signal_variance)
+
+    def diagonal(self, X) -> np.ndarray:
+        return np.full(np.atleast_2d(X).shape[0], self._signal_variance)
+
+    @property
+    def n_params(self) -> int:
+        return int(self.learn_signal_variance) + (self.input_dim if self.learn_lengthscales else 0)
+
+    @property
+    def param_names(self) -> List[str]:
+        names = ["log_signal_variance"] if self.learn_signal_variance else []
+        if self.learn_lengthscales:
+            names += [f"log_lengthscale_{i}" for i in range(self.input_dim)]
+        return names
+
+    def get_params(self) -> np.ndarray:
+        p = [np.log(self._signal_variance)] if self.learn_signal_variance else []
+        if self.learn_lengthscales:
+            p.extend(np.log(self._lengthscales))
+        return np.array(p)
+
+    def set_params(self, params) -> None:
+        params = np.asarray(params, float).flatten()
+        i = 0
+        if self.learn_signal_variance:
+            self._signal_variance = float(np.exp(params[i])); i += 1
+        if self.learn_lengthscales:
+            self._lengthscales = np.exp(params[i:i + self.input_dim])
+
+    def __repr__(self) -> str:
+        return f"{type(self).__name__}(input_dim={self.input_dim}, σ²={self._signal_variance:.4g})"
+
+
+class SquaredExponentialARD(_StationaryARD):
+    """kernels.py:130-384: sigma2 exp(-r^2/2), r^2 = |x/l - x'/l|^2."""
+    KIND = _lib.SE_ARD
+
+
+class Matern32(_StationaryARD):
+    """kernels.py:482-576: sigma2 (1 + sqrt3 r) exp(-sqrt3 r)."""
+    KIND = _lib.MATERN32
+
+    def __init__(self, input_dim: int, signal_variance: float = 1.0, lengthscales=None):
+        super().__init__(input_dim, signal_variance, lengthscales)
+
+
+class Matern52(_StationaryARD):
+    """kernels.py:579-673: sigma2 (1 + sqrt5 r + 5 r^2/3) exp(-sqrt5 r)."""
+    KIND = _lib.MATERN52
+
+    def __init__(self, input_dim: int, signal_variance: float = 1.0, lengthscales=None):
+        super().__init__(input_dim, signal_variance, lengthscales)
+
+
+class SquaredExponential(Kernel):
+    """kernels.py:392-479: isotropic SE (one lengthscale)."""
+
+    def __init__(self, signal_variance: float = 1.0, lengthscale: float = 1.0):
+        self._signal_variance = float(signal_variance)
+        self._lengthscale = float(lengthscale)
+
+    @property
+    def signal_variance(self) -> float:
+        return self._signal_variance
+
+    @property
+    def lengthscale(self) -> float:
+        return self._lengthscale
+
+    def _device_spec(self):
+        return _lib.SE_ISO, np.array([self._lengthscale]), self._signal_variance
+
+    def __call__(self, X1, X2=None) -> np.ndarray:
+        return _lib.gram(_ctx(), _lib.SE_ISO, X1, X2, np.array([self._lengthscale]), self._signal_variance)
+
+    def diagonal(self, X) -> np.ndarray:
+        return np.full(np.atleast_2d(X).shape[0], self._signal_variance)
+
+    @property
+    def n_params(self) -> int:
+        return 2
+
+    @property
+    def param_names(self) -> List[str]:
+        return ["log_signal_variance", "log_lengthscale"]
+
+    def get_params(self) -> np.ndarray:
+        return np.log([self._signal_variance, self._lengthscale])
+
+    def set_params(self, params) -> None:
+        self._signal_variance, self._lengthscale = (float(v) for v in np.exp(np.asarray(params)[:2]))
+
+
+class SumKernel(Kernel):
+    """kernels.py:676-726."""
+
+    def __init__(self, k1: Kernel, k2: Kernel):
+        self.k1, self.k2 = k1, k2
+
+    def __call__(self, X1, X2=None):
+        return self.k1(X1, X2) + self.k2(X1, X2)
+
+    def diagonal(self, X):
+        return self.k1.diagonal(X) + self.k2.diagonal(X)
+
+    @property
+    def n_params(self):
+        return self.k1.n_params + self.k2.n_params
+
+    @property
+    def param_names(self):
+        return [f"k1_{n}" for n in self.k1.param_names] + [f"k2_{n}" for n in self.k2.param_names]
+
+    def get_params(self):
+        return np.concatenate([self.k1.get_params(), self.k2.get_params()])
+
+    def set_params(self, params):
+        params = np.asarray(params)
+        self.k1.set_params(params[:self.k1.n_params])
+        self.k2.set_params(params[self.k1.n_params:])
+
+
+class ProductKernel(SumKernel):
+    """kernels.py:729-782."""
+
+    def __call__(self, X1, X2=None):
+        return self.k1(X1, X2) * self.k2(X1, X2)
+
+    def diagonal(self, X):
+        return self.k1.diagonal(X) * self.k2.diagonal(X)
+
+
+class WhiteNoise(Kernel):
+    """kernels.py:790-844: sigma2 I on the training set, zero cross-covariance."""
+
+    def __init__(self, noise_variance: float = 1e-6):
+        self._noise_variance = float(noise_variance)
+
+    @property
+    def noise_variance(self) -> float:
+        return self._noise_variance
+
+    def __call__(self, X1, X2=None):
+        X1 = np.atleast_2d(X1)
+        if X2 is None:
+            return self._noise_variance * np.eye(X1.shape[0])
+        return np.zeros((X1.shape[0], np.atleast_2d(X2).shape[0]))
+
+    def diagonal(self, X):
+        return np.full(np.atleast_2d(X).shape[0], self._noise_variance)
+
+    @property
+    def n_params(self):
+        return 1
+
+    @property
+    def param_names(self):
+        return ["log_noise_variance"]
+
+    def get_params(self):
+        return np.array([np.log(self._noise_variance)])
+
+    def set_params(self, params):
+        self._noise_variance = float(np.exp(np.asarray(params)[0]))
+
+
+# aliases (kernels.py:383-384)
+RBF = SquaredExponentialARD
+SE_ARD = SquaredExponentialARD
+
+
+def create_matern_kernel(input_dim: int, nu: float = 2.5, **kw) -> Kernel:
+    """kernels.py:875-898."""
+    if nu == 1.5:
+        return Matern32(input_dim, **kw)
+    if nu == 2.5:
+        return Matern52(input_dim, **kw)
+    raise ValueError(f"Unsupported nu={nu}. Use 1.5 or 2.5")

@@ -1,0 +1,90 @@
+"""Host-side logic of the product package (no GPU calls): QP assembly, plant,
+kernel parameter API and the surface defaults, against the CPU restatement."""
+import numpy as np
+import pytest
+
+from oracle import qp_oracle
+
+
+@pytest.mark.parametrize("sign", [1.0, -1.0])
+@pytest.mark.parametrize("N", [5, 20])
+def test_rti_qp_builder_matches_oracle(sign, N):
+    from gp_mpc_rocket_landing_amd.mpc.qp_builder import (RTIQPBuilder, solution_to_vector,
+                                                         vector_to_solution)
+    rs = np.random.RandomState(N)
+    b = RTIQPBuilder(N, 0.1)
+    x0 = np.array([2.0, 30.0, 1.0, -1.0, -3.0, 0.2, 0.1])
+    xt = np.array([1.8, 0, 0, 0, 0, 0, 0.0])
+    X, U = b.initial_guess(x0, xt)
+    Xo, Uo = qp_oracle.initial_guess(x0, xt, N)
+    np.testing.assert_array_equal(X, Xo); np.testing.assert_array_equal(U, Uo)
+    X = X + 0.1 * rs.randn(*X.shape); U = U + 0.1 * rs.randn(*U.shape)
+    dv = rs.randn(N, 3)
+    Av, l, u = b.constraints(X, U, x0, gp_dv=dv, sign=sign)
+    A, lo, uo = qp_oracle.constraints(X, U, x0, 0.1, gp_dv=dv, sign=sign, filter_small=False)
+    A = A.tocsr(); A.sort_indices()
+    np.testing.assert_array_equal(A.indptr, b.rowptr)
+    np.testing.assert_array_equal(A.indices, b.colidx)
+    np.testing.assert_allclose(Av, A.data, rtol=1e-15, atol=1e-15)
+    np.testing.assert_allclose(l, lo, rtol=1e-14, atol=1e-14)
+    np.testing.assert_allclose(u, uo, rtol=1e-14, atol=1e-14)
+    P, q = b.cost(np.tile(xt, (N + 1, 1)))
+    Po, qo = qp_oracle.cost(N, np.tile(xt, (N + 1, 1)))
+    np.testing.assert_array_equal(P, Po.diagonal()); np.testing.assert_array_equal(q, qo)
+    z = solution_to_vector(X, U)
+    np.testing.assert_array_equal(z, qp_oracle.to_vector(X, U))
+    X2, U2 = vector_to_solution(z, N)
+    np.testing.assert_array_equal(X2, X); np.testing.assert_array_equal(U2, U)
+    # the reduced KKT of this pattern has the stage-block structure the device
+    # block-tridiagonal solver needs (blocks of 10, coupling through x_{k+1})
+    for r in range(b.m):
+        cols = b.colidx[b.rowptr[r]:b.rowptr[r + 1]]
+        for i in cols:
+            for j in cols:
+                if j <= i:
+                    bi, bj = i // 10, j // 10
+                    assert bi == bj or (bi == bj + 1 and i - 10 * bi < 7)
+
+
+def test_plant_and_jacobians_match_oracle():
+    from gp_mpc_rocket_landing_amd.dynamics import create_normalized_rocket
+    dyn = create_normalized_rocket()
+    rs = np.random.RandomState(0)
+    for _ in range(5):
+        x = np.array([1.7, 20, 1, 2, -4, 0.5, 0.3]) + 0.1 * rs.randn(7)
+        u = np.array([2.0, 0.3, -0.2]) + 0.1 * rs.randn(3)
+        np.testing.assert_allclose(dyn.step(x, u, 0.1), qp_oracle.plant_step(x, u, 0.1), rtol=1e-15)
+        A, B = dyn.linearize(x, u, 0.1)
+        Ao, Bo = qp_oracle.linearize(x, u, 0.1)
+        np.testing.assert_allclose(A, Ao, rtol=1e-15, atol=1e-17)
+        np.testing.assert_allclose(B, Bo, rtol=1e-15, atol=1e-17)
+    assert dyn.params.g == 1.0 and abs(dyn.params.alpha - 1 / 30) < 1e-15
+
+
+def test_kernel_parameter_api():
+    from gp_mpc_rocket_landing_amd.gp import (Matern52, SquaredExponential, SquaredExponentialARD,
+                                              SumKernel, WhiteNoise)
+    k = SquaredExponentialARD(4, signal_variance=2.0, lengthscales=[1, 2, 3, 4])
+    assert k.n_params == 5
+    assert k.param_names == ["log_signal_variance"] + [f"log_lengthscale_{i}" for i in range(4)]
+    np.testing.assert_allclose(k.get_params(), np.log([2, 1, 2, 3, 4]))
+    k.set_params(np.log([3, 1, 1, 1, 5]))
+    assert k.signal_variance == pytest.approx(3) and k.lengthscales[-1] == pytest.approx(5)
+    k2 = SquaredExponentialARD(4, learn_signal_variance=False)
+    assert k2.n_params == 4
+    assert SquaredExponential(1.5, 0.5).param_names == ["log_signal_variance", "log_lengthscale"]
+    s = SumKernel(Matern52(3), WhiteNoise(1e-3))
+    assert s.n_params == 5 and s.param_names[-1] == "k2_log_noise_variance"
+    np.testing.assert_allclose(WhiteNoise(0.5)(np.zeros((3, 2))), 0.5 * np.eye(3))
+    np.testing.assert_allclose(k.diagonal(np.zeros((6, 4))), np.full(6, 3.0))
+
+
+def test_surface_defaults_match_reference():
+    from gp_mpc_rocket_landing_amd.mpc import GPMPCConfig, MPCConfig, OSQPRTIConfig
+    c = OSQPRTIConfig()  # osqp_rti.py:45-71
+    assert (c.N, c.dt, c.osqp_max_iter, c.osqp_eps_abs, c.osqp_eps_rel, c.osqp_polish,
+            c.osqp_warm_start, c.osqp_scaling) == (15, 0.1, 50, 1e-4, 1e-4, False, True, 3)
+    m = MPCConfig()      # nominal_mpc.py:41-64
+    assert (m.N, m.dt, m.max_iter) == (20, 0.1, 100)
+    g = GPMPCConfig()    # gp_mpc.py:48-63
+    assert (g.use_gp_mean, g.use_gp_uncertainty, g.confidence_level) == (True, True, 0.95)
