@@ -182,10 +182,8 @@ def main():
         tmax = t.clone(); dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
         tsum = t.clone(); dist.all_reduce(tsum, op=dist.ReduceOp.SUM)
         el_max, steps_all, iters_all = float(tmax[0]), float(tsum[1]), float(tsum[2])
-        recs = torch.from_numpy(rec1).to("cuda")
-        gl = [torch.empty_like(recs) for _ in range(world)] if rank == 0 else None
-        dist.gather(recs, gl, dst=0)
-        all_rec = torch.cat(gl).cpu().numpy() if rank == 0 else None
+        from gp_mpc_rocket_landing_amd.sharding import gather_records
+        all_rec = gather_records(rec1, world * B, device="cuda")   # the one RCCL gather
     else:
         el_max, steps_all, iters_all = el, steps_done, admm_iters
         all_rec = rec1

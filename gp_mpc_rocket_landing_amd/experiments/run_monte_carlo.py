@@ -1,0 +1,101 @@
+"""Sharded Monte-Carlo landings (scripts/run_monte_carlo.py / run_experiments.py
+shapes) on one or more MI355X.
+
+    python -m gp_mpc_rocket_landing_amd.experiments.run_monte_carlo --landings 1024
+    python -m torch.distributed.run --nproc-per-node 8 --master-addr 127.0.0.1 \
+        -m gp_mpc_rocket_landing_amd.experiments.run_monte_carlo --landings 1024
+
+Each rank flies its contiguous shard of landings (initial conditions of seeds
+42 + global index) to termination on its own GPU -- GP posterior, RTI QP and
+ADMM, plant and the MonteCarloSimulator termination rules all device-resident
+-- then the 16-double records are gathered to rank 0 with one collective and
+summarised like MonteCarloSimulator's statistics (monte_carlo.py:186-272).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import time
+
+import numpy as np
+
+OUTCOME_NAMES = {1: "SUCCESS", 2: "CRASH", 3: "FUEL_EXHAUSTED", 4: "CONSTRAINT_VIOLATION",
+                 5: "TIMEOUT", 6: "DIVERGENCE"}
+
+
+def summarise(records: np.ndarray) -> dict:
+    from ..fleet import REC_ADMM_ITERS, REC_FUEL, REC_OUTCOME, REC_STEPS, REC_TIME
+    oc = records[:, REC_OUTCOME].astype(int)
+    ok = oc == 1
+    out = {"n_landings": int(len(oc)),
+           "outcomes": {OUTCOME_NAMES.get(c, str(c)): int(np.sum(oc == c)) for c in np.unique(oc)},
+           "success_rate": float(np.mean(ok)) if len(oc) else 0.0,
+           "control_steps": int(np.sum(records[:, REC_STEPS])),
+           "admm_iterations": int(np.sum(records[:, REC_ADMM_ITERS]))}
+    if np.any(ok):
+        out["fuel_used_mean_success"] = float(np.mean(records[ok, REC_FUEL]))
+        out["flight_time_mean_success"] = float(np.mean(records[ok, REC_TIME]))
+    return out
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--landings", type=int, default=1024)
+    ap.add_argument("--max-steps", type=int, default=300)
+    ap.add_argument("--chunk", type=int, default=25, help="control steps between termination polls")
+    ap.add_argument("--train", type=int, default=1000)
+    ap.add_argument("--seed0", type=int, default=42)
+    ap.add_argument("--out", default="")
+    args = ap.parse_args(argv)
+
+    import torch
+    import torch.distributed as dist
+    from .. import _lib
+    from ..fleet import REC_OUTCOME, Fleet, fit_gp, initial_conditions
+    from ..sharding import gather_records, shard_range
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    first, count = shard_range(args.landings, rank, world)
+    ctx = _lib.Context(local)
+    gp = fit_gp(ctx, n_train=args.train)          # every rank fits the same GP deterministically
+    fl = Fleet(ctx, gp, max(count, 1), max_steps=args.max_steps)
+    t0 = time.perf_counter()
+    rec = np.zeros((0, _lib.REC_LEN))
+    if count:
+        fl.reset(initial_conditions(count, args.seed0, first))
+        done = 0
+        while done < args.max_steps + 1:
+            fl.step(args.chunk)
+            done += args.chunk
+            rec, _ = fl.read()
+            if np.all(rec[:, REC_OUTCOME] != 0):
+                break
+    ctx.sync()
+    el = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([el], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t[0])
+        allrec = gather_records(rec, args.landings, device="cuda")
+    else:
+        allrec = rec
+    if rank == 0:
+        s = summarise(allrec)
+        s.update(n_gpus=world, wall_s=round(el, 3), control_steps_per_s=round(s["control_steps"] / el, 1))
+        print(json.dumps(s), flush=True)
+        if args.out:
+            np.savez(args.out, records=allrec)
+    fl.close()
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
