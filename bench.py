@@ -33,12 +33,31 @@ FP64_PEAK_TFLOPS = 78.6   # MI355X FP64 matrix (= vector) peak, spec
 HBM_PEAK_GBS = 8000.0     # MI355X HBM3E spec (MI355X_MICROARCH.md)
 
 
-def admm_flops(n=207, m=354, nnz=734, w=16):
+def admm_flops(n=207, m=354, nnz=734, sz=10, cm=7):
     """Algorithmic flops of one ADMM iteration and of one (re)factorisation of
-    the reduced KKT band (DESIGN.md 'ADMM kernel')."""
-    it = (2 * nnz + m) + 2 * (2 * n * w + n) + 2 * nnz + 12 * n + 14 * m
-    fac = n * (w * (w + 1)) + 3 * (nnz + 200)
+    the reduced KKT matrix in its block-tridiagonal form:
+    forward 2*cm*sz and backward 2*cm*sz per block boundary, diagonal 2*sz^2 per
+    block, two SpMVs with A, and the vector updates; the factor is Gauss-Jordan
+    2*sz^3 + G_k 2*cm*sz^2 + Schur 2*cm^2*sz per block plus the assembly."""
+    nblk = -(-n // sz)
+    kkt = 2 * (nblk - 1) * 2 * cm * sz + nblk * 2 * sz * sz
+    it = kkt + 2 * 2 * nnz + 12 * n + 14 * m
+    fac = nblk * (2 * sz ** 3 + 2 * cm * sz * sz + 2 * cm * cm * sz) + 3 * 1500
     return it, fac
+
+
+def pmc_traffic(kernel):
+    """Per-launch HBM bytes of ``kernel`` from the committed rocprofv3 --pmc
+    passes (profiles/*_pmc_traffic.json, scripts/pmc_traffic.py), else None."""
+    import glob
+    for path in sorted(glob.glob(os.path.join(REPO, "profiles", "*_pmc_traffic.json")), reverse=True):
+        try:
+            k = json.load(open(path))["kernels"].get(kernel)
+        except Exception:  # noqa: BLE001
+            continue
+        if k:
+            return float(k["traffic_bytes"]), os.path.basename(path)
+    return None, None
 
 
 def cpu_baseline(seconds, n_train=1000, horizon=20):
@@ -200,15 +219,15 @@ def main():
         steps_rank0 = steps_done / K
         admm_flop = (admm_iters / K) * it_f + steps_rank0 * 1.5 * fac_f
         kern = {
-            "gram_Kstar": dict(ms=ph_mean[0] * 1e3, bound="hbm",
+            "gram_Kstar": dict(kernel="k_gram<11>", ms=ph_mean[0] * 1e3, bound="hbm",
                                achieved=gram_bytes / ph_mean[0] / 1e9, peak=HBM_PEAK_GBS, unit="GB/s"),
-            "var_gemm_mfma": dict(ms=ph_mean[1] * 1e3, bound="mfma",
+            "var_gemm_mfma": dict(kernel="k_gemm_nt<1>", ms=ph_mean[1] * 1e3, bound="mfma",
                                   achieved=var_flops / ph_mean[1] / 1e12, peak=FP64_PEAK_TFLOPS,
                                   unit="TFLOP/s"),
-            "mean_gemm_finish": dict(ms=ph_mean[2] * 1e3, bound="hbm",
+            "mean_gemm_finish": dict(kernel="k_gemm_nt<0>", ms=ph_mean[2] * 1e3, bound="hbm",
                                      achieved=mean_bytes / ph_mean[2] / 1e9, peak=HBM_PEAK_GBS,
                                      unit="GB/s"),
-            "qp_admm_plant": dict(ms=ph_mean[3] * 1e3, bound="latency",
+            "qp_admm_plant": dict(kernel="k_fleet_control", ms=ph_mean[3] * 1e3, bound="mfma",
                                   achieved=admm_flop / ph_mean[3] / 1e12, peak=FP64_PEAK_TFLOPS,
                                   unit="TFLOP/s"),
         }
@@ -216,14 +235,24 @@ def main():
             v["frac"] = v["achieved"] / v["peak"]
             for kk in ("ms", "achieved", "frac"):
                 v[kk] = round(v[kk], 5)
-        # roofline object: the dominant MFMA/HBM kernel by measured time
-        cand = {k: v for k, v in kern.items() if v["bound"] in ("hbm", "mfma")}
-        dom = max(cand, key=lambda k: cand[k]["ms"])
+            tb, src = pmc_traffic(v["kernel"])
+            v["traffic"] = tb
+        # roofline object: the kernel that dominates the step's time.  The control
+        # kernel (ADMM) is priced against the FP64 compute ceiling (vector = matrix,
+        # 78.6 TF); its limiter is the serial KKT dependency chain of one wave per
+        # landing, not HBM or MFMA.
+        dom = max(kern, key=lambda k: kern[k]["ms"])
         d = kern[dom]
-        roof = dict(kernel=dom, bound=d["bound"], achieved=d["achieved"], peak=d["peak"],
-                    unit=d["unit"], frac=d["frac"], traffic=None,
-                    per_launch=("n^2 P flop" if d["bound"] == "mfma" else "bytes"),
-                    launches_per_step=1)
+        roof = dict(kernel=d["kernel"], bound=d["bound"], achieved=d["achieved"], peak=d["peak"],
+                    unit=d["unit"], frac=d["frac"], traffic=d["traffic"],
+                    per_launch={"qp_admm_plant": "ADMM iterations x block-KKT iteration flops + "
+                                                 "factorisations (admm_flops)",
+                                "var_gemm_mfma": "n^2 P flop", "gram_Kstar": "8 n P + 8 d (P+n) bytes",
+                                "mean_gemm_finish": "8 n P bytes"}[dom],
+                    traffic_source=pmc_traffic(d["kernel"])[1], launches_per_step=1)
+        if dom == "qp_admm_plant":
+            roof["limiter"] = ("latency: serial block-tridiagonal KKT chain, one wave per landing; "
+                               "~10 KB HBM per landing-step")
         out = {
             "metric": "GP-MPC control steps/sec (N=20, 1000 GP pts)",
             "value": round(steps_all / el_max, 2),

@@ -117,8 +117,11 @@ int gpmpc_fitc_destroy(gpmpc_fitc *gp);
  *     min 1/2 x'Px + q'x  s.t.  l <= Ax <= u
  * sharing one sparsity pattern of A (CSR: rowptr m+1, colidx nnz) and a
  * diagonal P.  Per problem: Aval (nnz), Pdiag (n), q (n), l/u (m).  The
- * reduced KKT matrix P + sigma I + A' diag(rho) A must be banded (the MPC
- * stage structure gives half-bandwidth 2*nx+nu-1); bandwidth <= 24.
+ * reduced KKT matrix M = P + sigma I + A' diag(rho) A is factored either
+ * block-tridiagonally (the MPC stage structure: blocks of 10 variables
+ * coupled through their first 7, n <= 216) or, for any other pattern, as a
+ * banded LDL^T with half-bandwidth <= 16.  Caps: n <= 216, m <= 360,
+ * nnz <= 736, <= 8 entries per row and <= 12 per column of A.
  * State carried between solves (OSQP keeps it in its workspace):
  *   rho (batch), y_scaled (batch x m).  x_ws: warm-start primal (unscaled).
  * Outputs: x (batch x n), y (batch x m) unscaled, iters, status, obj. */
