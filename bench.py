@@ -181,8 +181,8 @@ def main():
     for k in range(K):
         e = ev[k]
         e[0].record(stream); fl.phases(1)   # features + K* gram
-        e[1].record(stream); fl.phases(4)   # variance GEMM (MFMA)
-        e[2].record(stream); fl.phases(8)   # mean GEMM + finish
+        e[1].record(stream); fl.phases(4)   # variance + mean GEMM (MFMA, one pass over K*)
+        e[2].record(stream); fl.phases(8)   # posterior finish
         e[3].record(stream); fl.phases(2)   # QP assembly + ADMM + plant
         e[4].record(stream)
     ctx.sync(); torch.cuda.synchronize()
@@ -212,21 +212,22 @@ def main():
         n = args.train
         # per-launch algorithmic work: variance GEMM n^2 P flop
         # (lower-triangular L^-1 times K*^T), K* gram 8 n P bytes written
-        var_flops = float(n) * n * P
+        var_flops = float(n) * n * P + 2.0 * 3 * n * P      # W K*^T (triangular) + alpha^T K*^T
         gram_bytes = 8.0 * n * P + 8.0 * (P * 12 + n * 12)
-        mean_bytes = 8.0 * n * P
+        nrt = -(-(n + 3) // 64)
+        fin_bytes = 8.0 * P * (nrt + 3 + 6)                 # partials + means in, mean/var out
         it_f, fac_f = admm_flops()
         steps_rank0 = steps_done / K
         admm_flop = (admm_iters / K) * it_f + steps_rank0 * 1.5 * fac_f
         kern = {
             "gram_Kstar": dict(kernel="k_gram<11>", ms=ph_mean[0] * 1e3, bound="hbm",
                                achieved=gram_bytes / ph_mean[0] / 1e9, peak=HBM_PEAK_GBS, unit="GB/s"),
-            "var_gemm_mfma": dict(kernel="k_gemm_nt<1>", ms=ph_mean[1] * 1e3, bound="mfma",
-                                  achieved=var_flops / ph_mean[1] / 1e12, peak=FP64_PEAK_TFLOPS,
-                                  unit="TFLOP/s"),
-            "mean_gemm_finish": dict(kernel="k_gemm_nt<0>", ms=ph_mean[2] * 1e3, bound="hbm",
-                                     achieved=mean_bytes / ph_mean[2] / 1e9, peak=HBM_PEAK_GBS,
-                                     unit="GB/s"),
+            "var_mean_gemm_mfma": dict(kernel="k_gemm_nt<1>", ms=ph_mean[1] * 1e3, bound="mfma",
+                                       achieved=var_flops / ph_mean[1] / 1e12, peak=FP64_PEAK_TFLOPS,
+                                       unit="TFLOP/s"),
+            "post_finish": dict(kernel="k_post_finish", ms=ph_mean[2] * 1e3, bound="hbm",
+                                achieved=fin_bytes / ph_mean[2] / 1e9, peak=HBM_PEAK_GBS,
+                                unit="GB/s"),
             "qp_admm_plant": dict(kernel="k_fleet_control", ms=ph_mean[3] * 1e3, bound="mfma",
                                   achieved=admm_flop / ph_mean[3] / 1e12, peak=FP64_PEAK_TFLOPS,
                                   unit="TFLOP/s"),
@@ -247,8 +248,9 @@ def main():
                     unit=d["unit"], frac=d["frac"], traffic=d["traffic"],
                     per_launch={"qp_admm_plant": "ADMM iterations x block-KKT iteration flops + "
                                                  "factorisations (admm_flops)",
-                                "var_gemm_mfma": "n^2 P flop", "gram_Kstar": "8 n P + 8 d (P+n) bytes",
-                                "mean_gemm_finish": "8 n P bytes"}[dom],
+                                "var_mean_gemm_mfma": "n^2 P + 6 n P flop",
+                                "gram_Kstar": "8 n P + 8 d (P+n) bytes",
+                                "post_finish": "8 P (row tiles + 9) bytes"}[dom],
                     traffic_source=pmc_traffic(d["kernel"])[1], launches_per_step=1)
         if dom == "qp_admm_plant":
             roof["limiter"] = ("latency: serial block-tridiagonal KKT chain, one wave per landing; "

@@ -432,7 +432,7 @@ extern "C" int gpmpc_fleet_create(gpmpc_ctx *ctx, gpmpc_gp *gp, const gpmpc_flee
     return -1;
   }
   const size_t B = batch, P = (size_t)batch * N;
-  const int nrt = gemm_row_tiles(g.n);
+  const int nrt = gemm_row_tiles(g.n + 3);  // W rows + the 3 alpha^T rows
   if (f->x.alloc(sizeof(double) * B * NX) || f->Xw.alloc(sizeof(double) * B * (N + 1) * NX) ||
       f->Uw.alloc(sizeof(double) * B * N * NU) || f->ysc.alloc(sizeof(double) * B * m) ||
       f->rho.alloc(sizeof(double) * B) || f->rec.alloc(sizeof(double) * B * GPMPC_REC_LEN) ||
@@ -470,13 +470,13 @@ extern "C" int gpmpc_fleet_reset(gpmpc_fleet *f, int first, int count, const dou
 }
 
 // GP posterior of every landing's horizon, in three timed sub-phases:
-//   bit 0: features + K* gram;  bit 2: variance GEMM (W K*^T, SUMSQ epilogue);
-//   bit 3: mean GEMM (alpha^T K*^T) + finish
+//   bit 0: features + K* gram;  bit 2: one MFMA pass over K* with [W; alpha^T]:
+//   variance partial sums (SUMSQ epilogue) and the means;  bit 3: finish
 static hipError_t fleet_gp_posterior(gpmpc_fleet *f, int mask) {
   hipStream_t s = f->ctx->stream;
   const GpView g = gp_view(f->gp);
   const int P = f->B * f->N;
-  const int nrt = gemm_row_tiles(g.n);
+  const int nrt = gemm_row_tiles(g.n + 3);  // W rows + the 3 alpha^T rows
   hipError_t e = hipSuccess;
   if (mask & 1) {
     hipLaunchKernelGGL(k_fleet_queries, dim3((P + 255) / 256), dim3(256), 0, s, f->B, f->N,
@@ -487,14 +487,11 @@ static hipError_t fleet_gp_posterior(gpmpc_fleet *f, int mask) {
     if (e != hipSuccess) return e;
   }
   if (mask & 4) {
-    e = launch_gemm_nt(s, EPI_SUMSQ, g.n, P, g.n, g.W, g.n, f->Ks.as<double>(), g.n,
-                       f->part.as<double>(), P, 1.0, 0.0, 1, 0, 1, 0, 0, 0);
+    e = launch_gemm_sumsq_mean(s, g.n, 3, P, g.W, f->Ks.as<double>(), f->part.as<double>(), P,
+                               f->meanT.as<double>(), P);
     if (e != hipSuccess) return e;
   }
   if (mask & 8) {
-    e = launch_gemm_nt(s, EPI_STORE, 3, P, g.n, g.alphaT, g.n, f->Ks.as<double>(), g.n,
-                       f->meanT.as<double>(), P, 1.0, 0.0, 0, 0, 1, 0, 0, 0);
-    if (e != hipSuccess) return e;
     e = launch_post_finish(s, P, 3, nrt, f->part.as<double>(), P, f->meanT.as<double>(), P,
                            g.ymean, g.ystd, g.sigma2, f->mean.as<double>(), f->var.as<double>());
   }

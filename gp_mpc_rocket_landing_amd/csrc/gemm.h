@@ -16,4 +16,11 @@ hipError_t launch_trsm_lower_ex(hipStream_t s, int n, int nrhs, const double *L,
                                 double *X, int64_t ldx, int trans, int rhs_lower,
                                 double *Linv_blocks);
 
+// posterior in one pass: Wext = [W (n x n, lower); alpha^T (n_out x n)]:
+// part[t][j] = sum over W rows of tile t of (W K*^T)^2, meanT = alpha^T K*^T
+// (n_out x P).  part has gemm_row_tiles(n + n_out) rows.
+hipError_t launch_gemm_sumsq_mean(hipStream_t s, int n, int n_out, int P, const double *Wext,
+                                  const double *Ks, double *part, int64_t ldp, double *meanT,
+                                  int64_t ldm);
+
 inline int gemm_row_tiles(int M) { return (M + 63) / 64; }

@@ -12,6 +12,7 @@
 // Tile 64 x 64 per 256-thread workgroup, each wave a 32 x 32 quadrant
 // (2 x 2 MFMA blocks), K staged 16 at a time through LDS with an 18-double
 // pitch (conflict-free ds_read_b64 for the 16-row x 4-k operand gathers).
+#include <cstdlib>
 #include "internal.h"
 #include "mfma64.h"
 #include "gemm.h"
@@ -26,15 +27,27 @@ __global__ __launch_bounds__(256) void k_gemm_nt(int M, int N, int K, const doub
                                                  int64_t ldb, double *__restrict__ C, int64_t ldc,
                                                  double alpha, double beta, int tri_a,
                                                  int lower_c, int64_t sA_, int64_t sB_,
-                                                 int64_t sC_) {
+                                                 int64_t sC_, int msum, double *__restrict__ Cm,
+                                                 int64_t ldm, int remap_ty) {
   const int bz = blockIdx.z;
   A += bz * sA_;
   B += bz * sB_;
   C += bz * sC_;
-  const int r0 = blockIdx.y * GT, c0 = blockIdx.x * GT;
+  // optional XCD-aware order (1-D grid, GPMPC_GEMM_REMAP=1): workgroup i runs
+  // on XCD i % 8; each XCD gets whole column blocks and walks their row tiles
+  // back to back.  Off by default: for the posterior GEMM the plain order
+  // (concurrent workgroups share a W row block, K* streams from the 256 MB
+  // Infinity Cache) measured 0.46 ms vs 0.54 ms with the remap.
+  int bx = blockIdx.x, by = blockIdx.y;
+  if (remap_ty) {
+    const int i = blockIdx.x, slot = i >> 3;
+    bx = (i & 7) + 8 * (slot / remap_ty);
+    by = slot % remap_ty;
+  }
+  const int r0 = by * GT, c0 = bx * GT;
   if (lower_c && c0 > r0 + GT - 1) return;
-  __shared__ double sA[GT][GP];
-  __shared__ double sB[GT][GP];
+  __shared__ double sA[2][GT][GP];
+  __shared__ double sB[2][GT][GP];
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int qi = (wave >> 1) * 32, qj = (wave & 1) * 32;
   int kend = K;
@@ -44,33 +57,60 @@ __global__ __launch_bounds__(256) void k_gemm_nt(int M, int N, int K, const doub
   for (int x = 0; x < 2; ++x)
 #pragma unroll
     for (int y = 0; y < 2; ++y) acc[x][y] = (d4_t){0.0, 0.0, 0.0, 0.0};
-  // each thread loads 4 elements of A and 4 of B per K-step: row = tid/4, k = (tid%4)*4..+3
+  // each thread moves 4 consecutive k of one row of A and of B per K-step:
+  // row = tid/4, k = (tid%4)*4..+3.  The next step's operands are loaded into
+  // registers while the current step's MFMAs run (LDS double buffer, one
+  // barrier per K-step); rows are read as two 16-byte loads when aligned.
   const int lr = tid >> 2, lk = (tid & 3) * 4;
+  const bool ra = r0 + lr < M, rb = c0 + lr < N;
+  const double *pa = A + (int64_t)(ra ? r0 + lr : 0) * lda;
+  const double *pb = B + (int64_t)(rb ? c0 + lr : 0) * ldb;
+  const bool vec = ((lda | ldb) & 1) == 0 && ((((uintptr_t)A) | ((uintptr_t)B)) & 15) == 0;
+  double va[4], vb[4];
+  auto gload = [&](int k0) {
+    const int k = k0 + lk;
+    if (vec && k + 3 < kend) {
+      const double2 a01 = ra ? *(const double2 *)(pa + k) : make_double2(0.0, 0.0);
+      const double2 a23 = ra ? *(const double2 *)(pa + k + 2) : make_double2(0.0, 0.0);
+      const double2 b01 = rb ? *(const double2 *)(pb + k) : make_double2(0.0, 0.0);
+      const double2 b23 = rb ? *(const double2 *)(pb + k + 2) : make_double2(0.0, 0.0);
+      va[0] = a01.x; va[1] = a01.y; va[2] = a23.x; va[3] = a23.y;
+      vb[0] = b01.x; vb[1] = b01.y; vb[2] = b23.x; vb[3] = b23.y;
+    } else {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        va[q] = (ra && k + q < kend) ? pa[k + q] : 0.0;
+        vb[q] = (rb && k + q < kend) ? pb[k + q] : 0.0;
+      }
+    }
+  };
+  auto lstore = [&](int buf) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      sA[buf][lr][lk + q] = va[q];
+      sB[buf][lr][lk + q] = vb[q];
+    }
+  };
+  gload(0);
+  lstore(0);
+  __syncthreads();
+  int cur = 0;
   for (int k0 = 0; k0 < kend; k0 += GK) {
-    double va[4], vb[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int k = k0 + lk + q;
-      va[q] = (r0 + lr < M && k < kend) ? A[(int64_t)(r0 + lr) * lda + k] : 0.0;
-      vb[q] = (c0 + lr < N && k < kend) ? B[(int64_t)(c0 + lr) * ldb + k] : 0.0;
-    }
-    __syncthreads();
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      sA[lr][lk + q] = va[q];
-      sB[lr][lk + q] = vb[q];
-    }
-    __syncthreads();
+    const bool more = k0 + GK < kend;
+    if (more) gload(k0 + GK);
 #pragma unroll
     for (int kk = 0; kk < GK; kk += 4) {
       const int kc = kk + (lane >> 4);
-      const double a0 = sA[qi + (lane & 15)][kc], a1 = sA[qi + 16 + (lane & 15)][kc];
-      const double b0 = sB[qj + (lane & 15)][kc], b1 = sB[qj + 16 + (lane & 15)][kc];
+      const double a0 = sA[cur][qi + (lane & 15)][kc], a1 = sA[cur][qi + 16 + (lane & 15)][kc];
+      const double b0 = sB[cur][qj + (lane & 15)][kc], b1 = sB[cur][qj + 16 + (lane & 15)][kc];
       acc[0][0] = mfma_f64(a0, b0, acc[0][0]);
       acc[0][1] = mfma_f64(a0, b1, acc[0][1]);
       acc[1][0] = mfma_f64(a1, b0, acc[1][0]);
       acc[1][1] = mfma_f64(a1, b1, acc[1][1]);
     }
+    if (more) lstore(cur ^ 1);
+    __syncthreads();
+    cur ^= 1;
   }
   if (EPI == EPI_STORE) {
 #pragma unroll
@@ -87,15 +127,23 @@ __global__ __launch_bounds__(256) void k_gemm_nt(int M, int N, int K, const doub
           }
         }
   } else {
-    // sum of squares over rows (rows >= M contribute exact zeros)
+    // sum of squares over rows < msum (rows >= M contribute exact zeros);
+    // rows msum..M-1 (alpha^T appended to W) are stored to Cm: the mean
     __shared__ double red[4][32];
     double s0 = 0.0, s1 = 0.0;
 #pragma unroll
     for (int x = 0; x < 2; ++x)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        s0 = fma(acc[x][0][r], acc[x][0][r], s0);
-        s1 = fma(acc[x][1][r], acc[x][1][r], s1);
+        const int row = r0 + qi + x * 16 + mf_row(lane, r);
+        if (row < msum) {
+          s0 = fma(acc[x][0][r], acc[x][0][r], s0);
+          s1 = fma(acc[x][1][r], acc[x][1][r], s1);
+        } else if (row < M) {
+          const int col0 = c0 + qj + mf_col(lane);
+          if (col0 < N) Cm[(int64_t)(row - msum) * ldm + col0] = acc[x][0][r];
+          if (col0 + 16 < N) Cm[(int64_t)(row - msum) * ldm + col0 + 16] = acc[x][1][r];
+        }
       }
     s0 += __shfl_xor(s0, 16);
     s0 += __shfl_xor(s0, 32);
@@ -111,22 +159,45 @@ __global__ __launch_bounds__(256) void k_gemm_nt(int M, int N, int K, const doub
       const int half = tid >> 5, cc = tid & 31;
       const double v = red[half][cc] + red[2 + half][cc];  // waves (0,half) and (1,half)
       const int col = c0 + tid;
-      if (col < N) C[(int64_t)blockIdx.y * ldc + col] = v;
+      if (col < N) C[(int64_t)by * ldc + col] = v;
     }
   }
+}
+
+static hipError_t launch_gemm_impl(hipStream_t s, int epi, int M, int N, int K, const double *A,
+                                   int64_t lda, const double *B, int64_t ldb, double *C,
+                                   int64_t ldc, double alpha, double beta, int tri_a, int lower_c,
+                                   int batch, int64_t sA, int64_t sB, int64_t sC, int msum,
+                                   double *Cm, int64_t ldm) {
+  if (M <= 0 || N <= 0) return hipSuccess;
+  const int tx = (N + GT - 1) / GT, ty = (M + GT - 1) / GT;
+  static const int remap_env = [] {
+    const char *e = getenv("GPMPC_GEMM_REMAP");
+    return e ? atoi(e) : 0;  // measured slower for the posterior GEMM (W blocks thrash)
+  }();
+  const bool remap = remap_env && batch == 1 && ty > 1 && tx % 8 == 0;
+  dim3 g = remap ? dim3(tx * ty, 1, 1) : dim3(tx, ty, batch);
+  const int rt = remap ? ty : 0;
+  if (epi == EPI_STORE)
+    hipLaunchKernelGGL(k_gemm_nt<EPI_STORE>, g, dim3(256), 0, s, M, N, K, A, lda, B, ldb, C, ldc,
+                       alpha, beta, tri_a, lower_c, sA, sB, sC, M, nullptr, (int64_t)0, rt);
+  else
+    hipLaunchKernelGGL(k_gemm_nt<EPI_SUMSQ>, g, dim3(256), 0, s, M, N, K, A, lda, B, ldb, C, ldc,
+                       alpha, beta, tri_a, 0, sA, sB, sC, msum, Cm, ldm, rt);
+  return hipGetLastError();
 }
 
 hipError_t launch_gemm_nt(hipStream_t s, int epi, int M, int N, int K, const double *A,
                           int64_t lda, const double *B, int64_t ldb, double *C, int64_t ldc,
                           double alpha, double beta, int tri_a, int lower_c, int batch,
                           int64_t sA, int64_t sB, int64_t sC) {
-  if (M <= 0 || N <= 0) return hipSuccess;
-  dim3 g((N + GT - 1) / GT, (M + GT - 1) / GT, batch);
-  if (epi == EPI_STORE)
-    hipLaunchKernelGGL(k_gemm_nt<EPI_STORE>, g, dim3(256), 0, s, M, N, K, A, lda, B, ldb, C, ldc,
-                       alpha, beta, tri_a, lower_c, sA, sB, sC);
-  else
-    hipLaunchKernelGGL(k_gemm_nt<EPI_SUMSQ>, g, dim3(256), 0, s, M, N, K, A, lda, B, ldb, C, ldc,
-                       alpha, beta, tri_a, 0, sA, sB, sC);
-  return hipGetLastError();
+  return launch_gemm_impl(s, epi, M, N, K, A, lda, B, ldb, C, ldc, alpha, beta, tri_a, lower_c,
+                          batch, sA, sB, sC, M, nullptr, 0);
+}
+
+hipError_t launch_gemm_sumsq_mean(hipStream_t s, int n, int n_out, int P, const double *Wext,
+                                  const double *Ks, double *part, int64_t ldp, double *meanT,
+                                  int64_t ldm) {
+  return launch_gemm_impl(s, EPI_SUMSQ, n + n_out, P, n, Wext, n, Ks, n, part, ldp, 1.0, 0.0, 1, 0,
+                          1, 0, 0, 0, n, meanT, ldm);
 }

@@ -291,7 +291,8 @@ extern "C" int gpmpc_gp_fit_exact(gpmpc_ctx *ctx, int kind, const double *X, int
   if (dYraw.alloc(sizeof(double) * n * n_out) || dY.alloc(sizeof(double) * n * n_out) ||
       dyn.alloc(sizeof(double) * n * n_out) || dlml.alloc(sizeof(double) * n_out) ||
       g.ymean.alloc(sizeof(double) * n_out) || g.ystd.alloc(sizeof(double) * n_out) ||
-      g.alphaT.alloc(sizeof(double) * n_out * n) || g.W.alloc(sizeof(double) * (size_t)n * n))
+      g.alphaT.alloc(sizeof(double) * n_out * n) ||
+      g.W.alloc(sizeof(double) * (size_t)(n + n_out) * n))  // [W; alpha^T]
     return fail(-1);
   g.n_out = n_out;
   hipMemcpyAsync(dYraw.p, Y, sizeof(double) * n * n_out, hipMemcpyHostToDevice, s);
@@ -306,6 +307,9 @@ extern "C" int gpmpc_gp_fit_exact(gpmpc_ctx *ctx, int kind, const double *X, int
   // W = L^-1 (identity right-hand side, lower-triangular result)
   hipLaunchKernelGGL(k_eye, dim3((n + 255) / 256, n), dim3(256), 0, s, n, g.W.as<double>());
   launch_trsm_lower_ex(s, n, n, gp->L.as<double>(), n, g.W.as<double>(), n, 0, 1, nullptr);
+  // alpha^T below W: the variance GEMM produces the posterior mean in the same pass
+  hipMemcpyAsync(g.W.as<double>() + (size_t)n * n, g.alphaT.p, sizeof(double) * n_out * n,
+                 hipMemcpyDeviceToDevice, s);
   g.h_ymean.resize(n_out);
   g.h_ystd.resize(n_out);
   hipMemcpyAsync(g.h_ymean.data(), g.ymean.p, sizeof(double) * n_out, hipMemcpyDeviceToHost, s);
@@ -329,16 +333,13 @@ extern "C" int gpmpc_gp_fit_exact(gpmpc_ctx *ctx, int kind, const double *X, int
 static int core_posterior(gpmpc_ctx *ctx, const GpCore &g, const double *Ks, int p, double *dmean,
                           double *dvar) {
   hipStream_t s = ctx->stream;
-  const int nrt = gemm_row_tiles(g.n);
+  const int nrt = gemm_row_tiles(g.n + g.n_out);
   DevBuf part, meanT;
   GPMPC_HIP(part.alloc(sizeof(double) * (size_t)nrt * p));
   GPMPC_HIP(meanT.alloc(sizeof(double) * (size_t)g.n_out * p));
-  // sum_i (W K*^T)_ij^2 per query j
-  GPMPC_HIP(launch_gemm_nt(s, EPI_SUMSQ, g.n, p, g.n, g.W.as<double>(), g.n, Ks, g.n,
-                           part.as<double>(), p, 1.0, 0.0, 1, 0, 1, 0, 0, 0));
-  // K* alpha  -> (n_out x p)
-  GPMPC_HIP(launch_gemm_nt(s, EPI_STORE, g.n_out, p, g.n, g.alphaT.as<double>(), g.n, Ks, g.n,
-                           meanT.as<double>(), p, 1.0, 0.0, 0, 0, 1, 0, 0, 0));
+  // one pass over K*: sum_i (W K*^T)_ij^2 per query j and alpha^T K*^T
+  GPMPC_HIP(launch_gemm_sumsq_mean(s, g.n, g.n_out, p, g.W.as<double>(), Ks, part.as<double>(), p,
+                                   meanT.as<double>(), p));
   hipLaunchKernelGGL(k_post_finish, dim3((p + 255) / 256), dim3(256), 0, s, p, g.n_out, nrt,
                      part.as<double>(), (int64_t)p, meanT.as<double>(), (int64_t)p,
                      g.ymean.as<double>(), g.ystd.as<double>(), g.sigma2, dmean, dvar);

@@ -164,8 +164,9 @@ int gpmpc_fleet_reset(gpmpc_fleet *f, int first, int count, const double *x0);
 /* advance every active landing by nsteps control steps (async on the ctx stream) */
 int gpmpc_fleet_step(gpmpc_fleet *f, int nsteps);
 /* one step split in its phases, launched in the order 0, 2, 3, 1:
- * bit 0: horizon features + K* = k(Z*, X) Gram; bit 2: variance GEMM
- * (|L^-1 K*^T|^2 on FP64 MFMA); bit 3: mean GEMM + posterior finish;
+ * bit 0: horizon features + K* = k(Z*, X) Gram; bit 2: one FP64-MFMA pass
+ * over K* with [L^-1; alpha^T]: variance partial sums |L^-1 K*^T|^2 and the
+ * means alpha^T K*^T; bit 3: posterior finish;
  * bit 1: QP assembly + ADMM + plant step.  A full step = phases(15). */
 int gpmpc_fleet_step_phases(gpmpc_fleet *f, int phase_mask);
 /* records (batch x GPMPC_REC_LEN doubles): 0 outcome (0 running, 1..6 =
