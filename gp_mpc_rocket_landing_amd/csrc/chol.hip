@@ -4,189 +4,132 @@
 // scipy.linalg.solve_triangular and cho_solve (exact_gp.py:164-179, 251-260;
 // sparse_gp.py:187-232, 293-296).
 //
-// potrf, per 32-wide panel k (all matrices of a batch in the same launches):
-//   1. k_potrf_diag   one workgroup per matrix factors the 32x32 diagonal block
-//                     in LDS (LAPACK pivot test: fail unless a_jj > 0), stores
-//                     L_kk and its inverse;
-//   2. k_potrf_panel  A[i,k] <- A[i,k] L_kk^-T for the rows below (as a GEMM
-//                     with the precomputed inverse);
-//   3. k_syrk_mfma    trailing lower update A[i,j] -= A[i,k] A[j,k]^T on
-//                     v_mfma_f64_16x16x4_f64, 64x64 tiles, 4 waves x 32x32.
-// A failed pivot sets info[b] (1-based column) and freezes that matrix.
+// potrf (all matrices of a batch in the same launches): two-level blocking,
+// see launch_potrf_batched.  The 32x32 diagonal blocks are factored by
+// k_potrf_diag (LAPACK pivot test: fail unless a_jj > 0); panels, in-panel
+// updates and the trailing SYRK are MFMA GEMMs (gemm.hip).  A failed pivot
+// sets info[b] (1-based column) and freezes that matrix's diagonal steps.
 #include "internal.h"
 #include "mfma64.h"
+#include "gemm.h"
 
 #define NB 32
 #define TP 34  // LDS pitch (doubles) for 32-wide tiles: conflict-free ds_read_b64
 
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_potrf_diag(int n, int k0, double *A, int64_t lda,
-                                                    int64_t stride, int *info, double *Linv) {
+// 32x32 diagonal block: one wave per matrix, row i of the block in lane i's
+// registers.  Right-looking: the pivot comes by readlane, column j is
+// broadcast through LDS (one ds_write per lane, wave-ordered reads, no
+// barrier).  Then L^-1 by column-parallel forward substitution (lane c
+// computes column c; every lane reads the same L[r][k] -> LDS broadcast).
+__global__ __launch_bounds__(64) void k_potrf_diag(int n, int k0, double *A, int64_t lda,
+                                                   int64_t stride, int *info, double *Linv) {
   const int b = blockIdx.x;
   if (info[b]) return;
   double *M = A + (int64_t)b * stride;
   const int nb = min(NB, n - k0);
-  __shared__ double s[NB][NB + 1];
-  __shared__ double inv[NB][NB + 1];
-  __shared__ int fail;
-  const int tid = threadIdx.x;
-  for (int e = tid; e < NB * NB; e += 256) {
-    int i = e / NB, j = e % NB;
-    s[i][j] = (i < nb && j <= i) ? M[(int64_t)(k0 + i) * lda + k0 + j] : 0.0;
-  }
-  if (tid == 0) fail = 0;
-  __syncthreads();
-  for (int j = 0; j < nb; ++j) {
-    if (tid == 0) {
-      double v = s[j][j];
-      if (!(v > 0.0)) fail = j + 1;
-      else s[j][j] = sqrt(v);
+  const int lane = threadIdx.x;
+  __shared__ double col[NB];
+  __shared__ double sl[NB][NB + 2];
+  double a[NB];
+  const bool live = lane < nb;
+#pragma unroll
+  for (int j = 0; j < NB; ++j)
+    a[j] = (live && j <= lane) ? M[(int64_t)(k0 + lane) * lda + k0 + j] : (j == lane ? 1.0 : 0.0);
+  int fail = 0;
+#pragma unroll
+  for (int j = 0; j < NB; ++j) {
+    if (j < nb) {
+      const double piv = __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(a[j]), j),
+                                          __builtin_amdgcn_readlane(__double2loint(a[j]), j));
+      if (!(piv > 0.0)) {
+        fail = j + 1;
+        break;
+      }
+      const double d = sqrt(piv), id = 1.0 / d;
+      a[j] = (lane == j) ? d : a[j] * id;
+      if (lane < NB) col[lane] = a[j];
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      const double lij = a[j];
+#pragma unroll
+      for (int k = j + 1; k < NB; ++k) a[k] = fma(-lij, col[k], a[k]);  // upper part: unused
+      __builtin_amdgcn_wave_barrier();
     }
-    __syncthreads();
-    if (fail) break;
-    const double piv = s[j][j];
-    for (int i = j + 1 + tid; i < nb; i += 256) s[i][j] /= piv;
-    __syncthreads();
-    const int w = nb - j - 1;
-    for (int e = tid; e < w * w; e += 256) {
-      int i = j + 1 + e / w, c = j + 1 + e % w;
-      if (c <= i) s[i][c] -= s[i][j] * s[c][j];
-    }
-    __syncthreads();
   }
   if (fail) {
-    if (tid == 0) info[b] = k0 + fail;
+    if (lane == 0) info[b] = k0 + fail;
     return;
   }
-  for (int e = tid; e < nb * nb; e += 256) {
-    int i = e / nb, j = e % nb;
-    if (j <= i) M[(int64_t)(k0 + i) * lda + k0 + j] = s[i][j];
+  if (live) {
+#pragma unroll
+    for (int j = 0; j < NB; ++j)
+      if (j <= lane) M[(int64_t)(k0 + lane) * lda + k0 + j] = a[j];
   }
-  // inverse of the lower-triangular block, one column per thread
-  if (tid < NB) {
-    const int c = tid;
-    for (int r = 0; r < NB; ++r) {
-      double v;
-      if (r < c || r >= nb || c >= nb) v = (r == c) ? 1.0 : 0.0;
-      else {
-        double sum = (r == c) ? 1.0 : 0.0;
-        for (int k = c; k < r; ++k) sum -= s[r][k] * inv[k][c];
-        v = sum / s[r][r];
-      }
-      inv[r][c] = v;
-    }
+  // L (identity beyond nb) to LDS, then column c of L^-1 in lane c
+  if (lane < NB) {
+#pragma unroll
+    for (int j = 0; j < NB; ++j) sl[lane][j] = (j <= lane) ? a[j] : 0.0;
   }
-  __syncthreads();
-  double *Li = Linv + (int64_t)b * NB * NB;
-  for (int e = tid; e < NB * NB; e += 256) Li[e] = inv[e / NB][e % NB];
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  double x[NB];
+  const int c = lane;
+#pragma unroll
+  for (int r = 0; r < NB; ++r) {
+    double sum = (r == c) ? 1.0 : 0.0;
+#pragma unroll
+    for (int k = 0; k < r; ++k) sum = fma(-sl[r][k], x[k], sum);  // x[k] = 0 for k < c
+    x[r] = (r >= c) ? sum / sl[r][r] : 0.0;
+  }
+  if (lane < NB) {
+    double *Li = Linv + (int64_t)b * NB * NB;
+#pragma unroll
+    for (int r = 0; r < NB; ++r) Li[r * NB + c] = x[r];
+  }
 }
 
-// A[r, k0:k0+nb] <- A[r, k0:k0+nb] * Linv^T for rows r in [k0+nb, n)
-__global__ __launch_bounds__(256) void k_potrf_panel(int n, int k0, double *A, int64_t lda,
-                                                     int64_t stride, const int *info,
-                                                     const double *Linv) {
-  const int b = blockIdx.y;
-  if (info[b]) return;
-  double *M = A + (int64_t)b * stride;
-  const int nb = min(NB, n - k0);
-  const int r0 = k0 + nb + blockIdx.x * 64;
-  __shared__ double sA[64][TP];
-  __shared__ double sL[NB][TP];
-  const int tid = threadIdx.x;
-  for (int e = tid; e < 64 * NB; e += 256) {
-    int r = e / NB, j = e % NB;
-    sA[r][j] = (r0 + r < n && j < nb) ? M[(int64_t)(r0 + r) * lda + k0 + j] : 0.0;
-  }
-  const double *Li = Linv + (int64_t)b * NB * NB;
-  for (int e = tid; e < NB * NB; e += 256) sL[e / NB][e % NB] = Li[e];
-  __syncthreads();
-  const int r = tid >> 2, cb = (tid & 3) * 8;
-  if (r0 + r >= n) return;
-  double out[8];
-#pragma unroll
-  for (int q = 0; q < 8; ++q) out[q] = 0.0;
-  for (int j = 0; j < NB; ++j) {
-    const double a = sA[r][j];
-#pragma unroll
-    for (int q = 0; q < 8; ++q) out[q] = fma(a, sL[cb + q][j], out[q]);  // Linv[c][j], j<=c
-  }
-#pragma unroll
-  for (int q = 0; q < 8; ++q)
-    if (cb + q < nb) M[(int64_t)(r0 + r) * lda + k0 + cb + q] = out[q];
-}
-
-__device__ __forceinline__ void lower_tile_index(int t, int &ti, int &tj) {
-  int i = (int)((sqrt(8.0 * t + 1.0) - 1.0) * 0.5);
-  while ((i + 1) * (i + 2) / 2 <= t) ++i;
-  while (i * (i + 1) / 2 > t) --i;
-  ti = i;
-  tj = t - i * (i + 1) / 2;
-}
-
-// trailing update on the lower triangle of [t0, n) x [t0, n) with panel columns [k0, k0+kw)
-__global__ __launch_bounds__(256) void k_syrk_mfma(int n, int k0, int kw, int t0, double *A,
-                                                   int64_t lda, int64_t stride, const int *info) {
-  const int b = blockIdx.y;
-  if (info && info[b]) return;
-  double *M = A + (int64_t)b * stride;
-  int ti, tj;
-  lower_tile_index(blockIdx.x, ti, tj);
-  const int ri = t0 + ti * 64, rj = t0 + tj * 64;
-  __shared__ double sI[64][TP];
-  __shared__ double sJ[64][TP];
-  const int tid = threadIdx.x;
-  for (int e = tid; e < 64 * NB; e += 256) {
-    int r = e / NB, j = e % NB;
-    bool ok = j < kw;
-    sI[r][j] = (ok && ri + r < n) ? M[(int64_t)(ri + r) * lda + k0 + j] : 0.0;
-    sJ[r][j] = (ok && rj + r < n) ? M[(int64_t)(rj + r) * lda + k0 + j] : 0.0;
-  }
-  __syncthreads();
-  const int wave = tid >> 6, lane = tid & 63;
-  const int qi = (wave >> 1) * 32, qj = (wave & 1) * 32;
-  d4_t acc[2][2];
-#pragma unroll
-  for (int x = 0; x < 2; ++x)
-#pragma unroll
-    for (int y = 0; y < 2; ++y) acc[x][y] = (d4_t){0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-  for (int kk = 0; kk < NB; kk += 4) {
-    const int kc = kk + (lane >> 4);
-    double a0 = sI[qi + (lane & 15)][kc], a1 = sI[qi + 16 + (lane & 15)][kc];
-    double b0 = sJ[qj + (lane & 15)][kc], b1 = sJ[qj + 16 + (lane & 15)][kc];
-    acc[0][0] = mfma_f64(a0, b0, acc[0][0]);
-    acc[0][1] = mfma_f64(a0, b1, acc[0][1]);
-    acc[1][0] = mfma_f64(a1, b0, acc[1][0]);
-    acc[1][1] = mfma_f64(a1, b1, acc[1][1]);
-  }
-#pragma unroll
-  for (int x = 0; x < 2; ++x)
-#pragma unroll
-    for (int y = 0; y < 2; ++y)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = ri + qi + x * 16 + mf_row(lane, r);
-        const int col = rj + qj + y * 16 + mf_col(lane);
-        if (row < n && col <= row) M[(int64_t)row * lda + col] -= acc[x][y][r];
-      }
-}
-
+// Two-level blocking.  Outer panels of OB = 128 columns; inside a panel,
+// 32-wide steps (left-looking within the panel):
+//   1. A[k0:n, k0:k0+32] -= A[k0:n, K0:k0] A[k0:k0+32, K0:k0]^T   (MFMA GEMM, K <= 96)
+//   2. k_potrf_diag: L_kk and L_kk^-1
+//   3. A[k0+32:n, k0:k0+32] <- A[k0+32:n, k0:k0+32] L_kk^-T      (MFMA GEMM, K = 32, in place:
+//      one column tile per row block, every read precedes the epilogue)
+// then one trailing SYRK per outer panel, lower triangle only:
+//   A[t0:n, t0:n] -= A[t0:n, K0:t0] A[t0:n, K0:t0]^T             (MFMA GEMM, K = 128)
+// so the O(n^3) work runs as K = 128 GEMMs on v_mfma_f64_16x16x4.
+#define OB 128
 hipError_t launch_potrf_batched(hipStream_t s, int n, int batch, double *A, int64_t lda,
                                 int64_t stride, int *info, double *Linv_scratch) {
   hipError_t e = hipMemsetAsync(info, 0, sizeof(int) * batch, s);
   if (e != hipSuccess) return e;
-  for (int k0 = 0; k0 < n; k0 += NB) {
-    const int nb = min(NB, n - k0);
-    hipLaunchKernelGGL(k_potrf_diag, dim3(batch), dim3(256), 0, s, n, k0, A, lda, stride, info,
-                       Linv_scratch);
-    const int t0 = k0 + nb;
-    const int rest = n - t0;
-    if (rest <= 0) break;
-    hipLaunchKernelGGL(k_potrf_panel, dim3((rest + 63) / 64, batch), dim3(256), 0, s, n, k0, A,
-                       lda, stride, info, Linv_scratch);
-    const int nt = (rest + 63) / 64;
-    hipLaunchKernelGGL(k_syrk_mfma, dim3(nt * (nt + 1) / 2, batch), dim3(256), 0, s, n, k0, nb,
-                       t0, A, lda, stride, info);
+  auto at = [&](int r, int c) { return A + (int64_t)r * lda + c; };
+  for (int K0 = 0; K0 < n; K0 += OB) {
+    const int pw = min(OB, n - K0);
+    for (int k0 = K0; k0 < K0 + pw; k0 += NB) {
+      const int nb = min(NB, n - k0);
+      if (k0 > K0) {
+        e = launch_gemm_nt(s, EPI_STORE, n - k0, nb, k0 - K0, at(k0, K0), lda, at(k0, K0), lda,
+                           at(k0, k0), lda, -1.0, 1.0, 0, 1, batch, stride, stride, stride);
+        if (e != hipSuccess) return e;
+      }
+      hipLaunchKernelGGL(k_potrf_diag, dim3(batch), dim3(64), 0, s, n, k0, A, lda, stride, info,
+                         Linv_scratch);
+      if (k0 + nb < n) {
+        e = launch_gemm_nt(s, EPI_STORE, n - k0 - nb, nb, nb, at(k0 + nb, k0), lda, Linv_scratch,
+                           NB, at(k0 + nb, k0), lda, 1.0, 0.0, 0, 0, batch, stride,
+                           (int64_t)NB * NB, stride);
+        if (e != hipSuccess) return e;
+      }
+    }
+    const int t0 = K0 + pw;
+    if (t0 < n) {
+      e = launch_gemm_nt(s, EPI_STORE, n - t0, n - t0, pw, at(t0, K0), lda, at(t0, K0), lda,
+                         at(t0, t0), lda, -1.0, 1.0, 0, 1, batch, stride, stride, stride);
+      if (e != hipSuccess) return e;
+    }
   }
   return hipGetLastError();
 }
