@@ -129,11 +129,51 @@ def cholesky_bench(ctx, torch, n=1000, batch=64, reps=3):
     t = min(times)
     flops = batch * (n ** 3 / 3.0 + n ** 2 / 2.0 + n / 6.0)
     tf = flops / t / 1e12
-    # SYRK share: sum_k r_k^2 nb (lower, FMA = 2) with r_k = n - (k+1) nb, nb = 32
-    syrk = batch * sum(max(0, n - (k + 1) * 32) ** 2 * 32 for k in range(n // 32 + 1))
+    # SYRK = the trailing updates of the two-level blocked potrf (outer panels of
+    # 128): C[t0:n, t0:n] -= A[t0:n, K0:t0] A[t0:n, K0:t0]^T, lower, for
+    # t0 = 128, 256, ...; timed alone on the same shapes and batch.
+    shapes = [(n - t0, 128) for t0 in range(128, n, 128)]
+    syrk_flops = sum(batch * r * (r + 1) * k for r, k in shapes)   # lower incl. diagonal, FMA = 2
+    A.copy_(base)
+    torch.cuda.synchronize()
+    best = None
+    for _ in range(reps):
+        e0 = torch.cuda.Event(enable_timing=True); e1 = torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for r, k in shapes:
+            t0 = n - r
+            pa = A.data_ptr() + 8 * (t0 * n + t0 - k)
+            pc = A.data_ptr() + 8 * (t0 * n + t0)
+            _lib._chk(_lib._L.gpmpc_syrk_batched_dev(ctx.h, r, k, batch, pa, n, n * n, pc, n, n * n,
+                                                     -1e-3, 1.0), "syrk")
+        e1.record(stream)
+        ctx.sync()
+        el = e0.elapsed_time(e1) * 1e-3
+        best = el if best is None else min(best, el)
+    syrk_tf = syrk_flops / best / 1e12
+    # the FITC SYRK of BASELINE config 5: B = I + A_s A_s^T, A_s (M x N) = 2000 x 4000
+    m2, k2 = 2000, 4000
+    As = torch.randn(m2, k2, dtype=torch.float64, device=dev, generator=g) / k2 ** 0.5
+    Bm = torch.eye(m2, dtype=torch.float64, device=dev)
+    fb = None
+    for _ in range(reps):
+        e0 = torch.cuda.Event(enable_timing=True); e1 = torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        _lib._chk(_lib._L.gpmpc_syrk_batched_dev(ctx.h, m2, k2, 1, As.data_ptr(), k2, 0, Bm.data_ptr(),
+                                                 m2, 0, 1.0, 1.0), "syrk")
+        e1.record(stream)
+        ctx.sync()
+        el = e0.elapsed_time(e1) * 1e-3
+        fb = el if fb is None else min(fb, el)
+    fitc_tf = m2 * (m2 + 1) * k2 / fb / 1e12
     return dict(n=n, batch=batch, ms=round(t * 1e3, 3), tflops=round(tf, 3),
                 frac_fp64_peak=round(tf / FP64_PEAK_TFLOPS, 4),
-                syrk_gflop=round(syrk / 1e9, 2))
+                syrk_potrf={"shapes": "trailing updates (n-t0) x 128, t0 = 128..896", "gflop": round(syrk_flops / 1e9, 2),
+                            "ms": round(best * 1e3, 3), "tflops": round(syrk_tf, 3),
+                            "frac_fp64_peak": round(syrk_tf / FP64_PEAK_TFLOPS, 4)},
+                syrk_fitc={"shape": "B = I + A A^T, A 2000 x 4000 (config 5 FITC)",
+                           "gflop": round(m2 * (m2 + 1) * k2 / 1e9, 2), "ms": round(fb * 1e3, 3),
+                           "tflops": round(fitc_tf, 3), "frac_fp64_peak": round(fitc_tf / FP64_PEAK_TFLOPS, 4)})
 
 
 def main():

@@ -87,6 +87,8 @@ _sig("gpmpc_fleet_step", _c, _vp, _c)
 _sig("gpmpc_fleet_step_phases", _c, _vp, _c)
 _sig("gpmpc_fleet_set_stamps", _c, _vp, _vp)
 _sig("gpmpc_fleet_set_trace", _c, _vp, _vp)
+_sig("gpmpc_syrk_batched_dev", _c, _vp, _c, _c, _c, _vp, _c, ctypes.c_int64, _vp, _c, ctypes.c_int64,
+     ctypes.c_double, ctypes.c_double)
 _sig("gpmpc_fleet_read", _c, _vp, _dp, _dp)
 _sig("gpmpc_fleet_records_dev", _vp, _vp)
 _sig("gpmpc_fleet_destroy", _c, _vp)
@@ -99,6 +101,7 @@ EXPORTED = ["gpmpc_abi_version", "gpmpc_last_error", "gpmpc_ctx_create", "gpmpc_
             "gpmpc_qp_default_settings", "gpmpc_qp_solve_batched", "gpmpc_fleet_default_config",
             "gpmpc_fleet_create", "gpmpc_fleet_reset", "gpmpc_fleet_step", "gpmpc_fleet_read",
             "gpmpc_fleet_step_phases", "gpmpc_fleet_set_stamps", "gpmpc_fleet_set_trace",
+            "gpmpc_syrk_batched_dev",
             "gpmpc_fleet_records_dev", "gpmpc_fleet_destroy"]
 
 

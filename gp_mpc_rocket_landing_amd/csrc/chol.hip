@@ -341,3 +341,14 @@ extern "C" int gpmpc_potrs(gpmpc_ctx *ctx, int n, int nrhs, const double *L, int
                            int ldb) {
   return trsm_host(ctx, n, nrhs, L, ldl, B, ldb, 1);
 }
+
+// C (n x n, lower) = alpha A A^T + beta C for batch matrices (device pointers):
+// the trailing update of the blocked Cholesky as a standalone entry point.
+extern "C" int gpmpc_syrk_batched_dev(gpmpc_ctx *ctx, int n, int k, int batch, const double *dA,
+                                      int lda, int64_t strideA, double *dC, int ldc,
+                                      int64_t strideC, double alpha, double beta) {
+  GPMPC_CHECK_ARG(ctx && dA && dC && n >= 0 && k >= 0 && batch >= 1 && lda >= k && ldc >= n);
+  GPMPC_HIP(launch_gemm_nt(ctx->stream, EPI_STORE, n, n, k, dA, lda, dA, lda, dC, ldc, alpha, beta,
+                           0, 1, batch, strideA, strideA, strideC));
+  return 0;
+}

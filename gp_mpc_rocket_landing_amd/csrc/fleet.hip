@@ -39,9 +39,9 @@ struct gpmpc_fleet {
   unsigned long long *trace = nullptr;       // diagnostic (gpmpc_fleet_set_trace)
 };
 
-extern "C" int gpmpc_fleet_set_stamps(gpmpc_fleet *f, void *dev_u64x10) {
+extern "C" int gpmpc_fleet_set_stamps(gpmpc_fleet *f, void *dev_u64x16) {
   GPMPC_CHECK_ARG(f);
-  f->stamps = (unsigned long long *)dev_u64x10;
+  f->stamps = (unsigned long long *)dev_u64x16;
   return 0;
 }
 
@@ -432,7 +432,7 @@ extern "C" int gpmpc_fleet_create(gpmpc_ctx *ctx, gpmpc_gp *gp, const gpmpc_flee
     return -1;
   }
   const size_t B = batch, P = (size_t)batch * N;
-  const int nrt = gemm_row_tiles(g.n + 3);  // W rows + the 3 alpha^T rows
+  const int nrt = gemm_row_tiles(g.n + 3, (int)P, g.n);  // W rows + the 3 alpha^T rows
   if (f->x.alloc(sizeof(double) * B * NX) || f->Xw.alloc(sizeof(double) * B * (N + 1) * NX) ||
       f->Uw.alloc(sizeof(double) * B * N * NU) || f->ysc.alloc(sizeof(double) * B * m) ||
       f->rho.alloc(sizeof(double) * B) || f->rec.alloc(sizeof(double) * B * GPMPC_REC_LEN) ||
@@ -476,7 +476,7 @@ static hipError_t fleet_gp_posterior(gpmpc_fleet *f, int mask) {
   hipStream_t s = f->ctx->stream;
   const GpView g = gp_view(f->gp);
   const int P = f->B * f->N;
-  const int nrt = gemm_row_tiles(g.n + 3);  // W rows + the 3 alpha^T rows
+  const int nrt = gemm_row_tiles(g.n + 3, (int)P, g.n);  // W rows + the 3 alpha^T rows
   hipError_t e = hipSuccess;
   if (mask & 1) {
     hipLaunchKernelGGL(k_fleet_queries, dim3((P + 255) / 256), dim3(256), 0, s, f->B, f->N,

@@ -2,6 +2,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <cstdint>
+#include <cstdlib>
 
 enum { EPI_STORE = 0, EPI_SUMSQ = 1 };
 
@@ -23,4 +24,10 @@ hipError_t launch_gemm_sumsq_mean(hipStream_t s, int n, int n_out, int P, const 
                                   const double *Ks, double *part, int64_t ldp, double *meanT,
                                   int64_t ldm);
 
-inline int gemm_row_tiles(int M) { return (M + 63) / 64; }
+// rows of the SUMSQ partial buffer for an M x N x K product (tile height of
+// the kernel launch_gemm_* picks: 128 when M, N and K >= 256, else 64)
+inline int gemm_row_tiles(int M, int N = 0, int K = 0) {
+  const char *e = getenv("GPMPC_GEMM128");
+  const bool big = (!e || atoi(e)) && M >= 256 && N >= 256 && K >= 256;
+  return big ? (M + 127) / 128 : (M + 63) / 64;
+}

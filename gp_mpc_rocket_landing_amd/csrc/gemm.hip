@@ -164,12 +164,184 @@ __global__ __launch_bounds__(256) void k_gemm_nt(int M, int N, int K, const doub
   }
 }
 
+// ---------------------------------------------------------------------------
+// Large-tile variant: 128 x 128 per workgroup, each wave a 64 x 64 quadrant
+// (4 x 4 MFMA blocks: 8 fragment reads feed 16 MFMAs), K staged 16 at a time,
+// LDS double buffer + register prefetch, 16-byte global loads (two threads per
+// 16-double row segment).  Row tiles are dispatched longest-first when A is
+// triangular.  Used when both M and N are large (posterior GEMM, trailing SYRK).
+#define BT 128
+template <int EPI>
+__global__ __launch_bounds__(256, 2) void k_gemm128(int M, int N, int K, const double *__restrict__ A,
+                                                    int64_t lda, const double *__restrict__ B,
+                                                    int64_t ldb, double *__restrict__ C, int64_t ldc,
+                                                    double alpha, double beta, int tri_a, int lower_c,
+                                                    int64_t sA_, int64_t sB_, int64_t sC_, int msum,
+                                                    double *__restrict__ Cm, int64_t ldm, int ksplit) {
+  // grid z = batch x ksplit: split s of a matrix covers K range [s*kc, (s+1)*kc)
+  // and accumulates alpha*acc into C with fp64 atomics (beta must be 1 then)
+  const int bz = blockIdx.z / ksplit, sp = blockIdx.z % ksplit;
+  A += bz * sA_;
+  B += bz * sB_;
+  C += bz * sC_;
+  const int by = tri_a ? (int)gridDim.y - 1 - (int)blockIdx.y : (int)blockIdx.y;
+  const int r0 = by * BT, c0 = blockIdx.x * BT;
+  if (lower_c && c0 > r0 + BT - 1) return;
+  int kbeg = 0;
+  if (ksplit > 1) {
+    const int kc = ((K + ksplit - 1) / ksplit + GK - 1) / GK * GK;
+    kbeg = sp * kc;
+    if (kbeg >= K) return;
+    A += kbeg;
+    B += kbeg;
+    K = min(K - kbeg, kc);
+  }
+  __shared__ double sA[2][BT][GP];
+  __shared__ double sB[2][BT][GP];
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int qi = (wave >> 1) * 64, qj = (wave & 1) * 64;
+  int kend = K;
+  if (tri_a) kend = min(K, r0 + BT);
+  d4_t acc[4][4];
+#pragma unroll
+  for (int x = 0; x < 4; ++x)
+#pragma unroll
+    for (int y = 0; y < 4; ++y) acc[x][y] = (d4_t){0.0, 0.0, 0.0, 0.0};
+  const int lr = tid >> 1, lk = (tid & 1) * 8;
+  const bool ra = r0 + lr < M, rb = c0 + lr < N;
+  const double *pa = A + (int64_t)(ra ? r0 + lr : 0) * lda;
+  const double *pb = B + (int64_t)(rb ? c0 + lr : 0) * ldb;
+  const bool vec = ((lda | ldb) & 1) == 0 && ((((uintptr_t)A) | ((uintptr_t)B)) & 15) == 0;
+  double va[8], vb[8];
+  auto gload = [&](int k0) {
+    const int k = k0 + lk;
+    if (vec && k + 7 < kend) {
+#pragma unroll
+      for (int q = 0; q < 8; q += 2) {
+        const double2 av = ra ? *(const double2 *)(pa + k + q) : make_double2(0.0, 0.0);
+        const double2 bv = rb ? *(const double2 *)(pb + k + q) : make_double2(0.0, 0.0);
+        va[q] = av.x; va[q + 1] = av.y;
+        vb[q] = bv.x; vb[q + 1] = bv.y;
+      }
+    } else {
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        va[q] = (ra && k + q < kend) ? pa[k + q] : 0.0;
+        vb[q] = (rb && k + q < kend) ? pb[k + q] : 0.0;
+      }
+    }
+  };
+  auto lstore = [&](int buf) {
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      sA[buf][lr][lk + q] = va[q];
+      sB[buf][lr][lk + q] = vb[q];
+    }
+  };
+  gload(0);
+  lstore(0);
+  __syncthreads();
+  int cur = 0;
+  for (int k0 = 0; k0 < kend; k0 += GK) {
+    const bool more = k0 + GK < kend;
+    if (more) gload(k0 + GK);
+#pragma unroll
+    for (int kk = 0; kk < GK; kk += 4) {
+      const int kc = kk + (lane >> 4);
+      double a[4], b[4];
+#pragma unroll
+      for (int x = 0; x < 4; ++x) a[x] = sA[cur][qi + 16 * x + (lane & 15)][kc];
+#pragma unroll
+      for (int y = 0; y < 4; ++y) b[y] = sB[cur][qj + 16 * y + (lane & 15)][kc];
+#pragma unroll
+      for (int x = 0; x < 4; ++x)
+#pragma unroll
+        for (int y = 0; y < 4; ++y) acc[x][y] = mfma_f64(a[x], b[y], acc[x][y]);
+    }
+    if (more) lstore(cur ^ 1);
+    __syncthreads();
+    cur ^= 1;
+  }
+  if (EPI == EPI_STORE) {
+#pragma unroll
+    for (int x = 0; x < 4; ++x)
+#pragma unroll
+      for (int y = 0; y < 4; ++y)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = r0 + qi + x * 16 + mf_row(lane, r);
+          const int col = c0 + qj + y * 16 + mf_col(lane);
+          if (row < M && col < N && (!lower_c || col <= row)) {
+            double *p = C + (int64_t)row * ldc + col;
+            if (ksplit > 1) atomicAdd(p, alpha * acc[x][y][r]);
+            else *p = (beta == 0.0) ? alpha * acc[x][y][r] : alpha * acc[x][y][r] + beta * *p;
+          }
+        }
+  } else {
+    __shared__ double red[4][64];
+    double sq[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int x = 0; x < 4; ++x)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = r0 + qi + x * 16 + mf_row(lane, r);
+        if (row < msum) {
+#pragma unroll
+          for (int y = 0; y < 4; ++y) sq[y] = fma(acc[x][y][r], acc[x][y][r], sq[y]);
+        } else if (row < M) {
+#pragma unroll
+          for (int y = 0; y < 4; ++y) {
+            const int col = c0 + qj + y * 16 + mf_col(lane);
+            if (col < N) Cm[(int64_t)(row - msum) * ldm + col] = acc[x][y][r];
+          }
+        }
+      }
+#pragma unroll
+    for (int y = 0; y < 4; ++y) {
+      sq[y] += __shfl_xor(sq[y], 16);
+      sq[y] += __shfl_xor(sq[y], 32);
+    }
+    if (lane < 16) {
+#pragma unroll
+      for (int y = 0; y < 4; ++y) red[wave][y * 16 + lane] = sq[y];
+    }
+    __syncthreads();
+    if (tid < 128) {
+      const int half = tid >> 6, cc = tid & 63;        // column half qj = half * 64
+      const double v = red[half][cc] + red[2 + half][cc];  // waves (0, half) and (1, half)
+      const int col = c0 + tid;
+      if (col < N) C[(int64_t)by * ldc + col] = v;
+    }
+  }
+}
+
 static hipError_t launch_gemm_impl(hipStream_t s, int epi, int M, int N, int K, const double *A,
                                    int64_t lda, const double *B, int64_t ldb, double *C,
                                    int64_t ldc, double alpha, double beta, int tri_a, int lower_c,
                                    int batch, int64_t sA, int64_t sB, int64_t sC, int msum,
                                    double *Cm, int64_t ldm) {
   if (M <= 0 || N <= 0) return hipSuccess;
+  static const int big_env = [] {
+    const char *e = getenv("GPMPC_GEMM128");
+    return e ? atoi(e) : 1;
+  }();
+  if (big_env && M >= 2 * BT && N >= 2 * BT && K >= 2 * BT) {
+    const int tx = (N + BT - 1) / BT, ty = (M + BT - 1) / BT;
+    // split K when the tiles cannot give each CU ~4 workgroups to interleave (STORE
+    // with beta = 1: partial products are added atomically); >= 512 of K per split
+    const int tiles = (lower_c ? ty * (ty + 1) / 2 : tx * ty) * batch;
+    int ksplit = 1;
+    if (epi == EPI_STORE && beta == 1.0 && tiles < 1024 && K >= 1024)
+      ksplit = max(1, min((1024 + tiles - 1) / tiles, K / 512));
+    dim3 g(tx, ty, batch * ksplit);
+    if (epi == EPI_STORE)
+      hipLaunchKernelGGL(k_gemm128<EPI_STORE>, g, dim3(256), 0, s, M, N, K, A, lda, B, ldb, C, ldc,
+                         alpha, beta, tri_a, lower_c, sA, sB, sC, M, nullptr, (int64_t)0, ksplit);
+    else
+      hipLaunchKernelGGL(k_gemm128<EPI_SUMSQ>, g, dim3(256), 0, s, M, N, K, A, lda, B, ldb, C, ldc,
+                         alpha, beta, tri_a, 0, sA, sB, sC, msum, Cm, ldm, 1);
+    return hipGetLastError();
+  }
   const int tx = (N + GT - 1) / GT, ty = (M + GT - 1) / GT;
   static const int remap_env = [] {
     const char *e = getenv("GPMPC_GEMM_REMAP");

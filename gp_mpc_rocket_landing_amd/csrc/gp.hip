@@ -333,7 +333,7 @@ extern "C" int gpmpc_gp_fit_exact(gpmpc_ctx *ctx, int kind, const double *X, int
 static int core_posterior(gpmpc_ctx *ctx, const GpCore &g, const double *Ks, int p, double *dmean,
                           double *dvar) {
   hipStream_t s = ctx->stream;
-  const int nrt = gemm_row_tiles(g.n + g.n_out);
+  const int nrt = gemm_row_tiles(g.n + g.n_out, p, g.n);
   DevBuf part, meanT;
   GPMPC_HIP(part.alloc(sizeof(double) * (size_t)nrt * p));
   GPMPC_HIP(meanT.alloc(sizeof(double) * (size_t)g.n_out * p));
@@ -559,7 +559,7 @@ extern "C" int gpmpc_fitc_predict(gpmpc_ctx *ctx, gpmpc_fitc *gp, const double *
   GPMPC_HIP(hipMemcpyAsync(dq.p, Xq, sizeof(double) * p * g.d, hipMemcpyHostToDevice, s));
   int rc = core_cross(ctx, g, dq.as<double>(), p, Ks);  // K*u (p x m)
   if (rc) return rc;
-  const int nrt = gemm_row_tiles(m);
+  const int nrt = gemm_row_tiles(m, p, m);
   GPMPC_HIP(V.alloc(sizeof(double) * (size_t)p * m));
   GPMPC_HIP(pv.alloc(sizeof(double) * (size_t)nrt * p));
   GPMPC_HIP(pw.alloc(sizeof(double) * (size_t)nrt * p));

@@ -22,7 +22,7 @@
 // Storage (doubles, in the factor area of QPSmem), block stride
 // BS = SZ*SZ + SZ*CM:
 //   [k*BS, +SZ*SZ)       S_k^-1  column-major (symmetric)   slot j*SZ + r = S^-1[r][j]
-//   [k*BS + SZ*SZ, +SZ*CM) G_k   column-major               slot j*CM + r = G_k[r][j]
+//   [k*BS + SZ*SZ, +SZ*CM) -G_k  column-major               slot j*CM + r = -G_k[r][j]
 // (before factoring the same slots hold M_kk and C_k; a last block shorter
 // than SZ is padded with identity rows by the host).
 #pragma once
@@ -71,6 +71,35 @@ __device__ __forceinline__ double dot_bc(double src, const double *mul, std::int
   double a0 = 0.0, a1 = 0.0;
   ((J % 2 == 0 ? fmac_bc<J, J == 0>(a0, src, mul[J]) : fmac_bc<J, false>(a1, src, mul[J])), ...);
   return a0 + a1;
+}
+// init + sum_j mul[j] * bcast_j(src)
+template <int... J>
+__device__ __forceinline__ double dot_bc_init(double init, double src, const double *mul,
+                                              std::integer_sequence<int, J...>) {
+  double a0 = init, a1 = 0.0;
+  ((J % 2 == 0 ? fmac_bc<J, J == 0>(a0, src, mul[J]) : fmac_bc<J, false>(a1, src, mul[J])), ...);
+  return a0 + a1;
+}
+template <int K>
+__device__ __forceinline__ double dot_bc_init(double init, double src, const double *mul) {
+  return dot_bc_init(init, src, mul, std::make_integer_sequence<int, K>{});
+}
+// two products of the same broadcast source, interleaved (4 accumulators):
+//   r0 = init0 + sum_j m0[j] bcast_j(src),  r1 = sum_j m1[j] bcast_j(src)
+template <int... J>
+__device__ __forceinline__ void dot2_bc(double init0, double src, const double *m0,
+                                        const double *m1, double &r0, double &r1,
+                                        std::integer_sequence<int, J...>) {
+  double a0 = init0, a1 = 0.0, c0 = 0.0, c1 = 0.0;
+  ((J % 2 == 0 ? (fmac_bc<J, J == 0>(a0, src, m0[J]), fmac_bc<J, false>(c0, src, m1[J]))
+               : (fmac_bc<J, false>(a1, src, m0[J]), fmac_bc<J, false>(c1, src, m1[J]))), ...);
+  r0 = a0 + a1;
+  r1 = c0 + c1;
+}
+template <int K>
+__device__ __forceinline__ void dot2_bc(double init0, double src, const double *m0, const double *m1,
+                                        double &r0, double &r1) {
+  dot2_bc(init0, src, m0, m1, r0, r1, std::make_integer_sequence<int, K>{});
 }
 // same with compiler-visible DPP moves (2 VALU per term, exact waitcnts)
 template <int... J>
@@ -141,9 +170,9 @@ __device__ int blk_factor(const QPPattern &pt, S &s) {
 #pragma unroll
         for (int j = 0; j < SZ; ++j) g[j] = fma(c[l], bc16_rt(a[j], l), g[j]);
       }
-      if (wr && rr < CM) {
+      if (wr && rr < CM) {  // stored negated: the solve's chains accumulate into b / u
 #pragma unroll
-        for (int j = 0; j < SZ; ++j) Ck[j * CM + rr] = g[j];
+        for (int j = 0; j < SZ; ++j) Ck[j * CM + rr] = -g[j];
       }
       // u[rr][i] = sum_j G[rr][j] C[i][j]
 #pragma unroll
@@ -167,9 +196,10 @@ __device__ int blk_factor(const QPPattern &pt, S &s) {
 // stores are masked.  Per-lane pointers advance by constants; operands sit at
 // immediate offsets.
 template <int SZ, int CM, class S>
-__device__ void blk_solve(const QPPattern &pt, S &s, double *b) {
+__device__ void blk_solve(const QPPattern &pt, S &s, double *b, QPStamps *T = nullptr) {
   if (threadIdx.x >= 64) return;
   constexpr int BS = SZ * SZ + SZ * CM;
+  static_assert(BS + SZ * CM <= sizeof(s.gzero) / sizeof(double), "gzero too small");
   const int lane = threadIdx.x, rr = lane & 15, row = lane >> 4;
   const int rs = rr < SZ ? rr : SZ - 1, rc = rr < CM ? rr : CM - 1;
   const bool wr = rr < SZ;
@@ -184,111 +214,107 @@ __device__ void blk_solve(const QPPattern &pt, S &s, double *b) {
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
     return;
   }
-  // ---- forward: y_{k+1} = b_{k+1} - G_k y_k on the first CM rows of block k+1
+  // ---- forward + diagonal in one pass over the blocks:
+  //        y_{k+1} = b_{k+1} + (-G_k) y_k     (first CM rows of block k+1)
+  //        u_k     = S_k^-1 y_k               (stored over b_k)
+  //      both products broadcast the same y_k, so their two FMA chains
+  //      interleave.  Lanes rr >= CM read their "-G row" from a zero region
+  //      (their y is exactly b); lanes rr >= SZ compute bit-identical values
+  //      to lane SZ-1 (same clamped inputs), so every store is unconditional.
   {
     double *pb = b + rs;                          // block k of b
-    const double *pg = F + SZ * SZ + rc;          // G_k row rc
+    const bool cpl = rr < CM;
+    const double *pg = cpl ? F + SZ * SZ + rc : s.gzero;   // -G_k row rc
+    const int gstep = cpl ? BS : 0;
+    const double *ps = F + rs;                    // S_k^-1 row rs: ps[k*BS + j*SZ]
     double y = pb[0];
-    double gA[SZ], gB[SZ];
+    double gA[SZ], gB[SZ], sA[SZ], sB[SZ];
+    double bA = pb[SZ], bB;                       // b_{k+1}: the next accumulator's start
 #pragma unroll
-    for (int j = 0; j < SZ; ++j) gA[j] = pg[j * CM];
+    for (int j = 0; j < SZ; ++j) {
+      gA[j] = pg[j * CM];
+      sA[j] = ps[j * SZ];
+    }
     for (int k = 0;;) {
       {
-        const double bn = pb[SZ];
+        bB = pb[2 * SZ];                           // b_{k+2} (past the end: unused)
 #pragma unroll
-        for (int j = 0; j < SZ; ++j) gB[j] = pg[BS + j * CM];  // G_{k+1} (past the end: unused)
-        const double acc = dot_bc<SZ>(y, gA);
-        if (wr) pb[0] = y;
-        y = (rr < CM) ? bn - acc : bn;
+        for (int j = 0; j < SZ; ++j) {
+          gB[j] = pg[gstep + j * CM];              // -G_{k+1} (past the end: unused)
+          sB[j] = ps[BS + j * SZ];                 // S_{k+1}^-1
+        }
+        double yn, u;
+        dot2_bc<SZ>(bA, y, gA, sA, yn, u);
+        pb[0] = u;
+        y = yn;
         pb += SZ;
-        pg += BS;
+        pg += gstep;
+        ps += BS;
         if (++k >= nblk - 1) break;
       }
       {
-        const double bn = pb[SZ];
+        bA = pb[2 * SZ];
 #pragma unroll
-        for (int j = 0; j < SZ; ++j) gA[j] = pg[BS + j * CM];
-        const double acc = dot_bc<SZ>(y, gB);
-        if (wr) pb[0] = y;
-        y = (rr < CM) ? bn - acc : bn;
+        for (int j = 0; j < SZ; ++j) {
+          gA[j] = pg[gstep + j * CM];
+          sA[j] = ps[BS + j * SZ];
+        }
+        double yn, u;
+        dot2_bc<SZ>(bB, y, gB, sB, yn, u);
+        pb[0] = u;
+        y = yn;
         pb += SZ;
-        pg += BS;
+        pg += gstep;
+        ps += BS;
         if (++k >= nblk - 1) break;
       }
     }
-    if (wr) pb[0] = y;
+    // last block: u = S^-1 y (its operands were prefetched into whichever buffer is current)
+    double sl[SZ];
+#pragma unroll
+    for (int j = 0; j < SZ; ++j) sl[j] = ps[j * SZ];
+    pb[0] = dot_bc<SZ>(y, sl);
   }
   __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-  // ---- diagonal blocks, four at a time (one per DPP row): u_k = S_k^-1 y_k
-  {
-    const int nr = (nblk + 3) >> 2;
-    double *pb = b + row * SZ + rs;
-    const double *ps = F + row * BS + rs;
-    double sA[SZ], sB[SZ];
-#pragma unroll
-    for (int j = 0; j < SZ; ++j) sA[j] = ps[j * SZ];
-    double yA = pb[0];
-    for (int t = 0;;) {
-      {
-#pragma unroll
-        for (int j = 0; j < SZ; ++j) sB[j] = ps[4 * BS + j * SZ];  // next round (past the end: unused)
-        const double yB = pb[4 * SZ];
-        const double uv = dot_bc<SZ>(yA, sA);
-        if (wr && t * 4 + row < nblk) pb[0] = uv;
-        yA = yB;
-        pb += 4 * SZ;
-        ps += 4 * BS;
-        if (++t >= nr) break;
-      }
-      {
-#pragma unroll
-        for (int j = 0; j < SZ; ++j) sA[j] = ps[4 * BS + j * SZ];
-        const double yB = pb[4 * SZ];
-        const double uv = dot_bc<SZ>(yA, sB);
-        if (wr && t * 4 + row < nblk) pb[0] = uv;
-        yA = yB;
-        pb += 4 * SZ;
-        ps += 4 * BS;
-        if (++t >= nr) break;
-      }
-    }
-  }
-  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-  // ---- backward: x_k = u_k - G_k^T x_{k+1}
+  if (T) T->mark(8);
+  if (T) T->mark(9);
+  // ---- backward: x_k = u_k + (-G_k)^T x_{k+1}
   {
     double *pb = b + (nblk - 1) * SZ + rs;        // block k+1 of b
-    const double *pg = F + (nblk - 2) * BS + SZ * SZ + rs * CM;  // G_k column rs
+    const double *pg = F + (nblk - 2) * BS + SZ * SZ + rs * CM;  // -G_k column rs
     double x = pb[0];
     double gA[CM], gB[CM];
+    double uA = pb[-SZ], uB;                      // u_k: the next accumulator's start
 #pragma unroll
     for (int i = 0; i < CM; ++i) gA[i] = pg[i];
     for (int k = nblk - 2;;) {
       {
-        const double un = pb[-SZ];
+        uB = pb[-2 * SZ];                          // u_{k-1} (before the start: unused)
 #pragma unroll
-        for (int i = 0; i < CM; ++i) gB[i] = pg[i - BS];  // G_{k-1} (before the start: unused)
-        const double acc = dot_bc<CM>(x, gA);
-        if (wr) pb[0] = x;
-        x = un - acc;
+        for (int i = 0; i < CM; ++i) gB[i] = pg[i - BS];  // -G_{k-1} (before the start: unused)
+        const double xn = dot_bc_init<CM>(uA, x, gA);
+        pb[0] = x;
+        x = xn;
         pb -= SZ;
         pg -= BS;
         if (--k < 0) break;
       }
       {
-        const double un = pb[-SZ];
+        uA = pb[-2 * SZ];
 #pragma unroll
         for (int i = 0; i < CM; ++i) gA[i] = pg[i - BS];
-        const double acc = dot_bc<CM>(x, gB);
-        if (wr) pb[0] = x;
-        x = un - acc;
+        const double xn = dot_bc_init<CM>(uB, x, gB);
+        pb[0] = x;
+        x = xn;
         pb -= SZ;
         pg -= BS;
         if (--k < 0) break;
       }
     }
-    if (wr) pb[0] = x;
+    pb[0] = x;
   }
   __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+  if (T) T->mark(10);
 }
 
 // the compiled (SZ, CM) instantiations; the host only selects mode 1 for these
@@ -300,6 +326,6 @@ __device__ int blk_factor_dispatch(const QPPattern &pt, S &s) {
   return blk_factor<QP_BLK_SZ, QP_BLK_CM>(pt, s);
 }
 template <class S>
-__device__ void blk_solve_dispatch(const QPPattern &pt, S &s, double *b) {
-  blk_solve<QP_BLK_SZ, QP_BLK_CM>(pt, s, b);
+__device__ void blk_solve_dispatch(const QPPattern &pt, S &s, double *b, QPStamps *T = nullptr) {
+  blk_solve<QP_BLK_SZ, QP_BLK_CM>(pt, s, b, T);
 }

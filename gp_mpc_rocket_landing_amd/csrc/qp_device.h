@@ -67,6 +67,7 @@ struct QPSmem {
   double band_store[NMAX * (W + 1) + 4 * (W + 1) + 64];
   double red[4][8];
   double zslot, sink;  // block solve: a 0.0 source and a write sink for idle lanes
+  double gzero[240];   // block solve: zero "-G rows" of non-coupled lanes (>= BS + SZ*CM)
   double c, rho_s;
   int flag;
 };
@@ -235,6 +236,7 @@ __device__ int qp_factor(const QPPattern &pt, S &s, double sigma) {
   }
   if (pt.mode == 1) {
     if (tid == 0) s.zslot = 0.0;
+    for (int e = tid; e < (int)(sizeof(s.gzero) / sizeof(double)); e += nt) s.gzero[e] = 0.0;
     __syncthreads();
     int f = 0;
     if (tid < 64) f = blk_factor_dispatch(pt, s);
@@ -398,6 +400,33 @@ __device__ void qp_band_solve(const QPPattern &pt, S &s, double *b) {
   __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
 }
 
+// diagnostic phase stamps (s_memtime), thread 0 only, enabled by a non-null pointer
+struct QPStamps {
+  unsigned long long *out = nullptr;
+  unsigned long long acc[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+  unsigned long long last = 0, first = 0, rt0 = 0;
+  __device__ void start() {
+    if (out && threadIdx.x == 0) {
+      last = first = __builtin_amdgcn_s_memtime();
+      rt0 = __builtin_amdgcn_s_memrealtime();
+    }
+  }
+  __device__ void mark(int k) {
+    if (out && threadIdx.x == 0) {
+      const unsigned long long t = __builtin_amdgcn_s_memtime();
+      acc[k] += t - last;
+      last = t;
+    }
+  }
+  __device__ void flush() {
+    if (out && threadIdx.x == 0) {
+      for (int k = 0; k < 12; ++k) out[k] += acc[k];
+      out[14] += __builtin_amdgcn_s_memrealtime() - rt0;  // 100 MHz constant clock
+      out[15] += last - first;                            // shader clock
+    }
+  }
+};
+
 #include "qp_block.h"
 
 // residuals (auxil.c update_info): tmpm <- A x, aux <- P x, tmpn <- A' y.
@@ -532,33 +561,6 @@ __device__ double qp_rho_estimate(const QPPattern &pt, S &s) {
   return fmin(fmax(est, QP_RHO_MIN), QP_RHO_MAX);
 }
 
-// diagnostic phase stamps (s_memtime), thread 0 only, enabled by a non-null pointer
-struct QPStamps {
-  unsigned long long *out = nullptr;
-  unsigned long long acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  unsigned long long last = 0, first = 0, rt0 = 0;
-  __device__ void start() {
-    if (out && threadIdx.x == 0) {
-      last = first = __builtin_amdgcn_s_memtime();
-      rt0 = __builtin_amdgcn_s_memrealtime();
-    }
-  }
-  __device__ void mark(int k) {
-    if (out && threadIdx.x == 0) {
-      const unsigned long long t = __builtin_amdgcn_s_memtime();
-      acc[k] += t - last;
-      last = t;
-    }
-  }
-  __device__ void flush() {
-    if (out && threadIdx.x == 0) {
-      for (int k = 0; k < 8; ++k) out[k] += acc[k];
-      out[8] += __builtin_amdgcn_s_memrealtime() - rt0;  // 100 MHz constant clock
-      out[9] += last - first;                           // shader clock
-    }
-  }
-};
-
 struct QPResult {
   int status, iter;
   double obj;
@@ -643,7 +645,7 @@ __device__ QPResult qp_solve(const QPPattern &pt, S &s, const QPSettingsDev &st,
     }
     __syncthreads();
     T.mark(3);
-    if (pt.mode == 1) blk_solve_dispatch(pt, s, s.rhs);  // x~
+    if (pt.mode == 1) blk_solve_dispatch(pt, s, s.rhs, &T);  // x~
     else qp_band_solve(pt, s, s.rhs);
     __syncthreads();
     T.mark(4);

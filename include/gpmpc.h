@@ -70,6 +70,12 @@ int gpmpc_potrf(gpmpc_ctx *ctx, int n, double *A, int lda, int *info);
  * dinfo: device int[batch]. */
 int gpmpc_potrf_batched_dev(gpmpc_ctx *ctx, int n, int batch, double *dA, int lda, int64_t stride,
                             int *dinfo);
+/* C = alpha A A^T + beta C on the lower triangle (dsyrk 'L','N') for batch
+ * device matrices: A (n x k, lda), C (n x n, ldc); the trailing update of the
+ * blocked potrf (FP64 MFMA). */
+int gpmpc_syrk_batched_dev(gpmpc_ctx *ctx, int n, int k, int batch, const double *dA, int lda,
+                           int64_t strideA, double *dC, int ldc, int64_t strideC, double alpha,
+                           double beta);
 /* Replaces scipy.linalg.solve_triangular(L, B, lower=True) (exact_gp.py:251,260;
  * sparse_gp.py:190,293,296): B (n x nrhs) overwritten by L^-1 B. */
 int gpmpc_trsm_lower(gpmpc_ctx *ctx, int n, int nrhs, const double *L, int ldl, double *B, int ldb);
@@ -176,11 +182,13 @@ int gpmpc_fleet_step_phases(gpmpc_fleet *f, int phase_mask);
 #define GPMPC_REC_LEN 16
 int gpmpc_fleet_read(gpmpc_fleet *f, double *records, double *x /* batch x 7, may be NULL */);
 /* diagnostic: accumulate s_memtime cycles of landing 0's control kernel per
- * phase into dev_u64x10 (10 x uint64 device buffer; NULL disables):
- * 0 assembly, 1 scaling, 2 factor, 3 A' rhs, 4 band sweeps, 5 fused z/y update,
- * 6 checks + adaptive rho, 7 tail (plant step, records); 8 s_memrealtime
- * ticks (100 MHz) and 9 shader-clock ticks over the same solves */
-int gpmpc_fleet_set_stamps(gpmpc_fleet *f, void *dev_u64x10);
+ * phase into dev_u64x16 (16 x uint64 device buffer; NULL disables):
+ * 0 assembly, 1 scaling, 2 factor, 3 A' rhs, 4 KKT solve (band path, or the
+ * block path's barrier tail), 5 fused z/y update, 6 checks + adaptive rho,
+ * 7 tail (plant step, records), 8/9/10 block KKT solve forward / diagonal /
+ * backward; 14 s_memrealtime ticks (100 MHz) and 15 shader-clock ticks over
+ * the same solves */
+int gpmpc_fleet_set_stamps(gpmpc_fleet *f, void *dev_u64x16);
 /* diagnostic: per-landing control-kernel trace into dev_u64xbx4 (batch x 4
  * uint64 device buffer; NULL disables): start and end s_memrealtime (100 MHz),
  * HW_ID and XCC_ID of the landing's first wave */

@@ -162,3 +162,23 @@ def test_fleet_runs_and_is_deterministic(gpu_ctx):
     r2 = fleet.run_fleet(gpu_ctx, 8, steps=30)
     np.testing.assert_array_equal(r1["records"], r2["records"])
     assert np.all(r1["records"][:, 1] > 0)
+
+
+@pytest.mark.parametrize("n,k,batch", [(100, 40, 3), (512, 512, 2), (300, 4096, 1)])
+def test_syrk_batched_paths(gpu_ctx, n, k, batch):
+    """C = I - A A^T (lower) through the 64-tile, 128-tile and split-K (fp64 atomics) GEMM paths."""
+    import torch
+    L = _lib()
+    g = torch.Generator(device="cuda").manual_seed(n + k)
+    A = torch.randn(batch, n, k, dtype=torch.float64, device="cuda", generator=g) / k ** 0.5
+    C = torch.eye(n, dtype=torch.float64, device="cuda").repeat(batch, 1, 1).contiguous()
+    rc = L._L.gpmpc_syrk_batched_dev(gpu_ctx.h, n, k, batch, A.data_ptr(), k, n * k, C.data_ptr(), n,
+                                     n * n, -1.0, 1.0)
+    assert rc == 0
+    gpu_ctx.sync()
+    ref = torch.eye(n, dtype=torch.float64, device="cuda") - A @ A.transpose(1, 2)
+    low = torch.tril(torch.ones(n, n, dtype=torch.bool, device="cuda"))
+    err = (C - ref).abs()[:, low].max().item()
+    assert err < 1e-12 * k, err
+    # the strict upper triangle is untouched
+    assert torch.equal(C[:, ~low], torch.zeros_like(C[:, ~low]))
