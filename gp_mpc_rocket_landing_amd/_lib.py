@@ -26,6 +26,28 @@ if not os.path.exists(LIB_PATH):
     raise ImportError(f"HIP library missing: {LIB_PATH} (build it with __graft_entry__.build(); "
                       "there is no CPU fallback)")
 
+
+def _share_torch_hip_runtime():
+    """Make this process use ONE HIP runtime.  torch bundles its own
+    libamdhip64 (SONAME libamdhip64.so.7, loaded by the unversioned name from
+    torch/lib).  If our library pulled /opt/rocm's copy in first, torch would
+    later load a second runtime, and whichever initialises second sees no
+    device.  Preloading torch's copy globally lets our NEEDED libamdhip64.so.7
+    resolve to it (GPMPC_HIP_RUNTIME=system keeps /opt/rocm's instead)."""
+    if os.environ.get("GPMPC_HIP_RUNTIME", "") == "system":
+        return
+    import importlib.util
+    spec = importlib.util.find_spec("torch")
+    if spec is None or not spec.origin:
+        return
+    tlib = os.path.join(os.path.dirname(spec.origin), "lib")
+    for name in ("libhsa-runtime64.so", "libamdhip64.so"):
+        p = os.path.join(tlib, name)
+        if os.path.exists(p):
+            ctypes.CDLL(p, mode=ctypes.RTLD_GLOBAL)
+
+
+_share_torch_hip_runtime()
 _L = ctypes.CDLL(LIB_PATH)
 _dp = ctypes.POINTER(ctypes.c_double)
 _ip = ctypes.POINTER(ctypes.c_int)

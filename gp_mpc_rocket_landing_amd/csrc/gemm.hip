@@ -12,6 +12,7 @@
 // Tile 64 x 64 per 256-thread workgroup, each wave a 32 x 32 quadrant
 // (2 x 2 MFMA blocks), K staged 16 at a time through LDS with an 18-double
 // pitch (conflict-free ds_read_b64 for the 16-row x 4-k operand gathers).
+#include <algorithm>
 #include <cstdlib>
 #include "internal.h"
 #include "mfma64.h"
@@ -21,6 +22,15 @@
 #define GK 16
 #define GP 18
 
+// lower-triangular tile t -> (row tile ti, col tile tj), tj <= ti
+__device__ __forceinline__ void tri_tile(int t, int &ti, int &tj) {
+  int i = (int)((sqrt(8.0 * t + 1.0) - 1.0) * 0.5);
+  while ((i + 1) * (i + 2) / 2 <= t) ++i;
+  while (i * (i + 1) / 2 > t) --i;
+  ti = i;
+  tj = t - i * (i + 1) / 2;
+}
+
 template <int EPI>
 __global__ __launch_bounds__(256) void k_gemm_nt(int M, int N, int K, const double *__restrict__ A,
                                                  int64_t lda, const double *__restrict__ B,
@@ -28,8 +38,19 @@ __global__ __launch_bounds__(256) void k_gemm_nt(int M, int N, int K, const doub
                                                  double alpha, double beta, int tri_a,
                                                  int lower_c, int64_t sA_, int64_t sB_,
                                                  int64_t sC_, int msum, double *__restrict__ Cm,
-                                                 int64_t ldm, int remap_ty) {
-  const int bz = blockIdx.z;
+                                                 int64_t ldm, int remap_ty, int xcd_batch) {
+  int bz = blockIdx.z;
+  int bx = blockIdx.x, by = blockIdx.y;
+  if (xcd_batch) {
+    // lower-triangular batch, one matrix per XCD at a time: workgroup i runs
+    // on XCD i % 8, so matrix b's tiles all land on XCD b % 8 and its row and
+    // column panels are re-read from that XCD's L2 instead of crossing all 8
+    const int T = ((M + GT - 1) / GT) * ((M + GT - 1) / GT + 1) / 2;
+    const int i = blockIdx.x, slot = i >> 3;
+    bz = (i & 7) + 8 * (slot / T);
+    if (bz >= xcd_batch) return;
+    tri_tile(slot % T, by, bx);
+  }
   A += bz * sA_;
   B += bz * sB_;
   C += bz * sC_;
@@ -38,11 +59,13 @@ __global__ __launch_bounds__(256) void k_gemm_nt(int M, int N, int K, const doub
   // back to back.  Off by default: for the posterior GEMM the plain order
   // (concurrent workgroups share a W row block, K* streams from the 256 MB
   // Infinity Cache) measured 0.46 ms vs 0.54 ms with the remap.
-  int bx = blockIdx.x, by = blockIdx.y;
-  if (remap_ty) {
+  if (xcd_batch) {
+  } else if (remap_ty > 0) {
     const int i = blockIdx.x, slot = i >> 3;
     bx = (i & 7) + 8 * (slot / remap_ty);
     by = slot % remap_ty;
+  } else if (remap_ty < 0) {  // 1-D grid over the lower-triangular tiles only
+    tri_tile(blockIdx.x, by, bx);
   }
   const int r0 = by * GT, c0 = bx * GT;
   if (lower_c && c0 > r0 + GT - 1) return;
@@ -171,38 +194,16 @@ __global__ __launch_bounds__(256) void k_gemm_nt(int M, int N, int K, const doub
 // 16-double row segment).  Row tiles are dispatched longest-first when A is
 // triangular.  Used when both M and N are large (posterior GEMM, trailing SYRK).
 #define BT 128
-template <int EPI>
-__global__ __launch_bounds__(256, 2) void k_gemm128(int M, int N, int K, const double *__restrict__ A,
-                                                    int64_t lda, const double *__restrict__ B,
-                                                    int64_t ldb, double *__restrict__ C, int64_t ldc,
-                                                    double alpha, double beta, int tri_a, int lower_c,
-                                                    int64_t sA_, int64_t sB_, int64_t sC_, int msum,
-                                                    double *__restrict__ Cm, int64_t ldm, int ksplit) {
-  // grid z = batch x ksplit: split s of a matrix covers K range [s*kc, (s+1)*kc)
-  // and accumulates alpha*acc into C with fp64 atomics (beta must be 1 then)
-  const int bz = blockIdx.z / ksplit, sp = blockIdx.z % ksplit;
-  A += bz * sA_;
-  B += bz * sB_;
-  C += bz * sC_;
-  const int by = tri_a ? (int)gridDim.y - 1 - (int)blockIdx.y : (int)blockIdx.y;
-  const int r0 = by * BT, c0 = blockIdx.x * BT;
-  if (lower_c && c0 > r0 + BT - 1) return;
-  int kbeg = 0;
-  if (ksplit > 1) {
-    const int kc = ((K + ksplit - 1) / ksplit + GK - 1) / GK * GK;
-    kbeg = sp * kc;
-    if (kbeg >= K) return;
-    A += kbeg;
-    B += kbeg;
-    K = min(K - kbeg, kc);
-  }
-  __shared__ double sA[2][BT][GP];
-  __shared__ double sB[2][BT][GP];
+// acc = A[r0.., k_lo:k_hi] B[c0.., k_lo:k_hi]^T for one 128 x 128 tile (wave w
+// owns quadrant (w/2, w%2)); k_lo must be a multiple of GK.  Ends on a barrier,
+// so the LDS can be reused by the caller straight away.
+__device__ __forceinline__ void mma128_tile(const double *__restrict__ A, int64_t lda,
+                                            const double *__restrict__ B, int64_t ldb, int M, int N,
+                                            int r0, int c0, int k_lo, int k_hi,
+                                            double (*sA)[BT][GP], double (*sB)[BT][GP],
+                                            d4_t (&acc)[4][4]) {
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int qi = (wave >> 1) * 64, qj = (wave & 1) * 64;
-  int kend = K;
-  if (tri_a) kend = min(K, r0 + BT);
-  d4_t acc[4][4];
 #pragma unroll
   for (int x = 0; x < 4; ++x)
 #pragma unroll
@@ -215,7 +216,7 @@ __global__ __launch_bounds__(256, 2) void k_gemm128(int M, int N, int K, const d
   double va[8], vb[8];
   auto gload = [&](int k0) {
     const int k = k0 + lk;
-    if (vec && k + 7 < kend) {
+    if (vec && k + 7 < k_hi) {
 #pragma unroll
       for (int q = 0; q < 8; q += 2) {
         const double2 av = ra ? *(const double2 *)(pa + k + q) : make_double2(0.0, 0.0);
@@ -226,8 +227,8 @@ __global__ __launch_bounds__(256, 2) void k_gemm128(int M, int N, int K, const d
     } else {
 #pragma unroll
       for (int q = 0; q < 8; ++q) {
-        va[q] = (ra && k + q < kend) ? pa[k + q] : 0.0;
-        vb[q] = (rb && k + q < kend) ? pb[k + q] : 0.0;
+        va[q] = (ra && k + q < k_hi) ? pa[k + q] : 0.0;
+        vb[q] = (rb && k + q < k_hi) ? pb[k + q] : 0.0;
       }
     }
   };
@@ -238,12 +239,12 @@ __global__ __launch_bounds__(256, 2) void k_gemm128(int M, int N, int K, const d
       sB[buf][lr][lk + q] = vb[q];
     }
   };
-  gload(0);
+  gload(k_lo);
   lstore(0);
   __syncthreads();
   int cur = 0;
-  for (int k0 = 0; k0 < kend; k0 += GK) {
-    const bool more = k0 + GK < kend;
+  for (int k0 = k_lo; k0 < k_hi; k0 += GK) {
+    const bool more = k0 + GK < k_hi;
     if (more) gload(k0 + GK);
 #pragma unroll
     for (int kk = 0; kk < GK; kk += 4) {
@@ -262,6 +263,43 @@ __global__ __launch_bounds__(256, 2) void k_gemm128(int M, int N, int K, const d
     __syncthreads();
     cur ^= 1;
   }
+}
+
+template <int EPI>
+__global__ __launch_bounds__(256, 2) void k_gemm128(int M, int N, int K, const double *__restrict__ A,
+                                                    int64_t lda, const double *__restrict__ B,
+                                                    int64_t ldb, double *__restrict__ C, int64_t ldc,
+                                                    double alpha, double beta, int tri_a, int lower_c,
+                                                    int64_t sA_, int64_t sB_, int64_t sC_, int msum,
+                                                    double *__restrict__ Cm, int64_t ldm, int ksplit,
+                                                    int tri_grid) {
+  // grid z = batch x ksplit: split s of a matrix covers K range [s*kc, (s+1)*kc)
+  // and accumulates alpha*acc into C with fp64 atomics (beta must be 1 then)
+  const int bz = blockIdx.z / ksplit, sp = blockIdx.z % ksplit;
+  A += bz * sA_;
+  B += bz * sB_;
+  C += bz * sC_;
+  int by = tri_a ? (int)gridDim.y - 1 - (int)blockIdx.y : (int)blockIdx.y, bx = blockIdx.x;
+  if (tri_grid) tri_tile(blockIdx.x, by, bx);  // 1-D grid over the lower-triangular tiles
+  const int r0 = by * BT, c0 = bx * BT;
+  if (lower_c && c0 > r0 + BT - 1) return;
+  int kbeg = 0;
+  if (ksplit > 1) {
+    const int kc = ((K + ksplit - 1) / ksplit + GK - 1) / GK * GK;
+    kbeg = sp * kc;
+    if (kbeg >= K) return;
+    A += kbeg;
+    B += kbeg;
+    K = min(K - kbeg, kc);
+  }
+  __shared__ double sA[2][BT][GP];
+  __shared__ double sB[2][BT][GP];
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int qi = (wave >> 1) * 64, qj = (wave & 1) * 64;
+  int kend = K;
+  if (tri_a) kend = min(K, r0 + BT);
+  d4_t acc[4][4];
+  mma128_tile(A, lda, B, ldb, M, N, r0, c0, 0, kend, sA, sB, acc);
   if (EPI == EPI_STORE) {
 #pragma unroll
     for (int x = 0; x < 4; ++x)
@@ -315,6 +353,54 @@ __global__ __launch_bounds__(256, 2) void k_gemm128(int M, int N, int K, const d
   }
 }
 
+
+// Stream-K (C += alpha A B^T, STORE epilogue with beta = 1): the batch's
+// (tile, K-step) units are cut into gridDim.x equal contiguous ranges, one per
+// workgroup, so every resident slot does the same work whatever the tile count
+// (no quantisation tail); each tile segment is added into C with fp64 atomics.
+// Tiles are lower-triangular (tri) or the full tx x ty grid.
+__global__ __launch_bounds__(256, 2) void k_gemm128_sk(int M, int N, int K,
+                                                       const double *__restrict__ A, int64_t lda,
+                                                       const double *__restrict__ B, int64_t ldb,
+                                                       double *__restrict__ C, int64_t ldc,
+                                                       double alpha, int tri, int tx, int T,
+                                                       int64_t sA_, int64_t sB_, int64_t sC_,
+                                                       int64_t total) {
+  __shared__ double sA[2][BT][GP];
+  __shared__ double sB[2][BT][GP];
+  const int kiters = (K + GK - 1) / GK;
+  int64_t u = (int64_t)blockIdx.x * total / gridDim.x;
+  const int64_t u1 = (int64_t)(blockIdx.x + 1) * total / gridDim.x;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int qi = (wave >> 1) * 64, qj = (wave & 1) * 64;
+  while (u < u1) {
+    const int64_t g = u / kiters;
+    const int j0 = (int)(u - g * kiters);
+    const int j1 = (int)min((int64_t)kiters, (int64_t)j0 + (u1 - u));
+    const int bz = (int)(g / T), t = (int)(g % T);
+    int by, bx;
+    if (tri) tri_tile(t, by, bx);
+    else by = t / tx, bx = t % tx;
+    const int r0 = by * BT, c0 = bx * BT;
+    d4_t acc[4][4];
+    mma128_tile(A + bz * sA_, lda, B + bz * sB_, ldb, M, N, r0, c0, j0 * GK, min(K, j1 * GK), sA,
+                sB, acc);
+    double *Cb = C + bz * sC_;
+#pragma unroll
+    for (int x = 0; x < 4; ++x)
+#pragma unroll
+      for (int y = 0; y < 4; ++y)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = r0 + qi + x * 16 + mf_row(lane, r);
+          const int col = c0 + qj + y * 16 + mf_col(lane);
+          if (row < M && col < N && (!tri || col <= row))
+            atomicAdd(Cb + (int64_t)row * ldc + col, alpha * acc[x][y][r]);
+        }
+    u += j1 - j0;
+  }
+}
+
 static hipError_t launch_gemm_impl(hipStream_t s, int epi, int M, int N, int K, const double *A,
                                    int64_t lda, const double *B, int64_t ldb, double *C,
                                    int64_t ldc, double alpha, double beta, int tri_a, int lower_c,
@@ -325,21 +411,63 @@ static hipError_t launch_gemm_impl(hipStream_t s, int epi, int M, int N, int K, 
     const char *e = getenv("GPMPC_GEMM128");
     return e ? atoi(e) : 1;
   }();
-  if (big_env && M >= 2 * BT && N >= 2 * BT && K >= 2 * BT) {
+  const bool tg = lower_c && M == N && !tri_a;
+  // a lower-triangular batch takes 128-tiles only when they fill >= 2 rounds
+  // of 512 resident workgroups or K is long enough to split; otherwise they
+  // quantise badly (1.1-1.25 rounds: 21-36% vs 44-50% for 64-tiles).  FITC
+  // 2000 x 4000: 128-tiles + split-K 56% vs 39%
+  const int t128 = ((M + BT - 1) / BT) * ((M + BT - 1) / BT + 1) / 2 * batch;
+  static const int syrk128_env = [] {
+    const char *e = getenv("GPMPC_SYRK128");
+    return e ? atoi(e) : -1;
+  }();
+  const bool tri_ok = !tg || (syrk128_env >= 0 ? syrk128_env != 0 : t128 >= 1024 || K >= 1024);
+  static const int sk_env = [] {
+    const char *e = getenv("GPMPC_STREAMK");
+    return e ? atoi(e) : -1;
+  }();
+  if (sk_env > 0 && epi == EPI_STORE && beta == 1.0 && !tri_a && M >= 2 * BT && N >= 2 * BT &&
+      K >= 2 * BT) {
+    const int tx = (N + BT - 1) / BT, ty = (M + BT - 1) / BT;
+    const int T = tg ? ty * (ty + 1) / 2 : tx * ty;
+    const int64_t total = (int64_t)T * batch * ((K + GK - 1) / GK);
+    const int nwg = (int)std::min<int64_t>(512, total);
+    hipLaunchKernelGGL(k_gemm128_sk, dim3(nwg), dim3(256), 0, s, M, N, K, A, lda, B, ldb, C, ldc,
+                       alpha, (int)tg, tx, T, sA, sB, sC, total);
+    return hipGetLastError();
+  }
+  if (big_env && tri_ok && M >= 2 * BT && N >= 2 * BT && K >= 2 * BT) {
     const int tx = (N + BT - 1) / BT, ty = (M + BT - 1) / BT;
     // split K when the tiles cannot give each CU ~4 workgroups to interleave (STORE
     // with beta = 1: partial products are added atomically); >= 512 of K per split
     const int tiles = (lower_c ? ty * (ty + 1) / 2 : tx * ty) * batch;
+    // cost model: rounds of 512 resident workgroups (2 per CU) x (K per split
+    // + ~256 of fixed cost: prologue, atomic C update).  Measured on 2000^2 x
+    // 4000: ks 1/2/3/4/6/8 -> 30/38/53/43/49/45% (ks 4 leaves a 32-WG tail)
     int ksplit = 1;
-    if (epi == EPI_STORE && beta == 1.0 && tiles < 1024 && K >= 1024)
-      ksplit = max(1, min((1024 + tiles - 1) / tiles, K / 512));
-    dim3 g(tx, ty, batch * ksplit);
+    if (epi == EPI_STORE && beta == 1.0 && K >= 1024) {
+      double best = 1e30;
+      for (int ks = 1; ks <= K / 256 && ks <= 16; ++ks) {
+        const double c = (double)((tiles * ks + 511) / 512) * ((double)K / ks + 256.0);
+        if (c < best * 0.98) best = c, ksplit = ks;
+      }
+    }
+    static const int ks_env = [] {
+      const char *e = getenv("GPMPC_KSPLIT");
+      return e ? atoi(e) : 0;
+    }();
+    if (ks_env > 0 && epi == EPI_STORE && beta == 1.0) ksplit = ks_env;
+    // lower-triangular square products launch only their lower tiles, in a
+    // 1-D order that interleaves them over the 8 XCDs (a 2-D grid whose
+    // column count is a multiple of 8 pins columns to XCDs: 8x imbalance)
+    dim3 g(tg ? ty * (ty + 1) / 2 : tx, tg ? 1 : ty, batch * ksplit);
     if (epi == EPI_STORE)
       hipLaunchKernelGGL(k_gemm128<EPI_STORE>, g, dim3(256), 0, s, M, N, K, A, lda, B, ldb, C, ldc,
-                         alpha, beta, tri_a, lower_c, sA, sB, sC, M, nullptr, (int64_t)0, ksplit);
+                         alpha, beta, tri_a, lower_c, sA, sB, sC, M, nullptr, (int64_t)0, ksplit,
+                         (int)tg);
     else
       hipLaunchKernelGGL(k_gemm128<EPI_SUMSQ>, g, dim3(256), 0, s, M, N, K, A, lda, B, ldb, C, ldc,
-                         alpha, beta, tri_a, 0, sA, sB, sC, msum, Cm, ldm, 1);
+                         alpha, beta, tri_a, 0, sA, sB, sC, msum, Cm, ldm, 1, 0);
     return hipGetLastError();
   }
   const int tx = (N + GT - 1) / GT, ty = (M + GT - 1) / GT;
@@ -348,14 +476,21 @@ static hipError_t launch_gemm_impl(hipStream_t s, int epi, int M, int N, int K, 
     return e ? atoi(e) : 0;  // measured slower for the posterior GEMM (W blocks thrash)
   }();
   const bool remap = remap_env && batch == 1 && ty > 1 && tx % 8 == 0;
-  dim3 g = remap ? dim3(tx * ty, 1, 1) : dim3(tx, ty, batch);
-  const int rt = remap ? ty : 0;
+  static const int xb_env = [] {
+    const char *e = getenv("GPMPC_XCD_BATCH");
+    return e ? atoi(e) : 1;
+  }();
+  const int T = ty * (ty + 1) / 2;
+  const int xb = (tg && xb_env && batch >= 8) ? batch : 0;
+  dim3 g = xb ? dim3(T * ((batch + 7) / 8) * 8, 1, 1)
+         : tg ? dim3(T, 1, batch) : remap ? dim3(tx * ty, 1, 1) : dim3(tx, ty, batch);
+  const int rt = tg ? -1 : remap ? ty : 0;
   if (epi == EPI_STORE)
     hipLaunchKernelGGL(k_gemm_nt<EPI_STORE>, g, dim3(256), 0, s, M, N, K, A, lda, B, ldb, C, ldc,
-                       alpha, beta, tri_a, lower_c, sA, sB, sC, M, nullptr, (int64_t)0, rt);
+                       alpha, beta, tri_a, lower_c, sA, sB, sC, M, nullptr, (int64_t)0, rt, xb);
   else
     hipLaunchKernelGGL(k_gemm_nt<EPI_SUMSQ>, g, dim3(256), 0, s, M, N, K, A, lda, B, ldb, C, ldc,
-                       alpha, beta, tri_a, 0, sA, sB, sC, msum, Cm, ldm, rt);
+                       alpha, beta, tri_a, 0, sA, sB, sC, msum, Cm, ldm, rt, 0);
   return hipGetLastError();
 }
 
