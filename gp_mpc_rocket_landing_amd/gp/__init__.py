@@ -6,10 +6,11 @@ from .features import (AtmosphereModel, CombinedFeatureExtractor, RocketFeatureE
 from .kernels import (RBF, SE_ARD, Matern32, Matern52, ProductKernel, SquaredExponential,
                       SquaredExponentialARD, SumKernel, WhiteNoise, create_matern_kernel)
 from .sparse_gp import MultiOutputSparseGP, SparseGP
-from .structured_gp import Simple3DoFGP
+from .structured_gp import Simple3DoFGP, StructuredGPConfig, StructuredRocketGP
 
 __all__ = ["ExactGP", "GPPrediction", "MultiOutputExactGP", "AtmosphereModel", "CombinedFeatureExtractor",
            "RocketFeatureExtractor", "RotationalFeatureExtractor", "Simple3DoFFeatureExtractor",
            "TranslationalFeatureExtractor", "RBF", "SE_ARD", "Matern32", "Matern52", "ProductKernel",
            "SquaredExponential", "SquaredExponentialARD", "SumKernel", "WhiteNoise", "create_matern_kernel",
-           "MultiOutputSparseGP", "SparseGP", "Simple3DoFGP"]
+           "MultiOutputSparseGP", "SparseGP", "Simple3DoFGP", "StructuredGPConfig",
+           "StructuredRocketGP"]

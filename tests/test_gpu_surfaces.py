@@ -51,6 +51,33 @@ def test_simple3dof_sparse_vs_f4(gpu_ctx):
     np.testing.assert_allclose([p.log_marginal_likelihood for p in gp.gp.gps], g["lml"], rtol=1e-8)
 
 
+@pytest.mark.parametrize("tag", ["exact", "fitc"])
+def test_structured_rocket_gp_vs_f5(gpu_ctx, tag):
+    """6-DoF StructuredRocketGP (structured_gp.py:66-305), exact and FITC M=50, N=300:
+    the 4-tuple of predict_batch and of the single-point predict vs the reference."""
+    _ctx_default(gpu_ctx)
+    from gp_mpc_rocket_landing_amd.gp import StructuredGPConfig, StructuredRocketGP
+    g = golden("f5_structured_6dof.npz")
+    np.random.seed(77)                   # as the fixture: kmeans2 draws from the global RNG
+    gp = StructuredRocketGP(StructuredGPConfig(n_inducing=50, use_sparse=(tag == "fitc")))
+    gp.add_data(g["X"], g["U"], g["Dv"], g["Dw"])
+    gp.fit()
+    if tag == "fitc":
+        np.testing.assert_allclose(gp.gp_v.gps[0].inducing_points, g["fitc_Zv"], rtol=0, atol=1e-13)
+        np.testing.assert_allclose(gp.gp_omega.gps[0].inducing_points, g["fitc_Zw"], rtol=0, atol=1e-13)
+    sv, sw = np.std(g["Dv"], axis=0), np.std(g["Dw"], axis=0)   # the GPs' y_std (target scale)
+    mv, mw, vv, vw = gp.predict_batch(g["Xq"], g["Uq"])
+    for got, key, s in ((mv, "dv_mean", sv), (mw, "dw_mean", sw), (vv, "dv_var", sv ** 2), (vw, "dw_var", sw ** 2)):
+        ok, e = close(got, g[f"{tag}_{key}"], s[None, :])
+        assert ok, (key, e)
+    one = np.stack(gp.predict(g["Xq"][0], g["Uq"][0]))
+    for i, s in enumerate((sv, sw, sv ** 2, sw ** 2)):
+        assert close(one[i], g[f"{tag}_single"][i], s)[0], i
+    d_mean, d_var = gp.get_full_residual(g["Xq"][0], g["Uq"][0])
+    np.testing.assert_array_equal(d_mean[4:7], one[0]); np.testing.assert_array_equal(d_var[11:14], one[3])
+    assert d_mean[[0, 1, 2, 3, 7, 8, 9, 10]].tolist() == [0.0] * 8
+
+
 def test_exact_gp_surface_f2(gpu_ctx):
     _ctx_default(gpu_ctx)
     from gp_mpc_rocket_landing_amd.gp import ExactGP, MultiOutputExactGP, SquaredExponentialARD

@@ -88,3 +88,27 @@ def test_surface_defaults_match_reference():
     assert (m.N, m.dt, m.max_iter) == (20, 0.1, 100)
     g = GPMPCConfig()    # gp_mpc.py:48-63
     assert (g.use_gp_mean, g.use_gp_uncertainty, g.confidence_level) == (True, True, 0.95)
+
+
+def test_structured_rocket_gp_host_logic(tmp_path):
+    """StructuredRocketGP data handling without a device fit (structured_gp.py:170-204,
+    225-245, 375-406): the max_data_points window, the unfitted prior and a
+    pickle-free save/load round trip."""
+    from gp_mpc_rocket_landing_amd.gp import StructuredGPConfig, StructuredRocketGP
+    gp = StructuredRocketGP(StructuredGPConfig(max_data_points=5, signal_variance=0.3))
+    mv, mw, vv, vw = gp.predict(np.zeros(14), np.zeros(3))
+    assert mv.tolist() == [0.0] * 3 and vw.tolist() == [0.3] * 3
+    pb = gp.predict_batch(np.zeros((4, 14)), np.zeros((4, 3)))
+    assert [a.shape for a in pb] == [(4, 3)] * 4 and np.all(pb[2] == 0.3)
+    X = np.arange(8 * 14, dtype=float).reshape(8, 14)
+    gp.add_data(X, np.ones((8, 3)), np.zeros((8, 3)), np.zeros((8, 3)))
+    assert gp.n_data == 5 and np.array_equal(gp.X_data[0], X[3])   # newest 5 kept
+    with pytest.raises(RuntimeError, match="No data to fit"):
+        StructuredRocketGP().fit()
+    p = str(tmp_path / "sgp.npy")
+    gp.save(p)
+    g2 = StructuredRocketGP()
+    g2.load(p)                        # not fitted when saved -> no refit, no device work
+    assert g2.n_data == 5 and np.array_equal(np.array(g2.X_data), X[3:])
+    assert gp.feature_extractor.n_features_translational == 13
+    assert gp.feature_extractor.n_features_rotational == 12
