@@ -176,6 +176,36 @@ def cholesky_bench(ctx, torch, n=1000, batch=64, reps=3):
                            "tflops": round(fitc_tf, 3), "frac_fp64_peak": round(fitc_tf / FP64_PEAK_TFLOPS, 4)})
 
 
+def structured_fitc_bench(ctx, reps=2):
+    """BASELINE config 5 GP: StructuredRocketGP with FITC M = 2000, N_train = 4000
+    (two 3-output GPs, D = 13 translational / 12 rotational features), and one
+    batched predict over 512 rollouts x 30 horizon points.  Synthetic features;
+    inducing points are a random training subset (host kmeans2 is not timed)."""
+    import time
+    from gp_mpc_rocket_landing_amd import _lib
+    rs = np.random.RandomState(11)
+    M, N, P = 2000, 4000, 512 * 30
+    fit_t, pred_t = [], []
+    for _ in range(reps):
+        hs = []
+        t0 = time.perf_counter()
+        for d in (13, 12):
+            X = rs.uniform(0.0, 1.5, (N, d))
+            Y = np.stack([np.sin(X.sum(1)), np.cos(X[:, 0]), X[:, 1] ** 2], 1)
+            hs.append(_lib.FITCHandle(ctx, X[rs.choice(N, M, replace=False)], X, Y, np.ones(d), 1.0, 1e-4))
+        fit_t.append(time.perf_counter() - t0)
+        Q = [rs.uniform(0.0, 1.5, (P, d)) for d in (13, 12)]
+        t0 = time.perf_counter()
+        for h, q in zip(hs, Q):
+            h.predict(q)
+        pred_t.append(time.perf_counter() - t0)
+    f, p = min(fit_t), min(pred_t)
+    return {"workload": "StructuredRocketGP FITC, M=2000, N=4000, 2 x 3 outputs (config 5)",
+            "fit_ms": round(f * 1e3, 2), "predict_points": P, "predict_ms": round(p * 1e3, 2),
+            "predict_points_per_s": round(P / p, 1),
+            "note": "host-boundary times (H2D inputs, D2H results) around the device fit/predict"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -323,6 +353,7 @@ def main():
         if not args.no_chol:
             try:
                 out["cholesky"] = cholesky_bench(ctx, torch)
+                out["structured_fitc"] = structured_fitc_bench(ctx)
             except Exception as e:  # noqa: BLE001
                 out["cholesky"] = {"error": str(e)[:200]}
         if not args.no_cpu:

@@ -1,3 +1,4 @@
+#include <algorithm>
 // chol.hip -- blocked right-looking fp64 Cholesky (single and batched), TRSM, POTRS.
 //
 // Replaces LAPACK dpotrf / dtrtrs / dpotrs reached from np.linalg.cholesky,
@@ -145,6 +146,8 @@ hipError_t launch_potrf_batched(hipStream_t s, int n, int batch, double *A, int6
 // Triangular solves.  Inverses of the 32x32 diagonal blocks of L first, then
 // one workgroup per 64-column panel of X walks the row blocks (forward for
 // L X = B, backward for L^T X = B).
+#define TB 128  // row block of the blocked TRSM
+
 __global__ __launch_bounds__(64) void k_tri_inv_blocks(int n, const double *L, int64_t ldl,
                                                        double *Linv) {
   const int ib = blockIdx.x, r0 = ib * NB;
@@ -271,8 +274,44 @@ hipError_t launch_trsm_lower_ex(hipStream_t s, int n, int nrhs, const double *L,
   if (!Linv) Linv = (double *)gpmpc_scratch(0, sizeof(double) * NB * NB * (size_t)nblk);
   if (!Linv) return hipErrorOutOfMemory;
   hipLaunchKernelGGL(k_tri_inv_blocks, dim3(nblk), dim3(64), 0, s, n, L, ldl, Linv);
-  hipLaunchKernelGGL(k_trsm_panel, dim3((nrhs + 63) / 64), dim3(256), 0, s, n, nrhs, L, ldl, Linv,
-                     X, ldx, trans, rhs_lower);
+  if (n <= TB) {
+    hipLaunchKernelGGL(k_trsm_panel, dim3((nrhs + 63) / 64), dim3(256), 0, s, n, nrhs, L, ldl, Linv,
+                       X, ldx, trans, rhs_lower);
+    return hipGetLastError();
+  }
+  // blocked right-looking L X = B (FITC L_uu^-1 K_uf, W = L^-1, and the alpha
+  // solves, whose few columns used to walk all of L on one CU): per 128-row block, the panel walk against the block's own
+  // diagonal (32 x 32 inverses above), then X[r1:, :] -= L[r1:, r0:r1] X[r0:r1, :]
+  // as one MFMA GEMM.  With a lower-triangular right-hand side (identity) the
+  // block's rows are zero beyond column r1, so only r1 columns are touched.
+  if (trans) {
+    // L^T X = B from the bottom: X[r0:r1] = L_blk^-T X[r0:r1], then
+    // X[:r0, :] -= L[r0:r1, :r0]^T X[r0:r1, :]  (A^T B form of the GEMM)
+    for (int r0 = ((n - 1) / TB) * TB; r0 >= 0; r0 -= TB) {
+      const int nb = std::min(TB, n - r0);
+      hipLaunchKernelGGL(k_trsm_panel, dim3((nrhs + 63) / 64), dim3(256), 0, s, nb, nrhs,
+                         L + (int64_t)r0 * ldl + r0, ldl, Linv + (int64_t)(r0 / NB) * NB * NB,
+                         X + (int64_t)r0 * ldx, ldx, 1, 0);
+      if (r0 > 0) {
+        hipError_t e = launch_gemm_tn(s, r0, nrhs, nb, L + (int64_t)r0 * ldl, ldl,
+                                      X + (int64_t)r0 * ldx, ldx, X, ldx, -1.0, 1.0);
+        if (e != hipSuccess) return e;
+      }
+    }
+    return hipGetLastError();
+  }
+  for (int r0 = 0; r0 < n; r0 += TB) {
+    const int nb = std::min(TB, n - r0), r1 = r0 + nb;
+    const int cols = rhs_lower ? std::min(nrhs, r1) : nrhs;
+    hipLaunchKernelGGL(k_trsm_panel, dim3((cols + 63) / 64), dim3(256), 0, s, nb, cols,
+                       L + (int64_t)r0 * ldl + r0, ldl, Linv + (int64_t)(r0 / NB) * NB * NB,
+                       X + (int64_t)r0 * ldx, ldx, 0, 0);
+    if (r1 < n) {
+      hipError_t e = launch_gemm_nn(s, n - r1, cols, nb, L + (int64_t)r1 * ldl + r0, ldl,
+                                    X + (int64_t)r0 * ldx, ldx, X + (int64_t)r1 * ldx, ldx, -1.0, 1.0);
+      if (e != hipSuccess) return e;
+    }
+  }
   return hipGetLastError();
 }
 

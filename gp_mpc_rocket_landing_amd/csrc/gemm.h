@@ -13,6 +13,16 @@ hipError_t launch_gemm_nt(hipStream_t s, int epi, int M, int N, int K, const dou
                           double alpha, double beta, int tri_a, int lower_c, int batch,
                           int64_t sA, int64_t sB, int64_t sC);
 
+// C = alpha A B + beta C with B (K x N) row-major ("NN")
+hipError_t launch_gemm_nn(hipStream_t s, int M, int N, int K, const double *A, int64_t lda,
+                          const double *B, int64_t ldb, double *C, int64_t ldc, double alpha,
+                          double beta);
+
+// C = alpha A^T B + beta C with A (K x M) and B (K x N) row-major ("TN")
+hipError_t launch_gemm_tn(hipStream_t s, int M, int N, int K, const double *A, int64_t lda,
+                          const double *B, int64_t ldb, double *C, int64_t ldc, double alpha,
+                          double beta);
+
 hipError_t launch_trsm_lower_ex(hipStream_t s, int n, int nrhs, const double *L, int64_t ldl,
                                 double *X, int64_t ldx, int trans, int rhs_lower,
                                 double *Linv_blocks);

@@ -21,6 +21,7 @@
 #define GT 64
 #define GK 16
 #define GP 18
+static_assert(GK * (GT + 2) <= GT * GP, "k-major B tile must fit the row-major B buffer");
 
 // lower-triangular tile t -> (row tile ti, col tile tj), tj <= ti
 __device__ __forceinline__ void tri_tile(int t, int &ti, int &tj) {
@@ -31,7 +32,11 @@ __device__ __forceinline__ void tri_tile(int t, int &ti, int &tj) {
   tj = t - i * (i + 1) / 2;
 }
 
-template <int EPI>
+// BKN = 1: B is K x N row-major (C = alpha A B + beta C, the "NN" form); its
+// tile is staged k-major (sBk[k][col]) so the MFMA fragment read stays
+// contiguous.  Used by the blocked TRSM's trailing updates.
+// AKM = 1: A is K x M row-major (C = alpha A^T B + ...), staged k-major the same way.
+template <int EPI, int BKN = 0, int AKM = 0>
 __global__ __launch_bounds__(256) void k_gemm_nt(int M, int N, int K, const double *__restrict__ A,
                                                  int64_t lda, const double *__restrict__ B,
                                                  int64_t ldb, double *__restrict__ C, int64_t ldc,
@@ -85,33 +90,65 @@ __global__ __launch_bounds__(256) void k_gemm_nt(int M, int N, int K, const doub
   // registers while the current step's MFMAs run (LDS double buffer, one
   // barrier per K-step); rows are read as two 16-byte loads when aligned.
   const int lr = tid >> 2, lk = (tid & 3) * 4;
-  const bool ra = r0 + lr < M, rb = c0 + lr < N;
-  const double *pa = A + (int64_t)(ra ? r0 + lr : 0) * lda;
-  const double *pb = B + (int64_t)(rb ? c0 + lr : 0) * ldb;
+  // BKN: thread loads k-row kb = tid/16 of B, columns c0 + (tid%16)*4 .. +3
+  const int kb = tid >> 4, cb = (tid & 15) * 4;
+  double (*sBk)[GK][GT + 2] = reinterpret_cast<double (*)[GK][GT + 2]>(&sB[0][0][0]);
+  double (*sAk)[GK][GT + 2] = reinterpret_cast<double (*)[GK][GT + 2]>(&sA[0][0][0]);
+  const bool ra = AKM ? true : r0 + lr < M, rb = BKN ? true : c0 + lr < N;
+  const double *pa = AKM ? A + r0 + cb : A + (int64_t)(ra ? r0 + lr : 0) * lda;
+  const bool veca = AKM ? (((lda | ldb) & 1) == 0 && ((((uintptr_t)A) | ((uintptr_t)B)) & 15) == 0 &&
+                           r0 + cb + 3 < M)
+                        : false;
+  const double *pb = BKN ? B + c0 + cb : B + (int64_t)(rb ? c0 + lr : 0) * ldb;
   const bool vec = ((lda | ldb) & 1) == 0 && ((((uintptr_t)A) | ((uintptr_t)B)) & 15) == 0;
+  const bool vecb = BKN ? (vec && c0 + cb + 3 < N) : vec;
   double va[4], vb[4];
   auto gload = [&](int k0) {
     const int k = k0 + lk;
-    if (vec && k + 3 < kend) {
+    if (AKM) {
+      const int kr = k0 + kb;
+      const double *p = pa + (int64_t)kr * lda;
+      if (kr < kend && veca) {
+        const double2 a01 = *(const double2 *)p, a23 = *(const double2 *)(p + 2);
+        va[0] = a01.x; va[1] = a01.y; va[2] = a23.x; va[3] = a23.y;
+      } else {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) va[q] = (kr < kend && r0 + cb + q < M) ? p[q] : 0.0;
+      }
+    } else if (vec && k + 3 < kend) {
       const double2 a01 = ra ? *(const double2 *)(pa + k) : make_double2(0.0, 0.0);
       const double2 a23 = ra ? *(const double2 *)(pa + k + 2) : make_double2(0.0, 0.0);
+      va[0] = a01.x; va[1] = a01.y; va[2] = a23.x; va[3] = a23.y;
+    } else {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) va[q] = (ra && k + q < kend) ? pa[k + q] : 0.0;
+    }
+    if (BKN) {
+      const int kr = k0 + kb;
+      const double *p = pb + (int64_t)kr * ldb;
+      if (kr < kend && vecb) {
+        const double2 b01 = *(const double2 *)p, b23 = *(const double2 *)(p + 2);
+        vb[0] = b01.x; vb[1] = b01.y; vb[2] = b23.x; vb[3] = b23.y;
+      } else {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) vb[q] = (kr < kend && c0 + cb + q < N) ? p[q] : 0.0;
+      }
+    } else if (vec && k + 3 < kend) {
       const double2 b01 = rb ? *(const double2 *)(pb + k) : make_double2(0.0, 0.0);
       const double2 b23 = rb ? *(const double2 *)(pb + k + 2) : make_double2(0.0, 0.0);
-      va[0] = a01.x; va[1] = a01.y; va[2] = a23.x; va[3] = a23.y;
       vb[0] = b01.x; vb[1] = b01.y; vb[2] = b23.x; vb[3] = b23.y;
     } else {
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        va[q] = (ra && k + q < kend) ? pa[k + q] : 0.0;
-        vb[q] = (rb && k + q < kend) ? pb[k + q] : 0.0;
-      }
+      for (int q = 0; q < 4; ++q) vb[q] = (rb && k + q < kend) ? pb[k + q] : 0.0;
     }
   };
   auto lstore = [&](int buf) {
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      sA[buf][lr][lk + q] = va[q];
-      sB[buf][lr][lk + q] = vb[q];
+      if (AKM) sAk[buf][kb][cb + q] = va[q];
+      else sA[buf][lr][lk + q] = va[q];
+      if (BKN) sBk[buf][kb][cb + q] = vb[q];
+      else sB[buf][lr][lk + q] = vb[q];
     }
   };
   gload(0);
@@ -124,8 +161,10 @@ __global__ __launch_bounds__(256) void k_gemm_nt(int M, int N, int K, const doub
 #pragma unroll
     for (int kk = 0; kk < GK; kk += 4) {
       const int kc = kk + (lane >> 4);
-      const double a0 = sA[cur][qi + (lane & 15)][kc], a1 = sA[cur][qi + 16 + (lane & 15)][kc];
-      const double b0 = sB[cur][qj + (lane & 15)][kc], b1 = sB[cur][qj + 16 + (lane & 15)][kc];
+      const double a0 = AKM ? sAk[cur][kc][qi + (lane & 15)] : sA[cur][qi + (lane & 15)][kc];
+      const double a1 = AKM ? sAk[cur][kc][qi + 16 + (lane & 15)] : sA[cur][qi + 16 + (lane & 15)][kc];
+      const double b0 = BKN ? sBk[cur][kc][qj + (lane & 15)] : sB[cur][qj + (lane & 15)][kc];
+      const double b1 = BKN ? sBk[cur][kc][qj + 16 + (lane & 15)] : sB[cur][qj + 16 + (lane & 15)][kc];
       acc[0][0] = mfma_f64(a0, b0, acc[0][0]);
       acc[0][1] = mfma_f64(a0, b1, acc[0][1]);
       acc[1][0] = mfma_f64(a1, b0, acc[1][0]);
@@ -496,6 +535,30 @@ static hipError_t launch_gemm_impl(hipStream_t s, int epi, int M, int N, int K, 
   else
     hipLaunchKernelGGL(k_gemm_nt<EPI_SUMSQ>, g, dim3(256), 0, s, M, N, K, A, lda, B, ldb, C, ldc,
                        alpha, beta, tri_a, 0, sA, sB, sC, msum, Cm, ldm, rt, 0);
+  return hipGetLastError();
+}
+
+// C (M x N) = alpha A (M x K) B (K x N) + beta C, all row-major (64-tile kernel)
+hipError_t launch_gemm_nn(hipStream_t s, int M, int N, int K, const double *A, int64_t lda,
+                          const double *B, int64_t ldb, double *C, int64_t ldc, double alpha,
+                          double beta) {
+  if (M <= 0 || N <= 0) return hipSuccess;
+  dim3 g((N + GT - 1) / GT, (M + GT - 1) / GT, 1);
+  hipLaunchKernelGGL((k_gemm_nt<EPI_STORE, 1, 0>), g, dim3(256), 0, s, M, N, K, A, lda, B, ldb, C,
+                     ldc, alpha, beta, 0, 0, (int64_t)0, (int64_t)0, (int64_t)0, M, nullptr,
+                     (int64_t)0, 0, 0);
+  return hipGetLastError();
+}
+
+// C (M x N) = alpha A^T B + beta C with A (K x M) and B (K x N) row-major ("TN")
+hipError_t launch_gemm_tn(hipStream_t s, int M, int N, int K, const double *A, int64_t lda,
+                          const double *B, int64_t ldb, double *C, int64_t ldc, double alpha,
+                          double beta) {
+  if (M <= 0 || N <= 0) return hipSuccess;
+  dim3 g((N + GT - 1) / GT, (M + GT - 1) / GT, 1);
+  hipLaunchKernelGGL((k_gemm_nt<EPI_STORE, 1, 1>), g, dim3(256), 0, s, M, N, K, A, lda, B, ldb, C,
+                     ldc, alpha, beta, 0, 0, (int64_t)0, (int64_t)0, (int64_t)0, M, nullptr,
+                     (int64_t)0, 0, 0);
   return hipGetLastError();
 }
 

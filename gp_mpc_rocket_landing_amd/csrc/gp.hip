@@ -34,7 +34,7 @@ struct gpmpc_gp {
 
 struct gpmpc_fitc {
   GpCore core;  // core.Xs = scaled inducing rows (m), W = L_uu^-1, alphaT, ...
-  DevBuf WB;    // m x m, L_B^-1
+  DevBuf W2;    // m x m, L_B^-1 L_uu^-1 (lower): w = L_B^-1 v = W2 k*
   int m = 0;
 };
 
@@ -69,8 +69,8 @@ hipError_t launch_post_finish(hipStream_t s, int P, int n_out, int nrt, const do
   return hipGetLastError();
 }
 
-// FITC: part2 holds colsums for v = Luu^-1 Ku* (rows tiles) and w = LB^-1 v.
-__global__ void k_fitc_finish(int P, int n_out, int nrt, const double *__restrict__ pv,
+// FITC: pv / pw hold per-row-tile column sums of v^2 (v = Luu^-1 k*) and w^2 (w = W2 k*).
+__global__ void k_fitc_finish(int P, int n_out, int nrv, int nrw, const double *__restrict__ pv,
                               const double *__restrict__ pw, int64_t ldp,
                               const double *__restrict__ meanT, int64_t ldm,
                               const double *__restrict__ ymean, const double *__restrict__ ystd,
@@ -78,10 +78,8 @@ __global__ void k_fitc_finish(int P, int n_out, int nrt, const double *__restric
   int j = blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= P) return;
   double sv = 0.0, sw = 0.0;
-  for (int t = 0; t < nrt; ++t) {
-    sv += pv[(int64_t)t * ldp + j];
-    sw += pw[(int64_t)t * ldp + j];
-  }
+  for (int t = 0; t < nrv; ++t) sv += pv[(int64_t)t * ldp + j];
+  for (int t = 0; t < nrw; ++t) sw += pw[(int64_t)t * ldp + j];
   double lat = sigma2 - sv + sw;
   lat = lat > 1e-10 ? lat : 1e-10;
   for (int c = 0; c < n_out; ++c) {
@@ -459,7 +457,8 @@ extern "C" int gpmpc_fitc_fit(gpmpc_ctx *ctx, const double *Z, int m, const doub
       Luu.alloc(sizeof(double) * (size_t)m * m) || B.alloc(sizeof(double) * (size_t)m * m) ||
       dinfo.alloc(sizeof(int)) || lam.alloc(sizeof(double) * n) ||
       Xs.alloc(sizeof(double) * n * d) || Xn.alloc(sizeof(double) * n) ||
-      g.W.alloc(sizeof(double) * (size_t)m * m) || gp->WB.alloc(sizeof(double) * (size_t)m * m)) {
+      g.W.alloc(sizeof(double) * (size_t)(m + n_out) * m) ||  // [L_uu^-1; alpha^T]
+      gp->W2.alloc(sizeof(double) * (size_t)m * m)) {
     gpmpc_set_error("fitc_fit: out of device memory");
     return fail(-1);
   }
@@ -507,8 +506,9 @@ extern "C" int gpmpc_fitc_fit(gpmpc_ctx *ctx, const double *Z, int m, const doub
   hipLaunchKernelGGL(k_scale_cols, dim3((n + 255) / 256, m), dim3(256), 0, s, m, n,
                      Kuf.as<double>(), (int64_t)n, isq.as<double>());
   hipLaunchKernelGGL(k_eye, dim3((m + 255) / 256, m), dim3(256), 0, s, m, B.as<double>());
+  // lower triangle only (potrf, the TRSMs and the lml read nothing above the diagonal)
   launch_gemm_nt(s, EPI_STORE, m, m, n, Kuf.as<double>(), n, Kuf.as<double>(), n, B.as<double>(), m,
-                 1.0, 1.0, 0, 0, 1, 0, 0, 0);
+                 1.0, 1.0, 0, 1, 1, 0, 0, 0);
   launch_potrf_batched(s, m, 1, B.as<double>(), m, 0, dinfo.as<int>());
   hipMemcpyAsync(&info, dinfo.p, sizeof(int), hipMemcpyDeviceToHost, s);
   GPMPC_HIP(hipStreamSynchronize(s));
@@ -516,8 +516,10 @@ extern "C" int gpmpc_fitc_fit(gpmpc_ctx *ctx, const double *Z, int m, const doub
     gpmpc_set_error("Matrix is not positive definite (B, column %d)", info);
     return fail(info);
   }
-  hipLaunchKernelGGL(k_eye, dim3((m + 255) / 256, m), dim3(256), 0, s, m, gp->WB.as<double>());
-  launch_trsm_lower_ex(s, m, m, B.as<double>(), m, gp->WB.as<double>(), m, 0, 1, nullptr);
+  // W2 = L_B^-1 L_uu^-1 (a lower right-hand side): the predict gets |w|^2 from one
+  // triangular pass over K*u instead of storing v = L_uu^-1 K*u^T and solving again
+  hipMemcpyAsync(gp->W2.p, g.W.p, sizeof(double) * (size_t)m * m, hipMemcpyDeviceToDevice, s);
+  launch_trsm_lower_ex(s, m, m, B.as<double>(), m, gp->W2.as<double>(), m, 0, 1, nullptr);
   // alpha = B^-1 c  and the FITC lml  (sparse_gp.py:207-218)
   hipMemcpyAsync(alpha.p, cvec.p, sizeof(double) * m * n_out, hipMemcpyDeviceToDevice, s);
   launch_trsm_lower_ex(s, m, n_out, B.as<double>(), m, alpha.as<double>(), n_out, 0, 0, nullptr);
@@ -525,6 +527,9 @@ extern "C" int gpmpc_fitc_fit(gpmpc_ctx *ctx, const double *Z, int m, const doub
   hipLaunchKernelGGL(k_lml_fitc, dim3(n_out), dim3(256), 0, s, m, n, n_out, B.as<double>(),
                      dyn.as<double>(), lam.as<double>(), cvec.as<double>(), alpha.as<double>(),
                      g.alphaT.as<double>(), dlml.as<double>());
+  // alpha^T below L_uu^-1: the predict's first pass yields the mean as well
+  hipMemcpyAsync(g.W.as<double>() + (size_t)m * m, g.alphaT.p, sizeof(double) * n_out * m,
+                 hipMemcpyDeviceToDevice, s);
   g.h_ymean.resize(n_out);
   g.h_ystd.resize(n_out);
   std::vector<double> hl(n_out);
@@ -554,28 +559,23 @@ extern "C" int gpmpc_fitc_predict(gpmpc_ctx *ctx, gpmpc_fitc *gp, const double *
   hipStream_t s = ctx->stream;
   const GpCore &g = gp->core;
   const int m = gp->m;
-  DevBuf dq, Ks, V, pv, pw, meanT, dmean, dvar;
+  DevBuf dq, Ks, pv, pw, meanT, dmean, dvar;
   GPMPC_HIP(dq.alloc(sizeof(double) * p * g.d));
   GPMPC_HIP(hipMemcpyAsync(dq.p, Xq, sizeof(double) * p * g.d, hipMemcpyHostToDevice, s));
   int rc = core_cross(ctx, g, dq.as<double>(), p, Ks);  // K*u (p x m)
   if (rc) return rc;
-  const int nrt = gemm_row_tiles(m, p, m);
-  GPMPC_HIP(V.alloc(sizeof(double) * (size_t)p * m));
-  GPMPC_HIP(pv.alloc(sizeof(double) * (size_t)nrt * p));
-  GPMPC_HIP(pw.alloc(sizeof(double) * (size_t)nrt * p));
+  const int nrv = gemm_row_tiles(m + g.n_out, p, m), nrw = gemm_row_tiles(m, p, m);
+  GPMPC_HIP(pv.alloc(sizeof(double) * (size_t)nrv * p));
+  GPMPC_HIP(pw.alloc(sizeof(double) * (size_t)nrw * p));
   GPMPC_HIP(meanT.alloc(sizeof(double) * (size_t)g.n_out * p));
-  // v^T = K*u Luu^-T  (p x m); |v|^2 via the SUMSQ epilogue of W_uu K*u^T
-  GPMPC_HIP(launch_gemm_nt(s, EPI_STORE, p, m, m, Ks.as<double>(), m, g.W.as<double>(), m,
-                           V.as<double>(), m, 1.0, 0.0, 0, 0, 1, 0, 0, 0));
-  GPMPC_HIP(launch_gemm_nt(s, EPI_SUMSQ, m, p, m, g.W.as<double>(), m, Ks.as<double>(), m,
-                           pv.as<double>(), p, 1.0, 0.0, 1, 0, 1, 0, 0, 0));
-  GPMPC_HIP(launch_gemm_nt(s, EPI_SUMSQ, m, p, m, gp->WB.as<double>(), m, V.as<double>(), m,
+  // |v|^2 = |L_uu^-1 k*|^2 and the mean alpha^T k* in one pass; |w|^2 = |W2 k*|^2
+  GPMPC_HIP(launch_gemm_sumsq_mean(s, m, g.n_out, p, g.W.as<double>(), Ks.as<double>(),
+                                   pv.as<double>(), p, meanT.as<double>(), p));
+  GPMPC_HIP(launch_gemm_nt(s, EPI_SUMSQ, m, p, m, gp->W2.as<double>(), m, Ks.as<double>(), m,
                            pw.as<double>(), p, 1.0, 0.0, 1, 0, 1, 0, 0, 0));
-  GPMPC_HIP(launch_gemm_nt(s, EPI_STORE, g.n_out, p, m, g.alphaT.as<double>(), m, Ks.as<double>(),
-                           m, meanT.as<double>(), p, 1.0, 0.0, 0, 0, 1, 0, 0, 0));
   GPMPC_HIP(dmean.alloc(sizeof(double) * p * g.n_out));
   GPMPC_HIP(dvar.alloc(sizeof(double) * p * g.n_out));
-  hipLaunchKernelGGL(k_fitc_finish, dim3((p + 255) / 256), dim3(256), 0, s, p, g.n_out, nrt,
+  hipLaunchKernelGGL(k_fitc_finish, dim3((p + 255) / 256), dim3(256), 0, s, p, g.n_out, nrv, nrw,
                      pv.as<double>(), pw.as<double>(), (int64_t)p, meanT.as<double>(), (int64_t)p,
                      g.ymean.as<double>(), g.ystd.as<double>(), g.sigma2, dmean.as<double>(),
                      dvar.as<double>());

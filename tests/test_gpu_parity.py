@@ -41,6 +41,19 @@ def test_potrf_trsm_potrs(gpu_ctx, n):
     np.testing.assert_allclose(L.potrs(gpu_ctx, Lr, B), np.linalg.solve(A, B), rtol=1e-9, atol=1e-11)
 
 
+@pytest.mark.parametrize("n,nrhs", [(129, 64), (300, 333), (1000, 258), (517, 3)])
+def test_blocked_trsm_paths(gpu_ctx, n, nrhs):
+    """Blocked TRSM: 128-row diagonal solves + NN (forward) / TN (backward) MFMA
+    updates; odd widths exercise the unaligned and edge loads."""
+    L = _lib()
+    rs = np.random.RandomState(n + nrhs)
+    A = rs.normal(size=(n, n)); A = A @ A.T + n * np.eye(n)
+    Lr = np.linalg.cholesky(A)
+    B = rs.normal(size=(n, nrhs))
+    np.testing.assert_allclose(L.trsm_lower(gpu_ctx, Lr, B), np.linalg.solve(Lr, B), rtol=1e-9, atol=1e-11)
+    np.testing.assert_allclose(L.potrs(gpu_ctx, Lr, B), np.linalg.solve(A, B), rtol=1e-9, atol=1e-11)
+
+
 def test_potrf_reports_first_bad_pivot(gpu_ctx):
     L = _lib()
     A = np.eye(70); A[40, 40] = -1.0
@@ -182,3 +195,24 @@ def test_syrk_batched_paths(gpu_ctx, n, k, batch):
     assert err < 1e-12 * k, err
     # the strict upper triangle is untouched
     assert torch.equal(C[:, ~low], torch.zeros_like(C[:, ~low]))
+
+
+def test_fitc_config5_scale(gpu_ctx):
+    """FITC at the config-5 size (M = 2000 inducing points, N = 4000, D = 13, three
+    outputs): B = I + A A^T is the 2000 x 4000 lower SYRK (stream-K),
+    then potrf(2000), TRSMs and the posterior GEMMs, vs the numpy restatement."""
+    from gp_mpc_rocket_landing_amd import _lib as L
+    from oracle import gp_oracle
+    rs = np.random.RandomState(5)
+    X = rs.uniform(0.0, 1.5, (4000, 13))
+    Y = np.stack([np.sin(X @ rs.randn(13)), np.cos(X[:, 0] * X[:, 1]), X[:, 2] ** 2], 1) + 0.01 * rs.randn(4000, 3)
+    Zi = X[rs.choice(4000, 2000, replace=False)]
+    Xq = rs.uniform(0.0, 1.5, (300, 13))
+    h = L.FITCHandle(gpu_ctx, Zi, X, Y, np.ones(13), 1.0, 1e-4, 1e-6)
+    mean, var = h.predict(Xq)
+    st = gp_oracle.fitc_fit(Zi, X, Y)
+    rm, rv = gp_oracle.fitc_predict(st, Xq)
+    ok, e = close(mean, rm, st["y_std"][None, :]); assert ok, e
+    ok, e = close(var, rv, (st["y_std"] ** 2)[None, :]); assert ok, e
+    np.testing.assert_allclose(h.lml, st["lml"], rtol=1e-8)
+    np.testing.assert_allclose(h.lam, st["lam"], rtol=1e-10, atol=1e-14)
