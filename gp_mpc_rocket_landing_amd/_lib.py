@@ -111,6 +111,8 @@ _sig("gpmpc_fleet_set_stamps", _c, _vp, _vp)
 _sig("gpmpc_fleet_set_trace", _c, _vp, _vp)
 _sig("gpmpc_syrk_batched_dev", _c, _vp, _c, _c, _c, _vp, _c, ctypes.c_int64, _vp, _c, ctypes.c_int64,
      ctypes.c_double, ctypes.c_double)
+_sig("gpmpc_cov_propagate", _c, _vp, _c, _c, _c, _dp, _dp, _vp, ctypes.c_double, _dp)
+_sig("gpmpc_cov_propagate_dev", _c, _vp, _c, _c, _c, _vp, _vp, _vp, ctypes.c_double, _vp)
 _sig("gpmpc_fleet_read", _c, _vp, _dp, _dp)
 _sig("gpmpc_fleet_records_dev", _vp, _vp)
 _sig("gpmpc_fleet_destroy", _c, _vp)
@@ -123,7 +125,7 @@ EXPORTED = ["gpmpc_abi_version", "gpmpc_last_error", "gpmpc_ctx_create", "gpmpc_
             "gpmpc_qp_default_settings", "gpmpc_qp_solve_batched", "gpmpc_fleet_default_config",
             "gpmpc_fleet_create", "gpmpc_fleet_reset", "gpmpc_fleet_step", "gpmpc_fleet_read",
             "gpmpc_fleet_step_phases", "gpmpc_fleet_set_stamps", "gpmpc_fleet_set_trace",
-            "gpmpc_syrk_batched_dev",
+            "gpmpc_syrk_batched_dev", "gpmpc_cov_propagate", "gpmpc_cov_propagate_dev",
             "gpmpc_fleet_records_dev", "gpmpc_fleet_destroy"]
 
 
@@ -379,3 +381,22 @@ QP_STATUS_TEXT = {1: "solved", 2: "solved_inaccurate", -2: "maximum iterations r
                   -3: "primal infeasible", 3: "primal infeasible inaccurate",
                   -4: "dual infeasible", 4: "dual infeasible inaccurate", -7: "problem non convex",
                   -10: "unsolved", -100: "kkt factorisation failed"}
+
+
+def cov_propagate(ctx, A, q, S0=None, s0_diag=1e-6):
+    """Batched Sigma_{k+1} = A_k Sigma_k A_k^T + diag(q_k) on the device.
+    A (B, N, nx, nx), q (B, N, nx), S0 (B, nx, nx) or None -> (B, N+1, nx, nx)."""
+    A = f64(A); q = f64(q)
+    B, N, nx = A.shape[0], A.shape[1], A.shape[-1]
+    if A.shape != (B, N, nx, nx) or q.shape != (B, N, nx):
+        raise ValueError(f"cov_propagate: shapes A {A.shape}, q {q.shape}")
+    out = np.empty((B, N + 1, nx, nx))
+    s0 = None
+    if S0 is not None:
+        S0 = f64(S0)
+        if S0.shape != (B, nx, nx):
+            raise ValueError(f"cov_propagate: S0 shape {S0.shape}")
+        s0 = S0.ctypes.data_as(_vp)
+    _chk(_L.gpmpc_cov_propagate(ctx.h, B, N, nx, _d(A), _d(q), s0, float(s0_diag), _d(out)),
+         "cov_propagate")
+    return out

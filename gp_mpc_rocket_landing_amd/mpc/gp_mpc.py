@@ -16,9 +16,15 @@ is the control step the fleet runs on the device for every landing (SURVEY
 
 ``max_sqp_iter`` > 1 re-linearises around each QP solution like the
 reference's outer loop (gp_mpc.py:296-345, stop at 1e-4), success = converged.
-Uncertainty propagation / constraint tightening is not on this
-path; the GP variances along the horizon are kept for
-get_uncertainty_at_horizon().
+With ``use_gp_uncertainty`` (the default) each solve also propagates the
+state covariance along the linearisation trajectory (UncertaintyPropagator,
+linear: one batched GP call per step + the device covariance kernel;
+gp_mpc.py:284-290) and derives the step-0 tightened constraint parameters
+(gp_mpc.py:177-215, 414).  As in the reference these change nothing the QP
+uses (only thrust bounds and the glideslope enter it, and neither
+is tightened); they are exposed through ``last_uncertainty``,
+``last_tightened_params`` and ``get_uncertainty_at_horizon(k)``.  Propagation
+uses the propagator's default dt = 0.1 like the reference (D6).
 """
 from __future__ import annotations
 
@@ -29,8 +35,10 @@ from typing import Optional
 import numpy as np
 
 from .. import _lib
+from .constraints import ConstraintParams, TightenedConstraints
 from .nominal_mpc import MPCConfig, MPCSolution, _SQPBase, trajectory_cost
 from .qp_builder import solution_to_vector, vector_to_solution
+from .uncertainty_prop import PropagatedUncertainty, UncertaintyPropagator
 
 
 @dataclass
@@ -52,8 +60,13 @@ class GPMPC(_SQPBase):
             raise NotImplementedError("this GPMPC runs the 3-DoF model (n_x = 7)")
         super().__init__(dynamics, config or GPMPCConfig(), ctx=ctx)
         self.gp = gp_model
-        self.constraint_params = constraint_params
+        self.constraint_params = constraint_params or ConstraintParams()
         self.cost_weights = cost_weights
+        self._tightened_constraints = TightenedConstraints(base_params=self.constraint_params,
+                                                           confidence_level=self.config.confidence_level)
+        self._uncertainty_prop = UncertaintyPropagator(dynamics, gp_model, ctx=ctx)
+        self.last_uncertainty: Optional[PropagatedUncertainty] = None
+        self.last_tightened_params: Optional[ConstraintParams] = None
         self._last_var = None
         self._is_setup = False
 
@@ -81,11 +94,37 @@ class GPMPC(_SQPBase):
         U = np.zeros((N, self.n_u)); U[:, 0] = x0[0] * 1.0
         return X, U
 
+    def _get_tightened_params(self, unc: PropagatedUncertainty, k: int) -> ConstraintParams:
+        """gp_mpc.py:177-215; the 7-state model has no attitude / rate rows (0 std)."""
+        if not self.config.use_gp_uncertainty:
+            return self.constraint_params
+        std = np.sqrt(np.diag(unc.covariances[k]))
+        position_std = float(np.mean(std[1:4]))
+        velocity_std = float(np.mean(std[4:7]))
+        attitude_std = float(np.mean(std[8:10])) if std.size >= 14 else 0.0
+        omega_std = float(np.mean(std[11:14])) if std.size >= 14 else 0.0
+        if velocity_std > self.config.max_variance_for_constraint:
+            return self.constraint_params
+        return self._tightened_constraints.get_tightened_params(position_std=position_std,
+                                                                velocity_std=velocity_std,
+                                                                attitude_std=attitude_std,
+                                                                omega_std=omega_std)
+
+    def _propagate(self, x0, U):
+        if not (self.config.use_gp_uncertainty and self.gp is not None):
+            self.last_uncertainty = None
+            self.last_tightened_params = self.constraint_params
+            return
+        self.last_uncertainty = self._uncertainty_prop.propagate(
+            x0=x0, U=U[: self.config.N], Sigma_0=np.eye(self.n_x) * 1e-6)
+        self.last_tightened_params = self._get_tightened_params(self.last_uncertainty, 0)
+
     def solve(self, x0, x_target, X_ref=None, U_ref=None) -> MPCSolution:  # noqa: ARG002
         if not self._is_setup:
             self.setup()
         x0 = np.asarray(x0, float); x_target = np.asarray(x_target, float)
         X, U = self._initial(x0, x_target)
+        self._propagate(x0, U)
         if self.config.max_sqp_iter <= 1:
             t0 = time.perf_counter()
             P, q = self._qp.cost(np.tile(x_target, (self.config.N + 1, 1)))
@@ -107,6 +146,10 @@ class GPMPC(_SQPBase):
         return MPCSolution(success=conv, X_opt=X, U_opt=U, cost=trajectory_cost(X, U, x_target),
                            solve_time=dt, iterations=it, status="Converged" if conv else "Max iterations")
 
-    def get_uncertainty_at_horizon(self):
-        """GP variances (N, 3) at the last solve's horizon points."""
-        return None if self._last_var is None else self._last_var.copy()
+    def get_uncertainty_at_horizon(self, k: Optional[int] = None):
+        """gp_mpc.py:486-492 (a stub returning None in the reference): the propagated
+        covariance (n_x, n_x) at horizon step k of the last solve; with no k, the
+        GP variances (N, 3) at the last solve's horizon points."""
+        if k is None:
+            return None if self._last_var is None else self._last_var.copy()
+        return None if self.last_uncertainty is None else self.last_uncertainty.covariances[k].copy()

@@ -193,6 +193,19 @@ int gpmpc_fleet_set_stamps(gpmpc_fleet *f, void *dev_u64x16);
  * uint64 device buffer; NULL disables): start and end s_memrealtime (100 MHz),
  * HW_ID and XCC_ID of the landing's first wave */
 int gpmpc_fleet_set_trace(gpmpc_fleet *f, void *dev_u64xbx4);
+/* ---- uncertainty propagation (uncertainty_prop.py:117-177) ------------------
+ * Replaces the covariance recursion of UncertaintyPropagator._propagate_linear
+ * (Sigma_next = A_d @ Sigma_k @ A_d.T + Q_gp, uncertainty_prop.py:163-167) for
+ * batch trajectories at once: A (batch x N x nx x nx), q (batch x N x nx, the
+ * diagonal of Q_gp), S0 (batch x nx x nx, or NULL for s0_diag * I, the
+ * reference's default 1e-6 I), out (batch x (N+1) x nx x nx), all row-major;
+ * nx <= 16.  The host version copies in and out; _dev takes device pointers and
+ * is asynchronous on the context stream. */
+int gpmpc_cov_propagate(gpmpc_ctx *ctx, int batch, int N, int nx, const double *A, const double *q,
+                        const double *S0, double s0_diag, double *out);
+int gpmpc_cov_propagate_dev(gpmpc_ctx *ctx, int batch, int N, int nx, const double *dA,
+                            const double *dq, const double *dS0, double s0_diag, double *dout);
+
 /* device pointer of the record array (for collectives) */
 double *gpmpc_fleet_records_dev(gpmpc_fleet *f);
 int gpmpc_fleet_destroy(gpmpc_fleet *f);

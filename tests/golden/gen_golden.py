@@ -1,4 +1,4 @@
-"""Generate the golden fixtures F1-F8 from the reference itself.
+"""Generate the golden fixtures F1-F9 from the reference itself.
 
 Container-only: it imports /root/reference/src/{gp,mpc,experiments} through a
 namespace shim that bypasses src/__init__.py (which needs the absent simdyn /
@@ -40,6 +40,7 @@ sparse_gp = importlib.import_module("refgp.sparse_gp")
 features = importlib.import_module("refgp.features")
 structured_gp = importlib.import_module("refgp.structured_gp")
 osqp_rti = importlib.import_module("refmpc.osqp_rti")
+uncertainty_prop = importlib.import_module("refmpc.uncertainty_prop")
 monte_carlo = importlib.import_module("refexp.monte_carlo")
 
 
@@ -267,7 +268,32 @@ def f7_f8():
     save("f8_check_landing.npz", states=states, m0=m0, ok=np.array(ok), reason=np.array(reason))
 
 
+# ---------------------------------------------------------------- F9
+def f9():
+    """Reference UncertaintyPropagator (linear / unscented / Monte Carlo,
+    uncertainty_prop.py:117-315) with the exact 6-DoF StructuredRocketGP on the
+    F5 training set and the toy 14-state plant of toy_dynamics.py."""
+    sys.path.insert(0, HERE)
+    from toy_dynamics import ToyRocket14, toy_case
+    f5 = np.load(os.path.join(HERE, "f5_structured_6dof.npz"))
+    g = structured_gp.StructuredRocketGP(structured_gp.StructuredGPConfig(use_sparse=False))
+    g.add_data(f5["X"], f5["U"], f5["Dv"], f5["Dw"])
+    g.fit()
+    dyn = ToyRocket14()
+    x0, U = toy_case()
+    out = dict(x0=x0, U=U)
+    S0 = np.diag(np.linspace(1e-6, 1e-4, 14))
+    for method in ("linear", "unscented", "monte_carlo"):
+        np.random.seed(123)
+        p = uncertainty_prop.UncertaintyPropagator(dyn, g, method=method)
+        r = p.propagate(x0, U, Sigma_0=None if method != "unscented" else S0, dt=0.1)
+        out[f"{method}_means"] = r.means
+        out[f"{method}_covs"] = r.covariances
+    out["S0_unscented"] = S0
+    save("f9_uncertainty_prop.npz", **out)
+
+
 if __name__ == "__main__":
-    which = sys.argv[1:] or ["f1", "f2", "f3", "f4", "f5", "f6", "f7_f8"]
+    which = sys.argv[1:] or ["f1", "f2", "f3", "f4", "f5", "f6", "f7_f8", "f9"]
     for w in which:
         globals()[w]()

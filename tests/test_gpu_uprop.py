@@ -1,0 +1,114 @@
+"""Uncertainty propagation (uncertainty_prop.py:117-315) on the device path:
+the mirror vs the reference's own output (F9), the batched covariance kernel
+vs numpy, and the batched 3-DoF propagation vs the numpy restatement."""
+import os
+import sys
+
+import numpy as np
+import pytest
+
+from conftest import golden
+
+pytestmark = pytest.mark.gpu
+sys.path.insert(0, os.path.join(os.path.dirname(__file__), "golden"))
+
+
+def _ctx_default(gpu_ctx):
+    from gp_mpc_rocket_landing_amd import _lib
+    _lib._default_ctx = gpu_ctx
+
+
+@pytest.mark.parametrize("method", ["linear", "unscented", "monte_carlo"])
+def test_propagation_vs_f9(gpu_ctx, method):
+    _ctx_default(gpu_ctx)
+    from toy_dynamics import ToyRocket14
+    from gp_mpc_rocket_landing_amd.gp import StructuredGPConfig, StructuredRocketGP
+    from gp_mpc_rocket_landing_amd.mpc import UncertaintyPropagator
+    f5 = golden("f5_structured_6dof.npz"); f9 = golden("f9_uncertainty_prop.npz")
+    g = StructuredRocketGP(StructuredGPConfig(use_sparse=False))
+    g.add_data(f5["X"], f5["U"], f5["Dv"], f5["Dw"])
+    g.fit()
+    p = UncertaintyPropagator(ToyRocket14(), g, method=method, ctx=gpu_ctx)
+    np.random.seed(123)                                   # as the fixture (MC draws)
+    r = p.propagate(f9["x0"], f9["U"], Sigma_0=f9["S0_unscented"] if method == "unscented" else None, dt=0.1)
+    if method == "unscented":
+        # the reference's UT (alpha = 1e-3, uncertainty_prop.py:196-210) weights the
+        # centre sigma point by lambda/(n+lambda) ~ -1e6, so 1e-13 differences in the
+        # features reach the mean at ~1e-6: the numpy restatement of the same
+        # arithmetic lands 5.5e-7 from the fixture (covariances 1.3e-10 of 6.9e-4)
+        np.testing.assert_allclose(r.means, f9[f"{method}_means"], rtol=0, atol=2e-6)
+        np.testing.assert_allclose(r.covariances, f9[f"{method}_covs"], rtol=0, atol=1e-9)
+    else:
+        # GP parity is 1e-6 relative on the residual; the states carry it times dt
+        np.testing.assert_allclose(r.means, f9[f"{method}_means"], rtol=1e-7, atol=1e-9)
+        np.testing.assert_allclose(r.covariances, f9[f"{method}_covs"], rtol=1e-6, atol=1e-12)
+    lo, hi = r.get_confidence_bounds(5)
+    assert np.all(lo < r.means[5]) and np.all(hi > r.means[5])
+
+
+@pytest.mark.parametrize("nx,B,N", [(7, 300, 30), (14, 64, 20), (16, 5, 3), (7, 1, 0)])
+def test_cov_propagate_kernel(gpu_ctx, nx, B, N):
+    from gp_mpc_rocket_landing_amd import _lib
+    rs = np.random.RandomState(nx * 100 + B)
+    A = np.eye(nx) + 0.1 * rs.randn(B, N, nx, nx)
+    q = rs.rand(B, N, nx) * 1e-3
+    S0 = None if nx != 14 else np.einsum("bij,bkj->bik", *(2 * [rs.randn(B, nx, nx) * 0.01]))
+    out = _lib.cov_propagate(gpu_ctx, A, q, S0)
+    S = np.broadcast_to(np.eye(nx) * 1e-6, (B, nx, nx)).copy() if S0 is None else S0.copy()
+    np.testing.assert_array_equal(out[:, 0], S)
+    for k in range(N):
+        S = A[:, k] @ S @ A[:, k].transpose(0, 2, 1) + np.einsum("bi,ij->bij", q[:, k], np.eye(nx))
+        np.testing.assert_allclose(out[:, k + 1], S, rtol=1e-12, atol=1e-18)
+
+
+def test_propagate_batch_3dof_vs_oracle(gpu_ctx):
+    """16 horizons of the normalised 3-DoF rocket with the exact Simple3DoFGP (F1
+    data): one batched GP call per step + one covariance launch, vs the numpy
+    restatement per trajectory."""
+    _ctx_default(gpu_ctx)
+    from oracle import uprop_oracle
+    from gp_mpc_rocket_landing_amd.dynamics import create_normalized_rocket
+    from gp_mpc_rocket_landing_amd.gp import Simple3DoFGP
+    from gp_mpc_rocket_landing_amd.mpc import UncertaintyPropagator
+    f1 = golden("f1_exact_simple3dof.npz")
+    gp = Simple3DoFGP(use_sparse=False)
+    gp.add_data(f1["X"], f1["U"], f1["D"]); gp.fit()
+    dyn = create_normalized_rocket()
+    rs = np.random.RandomState(4)
+    B, N = 16, 20
+    X0 = f1["X"][:B] + 0.01 * rs.randn(B, 7)
+    U = np.repeat(f1["U"][:B, None, :], N, axis=1) * (1 + 0.05 * rs.randn(B, N, 1))
+    means, covs = UncertaintyPropagator(dyn, gp, ctx=gpu_ctx).propagate_batch(X0, U, None, 0.1)
+    orc = uprop_oracle.simple3dof_exact_predictor(f1["X"], f1["U"], f1["D"])
+    for b in range(B):
+        m, c = uprop_oracle.propagate_linear(dyn, orc, X0[b], U[b], None, 0.1)
+        np.testing.assert_allclose(means[b], m, rtol=1e-9, atol=1e-10)
+        np.testing.assert_allclose(covs[b], c, rtol=1e-6, atol=1e-14)
+
+
+def test_gpmpc_propagates_and_tightens(gpu_ctx):
+    """GPMPC.solve propagates along its linearisation controls (gp_mpc.py:284-290)
+    and derives the step-0 tightened parameters (gp_mpc.py:177-215, 414)."""
+    _ctx_default(gpu_ctx)
+    from scipy.stats import norm
+    from oracle import uprop_oracle
+    from gp_mpc_rocket_landing_amd.dynamics import create_normalized_rocket
+    from gp_mpc_rocket_landing_amd.gp import Simple3DoFGP
+    from gp_mpc_rocket_landing_amd.mpc import GPMPC, GPMPCConfig
+    f1 = golden("f1_exact_simple3dof.npz")
+    gp = Simple3DoFGP(use_sparse=False)
+    gp.add_data(f1["X"], f1["U"], f1["D"]); gp.fit()
+    dyn = create_normalized_rocket()
+    mpc = GPMPC(dyn, gp, GPMPCConfig(N=20), ctx=gpu_ctx)
+    x0 = np.array([2.0, 30.0, 1.0, -1.0, -3.0, 0.2, 0.1]); xt = np.zeros(7); xt[0] = 1.5
+    _, U0 = mpc._initial(x0, xt)
+    sol = mpc.solve(x0, xt)
+    assert sol.success
+    orc = uprop_oracle.simple3dof_exact_predictor(f1["X"], f1["U"], f1["D"])
+    m, c = uprop_oracle.propagate_linear(dyn, orc, x0, U0, None, 0.1)
+    np.testing.assert_allclose(mpc.last_uncertainty.means, m, rtol=1e-9, atol=1e-10)
+    np.testing.assert_allclose(mpc.last_uncertainty.covariances, c, rtol=1e-6, atol=1e-14)
+    np.testing.assert_allclose(mpc.get_uncertainty_at_horizon(20), c[20], rtol=1e-6, atol=1e-14)
+    kappa = norm.ppf(0.95)
+    assert mpc.last_tightened_params.v_max == pytest.approx(50.0 - kappa * 1e-3, abs=1e-12)
+    assert mpc.last_tightened_params.T_max == 5.0 and mpc.last_tightened_params.gamma_gs == 30.0

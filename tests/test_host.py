@@ -112,3 +112,34 @@ def test_structured_rocket_gp_host_logic(tmp_path):
     assert g2.n_data == 5 and np.array_equal(np.array(g2.X_data), X[3:])
     assert gp.feature_extractor.n_features_translational == 13
     assert gp.feature_extractor.n_features_rotational == 12
+
+
+def test_tightening_arithmetic():
+    """TightenedConstraints / ConstraintTightening / TubeBasedRobustness
+    (constraints.py:427-509, uncertainty_prop.py:318-468) on hand-checked numbers."""
+    from scipy.stats import norm
+    from gp_mpc_rocket_landing_amd.mpc import (ConstraintParams, ConstraintTightening,
+                                               PropagatedUncertainty, TightenedConstraints,
+                                               TubeBasedRobustness)
+    tc = TightenedConstraints(ConstraintParams(), confidence_level=0.99)
+    k = norm.ppf(0.99)
+    p = tc.get_tightened_params(velocity_std=2.0, attitude_std=0.1, omega_std=0.05)
+    assert p.v_max == pytest.approx(50.0 - 2.0 * k)
+    assert p.theta_max == pytest.approx(90.0 - np.rad2deg(0.1 * k))
+    assert p.omega_max == pytest.approx(max(60.0 - np.rad2deg(0.05 * k), 10.0))
+    assert tc.get_tightened_params(velocity_std=100.0).v_max == 1.0        # floor
+    assert tc.tighten_scalar_constraint(3.0, 1.0) == pytest.approx(3.0 - k)
+    ct = ConstraintTightening(0.95)
+    S = np.diag([4.0, 9.0])
+    assert ct.tighten_linear_constraint(np.array([1.0, 1.0]), 2.0, None, S) == pytest.approx(
+        2.0 + norm.ppf(0.95) * np.sqrt(13.0))
+    unc = PropagatedUncertainty(means=np.zeros((3, 2)), covariances=np.stack([S] * 3))
+    bo = ct.compute_back_offs(unc, [[np.array([1.0, 0.0])]] * 2)
+    np.testing.assert_allclose(bo, norm.ppf(0.95) * 2.0 * np.ones((2, 1)))
+
+    class Lin:
+        def linearize(self, x, u, dt=0.1):
+            return np.eye(7) * 0.5, np.zeros((7, 3))
+    w = TubeBasedRobustness(Lin(), d_max=0.2).compute_tube(np.zeros((3, 7)), np.zeros((2, 3)), 0.1)
+    np.testing.assert_allclose(w[1, 4:7], 0.02); np.testing.assert_allclose(w[2, 4:7], 0.5 * 0.02 + 0.02)
+    assert np.all(w[:, :4] == 0)

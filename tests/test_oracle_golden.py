@@ -176,3 +176,17 @@ def test_admm_kkt_optimality():
     assert res["status"] in (1, 2)
     Ax = A @ res["x"]
     assert np.all(Ax >= l - 1e-2) and np.all(Ax <= u + 1e-2)
+
+
+def test_f9_linear_propagation_oracle():
+    """The numpy restatement of _propagate_linear against the reference's own
+    output (exact StructuredRocketGP on F5, toy 14-state plant)."""
+    import sys, os
+    sys.path.insert(0, os.path.join(os.path.dirname(__file__), "golden"))
+    from toy_dynamics import ToyRocket14
+    from oracle import uprop_oracle
+    f5 = golden("f5_structured_6dof.npz"); f9 = golden("f9_uncertainty_prop.npz")
+    gp = uprop_oracle.structured_exact_predictor(f5["X"], f5["U"], f5["Dv"], f5["Dw"])
+    means, covs = uprop_oracle.propagate_linear(ToyRocket14(), gp, f9["x0"], f9["U"], None, 0.1)
+    np.testing.assert_allclose(means, f9["linear_means"], rtol=1e-9, atol=1e-12)
+    np.testing.assert_allclose(covs, f9["linear_covs"], rtol=1e-7, atol=1e-14)
