@@ -20,6 +20,7 @@
 #include "internal.h"
 #include "gemm.h"
 #include "qp.h"
+#include "fleet_qp.h"
 #include <vector>
 
 #define NX 7
@@ -35,8 +36,11 @@ struct gpmpc_fleet {
   QPPatternHost pat;
   DevBuf x, Xw, Uw, ysc, rho, rec, xt;      // landing state
   DevBuf Q, Qn, Ks, part, meanT, mean, var;  // GP scratch
+  DevBuf order, lastit;                      // dispatch order: longest predicted solve first
   unsigned long long *stamps = nullptr;      // diagnostic (gpmpc_fleet_set_stamps)
   unsigned long long *trace = nullptr;       // diagnostic (gpmpc_fleet_set_trace)
+  bool use_order = true;                     // GPMPC_FLEET_ORDER=0 launches in landing order
+  bool use_fq = true;                        // fleet-specialised solver (GPMPC_FLEET_SOLVER=0: generic)
 };
 
 extern "C" int gpmpc_fleet_set_stamps(gpmpc_fleet *f, void *dev_u64x16) {
@@ -160,6 +164,8 @@ struct FleetArgs {
   double dt;
   double *x, *Xw, *Uw, *ysc, *rho, *rec, *xt;
   const double *gmean;  // (B*N) x 3
+  const int *order;     // workgroup -> landing (longest predicted first), or null
+  int *lastit;          // ADMM iterations of each landing's last solve
   unsigned long long *stamps;  // diagnostic phase cycles of block 0 (or null)
   unsigned long long *trace;   // diagnostic per-landing placement/timing (or null)
 };
@@ -168,7 +174,7 @@ __global__ __launch_bounds__(256) void k_fleet_control(FleetArgs a) {
   __shared__ QPSmemStd s;
   __shared__ double sx[NX], st_tgt[NX];
   __shared__ int s_out;
-  const int b = blockIdx.x, tid = threadIdx.x, nt = blockDim.x;
+  const int b = a.order ? a.order[blockIdx.x] : (int)blockIdx.x, tid = threadIdx.x, nt = blockDim.x;
   const int N = a.N, n = a.pt.n, m = a.pt.m;
   const double dt = a.dt;
   double *rec = a.rec + (int64_t)b * GPMPC_REC_LEN;
@@ -365,6 +371,7 @@ __global__ __launch_bounds__(256) void k_fleet_control(FleetArgs a) {
     rec[2] = rec[13] - xn[0];
     for (int i = 0; i < NX; ++i) rec[4 + i] = xn[i];
     rec[11] += res.iter;
+    a.lastit[b] = res.iter;
     rec[12] += (res.status == 1) ? 1.0 : 0.0;
     rec[14] = res.factor_fail ? -100 : res.status;
     rec[15] = s.rho_s;
@@ -375,6 +382,214 @@ __global__ __launch_bounds__(256) void k_fleet_control(FleetArgs a) {
 }
 
 // initial linearisation point: X linear to the target, U hover (osqp_rti.py:425-446)
+// The same control step on the fleet-specialised solver (fleet_qp.h): 128
+// threads and ~37 KB of LDS per landing, four landings per CU.  Assembly goes
+// straight into the owners' registers; results and the plant step as above.
+__global__ __launch_bounds__(FQ_T) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_fleet_control2(FleetArgs a) {
+  __shared__ FleetSmem s;
+  __shared__ double sx[NX], st_tgt[NX];
+  __shared__ int s_out;
+  const int b = a.order ? a.order[blockIdx.x] : (int)blockIdx.x, tid = threadIdx.x;
+  const int N = a.N, n = a.pt.n, m = a.pt.m;
+  const double dt = a.dt;
+  double *rec = a.rec + (int64_t)b * GPMPC_REC_LEN;
+  if (rec[0] != 0.0) return;  // terminated landing
+  QPStamps T;
+  T.out = (b == 0) ? a.stamps : nullptr;
+  T.start();
+  if (a.trace && tid == 0) {
+    unsigned long long *tr = a.trace + (int64_t)b * 4;
+    tr[0] = __builtin_amdgcn_s_memrealtime();
+    tr[2] = (unsigned)__builtin_amdgcn_s_getreg(4 | (31 << 11));
+    tr[3] = (unsigned)__builtin_amdgcn_s_getreg(20 | (31 << 11));
+  }
+  double *x = a.x + (int64_t)b * NX;
+  double *Xw = a.Xw + (int64_t)b * (N + 1) * NX;
+  double *Uw = a.Uw + (int64_t)b * N * NU;
+  if (tid < NX) sx[tid] = x[tid];
+  __syncthreads();
+  if (tid == 0) {  // termination checks (monte_carlo.py:458-488), as k_fleet_control
+    int out = 0;
+    const double m0 = rec[13];
+    bool div = false;
+    for (int i = 0; i < NX; ++i) div = div || !(fabs(sx[i]) <= 1e6);
+    if ((int)rec[1] >= a.max_steps) out = 5;
+    else if (sx[1] < 0.0) out = 2;
+    else if (sx[0] <= 1.0 + 0.01) out = 3;
+    else if (div) out = 6;
+    else if (sx[1] < 1.0 && fabs(sx[4]) < 5.0) out = landing_ok(sx, m0) ? 1 : 4;
+    s_out = out;
+    for (int i = 0; i < NX; ++i) st_tgt[i] = a.target_mode ? sx[i] : a.xt[(int64_t)b * NX + i];
+    if (a.target_mode) {
+      st_tgt[4] = st_tgt[5] = st_tgt[6] = 0.0;
+      st_tgt[1] = fmax(0.5, sx[1] - 2.0);
+    }
+  }
+  __syncthreads();
+  if (s_out) {
+    if (tid == 0) {
+      rec[0] = s_out;
+      rec[2] = rec[13] - sx[0];
+      for (int i = 0; i < NX; ++i) rec[4 + i] = sx[i];
+    }
+    return;
+  }
+  FleetRegs R;
+  fq_init_pattern(a.pt, R, n);
+  const int Nv = N * (NX + NU);
+  const int MD = NX * (N + 1);
+  // ---- QP data (osqp_rti.py:203-372 with the GPMPC sign): variables + bound rows
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    if (!R.vok[h]) continue;
+    const int j = R.vj[h];
+    double p, qq, lo, hi, xw;
+    const int i = (j >= Nv) ? j - Nv : j % (NX + NU);
+    if (j >= Nv) {
+      const double qd = (i == 0) ? 0.0 : (i < 4 ? 100.0 : 10.0);
+      p = qd; qq = -qd * st_tgt[i];
+      xw = Xw[N * NX + i];
+    } else {
+      const int k = j / (NX + NU);
+      if (i < NX) {
+        const double qd = (i == 0) ? 0.0 : (i < 4 ? 10.0 : 1.0);
+        p = qd; qq = -qd * st_tgt[i];
+        xw = Xw[k * NX + i];
+      } else {
+        p = 0.01; qq = 0.0;
+        xw = Uw[k * NU + (i - NX)];
+      }
+    }
+    if (i < NX) {
+      const double xmin[NX] = {-INFINITY, -100, -100, -100, -50, -50, -50};
+      const double xmax[NX] = {INFINITY, 500, 100, 100, 50, 50, 50};
+      lo = xmin[i]; hi = xmax[i];
+    } else {
+      const double umin[NU] = {0.3, -5, -5}, umax[NU] = {5, 5, 5};
+      lo = umin[i - NX]; hi = umax[i - NX];
+    }
+    R.P[h] = p; R.q[h] = qq; R.x[h] = xw;
+    R.Ab[h] = 1.0; R.lb[h] = lo; R.ub[h] = hi;
+    R.yb[h] = a.ysc[(int64_t)b * m + MD + j];
+  }
+  // dynamics rows: A values (one thread per stage) and c_k, staged in zt for the row owners
+  for (int r = tid; r < NX; r += FQ_T) {
+    s.A[r] = 1.0;
+    s.zt[r] = sx[r];
+  }
+  for (int k = tid; k < N; k += FQ_T) {
+    const double *xk = Xw + k * NX;
+    const double *uk = Uw + k * NU;
+    const double mk = xk[0], tx = uk[0], ty = uk[1], tz = uk[2];
+    const double tm = sqrt(tx * tx + ty * ty + tz * tz) + 1e-10;
+    const double al = 1.0 / 30.0;
+    const double a40 = -tx / (mk * mk) * dt, a50 = -ty / (mk * mk) * dt, a60 = -tz / (mk * mk) * dt;
+    const double b00 = -al * tx / tm * dt, b01 = -al * ty / tm * dt, b02 = -al * tz / tm * dt;
+    const double bv = dt / mk;
+    double *Ak = s.A + NX + k * DYN_NNZ;
+    Ak[0] = 1.0; Ak[1] = b00; Ak[2] = b01; Ak[3] = b02; Ak[4] = -1.0;
+    Ak[5] = 1.0; Ak[6] = dt; Ak[7] = -1.0;
+    Ak[8] = 1.0; Ak[9] = dt; Ak[10] = -1.0;
+    Ak[11] = 1.0; Ak[12] = dt; Ak[13] = -1.0;
+    Ak[14] = a40; Ak[15] = 1.0; Ak[16] = bv; Ak[17] = -1.0;
+    Ak[18] = a50; Ak[19] = 1.0; Ak[20] = bv; Ak[21] = -1.0;
+    Ak[22] = a60; Ak[23] = 1.0; Ak[24] = bv; Ak[25] = -1.0;
+    double f[NX];
+    plant_euler(xk, uk, dt, f);
+    double ax[NX], bu[NX];
+    ax[0] = xk[0];
+    ax[1] = xk[1] + dt * xk[4];
+    ax[2] = xk[2] + dt * xk[5];
+    ax[3] = xk[3] + dt * xk[6];
+    ax[4] = a40 * xk[0] + xk[4];
+    ax[5] = a50 * xk[0] + xk[5];
+    ax[6] = a60 * xk[0] + xk[6];
+    bu[0] = b00 * tx + b01 * ty + b02 * tz;
+    bu[1] = bu[2] = bu[3] = 0.0;
+    bu[4] = bv * tx; bu[5] = bv * ty; bu[6] = bv * tz;
+    const double *gm = a.gmean + ((int64_t)b * N + k) * 3;
+    for (int i = 0; i < NX; ++i) {
+      double c = (f[i] - ax[i]) - bu[i];
+      if (a.use_gp && i >= 4) c += gm[i - 4] * dt;
+      s.zt[NX * (k + 1) + i] = -c;
+    }
+  }
+  if (tid == 0) s.rho_s = a.rho[b];
+  __syncthreads();
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+    if (R.rok[h]) {
+      R.lr[h] = R.ur[h] = s.zt[R.rr[h]];
+      R.yr[h] = a.ysc[(int64_t)b * m + R.rr[h]];
+    }
+  __syncthreads();
+  T.mark(0);
+  QPResult res = fq_solve(a.pt, s, R, a.st, &T);
+  T.mark(7);
+  const bool has = !res.factor_fail && (res.status == 1 || res.status == 2 || res.status == -2);
+  if (has) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+      if (R.vok[h]) s.rhs[R.vj[h]] = R.D[h] * R.x[h];  // unscaled solution
+  }
+  __syncthreads();
+  if (!has && a.target_mode == 1) {
+    if (tid == 0) {
+      rec[0] = 6;
+      rec[14] = res.factor_fail ? -100 : res.status;
+      for (int i = 0; i < NX; ++i) rec[4 + i] = sx[i];
+      rec[2] = rec[13] - sx[0];
+    }
+    return;
+  }
+  if (has) {
+    for (int e = tid; e < (N + 1) * NX; e += FQ_T) {
+      const int k = e / NX, i = e - k * NX;
+      const int ks = (k + 1 <= N) ? k + 1 : N;
+      const int src = (ks == N) ? Nv + i : ks * (NX + NU) + i;
+      Xw[e] = s.rhs[src];
+    }
+    for (int e = tid; e < N * NU; e += FQ_T) {
+      const int k = e / NU, i = e - k * NU;
+      const int ks = (k + 1 < N) ? k + 1 : N - 1;
+      Uw[e] = s.rhs[ks * (NX + NU) + NX + i];
+    }
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      if (R.rok[h]) a.ysc[(int64_t)b * m + R.rr[h]] = R.yr[h];
+      if (R.vok[h]) a.ysc[(int64_t)b * m + MD + R.vj[h]] = R.yb[h];
+    }
+  }
+  if (tid == 0) {
+    double u0[NU];
+    if (has) {
+      u0[0] = s.rhs[NX]; u0[1] = s.rhs[NX + 1]; u0[2] = s.rhs[NX + 2];
+    } else {
+      u0[0] = Uw[0]; u0[1] = Uw[1]; u0[2] = Uw[2];
+    }
+    double xn[NX], dr[3];
+    plant_euler(sx, u0, dt, xn);
+    if (a.residual_model) {
+      drag_residual(sx, dr);
+      xn[4] += dr[0] * dt; xn[5] += dr[1] * dt; xn[6] += dr[2] * dt;
+    }
+    for (int i = 0; i < NX; ++i) x[i] = xn[i];
+    a.rho[b] = s.rho_s;
+    rec[1] += 1.0;
+    rec[3] = rec[1] * dt;
+    rec[2] = rec[13] - xn[0];
+    for (int i = 0; i < NX; ++i) rec[4 + i] = xn[i];
+    rec[11] += res.iter;
+    a.lastit[b] = res.iter;
+    rec[12] += (res.status == 1) ? 1.0 : 0.0;
+    rec[14] = res.factor_fail ? -100 : res.status;
+    rec[15] = s.rho_s;
+  }
+  T.mark(7);
+  T.flush();
+  if (a.trace && tid == 0) a.trace[(int64_t)b * 4 + 1] = __builtin_amdgcn_s_memrealtime();
+}
+
 __global__ void k_fleet_reset(int first, int count, int N, int target_mode,
                               const double *__restrict__ x0, double *x, double *Xw, double *Uw,
                               double *ysc, int m, double *rho, double rho0, double *rec,
@@ -439,7 +654,8 @@ extern "C" int gpmpc_fleet_create(gpmpc_ctx *ctx, gpmpc_gp *gp, const gpmpc_flee
       f->xt.alloc(sizeof(double) * B * NX) || f->Q.alloc(sizeof(double) * P * NFEAT) ||
       f->Qn.alloc(sizeof(double) * P) || f->Ks.alloc(sizeof(double) * P * g.n) ||
       f->part.alloc(sizeof(double) * nrt * P) || f->meanT.alloc(sizeof(double) * 3 * P) ||
-      f->mean.alloc(sizeof(double) * P * 3) || f->var.alloc(sizeof(double) * P * 3)) {
+      f->mean.alloc(sizeof(double) * P * 3) || f->var.alloc(sizeof(double) * P * 3) ||
+      f->order.alloc(sizeof(int) * B) || f->lastit.alloc(sizeof(int) * B)) {
     delete f;
     gpmpc_set_error("fleet: out of device memory");
     return -1;
@@ -448,6 +664,13 @@ extern "C" int gpmpc_fleet_create(gpmpc_ctx *ctx, gpmpc_gp *gp, const gpmpc_flee
   std::vector<double> r(B * GPMPC_REC_LEN, 0.0);
   for (size_t b = 0; b < B; ++b) r[b * GPMPC_REC_LEN] = -1.0;
   hipMemcpyAsync(f->rec.p, r.data(), sizeof(double) * r.size(), hipMemcpyHostToDevice, ctx->stream);
+  hipMemsetAsync(f->lastit.p, 0, sizeof(int) * B, ctx->stream);
+  const char *oe = getenv("GPMPC_FLEET_ORDER");
+  f->use_order = !oe || atoi(oe) != 0;
+  const char *se = getenv("GPMPC_FLEET_SOLVER");
+  // the specialised solver assumes the N = 20 stage layout of its LDS caps
+  f->use_fq = (!se || atoi(se) != 0) && N == 20 && f->pat.mode == 1 && f->pat.nblk == FQ_NBLK &&
+              m - n == FQ_MD && f->pat.nnz - n == FQ_NNZD;
   GPMPC_HIP(hipStreamSynchronize(ctx->stream));
   *out = f;
   return 0;
@@ -498,6 +721,38 @@ static hipError_t fleet_gp_posterior(gpmpc_fleet *f, int mask) {
   return e;
 }
 
+// Dispatch order for the control kernel.  Workgroups start in blockIdx order
+// and a landing's solve costs ~proportional to its ADMM iterations (25 or 50
+// here: 237 vs 490 us), so launching the landings whose last solve was
+// longest first is the LPT schedule over the 512 resident slots (measured
+// span 916 us vs 826 us LPT-ideal).  Terminated landings (they return at once)
+// go last.  Counting sort in one workgroup; the order inside a bucket is
+// arbitrary, which cannot change results: landings are independent.
+#define ORDER_BUCKETS 256
+__global__ __launch_bounds__(1024) void k_fleet_order(int B, const double *__restrict__ rec,
+                                                      const int *__restrict__ lastit,
+                                                      int *__restrict__ order) {
+  __shared__ int cnt[ORDER_BUCKETS];
+  for (int i = threadIdx.x; i < ORDER_BUCKETS; i += blockDim.x) cnt[i] = 0;
+  __syncthreads();
+  auto key = [&](int b) {  // larger = earlier; 0 = terminated
+    if (rec[(int64_t)b * GPMPC_REC_LEN] != 0.0) return 0;
+    return min(lastit[b], ORDER_BUCKETS - 2) + 1;
+  };
+  for (int b = threadIdx.x; b < B; b += blockDim.x) atomicAdd(&cnt[key(b)], 1);
+  __syncthreads();
+  if (threadIdx.x == 0) {  // descending exclusive scan
+    int run = 0;
+    for (int k = ORDER_BUCKETS - 1; k >= 0; --k) {
+      const int c = cnt[k];
+      cnt[k] = run;
+      run += c;
+    }
+  }
+  __syncthreads();
+  for (int b = threadIdx.x; b < B; b += blockDim.x) order[atomicAdd(&cnt[key(b)], 1)] = b;
+}
+
 static FleetArgs fleet_args(gpmpc_fleet *f) {
   FleetArgs a;
   a.pt = f->pat.dev;
@@ -512,6 +767,8 @@ static FleetArgs fleet_args(gpmpc_fleet *f) {
   a.ysc = f->ysc.as<double>(); a.rho = f->rho.as<double>(); a.rec = f->rec.as<double>();
   a.xt = f->xt.as<double>();
   a.gmean = f->mean.as<double>();
+  a.order = f->use_order ? f->order.as<int>() : nullptr;
+  a.lastit = f->lastit.as<int>();
   a.stamps = f->stamps;
   a.trace = f->trace;
   return a;
@@ -522,7 +779,13 @@ extern "C" int gpmpc_fleet_step_phases(gpmpc_fleet *f, int phase_mask) {
   GPMPC_HIP(hipSetDevice(f->ctx->device));
   if ((phase_mask & 13) && f->cfg.use_gp) GPMPC_HIP(fleet_gp_posterior(f, phase_mask));
   if (phase_mask & 2) {
-    hipLaunchKernelGGL(k_fleet_control, dim3(f->B), dim3(256), 0, f->ctx->stream, fleet_args(f));
+    if (f->use_order)
+      hipLaunchKernelGGL(k_fleet_order, dim3(1), dim3(1024), 0, f->ctx->stream, f->B,
+                         f->rec.as<double>(), f->lastit.as<int>(), f->order.as<int>());
+    if (f->use_fq)
+      hipLaunchKernelGGL(k_fleet_control2, dim3(f->B), dim3(FQ_T), 0, f->ctx->stream, fleet_args(f));
+    else
+      hipLaunchKernelGGL(k_fleet_control, dim3(f->B), dim3(256), 0, f->ctx->stream, fleet_args(f));
     GPMPC_HIP(hipGetLastError());
   }
   return 0;

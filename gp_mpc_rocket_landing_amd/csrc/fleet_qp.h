@@ -1,0 +1,579 @@
+// fleet_qp.h -- the fleet's OSQP-0.6 ADMM, specialised to the 3-DoF MPC QP so
+// that FOUR landings share a CU.
+//
+// The generic solver (qp_device.h) keeps every vector in LDS: 78 KB per QP,
+// two QPs per CU.  With 1024 landings on 512 slots and ~64% of solves running
+// the full 50 iterations (490 us vs 240 us for 25), 142 slots must run two
+// long solves back to back (measured span 916-967 us; no dispatch order can
+// beat 2 x 490 us).  At four per CU every landing starts at once.
+//
+// The MPC QP has a fixed row layout (fleet.hip mpc_pattern): rows 0..MD-1 are
+// the initial-state and dynamics equalities, rows MD..MD+n-1 are the identity
+// bound rows of variables 0..n-1.  A bound row touches only its own variable,
+// so a thread that owns variable j also owns row MD+j: the bound row's A entry,
+// l, u, E, y, z, rho z - y and delta y live in that thread's registers, as do
+// x, dx, P, q, D of the variable.  Only what crosses threads stays in LDS: the
+// dynamics rows' A values, their rho z - y (the A' operand), x~ (the block
+// solve's right-hand side) and the block-tridiagonal factor.  Checks stage x,
+// y, delta y, delta x through the x~ / (rho z - y) slots, which are dead then.
+//
+// 128 threads (2 waves): thread t owns variables t, t+128 and dynamics rows
+// 127-t, 255-t.  Every arithmetic expression is the generic solver's, in the
+// same order (same rounding), except the block-wide sums, whose tree now has
+// two waves.  LDS ~37 KB.
+#pragma once
+#include "qp_device.h"
+
+#define FQ_T 128
+#define FQ_MD 147     // dynamics rows: NX (N+1) at N = 20
+#define FQ_NNZD 527   // their nonzeros: NX + 26 N
+#define FQ_NMAX 224   // x~: n = 207 padded to whole blocks (210) + the solve's look-ahead reads
+#define FQ_NBLK 21
+#define FQ_FAC (FQ_NBLK * (QP_BLK_SZ * QP_BLK_SZ + QP_BLK_SZ * QP_BLK_CM) + 16)
+#define FQ_CMAX 6     // dynamics entries per column (<= 5) + 1
+#define FQ_RMAX 5     // entries per dynamics row
+
+struct FleetSmem {
+  double A[FQ_NNZD + 1];
+  double rhs[FQ_NMAX];   // x~ (block solve b); check-time scratch for x / dx
+  double zt[FQ_MD + 1];  // rho z - y of the dynamics rows; check-time scratch for y / dy
+  double band_store[FQ_FAC];
+  double gzero[64];      // zero "-G rows" of the non-coupled lanes (they read gzero[0..63])
+  double zslot, sink;
+  double red[2][16];
+  double c, rho_s;
+  int flag;
+  __device__ double *band() { return band_store; }
+};
+
+template <int K>
+__device__ __forceinline__ void fq_max(double (&v)[K], double (*red)[16]) {
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+#pragma unroll
+  for (int k = 0; k < K; ++k)
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v[k] = fmax(v[k], __shfl_xor(v[k], o));
+  __syncthreads();
+  if (lane == 0)
+#pragma unroll
+    for (int k = 0; k < K; ++k) red[wv][k] = v[k];
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < K; ++k) v[k] = fmax(red[0][k], red[1][k]);
+  __syncthreads();
+}
+
+template <int K>
+__device__ __forceinline__ void fq_sum(double (&v)[K], double (*red)[16]) {
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+#pragma unroll
+  for (int k = 0; k < K; ++k)
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v[k] += __shfl_xor(v[k], o);
+  __syncthreads();
+  if (lane == 0)
+#pragma unroll
+    for (int k = 0; k < K; ++k) red[wv][k] = v[k];
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < K; ++k) v[k] = red[0][k] + red[1][k];
+  __syncthreads();
+}
+
+__device__ __forceinline__ double fq_rho(double l, double u, double rs) {
+  if (l < -QP_OSQP_INFTY * QP_MIN_SCALING && u > QP_OSQP_INFTY * QP_MIN_SCALING) return QP_RHO_MIN;
+  if (u - l < QP_RHO_TOL) return QP_RHO_EQ * rs;
+  return rs;
+}
+
+// per-thread state: 2 variable slots (+ their bound rows), 2 dynamics-row slots
+struct FleetRegs {
+  bool vok[2], rok[2];
+  int vj[2], rr[2];
+  // variable j and bound row MD + j
+  double x[2], dx[2], P[2], q[2], D[2];
+  double Ab[2], lb[2], ub[2], Eb[2], yb[2], zb[2], dyb[2], ztb[2];
+  // dynamics rows
+  double lr[2], ur[2], Er[2], yr[2], zr[2], dyr[2];
+  // patterns: column j's dynamics entries (CSR value index, row), row r's entries
+  int cn[2], ca[2][FQ_CMAX], cr[2][FQ_CMAX];
+  int rb[2], rn[2], rc[2][FQ_RMAX];
+};
+
+__device__ __forceinline__ void fq_init_pattern(const QPPattern &pt, FleetRegs &R, int n) {
+  const int t = threadIdx.x;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int j = t + h * FQ_T;
+    R.vj[h] = j;
+    R.vok[h] = j < n;
+    R.cn[h] = 0;
+    if (R.vok[h]) {
+      const int k0 = pt.colptr[j], k1 = pt.colptr[j + 1] - 1;  // the last entry is the bound row
+      R.cn[h] = k1 - k0;
+#pragma unroll
+      for (int e = 0; e < FQ_CMAX; ++e) {
+        R.ca[h][e] = (e < R.cn[h]) ? pt.csc2csr[k0 + e] : 0;
+        R.cr[h][e] = (e < R.cn[h]) ? pt.cscrow[k0 + e] : 0;
+      }
+    }
+    const int r = (FQ_T - 1 - t) + h * FQ_T;
+    R.rr[h] = r;
+    R.rok[h] = r < FQ_MD;
+    R.rb[h] = R.rok[h] ? pt.rowptr[r] : 0;
+    R.rn[h] = R.rok[h] ? pt.rowptr[r + 1] - R.rb[h] : 0;
+#pragma unroll
+    for (int e = 0; e < FQ_RMAX; ++e) R.rc[h][e] = (e < R.rn[h]) ? pt.colidx[R.rb[h] + e] : 0;
+  }
+}
+
+// scaling.c scale_data over the split storage (qp_device.h qp_scale, same order)
+__device__ __forceinline__ void fq_scale(const QPPattern &pt, FleetSmem &s, FleetRegs &R, int iters) {
+  const int n = pt.n, tid = threadIdx.x;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) { R.D[h] = 1.0; R.Eb[h] = 1.0; R.Er[h] = 1.0; }
+  if (tid == 0) s.c = 1.0;
+  __syncthreads();
+  for (int it = 0; it < iters; ++it) {
+    // column factors -> rhs (scratch), row factors -> zt (dynamics) / register (bound)
+    double eb[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      if (R.vok[h]) {
+        double v = fabs(R.P[h]);
+        _Pragma("unroll") for (int e = 0; e < FQ_CMAX; ++e) if (e < R.cn[h]) v = fmax(v, fabs(s.A[R.ca[h][e]]));
+        v = fmax(v, fabs(R.Ab[h]));
+        s.rhs[R.vj[h]] = 1.0 / sqrt(qp_limit(v));
+        eb[h] = 1.0 / sqrt(qp_limit(fmax(0.0, fabs(R.Ab[h]))));
+      }
+      if (R.rok[h]) {
+        double v = 0.0;
+        _Pragma("unroll") for (int e = 0; e < FQ_RMAX; ++e) if (e < R.rn[h]) v = fmax(v, fabs(s.A[R.rb[h] + e]));
+        s.zt[R.rr[h]] = 1.0 / sqrt(qp_limit(v));
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      if (R.rok[h]) {
+        const double e = s.zt[R.rr[h]];
+        _Pragma("unroll") for (int k = 0; k < FQ_RMAX; ++k) if (k < R.rn[h]) {
+          const int a = R.rb[h] + k;
+          s.A[a] = e * s.A[a] * s.rhs[R.rc[h][k]];
+        }
+        R.Er[h] *= e;
+      }
+      if (R.vok[h]) {
+        const double d = s.rhs[R.vj[h]];
+        R.Ab[h] = eb[h] * R.Ab[h] * d;
+        R.Eb[h] *= eb[h];
+      }
+    }
+    double v[1] = {0.0};
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+      if (R.vok[h]) {
+        const double d = s.rhs[R.vj[h]];
+        R.P[h] = d * R.P[h] * d;
+        R.q[h] = d * R.q[h];
+        R.D[h] *= d;
+        v[0] += fabs(R.P[h]);
+      }
+    double mx[1] = {0.0};
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+      if (R.vok[h]) mx[0] = fmax(mx[0], fabs(R.q[h]));
+    fq_sum<1>(v, s.red);  // (its barriers also order the A / rhs updates above)
+    fq_max<1>(mx, s.red);
+    double ct = v[0] / n;
+    const double nq = qp_limit(mx[0]);
+    ct = qp_limit(fmax(ct, nq));
+    ct = 1.0 / ct;
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+      if (R.vok[h]) { R.P[h] *= ct; R.q[h] *= ct; }
+    if (tid == 0) s.c *= ct;
+    __syncthreads();
+  }
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    R.lb[h] = R.Eb[h] * R.lb[h]; R.ub[h] = R.Eb[h] * R.ub[h];
+    R.lr[h] = R.Er[h] * R.lr[h]; R.ur[h] = R.Er[h] * R.ur[h];
+  }
+}
+
+// assemble M = P + sigma I + A' R A into the block slots and factor it
+// (qp_device.h qp_factor, mode 1).  Diagonal slots are assembled by the owner
+// of their variable (its bound row is the slot's last term); the rest by all.
+__device__ __forceinline__ int fq_factor(const QPPattern &pt, FleetSmem &s, FleetRegs &R, double sigma) {
+  constexpr int SZ = QP_BLK_SZ, BS = SZ * SZ + SZ * QP_BLK_CM;
+  const int tid = threadIdx.x;
+  const double rs = s.rho_s;
+  for (int e = tid; e < pt.fac_len; e += FQ_T) {
+    const int d = pt.facdiag[e];
+    if (d >= 0) continue;
+    double v = (d == -2) ? 1.0 : 0.0;
+    for (int k = pt.facptr[e]; k < pt.facptr[e + 1]; ++k) {
+      const int r = pt.terms[3 * k], a = pt.terms[3 * k + 1], b = pt.terms[3 * k + 2];
+      const int h = 0;
+      (void)h;
+      v += QP_RHO_EQ * rs * s.A[a] * s.A[b];  // off-diagonal terms come from dynamics rows only
+      (void)r;
+    }
+    s.band_store[e] = v;
+  }
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    if (!R.vok[h]) continue;
+    const int j = R.vj[h], e = (j / SZ) * BS + (j % SZ) * (SZ + 1);
+    double v = R.P[h] + sigma;
+    for (int k = pt.facptr[e]; k < pt.facptr[e + 1]; ++k) {
+      const int r = pt.terms[3 * k], a = pt.terms[3 * k + 1], b = pt.terms[3 * k + 2];
+      if (r >= FQ_MD) v += fq_rho(R.lb[h], R.ub[h], rs) * R.Ab[h] * R.Ab[h];
+      else v += QP_RHO_EQ * rs * s.A[a] * s.A[b];
+    }
+    s.band_store[e] = v;
+  }
+  if (tid == 0) s.zslot = 0.0;
+  if (tid < 64) s.gzero[tid] = 0.0;
+  __syncthreads();
+  int f = 0;
+  if (tid < 64) f = blk_factor_dispatch(pt, s);
+  if (tid == 0) s.flag = f;
+  __syncthreads();
+  return s.flag;
+}
+
+// dynamics rows are equalities (l = u): their rho is rho_eq.  Checked once per
+// solve, so a pattern / data change that breaks it fails loudly.
+__device__ __forceinline__ bool fq_dyn_rows_are_equalities(FleetSmem &s, FleetRegs &R) {
+  double bad[1] = {0.0};
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+    if (R.rok[h] && !(R.ur[h] - R.lr[h] < QP_RHO_TOL)) bad[0] = 1.0;
+  fq_max<1>(bad, s.red);
+  return bad[0] == 0.0;
+}
+
+// residual norms (auxil.c update_info) and the rho-estimate quantities in one pass:
+// o: 0 pri  1 |z/E|  2 |Ax/E|  3 dua*c  4 |q/D|  5 |A'y/D|  6 |Px/D|
+// re: 0 |Ax - z|  1 max(|z|,|Ax|)  2 |q + Px + A'y|  3 max(|q|,|A'y|,|Px|)   (scaled)
+__device__ __forceinline__ void fq_update_info(FleetSmem &s, FleetRegs &R, double (&o)[8], double (&re)[4]) {
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    if (R.vok[h]) s.rhs[R.vj[h]] = R.x[h];
+    if (R.rok[h]) s.zt[R.rr[h]] = R.yr[h];
+  }
+  __syncthreads();
+  double v[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    if (R.rok[h]) {  // dynamics row: (A x)_r
+      double ax = 0.0;
+      _Pragma("unroll") for (int e = 0; e < FQ_RMAX; ++e) if (e < R.rn[h]) ax += s.A[R.rb[h] + e] * s.rhs[R.rc[h][e]];
+      const double e = R.Er[h], z = R.zr[h];
+      v[0] = fmax(v[0], fabs((ax - z) / e));
+      v[1] = fmax(v[1], fabs(z / e));
+      v[2] = fmax(v[2], fabs(ax / e));
+      v[8] = fmax(v[8], fabs(ax - z));
+      v[9] = fmax(v[9], fmax(fabs(z), fabs(ax)));
+    }
+    if (R.vok[h]) {
+      {  // bound row
+        const double ax = 0.0 + R.Ab[h] * R.x[h];
+        const double e = R.Eb[h], z = R.zb[h];
+        v[0] = fmax(v[0], fabs((ax - z) / e));
+        v[1] = fmax(v[1], fabs(z / e));
+        v[2] = fmax(v[2], fabs(ax / e));
+        v[8] = fmax(v[8], fabs(ax - z));
+        v[9] = fmax(v[9], fmax(fabs(z), fabs(ax)));
+      }
+      double aty = 0.0;  // (A' y)_j in CSC order, the bound row last
+      _Pragma("unroll") for (int e = 0; e < FQ_CMAX; ++e) if (e < R.cn[h]) aty += s.A[R.ca[h][e]] * s.zt[R.cr[h][e]];
+      aty += R.Ab[h] * R.yb[h];
+      const double px = R.P[h] * R.x[h], d = R.D[h], q = R.q[h];
+      v[3] = fmax(v[3], fabs((q + px + aty) / d));
+      v[4] = fmax(v[4], fabs(q / d));
+      v[5] = fmax(v[5], fabs(aty / d));
+      v[6] = fmax(v[6], fabs(px / d));
+      v[10] = fmax(v[10], fabs(q + px + aty));
+      v[11] = fmax(v[11], fmax(fmax(fabs(q), fabs(aty)), fabs(px)));
+    }
+  }
+  fq_max<12>(v, s.red);
+#pragma unroll
+  for (int k = 0; k < 8; ++k) o[k] = v[k];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) re[k] = v[8 + k];
+}
+
+__device__ __forceinline__ bool fq_primal_infeasible(FleetSmem &s, FleetRegs &R, double eps) {
+  double v[1] = {0.0};
+  auto proj = [](double d, double l, double u) {
+    const bool bu = u > QP_OSQP_INFTY * QP_MIN_SCALING;
+    const bool bl = l < -QP_OSQP_INFTY * QP_MIN_SCALING;
+    if (bu && bl) return 0.0;
+    if (bu) return fmin(d, 0.0);
+    if (bl) return fmax(d, 0.0);
+    return d;
+  };
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    if (R.rok[h]) {
+      R.dyr[h] = proj(R.dyr[h], R.lr[h], R.ur[h]);
+      v[0] = fmax(v[0], fabs(R.Er[h] * R.dyr[h]));
+    }
+    if (R.vok[h]) {
+      R.dyb[h] = proj(R.dyb[h], R.lb[h], R.ub[h]);
+      v[0] = fmax(v[0], fabs(R.Eb[h] * R.dyb[h]));
+    }
+  }
+  fq_max<1>(v, s.red);
+  const double nrm = v[0];
+  if (!(nrm > QP_DIV_TOL)) return false;
+  double sm[1] = {0.0};
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    if (R.rok[h]) sm[0] += R.ur[h] * fmax(R.dyr[h], 0.0) + R.lr[h] * fmin(R.dyr[h], 0.0);
+    if (R.vok[h]) sm[0] += R.ub[h] * fmax(R.dyb[h], 0.0) + R.lb[h] * fmin(R.dyb[h], 0.0);
+  }
+  fq_sum<1>(sm, s.red);
+  if (!(sm[0] < -eps * nrm)) return false;
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+    if (R.rok[h]) s.zt[R.rr[h]] = R.dyr[h];
+  __syncthreads();
+  double mx[1] = {0.0};
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+    if (R.vok[h]) {
+      double acc = 0.0;
+      _Pragma("unroll") for (int e = 0; e < FQ_CMAX; ++e) if (e < R.cn[h]) acc += s.A[R.ca[h][e]] * s.zt[R.cr[h][e]];
+      acc += R.Ab[h] * R.dyb[h];
+      mx[0] = fmax(mx[0], fabs(acc / R.D[h]));
+    }
+  fq_max<1>(mx, s.red);
+  return mx[0] < eps * nrm;
+}
+
+__device__ __forceinline__ bool fq_dual_infeasible(FleetSmem &s, FleetRegs &R, double eps) {
+  double v[1] = {0.0};
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+    if (R.vok[h]) v[0] = fmax(v[0], fabs(R.D[h] * R.dx[h]));
+  fq_max<1>(v, s.red);
+  const double nrm = v[0];
+  if (!(nrm > QP_DIV_TOL)) return false;
+  double a[1] = {0.0}, pm[1] = {0.0};
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+    if (R.vok[h]) {
+      a[0] += R.q[h] * R.dx[h];
+      pm[0] = fmax(pm[0], fabs(R.P[h] * R.dx[h] / R.D[h]));
+    }
+  fq_sum<1>(a, s.red);
+  fq_max<1>(pm, s.red);
+  if (!(a[0] < s.c * eps * nrm)) return false;
+  if (!(pm[0] < s.c * eps * nrm)) return false;
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+    if (R.vok[h]) s.rhs[R.vj[h]] = R.dx[h];
+  __syncthreads();
+  double bad[1] = {0.0};
+  auto test = [&](double vv, double l, double u) {
+    if ((u < QP_OSQP_INFTY * QP_MIN_SCALING && vv > eps * nrm) ||
+        (l > -QP_OSQP_INFTY * QP_MIN_SCALING && vv < -eps * nrm))
+      bad[0] = 1.0;
+  };
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    if (R.rok[h]) {
+      double adx = 0.0;
+      _Pragma("unroll") for (int e = 0; e < FQ_RMAX; ++e) if (e < R.rn[h]) adx += s.A[R.rb[h] + e] * s.rhs[R.rc[h][e]];
+      test(adx / R.Er[h], R.lr[h], R.ur[h]);
+    }
+    if (R.vok[h]) test((0.0 + R.Ab[h] * R.dx[h]) / R.Eb[h], R.lb[h], R.ub[h]);
+  }
+  fq_max<1>(bad, s.red);
+  return bad[0] == 0.0;
+}
+
+__device__ __forceinline__ bool fq_check(FleetSmem &s, FleetRegs &R, const QPSettingsDev &st, const double (&o)[8],
+                         bool approx, int &status) {
+  const double pri = o[0], dua = o[3] / s.c;
+  double ea = st.eps_abs, er = st.eps_rel, epi = st.eps_prim_inf, edi = st.eps_dual_inf;
+  if (pri > QP_OSQP_INFTY || dua > QP_OSQP_INFTY) {
+    status = -7;
+    return true;
+  }
+  if (approx) { ea *= 10; er *= 10; epi *= 10; edi *= 10; }
+  bool prim_ok = false, prim_inf = false, dual_ok = false, dual_inf = false;
+  if (pri < ea + er * fmax(o[1], o[2])) prim_ok = true;
+  else prim_inf = fq_primal_infeasible(s, R, epi);
+  if (dua < ea + er * fmax(fmax(o[4], o[5]), o[6]) / s.c) dual_ok = true;
+  else dual_inf = fq_dual_infeasible(s, R, edi);
+  if (prim_ok && dual_ok) { status = approx ? 2 : 1; return true; }
+  if (prim_inf) { status = approx ? 3 : -3; return true; }
+  if (dual_inf) { status = approx ? 4 : -4; return true; }
+  return false;
+}
+
+__device__ __forceinline__ double fq_rho_estimate(const FleetSmem &s, const double (&re)[4]) {
+  const double pr = re[0] / (re[1] + 1e-10);
+  const double du = re[2] / (re[3] + 1e-10);
+  const double est = s.rho_s * sqrt(pr / (du + 1e-10));
+  return fmin(fmax(est, QP_RHO_MIN), QP_RHO_MAX);
+}
+
+__device__ __forceinline__ void fq_rebuild_zt(FleetSmem &s, FleetRegs &R) {
+  const double rs = s.rho_s;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    if (R.rok[h]) s.zt[R.rr[h]] = QP_RHO_EQ * rs * R.zr[h] - R.yr[h];
+    if (R.vok[h]) R.ztb[h] = fq_rho(R.lb[h], R.ub[h], rs) * R.zb[h] - R.yb[h];
+  }
+  __syncthreads();
+}
+
+// The solve (qp_device.h qp_solve): on entry R holds the unscaled P, q, l, u,
+// bound-row A entries, the warm-start x and the persistent scaled y, s.A the
+// unscaled dynamics rows, s.rho_s the persistent rho.  On exit R.x / R.y* hold
+// the scaled iterates, R.D / E* and s.c the scaling.
+__device__ __forceinline__ QPResult fq_solve(const QPPattern &pt, FleetSmem &s, FleetRegs &R,
+                             const QPSettingsDev &st, QPStamps *ts = nullptr) {
+  const int n = pt.n, tid = threadIdx.x;
+  QPResult res{-10, 0, 0.0, 0};
+  QPStamps dummy;
+  QPStamps &T = ts ? *ts : dummy;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    R.lb[h] = fmax(R.lb[h], -QP_OSQP_INFTY); R.ub[h] = fmin(R.ub[h], QP_OSQP_INFTY);
+    R.lr[h] = fmax(R.lr[h], -QP_OSQP_INFTY); R.ur[h] = fmin(R.ur[h], QP_OSQP_INFTY);
+  }
+  if (st.scaling) fq_scale(pt, s, R, st.scaling);
+  else {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) { R.D[h] = 1.0; R.Eb[h] = 1.0; R.Er[h] = 1.0; }
+    if (tid == 0) s.c = 1.0;
+  }
+  // the block solve reads b in whole blocks (plus look-ahead): zero the tail
+  for (int j = n + tid; j < FQ_NMAX; j += FQ_T) s.rhs[j] = 0.0;
+  if (tid == 0) s.rho_s = fmin(fmax(s.rho_s, QP_RHO_MIN), QP_RHO_MAX);
+  __syncthreads();
+  if (!fq_dyn_rows_are_equalities(s, R)) { res.factor_fail = -1; return res; }
+  T.mark(1);
+  int f = fq_factor(pt, s, R, st.sigma);
+  T.mark(2);
+  if (f) { res.factor_fail = f; return res; }
+  if (st.warm_start) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+      if (R.vok[h]) { R.x[h] = R.x[h] / R.D[h]; s.rhs[R.vj[h]] = R.x[h]; }
+    __syncthreads();
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {  // z = A x
+      if (R.rok[h]) {
+        double acc = 0.0;
+        _Pragma("unroll") for (int e = 0; e < FQ_RMAX; ++e) if (e < R.rn[h]) acc += s.A[R.rb[h] + e] * s.rhs[R.rc[h][e]];
+        R.zr[h] = acc;
+      }
+      if (R.vok[h]) R.zb[h] = 0.0 + R.Ab[h] * R.x[h];
+    }
+  } else {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      R.x[h] = 0.0; R.zr[h] = 0.0; R.yr[h] = 0.0; R.zb[h] = 0.0; R.yb[h] = 0.0;
+    }
+  }
+  __syncthreads();
+  const double sig = st.sigma, al = st.alpha;
+  fq_rebuild_zt(s, R);
+  bool can_check = false;
+  int it;
+  double o[8], re[4];
+  for (it = 1; it <= st.max_iter; ++it) {
+    // rhs = sigma x - q + A'(rho z - y)
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+      if (R.vok[h]) {
+        double acc = 0.0;
+        _Pragma("unroll") for (int e = 0; e < FQ_CMAX; ++e) if (e < R.cn[h]) acc += s.A[R.ca[h][e]] * s.zt[R.cr[h][e]];
+        acc += R.Ab[h] * R.ztb[h];
+        s.rhs[R.vj[h]] = sig * R.x[h] - R.q[h] + acc;
+      }
+    __syncthreads();
+    T.mark(3);
+    blk_solve_dispatch(pt, s, s.rhs, &T);  // x~ (wave 0)
+    __syncthreads();
+    T.mark(4);
+    const double rs = s.rho_s;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      if (R.vok[h]) {
+        const double xt = s.rhs[R.vj[h]];
+        const double xo = R.x[h];
+        const double xn = al * xt + (1.0 - al) * xo;
+        R.dx[h] = xn - xo;
+        R.x[h] = xn;
+        // bound row: z~ = A_b x~_j
+        const double ztl = 0.0 + R.Ab[h] * xt;
+        const double rho = fq_rho(R.lb[h], R.ub[h], rs), zo = R.zb[h], yo = R.yb[h];
+        const double zr = al * ztl + (1.0 - al) * zo;
+        double zn = zr + yo / rho;
+        zn = fmin(fmax(zn, R.lb[h]), R.ub[h]);
+        const double d = rho * (zr - zn);
+        const double yn = yo + d;
+        R.dyb[h] = d; R.yb[h] = yn; R.zb[h] = zn;
+        R.ztb[h] = rho * zn - yn;
+      }
+      if (R.rok[h]) {
+        double ztl = 0.0;
+        _Pragma("unroll") for (int e = 0; e < FQ_RMAX; ++e) if (e < R.rn[h]) ztl += s.A[R.rb[h] + e] * s.rhs[R.rc[h][e]];
+        const double rho = QP_RHO_EQ * rs, zo = R.zr[h], yo = R.yr[h];
+        const double zr = al * ztl + (1.0 - al) * zo;
+        double zn = zr + yo / rho;
+        zn = fmin(fmax(zn, R.lr[h]), R.ur[h]);
+        const double d = rho * (zr - zn);
+        const double yn = yo + d;
+        R.dyr[h] = d; R.yr[h] = yn; R.zr[h] = zn;
+        s.zt[R.rr[h]] = rho * zn - yn;
+      }
+    }
+    __syncthreads();
+    T.mark(5);
+    can_check = st.check_termination && (it % st.check_termination == 0);
+    const bool adapt = st.adaptive_rho && st.adaptive_rho_interval && (it % st.adaptive_rho_interval == 0);
+    if (can_check || adapt) {
+      res.iter = it;
+      fq_update_info(s, R, o, re);
+    }
+    if (can_check && fq_check(s, R, st, o, false, res.status)) break;
+    if (adapt) {
+      const double est = fq_rho_estimate(s, re);
+      if (est > s.rho_s * st.adaptive_rho_tolerance || est < s.rho_s / st.adaptive_rho_tolerance) {
+        __syncthreads();
+        if (tid == 0) s.rho_s = est;
+        __syncthreads();
+        f = fq_factor(pt, s, R, st.sigma);
+        if (f) { res.factor_fail = f; return res; }
+      }
+    }
+    if (can_check || adapt) fq_rebuild_zt(s, R);
+    T.mark(6);
+  }
+  if (!can_check) {
+    res.iter = it - 1;
+    fq_update_info(s, R, o, re);
+    fq_check(s, R, st, o, false, res.status);
+  }
+  if (res.status == -10) {
+    if (!fq_check(s, R, st, o, true, res.status)) res.status = -2;
+  }
+  double ob[1] = {0.0};
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+    if (R.vok[h]) ob[0] += 0.5 * R.x[h] * (R.P[h] * R.x[h]) + R.q[h] * R.x[h];
+  fq_sum<1>(ob, s.red);
+  res.obj = ob[0] / s.c;
+  return res;
+}

@@ -199,7 +199,8 @@ template <int SZ, int CM, class S>
 __device__ void blk_solve(const QPPattern &pt, S &s, double *b, QPStamps *T = nullptr) {
   if (threadIdx.x >= 64) return;
   constexpr int BS = SZ * SZ + SZ * CM;
-  static_assert(BS + SZ * CM <= sizeof(s.gzero) / sizeof(double), "gzero too small");
+  // non-coupled lanes keep pg = gzero (gstep 0) and read gzero[j * CM], j < SZ
+  static_assert((SZ - 1) * CM + 1 <= sizeof(s.gzero) / sizeof(double), "gzero too small");
   const int lane = threadIdx.x, rr = lane & 15, row = lane >> 4;
   const int rs = rr < SZ ? rr : SZ - 1, rc = rr < CM ? rr : CM - 1;
   const bool wr = rr < SZ;

@@ -67,7 +67,7 @@ struct QPSmem {
   double band_store[NMAX * (W + 1) + 4 * (W + 1) + 64];
   double red[4][8];
   double zslot, sink;  // block solve: a 0.0 source and a write sink for idle lanes
-  double gzero[240];   // block solve: zero "-G rows" of non-coupled lanes (>= BS + SZ*CM)
+  double gzero[64];    // block solve: zero "-G rows" of non-coupled lanes (>= (SZ-1)*CM + 1)
   double c, rho_s;
   int flag;
 };
