@@ -41,6 +41,7 @@ struct gpmpc_fleet {
   unsigned long long *trace = nullptr;       // diagnostic (gpmpc_fleet_set_trace)
   bool use_order = true;                     // GPMPC_FLEET_ORDER=0 launches in landing order
   bool use_fq = true;                        // fleet-specialised solver (GPMPC_FLEET_SOLVER=0: generic)
+  int alt_wave = 0;                          // GPMPC_FLEET_ALTWAVE=1: alternate the chain wave
 };
 
 extern "C" int gpmpc_fleet_set_stamps(gpmpc_fleet *f, void *dev_u64x16) {
@@ -165,6 +166,7 @@ struct FleetArgs {
   double *x, *Xw, *Uw, *ysc, *rho, *rec, *xt;
   const double *gmean;  // (B*N) x 3
   const int *order;     // workgroup -> landing (longest predicted first), or null
+  int alt_wave;         // fleet solver: odd workgroups run the KKT chain on wave 1
   int *lastit;          // ADMM iterations of each landing's last solve
   unsigned long long *stamps;  // diagnostic phase cycles of block 0 (or null)
   unsigned long long *trace;   // diagnostic per-landing placement/timing (or null)
@@ -519,12 +521,12 @@ __global__ __launch_bounds__(FQ_T) __attribute__((amdgpu_waves_per_eu(2, 2))) vo
 #pragma unroll
   for (int h = 0; h < 2; ++h)
     if (R.rok[h]) {
-      R.lr[h] = R.ur[h] = s.zt[R.rr[h]];
+      R.ur[h] = s.zt[R.rr[h]];  // l = u
       R.yr[h] = a.ysc[(int64_t)b * m + R.rr[h]];
     }
   __syncthreads();
   T.mark(0);
-  QPResult res = fq_solve(a.pt, s, R, a.st, &T);
+  QPResult res = fq_solve(a.pt, s, R, a.st, &T, a.alt_wave ? (int)(blockIdx.x & 1) : 0);
   T.mark(7);
   const bool has = !res.factor_fail && (res.status == 1 || res.status == 2 || res.status == -2);
   if (has) {
@@ -667,6 +669,8 @@ extern "C" int gpmpc_fleet_create(gpmpc_ctx *ctx, gpmpc_gp *gp, const gpmpc_flee
   hipMemsetAsync(f->lastit.p, 0, sizeof(int) * B, ctx->stream);
   const char *oe = getenv("GPMPC_FLEET_ORDER");
   f->use_order = !oe || atoi(oe) != 0;
+  const char *aw = getenv("GPMPC_FLEET_ALTWAVE");
+  f->alt_wave = aw ? atoi(aw) != 0 : 0;
   const char *se = getenv("GPMPC_FLEET_SOLVER");
   // the specialised solver assumes the N = 20 stage layout of its LDS caps
   f->use_fq = (!se || atoi(se) != 0) && N == 20 && f->pat.mode == 1 && f->pat.nblk == FQ_NBLK &&
@@ -768,6 +772,7 @@ static FleetArgs fleet_args(gpmpc_fleet *f) {
   a.xt = f->xt.as<double>();
   a.gmean = f->mean.as<double>();
   a.order = f->use_order ? f->order.as<int>() : nullptr;
+  a.alt_wave = f->alt_wave;
   a.lastit = f->lastit.as<int>();
   a.stamps = f->stamps;
   a.trace = f->trace;

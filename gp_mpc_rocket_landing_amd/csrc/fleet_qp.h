@@ -20,7 +20,10 @@
 // 128 threads (2 waves): thread t owns variables t, t+128 and dynamics rows
 // 127-t, 255-t.  Every arithmetic expression is the generic solver's, in the
 // same order (same rounding), except the block-wide sums, whose tree now has
-// two waves.  LDS ~37 KB.
+// two waves.  The dynamics rows are equalities (l = u, built so by the fleet),
+// so one bound value serves both.  The row scaling E lives in LDS (only the
+// scaling and the checks read it); the row / column patterns are packed in
+// 16-bit pairs to keep the register budget at 256.  LDS ~39.7 KB.
 #pragma once
 #include "qp_device.h"
 
@@ -37,6 +40,7 @@ struct FleetSmem {
   double A[FQ_NNZD + 1];
   double rhs[FQ_NMAX];   // x~ (block solve b); check-time scratch for x / dx
   double zt[FQ_MD + 1];  // rho z - y of the dynamics rows; check-time scratch for y / dy
+  double E[FQ_MD + FQ_NMAX];  // row scaling: dynamics rows, then bound row MD + j
   double band_store[FQ_FAC];
   double gzero[64];      // zero "-G rows" of the non-coupled lanes (they read gzero[0..63])
   double zslot, sink;
@@ -92,12 +96,18 @@ struct FleetRegs {
   int vj[2], rr[2];
   // variable j and bound row MD + j
   double x[2], dx[2], P[2], q[2], D[2];
-  double Ab[2], lb[2], ub[2], Eb[2], yb[2], zb[2], dyb[2], ztb[2];
-  // dynamics rows
-  double lr[2], ur[2], Er[2], yr[2], zr[2], dyr[2];
-  // patterns: column j's dynamics entries (CSR value index, row), row r's entries
-  int cn[2], ca[2][FQ_CMAX], cr[2][FQ_CMAX];
-  int rb[2], rn[2], rc[2][FQ_RMAX];
+  double Ab[2], lb[2], ub[2], yb[2], zb[2], dyb[2], ztb[2];
+  // dynamics rows (l = u = ur)
+  double ur[2], yr[2], zr[2], dyr[2];
+  // patterns: column j's dynamics entries, (CSR value index) | (row << 16);
+  // row r: first value index | count << 16, column indices two per int
+  int cn[2], cp[2][FQ_CMAX];
+  int rbn[2], rcp[2][(FQ_RMAX + 1) / 2];
+  __device__ __forceinline__ int ca(int h, int e) const { return cp[h][e] & 0xffff; }
+  __device__ __forceinline__ int cr(int h, int e) const { return cp[h][e] >> 16; }
+  __device__ __forceinline__ int rb(int h) const { return rbn[h] & 0xffff; }
+  __device__ __forceinline__ int rn(int h) const { return rbn[h] >> 16; }
+  __device__ __forceinline__ int rc(int h, int e) const { return (rcp[h][e >> 1] >> (16 * (e & 1))) & 0xffff; }
 };
 
 __device__ __forceinline__ void fq_init_pattern(const QPPattern &pt, FleetRegs &R, int n) {
@@ -112,18 +122,24 @@ __device__ __forceinline__ void fq_init_pattern(const QPPattern &pt, FleetRegs &
       const int k0 = pt.colptr[j], k1 = pt.colptr[j + 1] - 1;  // the last entry is the bound row
       R.cn[h] = k1 - k0;
 #pragma unroll
-      for (int e = 0; e < FQ_CMAX; ++e) {
-        R.ca[h][e] = (e < R.cn[h]) ? pt.csc2csr[k0 + e] : 0;
-        R.cr[h][e] = (e < R.cn[h]) ? pt.cscrow[k0 + e] : 0;
-      }
+      for (int e = 0; e < FQ_CMAX; ++e)
+        R.cp[h][e] = (e < R.cn[h]) ? (pt.csc2csr[k0 + e] | (pt.cscrow[k0 + e] << 16)) : 0;
+    } else {
+#pragma unroll
+      for (int e = 0; e < FQ_CMAX; ++e) R.cp[h][e] = 0;
     }
     const int r = (FQ_T - 1 - t) + h * FQ_T;
     R.rr[h] = r;
     R.rok[h] = r < FQ_MD;
-    R.rb[h] = R.rok[h] ? pt.rowptr[r] : 0;
-    R.rn[h] = R.rok[h] ? pt.rowptr[r + 1] - R.rb[h] : 0;
+    const int rb = R.rok[h] ? pt.rowptr[r] : 0;
+    const int rn = R.rok[h] ? pt.rowptr[r + 1] - rb : 0;
+    R.rbn[h] = rb | (rn << 16);
 #pragma unroll
-    for (int e = 0; e < FQ_RMAX; ++e) R.rc[h][e] = (e < R.rn[h]) ? pt.colidx[R.rb[h] + e] : 0;
+    for (int e = 0; e < (FQ_RMAX + 1) / 2; ++e) {
+      const int c0 = (2 * e < rn) ? pt.colidx[rb + 2 * e] : 0;
+      const int c1 = (2 * e + 1 < rn) ? pt.colidx[rb + 2 * e + 1] : 0;
+      R.rcp[h][e] = c0 | (c1 << 16);
+    }
   }
 }
 
@@ -131,7 +147,11 @@ __device__ __forceinline__ void fq_init_pattern(const QPPattern &pt, FleetRegs &
 __device__ __forceinline__ void fq_scale(const QPPattern &pt, FleetSmem &s, FleetRegs &R, int iters) {
   const int n = pt.n, tid = threadIdx.x;
 #pragma unroll
-  for (int h = 0; h < 2; ++h) { R.D[h] = 1.0; R.Eb[h] = 1.0; R.Er[h] = 1.0; }
+  for (int h = 0; h < 2; ++h) {
+    R.D[h] = 1.0;
+    if (R.vok[h]) s.E[FQ_MD + R.vj[h]] = 1.0;
+    if (R.rok[h]) s.E[R.rr[h]] = 1.0;
+  }
   if (tid == 0) s.c = 1.0;
   __syncthreads();
   for (int it = 0; it < iters; ++it) {
@@ -141,14 +161,14 @@ __device__ __forceinline__ void fq_scale(const QPPattern &pt, FleetSmem &s, Flee
     for (int h = 0; h < 2; ++h) {
       if (R.vok[h]) {
         double v = fabs(R.P[h]);
-        _Pragma("unroll") for (int e = 0; e < FQ_CMAX; ++e) if (e < R.cn[h]) v = fmax(v, fabs(s.A[R.ca[h][e]]));
+        _Pragma("unroll") for (int e = 0; e < FQ_CMAX; ++e) if (e < R.cn[h]) v = fmax(v, fabs(s.A[R.ca(h, e)]));
         v = fmax(v, fabs(R.Ab[h]));
         s.rhs[R.vj[h]] = 1.0 / sqrt(qp_limit(v));
         eb[h] = 1.0 / sqrt(qp_limit(fmax(0.0, fabs(R.Ab[h]))));
       }
       if (R.rok[h]) {
         double v = 0.0;
-        _Pragma("unroll") for (int e = 0; e < FQ_RMAX; ++e) if (e < R.rn[h]) v = fmax(v, fabs(s.A[R.rb[h] + e]));
+        _Pragma("unroll") for (int e = 0; e < FQ_RMAX; ++e) if (e < R.rn(h)) v = fmax(v, fabs(s.A[R.rb(h) + e]));
         s.zt[R.rr[h]] = 1.0 / sqrt(qp_limit(v));
       }
     }
@@ -157,16 +177,16 @@ __device__ __forceinline__ void fq_scale(const QPPattern &pt, FleetSmem &s, Flee
     for (int h = 0; h < 2; ++h) {
       if (R.rok[h]) {
         const double e = s.zt[R.rr[h]];
-        _Pragma("unroll") for (int k = 0; k < FQ_RMAX; ++k) if (k < R.rn[h]) {
-          const int a = R.rb[h] + k;
-          s.A[a] = e * s.A[a] * s.rhs[R.rc[h][k]];
+        _Pragma("unroll") for (int k = 0; k < FQ_RMAX; ++k) if (k < R.rn(h)) {
+          const int a = R.rb(h) + k;
+          s.A[a] = e * s.A[a] * s.rhs[R.rc(h, k)];
         }
-        R.Er[h] *= e;
+        s.E[R.rr[h]] *= e;
       }
       if (R.vok[h]) {
         const double d = s.rhs[R.vj[h]];
         R.Ab[h] = eb[h] * R.Ab[h] * d;
-        R.Eb[h] *= eb[h];
+        s.E[FQ_MD + R.vj[h]] *= eb[h];
       }
     }
     double v[1] = {0.0};
@@ -197,15 +217,19 @@ __device__ __forceinline__ void fq_scale(const QPPattern &pt, FleetSmem &s, Flee
   }
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
-    R.lb[h] = R.Eb[h] * R.lb[h]; R.ub[h] = R.Eb[h] * R.ub[h];
-    R.lr[h] = R.Er[h] * R.lr[h]; R.ur[h] = R.Er[h] * R.ur[h];
+    if (R.vok[h]) {
+      const double e = s.E[FQ_MD + R.vj[h]];
+      R.lb[h] = e * R.lb[h]; R.ub[h] = e * R.ub[h];
+    }
+    if (R.rok[h]) R.ur[h] = s.E[R.rr[h]] * R.ur[h];
   }
 }
 
 // assemble M = P + sigma I + A' R A into the block slots and factor it
 // (qp_device.h qp_factor, mode 1).  Diagonal slots are assembled by the owner
 // of their variable (its bound row is the slot's last term); the rest by all.
-__device__ __forceinline__ int fq_factor(const QPPattern &pt, FleetSmem &s, FleetRegs &R, double sigma) {
+__device__ __forceinline__ int fq_factor(const QPPattern &pt, FleetSmem &s, FleetRegs &R, double sigma,
+                                         int cw) {
   constexpr int SZ = QP_BLK_SZ, BS = SZ * SZ + SZ * QP_BLK_CM;
   const int tid = threadIdx.x;
   const double rs = s.rho_s;
@@ -238,21 +262,10 @@ __device__ __forceinline__ int fq_factor(const QPPattern &pt, FleetSmem &s, Flee
   if (tid < 64) s.gzero[tid] = 0.0;
   __syncthreads();
   int f = 0;
-  if (tid < 64) f = blk_factor_dispatch(pt, s);
+  if ((tid >> 6) == cw) f = blk_factor_dispatch(pt, s);
   if (tid == 0) s.flag = f;
   __syncthreads();
   return s.flag;
-}
-
-// dynamics rows are equalities (l = u): their rho is rho_eq.  Checked once per
-// solve, so a pattern / data change that breaks it fails loudly.
-__device__ __forceinline__ bool fq_dyn_rows_are_equalities(FleetSmem &s, FleetRegs &R) {
-  double bad[1] = {0.0};
-#pragma unroll
-  for (int h = 0; h < 2; ++h)
-    if (R.rok[h] && !(R.ur[h] - R.lr[h] < QP_RHO_TOL)) bad[0] = 1.0;
-  fq_max<1>(bad, s.red);
-  return bad[0] == 0.0;
 }
 
 // residual norms (auxil.c update_info) and the rho-estimate quantities in one pass:
@@ -270,8 +283,8 @@ __device__ __forceinline__ void fq_update_info(FleetSmem &s, FleetRegs &R, doubl
   for (int h = 0; h < 2; ++h) {
     if (R.rok[h]) {  // dynamics row: (A x)_r
       double ax = 0.0;
-      _Pragma("unroll") for (int e = 0; e < FQ_RMAX; ++e) if (e < R.rn[h]) ax += s.A[R.rb[h] + e] * s.rhs[R.rc[h][e]];
-      const double e = R.Er[h], z = R.zr[h];
+      _Pragma("unroll") for (int e = 0; e < FQ_RMAX; ++e) if (e < R.rn(h)) ax += s.A[R.rb(h) + e] * s.rhs[R.rc(h, e)];
+      const double e = s.E[R.rr[h]], z = R.zr[h];
       v[0] = fmax(v[0], fabs((ax - z) / e));
       v[1] = fmax(v[1], fabs(z / e));
       v[2] = fmax(v[2], fabs(ax / e));
@@ -281,7 +294,7 @@ __device__ __forceinline__ void fq_update_info(FleetSmem &s, FleetRegs &R, doubl
     if (R.vok[h]) {
       {  // bound row
         const double ax = 0.0 + R.Ab[h] * R.x[h];
-        const double e = R.Eb[h], z = R.zb[h];
+        const double e = s.E[FQ_MD + R.vj[h]], z = R.zb[h];
         v[0] = fmax(v[0], fabs((ax - z) / e));
         v[1] = fmax(v[1], fabs(z / e));
         v[2] = fmax(v[2], fabs(ax / e));
@@ -289,7 +302,7 @@ __device__ __forceinline__ void fq_update_info(FleetSmem &s, FleetRegs &R, doubl
         v[9] = fmax(v[9], fmax(fabs(z), fabs(ax)));
       }
       double aty = 0.0;  // (A' y)_j in CSC order, the bound row last
-      _Pragma("unroll") for (int e = 0; e < FQ_CMAX; ++e) if (e < R.cn[h]) aty += s.A[R.ca[h][e]] * s.zt[R.cr[h][e]];
+      _Pragma("unroll") for (int e = 0; e < FQ_CMAX; ++e) if (e < R.cn[h]) aty += s.A[R.ca(h, e)] * s.zt[R.cr(h, e)];
       aty += R.Ab[h] * R.yb[h];
       const double px = R.P[h] * R.x[h], d = R.D[h], q = R.q[h];
       v[3] = fmax(v[3], fabs((q + px + aty) / d));
@@ -320,12 +333,12 @@ __device__ __forceinline__ bool fq_primal_infeasible(FleetSmem &s, FleetRegs &R,
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
     if (R.rok[h]) {
-      R.dyr[h] = proj(R.dyr[h], R.lr[h], R.ur[h]);
-      v[0] = fmax(v[0], fabs(R.Er[h] * R.dyr[h]));
+      R.dyr[h] = proj(R.dyr[h], R.ur[h], R.ur[h]);
+      v[0] = fmax(v[0], fabs(s.E[R.rr[h]] * R.dyr[h]));
     }
     if (R.vok[h]) {
       R.dyb[h] = proj(R.dyb[h], R.lb[h], R.ub[h]);
-      v[0] = fmax(v[0], fabs(R.Eb[h] * R.dyb[h]));
+      v[0] = fmax(v[0], fabs(s.E[FQ_MD + R.vj[h]] * R.dyb[h]));
     }
   }
   fq_max<1>(v, s.red);
@@ -334,7 +347,7 @@ __device__ __forceinline__ bool fq_primal_infeasible(FleetSmem &s, FleetRegs &R,
   double sm[1] = {0.0};
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
-    if (R.rok[h]) sm[0] += R.ur[h] * fmax(R.dyr[h], 0.0) + R.lr[h] * fmin(R.dyr[h], 0.0);
+    if (R.rok[h]) sm[0] += R.ur[h] * fmax(R.dyr[h], 0.0) + R.ur[h] * fmin(R.dyr[h], 0.0);
     if (R.vok[h]) sm[0] += R.ub[h] * fmax(R.dyb[h], 0.0) + R.lb[h] * fmin(R.dyb[h], 0.0);
   }
   fq_sum<1>(sm, s.red);
@@ -348,7 +361,7 @@ __device__ __forceinline__ bool fq_primal_infeasible(FleetSmem &s, FleetRegs &R,
   for (int h = 0; h < 2; ++h)
     if (R.vok[h]) {
       double acc = 0.0;
-      _Pragma("unroll") for (int e = 0; e < FQ_CMAX; ++e) if (e < R.cn[h]) acc += s.A[R.ca[h][e]] * s.zt[R.cr[h][e]];
+      _Pragma("unroll") for (int e = 0; e < FQ_CMAX; ++e) if (e < R.cn[h]) acc += s.A[R.ca(h, e)] * s.zt[R.cr(h, e)];
       acc += R.Ab[h] * R.dyb[h];
       mx[0] = fmax(mx[0], fabs(acc / R.D[h]));
     }
@@ -389,10 +402,10 @@ __device__ __forceinline__ bool fq_dual_infeasible(FleetSmem &s, FleetRegs &R, d
   for (int h = 0; h < 2; ++h) {
     if (R.rok[h]) {
       double adx = 0.0;
-      _Pragma("unroll") for (int e = 0; e < FQ_RMAX; ++e) if (e < R.rn[h]) adx += s.A[R.rb[h] + e] * s.rhs[R.rc[h][e]];
-      test(adx / R.Er[h], R.lr[h], R.ur[h]);
+      _Pragma("unroll") for (int e = 0; e < FQ_RMAX; ++e) if (e < R.rn(h)) adx += s.A[R.rb(h) + e] * s.rhs[R.rc(h, e)];
+      test(adx / s.E[R.rr[h]], R.ur[h], R.ur[h]);
     }
-    if (R.vok[h]) test((0.0 + R.Ab[h] * R.dx[h]) / R.Eb[h], R.lb[h], R.ub[h]);
+    if (R.vok[h]) test((0.0 + R.Ab[h] * R.dx[h]) / s.E[FQ_MD + R.vj[h]], R.lb[h], R.ub[h]);
   }
   fq_max<1>(bad, s.red);
   return bad[0] == 0.0;
@@ -440,7 +453,7 @@ __device__ __forceinline__ void fq_rebuild_zt(FleetSmem &s, FleetRegs &R) {
 // unscaled dynamics rows, s.rho_s the persistent rho.  On exit R.x / R.y* hold
 // the scaled iterates, R.D / E* and s.c the scaling.
 __device__ __forceinline__ QPResult fq_solve(const QPPattern &pt, FleetSmem &s, FleetRegs &R,
-                             const QPSettingsDev &st, QPStamps *ts = nullptr) {
+                             const QPSettingsDev &st, QPStamps *ts = nullptr, int cw = 0) {
   const int n = pt.n, tid = threadIdx.x;
   QPResult res{-10, 0, 0.0, 0};
   QPStamps dummy;
@@ -448,21 +461,24 @@ __device__ __forceinline__ QPResult fq_solve(const QPPattern &pt, FleetSmem &s, 
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
     R.lb[h] = fmax(R.lb[h], -QP_OSQP_INFTY); R.ub[h] = fmin(R.ub[h], QP_OSQP_INFTY);
-    R.lr[h] = fmax(R.lr[h], -QP_OSQP_INFTY); R.ur[h] = fmin(R.ur[h], QP_OSQP_INFTY);
+    R.ur[h] = fmin(fmax(R.ur[h], -QP_OSQP_INFTY), QP_OSQP_INFTY);
   }
   if (st.scaling) fq_scale(pt, s, R, st.scaling);
   else {
 #pragma unroll
-    for (int h = 0; h < 2; ++h) { R.D[h] = 1.0; R.Eb[h] = 1.0; R.Er[h] = 1.0; }
+    for (int h = 0; h < 2; ++h) {
+      R.D[h] = 1.0;
+      if (R.vok[h]) s.E[FQ_MD + R.vj[h]] = 1.0;
+      if (R.rok[h]) s.E[R.rr[h]] = 1.0;
+    }
     if (tid == 0) s.c = 1.0;
   }
   // the block solve reads b in whole blocks (plus look-ahead): zero the tail
   for (int j = n + tid; j < FQ_NMAX; j += FQ_T) s.rhs[j] = 0.0;
   if (tid == 0) s.rho_s = fmin(fmax(s.rho_s, QP_RHO_MIN), QP_RHO_MAX);
   __syncthreads();
-  if (!fq_dyn_rows_are_equalities(s, R)) { res.factor_fail = -1; return res; }
   T.mark(1);
-  int f = fq_factor(pt, s, R, st.sigma);
+  int f = fq_factor(pt, s, R, st.sigma, cw);
   T.mark(2);
   if (f) { res.factor_fail = f; return res; }
   if (st.warm_start) {
@@ -474,7 +490,7 @@ __device__ __forceinline__ QPResult fq_solve(const QPPattern &pt, FleetSmem &s, 
     for (int h = 0; h < 2; ++h) {  // z = A x
       if (R.rok[h]) {
         double acc = 0.0;
-        _Pragma("unroll") for (int e = 0; e < FQ_RMAX; ++e) if (e < R.rn[h]) acc += s.A[R.rb[h] + e] * s.rhs[R.rc[h][e]];
+        _Pragma("unroll") for (int e = 0; e < FQ_RMAX; ++e) if (e < R.rn(h)) acc += s.A[R.rb(h) + e] * s.rhs[R.rc(h, e)];
         R.zr[h] = acc;
       }
       if (R.vok[h]) R.zb[h] = 0.0 + R.Ab[h] * R.x[h];
@@ -497,13 +513,13 @@ __device__ __forceinline__ QPResult fq_solve(const QPPattern &pt, FleetSmem &s, 
     for (int h = 0; h < 2; ++h)
       if (R.vok[h]) {
         double acc = 0.0;
-        _Pragma("unroll") for (int e = 0; e < FQ_CMAX; ++e) if (e < R.cn[h]) acc += s.A[R.ca[h][e]] * s.zt[R.cr[h][e]];
+        _Pragma("unroll") for (int e = 0; e < FQ_CMAX; ++e) if (e < R.cn[h]) acc += s.A[R.ca(h, e)] * s.zt[R.cr(h, e)];
         acc += R.Ab[h] * R.ztb[h];
         s.rhs[R.vj[h]] = sig * R.x[h] - R.q[h] + acc;
       }
     __syncthreads();
     T.mark(3);
-    blk_solve_dispatch(pt, s, s.rhs, &T);  // x~ (wave 0)
+    blk_solve_dispatch(pt, s, s.rhs, &T, cw);  // x~ (wave cw)
     __syncthreads();
     T.mark(4);
     const double rs = s.rho_s;
@@ -528,11 +544,11 @@ __device__ __forceinline__ QPResult fq_solve(const QPPattern &pt, FleetSmem &s, 
       }
       if (R.rok[h]) {
         double ztl = 0.0;
-        _Pragma("unroll") for (int e = 0; e < FQ_RMAX; ++e) if (e < R.rn[h]) ztl += s.A[R.rb[h] + e] * s.rhs[R.rc[h][e]];
+        _Pragma("unroll") for (int e = 0; e < FQ_RMAX; ++e) if (e < R.rn(h)) ztl += s.A[R.rb(h) + e] * s.rhs[R.rc(h, e)];
         const double rho = QP_RHO_EQ * rs, zo = R.zr[h], yo = R.yr[h];
         const double zr = al * ztl + (1.0 - al) * zo;
         double zn = zr + yo / rho;
-        zn = fmin(fmax(zn, R.lr[h]), R.ur[h]);
+        zn = fmin(fmax(zn, R.ur[h]), R.ur[h]);
         const double d = rho * (zr - zn);
         const double yn = yo + d;
         R.dyr[h] = d; R.yr[h] = yn; R.zr[h] = zn;
@@ -554,7 +570,7 @@ __device__ __forceinline__ QPResult fq_solve(const QPPattern &pt, FleetSmem &s, 
         __syncthreads();
         if (tid == 0) s.rho_s = est;
         __syncthreads();
-        f = fq_factor(pt, s, R, st.sigma);
+        f = fq_factor(pt, s, R, st.sigma, cw);
         if (f) { res.factor_fail = f; return res; }
       }
     }

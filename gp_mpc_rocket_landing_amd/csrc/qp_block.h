@@ -122,7 +122,7 @@ __device__ __forceinline__ double dot_bc(double src, const double *mul) {
 template <int SZ, int CM, class S>
 __device__ int blk_factor(const QPPattern &pt, S &s) {
   constexpr int BS = SZ * SZ + SZ * CM;
-  const int lane = threadIdx.x, rr = lane & 15;
+  const int lane = threadIdx.x & 63, rr = lane & 15;
   const bool wr = lane < 16;
   const int rs = rr < SZ ? rr : SZ - 1, rc = rr < CM ? rr : CM - 1;
   double *F = s.band();
@@ -196,12 +196,12 @@ __device__ int blk_factor(const QPPattern &pt, S &s) {
 // stores are masked.  Per-lane pointers advance by constants; operands sit at
 // immediate offsets.
 template <int SZ, int CM, class S>
-__device__ void blk_solve(const QPPattern &pt, S &s, double *b, QPStamps *T = nullptr) {
-  if (threadIdx.x >= 64) return;
+__device__ void blk_solve(const QPPattern &pt, S &s, double *b, QPStamps *T = nullptr, int cw = 0) {
+  if ((int)(threadIdx.x >> 6) != cw) return;
   constexpr int BS = SZ * SZ + SZ * CM;
   // non-coupled lanes keep pg = gzero (gstep 0) and read gzero[j * CM], j < SZ
   static_assert((SZ - 1) * CM + 1 <= sizeof(s.gzero) / sizeof(double), "gzero too small");
-  const int lane = threadIdx.x, rr = lane & 15, row = lane >> 4;
+  const int lane = threadIdx.x & 63, rr = lane & 15, row = lane >> 4;
   const int rs = rr < SZ ? rr : SZ - 1, rc = rr < CM ? rr : CM - 1;
   const bool wr = rr < SZ;
   const int nblk = pt.nblk;
@@ -327,6 +327,7 @@ __device__ int blk_factor_dispatch(const QPPattern &pt, S &s) {
   return blk_factor<QP_BLK_SZ, QP_BLK_CM>(pt, s);
 }
 template <class S>
-__device__ void blk_solve_dispatch(const QPPattern &pt, S &s, double *b, QPStamps *T = nullptr) {
-  blk_solve<QP_BLK_SZ, QP_BLK_CM>(pt, s, b, T);
+__device__ void blk_solve_dispatch(const QPPattern &pt, S &s, double *b, QPStamps *T = nullptr,
+                                   int cw = 0) {
+  blk_solve<QP_BLK_SZ, QP_BLK_CM>(pt, s, b, T, cw);
 }
