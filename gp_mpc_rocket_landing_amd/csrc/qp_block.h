@@ -117,6 +117,43 @@ __device__ __forceinline__ double dot_bc(double src, const double *mul) {
   return dot_bcv(src, mul, std::make_integer_sequence<int, K>{});
 }
 
+// ---- factor helpers: every broadcast-multiply-add is one v_fmac_f64_dpp.
+// Gauss-Jordan step p: a[c] += bcast_p(a[c]) * f for c != p (the source and the
+// accumulator are the same register: DPP reads all lanes before the write).
+// The first FMA of a step waits the two DPP states after the last VALU write.
+template <int P, int... C>
+__device__ __forceinline__ void fq_gj_step(double *a, double f, std::integer_sequence<int, C...>) {
+  ((C != P ? fmac_bc<P, C == (P == 0 ? 1 : 0)>(a[C], a[C], f) : (void)0), ...);
+}
+template <int SZ, int... P>
+__device__ __forceinline__ void fq_gj_dispatch(double *a, double f, int p, std::integer_sequence<int, P...>) {
+  ((p == P ? fq_gj_step<P>(a, f, std::make_integer_sequence<int, SZ>{}) : (void)0), ...);
+}
+template <int SZ>
+__device__ __forceinline__ void fq_gj_update(double *a, double f, int p) {
+  fq_gj_dispatch<SZ>(a, f, p, std::make_integer_sequence<int, SZ>{});
+}
+// g[j] += c[l] * bcast_l(a[j]) for l = 0..SZ-1, j = 0..SZ-1
+template <int L, int... J>
+__device__ __forceinline__ void blk_gmul_l(double *g, const double *a, double cl, std::integer_sequence<int, J...>) {
+  ((fmac_bc<L, L == 0 && J == 0>(g[J], a[J], cl)), ...);
+}
+template <int SZ, int... L>
+__device__ __forceinline__ void blk_gmul(double *g, const double *a, const double *c, std::integer_sequence<int, L...>) {
+  (blk_gmul_l<L>(g, a, c[L], std::make_integer_sequence<int, SZ>{}), ...);
+}
+// u[i] = sum_j g[j] * bcast_i(c[j]) for i = 0..CM-1
+template <int I, int... J>
+__device__ __forceinline__ double blk_schur_i(const double *g, const double *c, std::integer_sequence<int, J...>) {
+  double t = 0.0;
+  ((fmac_bc<I, I == 0 && J == 0>(t, c[J], g[J])), ...);
+  return t;
+}
+template <int SZ, int CM, int... I>
+__device__ __forceinline__ void blk_schur(double *u, const double *g, const double *c, std::integer_sequence<int, I...>) {
+  ((u[I] = blk_schur_i<I>(g, c, std::make_integer_sequence<int, SZ>{})), ...);
+}
+
 // factor: returns 0 or the 1-based failing (non-positive pivot) variable.
 // Wave 0 only, all 64 lanes (rows replicate).
 template <int SZ, int CM, class S>
@@ -147,9 +184,7 @@ __device__ int blk_factor(const QPPattern &pt, S &s) {
       const double inv = 1.0 / piv;
       // lane p: row *= inv  (= row + row*(inv-1));  other lanes: row -= a[p]/piv * row_p
       const double f = (rr == p) ? inv - 1.0 : -a[p] * inv;
-#pragma unroll
-      for (int c = 0; c < SZ; ++c)
-        if (c != p) a[c] = fma(bc16_rt(a[c], p), f, a[c]);
+      fq_gj_update<SZ>(a, f, p);
       a[p] = (rr == p) ? inv : f;
     }
     if (wr && rr < SZ) {
@@ -164,24 +199,14 @@ __device__ int blk_factor(const QPPattern &pt, S &s) {
         c[j] = Ck[j * CM + rc];
         g[j] = 0.0;
       }
-      // G[rr][j] = sum_l C[rr][l] S^-1[l][j]
-#pragma unroll
-      for (int l = 0; l < SZ; ++l) {
-#pragma unroll
-        for (int j = 0; j < SZ; ++j) g[j] = fma(c[l], bc16_rt(a[j], l), g[j]);
-      }
+      // G[rr][j] = sum_l C[rr][l] S^-1[l][j]   (one v_fmac_f64_dpp per term)
+      blk_gmul<SZ>(g, a, c, std::make_integer_sequence<int, SZ>{});
       if (wr && rr < CM) {  // stored negated: the solve's chains accumulate into b / u
 #pragma unroll
         for (int j = 0; j < SZ; ++j) Ck[j * CM + rr] = -g[j];
       }
-      // u[rr][i] = sum_j G[rr][j] C[i][j]
-#pragma unroll
-      for (int i = 0; i < CM; ++i) {
-        double t = 0.0;
-#pragma unroll
-        for (int j = 0; j < SZ; ++j) t = fma(g[j], bc16_rt(c[j], i), t);
-        u[i] = t;
-      }
+      // u[rr][i] = sum_j G[rr][j] C[i][j]   (one v_fmac_f64_dpp per term)
+      blk_schur<SZ, CM>(u, g, c, std::make_integer_sequence<int, CM>{});
     }
   }
   __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
