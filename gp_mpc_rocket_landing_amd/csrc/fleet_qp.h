@@ -35,6 +35,9 @@
 #define FQ_FAC (FQ_NBLK * (QP_BLK_SZ * QP_BLK_SZ + QP_BLK_SZ * QP_BLK_CM) + 16)
 #define FQ_CMAX 6     // dynamics entries per column (<= 5) + 1
 #define FQ_RMAX 5     // entries per dynamics row
+#ifndef FQ_FUSED_DIAG
+#define FQ_FUSED_DIAG false  // block solve: G chain first, then the diagonal blocks 4 at a time
+#endif
 
 struct FleetSmem {
   double A[FQ_NNZD + 1];
@@ -519,7 +522,7 @@ __device__ __forceinline__ QPResult fq_solve(const QPPattern &pt, FleetSmem &s, 
       }
     __syncthreads();
     T.mark(3);
-    blk_solve_dispatch(pt, s, s.rhs, &T, cw);  // x~ (wave cw)
+    blk_solve_dispatch<FQ_FUSED_DIAG>(pt, s, s.rhs, &T, cw);  // x~ (wave cw)
     __syncthreads();
     T.mark(4);
     const double rs = s.rho_s;

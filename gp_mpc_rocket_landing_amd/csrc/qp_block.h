@@ -220,7 +220,7 @@ __device__ int blk_factor(const QPPattern &pt, S &s) {
 // rr >= SZ (never a broadcast source) read clamped addresses and only the
 // stores are masked.  Per-lane pointers advance by constants; operands sit at
 // immediate offsets.
-template <int SZ, int CM, class S>
+template <int SZ, int CM, bool FUSED = true, class S>
 __device__ void blk_solve(const QPPattern &pt, S &s, double *b, QPStamps *T = nullptr, int cw = 0) {
   if ((int)(threadIdx.x >> 6) != cw) return;
   constexpr int BS = SZ * SZ + SZ * CM;
@@ -247,7 +247,80 @@ __device__ void blk_solve(const QPPattern &pt, S &s, double *b, QPStamps *T = nu
   //      interleave.  Lanes rr >= CM read their "-G row" from a zero region
   //      (their y is exactly b); lanes rr >= SZ compute bit-identical values
   //      to lane SZ-1 (same clamped inputs), so every store is unconditional.
-  {
+  //  !FUSED: the chain carries the G product only (half the FMAs and operand
+  //      registers on the critical path) and the diagonal products run after
+  //      it, four independent blocks per round, one per DPP row.
+  if constexpr (!FUSED) {
+    double *pb = b + rs;
+    const bool cpl = rr < CM;
+    const double *pg = cpl ? F + SZ * SZ + rc : s.gzero;
+    const int gstep = cpl ? BS : 0;
+    double y = pb[0];
+    double gA[SZ], gB[SZ];
+    double bA = pb[SZ], bB;
+#pragma unroll
+    for (int j = 0; j < SZ; ++j) gA[j] = pg[j * CM];
+    for (int k = 0;;) {
+      {
+        bB = pb[2 * SZ];
+#pragma unroll
+        for (int j = 0; j < SZ; ++j) gB[j] = pg[gstep + j * CM];
+        const double yn = dot_bc_init<SZ>(bA, y, gA);
+        pb[0] = y;
+        y = yn;
+        pb += SZ;
+        pg += gstep;
+        if (++k >= nblk - 1) break;
+      }
+      {
+        bA = pb[2 * SZ];
+#pragma unroll
+        for (int j = 0; j < SZ; ++j) gA[j] = pg[gstep + j * CM];
+        const double yn = dot_bc_init<SZ>(bB, y, gB);
+        pb[0] = y;
+        y = yn;
+        pb += SZ;
+        pg += gstep;
+        if (++k >= nblk - 1) break;
+      }
+    }
+    pb[0] = y;
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    if (T) T->mark(8);
+    // diagonal: u_k = S_k^-1 y_k, block 4t + row in round t.  Rows past the
+    // last block read the last block (in bounds) and do not store.
+    const int nr = (nblk + 3) >> 2;
+    auto blk = [&](int t) { return min(4 * t + row, nblk - 1); };
+    double sA[SZ], sB[SZ];
+    {
+      const double *ps = F + blk(0) * BS + rs;
+#pragma unroll
+      for (int j = 0; j < SZ; ++j) sA[j] = ps[j * SZ];
+    }
+    double yA = b[blk(0) * SZ + rs], yB = 0.0;
+    for (int t = 0;;) {
+      {
+        const int kn = blk(t + 1 < nr ? t + 1 : t);
+        const double *ps = F + kn * BS + rs;
+#pragma unroll
+        for (int j = 0; j < SZ; ++j) sB[j] = ps[j * SZ];
+        yB = b[kn * SZ + rs];
+        const double uv = dot_bc<SZ>(yA, sA);
+        if (4 * t + row < nblk) b[(4 * t + row) * SZ + rs] = uv;
+        if (++t >= nr) break;
+      }
+      {
+        const int kn = blk(t + 1 < nr ? t + 1 : t);
+        const double *ps = F + kn * BS + rs;
+#pragma unroll
+        for (int j = 0; j < SZ; ++j) sA[j] = ps[j * SZ];
+        yA = b[kn * SZ + rs];
+        const double uv = dot_bc<SZ>(yB, sB);
+        if (4 * t + row < nblk) b[(4 * t + row) * SZ + rs] = uv;
+        if (++t >= nr) break;
+      }
+    }
+  } else {
     double *pb = b + rs;                          // block k of b
     const bool cpl = rr < CM;
     const double *pg = cpl ? F + SZ * SZ + rc : s.gzero;   // -G_k row rc
@@ -300,9 +373,9 @@ __device__ void blk_solve(const QPPattern &pt, S &s, double *b, QPStamps *T = nu
 #pragma unroll
     for (int j = 0; j < SZ; ++j) sl[j] = ps[j * SZ];
     pb[0] = dot_bc<SZ>(y, sl);
+    if (T) T->mark(8);
   }
   __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-  if (T) T->mark(8);
   if (T) T->mark(9);
   // ---- backward: x_k = u_k + (-G_k)^T x_{k+1}
   {
@@ -351,8 +424,8 @@ template <class S>
 __device__ int blk_factor_dispatch(const QPPattern &pt, S &s) {
   return blk_factor<QP_BLK_SZ, QP_BLK_CM>(pt, s);
 }
-template <class S>
+template <bool FUSED = true, class S>
 __device__ void blk_solve_dispatch(const QPPattern &pt, S &s, double *b, QPStamps *T = nullptr,
                                    int cw = 0) {
-  blk_solve<QP_BLK_SZ, QP_BLK_CM>(pt, s, b, T, cw);
+  blk_solve<QP_BLK_SZ, QP_BLK_CM, FUSED>(pt, s, b, T, cw);
 }
