@@ -387,6 +387,9 @@ __global__ __launch_bounds__(256) void k_fleet_control(FleetArgs a) {
 // The same control step on the fleet-specialised solver (fleet_qp.h): 128
 // threads and ~37 KB of LDS per landing, four landings per CU.  Assembly goes
 // straight into the owners' registers; results and the plant step as above.
+// STAMPS: the diagnostic phase-cycle instance (gpmpc_fleet_set_stamps); the
+// production instance has no stamp code or state at all.
+template <bool STAMPS>
 __global__ __launch_bounds__(FQ_T) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_fleet_control2(FleetArgs a) {
   __shared__ FleetSmem s;
   __shared__ double sx[NX], st_tgt[NX];
@@ -397,7 +400,7 @@ __global__ __launch_bounds__(FQ_T) __attribute__((amdgpu_waves_per_eu(2, 2))) vo
   double *rec = a.rec + (int64_t)b * GPMPC_REC_LEN;
   if (rec[0] != 0.0) return;  // terminated landing
   QPStamps T;
-  T.out = (b == 0) ? a.stamps : nullptr;
+  T.out = (STAMPS && b == 0) ? a.stamps : nullptr;
   T.start();
   if (a.trace && tid == 0) {
     unsigned long long *tr = a.trace + (int64_t)b * 4;
@@ -788,7 +791,14 @@ extern "C" int gpmpc_fleet_step_phases(gpmpc_fleet *f, int phase_mask) {
       hipLaunchKernelGGL(k_fleet_order, dim3(1), dim3(1024), 0, f->ctx->stream, f->B,
                          f->rec.as<double>(), f->lastit.as<int>(), f->order.as<int>());
     if (f->use_fq)
-      hipLaunchKernelGGL(k_fleet_control2, dim3(f->B), dim3(FQ_T), 0, f->ctx->stream, fleet_args(f));
+    {
+      if (f->stamps)
+        hipLaunchKernelGGL(k_fleet_control2<true>, dim3(f->B), dim3(FQ_T), 0, f->ctx->stream,
+                           fleet_args(f));
+      else
+        hipLaunchKernelGGL(k_fleet_control2<false>, dim3(f->B), dim3(FQ_T), 0, f->ctx->stream,
+                           fleet_args(f));
+    }
     else
       hipLaunchKernelGGL(k_fleet_control, dim3(f->B), dim3(256), 0, f->ctx->stream, fleet_args(f));
     GPMPC_HIP(hipGetLastError());

@@ -456,11 +456,10 @@ __device__ __forceinline__ void fq_rebuild_zt(FleetSmem &s, FleetRegs &R) {
 // unscaled dynamics rows, s.rho_s the persistent rho.  On exit R.x / R.y* hold
 // the scaled iterates, R.D / E* and s.c the scaling.
 __device__ __forceinline__ QPResult fq_solve(const QPPattern &pt, FleetSmem &s, FleetRegs &R,
-                             const QPSettingsDev &st, QPStamps *ts = nullptr, int cw = 0) {
+                             const QPSettingsDev &st, QPStamps *ts, int cw = 0) {
   const int n = pt.n, tid = threadIdx.x;
   QPResult res{-10, 0, 0.0, 0};
-  QPStamps dummy;
-  QPStamps &T = ts ? *ts : dummy;
+  QPStamps &T = *ts;  // the caller's (no pointer select: a null `out` folds the stamps away)
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
     R.lb[h] = fmax(R.lb[h], -QP_OSQP_INFTY); R.ub[h] = fmin(R.ub[h], QP_OSQP_INFTY);

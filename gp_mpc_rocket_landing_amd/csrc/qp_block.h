@@ -157,7 +157,7 @@ __device__ __forceinline__ void blk_schur(double *u, const double *g, const doub
 // factor: returns 0 or the 1-based failing (non-positive pivot) variable.
 // Wave 0 only, all 64 lanes (rows replicate).
 template <int SZ, int CM, class S>
-__device__ int blk_factor(const QPPattern &pt, S &s) {
+__device__ __forceinline__ int blk_factor(const QPPattern &pt, S &s) {
   constexpr int BS = SZ * SZ + SZ * CM;
   const int lane = threadIdx.x & 63, rr = lane & 15;
   const bool wr = lane < 16;
@@ -221,7 +221,7 @@ __device__ int blk_factor(const QPPattern &pt, S &s) {
 // stores are masked.  Per-lane pointers advance by constants; operands sit at
 // immediate offsets.
 template <int SZ, int CM, bool FUSED = true, class S>
-__device__ void blk_solve(const QPPattern &pt, S &s, double *b, QPStamps *T = nullptr, int cw = 0) {
+__device__ __forceinline__ void blk_solve(const QPPattern &pt, S &s, double *b, QPStamps *T = nullptr, int cw = 0) {
   if ((int)(threadIdx.x >> 6) != cw) return;
   constexpr int BS = SZ * SZ + SZ * CM;
   // non-coupled lanes keep pg = gzero (gstep 0) and read gzero[j * CM], j < SZ
@@ -421,11 +421,11 @@ __device__ void blk_solve(const QPPattern &pt, S &s, double *b, QPStamps *T = nu
 #define QP_BLK_CM 7   // coupled through x_{k+1}
 
 template <class S>
-__device__ int blk_factor_dispatch(const QPPattern &pt, S &s) {
+__device__ __forceinline__ int blk_factor_dispatch(const QPPattern &pt, S &s) {
   return blk_factor<QP_BLK_SZ, QP_BLK_CM>(pt, s);
 }
 template <bool FUSED = true, class S>
-__device__ void blk_solve_dispatch(const QPPattern &pt, S &s, double *b, QPStamps *T = nullptr,
+__device__ __forceinline__ void blk_solve_dispatch(const QPPattern &pt, S &s, double *b, QPStamps *T = nullptr,
                                    int cw = 0) {
   blk_solve<QP_BLK_SZ, QP_BLK_CM, FUSED>(pt, s, b, T, cw);
 }

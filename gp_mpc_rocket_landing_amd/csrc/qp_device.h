@@ -405,20 +405,20 @@ struct QPStamps {
   unsigned long long *out = nullptr;
   unsigned long long acc[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
   unsigned long long last = 0, first = 0, rt0 = 0;
-  __device__ void start() {
+  __device__ __forceinline__ void start() {
     if (out && threadIdx.x == 0) {
       last = first = __builtin_amdgcn_s_memtime();
       rt0 = __builtin_amdgcn_s_memrealtime();
     }
   }
-  __device__ void mark(int k) {
+  __device__ __forceinline__ void mark(int k) {
     if (out && threadIdx.x == 0) {
       const unsigned long long t = __builtin_amdgcn_s_memtime();
       acc[k] += t - last;
       last = t;
     }
   }
-  __device__ void flush() {
+  __device__ __forceinline__ void flush() {
     if (out && threadIdx.x == 0) {
       for (int k = 0; k < 12; ++k) out[k] += acc[k];
       out[14] += __builtin_amdgcn_s_memrealtime() - rt0;  // 100 MHz constant clock
