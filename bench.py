@@ -46,6 +46,10 @@ def admm_flops(n=207, m=354, nnz=734, sz=10, cm=7):
     return it, fac
 
 
+# the fleet's control kernel: the specialised solver unless GPMPC_FLEET_SOLVER=0
+CONTROL_KERNEL = "k_fleet_control" if os.environ.get("GPMPC_FLEET_SOLVER", "1") == "0" else "k_fleet_control2"
+
+
 def pmc_traffic(kernel):
     """Per-launch HBM bytes of ``kernel`` from the committed rocprofv3 --pmc
     passes (profiles/*_pmc_traffic.json, scripts/pmc_traffic.py), else None."""
@@ -292,13 +296,13 @@ def main():
         kern = {
             "gram_Kstar": dict(kernel="k_gram<11>", ms=ph_mean[0] * 1e3, bound="hbm",
                                achieved=gram_bytes / ph_mean[0] / 1e9, peak=HBM_PEAK_GBS, unit="GB/s"),
-            "var_mean_gemm_mfma": dict(kernel="k_gemm_nt<1>", ms=ph_mean[1] * 1e3, bound="mfma",
+            "var_mean_gemm_mfma": dict(kernel="k_gemm128<1>", ms=ph_mean[1] * 1e3, bound="mfma",
                                        achieved=var_flops / ph_mean[1] / 1e12, peak=FP64_PEAK_TFLOPS,
                                        unit="TFLOP/s"),
             "post_finish": dict(kernel="k_post_finish", ms=ph_mean[2] * 1e3, bound="hbm",
                                 achieved=fin_bytes / ph_mean[2] / 1e9, peak=HBM_PEAK_GBS,
                                 unit="GB/s"),
-            "qp_admm_plant": dict(kernel="k_fleet_control", ms=ph_mean[3] * 1e3, bound="mfma",
+            "qp_admm_plant": dict(kernel=CONTROL_KERNEL, ms=ph_mean[3] * 1e3, bound="mfma",
                                   achieved=admm_flop / ph_mean[3] / 1e12, peak=FP64_PEAK_TFLOPS,
                                   unit="TFLOP/s"),
         }
