@@ -47,7 +47,7 @@ def admm_flops(n=207, m=354, nnz=734, sz=10, cm=7):
 
 
 # the fleet's control kernel: the specialised solver unless GPMPC_FLEET_SOLVER=0
-CONTROL_KERNEL = "k_fleet_control" if os.environ.get("GPMPC_FLEET_SOLVER", "1") == "0" else "k_fleet_control2"
+CONTROL_KERNEL = "k_fleet_control" if os.environ.get("GPMPC_FLEET_SOLVER", "1") == "0" else "k_fleet_control2<false>"
 
 
 def pmc_traffic(kernel):

@@ -11,7 +11,7 @@ OUT=$ROOT/gpurun_out/prof_$TAG
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 420 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run -- \
-  python3 "$ROOT/bench.py" --steps 10 --warmup 3 --no-cpu > "$OUT/bench_trace.log" 2>&1
+  python3 "$ROOT/bench.py" --steps 10 --warmup 3 --no-cpu --no-chol > "$OUT/bench_trace.log" 2>&1
 timeout -k 10 420 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/fetch" -o run -- \
   python3 "$ROOT/bench.py" --steps 3 --warmup 1 --no-cpu --no-chol > "$OUT/bench_fetch.log" 2>&1
 timeout -k 10 420 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/write" -o run -- \
