@@ -327,8 +327,10 @@ def main():
                                 "post_finish": "8 P (row tiles + 9) bytes"}[dom],
                     traffic_source=pmc_traffic(d["kernel"])[1], launches_per_step=1)
         if dom == "qp_admm_plant":
-            roof["limiter"] = ("latency: serial block-tridiagonal KKT chain, one wave per landing; "
-                               "~10 KB HBM per landing-step")
+            roof["limiter"] = ("latency: serial block-tridiagonal KKT chain, one chain wave per "
+                               "landing, four landings per CU; ~10 KB of state in/out per "
+                               "landing-step, the rest of the measured traffic is register-spill "
+                               "scratch")
         out = {
             "metric": "GP-MPC control steps/sec (N=20, 1000 GP pts)",
             "value": round(steps_all / el_max, 2),
