@@ -524,8 +524,8 @@ __global__ __launch_bounds__(FQ_T) __attribute__((amdgpu_waves_per_eu(2, 2))) vo
 #pragma unroll
   for (int h = 0; h < 2; ++h)
     if (R.rok[h]) {
-      R.ur[h] = s.zt[R.rr[h]];  // l = u
-      R.yr[h] = a.ysc[(int64_t)b * m + R.rr[h]];
+      R.ur(h) = s.zt[R.rr[h]];  // l = u
+      R.yr(h) = a.ysc[(int64_t)b * m + R.rr[h]];
     }
   __syncthreads();
   T.mark(0);
@@ -561,7 +561,7 @@ __global__ __launch_bounds__(FQ_T) __attribute__((amdgpu_waves_per_eu(2, 2))) vo
     }
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
-      if (R.rok[h]) a.ysc[(int64_t)b * m + R.rr[h]] = R.yr[h];
+      if (R.rok[h]) a.ysc[(int64_t)b * m + R.rr[h]] = R.yr(h);
       if (R.vok[h]) a.ysc[(int64_t)b * m + MD + R.vj[h]] = R.yb[h];
     }
   }

@@ -100,18 +100,28 @@ struct FleetRegs {
   // variable j and bound row MD + j
   double x[2], dx[2], P[2], q[2], D[2];
   double Ab[2], lb[2], ub[2], yb[2], zb[2], dyb[2], ztb[2];
-  // dynamics rows (l = u = ur)
-  double ur[2], yr[2], zr[2], dyr[2];
+  // dynamics row 0 (l = u = ur).  No thread owns both a second variable and a
+  // second dynamics row (t < 79: 2 variables + 1 row; t >= 109: 1 + 2), so row
+  // slot 1 lives in variable slot 1's registers: ur <- P, yr <- yb, zr <- zb,
+  // dyr <- dyb, its pattern in cp[1][0..3]
+  double ur0, yr0, zr0, dyr0;
   // patterns: column j's dynamics entries, (CSR value index) | (row << 16);
   // row r: first value index | count << 16, column indices two per int
   int cn[2], cp[2][FQ_CMAX];
-  int rbn[2], rcp[2][(FQ_RMAX + 1) / 2];
+  int rbn0, rcp0[(FQ_RMAX + 1) / 2];
+  __device__ __forceinline__ double &ur(int h) { return h ? P[1] : ur0; }
+  __device__ __forceinline__ double &yr(int h) { return h ? yb[1] : yr0; }
+  __device__ __forceinline__ double &zr(int h) { return h ? zb[1] : zr0; }
+  __device__ __forceinline__ double &dyr(int h) { return h ? dyb[1] : dyr0; }
+  __device__ __forceinline__ int &rbn(int h) { return h ? cp[1][3] : rbn0; }
+  __device__ __forceinline__ int &rcp(int h, int e) { return h ? cp[1][e] : rcp0[e]; }
   __device__ __forceinline__ int ca(int h, int e) const { return cp[h][e] & 0xffff; }
   __device__ __forceinline__ int cr(int h, int e) const { return cp[h][e] >> 16; }
-  __device__ __forceinline__ int rb(int h) const { return rbn[h] & 0xffff; }
-  __device__ __forceinline__ int rn(int h) const { return rbn[h] >> 16; }
-  __device__ __forceinline__ int rc(int h, int e) const { return (rcp[h][e >> 1] >> (16 * (e & 1))) & 0xffff; }
+  __device__ __forceinline__ int rb(int h) { return rbn(h) & 0xffff; }
+  __device__ __forceinline__ int rn(int h) { return rbn(h) >> 16; }
+  __device__ __forceinline__ int rc(int h, int e) { return (rcp(h, e >> 1) >> (16 * (e & 1))) & 0xffff; }
 };
+static_assert((FQ_RMAX + 1) / 2 + 1 <= FQ_CMAX, "row slot 1 pattern must fit variable slot 1's");
 
 __device__ __forceinline__ void fq_init_pattern(const QPPattern &pt, FleetRegs &R, int n) {
   const int t = threadIdx.x;
@@ -134,14 +144,16 @@ __device__ __forceinline__ void fq_init_pattern(const QPPattern &pt, FleetRegs &
     const int r = (FQ_T - 1 - t) + h * FQ_T;
     R.rr[h] = r;
     R.rok[h] = r < FQ_MD;
-    const int rb = R.rok[h] ? pt.rowptr[r] : 0;
-    const int rn = R.rok[h] ? pt.rowptr[r + 1] - rb : 0;
-    R.rbn[h] = rb | (rn << 16);
+    if (h == 0 || R.rok[h]) {  // slot 1: only when this thread's second item is a row
+      const int rb = R.rok[h] ? pt.rowptr[r] : 0;
+      const int rn = R.rok[h] ? pt.rowptr[r + 1] - rb : 0;
+      R.rbn(h) = rb | (rn << 16);
 #pragma unroll
-    for (int e = 0; e < (FQ_RMAX + 1) / 2; ++e) {
-      const int c0 = (2 * e < rn) ? pt.colidx[rb + 2 * e] : 0;
-      const int c1 = (2 * e + 1 < rn) ? pt.colidx[rb + 2 * e + 1] : 0;
-      R.rcp[h][e] = c0 | (c1 << 16);
+      for (int e = 0; e < (FQ_RMAX + 1) / 2; ++e) {
+        const int c0 = (2 * e < rn) ? pt.colidx[rb + 2 * e] : 0;
+        const int c1 = (2 * e + 1 < rn) ? pt.colidx[rb + 2 * e + 1] : 0;
+        R.rcp(h, e) = c0 | (c1 << 16);
+      }
     }
   }
 }
@@ -224,7 +236,7 @@ __device__ __forceinline__ void fq_scale(const QPPattern &pt, FleetSmem &s, Flee
       const double e = s.E[FQ_MD + R.vj[h]];
       R.lb[h] = e * R.lb[h]; R.ub[h] = e * R.ub[h];
     }
-    if (R.rok[h]) R.ur[h] = s.E[R.rr[h]] * R.ur[h];
+    if (R.rok[h]) R.ur(h) = s.E[R.rr[h]] * R.ur(h);
   }
 }
 
@@ -278,7 +290,7 @@ __device__ __forceinline__ void fq_update_info(FleetSmem &s, FleetRegs &R, doubl
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
     if (R.vok[h]) s.rhs[R.vj[h]] = R.x[h];
-    if (R.rok[h]) s.zt[R.rr[h]] = R.yr[h];
+    if (R.rok[h]) s.zt[R.rr[h]] = R.yr(h);
   }
   __syncthreads();
   double v[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
@@ -287,7 +299,7 @@ __device__ __forceinline__ void fq_update_info(FleetSmem &s, FleetRegs &R, doubl
     if (R.rok[h]) {  // dynamics row: (A x)_r
       double ax = 0.0;
       _Pragma("unroll") for (int e = 0; e < FQ_RMAX; ++e) if (e < R.rn(h)) ax += s.A[R.rb(h) + e] * s.rhs[R.rc(h, e)];
-      const double e = s.E[R.rr[h]], z = R.zr[h];
+      const double e = s.E[R.rr[h]], z = R.zr(h);
       v[0] = fmax(v[0], fabs((ax - z) / e));
       v[1] = fmax(v[1], fabs(z / e));
       v[2] = fmax(v[2], fabs(ax / e));
@@ -336,8 +348,8 @@ __device__ __forceinline__ bool fq_primal_infeasible(FleetSmem &s, FleetRegs &R,
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
     if (R.rok[h]) {
-      R.dyr[h] = proj(R.dyr[h], R.ur[h], R.ur[h]);
-      v[0] = fmax(v[0], fabs(s.E[R.rr[h]] * R.dyr[h]));
+      R.dyr(h) = proj(R.dyr(h), R.ur(h), R.ur(h));
+      v[0] = fmax(v[0], fabs(s.E[R.rr[h]] * R.dyr(h)));
     }
     if (R.vok[h]) {
       R.dyb[h] = proj(R.dyb[h], R.lb[h], R.ub[h]);
@@ -350,14 +362,14 @@ __device__ __forceinline__ bool fq_primal_infeasible(FleetSmem &s, FleetRegs &R,
   double sm[1] = {0.0};
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
-    if (R.rok[h]) sm[0] += R.ur[h] * fmax(R.dyr[h], 0.0) + R.ur[h] * fmin(R.dyr[h], 0.0);
+    if (R.rok[h]) sm[0] += R.ur(h) * fmax(R.dyr(h), 0.0) + R.ur(h) * fmin(R.dyr(h), 0.0);
     if (R.vok[h]) sm[0] += R.ub[h] * fmax(R.dyb[h], 0.0) + R.lb[h] * fmin(R.dyb[h], 0.0);
   }
   fq_sum<1>(sm, s.red);
   if (!(sm[0] < -eps * nrm)) return false;
 #pragma unroll
   for (int h = 0; h < 2; ++h)
-    if (R.rok[h]) s.zt[R.rr[h]] = R.dyr[h];
+    if (R.rok[h]) s.zt[R.rr[h]] = R.dyr(h);
   __syncthreads();
   double mx[1] = {0.0};
 #pragma unroll
@@ -406,7 +418,7 @@ __device__ __forceinline__ bool fq_dual_infeasible(FleetSmem &s, FleetRegs &R, d
     if (R.rok[h]) {
       double adx = 0.0;
       _Pragma("unroll") for (int e = 0; e < FQ_RMAX; ++e) if (e < R.rn(h)) adx += s.A[R.rb(h) + e] * s.rhs[R.rc(h, e)];
-      test(adx / s.E[R.rr[h]], R.ur[h], R.ur[h]);
+      test(adx / s.E[R.rr[h]], R.ur(h), R.ur(h));
     }
     if (R.vok[h]) test((0.0 + R.Ab[h] * R.dx[h]) / s.E[FQ_MD + R.vj[h]], R.lb[h], R.ub[h]);
   }
@@ -445,7 +457,7 @@ __device__ __forceinline__ void fq_rebuild_zt(FleetSmem &s, FleetRegs &R) {
   const double rs = s.rho_s;
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
-    if (R.rok[h]) s.zt[R.rr[h]] = QP_RHO_EQ * rs * R.zr[h] - R.yr[h];
+    if (R.rok[h]) s.zt[R.rr[h]] = QP_RHO_EQ * rs * R.zr(h) - R.yr(h);
     if (R.vok[h]) R.ztb[h] = fq_rho(R.lb[h], R.ub[h], rs) * R.zb[h] - R.yb[h];
   }
   __syncthreads();
@@ -463,7 +475,7 @@ __device__ __forceinline__ QPResult fq_solve(const QPPattern &pt, FleetSmem &s, 
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
     R.lb[h] = fmax(R.lb[h], -QP_OSQP_INFTY); R.ub[h] = fmin(R.ub[h], QP_OSQP_INFTY);
-    R.ur[h] = fmin(fmax(R.ur[h], -QP_OSQP_INFTY), QP_OSQP_INFTY);
+    if (R.rok[h]) R.ur(h) = fmin(fmax(R.ur(h), -QP_OSQP_INFTY), QP_OSQP_INFTY);
   }
   if (st.scaling) fq_scale(pt, s, R, st.scaling);
   else {
@@ -493,14 +505,14 @@ __device__ __forceinline__ QPResult fq_solve(const QPPattern &pt, FleetSmem &s, 
       if (R.rok[h]) {
         double acc = 0.0;
         _Pragma("unroll") for (int e = 0; e < FQ_RMAX; ++e) if (e < R.rn(h)) acc += s.A[R.rb(h) + e] * s.rhs[R.rc(h, e)];
-        R.zr[h] = acc;
+        R.zr(h) = acc;
       }
       if (R.vok[h]) R.zb[h] = 0.0 + R.Ab[h] * R.x[h];
     }
   } else {
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
-      R.x[h] = 0.0; R.zr[h] = 0.0; R.yr[h] = 0.0; R.zb[h] = 0.0; R.yb[h] = 0.0;
+      R.x[h] = 0.0; R.zr(h) = 0.0; R.yr(h) = 0.0; R.zb[h] = 0.0; R.yb[h] = 0.0;
     }
   }
   __syncthreads();
@@ -547,13 +559,13 @@ __device__ __forceinline__ QPResult fq_solve(const QPPattern &pt, FleetSmem &s, 
       if (R.rok[h]) {
         double ztl = 0.0;
         _Pragma("unroll") for (int e = 0; e < FQ_RMAX; ++e) if (e < R.rn(h)) ztl += s.A[R.rb(h) + e] * s.rhs[R.rc(h, e)];
-        const double rho = QP_RHO_EQ * rs, zo = R.zr[h], yo = R.yr[h];
+        const double rho = QP_RHO_EQ * rs, zo = R.zr(h), yo = R.yr(h);
         const double zr = al * ztl + (1.0 - al) * zo;
         double zn = zr + yo / rho;
-        zn = fmin(fmax(zn, R.ur[h]), R.ur[h]);
+        zn = fmin(fmax(zn, R.ur(h)), R.ur(h));
         const double d = rho * (zr - zn);
         const double yn = yo + d;
-        R.dyr[h] = d; R.yr[h] = yn; R.zr[h] = zn;
+        R.dyr(h) = d; R.yr(h) = yn; R.zr(h) = zn;
         s.zt[R.rr[h]] = rho * zn - yn;
       }
     }
