@@ -108,6 +108,9 @@ __device__ __forceinline__ double dot_bcv(double src, const double *mul, std::in
   ((J % 2 == 0 ? (void)(a0 = fma(bc16<J>(src), mul[J], a0)) : (void)(a1 = fma(bc16<J>(src), mul[J], a1))), ...);
   return a0 + a1;
 }
+#ifndef QP_FAST_RECIP
+#define QP_FAST_RECIP 1
+#endif
 #ifndef QP_DOT_ASM
 #define QP_DOT_ASM 1
 #endif
@@ -115,6 +118,21 @@ template <int K>
 __device__ __forceinline__ double dot_bc(double src, const double *mul) {
   if (QP_DOT_ASM) return dot_bc(src, mul, std::make_integer_sequence<int, K>{});
   return dot_bcv(src, mul, std::make_integer_sequence<int, K>{});
+}
+
+// 1/p for a positive, normal pivot: v_rcp_f64 + two Newton steps (4 dependent
+// FMAs instead of the ~10-instruction IEEE division sequence on the factor's
+// critical path); within an ulp of the division.
+__device__ __forceinline__ double blk_recip(double p) {
+#if QP_FAST_RECIP
+  double r = __builtin_amdgcn_rcp(p);
+  double e = fma(-p, r, 1.0);
+  r = fma(r, e, r);
+  e = fma(-p, r, 1.0);
+  return fma(r, e, r);
+#else
+  return 1.0 / p;
+#endif
 }
 
 // ---- factor helpers: every broadcast-multiply-add is one v_fmac_f64_dpp.
@@ -181,7 +199,7 @@ __device__ __forceinline__ int blk_factor(const QPPattern &pt, S &s) {
     for (int p = 0; p < SZ; ++p) {
       const double piv = bc16_rt(a[p], p);
       if (!(piv > 0.0)) return k * SZ + p + 1;
-      const double inv = 1.0 / piv;
+      const double inv = blk_recip(piv);
       // lane p: row *= inv  (= row + row*(inv-1));  other lanes: row -= a[p]/piv * row_p
       const double f = (rr == p) ? inv - 1.0 : -a[p] * inv;
       fq_gj_update<SZ>(a, f, p);
