@@ -36,6 +36,7 @@ import numpy as np
 
 from .. import _lib
 from .constraints import ConstraintParams, TightenedConstraints
+from .cost_functions import CostWeights
 from .nominal_mpc import MPCConfig, MPCSolution, _SQPBase, trajectory_cost
 from .qp_builder import solution_to_vector, vector_to_solution
 from .uncertainty_prop import PropagatedUncertainty, UncertaintyPropagator
@@ -61,7 +62,7 @@ class GPMPC(_SQPBase):
         super().__init__(dynamics, config or GPMPCConfig(), ctx=ctx)
         self.gp = gp_model
         self.constraint_params = constraint_params or ConstraintParams()
-        self.cost_weights = cost_weights
+        self.cost_weights = cost_weights or CostWeights()
         self._tightened_constraints = TightenedConstraints(base_params=self.constraint_params,
                                                            confidence_level=self.config.confidence_level)
         self._uncertainty_prop = UncertaintyPropagator(dynamics, gp_model, ctx=ctx)
@@ -153,3 +154,49 @@ class GPMPC(_SQPBase):
         if k is None:
             return None if self._last_var is None else self._last_var.copy()
         return None if self.last_uncertainty is None else self.last_uncertainty.covariances[k].copy()
+
+
+class SimpleGPPredictor:
+    """gp_mpc.py:505-574: GP-augmented one-step prediction and rollout.
+
+    Works with either GP surface: a 4-tuple GP (StructuredRocketGP, 14 states:
+    residuals on v-dot 4:7 and omega-dot 11:14, as the reference) or a 2-tuple
+    GP (Simple3DoFGP, 7 states: residual on v-dot only).  ``simulate`` evaluates
+    the GP one step at a time like the reference (each step depends on the last).
+    """
+
+    def __init__(self, dynamics, gp_model):
+        self.dynamics = dynamics
+        self.gp = gp_model
+
+    def predict(self, x, u, dt: float):
+        x = np.asarray(x, float)
+        x_nom = np.asarray(self.dynamics.step(x, u, dt), float)
+        r = self.gp.predict(x, u)
+        n = x.size
+        x_next = x_nom.copy()
+        d_mean = np.zeros(14 if len(r) == 4 else n)
+        d_var = np.zeros_like(d_mean)
+        if len(r) == 4:
+            d_v, d_w, var_v, var_w = r
+            x_next[4:7] += d_v * dt
+            x_next[11:14] += d_w * dt
+            d_mean[4:7] = d_v; d_mean[11:14] = d_w
+            d_var[4:7] = var_v; d_var[11:14] = var_w
+        else:
+            d_v, var_v = r
+            x_next[4:7] += d_v * dt
+            d_mean[4:7] = d_v; d_var[4:7] = var_v
+        return x_next, d_mean, d_var
+
+    def simulate(self, x0, U, dt: float):
+        x0 = np.asarray(x0, float)
+        N = len(U)
+        X = np.zeros((N + 1, x0.size))
+        X[0] = x0
+        D_mean, D_var = [], []
+        for k in range(N):
+            X[k + 1], dm, dv = self.predict(X[k], U[k], dt)
+            D_mean.append(dm); D_var.append(dv)
+        width = D_mean[0].size if N else 14
+        return X, np.array(D_mean).reshape(N, width), np.array(D_var).reshape(N, width)

@@ -112,3 +112,21 @@ def test_gpmpc_propagates_and_tightens(gpu_ctx):
     kappa = norm.ppf(0.95)
     assert mpc.last_tightened_params.v_max == pytest.approx(50.0 - kappa * 1e-3, abs=1e-12)
     assert mpc.last_tightened_params.T_max == 5.0 and mpc.last_tightened_params.gamma_gs == 30.0
+
+
+def test_simple_gp_predictor_rollout_vs_f9(gpu_ctx):
+    """SimpleGPPredictor.simulate (gp_mpc.py:505-574) is the mean recursion of the
+    reference's _propagate_linear (uncertainty_prop.py:150-160): same x_nom + d dt on
+    v-dot / omega-dot, so F9's linear means pin it (gp_mpc.py itself needs CasADi)."""
+    _ctx_default(gpu_ctx)
+    from toy_dynamics import ToyRocket14
+    from gp_mpc_rocket_landing_amd.gp import StructuredGPConfig, StructuredRocketGP
+    from gp_mpc_rocket_landing_amd.mpc import SimpleGPPredictor
+    f5 = golden("f5_structured_6dof.npz"); f9 = golden("f9_uncertainty_prop.npz")
+    g = StructuredRocketGP(StructuredGPConfig(use_sparse=False))
+    g.add_data(f5["X"], f5["U"], f5["Dv"], f5["Dw"]); g.fit()
+    X, Dm, Dv = SimpleGPPredictor(ToyRocket14(), g).simulate(f9["x0"], f9["U"], 0.1)
+    np.testing.assert_allclose(X, f9["linear_means"], rtol=1e-7, atol=1e-9)
+    assert Dm.shape == (10, 14) and np.all(Dv[:, [0, 1, 2, 3, 7, 8, 9, 10]] == 0)
+    np.testing.assert_allclose(np.diff(X, axis=0)[:, 4:7] - (np.array([ToyRocket14().step(X[k], f9["U"][k], 0.1) for k in range(10)]) - X[:-1])[:, 4:7],
+                               Dm[:, 4:7] * 0.1, rtol=1e-9, atol=1e-12)

@@ -143,3 +143,25 @@ def test_tightening_arithmetic():
     w = TubeBasedRobustness(Lin(), d_max=0.2).compute_tube(np.zeros((3, 7)), np.zeros((2, 3)), 0.1)
     np.testing.assert_allclose(w[1, 4:7], 0.02); np.testing.assert_allclose(w[2, 4:7], 0.5 * 0.02 + 0.02)
     assert np.all(w[:, :4] == 0)
+
+
+def test_cost_weights_and_simple_predictor_host():
+    """CostWeights (cost_functions.py:39-105) defaults and the 2-tuple (3-DoF) path of
+    SimpleGPPredictor with a host stand-in GP."""
+    from gp_mpc_rocket_landing_amd.mpc import CostWeights, SimpleGPPredictor
+    c = CostWeights()
+    assert np.allclose(np.diag(c.Q), [0, 10, 10, 10, 1, 1, 1, 0, 5, 5, 0, 0.1, 0.1, 0.1])
+    assert np.allclose(c.R, 0.01 * np.eye(3)) and np.allclose(c.P, 10 * c.Q)
+    assert np.allclose(CostWeights(w_position=3.0).Q[1:4, 1:4], 3 * np.eye(3))
+
+    class Dyn:
+        def step(self, x, u, dt):
+            return np.asarray(x, float) + dt
+
+    class GP2:
+        def predict(self, x, u):
+            return np.array([1.0, 2.0, 3.0]), np.array([0.1, 0.2, 0.3])
+    X, Dm, Dv = SimpleGPPredictor(Dyn(), GP2()).simulate(np.zeros(7), np.zeros((4, 3)), 0.5)
+    assert X.shape == (5, 7) and Dm.shape == (4, 7)
+    np.testing.assert_allclose(X[1], [0.5, 0.5, 0.5, 0.5, 1.0, 1.5, 2.0])
+    np.testing.assert_allclose(Dv[0, 4:7], [0.1, 0.2, 0.3])
