@@ -95,6 +95,7 @@ _sig("gpmpc_gp_predict", _c, _vp, _vp, _dp, _c, _dp, _dp)
 _sig("gpmpc_gp_predict_cov", _c, _vp, _vp, _dp, _c, _dp, _dp)
 _sig("gpmpc_gp_get_state", _c, _vp, _vp, _dp, _dp)
 _sig("gpmpc_gp_destroy", _c, _vp)
+_sig("gpmpc_gp_lml_batched", _c, _vp, _c, _dp, _c, _c, _dp, _c, _dp, _dp, _dp, _dp, _ip)
 _sig("gpmpc_fitc_fit", _c, _vp, _dp, _c, _dp, _c, _c, _dp, _c, _dp, ctypes.c_double,
      ctypes.c_double, ctypes.c_double, ctypes.POINTER(_vp), _dp, _dp, _dp, _dp)
 _sig("gpmpc_fitc_predict", _c, _vp, _vp, _dp, _c, _dp, _dp)
@@ -121,6 +122,7 @@ EXPORTED = ["gpmpc_abi_version", "gpmpc_last_error", "gpmpc_ctx_create", "gpmpc_
             "gpmpc_ctx_sync", "gpmpc_ctx_stream", "gpmpc_gram", "gpmpc_potrf",
             "gpmpc_potrf_batched_dev", "gpmpc_trsm_lower", "gpmpc_potrs", "gpmpc_gp_fit_exact",
             "gpmpc_gp_predict", "gpmpc_gp_predict_cov", "gpmpc_gp_get_state", "gpmpc_gp_destroy",
+            "gpmpc_gp_lml_batched",
             "gpmpc_fitc_fit", "gpmpc_fitc_predict", "gpmpc_fitc_destroy",
             "gpmpc_qp_default_settings", "gpmpc_qp_solve_batched", "gpmpc_fleet_default_config",
             "gpmpc_fleet_create", "gpmpc_fleet_reset", "gpmpc_fleet_step", "gpmpc_fleet_read",
@@ -239,6 +241,25 @@ def potrs(ctx, L, B):
         B = B[:, None].copy()
     _chk(_L.gpmpc_potrs(ctx.h, L.shape[0], B.shape[1], _d(L), L.shape[0], _d(B), B.shape[1]), "potrs")
     return B[:, 0] if vec else B
+
+
+def gp_lml_batched(ctx, kind, X, y, ls, sigma2, noise):
+    """Log marginal likelihood of the exact GP at B parameter sets (rows of ls
+    (B x d; SE_ISO: B x 1), sigma2 (B,), noise (B,)): returns (lml (B,),
+    jitter_steps (B,)); -inf / -1 where the jitter ladder is exhausted."""
+    X = f64(np.atleast_2d(X)); n, d = X.shape
+    y = f64(np.asarray(y).reshape(-1))
+    assert y.size == n, "X and y must have same number of samples"
+    sigma2 = f64(np.atleast_1d(sigma2)); B = sigma2.size
+    noise = f64(np.broadcast_to(np.atleast_1d(noise), (B,)))
+    ls = np.atleast_2d(np.asarray(ls, dtype=np.float64))
+    L = np.empty((B, d))
+    L[:] = ls[:, :1] if ls.shape[1] == 1 else ls
+    L = f64(L)
+    lml = np.empty(B); steps = np.empty(B, np.int32)
+    _chk(_L.gpmpc_gp_lml_batched(ctx.h, kind, _d(X), n, d, _d(y), B, _d(L), _d(sigma2), _d(noise),
+                                 _d(lml), _i(steps)), "gp_lml_batched")
+    return lml, steps
 
 
 class ExactGPHandle:

@@ -5,11 +5,15 @@
 // scipy.linalg.solve_triangular and cho_solve (exact_gp.py:164-179, 251-260;
 // sparse_gp.py:187-232, 293-296).
 //
-// potrf (all matrices of a batch in the same launches): two-level blocking,
-// see launch_potrf_batched.  The 32x32 diagonal blocks are factored by
-// k_potrf_diag (LAPACK pivot test: fail unless a_jj > 0); panels, in-panel
-// updates and the trailing SYRK are MFMA GEMMs (gemm.hip).  A failed pivot
-// sets info[b] (1-based column) and freezes that matrix's diagonal steps.
+// potrf (all matrices of a batch in the same launches), default path
+// (launch_potrf_batched128): per 128-column panel, k_potrf_diag128 factors the
+// 128 x 128 diagonal block in LDS and emits its inverse, the panel below is
+// solved in place by one MFMA GEMM with that inverse, and one lower SYRK
+// (MFMA) updates the trailing matrix -- three launches per panel.  The older
+// 32-column two-level path (k_potrf_diag + GEMMs, ~100 launches at n = 1000)
+// stays behind GPMPC_POTRF128=0.  LAPACK pivot test (fail unless a_jj > 0); a
+// failed pivot sets info[b] (1-based column) and freezes that matrix's
+// diagonal steps.
 #include "internal.h"
 #include "mfma64.h"
 #include "gemm.h"
@@ -92,6 +96,266 @@ __global__ __launch_bounds__(64) void k_potrf_diag(int n, int k0, double *A, int
   }
 }
 
+// ---------------------------------------------------------------------------
+// 128 x 128 diagonal block of the outer panel, factored and inverted in one
+// workgroup per matrix with the whole block resident in LDS (128 x 130
+// doubles = 130 KB; pitch = 2 mod 32 makes the 16-row x 2-k MFMA operand
+// gathers conflict-free).  Four 32-column steps:
+//   1. wave 0: L_jj (rows in lane registers, pivot by readlane -- the
+//      k_potrf_diag algorithm) -> global memory; T_j = L_jj^-1 -> the
+//      block's lower triangle in LDS;
+//   2. panel below: X = A T_j^T (v_mfma_f64_16x16x4, K = 32), stored after a
+//      barrier (it overwrites its own operand);
+//   3. trailing lower update A -= X X^T (MFMA; disjoint from the operands).
+// Then the off-diagonal L blocks go to global memory and the full inverse
+// Linv = L^-1 (128 x 128, for the panel GEMM A[t0:n] <- A[t0:n] Linv^T) is
+// assembled block-row by block-row: X_ij = -T_i sum_{k=j}^{i-1} L_ik X_kj,
+// X_ij stored transposed in the (free) upper triangle.
+#define DB 128
+#define DP 130
+#define DIAG128_LDS (sizeof(double) * (DB * DP + NB + 2))
+__device__ __forceinline__ double rdlane(double v, int l) {
+  return __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(v), l),
+                          __builtin_amdgcn_readlane(__double2loint(v), l));
+}
+
+// diagnostic phase cycles of workgroup 0 (GPMPC_DIAG128_STAMPS=1 builds the <true> launch)
+__device__ unsigned long long g_d128_stamps[8];
+
+template <bool ST>
+__global__ __launch_bounds__(256) void k_potrf_diag128(int n, int K0, double *A, int64_t lda,
+                                                       int64_t stride, int *info, double *Linv) {
+  const int b = blockIdx.x;
+  if (info[b]) return;
+  unsigned long long tl = 0;
+  auto mark = [&](int k) {
+    if (ST && b == 0 && threadIdx.x == 0) {
+      const unsigned long long t = __builtin_amdgcn_s_memtime();
+      if (k >= 0) atomicAdd(&g_d128_stamps[k], t - tl);
+      tl = t;
+    }
+  };
+  mark(-1);
+  // one dynamic region (no static LDS in front of it): S, then col, then the fail flag
+  extern __shared__ double S_[];
+  double(*S)[DP] = reinterpret_cast<double(*)[DP]>(S_);
+  double *col = S_ + DB * DP;
+  int &sfail = *reinterpret_cast<int *>(S_ + DB * DP + NB);
+  double *M = A + (int64_t)b * stride + (int64_t)K0 * lda + K0;
+  const int pw = min(DB, n - K0);
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int li = lane & 15, lk = lane >> 4;
+  // lower triangle in, identity padding beyond pw, zero upper triangle; 32 loads
+  // in flight per lane before the LDS stores (a load-store loop waits out the
+  // HBM latency once per element)
+#pragma unroll 1
+  for (int q0 = 0; q0 < DB * DB / 256; q0 += 16) {
+    double v[16];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int e = tid + 256 * (q0 + q), i = e >> 7, j = e & 127;
+      v[q] = (j <= i && i < pw) ? M[(int64_t)i * lda + j] : (i == j ? 1.0 : 0.0);
+    }
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int e = tid + 256 * (q0 + q);
+      S[e >> 7][e & 127] = v[q];
+    }
+  }
+  if (tid == 0) sfail = 0;
+  __syncthreads();
+  mark(0);
+  for (int jb = 0; jb < DB / NB; ++jb) {
+    const int c0 = jb * NB;
+    // ---- 1. diagonal 32 x 32 block (wave 0).  Row `lane` of the block lives in
+    // a[]; every cross-lane operand comes by v_readlane (a uniform SGPR pair), so
+    // the serial column chain has no LDS round trips.
+    if (wave == 0) {
+      double a[NB], ig = 1.0;
+#pragma unroll
+      for (int j = 0; j < NB; ++j) a[j] = (lane < NB && j <= lane) ? S[c0 + lane][c0 + j] : 0.0;
+      int fail = 0;
+#pragma unroll
+      for (int j = 0; j < NB; ++j) {
+        const double piv = rdlane(a[j], j);
+        if (fail == 0 && !(piv > 0.0)) fail = j + 1;
+        if (fail) continue;  // (no break: keeps the loop fully unrolled, a[] in registers)
+        const double d = sqrt(piv), id = 1.0 / d;
+        if (lane == j) ig = id;
+        a[j] = (lane == j) ? d : a[j] * id;       // L[lane][j]
+#pragma unroll
+        for (int k = j + 1; k < NB; ++k) a[k] = fma(-a[j], rdlane(a[j], k), a[k]);
+      }
+      if (fail) {
+        if (lane == 0) {
+          info[b] = K0 + c0 + fail;
+          sfail = 1;
+        }
+      } else {
+        if (lane < NB && c0 + lane < pw) {
+#pragma unroll
+          for (int j = 0; j < NB; ++j)
+            if (j <= lane) M[(int64_t)(c0 + lane) * lda + c0 + j] = a[j];
+        }
+        // T = L_jj^-1 row by row (row `lane` in t[]): forward substitution,
+        // row k final once scaled by 1/L_kk, then eliminated from the rows below
+        double t[NB];
+#pragma unroll
+        for (int c = 0; c < NB; ++c) t[c] = (lane == c) ? 1.0 : 0.0;
+#pragma unroll
+        for (int k = 0; k < NB; ++k) {
+          if (lane == k) {
+#pragma unroll
+            for (int c = 0; c <= k; ++c) t[c] *= ig;
+          }
+          const double lrk = (lane > k) ? a[k] : 0.0;
+#pragma unroll
+          for (int c = 0; c <= k; ++c) t[c] = fma(-lrk, rdlane(t[c], k), t[c]);
+        }
+        if (lane < NB) {
+#pragma unroll
+          for (int c = 0; c < NB; ++c)
+            if (c <= lane) S[c0 + lane][c0 + c] = t[c];
+        }
+      }
+    }
+    __syncthreads();
+    mark(1);
+    if (sfail) return;
+    const int R = DB - c0 - NB;  // rows below the diagonal block
+    if (R == 0) break;
+    // ---- 2. panel X = A T^T: (R/16) x 2 tiles of 16 x 16, K = 32
+    {
+      const int nt = (R >> 4) * 2;
+      d4_t acc[3];
+#pragma unroll
+      for (int q = 0; q < 3; ++q) {
+        acc[q] = d4_t{0.0, 0.0, 0.0, 0.0};
+        const int t = wave + 4 * q;
+        if (t < nt) {
+          const int rb = c0 + NB + (t >> 1) * 16, cb = (t & 1) * 16;
+#pragma unroll
+          for (int kk = 0; kk < NB; kk += 4) {
+            const int k = kk + lk, cc = cb + li;
+            const double av = S[rb + li][c0 + k];
+            const double bv = (k <= cc) ? S[c0 + cc][c0 + k] : 0.0;  // T[cc][k], lower
+            acc[q] = mfma_f64(av, bv, acc[q]);
+          }
+        }
+      }
+      __syncthreads();
+#pragma unroll
+      for (int q = 0; q < 3; ++q) {
+        const int t = wave + 4 * q;
+        if (t < nt) {
+          const int rb = c0 + NB + (t >> 1) * 16, cb = (t & 1) * 16;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) S[rb + mf_row(lane, r)][c0 + cb + li] = acc[q][r];
+        }
+      }
+      __syncthreads();
+      mark(2);
+    }
+    // ---- 3. trailing lower update A[t][t] -= X X^T over 16 x 16 tiles (ti >= tj)
+    {
+      const int t0 = c0 + NB, nr = R >> 4, ntile = nr * (nr + 1) / 2;
+      for (int t = wave; t < ntile; t += 4) {
+        int ti = 0;
+        while ((ti + 1) * (ti + 2) / 2 <= t) ++ti;
+        const int tj = t - ti * (ti + 1) / 2;
+        const int rb = t0 + ti * 16, cb = t0 + tj * 16;
+        d4_t acc = d4_t{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int kk = 0; kk < NB; kk += 4) {
+          const int k = c0 + kk + lk;
+          acc = mfma_f64(S[rb + li][k], S[cb + li][k], acc);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) S[rb + mf_row(lane, r)][cb + li] -= acc[r];
+      }
+      __syncthreads();
+      mark(3);
+    }
+  }
+  // off-diagonal blocks of L to global memory (diagonal blocks went out in step 1)
+#pragma unroll 4
+  for (int e = tid; e < DB * DB; e += 256) {
+    const int i = e >> 7, j = e & 127;
+    if ((j >> 5) < (i >> 5) && i < pw) M[(int64_t)i * lda + j] = S[i][j];
+  }
+  mark(4);
+  if (pw < DB || !Linv) return;  // the last panel has no rows below: no inverse needed
+  // ---- inverse, block row i = 1..3:  Y_j = sum_k L_ik X_kj -> upper block (j, i)
+  // transposed; then X_ij = -T_i Y_j in place.  Jobs: (j, 16x16 tile) pairs.
+  for (int i = 1; i < DB / NB; ++i) {
+    const int njob = 4 * i;
+    d4_t acc[3];
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      acc[q] = d4_t{0.0, 0.0, 0.0, 0.0};
+      const int jt = wave + 4 * q;
+      if (jt < njob) {
+        const int j = jt >> 2, rb = (jt >> 1 & 1) * 16, cb = (jt & 1) * 16;
+        for (int k = j; k < i; ++k) {
+#pragma unroll
+          for (int mm = 0; mm < NB; mm += 4) {
+            const int m = mm + lk, cc = cb + li;
+            const double av = S[i * NB + rb + li][k * NB + m];            // L_ik[r][m]
+            double bv;                                                      // X_kj[m][cc]
+            if (k == j) bv = (cc <= m) ? S[j * NB + m][j * NB + cc] : 0.0;  // T_j lower
+            else bv = S[j * NB + cc][k * NB + m];                           // transposed X_kj
+            acc[q] = mfma_f64(av, bv, acc[q]);
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      const int jt = wave + 4 * q;
+      if (jt < njob) {
+        const int j = jt >> 2, rb = (jt >> 1 & 1) * 16, cb = (jt & 1) * 16;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) S[j * NB + cb + li][i * NB + rb + mf_row(lane, r)] = acc[q][r];
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      acc[q] = d4_t{0.0, 0.0, 0.0, 0.0};
+      const int jt = wave + 4 * q;
+      if (jt < njob) {
+        const int j = jt >> 2, rb = (jt >> 1 & 1) * 16, cb = (jt & 1) * 16;
+#pragma unroll
+        for (int mm = 0; mm < NB; mm += 4) {
+          const int m = mm + lk, rr = rb + li;
+          const double av = (m <= rr) ? S[i * NB + rr][i * NB + m] : 0.0;  // T_i[rr][m]
+          const double bv = S[j * NB + cb + li][i * NB + m];                // Y_j[m][cb+li]
+          acc[q] = mfma_f64(av, bv, acc[q]);
+        }
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      const int jt = wave + 4 * q;
+      if (jt < njob) {
+        const int j = jt >> 2, rb = (jt >> 1 & 1) * 16, cb = (jt & 1) * 16;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) S[j * NB + cb + li][i * NB + rb + mf_row(lane, r)] = -acc[q][r];
+      }
+    }
+    __syncthreads();
+  }
+  mark(5);
+  double *Li = Linv + (int64_t)b * DB * DB;
+#pragma unroll 4
+  for (int e = tid; e < DB * DB; e += 256) {
+    const int i = e >> 7, j = e & 127;
+    Li[e] = (j > i) ? 0.0 : ((i >> 5) == (j >> 5) ? S[i][j] : S[j][i]);
+  }
+  mark(6);
+}
+
 // Two-level blocking.  Outer panels of OB = 128 columns; inside a panel,
 // 32-wide steps (left-looking within the panel):
 //   1. A[k0:n, k0:k0+32] -= A[k0:n, K0:k0] A[k0:k0+32, K0:k0]^T   (MFMA GEMM, K <= 96)
@@ -135,8 +399,91 @@ hipError_t launch_potrf_batched(hipStream_t s, int n, int batch, double *A, int6
   return hipGetLastError();
 }
 
+// Outer panels of 128 with the fused diagonal kernel: per panel three launches
+//   k_potrf_diag128            L_KK (global) and Linv = L_KK^-1 (scratch)
+//   A[t0:n, K0:t0] <- A[t0:n, K0:t0] Linv^T      (MFMA, K = 128, in place)
+//   A[t0:n, t0:n]  -= A[t0:n, K0:t0] A[t0:n, K0:t0]^T  (lower SYRK, K = 128)
+static hipError_t launch_potrf_batched128(hipStream_t s, int n, int batch, double *A, int64_t lda,
+                                          int64_t stride, int *info, double *Linv) {
+  static const bool st = [] {
+    const char *e = getenv("GPMPC_DIAG128_STAMPS");
+    return e && atoi(e);
+  }();
+  static bool attr = [] {
+    return hipFuncSetAttribute((const void *)k_potrf_diag128<false>,
+                               hipFuncAttributeMaxDynamicSharedMemorySize,
+                               (int)DIAG128_LDS) == hipSuccess &&
+           hipFuncSetAttribute((const void *)k_potrf_diag128<true>,
+                               hipFuncAttributeMaxDynamicSharedMemorySize,
+                               (int)DIAG128_LDS) == hipSuccess;
+  }();
+  if (!attr) return hipErrorInvalidConfiguration;
+  hipError_t e = hipMemsetAsync(info, 0, sizeof(int) * batch, s);
+  if (e != hipSuccess) return e;
+  auto at = [&](int r, int c) { return A + (int64_t)r * lda + c; };
+  // panel solve A[c+128:n, c:c+128] <- A[c+128:n, c:c+128] Linv^T (in place)
+  auto psolve = [&](int c) {
+    const int r = c + DB;
+    return launch_gemm_nt_rowblock(s, n - r, DB, DB, at(r, c), lda, Linv, DB, at(r, c), lda, 1.0,
+                                   0.0, batch, stride, (int64_t)DB * DB, stride);
+  };
+  // Outer panels of OB = 128 m columns.  Inside a panel, 128-column steps are
+  // left-looking (a step's columns take the update of the panel's earlier
+  // steps, K = c - K0); across panels, one lower SYRK with K = OB, so the
+  // O(n^3) work runs as K = OB products (fewer C read-modify-writes, longer K).
+  static const int ob_env = [] {
+    const char *v = getenv("GPMPC_POTRF_OB");
+    const int m = v ? atoi(v) / DB : 1;  // 256 / 384 / 512 measured 5-10% slower at n = 1000
+    return DB * (m < 1 ? 1 : m > 8 ? 8 : m);
+  }();
+  const int OBk = ob_env;
+  for (int K0 = 0; K0 < n; K0 += OBk) {
+    const int pw = min(OBk, n - K0);
+    for (int c = K0; c < K0 + pw; c += DB) {
+      const int w = min(DB, n - c);
+      if (c > K0) {
+        e = launch_gemm_nt_rowblock(s, n - c, w, c - K0, at(c, K0), lda, at(c, K0), lda,
+                                    at(c, c), lda, -1.0, 1.0, batch, stride, stride, stride, 1);
+        if (e != hipSuccess) return e;
+      }
+      if (st)
+        hipLaunchKernelGGL(k_potrf_diag128<true>, dim3(batch), dim3(256), DIAG128_LDS, s, n, c, A,
+                           lda, stride, info, c + DB < n ? Linv : nullptr);
+      else
+        hipLaunchKernelGGL(k_potrf_diag128<false>, dim3(batch), dim3(256), DIAG128_LDS, s, n, c,
+                           A, lda, stride, info, c + DB < n ? Linv : nullptr);
+      if (c + DB < n && (e = psolve(c)) != hipSuccess) return e;
+    }
+    const int t0 = K0 + pw;
+    if (t0 < n) {
+      e = launch_gemm_nt(s, EPI_STORE, n - t0, n - t0, pw, at(t0, K0), lda, at(t0, K0), lda,
+                         at(t0, t0), lda, -1.0, 1.0, 0, 1, batch, stride, stride, stride);
+      if (e != hipSuccess) return e;
+    }
+  }
+  if (st) {  // diagnostic: accumulated phase cycles of workgroup 0 over all panels
+    unsigned long long h[8];
+    (void)hipStreamSynchronize(s);
+    (void)hipMemcpyFromSymbol(h, HIP_SYMBOL(g_d128_stamps), sizeof(h));
+    fprintf(stderr, "diag128 cycles: load %llu diag %llu panel %llu trail %llu lout %llu inv %llu "
+                    "linvout %llu\n", h[0], h[1], h[2], h[3], h[4], h[5], h[6]);
+    const unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(g_d128_stamps), z, sizeof(z));
+  }
+  return hipGetLastError();
+}
+
 hipError_t launch_potrf_batched(hipStream_t s, int n, int batch, double *A, int64_t lda,
                                 int64_t stride, int *info) {
+  static const int p128 = [] {
+    const char *e = getenv("GPMPC_POTRF128");
+    return e ? atoi(e) : 1;
+  }();
+  if (p128) {
+    double *Linv = (double *)gpmpc_scratch(2, sizeof(double) * DB * DB * (size_t)batch);
+    if (!Linv) return hipErrorOutOfMemory;
+    return launch_potrf_batched128(s, n, batch, A, lda, stride, info, Linv);
+  }
   double *Linv = (double *)gpmpc_scratch(1, sizeof(double) * NB * NB * (size_t)batch);
   if (!Linv) return hipErrorOutOfMemory;
   return launch_potrf_batched(s, n, batch, A, lda, stride, info, Linv);

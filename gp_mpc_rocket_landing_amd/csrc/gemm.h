@@ -13,6 +13,13 @@ hipError_t launch_gemm_nt(hipStream_t s, int epi, int M, int N, int K, const dou
                           double alpha, double beta, int tri_a, int lower_c, int batch,
                           int64_t sA, int64_t sB, int64_t sC);
 
+// C = alpha A B^T + beta C, N <= 128, one workgroup per 128-row block (C may alias
+// A); lower_c: only C[i][j] with j <= i (relative to C) is written
+hipError_t launch_gemm_nt_rowblock(hipStream_t s, int M, int N, int K, const double *A,
+                                   int64_t lda, const double *B, int64_t ldb, double *C,
+                                   int64_t ldc, double alpha, double beta, int batch, int64_t sA,
+                                   int64_t sB, int64_t sC, int lower_c = 0);
+
 // C = alpha A B + beta C with B (K x N) row-major ("NN")
 hipError_t launch_gemm_nn(hipStream_t s, int M, int N, int K, const double *A, int64_t lda,
                           const double *B, int64_t ldb, double *C, int64_t ldc, double alpha,

@@ -562,6 +562,21 @@ hipError_t launch_gemm_tn(hipStream_t s, int M, int N, int K, const double *A, i
   return hipGetLastError();
 }
 
+// C = alpha A B^T + beta C with N <= 128 on the 128 x 128 tile kernel: one
+// workgroup owns whole rows of C, so C may alias A (every A read of a row
+// block precedes its epilogue) -- the in-place panel solve of the potrf.
+hipError_t launch_gemm_nt_rowblock(hipStream_t s, int M, int N, int K, const double *A,
+                                   int64_t lda, const double *B, int64_t ldb, double *C,
+                                   int64_t ldc, double alpha, double beta, int batch, int64_t sA,
+                                   int64_t sB, int64_t sC, int lower_c) {
+  if (M <= 0 || N <= 0) return hipSuccess;
+  if (N > BT) return hipErrorInvalidValue;
+  dim3 g(1, (M + BT - 1) / BT, batch);
+  hipLaunchKernelGGL(k_gemm128<EPI_STORE>, g, dim3(256), 0, s, M, N, K, A, lda, B, ldb, C, ldc,
+                     alpha, beta, 0, lower_c, sA, sB, sC, M, nullptr, (int64_t)0, 1, 0);
+  return hipGetLastError();
+}
+
 hipError_t launch_gemm_nt(hipStream_t s, int epi, int M, int N, int K, const double *A,
                           int64_t lda, const double *B, int64_t ldb, double *C, int64_t ldc,
                           double alpha, double beta, int tri_a, int lower_c, int batch,

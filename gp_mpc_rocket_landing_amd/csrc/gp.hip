@@ -590,3 +590,166 @@ extern "C" int gpmpc_fitc_destroy(gpmpc_fitc *gp) {
   delete gp;
   return 0;
 }
+
+// ---------------------------------------------------------------------------
+// batched log marginal likelihood for hyperparameter search
+// (ExactGP.optimize_hyperparameters, exact_gp.py:357-421: every objective call
+// is a full ExactGP.fit, :118-204).  Per parameter set b: K_b + noise_b I,
+// Cholesky (all B in one batched potrf, the jitter ladder of :163-175 for the
+// ones that fail), then lml_b = -1/2 |L_b^-1 y|^2 - sum log L_ii - n/2 log 2 pi
+// (|L^-1 y|^2 = y^T alpha).
+//
+// k_lml_trsv: one workgroup per matrix, x = L^-1 y right-looking by 32-row
+// blocks: wave 0 solves the block's triangle in registers (readlane
+// broadcasts), then all 256 threads subtract L[r, blk] x_blk from the
+// remaining right-hand side (one row per thread, its 32 block entries are
+// contiguous), so L's lower triangle is read once.
+__global__ __launch_bounds__(256) void k_lml_trsv(int n, const double *__restrict__ L,
+                                                  int64_t stride, const double *__restrict__ yn,
+                                                  const int *__restrict__ info,
+                                                  double *__restrict__ lml) {
+  const int b = blockIdx.x;
+  if (info[b]) return;
+  const double *M = L + (int64_t)b * stride;
+  extern __shared__ double s_[];  // rhs / solution (n), then 4 reduction slots
+  double *x = s_, *red = s_ + n;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  for (int i = tid; i < n; i += 256) x[i] = yn[i];
+  __syncthreads();
+  double logdet = 0.0;
+  for (int r0 = 0; r0 < n; r0 += 32) {
+    const int nb = min(32, n - r0);
+    if (wave == 0) {
+      double a[32];
+#pragma unroll
+      for (int j = 0; j < 32; ++j)
+        a[j] = (lane < nb && j <= lane) ? M[(int64_t)(r0 + lane) * n + r0 + j] : 1.0;
+      double s = lane < nb ? x[r0 + lane] : 0.0, dg = 1.0;
+#pragma unroll
+      for (int j = 0; j < 32; ++j) {
+        if (j < nb) {
+          if (lane == j) {
+            dg = a[j];
+            s = s / a[j];
+          }
+          const double xj = __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(s), j),
+                                             __builtin_amdgcn_readlane(__double2loint(s), j));
+          if (lane > j) s = fma(-a[j], xj, s);
+        }
+      }
+      if (lane < nb) {
+        x[r0 + lane] = s;
+        logdet += log(dg);
+      }
+    }
+    __syncthreads();
+    const int r1 = r0 + nb;
+    if (r1 < n) {
+      double xb[32];
+#pragma unroll
+      for (int j = 0; j < 32; ++j) xb[j] = x[r0 + j];  // LDS broadcast
+      for (int r = r1 + tid; r < n; r += 256) {
+        const double *row = M + (int64_t)r * n + r0;
+        double acc = 0.0;
+#pragma unroll
+        for (int j = 0; j < 32; ++j) acc = fma(row[j], xb[j], acc);
+        x[r] -= acc;
+      }
+    }
+    __syncthreads();
+  }
+  double fit = 0.0;
+  for (int i = tid; i < n; i += 256) fit = fma(x[i], x[i], fit);
+  fit = block_sum(fit, red);
+  const double ld = block_sum(logdet, red);
+  if (tid == 0) lml[b] = -0.5 * fit - ld - 0.5 * n * log(2.0 * M_PI);
+}
+
+extern "C" int gpmpc_gp_lml_batched(gpmpc_ctx *ctx, int kind, const double *X, int n, int d,
+                                    const double *y, int B, const double *ls,
+                                    const double *sigma2, const double *noise, double *lml,
+                                    int *jitter_steps) {
+  GPMPC_CHECK_ARG(ctx && X && y && ls && sigma2 && noise && lml && jitter_steps);
+  GPMPC_CHECK_ARG(n >= 1 && d >= 1 && d <= 32 && B >= 1 && kind >= 0 && kind <= 3);
+  GPMPC_CHECK_ARG((size_t)n * sizeof(double) + 64 <= 160 * 1024);
+  GPMPC_HIP(hipSetDevice(ctx->device));
+  hipStream_t s = ctx->stream;
+  const int iso = (kind == GPMPC_SE_ISO);
+  const size_t nn = (size_t)n * n;
+  DevBuf dX, dY, dyn, dm, dsd, dls, Xs, Xn, K, dinfo, dlml;
+  GPMPC_HIP(dX.alloc(sizeof(double) * n * d));
+  GPMPC_HIP(dY.alloc(sizeof(double) * n));
+  GPMPC_HIP(dyn.alloc(sizeof(double) * n));
+  GPMPC_HIP(dm.alloc(sizeof(double)));
+  GPMPC_HIP(dsd.alloc(sizeof(double)));
+  GPMPC_HIP(dls.alloc(sizeof(double) * B * d));
+  GPMPC_HIP(Xs.alloc(sizeof(double) * (size_t)B * n * d));
+  GPMPC_HIP(Xn.alloc(sizeof(double) * (size_t)B * n));
+  if (K.alloc(sizeof(double) * nn * B) != hipSuccess) {
+    gpmpc_set_error("gp_lml_batched: out of device memory for %d x %d^2 doubles", B, n);
+    return -1;
+  }
+  GPMPC_HIP(dinfo.alloc(sizeof(int) * B));
+  GPMPC_HIP(dlml.alloc(sizeof(double) * B));
+  GPMPC_HIP(hipMemcpyAsync(dX.p, X, sizeof(double) * n * d, hipMemcpyHostToDevice, s));
+  GPMPC_HIP(hipMemcpyAsync(dY.p, y, sizeof(double) * n, hipMemcpyHostToDevice, s));
+  GPMPC_HIP(hipMemcpyAsync(dls.p, ls, sizeof(double) * B * d, hipMemcpyHostToDevice, s));
+  // exact_gp.py:141-150 (the same normalisation for every parameter set)
+  hipLaunchKernelGGL(k_normalise, dim3(1), dim3(256), 0, s, n, 1, dY.as<double>(), dyn.as<double>(),
+                     dm.as<double>(), dsd.as<double>());
+  auto build = [&](int b, double jit) -> hipError_t {  // K_b + noise_b I (+ jit I)
+    double *Kb = K.as<double>() + nn * b;
+    hipError_t e = launch_gram(s, kind, Xs.as<double>() + (size_t)b * n * d,
+                               Xn.as<double>() + (size_t)b * n, n,
+                               Xs.as<double>() + (size_t)b * n * d, Xn.as<double>() + (size_t)b * n,
+                               n, d, sigma2[b], iso ? 1.0 / (2.0 * ls[(size_t)b * d] * ls[(size_t)b * d]) : 0.0,
+                               Kb, n, 0);
+    if (e == hipSuccess) e = launch_add_diag(s, n, Kb, n, noise[b], 1, 0);
+    if (e == hipSuccess && jit > 0.0) e = launch_add_diag(s, n, Kb, n, jit, 1, 0);
+    return e;
+  };
+  for (int b = 0; b < B; ++b) {
+    GPMPC_HIP(launch_scale_rows(s, dX.as<double>(), n, d, dls.as<double>() + (size_t)b * d, iso,
+                                Xs.as<double>() + (size_t)b * n * d, Xn.as<double>() + (size_t)b * n));
+    GPMPC_HIP(build(b, 0.0));
+  }
+  GPMPC_HIP(launch_potrf_batched(s, n, B, K.as<double>(), n, (int64_t)nn, dinfo.as<int>()));
+  std::vector<int> info(B);
+  GPMPC_HIP(hipMemcpyAsync(info.data(), dinfo.p, sizeof(int) * B, hipMemcpyDeviceToHost, s));
+  GPMPC_HIP(hipStreamSynchronize(s));
+  // jitter ladder (exact_gp.py:163-175) for the sets whose first factorisation failed
+  for (int b = 0; b < B; ++b) {
+    jitter_steps[b] = 0;
+    if (!info[b]) continue;
+    double jit = 1e-6;
+    int steps = 1, ok = 0;
+    while (jit < 1.0) {
+      GPMPC_HIP(build(b, jit));
+      GPMPC_HIP(launch_potrf_batched(s, n, 1, K.as<double>() + nn * b, n, 0,
+                                     dinfo.as<int>() + b));
+      int ib = 0;
+      GPMPC_HIP(hipMemcpyAsync(&ib, dinfo.as<int>() + b, sizeof(int), hipMemcpyDeviceToHost, s));
+      GPMPC_HIP(hipStreamSynchronize(s));
+      if (!ib) { ok = 1; break; }
+      jit *= 10;
+      ++steps;
+    }
+    jitter_steps[b] = ok ? steps : -1;
+  }
+  static const bool attr = hipFuncSetAttribute((const void *)k_lml_trsv,
+                                                hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                160 * 1024) == hipSuccess;
+  if (!attr) {
+    gpmpc_set_error("gp_lml_batched: LDS attribute");
+    return -1;
+  }
+  hipLaunchKernelGGL(k_lml_trsv, dim3(B), dim3(256), sizeof(double) * (n + 4), s, n,
+                     K.as<double>(), (int64_t)nn, dyn.as<double>(), dinfo.as<int>(),
+                     dlml.as<double>());
+  GPMPC_HIP(hipGetLastError());
+  GPMPC_HIP(hipMemcpyAsync(lml, dlml.p, sizeof(double) * B, hipMemcpyDeviceToHost, s));
+  GPMPC_HIP(hipStreamSynchronize(s));
+  for (int b = 0; b < B; ++b)
+    if (jitter_steps[b] < 0) lml[b] = -INFINITY;
+  return 0;
+}

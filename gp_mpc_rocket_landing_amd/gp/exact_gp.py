@@ -11,11 +11,18 @@ MultiOutputExactGP fits every output with ONE Gram + ONE Cholesky when the
 per-output kernels and noise are identical (the default construction; SURVEY
 D13) -- the reference repeats both per output.
 
+ExactGP.optimize_hyperparameters keeps the reference's L-BFGS-B
+with finite-difference gradients, but evaluates f(x) and the n_params probes
+f(x + h e_i) of each gradient as ONE batched device call
+(gpmpc_gp_lml_batched: all Grams, one batched Cholesky, batched triangular
+solves).
+
 Not on this path: mean_function / normalize_y=False (NotImplementedError),
-composite kernels in a fitted GP, optimize_hyperparameters.
+composite kernels in a fitted GP.
 """
 from __future__ import annotations
 
+import copy
 from dataclasses import dataclass
 from typing import Optional, Tuple
 
@@ -179,6 +186,84 @@ class ExactGP:
         if info:
             raise np.linalg.LinAlgError("Matrix is not positive definite")
         return (mean[:, None] + L @ np.random.randn(np.atleast_2d(X).shape[0], n_samples)).T
+
+    def _lml_batch(self, P, X, y):
+        """Log marginal likelihoods at the rows of P = [kernel params (log
+        space, kernels.py:320-371 order), log noise] -- the objective of
+        exact_gp.py:375-386 for every row, one device call."""
+        P = np.atleast_2d(P)
+        nk = self.kernel.n_params
+        k2 = copy.deepcopy(self.kernel)
+        kind = None
+        ls, s2 = [], []
+        for p in P:
+            k2.set_params(p[:nk])
+            kd, l, s = _spec(k2)
+            kind = kd
+            ls.append(np.asarray(l, float).reshape(-1)); s2.append(float(s))
+        lml, steps = _lib.gp_lml_batched(_lib.default_context(), kind, X, y, np.stack(ls),
+                                         np.array(s2), np.exp(P[:, nk]))
+        return lml, steps
+
+    def optimize_hyperparameters(self, n_restarts: int = 5, verbose: bool = False) -> dict:
+        """exact_gp.py:357-421: maximise the LML over [kernel params, log noise]
+        with L-BFGS-B (maxiter 100) from the current parameters, then
+        n_restarts - 1 restarts perturbed by 0.5 * np.random.randn (global RNG);
+        the best result is set and refitted.  The gradient is scipy's 2-point
+        rule with L-BFGS-B's absolute step eps = 1e-8 (scipy/_numdiff.py:
+        h = 1e-8, dx = (x + h) - x, g_i = (f(x + dx e_i) - f(x)) / dx), so the
+        optimiser sees what the reference's sees; f(x) and the n_params probes
+        are one batched device evaluation.  A failed fit (jitter ladder
+        exhausted) is +inf, as in the reference."""
+        if self.X_train is None:
+            raise RuntimeError("Must call fit() before optimize_hyperparameters()")
+        from scipy.optimize import minimize
+        X = self.X_train
+        y = self.y_train * self._y_std + self._y_mean  # what the objective refits with (:382)
+        nk = self.kernel.n_params
+        eps_fallback = np.finfo(float).eps ** 0.5
+
+        def fun_and_grad(x):
+            x = np.asarray(x, float)
+            h = np.full(x.size, 1e-8)
+            dx = (x + h) - x
+            sign = (x >= 0).astype(float) * 2 - 1
+            h = np.where(dx == 0, eps_fallback * sign * np.maximum(1.0, np.abs(x)), h)
+            P = np.repeat(x[None, :], x.size + 1, axis=0)
+            steps = np.empty(x.size)
+            for i in range(x.size):
+                P[i + 1, i] += h[i]
+                steps[i] = P[i + 1, i] - x[i]
+            lml, _ = self._lml_batch(P, X, y)
+            f = -lml
+            with np.errstate(invalid="ignore", over="ignore"):
+                g = (f[1:] - f[0]) / steps
+            return float(f[0]), g
+
+        initial = np.concatenate([self.kernel.get_params(), [np.log(self._noise_variance)]])
+        best_result, best_nll = None, np.inf
+        for restart in range(n_restarts):
+            params0 = initial if restart == 0 else initial + 0.5 * np.random.randn(len(initial))
+            try:
+                result = minimize(fun_and_grad, params0, jac=True, method="L-BFGS-B",
+                                  options={"maxiter": 100, "disp": verbose})
+                if result.fun < best_nll:
+                    best_nll, best_result = result.fun, result
+            except Exception as e:  # noqa: BLE001  (exact_gp.py:407-409)
+                if verbose:
+                    print(f"Restart {restart} failed: {e}")
+        if best_result is not None:
+            self.kernel.set_params(best_result.x[:nk])
+            self._noise_variance = float(np.exp(best_result.x[nk]))
+            try:
+                self.fit(X, y)
+            except ValueError:
+                self._invalidate_cache()
+        return {
+            "success": best_result is not None and bool(best_result.success),
+            "log_marginal_likelihood": -best_nll if best_result else None,
+            "n_iterations": best_result.nit if best_result else 0,
+        }
 
     def __repr__(self) -> str:
         return f"ExactGP(n_train={self.n_train}, kernel={self.kernel!r})"

@@ -104,6 +104,20 @@ int gpmpc_gp_predict_cov(gpmpc_ctx *ctx, gpmpc_gp *gp, const double *Xq, int p, 
 int gpmpc_gp_get_state(gpmpc_ctx *ctx, gpmpc_gp *gp, double *L, double *alpha);
 int gpmpc_gp_destroy(gpmpc_gp *gp);
 
+/* ---- 8f-3: batched log marginal likelihood (hyperparameter search) --------
+ * Replaces the objective of ExactGP.optimize_hyperparameters
+ * (exact_gp.py:357-421), each call of which is a full ExactGP.fit
+ * (exact_gp.py:118-204), for B parameter sets at once: per set b the Gram of
+ * X (n x d) with lengthscales ls[b*d .. b*d+d) (SE_ISO: ls[b*d]) and signal
+ * variance sigma2[b], + noise[b] I, Cholesky (one batched launch; the
+ * exact_gp.py:163-175 jitter ladder for sets that fail), and
+ * lml[b] = -1/2 y^T alpha - sum log L_ii - n/2 log 2 pi on the normalised y.
+ * jitter_steps[b] = 0..6, or -1 (and lml[b] = -inf) when the ladder is
+ * exhausted -- the reference objective's ValueError -> inf. */
+int gpmpc_gp_lml_batched(gpmpc_ctx *ctx, int kind, const double *X, int n, int d,
+                         const double *y, int B, const double *ls, const double *sigma2,
+                         const double *noise, double *lml, int *jitter_steps);
+
 /* ---- a8-a10: FITC sparse GP ----------------------------------------------
  * MultiOutputSparseGP.fit (sparse_gp.py:430-456 -> SparseGP.fit FITC :150-219)
  * with caller-supplied inducing points Z (m x d) shared by all outputs.

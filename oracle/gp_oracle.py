@@ -257,3 +257,48 @@ def simple3dof_fit_predict_exact(X, U, D, Xq, Uq, noise=1e-4):
     """Simple3DoFGP(use_sparse=False).fit / predict (structured_gp.py:470-493)."""
     st = exact_fit(features_3dof(X, U), D, noise=noise)
     return st, exact_predict(st, features_3dof(Xq, Uq))
+
+
+# --------------------------------------------------------------------------
+# hyperparameter search (SURVEY 8f-3)
+# --------------------------------------------------------------------------
+def lml_at(Z, y, sigma2, ls, noise, kind="se_ard"):
+    """The objective of ExactGP.optimize_hyperparameters (exact_gp.py:375-386):
+    a full ExactGP.fit (exact_gp.py:118-204) at one parameter set; returns
+    (lml, jitter_steps), (-inf, -1) where the fit raises ValueError."""
+    try:
+        st = exact_fit(Z, y, kind=kind, sigma2=sigma2, ls=ls, noise=noise)
+    except ValueError:
+        return -np.inf, -1
+    return float(st["lml"][0]), st["jitter_steps"]
+
+
+def optimize_hyperparameters(Z, y, params0, noise0, n_restarts=5, kind="se_ard"):
+    """ExactGP.optimize_hyperparameters (exact_gp.py:357-421) for SE-ARD:
+    params = [log sigma2, log l_0..l_{D-1}] (kernels.py:320-371 order) + log
+    noise; L-BFGS-B (maxiter 100) with scipy's own finite-difference gradient;
+    restarts perturb with 0.5 * np.random.randn (global RNG, as the reference).
+    Returns (result dict, best params (kernel), best noise)."""
+    from scipy.optimize import minimize
+    y = np.asarray(y, float).reshape(-1)
+
+    def objective(p):
+        lml, _ = lml_at(Z, y, float(np.exp(p[0])), np.exp(p[1:-1]), float(np.exp(p[-1])), kind)
+        return -lml
+
+    initial = np.concatenate([np.asarray(params0, float), [np.log(noise0)]])
+    best, best_nll = None, np.inf
+    for r in range(n_restarts):
+        p0 = initial if r == 0 else initial + 0.5 * np.random.randn(len(initial))
+        try:
+            res = minimize(objective, p0, method="L-BFGS-B", options={"maxiter": 100, "disp": False})
+            if res.fun < best_nll:
+                best_nll, best = res.fun, res
+        except Exception:  # noqa: BLE001  (the reference swallows restart failures)
+            pass
+    out = {"success": best is not None and best.success,
+           "log_marginal_likelihood": -best_nll if best else None,
+           "n_iterations": best.nit if best else 0}
+    if best is None:
+        return out, np.asarray(params0, float), noise0
+    return out, best.x[:-1].copy(), float(np.exp(best.x[-1]))

@@ -293,7 +293,55 @@ def f9():
     save("f9_uncertainty_prop.npz", **out)
 
 
+# ---------------------------------------------------------------- F10
+def f10():
+    """Reference ExactGP (SE-ARD, D = 11 3-DoF features) log marginal likelihood
+    at a grid of hyperparameter vectors (exact_gp.py:118-204 via the objective
+    of :375-386), one vector whose K needs the jitter ladder (duplicated rows,
+    noise 1e-14), and ExactGP.optimize_hyperparameters (:357-421, L-BFGS-B with
+    scipy's finite differences, 2 restarts under np.random.seed(5))."""
+    X, U, D = synthetic_training_data(120, seed=3)
+    Z = features.Simple3DoFFeatureExtractor().extract_batch(X, U)
+    y = D[:, 0].copy()
+    rs = np.random.RandomState(11)
+    p0 = np.concatenate([np.zeros(12), [np.log(1e-4)]])   # [log s2, log l (11), log noise]
+    grid = p0 + 0.4 * rs.normal(size=(15, 13))
+    grid = np.vstack([p0, grid])
+    lml = []
+    for p in grid:
+        gp = exact_gp.ExactGP(kernels.SquaredExponentialARD(11), noise_variance=np.exp(p[-1]))
+        gp.kernel.set_params(p[:-1])
+        gp.fit(Z, y)
+        lml.append(gp.log_marginal_likelihood)
+    # jitter ladder: duplicated rows make K singular, a negative "noise" of -2e-3
+    # makes K + s_n^2 I clearly indefinite; jitters 1e-6 .. 1e-3 still fail and
+    # 1e-2 succeeds with margins far above rounding (a robust 5-step case)
+    Zd = np.vstack([Z[:40], Z[:40]]); yd = np.concatenate([y[:40], y[:40] + 1e-3])
+    gpj = exact_gp.ExactGP(kernels.SquaredExponentialARD(11), noise_variance=-2e-3)
+    gpj.fit(Zd, yd)
+    gpo = exact_gp.ExactGP(kernels.SquaredExponentialARD(11), noise_variance=1e-4)
+    gpo.fit(Z, y)
+    lml_init = gpo.log_marginal_likelihood
+    np.random.seed(5)
+    res = gpo.optimize_hyperparameters(n_restarts=2)
+    # refinement from the optimum found: converges (success) in a few iterations
+    p_opt, n_opt = gpo.kernel.get_params(), gpo.noise_variance
+    gpr = exact_gp.ExactGP(kernels.SquaredExponentialARD(11), noise_variance=n_opt)
+    gpr.kernel.set_params(p_opt)
+    gpr.fit(Z, y)
+    np.random.seed(5)
+    rr = gpr.optimize_hyperparameters(n_restarts=1)
+    save("f10_hyperparameters.npz", Z=Z, y=y, grid=grid, lml=np.array(lml), Zd=Zd, yd=yd,
+         ref_start_params=p_opt, ref_start_noise=n_opt, ref_params=gpr.kernel.get_params(),
+         ref_noise=gpr.noise_variance, ref_lml=rr["log_marginal_likelihood"],
+         ref_nit=rr["n_iterations"], ref_success=rr["success"],
+         lml_jitter=gpj.log_marginal_likelihood, L_jitter_diag=np.diag(gpj._L),
+         lml_init=lml_init, opt_params=gpo.kernel.get_params(), opt_noise=gpo.noise_variance,
+         opt_lml=res["log_marginal_likelihood"], opt_nit=res["n_iterations"],
+         opt_success=res["success"])
+
+
 if __name__ == "__main__":
-    which = sys.argv[1:] or ["f1", "f2", "f3", "f4", "f5", "f6", "f7_f8", "f9"]
+    which = sys.argv[1:] or ["f1", "f2", "f3", "f4", "f5", "f6", "f7_f8", "f9", "f10"]
     for w in which:
         globals()[w]()

@@ -54,6 +54,39 @@ def test_blocked_trsm_paths(gpu_ctx, n, nrhs):
     np.testing.assert_allclose(L.potrs(gpu_ctx, Lr, B), np.linalg.solve(A, B), rtol=1e-9, atol=1e-11)
 
 
+@pytest.mark.parametrize("n,batch", [(100, 3), (128, 2), (129, 3), (256, 2), (300, 4), (1000, 3)])
+def test_potrf_batched_dev(gpu_ctx, n, batch):
+    """Batched device potrf (fused 128 x 128 diagonal factor + inverse, in-place
+    panel GEMM, lower SYRK) vs np.linalg.cholesky per matrix (exact_gp.py:164);
+    the strict upper triangle is left untouched; a matrix with a bad pivot
+    reports its 1-based column without disturbing the others."""
+    import torch
+    L = _lib()
+    rs = np.random.RandomState(7 * n + batch)
+    As = []
+    for b in range(batch):
+        G = rs.normal(size=(n, n))
+        As.append(G @ G.T / n + np.eye(n))
+    bad = min(n - 1, 130 if n > 130 else n // 2)
+    As[-1][bad, :] = 0.0; As[-1][:, bad] = 0.0; As[-1][bad, bad] = -1.0
+    A = torch.tensor(np.stack(As), dtype=torch.float64, device="cuda")
+    up = torch.triu(torch.ones(n, n, dtype=torch.bool, device="cuda"), 1)
+    up_before = A[:, up].clone()
+    info = torch.full((batch,), 7, dtype=torch.int32, device="cuda")
+    torch.cuda.synchronize()
+    rc = L._L.gpmpc_potrf_batched_dev(gpu_ctx.h, n, batch, A.data_ptr(), n, n * n, info.data_ptr())
+    L._chk(rc, "potrf_batched_dev")
+    gpu_ctx.sync()
+    inf = info.cpu().numpy()
+    assert list(inf[:-1]) == [0] * (batch - 1)
+    assert inf[-1] == bad + 1
+    Ah = A.cpu().numpy()
+    for b in range(batch - 1):
+        Lr = np.linalg.cholesky(As[b])
+        np.testing.assert_allclose(np.tril(Ah[b]), Lr, rtol=1e-10, atol=1e-12)
+    assert torch.equal(A[:-1, up], up_before[:-1])
+
+
 def test_potrf_reports_first_bad_pivot(gpu_ctx):
     L = _lib()
     A = np.eye(70); A[40, 40] = -1.0

@@ -190,3 +190,23 @@ def test_f9_linear_propagation_oracle():
     means, covs = uprop_oracle.propagate_linear(ToyRocket14(), gp, f9["x0"], f9["U"], None, 0.1)
     np.testing.assert_allclose(means, f9["linear_means"], rtol=1e-9, atol=1e-12)
     np.testing.assert_allclose(covs, f9["linear_covs"], rtol=1e-7, atol=1e-14)
+
+
+def test_oracle_lml_and_optimiser_vs_f10():
+    """SURVEY 8f-3 oracle pinned to F10: the LML objective at 16 parameter sets
+    (exact), the 5-step jitter case, and the optimiser's converged refinement
+    (exact_gp.py:357-421) from the reference optimum."""
+    from oracle import gp_oracle
+    f = golden("f10_hyperparameters.npz")
+    Z, y = f["Z"], f["y"]
+    lml = [gp_oracle.lml_at(Z, y, np.exp(p[0]), np.exp(p[1:-1]), np.exp(p[-1]))[0] for p in f["grid"]]
+    np.testing.assert_allclose(lml, f["lml"], rtol=1e-12)
+    lj, sj = gp_oracle.lml_at(f["Zd"], f["yd"], 1.0, np.ones(11), -2e-3)
+    assert sj == 5 and np.isclose(lj, float(f["lml_jitter"]), rtol=1e-12)
+    assert gp_oracle.lml_at(f["Zd"], f["yd"], 1.0, np.ones(11), -10.0) == (-np.inf, -1)
+    np.random.seed(5)
+    r, p, nz = gp_oracle.optimize_hyperparameters(Z, y, f["ref_start_params"],
+                                                  float(f["ref_start_noise"]), n_restarts=1)
+    assert r["success"] and bool(f["ref_success"])
+    assert abs(r["log_marginal_likelihood"] - float(f["ref_lml"])) < 1e-8 * abs(float(f["ref_lml"]))
+    assert np.max(np.abs(p - f["ref_params"])) < 1e-2
