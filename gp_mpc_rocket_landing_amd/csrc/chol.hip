@@ -114,6 +114,16 @@ __global__ __launch_bounds__(64) void k_potrf_diag(int n, int k0, double *A, int
 #define DB 128
 #define DP 130
 #define DIAG128_LDS (sizeof(double) * (DB * DP + NB + 2))
+// LDS-only ordering.  A release fence (and __syncthreads, which carries one)
+// waits for every outstanding global store (vmcnt(0)) -- here the L blocks
+// streamed out behind the factor -- which put ~1-2 us of store latency on the
+// serial chain at every sync.  The data exchanged between lanes and waves in
+// k_potrf_diag128 is LDS only, so LDS completion (lgkmcnt(0)) is enough; the
+// "memory" clobber keeps the compiler from moving accesses across.
+__device__ __forceinline__ void wave_lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
 __device__ __forceinline__ double rdlane(double v, int l) {
   return __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(v), l),
                           __builtin_amdgcn_readlane(__double2loint(v), l));
@@ -163,28 +173,62 @@ __global__ __launch_bounds__(256) void k_potrf_diag128(int n, int K0, double *A,
     }
   }
   if (tid == 0) sfail = 0;
-  __syncthreads();
+  lds_barrier();
   mark(0);
   for (int jb = 0; jb < DB / NB; ++jb) {
     const int c0 = jb * NB;
-    // ---- 1. diagonal 32 x 32 block (wave 0).  Row `lane` of the block lives in
-    // a[]; every cross-lane operand comes by v_readlane (a uniform SGPR pair), so
-    // the serial column chain has no LDS round trips.
+    // ---- 1. diagonal 32 x 32 block (wave 0).  Every wave instruction costs
+    // >= 4 cycles and this chain is serial, so the block is factored in 4-column
+    // steps: the 4 panel columns right-looking in lane registers (row = lane,
+    // readlane broadcasts of 3 + 2 + 1 entries), the rest of the block by one
+    // K = 4 MFMA per 16 x 16 tile.  Then T = L^-1 by 16 x 16 halves: T11 and T22
+    // at once (lanes 0-15 / 16-31, one column each, LDS-broadcast L rows) and
+    // T21 = -T22 (L21 T11) with two K = 16 MFMA products.
     if (wave == 0) {
-      double a[NB], ig = 1.0;
-#pragma unroll
-      for (int j = 0; j < NB; ++j) a[j] = (lane < NB && j <= lane) ? S[c0 + lane][c0 + j] : 0.0;
+      double *dinv = col;  // 1 / L_jj
       int fail = 0;
+      const bool lv = lane < NB;
 #pragma unroll
-      for (int j = 0; j < NB; ++j) {
-        const double piv = rdlane(a[j], j);
-        if (fail == 0 && !(piv > 0.0)) fail = j + 1;
-        if (fail) continue;  // (no break: keeps the loop fully unrolled, a[] in registers)
-        const double d = sqrt(piv), id = 1.0 / d;
-        if (lane == j) ig = id;
-        a[j] = (lane == j) ? d : a[j] * id;       // L[lane][j]
+      for (int j = 0; j < NB; j += 4) {
+        double p[4];
 #pragma unroll
-        for (int k = j + 1; k < NB; ++k) a[k] = fma(-a[j], rdlane(a[j], k), a[k]);
+        for (int q = 0; q < 4; ++q) p[q] = (lv && lane >= j) ? S[c0 + lane][c0 + j + q] : 0.0;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const double piv = rdlane(p[q], j + q);
+          if (fail == 0 && !(piv > 0.0)) fail = j + q + 1;
+          if (fail) continue;
+          const double d = sqrt(piv), id = 1.0 / d;
+          if (lane == j + q) dinv[j + q] = id;
+          p[q] = (lane < j + q) ? 0.0 : (lane == j + q ? d : p[q] * id);
+#pragma unroll
+          for (int q2 = q + 1; q2 < 4; ++q2) p[q2] = fma(-p[q], rdlane(p[q], j + q2), p[q2]);
+        }
+        if (fail) break;
+        if (lv && lane >= j) {
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+            if (lane >= j + q) {
+              S[c0 + lane][c0 + j + q] = p[q];
+              if (c0 + lane < pw) M[(int64_t)(c0 + lane) * lda + c0 + j + q] = p[q];
+            }
+        }
+        wave_lds_sync();
+        const int j4 = j + 4;
+        if (j4 < NB) {
+          // lower 16 x 16 tiles meeting rows/cols >= j4: (1,1) always, (1,0) and (0,0) while j4 < 16
+#pragma unroll
+          for (int t = 0; t < 3; ++t) {
+            const int rb = (t == 2) ? 0 : 16, cb = (t == 0) ? 16 : 0;
+            if (t > 0 && j4 >= 16) continue;
+            const double av = (rb + li >= j4) ? S[c0 + rb + li][c0 + j + lk] : 0.0;
+            const double bv = (cb + li >= j4) ? S[c0 + cb + li][c0 + j + lk] : 0.0;
+            const d4_t acc = mfma_f64(av, bv, d4_t{0.0, 0.0, 0.0, 0.0});
+#pragma unroll
+            for (int r = 0; r < 4; ++r) S[c0 + rb + mf_row(lane, r)][c0 + cb + li] -= acc[r];
+          }
+          wave_lds_sync();
+        }
       }
       if (fail) {
         if (lane == 0) {
@@ -192,34 +236,47 @@ __global__ __launch_bounds__(256) void k_potrf_diag128(int n, int K0, double *A,
           sfail = 1;
         }
       } else {
-        if (lane < NB && c0 + lane < pw) {
+        // T11 (lanes 0-15) and T22 (lanes 16-31): column c of the half in lane c
+        const int base = lane & 16, c = lane & 15;
+        double x[16];
 #pragma unroll
-          for (int j = 0; j < NB; ++j)
-            if (j <= lane) M[(int64_t)(c0 + lane) * lda + c0 + j] = a[j];
+        for (int r = 0; r < 16; ++r) {
+          double sum = (r == c) ? 1.0 : 0.0;
+#pragma unroll
+          for (int k = 0; k < r; ++k) sum = fma(-S[c0 + base + r][c0 + base + k], x[k], sum);
+          x[r] = (r >= c) ? sum * dinv[base + r] : 0.0;
         }
-        // T = L_jj^-1 row by row (row `lane` in t[]): forward substitution,
-        // row k final once scaled by 1/L_kk, then eliminated from the rows below
-        double t[NB];
+        wave_lds_sync();
+        if (lv) {
 #pragma unroll
-        for (int c = 0; c < NB; ++c) t[c] = (lane == c) ? 1.0 : 0.0;
-#pragma unroll
-        for (int k = 0; k < NB; ++k) {
-          if (lane == k) {
-#pragma unroll
-            for (int c = 0; c <= k; ++c) t[c] *= ig;
-          }
-          const double lrk = (lane > k) ? a[k] : 0.0;
-#pragma unroll
-          for (int c = 0; c <= k; ++c) t[c] = fma(-lrk, rdlane(t[c], k), t[c]);
+          for (int r = 0; r < 16; ++r)
+            if (r >= c) S[c0 + base + r][c0 + base + c] = x[r];
         }
-        if (lane < NB) {
+        wave_lds_sync();
+        // Y = L21 T11 -> upper-right 16 x 16 of the block (free space)
+        d4_t y = d4_t{0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-          for (int c = 0; c < NB; ++c)
-            if (c <= lane) S[c0 + lane][c0 + c] = t[c];
+        for (int kk = 0; kk < 16; kk += 4) {
+          const int m = kk + lk;
+          y = mfma_f64(S[c0 + 16 + li][c0 + m], (m >= li) ? S[c0 + m][c0 + li] : 0.0, y);
         }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) S[c0 + mf_row(lane, r)][c0 + 16 + li] = y[r];
+        wave_lds_sync();
+        // T21 = -T22 Y over L21
+        d4_t t21 = d4_t{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int kk = 0; kk < 16; kk += 4) {
+          const int m = kk + lk;
+          t21 = mfma_f64((m <= li) ? S[c0 + 16 + li][c0 + 16 + m] : 0.0, S[c0 + m][c0 + 16 + li],
+                         t21);
+        }
+        wave_lds_sync();
+#pragma unroll
+        for (int r = 0; r < 4; ++r) S[c0 + 16 + mf_row(lane, r)][c0 + li] = -t21[r];
       }
     }
-    __syncthreads();
+    lds_barrier();
     mark(1);
     if (sfail) return;
     const int R = DB - c0 - NB;  // rows below the diagonal block
@@ -243,7 +300,7 @@ __global__ __launch_bounds__(256) void k_potrf_diag128(int n, int K0, double *A,
           }
         }
       }
-      __syncthreads();
+      lds_barrier();
 #pragma unroll
       for (int q = 0; q < 3; ++q) {
         const int t = wave + 4 * q;
@@ -253,7 +310,7 @@ __global__ __launch_bounds__(256) void k_potrf_diag128(int n, int K0, double *A,
           for (int r = 0; r < 4; ++r) S[rb + mf_row(lane, r)][c0 + cb + li] = acc[q][r];
         }
       }
-      __syncthreads();
+      lds_barrier();
       mark(2);
     }
     // ---- 3. trailing lower update A[t][t] -= X X^T over 16 x 16 tiles (ti >= tj)
@@ -273,7 +330,7 @@ __global__ __launch_bounds__(256) void k_potrf_diag128(int n, int K0, double *A,
 #pragma unroll
         for (int r = 0; r < 4; ++r) S[rb + mf_row(lane, r)][cb + li] -= acc[r];
       }
-      __syncthreads();
+      lds_barrier();
       mark(3);
     }
   }
@@ -318,7 +375,7 @@ __global__ __launch_bounds__(256) void k_potrf_diag128(int n, int K0, double *A,
         for (int r = 0; r < 4; ++r) S[j * NB + cb + li][i * NB + rb + mf_row(lane, r)] = acc[q][r];
       }
     }
-    __syncthreads();
+    lds_barrier();
 #pragma unroll
     for (int q = 0; q < 3; ++q) {
       acc[q] = d4_t{0.0, 0.0, 0.0, 0.0};
@@ -334,7 +391,7 @@ __global__ __launch_bounds__(256) void k_potrf_diag128(int n, int K0, double *A,
         }
       }
     }
-    __syncthreads();
+    lds_barrier();
 #pragma unroll
     for (int q = 0; q < 3; ++q) {
       const int jt = wave + 4 * q;
@@ -344,7 +401,7 @@ __global__ __launch_bounds__(256) void k_potrf_diag128(int n, int K0, double *A,
         for (int r = 0; r < 4; ++r) S[j * NB + cb + li][i * NB + rb + mf_row(lane, r)] = -acc[q][r];
       }
     }
-    __syncthreads();
+    lds_barrier();
   }
   mark(5);
   double *Li = Linv + (int64_t)b * DB * DB;

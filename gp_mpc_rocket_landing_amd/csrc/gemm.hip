@@ -480,7 +480,11 @@ static hipError_t launch_gemm_impl(hipStream_t s, int epi, int M, int N, int K, 
                        alpha, (int)tg, tx, T, sA, sB, sC, total);
     return hipGetLastError();
   }
-  if (big_env && tri_ok && M >= 2 * BT && N >= 2 * BT && K >= 2 * BT) {
+  static const int kmin_env = [] {
+    const char *e = getenv("GPMPC_GEMM128_KMIN");
+    return e ? atoi(e) : 2 * BT;
+  }();
+  if (big_env && tri_ok && M >= 2 * BT && N >= 2 * BT && K >= kmin_env) {
     const int tx = (N + BT - 1) / BT, ty = (M + BT - 1) / BT;
     // split K when the tiles cannot give each CU ~4 workgroups to interleave (STORE
     // with beta = 1: partial products are added atomically); >= 512 of K per split
