@@ -170,14 +170,76 @@ def cholesky_bench(ctx, torch, n=1000, batch=64, reps=3):
         el = e0.elapsed_time(e1) * 1e-3
         fb = el if fb is None else min(fb, el)
     fitc_tf = m2 * (m2 + 1) * k2 / fb / 1e12
+    del A, base, G, As, Bm
+    # the same factorisation at the other batch sizes of SURVEY 8d (1, 64, 256, 1024)
+    by_batch = {}
+    for bb in (1, 256, 1024):
+        Gb = torch.randn(bb, n, n, dtype=torch.float64, device=dev, generator=g) / n ** 0.5
+        Bb = torch.baddbmm(torch.eye(n, dtype=torch.float64, device=dev).expand(bb, n, n), Gb,
+                           Gb.transpose(1, 2))
+        del Gb
+        Ab = Bb.clone()
+        ib = torch.zeros(bb, dtype=torch.int32, device=dev)
+        tb = None
+        for _ in range(reps):
+            Ab.copy_(Bb)
+            torch.cuda.synchronize()
+            e0 = torch.cuda.Event(enable_timing=True); e1 = torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            _lib._chk(_lib._L.gpmpc_potrf_batched_dev(ctx.h, n, bb, Ab.data_ptr(), n, n * n,
+                                                       ib.data_ptr()), "potrf_batched_dev")
+            e1.record(stream)
+            ctx.sync()
+            el = e0.elapsed_time(e1) * 1e-3
+            tb = el if tb is None else min(tb, el)
+        assert int(ib.abs().sum().item()) == 0
+        fb_ = bb * (n ** 3 / 3.0 + n ** 2 / 2.0 + n / 6.0) / tb / 1e12
+        by_batch[str(bb)] = {"ms": round(tb * 1e3, 3), "tflops": round(fb_, 3),
+                             "frac_fp64_peak": round(fb_ / FP64_PEAK_TFLOPS, 4)}
+        del Ab, Bb, ib
+    by_batch[str(batch)] = {"ms": round(t * 1e3, 3), "tflops": round(tf, 3),
+                            "frac_fp64_peak": round(tf / FP64_PEAK_TFLOPS, 4)}
     return dict(n=n, batch=batch, ms=round(t * 1e3, 3), tflops=round(tf, 3),
                 frac_fp64_peak=round(tf / FP64_PEAK_TFLOPS, 4),
+                by_batch=dict(sorted(by_batch.items(), key=lambda kv: int(kv[0]))),
                 syrk_potrf={"shapes": "trailing updates (n-t0) x 128, t0 = 128..896", "gflop": round(syrk_flops / 1e9, 2),
                             "ms": round(best * 1e3, 3), "tflops": round(syrk_tf, 3),
                             "frac_fp64_peak": round(syrk_tf / FP64_PEAK_TFLOPS, 4)},
                 syrk_fitc={"shape": "B = I + A A^T, A 2000 x 4000 (config 5 FITC)",
                            "gflop": round(m2 * (m2 + 1) * k2 / 1e9, 2), "ms": round(fb * 1e3, 3),
                            "tflops": round(fitc_tf, 3), "frac_fp64_peak": round(fitc_tf / FP64_PEAK_TFLOPS, 4)})
+
+
+def lml_bench(ctx, n=1000, sets=14, reps=3, cpu=True):
+    """one finite-difference gradient of ExactGP.optimize_hyperparameters
+    (exact_gp.py:357-421) for the default 3-DoF GP -- the LML at 14 parameter sets
+    (13 SE-ARD parameters + the base point), n = 1000 training points -- as one
+    gpmpc_gp_lml_batched call (host-boundary time), next to the numpy restatement
+    (the reference's per-set ExactGP.fit, one host core)."""
+    from gp_mpc_rocket_landing_amd import _lib
+    from gp_mpc_rocket_landing_amd.data import synthetic_training_data
+    from oracle import gp_oracle
+    X, U, D = synthetic_training_data(n, seed=0)
+    Z = gp_oracle.features_3dof(X, U)
+    rs = np.random.RandomState(2)
+    P = np.concatenate([np.zeros(12), [np.log(1e-4)]]) + 0.2 * rs.normal(size=(sets, 13))
+    ts = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        lml, _ = _lib.gp_lml_batched(ctx, _lib.SE_ARD, Z, D[:, 1], np.exp(P[:, 1:-1]),
+                                     np.exp(P[:, 0]), np.exp(P[:, -1]))
+        ts.append(time.perf_counter() - t0)
+    out = {"workload": f"LML at {sets} SE-ARD parameter sets, n = {n} (one FD gradient)",
+           "ms": round(min(ts) * 1e3, 3), "gradients_per_s": round(1.0 / min(ts), 2)}
+    if cpu:
+        from threadpoolctl import threadpool_limits
+        with threadpool_limits(1):
+            t0 = time.perf_counter()
+            ref = [gp_oracle.lml_at(Z, D[:, 1], np.exp(p[0]), np.exp(p[1:-1]), np.exp(p[-1]))[0] for p in P]
+            tc = time.perf_counter() - t0
+        out["cpu_ms_1core"] = round(tc * 1e3, 2)
+        out["max_rel_diff_vs_cpu"] = float(np.max(np.abs(lml - ref) / np.abs(ref)))
+    return out
 
 
 def structured_fitc_bench(ctx, reps=2):
@@ -360,6 +422,7 @@ def main():
             try:
                 out["cholesky"] = cholesky_bench(ctx, torch)
                 out["structured_fitc"] = structured_fitc_bench(ctx)
+                out["lml_batched"] = lml_bench(ctx, cpu=not args.no_cpu)
             except Exception as e:  # noqa: BLE001
                 out["cholesky"] = {"error": str(e)[:200]}
         if not args.no_cpu:
