@@ -95,6 +95,7 @@ _sig("gpmpc_gp_predict", _c, _vp, _vp, _dp, _c, _dp, _dp)
 _sig("gpmpc_gp_predict_cov", _c, _vp, _vp, _dp, _c, _dp, _dp)
 _sig("gpmpc_gp_get_state", _c, _vp, _vp, _dp, _dp)
 _sig("gpmpc_gp_destroy", _c, _vp)
+_sig("gpmpc_gp_append", _c, _vp, _vp, _dp, _c, _dp, _dp, _dp, _dp)
 _sig("gpmpc_gp_lml_batched", _c, _vp, _c, _dp, _c, _c, _dp, _c, _dp, _dp, _dp, _dp, _ip)
 _sig("gpmpc_fitc_fit", _c, _vp, _dp, _c, _dp, _c, _c, _dp, _c, _dp, ctypes.c_double,
      ctypes.c_double, ctypes.c_double, ctypes.POINTER(_vp), _dp, _dp, _dp, _dp)
@@ -122,7 +123,7 @@ EXPORTED = ["gpmpc_abi_version", "gpmpc_last_error", "gpmpc_ctx_create", "gpmpc_
             "gpmpc_ctx_sync", "gpmpc_ctx_stream", "gpmpc_gram", "gpmpc_potrf",
             "gpmpc_potrf_batched_dev", "gpmpc_trsm_lower", "gpmpc_potrs", "gpmpc_gp_fit_exact",
             "gpmpc_gp_predict", "gpmpc_gp_predict_cov", "gpmpc_gp_get_state", "gpmpc_gp_destroy",
-            "gpmpc_gp_lml_batched",
+            "gpmpc_gp_lml_batched", "gpmpc_gp_append",
             "gpmpc_fitc_fit", "gpmpc_fitc_predict", "gpmpc_fitc_destroy",
             "gpmpc_qp_default_settings", "gpmpc_qp_solve_batched", "gpmpc_fleet_default_config",
             "gpmpc_fleet_create", "gpmpc_fleet_reset", "gpmpc_fleet_step", "gpmpc_fleet_read",
@@ -285,6 +286,24 @@ class ExactGPHandle:
         _chk(rc, "gp_fit_exact")
         self.h = h
         self.jitter_steps = int(js[0])
+
+    def append(self, Xnew, Yall):
+        """Grow the GP by the rows Xnew (k x d) in O(n^2 k) (gpmpc_gp_append);
+        Yall = the targets of all n + k rows.  False (handle unchanged) when the
+        caller must refit instead (jitter-fitted GP / indefinite Schur complement)."""
+        Xnew = f64(np.atleast_2d(Xnew)); k = Xnew.shape[0]
+        Yall = f64(Yall)
+        if Yall.ndim == 1:
+            Yall = Yall[:, None]
+        assert Xnew.shape[1] == self.d and Yall.shape == (self.n + k, self.n_out)
+        ym = np.empty(self.n_out); ys = np.empty(self.n_out); lml = np.empty(self.n_out)
+        rc = _L.gpmpc_gp_append(self.ctx.h, self.h, _d(Xnew), k, _d(Yall), _d(ym), _d(ys), _d(lml))
+        if rc == ERR_NOT_PD:
+            return False
+        _chk(rc, "gp_append")
+        self.n += k
+        self.y_mean, self.y_std, self.lml = ym, ys, lml
+        return True
 
     def predict(self, Xq):
         Xq = f64(np.atleast_2d(Xq)); p = Xq.shape[0]

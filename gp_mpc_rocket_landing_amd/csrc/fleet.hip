@@ -33,6 +33,7 @@ struct gpmpc_fleet {
   gpmpc_gp *gp = nullptr;
   gpmpc_fleet_config cfg{};
   int B = 0, N = 0, n = 0, m = 0;
+  int gp_n = 0;  // training rows of the GP when the GP scratch was sized
   QPPatternHost pat;
   DevBuf x, Xw, Uw, ysc, rho, rec, xt;      // landing state
   DevBuf Q, Qn, Ks, part, meanT, mean, var;  // GP scratch
@@ -644,6 +645,7 @@ extern "C" int gpmpc_fleet_create(gpmpc_ctx *ctx, gpmpc_gp *gp, const gpmpc_flee
   GPMPC_HIP(hipSetDevice(ctx->device));
   auto *f = new gpmpc_fleet();
   f->ctx = ctx; f->gp = gp; f->cfg = *cfg; f->B = batch; f->N = N; f->n = n; f->m = m;
+  f->gp_n = g.n;
   std::vector<int> rp, ci;
   mpc_pattern(N, rp, ci);
   if (f->pat.build(n, m, rp.data(), ci.data(), ctx->stream) || !f->pat.fits()) {
@@ -784,6 +786,11 @@ static FleetArgs fleet_args(gpmpc_fleet *f) {
 
 extern "C" int gpmpc_fleet_step_phases(gpmpc_fleet *f, int phase_mask) {
   GPMPC_CHECK_ARG(f);
+  if (gp_view(f->gp).n != f->gp_n) {  // gpmpc_gp_append grew the GP under the fleet
+    gpmpc_set_error("fleet: the GP has %d training rows, the fleet was built for %d; recreate it",
+                    gp_view(f->gp).n, f->gp_n);
+    return -2;
+  }
   GPMPC_HIP(hipSetDevice(f->ctx->device));
   if ((phase_mask & 13) && f->cfg.use_gp) GPMPC_HIP(fleet_gp_posterior(f, phase_mask));
   if (phase_mask & 2) {

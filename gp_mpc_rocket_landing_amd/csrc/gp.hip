@@ -30,6 +30,7 @@ struct gpmpc_gp {
   GpCore core;
   DevBuf L;  // n x n lower Cholesky factor
   double noise = 1e-4;
+  int jitter_steps = 0;
 };
 
 struct gpmpc_fitc {
@@ -284,6 +285,7 @@ extern "C" int gpmpc_gp_fit_exact(gpmpc_ctx *ctx, int kind, const double *X, int
     ++steps;
   }
   if (jitter_steps) *jitter_steps = steps;
+  gp->jitter_steps = steps;
   // normalised targets, alpha = L^-T L^-1 y for all outputs (exact_gp.py:141-150, 179)
   DevBuf dYraw, dY, dyn, dlml;
   if (dYraw.alloc(sizeof(double) * n * n_out) || dY.alloc(sizeof(double) * n * n_out) ||
@@ -751,5 +753,131 @@ extern "C" int gpmpc_gp_lml_batched(gpmpc_ctx *ctx, int kind, const double *X, i
   GPMPC_HIP(hipStreamSynchronize(s));
   for (int b = 0; b < B; ++b)
     if (jitter_steps[b] < 0) lml[b] = -INFINITY;
+  return 0;
+}
+
+// ---------------------------------------------------------------------------
+// incremental exact GP -- append k training rows to a fitted GP in
+// O(n^2 k) instead of the O(n^3) refit on the concatenated data
+// (SparseGP.update semantics, sparse_gp.py:328-353; the online refit cadence of
+// online_update.py:361-408).  With K = [[K11, K12], [K21, K22]]:
+//   B^T = K21 W^T              (W = L11^-1, the stored inverse)
+//   S   = K22 + noise I - B^T B,  Ls = chol(S)
+//   L   = [[L11, 0], [B^T, Ls]],  W = [[W, 0], [-Ls^-1 B^T W, Ls^-1]]
+// then the targets of all n + k rows are renormalised (exact_gp.py:141-150) and
+// alpha = W^T W y, lml as in the fit.  The refit's plain Cholesky of K succeeds
+// exactly when L11's did and S is positive definite; a GP fitted with jitter, or
+// an indefinite S, returns GPMPC_ERR_NOT_PD with the handle unchanged, and the
+// caller refits (the refit reruns the jitter ladder on the whole matrix).
+extern "C" int gpmpc_gp_append(gpmpc_ctx *ctx, gpmpc_gp *gp, const double *Xnew, int k,
+                               const double *Yall, double *y_mean, double *y_std, double *lml) {
+  GPMPC_CHECK_ARG(ctx && gp && Xnew && Yall && k >= 1);
+  GPMPC_HIP(hipSetDevice(ctx->device));
+  hipStream_t s = ctx->stream;
+  GpCore &g = gp->core;
+  if (gp->jitter_steps != 0) {
+    gpmpc_set_error("gp_append: the GP was fitted with jitter; refit the concatenated data");
+    return GPMPC_ERR_NOT_PD;
+  }
+  const int n = g.n, m = n + k, d = g.d, no = g.n_out;
+  DevBuf xr, xs, xn, Kt, Bt, Sm, dinfo, Li, C;
+  GPMPC_HIP(xr.alloc(sizeof(double) * k * d));
+  GPMPC_HIP(xs.alloc(sizeof(double) * k * d));
+  GPMPC_HIP(xn.alloc(sizeof(double) * k));
+  GPMPC_HIP(Kt.alloc(sizeof(double) * (size_t)k * n));
+  GPMPC_HIP(Bt.alloc(sizeof(double) * (size_t)k * n));
+  GPMPC_HIP(Sm.alloc(sizeof(double) * (size_t)k * k));
+  GPMPC_HIP(Li.alloc(sizeof(double) * (size_t)k * k));
+  GPMPC_HIP(C.alloc(sizeof(double) * (size_t)k * n));
+  GPMPC_HIP(dinfo.alloc(sizeof(int)));
+  GPMPC_HIP(hipMemcpyAsync(xr.p, Xnew, sizeof(double) * k * d, hipMemcpyHostToDevice, s));
+  GPMPC_HIP(launch_scale_rows(s, xr.as<double>(), k, d, g.ls.as<double>(), g.kind == GPMPC_SE_ISO,
+                              xs.as<double>(), xn.as<double>()));
+  // K21 (k x n), B^T = K21 W^T, S = K22 + noise I - B^T B
+  GPMPC_HIP(launch_gram(s, g.kind, xs.as<double>(), xn.as<double>(), k, g.Xs.as<double>(),
+                        g.Xn.as<double>(), n, d, g.sigma2, g.iso_scale, Kt.as<double>(), n, 0));
+  GPMPC_HIP(launch_gemm_nt(s, EPI_STORE, k, n, n, Kt.as<double>(), n, g.W.as<double>(), n,
+                           Bt.as<double>(), n, 1.0, 0.0, 0, 0, 1, 0, 0, 0));
+  GPMPC_HIP(launch_gram(s, g.kind, xs.as<double>(), xn.as<double>(), k, xs.as<double>(),
+                        xn.as<double>(), k, d, g.sigma2, g.iso_scale, Sm.as<double>(), k, 0));
+  GPMPC_HIP(launch_add_diag(s, k, Sm.as<double>(), k, gp->noise, 1, 0));
+  GPMPC_HIP(launch_gemm_nt(s, EPI_STORE, k, k, n, Bt.as<double>(), n, Bt.as<double>(), n,
+                           Sm.as<double>(), k, -1.0, 1.0, 0, 0, 1, 0, 0, 0));
+  GPMPC_HIP(launch_potrf_batched(s, k, 1, Sm.as<double>(), k, 0, dinfo.as<int>()));
+  int info = 0;
+  GPMPC_HIP(hipMemcpyAsync(&info, dinfo.p, sizeof(int), hipMemcpyDeviceToHost, s));
+  GPMPC_HIP(hipStreamSynchronize(s));
+  if (info) {
+    gpmpc_set_error("gp_append: Schur complement not positive definite (pivot %d); refit", info);
+    return GPMPC_ERR_NOT_PD;
+  }
+  // Ls^-1 (lower) and the new rows of W: [-(Ls^-1 (B^T W)) | Ls^-1]
+  hipLaunchKernelGGL(k_eye, dim3((k + 255) / 256, k), dim3(256), 0, s, k, Li.as<double>());
+  GPMPC_HIP(launch_trsm_lower_ex(s, k, k, Sm.as<double>(), k, Li.as<double>(), k, 0, 1, nullptr));
+  GPMPC_HIP(launch_gemm_nn(s, k, n, n, Bt.as<double>(), n, g.W.as<double>(), n, C.as<double>(), n,
+                           1.0, 0.0));
+  DevBuf L2, W2, Xs2, Xn2, yraw, yn, t, alpha, alphaT, dlml;
+  GPMPC_HIP(L2.alloc(sizeof(double) * (size_t)m * m));
+  GPMPC_HIP(W2.alloc(sizeof(double) * (size_t)(m + no) * m));
+  GPMPC_HIP(Xs2.alloc(sizeof(double) * (size_t)m * d));
+  GPMPC_HIP(Xn2.alloc(sizeof(double) * m));
+  GPMPC_HIP(yraw.alloc(sizeof(double) * (size_t)m * no));
+  GPMPC_HIP(yn.alloc(sizeof(double) * (size_t)m * no));
+  GPMPC_HIP(t.alloc(sizeof(double) * (size_t)m * no));
+  GPMPC_HIP(alpha.alloc(sizeof(double) * (size_t)m * no));
+  GPMPC_HIP(alphaT.alloc(sizeof(double) * (size_t)no * m));
+  GPMPC_HIP(dlml.alloc(sizeof(double) * no));
+  GPMPC_HIP(hipMemsetAsync(L2.p, 0, sizeof(double) * (size_t)m * m, s));
+  GPMPC_HIP(hipMemsetAsync(W2.p, 0, sizeof(double) * (size_t)(m + no) * m, s));
+  const size_t rowb = sizeof(double) * n;
+  GPMPC_HIP(hipMemcpy2DAsync(L2.p, sizeof(double) * m, gp->L.p, rowb, rowb, n,
+                             hipMemcpyDeviceToDevice, s));
+  GPMPC_HIP(hipMemcpy2DAsync(L2.as<double>() + (size_t)n * m, sizeof(double) * m, Bt.p, rowb, rowb,
+                             k, hipMemcpyDeviceToDevice, s));
+  GPMPC_HIP(hipMemcpy2DAsync(L2.as<double>() + (size_t)n * m + n, sizeof(double) * m, Sm.p,
+                             sizeof(double) * k, sizeof(double) * k, k, hipMemcpyDeviceToDevice, s));
+  GPMPC_HIP(hipMemcpy2DAsync(W2.p, sizeof(double) * m, g.W.p, rowb, rowb, n,
+                             hipMemcpyDeviceToDevice, s));
+  GPMPC_HIP(launch_gemm_nn(s, k, n, k, Li.as<double>(), k, C.as<double>(), n,
+                           W2.as<double>() + (size_t)n * m, m, -1.0, 0.0));
+  GPMPC_HIP(hipMemcpy2DAsync(W2.as<double>() + (size_t)n * m + n, sizeof(double) * m, Li.p,
+                             sizeof(double) * k, sizeof(double) * k, k, hipMemcpyDeviceToDevice, s));
+  // training rows
+  GPMPC_HIP(hipMemcpyAsync(Xs2.p, g.Xs.p, sizeof(double) * (size_t)n * d, hipMemcpyDeviceToDevice, s));
+  GPMPC_HIP(hipMemcpyAsync(Xs2.as<double>() + (size_t)n * d, xs.p, sizeof(double) * (size_t)k * d,
+                           hipMemcpyDeviceToDevice, s));
+  GPMPC_HIP(hipMemcpyAsync(Xn2.p, g.Xn.p, sizeof(double) * n, hipMemcpyDeviceToDevice, s));
+  GPMPC_HIP(hipMemcpyAsync(Xn2.as<double>() + n, xn.p, sizeof(double) * k, hipMemcpyDeviceToDevice, s));
+  // all targets renormalised; alpha = W^T (W y); lml
+  GPMPC_HIP(hipMemcpyAsync(yraw.p, Yall, sizeof(double) * (size_t)m * no, hipMemcpyHostToDevice, s));
+  hipLaunchKernelGGL(k_normalise, dim3(no), dim3(256), 0, s, m, no, yraw.as<double>(),
+                     yn.as<double>(), g.ymean.as<double>(), g.ystd.as<double>());
+  GPMPC_HIP(launch_gemm_nn(s, m, no, m, W2.as<double>(), m, yn.as<double>(), no, t.as<double>(), no,
+                           1.0, 0.0));
+  GPMPC_HIP(launch_gemm_tn(s, m, no, m, W2.as<double>(), m, t.as<double>(), no, alpha.as<double>(),
+                           no, 1.0, 0.0));
+  hipLaunchKernelGGL(k_lml_exact, dim3(no), dim3(256), 0, s, m, no, L2.as<double>(), yn.as<double>(),
+                     alpha.as<double>(), alphaT.as<double>(), dlml.as<double>());
+  GPMPC_HIP(hipMemcpyAsync(W2.as<double>() + (size_t)m * m, alphaT.p, sizeof(double) * (size_t)no * m,
+                           hipMemcpyDeviceToDevice, s));
+  std::vector<double> hl(no);
+  g.h_ymean.resize(no);
+  g.h_ystd.resize(no);
+  GPMPC_HIP(hipMemcpyAsync(g.h_ymean.data(), g.ymean.p, sizeof(double) * no, hipMemcpyDeviceToHost, s));
+  GPMPC_HIP(hipMemcpyAsync(g.h_ystd.data(), g.ystd.p, sizeof(double) * no, hipMemcpyDeviceToHost, s));
+  GPMPC_HIP(hipMemcpyAsync(hl.data(), dlml.p, sizeof(double) * no, hipMemcpyDeviceToHost, s));
+  GPMPC_HIP(hipStreamSynchronize(s));
+  // commit: swap the grown buffers into the handle
+  std::swap(gp->L.p, L2.p); std::swap(gp->L.bytes, L2.bytes);
+  std::swap(g.W.p, W2.p); std::swap(g.W.bytes, W2.bytes);
+  std::swap(g.alphaT.p, alphaT.p); std::swap(g.alphaT.bytes, alphaT.bytes);
+  std::swap(g.Xs.p, Xs2.p); std::swap(g.Xs.bytes, Xs2.bytes);
+  std::swap(g.Xn.p, Xn2.p); std::swap(g.Xn.bytes, Xn2.bytes);
+  g.n = m;
+  for (int c = 0; c < no; ++c) {
+    if (lml) lml[c] = hl[c];
+    if (y_mean) y_mean[c] = g.h_ymean[c];
+    if (y_std) y_std[c] = g.h_ystd[c];
+  }
   return 0;
 }

@@ -187,6 +187,24 @@ class ExactGP:
             raise np.linalg.LinAlgError("Matrix is not positive definite")
         return (mean[:, None] + L @ np.random.randn(np.atleast_2d(X).shape[0], n_samples)).T
 
+    def update(self, X_new, y_new) -> "ExactGP":
+        """Refit on the concatenated data (the SparseGP.update semantics,
+        sparse_gp.py:328-353), done incrementally on the device when possible
+        (gpmpc_gp_append, SURVEY 8f-4: O(n^2 k) instead of O(n^3)); a GP fitted
+        with jitter or an indefinite Schur complement falls back to the refit."""
+        if self._dev is None:
+            return self.fit(X_new, y_new)
+        X_new = np.atleast_2d(X_new)
+        y_new = np.atleast_1d(y_new).flatten()
+        X = np.vstack([self.X_train, X_new])
+        y = np.concatenate([self.y_train * self._y_std + self._y_mean, y_new])
+        h = self._dev.h
+        if h.n_out == 1 and h.append(X_new, y[:, None]):
+            self._dev._cache_key = None
+            self._attach(X, y, self._dev, 0)
+            return self
+        return self.fit(X, y)
+
     def _lml_batch(self, P, X, y):
         """Log marginal likelihoods at the rows of P = [kernel params (log
         space, kernels.py:320-371 order), log noise] -- the objective of
@@ -315,6 +333,29 @@ class MultiOutputExactGP:
             for i, g in enumerate(self.gps):
                 g.fit(X, Y[:, i])
         return self
+
+    def update(self, X_new, Y_new) -> "MultiOutputExactGP":
+        """Refit on the concatenated data (MultiOutputSparseGP.update semantics,
+        sparse_gp.py:486-504), incrementally on the device (gpmpc_gp_append)
+        when every output shares the factor; otherwise a full refit."""
+        h = self.device_handle
+        g0 = self.gps[0]
+        if h is None or g0.X_train is None:
+            return self.fit(X_new, Y_new)
+        X_new = np.atleast_2d(X_new)
+        Y_new = np.atleast_2d(Y_new)
+        if Y_new.shape[1] != self.output_dim and Y_new.shape[0] == self.output_dim:
+            Y_new = Y_new.T
+        X = np.vstack([g0.X_train, X_new])
+        Y_old = np.stack([g.y_train * g._y_std + g._y_mean for g in self.gps], axis=1)
+        Y = np.vstack([Y_old, Y_new])
+        if h.append(X_new, Y):
+            shared = self.gps[0]._dev
+            shared._cache_key = None
+            for i, g in enumerate(self.gps):
+                g._attach(X, Y[:, i], shared, i)
+            return self
+        return self.fit(X, Y)
 
     def predict(self, X) -> Tuple[np.ndarray, np.ndarray]:
         X = np.atleast_2d(X)

@@ -204,11 +204,22 @@ class Simple3DoFGP:
         self._is_fitted = False
 
     def fit(self) -> None:
+        """structured_gp.py:470-481.  With the exact GP, a refit after add_data
+        only appended rows grows the device factor in O(n^2 k) (gpmpc_gp_append,
+        SURVEY 8f-4) -- the same GP as the full refit, which remains the
+        fallback (first fit, jitter, indefinite Schur complement)."""
         if self.n_data == 0:
             raise RuntimeError("No data")
         X = np.array(self.X_data); U = np.array(self.U_data); D = np.array(self.D_data)
-        Z = self.feature_extractor.extract_batch(X, U)
-        self.gp.fit(Z, D)
+        n_old = getattr(self, "_n_fitted", 0)
+        if (not self.use_sparse and 0 < n_old < self.n_data
+                and self.gp.device_handle is not None and self.gp.device_handle.n == n_old):
+            Znew = self.feature_extractor.extract_batch(X[n_old:], U[n_old:])
+            self.gp.update(Znew, D[n_old:])
+        else:
+            Z = self.feature_extractor.extract_batch(X, U)
+            self.gp.fit(Z, D)
+        self._n_fitted = self.n_data
         self._is_fitted = True
 
     def predict(self, x, u) -> Tuple[np.ndarray, np.ndarray]:

@@ -100,6 +100,18 @@ int gpmpc_gp_predict(gpmpc_ctx *ctx, gpmpc_gp *gp, const double *Xq, int p, doub
  * latent posterior in normalised units (caller multiplies by y_std^2). */
 int gpmpc_gp_predict_cov(gpmpc_ctx *ctx, gpmpc_gp *gp, const double *Xq, int p, double *mean,
                          double *cov);
+/* append k training rows Xnew (k x d) to a fitted GP in O(n^2 k)
+ * -- the result of gpmpc_gp_fit_exact on the concatenated data without the
+ * O(n^3) refit (SparseGP.update's refit-with-concatenation semantics,
+ * sparse_gp.py:328-353; online_update.py:361-408).  Yall holds the targets of
+ * all n + k rows ((n + k) x n_out, old rows first): normalisation, alpha and
+ * lml are recomputed over all of them.  Returns GPMPC_ERR_NOT_PD, with the
+ * handle unchanged, when the GP was fitted with jitter or the new rows' Schur
+ * complement is not positive definite: the caller refits the whole set (which
+ * reruns the exact_gp.py:163-175 ladder).  A fleet built on the GP must be
+ * recreated after an append (its scratch is sized for the old row count). */
+int gpmpc_gp_append(gpmpc_ctx *ctx, gpmpc_gp *gp, const double *Xnew, int k, const double *Yall,
+                    double *y_mean, double *y_std, double *lml);
 /* Copies of the device state (L lower, n x n; alpha n x n_out). Either may be NULL. */
 int gpmpc_gp_get_state(gpmpc_ctx *ctx, gpmpc_gp *gp, double *L, double *alpha);
 int gpmpc_gp_destroy(gpmpc_gp *gp);
