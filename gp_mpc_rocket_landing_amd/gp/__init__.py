@@ -5,6 +5,8 @@ from .features import (AtmosphereModel, CombinedFeatureExtractor, RocketFeatureE
                        TranslationalFeatureExtractor)
 from .kernels import (RBF, SE_ARD, Matern32, Matern52, ProductKernel, SquaredExponential,
                       SquaredExponentialARD, SumKernel, WhiteNoise, create_matern_kernel)
+from .online_update import (DataBuffer, DataPoint, OnlineGPUpdater, OnlineStructuredGPUpdater,
+                            OnlineUpdateConfig, ResidualCollector)
 from .sparse_gp import MultiOutputSparseGP, SparseGP
 from .structured_gp import Simple3DoFGP, StructuredGPConfig, StructuredRocketGP
 
@@ -13,4 +15,5 @@ __all__ = ["ExactGP", "GPPrediction", "MultiOutputExactGP", "AtmosphereModel", "
            "TranslationalFeatureExtractor", "RBF", "SE_ARD", "Matern32", "Matern52", "ProductKernel",
            "SquaredExponential", "SquaredExponentialARD", "SumKernel", "WhiteNoise", "create_matern_kernel",
            "MultiOutputSparseGP", "SparseGP", "Simple3DoFGP", "StructuredGPConfig",
-           "StructuredRocketGP"]
+           "StructuredRocketGP", "DataBuffer", "DataPoint", "OnlineGPUpdater",
+           "OnlineStructuredGPUpdater", "OnlineUpdateConfig", "ResidualCollector"]

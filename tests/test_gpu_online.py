@@ -118,3 +118,38 @@ def test_fleet_refuses_grown_gp(gpu_ctx):
     with pytest.raises(_lib.HIPError):
         fl.step(1)
     fl.close()
+
+
+@pytest.mark.parametrize("buffer_size", [1000, 100])
+def test_online_updater_exact_gp(gpu_ctx, buffer_size):
+    """OnlineGPUpdater (online_update.py:232-425) on the device ExactGP: 150
+    streamed observations, an update every 10; with room in the buffer every
+    update after the first is an O(n^2 k) append, after evictions (buffer 100)
+    a refit; either way the GP equals the oracle's fit on the buffer."""
+    from gp_mpc_rocket_landing_amd.data import synthetic_training_data
+    from gp_mpc_rocket_landing_amd.gp.exact_gp import ExactGP
+    from gp_mpc_rocket_landing_amd.gp.features import Simple3DoFFeatureExtractor
+    from gp_mpc_rocket_landing_amd.gp.kernels import SquaredExponentialARD
+    from gp_mpc_rocket_landing_amd.gp.online_update import OnlineGPUpdater, OnlineUpdateConfig
+    from oracle import gp_oracle
+    X, U, D = synthetic_training_data(150, seed=6)
+    fe = Simple3DoFFeatureExtractor()
+    gp = ExactGP(SquaredExponentialARD(11), noise_variance=1e-4)
+    up = OnlineGPUpdater(gp, OnlineUpdateConfig(buffer_size=buffer_size, use_novelty_filter=False,
+                                                update_interval=10), feature_extractor=fe.extract)
+    for i in range(150):
+        up.add_observation(X[i], U[i], D[i])
+        if up.should_update():
+            assert up.update()["status"] == "success"
+    Z, T = up._buffer.get_data()
+    assert Z.shape[0] == min(150, buffer_size) and gp.n_train == Z.shape[0]
+    if buffer_size == 1000:
+        assert up.incremental_updates == 13   # fits at 20, then appends at 30 .. 150
+    else:
+        assert up.incremental_updates == 8    # appends 30 .. 100, refits once the ring evicts
+    st = gp_oracle.exact_fit(Z, T.mean(axis=1))
+    Zq = Z[::7] + 0.01
+    mo, vo = gp_oracle.exact_predict(st, Zq)
+    p = gp.predict(Zq)
+    assert close(p.mean, mo[:, 0], st["y_std"][0])[0]
+    assert close(p.variance, vo[:, 0], st["y_std"][0] ** 2)[0]

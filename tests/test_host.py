@@ -165,3 +165,68 @@ def test_cost_weights_and_simple_predictor_host():
     assert X.shape == (5, 7) and Dm.shape == (4, 7)
     np.testing.assert_allclose(X[1], [0.5, 0.5, 0.5, 0.5, 1.0, 1.5, 2.0])
     np.testing.assert_allclose(Dv[0, 4:7], [0.1, 0.2, 0.3])
+
+
+# ---------------------------------------------------------------- online updates (8f-4)
+class _FakeGP:
+    """Stands in for a device GP on the CPU: records fit / update calls."""
+
+    class _K:
+        signal_variance = 1.0
+
+    def __init__(self):
+        self.kernel = self._K()
+        self._dev = None
+        self.calls = []
+
+    def fit(self, Z, y):
+        self.calls.append(("fit", len(Z)))
+        self._dev = object()
+        return self
+
+    def predict(self, Z):
+        from types import SimpleNamespace
+        return SimpleNamespace(variance=np.full(len(Z), 0.5))
+
+
+def test_data_buffer_novelty_and_eviction():
+    from gp_mpc_rocket_landing_amd.gp.online_update import DataBuffer
+    b = DataBuffer(max_size=3, feature_dim=2, target_dim=1)
+    assert not b.add_if_novel(np.zeros(2), np.ones(1), novelty=0.1, threshold=0.3)
+    assert b.add_if_novel(np.zeros(2), np.ones(1), novelty=0.5, threshold=0.3, min_distance=0.1)
+    assert not b.add_if_novel(np.full(2, 0.01), np.ones(1), novelty=0.5, min_distance=0.1)
+    for i in range(3):
+        b.add(np.full(2, i + 1.0), np.ones(1))
+    st = b.get_statistics()
+    assert b.size == 3 and b.total_added == 4 and st["total_rejected"] == 2
+    assert np.array_equal(b.get_features()[:, 0], [1.0, 2.0, 3.0])   # oldest evicted
+    Zr, _ = b.get_recent(2)
+    assert np.array_equal(Zr[:, 0], [2.0, 3.0])
+
+
+def test_online_updater_cadence_and_novelty():
+    """online_update.py:293-408: the first fit needs min_data_for_fit points and
+    update_interval new ones; novelty = predicted variance / signal variance."""
+    from gp_mpc_rocket_landing_amd.gp.online_update import OnlineGPUpdater, OnlineUpdateConfig
+    gp = _FakeGP()
+    up = OnlineGPUpdater(gp, OnlineUpdateConfig(min_data_for_fit=5, update_interval=5,
+                                                novelty_threshold=0.3, min_distance=None))
+    for i in range(4):
+        assert up.add_observation(np.array([float(i)]), np.array([0.0]), np.array([1.0]))
+    assert not up.should_update() and up.update()["status"] == "skipped"
+    up.add_observation(np.array([4.0]), np.array([0.0]), np.array([1.0]))
+    assert up.update()["status"] == "success" and gp.calls == [("fit", 5)]
+    up.config.novelty_threshold = 0.6   # fitted now: novelty 0.5 -> rejected
+    assert not up.add_observation(np.array([9.0]), np.array([0.0]), np.array([1.0]))
+    assert up.get_statistics()["total_updates"] == 1
+
+
+def test_residual_collector():
+    from gp_mpc_rocket_landing_amd.gp.online_update import ResidualCollector
+    rc = ResidualCollector(lambda x, u, dt: x.copy(), max_samples=2)
+    for i in range(3):
+        x = np.zeros(14); xn = np.zeros(14); xn[4:7] = 0.1 * (i + 1); xn[11:14] = 0.2
+        rc.record(x, np.zeros(3), xn, 0.1)
+    X, U, Dv, Dw = rc.get_training_data()
+    assert rc.n_samples == 2 and np.allclose(Dv[:, 0], [2.0, 3.0]) and np.allclose(Dw, 2.0)
+    assert rc.get_statistics()["n_samples"] == 2
