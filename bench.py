@@ -242,6 +242,31 @@ def lml_bench(ctx, n=1000, sets=14, reps=3, cpu=True):
     return out
 
 
+def append_bench(ctx, n=1000, k=10, reps=3):
+    """k new residual observations into the n = 1000 exact GP of
+    the control loop -- the O(n^2 k) device append (gpmpc_gp_append) vs the full
+    device refit of the n + k rows it is equivalent to (host-boundary times)."""
+    from gp_mpc_rocket_landing_amd import _lib
+    from gp_mpc_rocket_landing_amd.data import synthetic_training_data
+    from oracle import gp_oracle
+    X, U, D = synthetic_training_data(n + k, seed=0)
+    Z = gp_oracle.features_3dof(X, U)
+    ta, tf = [], []
+    for _ in range(reps):
+        h = _lib.ExactGPHandle(ctx, _lib.SE_ARD, Z[:n], D[:n], np.ones(11), 1.0, 1e-4)
+        t0 = time.perf_counter()
+        ok = h.append(Z[n:], D)
+        ta.append(time.perf_counter() - t0)
+        assert ok
+        t0 = time.perf_counter()
+        h2 = _lib.ExactGPHandle(ctx, _lib.SE_ARD, Z, D, np.ones(11), 1.0, 1e-4)
+        tf.append(time.perf_counter() - t0)
+        del h, h2
+    return {"workload": f"append {k} rows to the n = {n} exact GP (3 outputs)",
+            "append_ms": round(min(ta) * 1e3, 3), "refit_ms": round(min(tf) * 1e3, 3),
+            "speedup": round(min(tf) / min(ta), 2)}
+
+
 def structured_fitc_bench(ctx, reps=2):
     """BASELINE config 5 GP: StructuredRocketGP with FITC M = 2000, N_train = 4000
     (two 3-output GPs, D = 13 translational / 12 rotational features), and one
@@ -423,6 +448,7 @@ def main():
                 out["cholesky"] = cholesky_bench(ctx, torch)
                 out["structured_fitc"] = structured_fitc_bench(ctx)
                 out["lml_batched"] = lml_bench(ctx, cpu=not args.no_cpu)
+                out["gp_append"] = append_bench(ctx)
             except Exception as e:  # noqa: BLE001
                 out["cholesky"] = {"error": str(e)[:200]}
         if not args.no_cpu:

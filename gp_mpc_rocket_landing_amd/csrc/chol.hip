@@ -175,7 +175,10 @@ __global__ __launch_bounds__(256) void k_potrf_diag128(int n, int K0, double *A,
   if (tid == 0) sfail = 0;
   lds_barrier();
   mark(0);
-  for (int jb = 0; jb < DB / NB; ++jb) {
+  // 32-column blocks holding real rows; the identity padding beyond pw is its
+  // own factor and inverse, so a short last panel (or a small matrix) skips it
+  const int nblk = (pw + NB - 1) / NB;
+  for (int jb = 0; jb < nblk; ++jb) {
     const int c0 = jb * NB;
     // ---- 1. diagonal 32 x 32 block (wave 0).  Every wave instruction costs
     // >= 4 cycles and this chain is serial, so the block is factored in 4-column
@@ -279,7 +282,7 @@ __global__ __launch_bounds__(256) void k_potrf_diag128(int n, int K0, double *A,
     lds_barrier();
     mark(1);
     if (sfail) return;
-    const int R = DB - c0 - NB;  // rows below the diagonal block
+    const int R = nblk * NB - c0 - NB;  // rows below the diagonal block (real blocks only)
     if (R == 0) break;
     // ---- 2. panel X = A T^T: (R/16) x 2 tiles of 16 x 16, K = 32
     {
