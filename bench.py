@@ -64,11 +64,11 @@ def pmc_traffic(kernel):
     return None, None
 
 
-def cpu_baseline(seconds, n_train=1000, horizon=20):
-    """The reference CPU path restated (oracle): numpy/scipy GP posterior at the N
-    horizon points (same LAPACK calls as exact_gp.py), numpy QP assembly
-    (osqp_rti.py semantics) and the C restatement of the OSQP ADMM, one landing
-    closed loop, BLAS limited to one thread."""
+def _cpu_landing_loop(seconds, n_train=1000, horizon=20, seed=42):
+    """One landing closed loop of the reference CPU path restated (oracle):
+    numpy/scipy GP posterior at the N horizon points (same LAPACK calls as
+    exact_gp.py), numpy QP assembly (osqp_rti.py semantics) and the C
+    restatement of the OSQP ADMM, BLAS on one thread.  Returns (steps, seconds)."""
     from threadpoolctl import threadpool_limits
     from oracle import admm_ref, gp_oracle, mc_oracle, qp_oracle
     from gp_mpc_rocket_landing_amd.data import synthetic_training_data
@@ -76,7 +76,7 @@ def cpu_baseline(seconds, n_train=1000, horizon=20):
     X, U, D = synthetic_training_data(n_train, seed=0)
     with threadpool_limits(1):
         st = gp_oracle.exact_fit(gp_oracle.features_3dof(X, U), D)
-        x = mc_oracle.sample_initial_condition(42)
+        x = mc_oracle.sample_initial_condition(seed)
         tgt = mc_oracle.incremental_target(x)
         Xw, Uw = qp_oracle.initial_guess(x, tgt, horizon)
         P0, _ = qp_oracle.cost(horizon, np.tile(tgt, (horizon + 1, 1)))
@@ -86,7 +86,7 @@ def cpu_baseline(seconds, n_train=1000, horizon=20):
         deadline = t0 + seconds
         while time.perf_counter() < deadline:
             if mc_oracle.pre_step_outcome(x, 2.0):
-                x = mc_oracle.sample_initial_condition(43 + steps)
+                x = mc_oracle.sample_initial_condition(seed + 1 + steps)
                 qp = admm_ref.RefQP(qp.y.size)
             tgt = mc_oracle.incremental_target(x)
             mean, var = gp_oracle.exact_predict(st, gp_oracle.features_3dof(Xw[:-1], Uw))
@@ -101,10 +101,41 @@ def cpu_baseline(seconds, n_train=1000, horizon=20):
             Xw = np.vstack([Xo[1:], Xo[-1:]]); Uw = np.vstack([Uo[1:], Uo[-1:]])
             steps += 1
         el = time.perf_counter() - t0
-    return dict(value=steps / el, unit="control steps/s", cores=1, kind="port",
-                sample=f"1 landing closed loop, {steps} control steps in {el:.1f} s "
-                       f"(numpy/scipy GP N={n_train}, P={horizon}; numpy QP assembly; "
-                       f"C OSQP-0.6 ADMM restatement; OPENBLAS 1 thread)")
+    return steps, el
+
+
+def cpu_baseline(seconds, n_train=1000, horizon=20, workers=None):
+    """SURVEY 8d CPU baseline, throughput mode: one process per host core (at
+    most the box's 16-core share), one landing each, BLAS on one thread, for
+    ``seconds``; value = all processes' control steps / the longest elapsed.
+    Runs before the GPU is initialised (spawned workers, fresh interpreters)."""
+    import concurrent.futures as cf
+    import multiprocessing as mp
+    import platform
+    aff = len(os.sched_getaffinity(0))
+    workers = workers or max(1, min(16, aff))
+    with cf.ProcessPoolExecutor(workers, mp_context=mp.get_context("spawn")) as ex:
+        res = list(ex.map(_cpu_landing_loop, [seconds] * workers, [n_train] * workers,
+                          [horizon] * workers, [42 + 1000 * i for i in range(workers)]))
+    steps = sum(r[0] for r in res)
+    el = max(r[1] for r in res)
+    per_core = float(np.mean([r[0] / r[1] for r in res]))
+    cpu = platform.processor() or platform.machine()
+    try:
+        with open("/proc/cpuinfo") as f:
+            cpu = next(ln.split(":", 1)[1].strip() for ln in f if ln.startswith("model name"))
+    except Exception:  # noqa: BLE001
+        pass
+    try:
+        blas = np.__config__.CONFIG["Build Dependencies"]["blas"]["name"]
+    except Exception:  # noqa: BLE001
+        blas = "unknown"
+    return dict(value=steps / el, unit="control steps/s", cores=workers, kind="port",
+                per_core=round(per_core, 3),
+                sample=f"{workers} processes x 1 landing closed loop, {steps} control steps in "
+                       f"{el:.1f} s (numpy/scipy GP N={n_train}, P={horizon}; numpy QP assembly; "
+                       f"C OSQP-0.6 ADMM restatement; {blas} on 1 thread per process; "
+                       f"{aff} CPUs in affinity; {cpu})")
 
 
 def cholesky_bench(ctx, torch, n=1000, batch=64, reps=3):
@@ -305,12 +336,18 @@ def main():
     ap.add_argument("--landings", type=int, default=1024, help="landings per GPU")
     ap.add_argument("--horizon", type=int, default=20)
     ap.add_argument("--train", type=int, default=1000)
-    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-chol", action="store_true")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
+    world0 = int(os.environ.get("WORLD_SIZE", "1"))
+    # the CPU baseline first: its worker processes start before this process
+    # touches the GPU
+    cb = None
+    if rank == 0 and world0 == 1 and not args.no_cpu:
+        cb = cpu_baseline(args.cpu_seconds, n_train=args.train, horizon=args.horizon)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     import torch
@@ -451,8 +488,7 @@ def main():
                 out["gp_append"] = append_bench(ctx)
             except Exception as e:  # noqa: BLE001
                 out["cholesky"] = {"error": str(e)[:200]}
-        if not args.no_cpu:
-            cb = cpu_baseline(args.cpu_seconds, n_train=n, horizon=args.horizon)
+        if cb is not None:
             cb["value"] = round(cb["value"], 3)
             out["cpu_baseline"] = cb
         print(json.dumps(out), flush=True)
