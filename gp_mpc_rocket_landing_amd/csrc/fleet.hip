@@ -34,6 +34,11 @@ struct gpmpc_fleet {
   gpmpc_fleet_config cfg{};
   int B = 0, N = 0, n = 0, m = 0;
   int gp_n = 0;  // training rows of the GP when the GP scratch was sized
+  // upper bound on the running landings, refreshed whenever the host reads the
+  // records (landings only terminate between resets): with the dispatch order
+  // putting running landings first, the GP posterior and the control launch
+  // cover only the first n_active slots
+  int n_active = 0;
   QPPatternHost pat;
   DevBuf x, Xw, Uw, ysc, rho, rec, xt;      // landing state
   DevBuf Q, Qn, Ks, part, meanT, mean, var;  // GP scratch
@@ -107,10 +112,12 @@ __device__ __forceinline__ void features3(const double *x, const double *u, doub
 
 __global__ void k_fleet_queries(int B, int N, const double *__restrict__ Xw,
                                 const double *__restrict__ Uw, const double *__restrict__ ls,
-                                int iso, double *__restrict__ Q, double *__restrict__ Qn) {
-  const int g = blockIdx.x * blockDim.x + threadIdx.x;  // = b*N + k
+                                int iso, const int *__restrict__ order, double *__restrict__ Q,
+                                double *__restrict__ Qn) {
+  const int g = blockIdx.x * blockDim.x + threadIdx.x;  // = slot*N + k
   if (g >= B * N) return;
-  const int b = g / N, k = g - b * N;
+  const int sl = g / N, k = g - sl * N;
+  const int b = order ? order[sl] : sl;
   double z[NFEAT];
   features3(Xw + ((int64_t)b * (N + 1) + k) * NX, Uw + ((int64_t)b * N + k) * NU, z);
   double s = 0.0;
@@ -165,7 +172,8 @@ struct FleetArgs {
   int N, target_mode, use_gp, residual_model, max_steps;
   double dt;
   double *x, *Xw, *Uw, *ysc, *rho, *rec, *xt;
-  const double *gmean;  // (B*N) x 3
+  const double *gmean;  // (B*N) x 3, row (slot or landing)*N + k
+  int gp_by_slot;       // gmean rows follow the dispatch slot (order[]) instead of the landing
   const int *order;     // workgroup -> landing (longest predicted first), or null
   int alt_wave;         // fleet solver: odd workgroups run the KKT chain on wave 1
   int *lastit;          // ADMM iterations of each landing's last solve
@@ -308,7 +316,7 @@ __global__ __launch_bounds__(256) void k_fleet_control(FleetArgs a) {
     bu[0] = b00 * tx + b01 * ty + b02 * tz;
     bu[1] = bu[2] = bu[3] = 0.0;
     bu[4] = bv * tx; bu[5] = bv * ty; bu[6] = bv * tz;
-    const double *gm = a.gmean + ((int64_t)b * N + k) * 3;
+    const double *gm = a.gmean + ((int64_t)(a.gp_by_slot ? (int)blockIdx.x : b) * N + k) * 3;
     for (int i = 0; i < NX; ++i) {
       double c = (f[i] - ax[i]) - bu[i];
       if (a.use_gp && i >= 4) c += gm[i - 4] * dt;
@@ -513,7 +521,7 @@ __global__ __launch_bounds__(FQ_T) __attribute__((amdgpu_waves_per_eu(2, 2))) vo
     bu[0] = b00 * tx + b01 * ty + b02 * tz;
     bu[1] = bu[2] = bu[3] = 0.0;
     bu[4] = bv * tx; bu[5] = bv * ty; bu[6] = bv * tz;
-    const double *gm = a.gmean + ((int64_t)b * N + k) * 3;
+    const double *gm = a.gmean + ((int64_t)(a.gp_by_slot ? (int)blockIdx.x : b) * N + k) * 3;
     for (int i = 0; i < NX; ++i) {
       double c = (f[i] - ax[i]) - bu[i];
       if (a.use_gp && i >= 4) c += gm[i - 4] * dt;
@@ -646,6 +654,7 @@ extern "C" int gpmpc_fleet_create(gpmpc_ctx *ctx, gpmpc_gp *gp, const gpmpc_flee
   auto *f = new gpmpc_fleet();
   f->ctx = ctx; f->gp = gp; f->cfg = *cfg; f->B = batch; f->N = N; f->n = n; f->m = m;
   f->gp_n = g.n;
+  f->n_active = batch;
   std::vector<int> rp, ci;
   mpc_pattern(N, rp, ci);
   if (f->pat.build(n, m, rp.data(), ci.data(), ctx->stream) || !f->pat.fits()) {
@@ -672,6 +681,12 @@ extern "C" int gpmpc_fleet_create(gpmpc_ctx *ctx, gpmpc_gp *gp, const gpmpc_flee
   for (size_t b = 0; b < B; ++b) r[b * GPMPC_REC_LEN] = -1.0;
   hipMemcpyAsync(f->rec.p, r.data(), sizeof(double) * r.size(), hipMemcpyHostToDevice, ctx->stream);
   hipMemsetAsync(f->lastit.p, 0, sizeof(int) * B, ctx->stream);
+  {  // identity dispatch order until the first order kernel (every slot maps in range)
+    std::vector<int> id(B);
+    for (size_t b = 0; b < B; ++b) id[b] = (int)b;
+    hipMemcpyAsync(f->order.p, id.data(), sizeof(int) * B, hipMemcpyHostToDevice, ctx->stream);
+    GPMPC_HIP(hipStreamSynchronize(ctx->stream));
+  }
   const char *oe = getenv("GPMPC_FLEET_ORDER");
   f->use_order = !oe || atoi(oe) != 0;
   const char *aw = getenv("GPMPC_FLEET_ALTWAVE");
@@ -698,6 +713,7 @@ extern "C" int gpmpc_fleet_reset(gpmpc_fleet *f, int first, int count, const dou
                      f->cfg.qp.rho, f->rec.as<double>(), f->xt.as<double>());
   GPMPC_HIP(hipGetLastError());
   GPMPC_HIP(hipStreamSynchronize(s));
+  f->n_active = f->B;  // conservative until the host reads the records
   return 0;
 }
 
@@ -707,13 +723,16 @@ extern "C" int gpmpc_fleet_reset(gpmpc_fleet *f, int first, int count, const dou
 static hipError_t fleet_gp_posterior(gpmpc_fleet *f, int mask) {
   hipStream_t s = f->ctx->stream;
   const GpView g = gp_view(f->gp);
-  const int P = f->B * f->N;
+  const int nb = f->use_order ? f->n_active : f->B;  // slots 0 .. nb-1 (running first)
+  const int P = nb * f->N;
+  if (P == 0) return hipSuccess;
   const int nrt = gemm_row_tiles(g.n + 3, (int)P, g.n);  // W rows + the 3 alpha^T rows
   hipError_t e = hipSuccess;
   if (mask & 1) {
-    hipLaunchKernelGGL(k_fleet_queries, dim3((P + 255) / 256), dim3(256), 0, s, f->B, f->N,
+    hipLaunchKernelGGL(k_fleet_queries, dim3((P + 255) / 256), dim3(256), 0, s, nb, f->N,
                        f->Xw.as<double>(), f->Uw.as<double>(), g.ls, g.kind == GPMPC_SE_ISO,
-                       f->Q.as<double>(), f->Qn.as<double>());
+                       f->use_order ? f->order.as<int>() : nullptr, f->Q.as<double>(),
+                       f->Qn.as<double>());
     e = launch_gram(s, g.kind, f->Q.as<double>(), f->Qn.as<double>(), P, g.Xs, g.Xn, g.n, g.d,
                     g.sigma2, g.iso_scale, f->Ks.as<double>(), g.n, 0);
     if (e != hipSuccess) return e;
@@ -776,6 +795,7 @@ static FleetArgs fleet_args(gpmpc_fleet *f) {
   a.ysc = f->ysc.as<double>(); a.rho = f->rho.as<double>(); a.rec = f->rec.as<double>();
   a.xt = f->xt.as<double>();
   a.gmean = f->mean.as<double>();
+  a.gp_by_slot = f->use_order && f->cfg.use_gp;
   a.order = f->use_order ? f->order.as<int>() : nullptr;
   a.alt_wave = f->alt_wave;
   a.lastit = f->lastit.as<int>();
@@ -792,22 +812,28 @@ extern "C" int gpmpc_fleet_step_phases(gpmpc_fleet *f, int phase_mask) {
     return -2;
   }
   GPMPC_HIP(hipSetDevice(f->ctx->device));
+  // the dispatch order of this step, before the GP phase when there is one:
+  // the posterior rows then follow the same slots as the control workgroups
+  const bool order_now = f->use_order && ((f->cfg.use_gp && (phase_mask & 1)) ||
+                                          (!f->cfg.use_gp && (phase_mask & 2)));
+  if (order_now)
+    hipLaunchKernelGGL(k_fleet_order, dim3(1), dim3(1024), 0, f->ctx->stream, f->B,
+                       f->rec.as<double>(), f->lastit.as<int>(), f->order.as<int>());
   if ((phase_mask & 13) && f->cfg.use_gp) GPMPC_HIP(fleet_gp_posterior(f, phase_mask));
   if (phase_mask & 2) {
-    if (f->use_order)
-      hipLaunchKernelGGL(k_fleet_order, dim3(1), dim3(1024), 0, f->ctx->stream, f->B,
-                         f->rec.as<double>(), f->lastit.as<int>(), f->order.as<int>());
-    if (f->use_fq)
-    {
-      if (f->stamps)
-        hipLaunchKernelGGL(k_fleet_control2<true>, dim3(f->B), dim3(FQ_T), 0, f->ctx->stream,
-                           fleet_args(f));
-      else
-        hipLaunchKernelGGL(k_fleet_control2<false>, dim3(f->B), dim3(FQ_T), 0, f->ctx->stream,
-                           fleet_args(f));
+    const int nb = f->use_order ? f->n_active : f->B;
+    if (nb > 0) {
+      if (f->use_fq) {
+        if (f->stamps)
+          hipLaunchKernelGGL(k_fleet_control2<true>, dim3(nb), dim3(FQ_T), 0, f->ctx->stream,
+                             fleet_args(f));
+        else
+          hipLaunchKernelGGL(k_fleet_control2<false>, dim3(nb), dim3(FQ_T), 0, f->ctx->stream,
+                             fleet_args(f));
+      } else {
+        hipLaunchKernelGGL(k_fleet_control, dim3(nb), dim3(256), 0, f->ctx->stream, fleet_args(f));
+      }
     }
-    else
-      hipLaunchKernelGGL(k_fleet_control, dim3(f->B), dim3(256), 0, f->ctx->stream, fleet_args(f));
     GPMPC_HIP(hipGetLastError());
   }
   return 0;
@@ -830,6 +856,11 @@ extern "C" int gpmpc_fleet_read(gpmpc_fleet *f, double *records, double *x) {
                              hipMemcpyDeviceToHost, s));
   if (x) GPMPC_HIP(hipMemcpyAsync(x, f->x.p, sizeof(double) * f->B * NX, hipMemcpyDeviceToHost, s));
   GPMPC_HIP(hipStreamSynchronize(s));
+  if (records) {
+    int run = 0;
+    for (int b = 0; b < f->B; ++b) run += records[(size_t)b * GPMPC_REC_LEN] == 0.0;
+    f->n_active = run;
+  }
   return 0;
 }
 
