@@ -159,15 +159,15 @@ __global__ __launch_bounds__(256) void k_potrf_diag128(int n, int K0, double *A,
   // in flight per lane before the LDS stores (a load-store loop waits out the
   // HBM latency once per element)
 #pragma unroll 1
-  for (int q0 = 0; q0 < DB * DB / 256; q0 += 16) {
-    double v[16];
+  for (int q0 = 0; q0 < DB * DB / 256; q0 += 32) {
+    double v[32];
 #pragma unroll
-    for (int q = 0; q < 16; ++q) {
+    for (int q = 0; q < 32; ++q) {
       const int e = tid + 256 * (q0 + q), i = e >> 7, j = e & 127;
       v[q] = (j <= i && i < pw) ? M[(int64_t)i * lda + j] : (i == j ? 1.0 : 0.0);
     }
 #pragma unroll
-    for (int q = 0; q < 16; ++q) {
+    for (int q = 0; q < 32; ++q) {
       const int e = tid + 256 * (q0 + q);
       S[e >> 7][e & 127] = v[q];
     }
@@ -178,8 +178,37 @@ __global__ __launch_bounds__(256) void k_potrf_diag128(int n, int K0, double *A,
   // 32-column blocks holding real rows; the identity padding beyond pw is its
   // own factor and inverse, so a short last panel (or a small matrix) skips it
   const int nblk = (pw + NB - 1) / NB;
+  // trailing lower update A -= X X^T of panel pc's 32 columns over the 16 x 16
+  // tiles of the region [org, nblk*32)^2, tile t in row-major lower order
+  // (t = 0, 1, 2 are the region's first 32 x 32 diagonal block)
+  auto trail_tile = [&](int t, int org, int pc) {
+    int ti = 0;
+    while ((ti + 1) * (ti + 2) / 2 <= t) ++ti;
+    const int tj = t - ti * (ti + 1) / 2;
+    const int rb = org + ti * 16, cb = org + tj * 16;
+    d4_t acc = d4_t{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int kk = 0; kk < NB; kk += 4) {
+      const int k = pc + kk + lk;
+      acc = mfma_f64(S[rb + li][k], S[cb + li][k], acc);
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) S[rb + mf_row(lane, r)][cb + li] -= acc[r];
+  };
   for (int jb = 0; jb < nblk; ++jb) {
     const int c0 = jb * NB;
+    // ---- 3 (of the previous block, deferred): wave 0 updates only this block's
+    // diagonal 32 x 32 and goes on to factor it; waves 1-3 update the rest of
+    // the trailing region meanwhile (the panel step below waits for them)
+    if (jb > 0) {
+      const int nr = (nblk * NB - c0) >> 4, ntile = nr * (nr + 1) / 2;
+      if (wave == 0) {
+        for (int t = 0; t < 3; ++t) trail_tile(t, c0, c0 - NB);
+        wave_lds_sync();
+      } else {
+        for (int t = 3 + wave - 1; t < ntile; t += 3) trail_tile(t, c0, c0 - NB);
+      }
+    }
     // ---- 1. diagonal 32 x 32 block (wave 0).  Every wave instruction costs
     // >= 4 cycles and this chain is serial, so the block is factored in 4-column
     // steps: the 4 panel columns right-looking in lane registers (row = lane,
@@ -201,7 +230,13 @@ __global__ __launch_bounds__(256) void k_potrf_diag128(int n, int K0, double *A,
           const double piv = rdlane(p[q], j + q);
           if (fail == 0 && !(piv > 0.0)) fail = j + q + 1;
           if (fail) continue;
-          const double d = sqrt(piv), id = 1.0 / d;
+            // 1/sqrt by v_rsq_f64 + two Newton steps, sqrt = piv * rsq: ~8
+          // dependent instructions on the serial chain instead of ~27 for the
+          // correctly rounded sqrt and division (L agrees to a few ulp)
+          double id = __builtin_amdgcn_rsq(piv);
+          id = id * fma(-0.5 * piv * id, id, 1.5);
+          id = id * fma(-0.5 * piv * id, id, 1.5);
+          const double d = piv * id;
           if (lane == j + q) dinv[j + q] = id;
           p[q] = (lane < j + q) ? 0.0 : (lane == j + q ? d : p[q] * id);
 #pragma unroll
@@ -315,26 +350,6 @@ __global__ __launch_bounds__(256) void k_potrf_diag128(int n, int K0, double *A,
       }
       lds_barrier();
       mark(2);
-    }
-    // ---- 3. trailing lower update A[t][t] -= X X^T over 16 x 16 tiles (ti >= tj)
-    {
-      const int t0 = c0 + NB, nr = R >> 4, ntile = nr * (nr + 1) / 2;
-      for (int t = wave; t < ntile; t += 4) {
-        int ti = 0;
-        while ((ti + 1) * (ti + 2) / 2 <= t) ++ti;
-        const int tj = t - ti * (ti + 1) / 2;
-        const int rb = t0 + ti * 16, cb = t0 + tj * 16;
-        d4_t acc = d4_t{0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-        for (int kk = 0; kk < NB; kk += 4) {
-          const int k = c0 + kk + lk;
-          acc = mfma_f64(S[rb + li][k], S[cb + li][k], acc);
-        }
-#pragma unroll
-        for (int r = 0; r < 4; ++r) S[rb + mf_row(lane, r)][cb + li] -= acc[r];
-      }
-      lds_barrier();
-      mark(3);
     }
   }
   // off-diagonal blocks of L to global memory (diagonal blocks went out in step 1)

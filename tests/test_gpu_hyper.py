@@ -87,7 +87,10 @@ def test_lml_batched_config2_size(gpu_ctx):
 
 def test_optimize_hyperparameters_converged_refinement(gpu_ctx):
     """From the reference optimum: L-BFGS-B converges in a few iterations to the
-    reference's result (exact_gp.py:357-421), LML within 1e-8 relative."""
+    reference's result (exact_gp.py:357-421).  LML within 1e-6 relative (SURVEY
+    8c's GP tolerance): the stopping point moves with ulp-level LML differences
+    through the finite-difference gradient -- numpy's own restatement lands
+    3e-11 away, a device factor differing by a few ulp ~5e-8 away."""
     from gp_mpc_rocket_landing_amd.gp.exact_gp import ExactGP
     from gp_mpc_rocket_landing_amd.gp.kernels import SquaredExponentialARD
     f = golden("f10_hyperparameters.npz")
@@ -97,8 +100,8 @@ def test_optimize_hyperparameters_converged_refinement(gpu_ctx):
     np.random.seed(5)
     r = gp.optimize_hyperparameters(n_restarts=1)
     assert r["success"] and bool(f["ref_success"])
-    assert _rel(r["log_marginal_likelihood"], f["ref_lml"]) < 1e-8
-    assert _rel(gp.log_marginal_likelihood, f["ref_lml"]) < 1e-8
+    assert _rel(r["log_marginal_likelihood"], f["ref_lml"]) < 1e-6
+    assert _rel(gp.log_marginal_likelihood, f["ref_lml"]) < 1e-6
     assert np.max(np.abs(gp.kernel.get_params() - f["ref_params"])) < 1e-2
     assert abs(np.log(gp.noise_variance) - np.log(float(f["ref_noise"]))) < 1e-2
 
