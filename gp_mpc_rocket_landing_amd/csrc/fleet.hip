@@ -726,20 +726,37 @@ static hipError_t fleet_gp_posterior(gpmpc_fleet *f, int mask) {
   const int nb = f->use_order ? f->n_active : f->B;  // slots 0 .. nb-1 (running first)
   const int P = nb * f->N;
   if (P == 0) return hipSuccess;
-  const int nrt = gemm_row_tiles(g.n + 3, (int)P, g.n);  // W rows + the 3 alpha^T rows
+  // GPMPC_POST_FUSED=1: K* formed inside the posterior GEMM (no K* in HBM).
+  // Measured slower (0.60 ms vs 0.062 ms gram + 0.415 ms GEMM at 1024 x 20):
+  // each of the 8 row tiles regenerates its K* columns (4.6x the exps of the
+  // gram kernel) and the exp/scalar-load stream does not hide under the FP64
+  // MFMAs at 2 waves per SIMD.  Off by default.
+  static const int fused_env = [] {
+    const char *v = getenv("GPMPC_POST_FUSED");
+    return v ? atoi(v) : 0;
+  }();
+  const bool fused = fused_env && g.d >= 11 && g.d <= 13;
+  const int nrt = fused ? (g.n + 3 + 127) / 128 : gemm_row_tiles(g.n + 3, (int)P, g.n);
   hipError_t e = hipSuccess;
   if (mask & 1) {
     hipLaunchKernelGGL(k_fleet_queries, dim3((P + 255) / 256), dim3(256), 0, s, nb, f->N,
                        f->Xw.as<double>(), f->Uw.as<double>(), g.ls, g.kind == GPMPC_SE_ISO,
                        f->use_order ? f->order.as<int>() : nullptr, f->Q.as<double>(),
                        f->Qn.as<double>());
-    e = launch_gram(s, g.kind, f->Q.as<double>(), f->Qn.as<double>(), P, g.Xs, g.Xn, g.n, g.d,
-                    g.sigma2, g.iso_scale, f->Ks.as<double>(), g.n, 0);
-    if (e != hipSuccess) return e;
+    if (!fused) {
+      e = launch_gram(s, g.kind, f->Q.as<double>(), f->Qn.as<double>(), P, g.Xs, g.Xn, g.n, g.d,
+                      g.sigma2, g.iso_scale, f->Ks.as<double>(), g.n, 0);
+      if (e != hipSuccess) return e;
+    }
   }
   if (mask & 4) {
-    e = launch_gemm_sumsq_mean(s, g.n, 3, P, g.W, f->Ks.as<double>(), f->part.as<double>(), P,
-                               f->meanT.as<double>(), P);
+    if (fused)
+      e = launch_gemm_post_fused(s, g.n, 3, P, g.W, f->Q.as<double>(), f->Qn.as<double>(), g.Xs,
+                                 g.Xn, g.d, g.kind, g.sigma2, g.iso_scale, f->part.as<double>(), P,
+                                 f->meanT.as<double>(), P);
+    else
+      e = launch_gemm_sumsq_mean(s, g.n, 3, P, g.W, f->Ks.as<double>(), f->part.as<double>(), P,
+                                 f->meanT.as<double>(), P);
     if (e != hipSuccess) return e;
   }
   if (mask & 8) {

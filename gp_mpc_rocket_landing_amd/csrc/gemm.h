@@ -41,6 +41,16 @@ hipError_t launch_gemm_sumsq_mean(hipStream_t s, int n, int n_out, int P, const 
                                   const double *Ks, double *part, int64_t ldp, double *meanT,
                                   int64_t ldm);
 
+// the same pass with K* formed in the operand load from the scaled query rows
+// Qs (P x d) / norms Qn and training rows Xs (n x d) / norms Xn (d = 11..13;
+// hipErrorInvalidValue otherwise): no K* buffer.  128-row tiles: part has
+// ceil((n + n_out) / 128) rows.
+hipError_t launch_gemm_post_fused(hipStream_t s, int n, int n_out, int P, const double *Wext,
+                                  const double *Qs, const double *Qn, const double *Xs,
+                                  const double *Xn, int d, int kind, double sigma2,
+                                  double iso_scale, double *part, int64_t ldp, double *meanT,
+                                  int64_t ldm);
+
 // rows of the SUMSQ partial buffer for an M x N x K product (tile height of
 // the kernel launch_gemm_* picks: 128 when M, N and K >= 256, else 64)
 inline int gemm_row_tiles(int M, int N = 0, int K = 0) {

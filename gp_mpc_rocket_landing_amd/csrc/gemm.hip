@@ -393,6 +393,171 @@ __global__ __launch_bounds__(256, 2) void k_gemm128(int M, int N, int K, const d
 }
 
 
+// Posterior pass with K* generated in the operand load (no K* in HBM):
+//   part[t][j] = sum over the W rows of row tile t of ((W K*^T)_ij)^2,
+//   meanT = alpha^T K*^T   (rows msum.. of A = [W; alpha^T])
+// where K*[j][k] = k(q_j, x_k) is formed while the tile is staged, from the
+// length-scaled query rows Qs (N x D) and training rows Xs (K x D) with the
+// k_gram arithmetic (same fma order, same kernel_epilogue: the same bits).
+// B-tile thread map: query row lr = tid & 127 (its D features in registers),
+// k offset lk = 0 / 8 per wave pair, so each wave's training rows are uniform
+// (scalar loads).  A (W) loads, LDS tiles, MFMA loop and epilogue as k_gemm128.
+template <int D>
+__global__ __launch_bounds__(256, 2) void k_gemm128_post(
+    int M, int N, int K, const double *__restrict__ A, int64_t lda, const double *__restrict__ Qs,
+    const double *__restrict__ Qn, const double *__restrict__ Xs, const double *__restrict__ Xn,
+    int kind, double sigma2, double iso_scale, double *__restrict__ C, int64_t ldc, int msum,
+    double *__restrict__ Cm, int64_t ldm) {
+  const int by = (int)gridDim.y - 1 - (int)blockIdx.y, bx = blockIdx.x;  // longest row tiles first
+  const int r0 = by * BT, c0 = bx * BT;
+  const int kend = min(K, r0 + BT);  // W lower triangular; the alpha rows sit in the last tile
+  __shared__ double sA[2][BT][GP];
+  __shared__ double sB[2][BT][GP];
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int qi = (wave >> 1) * 64, qj = (wave & 1) * 64;
+  d4_t acc[4][4];
+#pragma unroll
+  for (int x = 0; x < 4; ++x)
+#pragma unroll
+    for (int y = 0; y < 4; ++y) acc[x][y] = (d4_t){0.0, 0.0, 0.0, 0.0};
+  // A (W rows): row tid/2, k half (tid&1)*8
+  const int lr = tid >> 1, lk = (tid & 1) * 8;
+  const bool ra = r0 + lr < M;
+  const double *pa = A + (int64_t)(ra ? r0 + lr : 0) * lda;
+  const bool veca = (lda & 1) == 0 && (((uintptr_t)A) & 15) == 0;
+  // B (K*): query row qr, wave-uniform k half
+  const int qr = tid & 127;
+  const int bk = __builtin_amdgcn_readfirstlane((tid >> 7) * 8);
+  const int qrow = c0 + qr;
+  const bool rq = qrow < N;
+  double qv[D];
+#pragma unroll
+  for (int d = 0; d < D; ++d) qv[d] = rq ? Qs[(int64_t)qrow * D + d] : 0.0;
+  const double qn = rq ? Qn[qrow] : 0.0;
+  double va[8], vb[8];
+  auto gload = [&](int k0) {
+    const int k = k0 + lk;
+    if (veca && k + 7 < kend) {
+#pragma unroll
+      for (int q = 0; q < 8; q += 2) {
+        const double2 av = ra ? *(const double2 *)(pa + k + q) : make_double2(0.0, 0.0);
+        va[q] = av.x; va[q + 1] = av.y;
+      }
+    } else {
+#pragma unroll
+      for (int q = 0; q < 8; ++q) va[q] = (ra && k + q < kend) ? pa[k + q] : 0.0;
+    }
+    const int kb = k0 + bk;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int kq = kb + q;
+      double v = 0.0;
+      if (kq < kend) {  // wave-uniform
+        const double *x = Xs + (int64_t)kq * D;
+        double dot = 0.0;
+#pragma unroll
+        for (int d = 0; d < D; ++d) dot = fma(qv[d], x[d], dot);
+        const double d2 = (qn + Xn[kq]) - 2.0 * dot;
+        v = rq ? kernel_epilogue(kind, d2, sigma2, iso_scale) : 0.0;
+      }
+      vb[q] = v;
+    }
+  };
+  auto lstore = [&](int buf) {
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      sA[buf][lr][lk + q] = va[q];
+      sB[buf][qr][bk + q] = vb[q];
+    }
+  };
+  gload(0);
+  lstore(0);
+  __syncthreads();
+  int cur = 0;
+  for (int k0 = 0; k0 < kend; k0 += GK) {
+    const bool more = k0 + GK < kend;
+    if (more) gload(k0 + GK);
+#pragma unroll
+    for (int kk = 0; kk < GK; kk += 4) {
+      const int kc = kk + (lane >> 4);
+      double a[4], b[4];
+#pragma unroll
+      for (int x = 0; x < 4; ++x) a[x] = sA[cur][qi + 16 * x + (lane & 15)][kc];
+#pragma unroll
+      for (int y = 0; y < 4; ++y) b[y] = sB[cur][qj + 16 * y + (lane & 15)][kc];
+#pragma unroll
+      for (int x = 0; x < 4; ++x)
+#pragma unroll
+        for (int y = 0; y < 4; ++y) acc[x][y] = mfma_f64(a[x], b[y], acc[x][y]);
+    }
+    if (more) lstore(cur ^ 1);
+    __syncthreads();
+    cur ^= 1;
+  }
+  // SUMSQ epilogue (k_gemm128<EPI_SUMSQ>)
+  __shared__ double red[4][64];
+  double sq[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+  for (int x = 0; x < 4; ++x)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = r0 + qi + x * 16 + mf_row(lane, r);
+      if (row < msum) {
+#pragma unroll
+        for (int y = 0; y < 4; ++y) sq[y] = fma(acc[x][y][r], acc[x][y][r], sq[y]);
+      } else if (row < M) {
+#pragma unroll
+        for (int y = 0; y < 4; ++y) {
+          const int col = c0 + qj + y * 16 + mf_col(lane);
+          if (col < N) Cm[(int64_t)(row - msum) * ldm + col] = acc[x][y][r];
+        }
+      }
+    }
+#pragma unroll
+  for (int y = 0; y < 4; ++y) {
+    sq[y] += __shfl_xor(sq[y], 16);
+    sq[y] += __shfl_xor(sq[y], 32);
+  }
+  if (lane < 16) {
+#pragma unroll
+    for (int y = 0; y < 4; ++y) red[wave][y * 16 + lane] = sq[y];
+  }
+  __syncthreads();
+  if (tid < 128) {
+    const int half = tid >> 6, cc = tid & 63;
+    const double v = red[half][cc] + red[2 + half][cc];
+    const int col = c0 + tid;
+    if (col < N) C[(int64_t)by * ldc + col] = v;
+  }
+}
+
+hipError_t launch_gemm_post_fused(hipStream_t s, int n, int n_out, int P, const double *Wext,
+                                  const double *Qs, const double *Qn, const double *Xs,
+                                  const double *Xn, int d, int kind, double sigma2,
+                                  double iso_scale, double *part, int64_t ldp, double *meanT,
+                                  int64_t ldm) {
+  const int M = n + n_out;
+  if (P <= 0) return hipSuccess;
+  dim3 g((P + BT - 1) / BT, (M + BT - 1) / BT, 1);
+  switch (d) {
+    case 11:
+      hipLaunchKernelGGL(k_gemm128_post<11>, g, dim3(256), 0, s, M, P, n, Wext, (int64_t)n, Qs, Qn,
+                         Xs, Xn, kind, sigma2, iso_scale, part, ldp, n, meanT, ldm);
+      break;
+    case 12:
+      hipLaunchKernelGGL(k_gemm128_post<12>, g, dim3(256), 0, s, M, P, n, Wext, (int64_t)n, Qs, Qn,
+                         Xs, Xn, kind, sigma2, iso_scale, part, ldp, n, meanT, ldm);
+      break;
+    case 13:
+      hipLaunchKernelGGL(k_gemm128_post<13>, g, dim3(256), 0, s, M, P, n, Wext, (int64_t)n, Qs, Qn,
+                         Xs, Xn, kind, sigma2, iso_scale, part, ldp, n, meanT, ldm);
+      break;
+    default:
+      return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
 // Stream-K (C += alpha A B^T, STORE epilogue with beta = 1): the batch's
 // (tile, K-step) units are cut into gridDim.x equal contiguous ranges, one per
 // workgroup, so every resident slot does the same work whatever the tile count

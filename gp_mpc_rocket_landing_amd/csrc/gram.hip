@@ -37,25 +37,6 @@ hipError_t launch_scale_rows(hipStream_t s, const double *X, int n, int d, const
   return hipGetLastError();
 }
 
-__device__ __forceinline__ double kernel_epilogue(int kind, double d2, double sigma2,
-                                                  double iso_scale) {
-  d2 = d2 > 0.0 ? d2 : 0.0;  // np.maximum(dist_sq, 0.0)
-  switch (kind) {
-    case GPMPC_SE_ARD: return sigma2 * exp(-0.5 * d2);
-    case GPMPC_SE_ISO: return sigma2 * exp(-d2 * iso_scale);
-    case GPMPC_MATERN32: {
-      double r = sqrt(d2);
-      double s3 = 1.7320508075688772 * r;
-      return sigma2 * (1.0 + s3) * exp(-s3);
-    }
-    default: {
-      double r = sqrt(d2);
-      double s5 = 2.23606797749979 * r;
-      return sigma2 * (1.0 + s5 + 5.0 * (r * r) / 3.0) * exp(-s5);
-    }
-  }
-}
-
 template <int D>
 __global__ __launch_bounds__(256) void k_gram(int kind, const double *__restrict__ a,
                                               const double *__restrict__ na, int n1,

@@ -48,6 +48,27 @@ struct DevBuf {
   template <class T> T *as() const { return static_cast<T *>(p); }
 };
 
+// kernel value from r^2 of the length-scaled rows (the k_gram epilogue; shared
+// so that every kernel that forms K*(x, x') produces the same bits)
+__device__ __forceinline__ double kernel_epilogue(int kind, double d2, double sigma2,
+                                                  double iso_scale) {
+  d2 = d2 > 0.0 ? d2 : 0.0;  // np.maximum(dist_sq, 0.0)
+  switch (kind) {
+    case GPMPC_SE_ARD: return sigma2 * exp(-0.5 * d2);
+    case GPMPC_SE_ISO: return sigma2 * exp(-d2 * iso_scale);
+    case GPMPC_MATERN32: {
+      double r = sqrt(d2);
+      double s3 = 1.7320508075688772 * r;
+      return sigma2 * (1.0 + s3) * exp(-s3);
+    }
+    default: {
+      double r = sqrt(d2);
+      double s5 = 2.23606797749979 * r;
+      return sigma2 * (1.0 + s5 + 5.0 * (r * r) / 3.0) * exp(-s5);
+    }
+  }
+}
+
 // ---- internal device entry points shared across translation units ----------
 // Gram: K (n1 x n2, ldk) from pre-scaled rows (a = X1/ls, b = X2/ls) and their
 // squared norms; kind selects the epilogue.
