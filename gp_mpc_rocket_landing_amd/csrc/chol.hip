@@ -17,6 +17,7 @@
 #include "internal.h"
 #include "mfma64.h"
 #include "gemm.h"
+#include "mma128.h"
 
 #define NB 32
 #define TP 34  // LDS pitch (doubles) for 32-wide tiles: conflict-free ds_read_b64
@@ -132,49 +133,26 @@ __device__ __forceinline__ double rdlane(double v, int l) {
 // diagnostic phase cycles of workgroup 0 (GPMPC_DIAG128_STAMPS=1 builds the <true> launch)
 __device__ unsigned long long g_d128_stamps[8];
 
+// The factor + inverse of a 128 x 128 diagonal block already in LDS (S: lower
+// triangle, identity padding beyond pw, zero upper triangle; sfail = 0), for
+// k_potrf_diag128 and the per-matrix k_potrf_persist.  Writes L (rows < pw) at
+// M and, when Li is non-null and pw == 128, Linv (128 x 128, upper zero) at Li.
+// Returns 1 (uniformly) when a pivot fails, after setting *infob.
 template <bool ST>
-__global__ __launch_bounds__(256) void k_potrf_diag128(int n, int K0, double *A, int64_t lda,
-                                                       int64_t stride, int *info, double *Linv) {
-  const int b = blockIdx.x;
-  if (info[b]) return;
+__device__ __forceinline__ int diag128_core(double (*S)[DP], double *col, int &sfail, double *M,
+                                            int64_t lda, int pw, int K0, int *infob, double *Li,
+                                            bool stamp) {
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int li = lane & 15, lk = lane >> 4;
   unsigned long long tl = 0;
   auto mark = [&](int k) {
-    if (ST && b == 0 && threadIdx.x == 0) {
+    if (ST && stamp && threadIdx.x == 0) {
       const unsigned long long t = __builtin_amdgcn_s_memtime();
       if (k >= 0) atomicAdd(&g_d128_stamps[k], t - tl);
       tl = t;
     }
   };
   mark(-1);
-  // one dynamic region (no static LDS in front of it): S, then col, then the fail flag
-  extern __shared__ double S_[];
-  double(*S)[DP] = reinterpret_cast<double(*)[DP]>(S_);
-  double *col = S_ + DB * DP;
-  int &sfail = *reinterpret_cast<int *>(S_ + DB * DP + NB);
-  double *M = A + (int64_t)b * stride + (int64_t)K0 * lda + K0;
-  const int pw = min(DB, n - K0);
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  const int li = lane & 15, lk = lane >> 4;
-  // lower triangle in, identity padding beyond pw, zero upper triangle; 32 loads
-  // in flight per lane before the LDS stores (a load-store loop waits out the
-  // HBM latency once per element)
-#pragma unroll 1
-  for (int q0 = 0; q0 < DB * DB / 256; q0 += 32) {
-    double v[32];
-#pragma unroll
-    for (int q = 0; q < 32; ++q) {
-      const int e = tid + 256 * (q0 + q), i = e >> 7, j = e & 127;
-      v[q] = (j <= i && i < pw) ? M[(int64_t)i * lda + j] : (i == j ? 1.0 : 0.0);
-    }
-#pragma unroll
-    for (int q = 0; q < 32; ++q) {
-      const int e = tid + 256 * (q0 + q);
-      S[e >> 7][e & 127] = v[q];
-    }
-  }
-  if (tid == 0) sfail = 0;
-  lds_barrier();
-  mark(0);
   // 32-column blocks holding real rows; the identity padding beyond pw is its
   // own factor and inverse, so a short last panel (or a small matrix) skips it
   const int nblk = (pw + NB - 1) / NB;
@@ -270,7 +248,7 @@ __global__ __launch_bounds__(256) void k_potrf_diag128(int n, int K0, double *A,
       }
       if (fail) {
         if (lane == 0) {
-          info[b] = K0 + c0 + fail;
+          *infob = K0 + c0 + fail;
           sfail = 1;
         }
       } else {
@@ -316,7 +294,7 @@ __global__ __launch_bounds__(256) void k_potrf_diag128(int n, int K0, double *A,
     }
     lds_barrier();
     mark(1);
-    if (sfail) return;
+    if (sfail) return 1;
     const int R = nblk * NB - c0 - NB;  // rows below the diagonal block (real blocks only)
     if (R == 0) break;
     // ---- 2. panel X = A T^T: (R/16) x 2 tiles of 16 x 16, K = 32
@@ -359,7 +337,7 @@ __global__ __launch_bounds__(256) void k_potrf_diag128(int n, int K0, double *A,
     if ((j >> 5) < (i >> 5) && i < pw) M[(int64_t)i * lda + j] = S[i][j];
   }
   mark(4);
-  if (pw < DB || !Linv) return;  // the last panel has no rows below: no inverse needed
+  if (pw < DB || !Li) return 0;  // the last panel has no rows below: no inverse needed
   // ---- inverse, block row i = 1..3:  Y_j = sum_k L_ik X_kj -> upper block (j, i)
   // transposed; then X_ij = -T_i Y_j in place.  Jobs: (j, 16x16 tile) pairs.
   for (int i = 1; i < DB / NB; ++i) {
@@ -422,13 +400,152 @@ __global__ __launch_bounds__(256) void k_potrf_diag128(int n, int K0, double *A,
     lds_barrier();
   }
   mark(5);
-  double *Li = Linv + (int64_t)b * DB * DB;
 #pragma unroll 4
   for (int e = tid; e < DB * DB; e += 256) {
     const int i = e >> 7, j = e & 127;
     Li[e] = (j > i) ? 0.0 : ((i >> 5) == (j >> 5) ? S[i][j] : S[j][i]);
   }
   mark(6);
+  return 0;
+}
+
+template <bool ST>
+__global__ __launch_bounds__(256) void k_potrf_diag128(int n, int K0, double *A, int64_t lda,
+                                                       int64_t stride, int *info, double *Linv) {
+  const int b = blockIdx.x;
+  if (info[b]) return;
+  // one dynamic region (no static LDS in front of it): S, then col, then the fail flag
+  extern __shared__ double S_[];
+  double(*S)[DP] = reinterpret_cast<double(*)[DP]>(S_);
+  double *col = S_ + DB * DP;
+  int &sfail = *reinterpret_cast<int *>(S_ + DB * DP + NB);
+  double *M = A + (int64_t)b * stride + (int64_t)K0 * lda + K0;
+  const int pw = min(DB, n - K0);
+  const int tid = threadIdx.x;
+  // lower triangle in, identity padding beyond pw, zero upper triangle; 32 loads
+  // in flight per lane before the LDS stores (a load-store loop waits out the
+  // HBM latency once per element)
+#pragma unroll 1
+  for (int q0 = 0; q0 < DB * DB / 256; q0 += 32) {
+    double v[32];
+#pragma unroll
+    for (int q = 0; q < 32; ++q) {
+      const int e = tid + 256 * (q0 + q), i = e >> 7, j = e & 127;
+      v[q] = (j <= i && i < pw) ? M[(int64_t)i * lda + j] : (i == j ? 1.0 : 0.0);
+    }
+#pragma unroll
+    for (int q = 0; q < 32; ++q) {
+      const int e = tid + 256 * (q0 + q);
+      S[e >> 7][e & 127] = v[q];
+    }
+  }
+  if (tid == 0) sfail = 0;
+  lds_barrier();
+  diag128_core<ST>(S, col, sfail, M, lda, pw, K0, info + b, Linv ? Linv + (int64_t)b * DB * DB : nullptr,
+                   b == 0);
+}
+
+// ---------------------------------------------------------------------------
+// One workgroup per matrix for the whole factorisation (large batches: every CU
+// owns a matrix, no launch-level serial chain).  Left-looking 128-column panels:
+//   1. update: panel rows [J, n) -= L[rows, 0:J] L[J:J+128, 0:J]^T, one 128 x 128
+//      MFMA tile at a time (mma128_tile, K = J); the row tiles below go back to
+//      the matrix in place, the diagonal tile straight into the LDS block;
+//   2. diag128_core factors and inverts the diagonal block (L_JJ out, Linv to a
+//      per-matrix workspace);
+//   3. panel solve: rows [J+128, n) <- X Linv^T, one K = 128 tile at a time.
+// Data written by one wave and read by another in a later phase crosses the
+// (per-CU, not store-refreshed) vector L1, so every phase boundary is a release
+// fence + barrier + agent acquire (L1 invalidate).  The GEMM staging buffers
+// alias the LDS block (they are never live at the same time).
+__device__ __forceinline__ void wg_global_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+  __syncthreads();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+}
+
+__global__ __launch_bounds__(256) void k_potrf_persist(int n, double *A, int64_t lda, int64_t stride,
+                                                       int *info, double *Lws) {
+  const int b = blockIdx.x;
+  extern __shared__ double S_[];
+  double(*S)[DP] = reinterpret_cast<double(*)[DP]>(S_);
+  double *col = S_ + DB * DP;
+  int &sfail = *reinterpret_cast<int *>(S_ + DB * DP + NB);
+  double(*sA)[BT][GP] = reinterpret_cast<double(*)[BT][GP]>(S_);
+  double(*sB)[BT][GP] = reinterpret_cast<double(*)[BT][GP]>(S_ + 2 * BT * GP);
+  double *Mb = A + (int64_t)b * stride;
+  double *Li = Lws + (int64_t)b * DB * DB;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int qi = (wave >> 1) * 64, qj = (wave & 1) * 64;
+  for (int J = 0; J < n; J += DB) {
+    const int pw = min(DB, n - J);
+    const int nrt = (n - J + DB - 1) / DB;
+    if (J > 0) {
+      // 1. update, bottom row tile first: the diagonal tile (rt = 0) lands in LDS last
+      for (int rt = nrt - 1; rt >= 0; --rt) {
+        d4_t acc[4][4];
+        const int r0 = J + rt * DB;
+        mma128_tile(Mb + (int64_t)r0 * lda, lda, Mb + (int64_t)J * lda, lda, n - r0, pw, 0, 0, 0, J,
+                    sA, sB, acc);
+#pragma unroll
+        for (int x = 0; x < 4; ++x)
+#pragma unroll
+          for (int y = 0; y < 4; ++y)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const int i = qi + x * 16 + mf_row(lane, r), j = qj + y * 16 + mf_col(lane);
+              if (rt > 0) {
+                if (r0 + i < n && j < pw) {
+                  double *p = Mb + (int64_t)(r0 + i) * lda + J + j;
+                  *p = *p - acc[x][y][r];
+                }
+              } else {
+                S[i][j] = (j <= i && i < pw) ? Mb[(int64_t)(J + i) * lda + J + j] - acc[x][y][r]
+                                             : (i == j ? 1.0 : 0.0);
+              }
+            }
+      }
+    } else {
+#pragma unroll 1
+      for (int q0 = 0; q0 < DB * DB / 256; q0 += 32) {
+        double v[32];
+#pragma unroll
+        for (int q = 0; q < 32; ++q) {
+          const int e = tid + 256 * (q0 + q), i = e >> 7, j = e & 127;
+          v[q] = (j <= i && i < pw) ? Mb[(int64_t)i * lda + j] : (i == j ? 1.0 : 0.0);
+        }
+#pragma unroll
+        for (int q = 0; q < 32; ++q) {
+          const int e = tid + 256 * (q0 + q);
+          S[e >> 7][e & 127] = v[q];
+        }
+      }
+    }
+    if (tid == 0) sfail = 0;
+    lds_barrier();
+    // 2. diagonal block: L_JJ to the matrix, Linv to the workspace
+    if (diag128_core<false>(S, col, sfail, Mb + (int64_t)J * lda + J, lda, pw, J, info + b,
+                            J + DB < n ? Li : nullptr, false))
+      return;
+    if (J + DB >= n) break;
+    wg_global_sync();
+    // 3. panel solve, in place (each tile's reads end on mma128_tile's barrier)
+    for (int rt = 1; rt < nrt; ++rt) {
+      d4_t acc[4][4];
+      const int r0 = J + rt * DB;
+      mma128_tile(Mb + (int64_t)r0 * lda + J, lda, Li, DB, n - r0, DB, 0, 0, 0, DB, sA, sB, acc);
+#pragma unroll
+      for (int x = 0; x < 4; ++x)
+#pragma unroll
+        for (int y = 0; y < 4; ++y)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int i = qi + x * 16 + mf_row(lane, r), j = qj + y * 16 + mf_col(lane);
+            if (r0 + i < n) Mb[(int64_t)(r0 + i) * lda + J + j] = acc[x][y][r];
+          }
+    }
+    wg_global_sync();
+  }
 }
 
 // Two-level blocking.  Outer panels of OB = 128 columns; inside a panel,
@@ -554,6 +671,27 @@ hipError_t launch_potrf_batched(hipStream_t s, int n, int batch, double *A, int6
     const char *e = getenv("GPMPC_POTRF128");
     return e ? atoi(e) : 1;
   }();
+  // one workgroup per matrix (GPMPC_POTRF_PERSIST=1; read per call, tests switch
+  // it).  Off by default: measured 3.67 ms per round of <= 256 matrices of
+  // n = 1000 (20.8% of FP64 peak at batch 256) against 3.9 ms (28%) for the
+  // launch-per-panel path -- one wave per SIMD (130 KB of LDS per workgroup)
+  // leaves the MFMA tile loop's LDS and barrier latency exposed, and the
+  // diagonal chain idles the CU.
+  const char *pe = getenv("GPMPC_POTRF_PERSIST");
+  const bool persist = pe && atoi(pe) > 0;
+  if (p128 && persist) {
+    static bool attr = hipFuncSetAttribute((const void *)k_potrf_persist,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize,
+                                           (int)DIAG128_LDS) == hipSuccess;
+    if (!attr) return hipErrorInvalidConfiguration;
+    double *Lws = (double *)gpmpc_scratch(2, sizeof(double) * DB * DB * (size_t)batch);
+    if (!Lws) return hipErrorOutOfMemory;
+    hipError_t e = hipMemsetAsync(info, 0, sizeof(int) * batch, s);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_potrf_persist, dim3(batch), dim3(256), DIAG128_LDS, s, n, A, lda, stride,
+                       info, Lws);
+    return hipGetLastError();
+  }
   if (p128) {
     double *Linv = (double *)gpmpc_scratch(2, sizeof(double) * DB * DB * (size_t)batch);
     if (!Linv) return hipErrorOutOfMemory;

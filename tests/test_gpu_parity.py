@@ -87,6 +87,39 @@ def test_potrf_batched_dev(gpu_ctx, n, batch):
     assert torch.equal(A[:-1, up], up_before[:-1])
 
 
+@pytest.mark.parametrize("n", [100, 129, 256, 300, 1000])
+def test_potrf_batched_persistent(gpu_ctx, n):
+    """The one-workgroup-per-matrix potrf (k_potrf_persist: left-looking 128-column
+    panels, MFMA update and panel-solve tiles, the diag128 factor in between; the
+    large-batch path) forced on a small batch: equal to np.linalg.cholesky, upper
+    triangle untouched, a bad pivot reported without disturbing the others."""
+    import os
+    import torch
+    L = _lib()
+    rs = np.random.RandomState(3 * n)
+    As = [(lambda G: G @ G.T / n + np.eye(n))(rs.normal(size=(n, n))) for _ in range(3)]
+    bad = min(n - 1, 130 if n > 130 else n // 2)
+    As[-1][bad, :] = 0.0; As[-1][:, bad] = 0.0; As[-1][bad, bad] = -1.0
+    A = torch.tensor(np.stack(As), dtype=torch.float64, device="cuda")
+    up = torch.triu(torch.ones(n, n, dtype=torch.bool, device="cuda"), 1)
+    up_before = A[:, up].clone()
+    info = torch.full((3,), 7, dtype=torch.int32, device="cuda")
+    torch.cuda.synchronize()
+    os.environ["GPMPC_POTRF_PERSIST"] = "1"
+    try:
+        rc = L._L.gpmpc_potrf_batched_dev(gpu_ctx.h, n, 3, A.data_ptr(), n, n * n, info.data_ptr())
+        L._chk(rc, "potrf_batched_dev")
+        gpu_ctx.sync()
+    finally:
+        os.environ.pop("GPMPC_POTRF_PERSIST", None)
+    inf = info.cpu().numpy()
+    assert list(inf) == [0, 0, bad + 1]
+    Ah = A.cpu().numpy()
+    for b in range(2):
+        np.testing.assert_allclose(np.tril(Ah[b]), np.linalg.cholesky(As[b]), rtol=1e-10, atol=1e-12)
+    assert torch.equal(A[:2, up], up_before[:2])
+
+
 def test_potrf_reports_first_bad_pivot(gpu_ctx):
     L = _lib()
     A = np.eye(70); A[40, 40] = -1.0
