@@ -678,7 +678,7 @@ extern "C" int gpmpc_gp_lml_batched(gpmpc_ctx *ctx, int kind, const double *X, i
   hipStream_t s = ctx->stream;
   const int iso = (kind == GPMPC_SE_ISO);
   const size_t nn = (size_t)n * n;
-  DevBuf dX, dY, dyn, dm, dsd, dls, Xs, Xn, K, dinfo, dlml;
+  DevBuf dX, dY, dyn, dm, dsd, dls, Xs, Xn, dinfo, dlml;
   GPMPC_HIP(dX.alloc(sizeof(double) * n * d));
   GPMPC_HIP(dY.alloc(sizeof(double) * n));
   GPMPC_HIP(dyn.alloc(sizeof(double) * n));
@@ -687,7 +687,11 @@ extern "C" int gpmpc_gp_lml_batched(gpmpc_ctx *ctx, int kind, const double *X, i
   GPMPC_HIP(dls.alloc(sizeof(double) * B * d));
   GPMPC_HIP(Xs.alloc(sizeof(double) * (size_t)B * n * d));
   GPMPC_HIP(Xn.alloc(sizeof(double) * (size_t)B * n));
-  if (K.alloc(sizeof(double) * nn * B) != hipSuccess) {
+  // the B Gram / factor matrices live in persistent scratch (slot 3): one
+  // optimiser gradient per call, so a per-call hipMalloc of B n^2 doubles
+  // (112 MB at n = 1000) would cost more than the factorisations
+  double *Kbuf = (double *)gpmpc_scratch(3, sizeof(double) * nn * B);
+  if (!Kbuf) {
     gpmpc_set_error("gp_lml_batched: out of device memory for %d x %d^2 doubles", B, n);
     return -1;
   }
@@ -700,7 +704,7 @@ extern "C" int gpmpc_gp_lml_batched(gpmpc_ctx *ctx, int kind, const double *X, i
   hipLaunchKernelGGL(k_normalise, dim3(1), dim3(256), 0, s, n, 1, dY.as<double>(), dyn.as<double>(),
                      dm.as<double>(), dsd.as<double>());
   auto build = [&](int b, double jit) -> hipError_t {  // K_b + noise_b I (+ jit I)
-    double *Kb = K.as<double>() + nn * b;
+    double *Kb = Kbuf + nn * b;
     hipError_t e = launch_gram(s, kind, Xs.as<double>() + (size_t)b * n * d,
                                Xn.as<double>() + (size_t)b * n, n,
                                Xs.as<double>() + (size_t)b * n * d, Xn.as<double>() + (size_t)b * n,
@@ -715,7 +719,7 @@ extern "C" int gpmpc_gp_lml_batched(gpmpc_ctx *ctx, int kind, const double *X, i
                                 Xs.as<double>() + (size_t)b * n * d, Xn.as<double>() + (size_t)b * n));
     GPMPC_HIP(build(b, 0.0));
   }
-  GPMPC_HIP(launch_potrf_batched(s, n, B, K.as<double>(), n, (int64_t)nn, dinfo.as<int>()));
+  GPMPC_HIP(launch_potrf_batched(s, n, B, Kbuf, n, (int64_t)nn, dinfo.as<int>()));
   std::vector<int> info(B);
   GPMPC_HIP(hipMemcpyAsync(info.data(), dinfo.p, sizeof(int) * B, hipMemcpyDeviceToHost, s));
   GPMPC_HIP(hipStreamSynchronize(s));
@@ -727,7 +731,7 @@ extern "C" int gpmpc_gp_lml_batched(gpmpc_ctx *ctx, int kind, const double *X, i
     int steps = 1, ok = 0;
     while (jit < 1.0) {
       GPMPC_HIP(build(b, jit));
-      GPMPC_HIP(launch_potrf_batched(s, n, 1, K.as<double>() + nn * b, n, 0,
+      GPMPC_HIP(launch_potrf_batched(s, n, 1, Kbuf + nn * b, n, 0,
                                      dinfo.as<int>() + b));
       int ib = 0;
       GPMPC_HIP(hipMemcpyAsync(&ib, dinfo.as<int>() + b, sizeof(int), hipMemcpyDeviceToHost, s));
@@ -746,7 +750,7 @@ extern "C" int gpmpc_gp_lml_batched(gpmpc_ctx *ctx, int kind, const double *X, i
     return -1;
   }
   hipLaunchKernelGGL(k_lml_trsv, dim3(B), dim3(256), sizeof(double) * (n + 4), s, n,
-                     K.as<double>(), (int64_t)nn, dyn.as<double>(), dinfo.as<int>(),
+                     Kbuf, (int64_t)nn, dyn.as<double>(), dinfo.as<int>(),
                      dlml.as<double>());
   GPMPC_HIP(hipGetLastError());
   GPMPC_HIP(hipMemcpyAsync(lml, dlml.p, sizeof(double) * B, hipMemcpyDeviceToHost, s));
