@@ -11,6 +11,7 @@
 // stores 64 consecutive doubles (512 B) per row -- fully coalesced.  The
 // kernel is HBM-store-bound for n1 = n2 = 1000 (8 MB out, 88 KB in).
 #include "internal.h"
+#include <cstdlib>
 
 #define GRAM_TILE 64
 #define GRAM_MAXD 32
@@ -82,11 +83,87 @@ __global__ __launch_bounds__(256) void k_gram(int kind, const double *__restrict
   }
 }
 
+// Row-major K (no transpose), compile-time kernel kind and width: 64 columns x
+// 128 rows per workgroup (each thread one column, 32 rows, 8 independent
+// exponentials in flight), same arithmetic as k_gram (identical bits).
+#define GRAM_ROWS 128
+template <int D, int KIND>
+__global__ __launch_bounds__(256) void k_gram_rows(const double *__restrict__ a,
+                                                   const double *__restrict__ na, int n1,
+                                                   const double *__restrict__ b,
+                                                   const double *__restrict__ nb, int n2,
+                                                   double sigma2, double iso_scale,
+                                                   double *__restrict__ K, int64_t ldk) {
+  __shared__ double sa[GRAM_ROWS][D + 1];
+  __shared__ double sna[GRAM_ROWS];
+  const int r0 = blockIdx.y * GRAM_ROWS, c0 = blockIdx.x * GRAM_TILE;
+  const int tid = threadIdx.x;
+  for (int e = tid; e < GRAM_ROWS * D; e += 256) {
+    const int r = e / D, k = e - r * D;
+    sa[r][k] = (r0 + r < n1) ? a[(int64_t)(r0 + r) * D + k] : 0.0;
+  }
+  if (tid < GRAM_ROWS) sna[tid] = (r0 + tid < n1) ? na[r0 + tid] : 0.0;
+  const int col = c0 + (tid & 63);
+  const int rb = (tid >> 6) * 32;
+  double bj[D];
+  double nbj = 0.0;
+  const bool cv = col < n2;
+#pragma unroll
+  for (int k = 0; k < D; ++k) bj[k] = cv ? b[(int64_t)col * D + k] : 0.0;
+  if (cv) nbj = nb[col];
+  __syncthreads();
+  if (!cv) return;
+#pragma unroll 8
+  for (int rr = 0; rr < 32; ++rr) {
+    const int r = rb + rr, row = r0 + r;
+    double dot = 0.0;
+#pragma unroll
+    for (int k = 0; k < D; ++k) dot = fma(sa[r][k], bj[k], dot);
+    const double d2 = (sna[r] + nbj) - 2.0 * dot;
+    const double v = kernel_epilogue(KIND, d2, sigma2, iso_scale);
+    if (row < n1) K[(int64_t)row * ldk + col] = v;
+  }
+}
+
+template <int D>
+static hipError_t launch_gram_rows(hipStream_t s, int kind, const double *a, const double *na,
+                                   int n1, const double *b, const double *nb, int n2,
+                                   double sigma2, double iso_scale, double *K, int64_t ldk) {
+  dim3 g((n2 + GRAM_TILE - 1) / GRAM_TILE, (n1 + GRAM_ROWS - 1) / GRAM_ROWS);
+  switch (kind) {
+    case GPMPC_SE_ARD:
+      hipLaunchKernelGGL((k_gram_rows<D, GPMPC_SE_ARD>), g, dim3(256), 0, s, a, na, n1, b, nb, n2,
+                         sigma2, iso_scale, K, ldk);
+      break;
+    case GPMPC_SE_ISO:
+      hipLaunchKernelGGL((k_gram_rows<D, GPMPC_SE_ISO>), g, dim3(256), 0, s, a, na, n1, b, nb, n2,
+                         sigma2, iso_scale, K, ldk);
+      break;
+    case GPMPC_MATERN32:
+      hipLaunchKernelGGL((k_gram_rows<D, GPMPC_MATERN32>), g, dim3(256), 0, s, a, na, n1, b, nb,
+                         n2, sigma2, iso_scale, K, ldk);
+      break;
+    default:
+      hipLaunchKernelGGL((k_gram_rows<D, GPMPC_MATERN52>), g, dim3(256), 0, s, a, na, n1, b, nb,
+                         n2, sigma2, iso_scale, K, ldk);
+  }
+  return hipGetLastError();
+}
+
 hipError_t launch_gram(hipStream_t s, int kind, const double *a, const double *na, int n1,
                        const double *b, const double *nb, int n2, int d, double sigma2,
                        double iso_scale, double *K, int64_t ldk, int transpose_out) {
   if (n1 <= 0 || n2 <= 0) return hipSuccess;
   if (d > GRAM_MAXD) return hipErrorInvalidValue;
+  static const int rows_env = [] {
+    const char *v = getenv("GPMPC_GRAM_ROWS");
+    return v ? atoi(v) : 1;
+  }();
+  if (rows_env && !transpose_out && n1 >= 4 * GRAM_ROWS) {
+    if (d == 11) return launch_gram_rows<11>(s, kind, a, na, n1, b, nb, n2, sigma2, iso_scale, K, ldk);
+    if (d == 12) return launch_gram_rows<12>(s, kind, a, na, n1, b, nb, n2, sigma2, iso_scale, K, ldk);
+    if (d == 13) return launch_gram_rows<13>(s, kind, a, na, n1, b, nb, n2, sigma2, iso_scale, K, ldk);
+  }
   dim3 g((n2 + GRAM_TILE - 1) / GRAM_TILE, (n1 + GRAM_TILE - 1) / GRAM_TILE);
   switch (d) {
     case 11:
