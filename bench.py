@@ -64,17 +64,17 @@ def pmc_traffic(kernel):
     return None, None
 
 
-def _cpu_landing_loop(seconds, n_train=1000, horizon=20, seed=42):
+def _cpu_landing_loop(seconds, n_train=1000, horizon=20, seed=42, threads=1):
     """One landing closed loop of the reference CPU path restated (oracle):
     numpy/scipy GP posterior at the N horizon points (same LAPACK calls as
     exact_gp.py), numpy QP assembly (osqp_rti.py semantics) and the C
-    restatement of the OSQP ADMM, BLAS on one thread.  Returns (steps, seconds)."""
+    restatement of the OSQP ADMM, BLAS on ``threads`` threads.  Returns (steps, seconds)."""
     from threadpoolctl import threadpool_limits
     from oracle import admm_ref, gp_oracle, mc_oracle, qp_oracle
     from gp_mpc_rocket_landing_amd.data import synthetic_training_data
 
     X, U, D = synthetic_training_data(n_train, seed=0)
-    with threadpool_limits(1):
+    with threadpool_limits(threads):
         st = gp_oracle.exact_fit(gp_oracle.features_3dof(X, U), D)
         x = mc_oracle.sample_initial_condition(seed)
         tgt = mc_oracle.incremental_target(x)
@@ -130,8 +130,11 @@ def cpu_baseline(seconds, n_train=1000, horizon=20, workers=None):
         blas = np.__config__.CONFIG["Build Dependencies"]["blas"]["name"]
     except Exception:  # noqa: BLE001
         blas = "unknown"
+    # SURVEY 8d mode (i): one landing with BLAS on all the workers' cores
+    st1, el1 = _cpu_landing_loop(min(5.0, seconds), n_train, horizon, 42, workers)
     return dict(value=steps / el, unit="control steps/s", cores=workers, kind="port",
                 per_core=round(per_core, 3),
+                single_landing_all_cores=round(st1 / el1, 3),
                 sample=f"{workers} processes x 1 landing closed loop, {steps} control steps in "
                        f"{el:.1f} s (numpy/scipy GP N={n_train}, P={horizon}; numpy QP assembly; "
                        f"C OSQP-0.6 ADMM restatement; {blas} on 1 thread per process; "
@@ -418,7 +421,7 @@ def main():
         steps_rank0 = steps_done / K
         admm_flop = (admm_iters / K) * it_f + steps_rank0 * 1.5 * fac_f
         kern = {
-            "gram_Kstar": dict(kernel="k_gram<11>", ms=ph_mean[0] * 1e3, bound="hbm",
+            "gram_Kstar": dict(kernel="k_gram_rows<11, 0>", ms=ph_mean[0] * 1e3, bound="hbm",
                                achieved=gram_bytes / ph_mean[0] / 1e9, peak=HBM_PEAK_GBS, unit="GB/s"),
             "var_mean_gemm_mfma": dict(kernel="k_gemm128<1>", ms=ph_mean[1] * 1e3, bound="mfma",
                                        achieved=var_flops / ph_mean[1] / 1e12, peak=FP64_PEAK_TFLOPS,
