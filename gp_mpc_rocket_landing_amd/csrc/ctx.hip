@@ -16,14 +16,15 @@ void gpmpc_set_error(const char *fmt, ...) {
 // device sync.  (Stream-ordered hipMallocAsync scratch returned buffers the next
 // kernel on the same stream did not see written on ROCm 7.2 -- see DESIGN.md.)
 static std::mutex g_scratch_mu;
-static void *g_scratch[64][4];
-static size_t g_scratch_bytes[64][4];
+#define GPMPC_SCRATCH_SLOTS 8
+static void *g_scratch[64][GPMPC_SCRATCH_SLOTS];
+static size_t g_scratch_bytes[64][GPMPC_SCRATCH_SLOTS];
 
 void *gpmpc_scratch(int slot, size_t bytes) {
   int dev = 0;
   (void)hipGetDevice(&dev);
   std::lock_guard<std::mutex> lk(g_scratch_mu);
-  if (dev < 0 || dev >= 64 || slot < 0 || slot >= 4) return nullptr;
+  if (dev < 0 || dev >= 64 || slot < 0 || slot >= GPMPC_SCRATCH_SLOTS) return nullptr;
   if (g_scratch_bytes[dev][slot] < bytes) {
     (void)hipDeviceSynchronize();
     if (g_scratch[dev][slot]) (void)hipFree(g_scratch[dev][slot]);

@@ -411,11 +411,12 @@ __global__ __launch_bounds__(FQ_T) __attribute__((amdgpu_waves_per_eu(2, 2))) vo
   QPStamps T;
   T.out = (STAMPS && b == 0) ? a.stamps : nullptr;
   T.start();
-  if (a.trace && tid == 0) {
+  if (a.trace && (tid & 63) == 0) {
+    // [0] start, [1] end (realtime), [2] wave 0 HW_ID | XCC_ID << 32, [3] wave 1 the same
     unsigned long long *tr = a.trace + (int64_t)b * 4;
-    tr[0] = __builtin_amdgcn_s_memrealtime();
-    tr[2] = (unsigned)__builtin_amdgcn_s_getreg(4 | (31 << 11));
-    tr[3] = (unsigned)__builtin_amdgcn_s_getreg(20 | (31 << 11));
+    if (tid == 0) tr[0] = __builtin_amdgcn_s_memrealtime();
+    tr[2 + (tid >> 6)] = (unsigned long long)(unsigned)__builtin_amdgcn_s_getreg(4 | (31 << 11)) |
+                         ((unsigned long long)(unsigned)__builtin_amdgcn_s_getreg(20 | (31 << 11)) << 32);
   }
   double *x = a.x + (int64_t)b * NX;
   double *Xw = a.Xw + (int64_t)b * (N + 1) * NX;

@@ -135,8 +135,9 @@ __device__ __forceinline__ void fq_init_pattern(const QPPattern &pt, FleetRegs &
       const int k0 = pt.colptr[j], k1 = pt.colptr[j + 1] - 1;  // the last entry is the bound row
       R.cn[h] = k1 - k0;
 #pragma unroll
-      for (int e = 0; e < FQ_CMAX; ++e)
-        R.cp[h][e] = (e < R.cn[h]) ? (pt.csc2csr[k0 + e] | (pt.cscrow[k0 + e] << 16)) : 0;
+      for (int e = 0; e < FQ_CMAX; ++e)  // past the column: the zero pads A[FQ_NNZD], zt[FQ_MD]
+        R.cp[h][e] = (e < R.cn[h]) ? (pt.csc2csr[k0 + e] | (pt.cscrow[k0 + e] << 16))
+                                   : (FQ_NNZD | (FQ_MD << 16));
     } else {
 #pragma unroll
       for (int e = 0; e < FQ_CMAX; ++e) R.cp[h][e] = 0;
@@ -150,12 +151,50 @@ __device__ __forceinline__ void fq_init_pattern(const QPPattern &pt, FleetRegs &
       R.rbn(h) = rb | (rn << 16);
 #pragma unroll
       for (int e = 0; e < (FQ_RMAX + 1) / 2; ++e) {
-        const int c0 = (2 * e < rn) ? pt.colidx[rb + 2 * e] : 0;
-        const int c1 = (2 * e + 1 < rn) ? pt.colidx[rb + 2 * e + 1] : 0;
+        // past the row: column FQ_NMAX - 1, a zero slot of x~ (never written)
+        const int c0 = (2 * e < rn) ? pt.colidx[rb + 2 * e] : FQ_NMAX - 1;
+        const int c1 = (2 * e + 1 < rn) ? pt.colidx[rb + 2 * e + 1] : FQ_NMAX - 1;
         R.rcp(h, e) = c0 | (c1 << 16);
       }
     }
   }
+}
+
+// K-term LDS dot products with all 2K reads in flight at once.  The empty asm
+// takes every loaded value as an operand, so the reads issue before it and one
+// wait covers them; left alone, the compiler (at the 256-VGPR budget)
+// serialises read -> wait -> FMA per term.  Same terms, same order as the
+// plain loop.
+__device__ __forceinline__ double fq_col_dot(const FleetSmem &s, const FleetRegs &R, int h) {
+  static_assert(FQ_CMAX == 6, "fq_col_dot holds 6 terms");
+  double a[FQ_CMAX], z[FQ_CMAX];
+#pragma unroll
+  for (int e = 0; e < FQ_CMAX; ++e) {
+    a[e] = s.A[R.ca(h, e)];
+    z[e] = s.zt[R.cr(h, e)];
+  }
+  asm volatile("" : "+v"(a[0]), "+v"(a[1]), "+v"(a[2]), "+v"(a[3]), "+v"(a[4]), "+v"(a[5]),
+                    "+v"(z[0]), "+v"(z[1]), "+v"(z[2]), "+v"(z[3]), "+v"(z[4]), "+v"(z[5]));
+  double acc = 0.0;
+#pragma unroll
+  for (int e = 0; e < FQ_CMAX; ++e) acc += a[e] * z[e];
+  return acc;
+}
+__device__ __forceinline__ double fq_row_dot(const FleetSmem &s, FleetRegs &R, int h) {
+  static_assert(FQ_RMAX == 5, "fq_row_dot holds 5 terms");
+  double a[FQ_RMAX], v[FQ_RMAX];
+  const int rb = R.rb(h);
+#pragma unroll
+  for (int e = 0; e < FQ_RMAX; ++e) {
+    a[e] = s.A[rb + e];
+    v[e] = s.rhs[R.rc(h, e)];
+  }
+  asm volatile("" : "+v"(a[0]), "+v"(a[1]), "+v"(a[2]), "+v"(a[3]), "+v"(a[4]),
+                    "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]), "+v"(v[4]));
+  double acc = 0.0;
+#pragma unroll
+  for (int e = 0; e < FQ_RMAX; ++e) acc += a[e] * v[e];
+  return acc;
 }
 
 // scaling.c scale_data over the split storage (qp_device.h qp_scale, same order)
@@ -298,7 +337,7 @@ __device__ __forceinline__ void fq_update_info(FleetSmem &s, FleetRegs &R, doubl
   for (int h = 0; h < 2; ++h) {
     if (R.rok[h]) {  // dynamics row: (A x)_r
       double ax = 0.0;
-      _Pragma("unroll") for (int e = 0; e < FQ_RMAX; ++e) if (e < R.rn(h)) ax += s.A[R.rb(h) + e] * s.rhs[R.rc(h, e)];
+      _Pragma("unroll") for (int e = 0; e < FQ_RMAX; ++e) ax += s.A[R.rb(h) + e] * s.rhs[R.rc(h, e)];
       const double e = s.E[R.rr[h]], z = R.zr(h);
       v[0] = fmax(v[0], fabs((ax - z) / e));
       v[1] = fmax(v[1], fabs(z / e));
@@ -317,7 +356,7 @@ __device__ __forceinline__ void fq_update_info(FleetSmem &s, FleetRegs &R, doubl
         v[9] = fmax(v[9], fmax(fabs(z), fabs(ax)));
       }
       double aty = 0.0;  // (A' y)_j in CSC order, the bound row last
-      _Pragma("unroll") for (int e = 0; e < FQ_CMAX; ++e) if (e < R.cn[h]) aty += s.A[R.ca(h, e)] * s.zt[R.cr(h, e)];
+      _Pragma("unroll") for (int e = 0; e < FQ_CMAX; ++e) aty += s.A[R.ca(h, e)] * s.zt[R.cr(h, e)];
       aty += R.Ab[h] * R.yb[h];
       const double px = R.P[h] * R.x[h], d = R.D[h], q = R.q[h];
       v[3] = fmax(v[3], fabs((q + px + aty) / d));
@@ -376,7 +415,7 @@ __device__ __forceinline__ bool fq_primal_infeasible(FleetSmem &s, FleetRegs &R,
   for (int h = 0; h < 2; ++h)
     if (R.vok[h]) {
       double acc = 0.0;
-      _Pragma("unroll") for (int e = 0; e < FQ_CMAX; ++e) if (e < R.cn[h]) acc += s.A[R.ca(h, e)] * s.zt[R.cr(h, e)];
+      _Pragma("unroll") for (int e = 0; e < FQ_CMAX; ++e) acc += s.A[R.ca(h, e)] * s.zt[R.cr(h, e)];
       acc += R.Ab[h] * R.dyb[h];
       mx[0] = fmax(mx[0], fabs(acc / R.D[h]));
     }
@@ -417,7 +456,7 @@ __device__ __forceinline__ bool fq_dual_infeasible(FleetSmem &s, FleetRegs &R, d
   for (int h = 0; h < 2; ++h) {
     if (R.rok[h]) {
       double adx = 0.0;
-      _Pragma("unroll") for (int e = 0; e < FQ_RMAX; ++e) if (e < R.rn(h)) adx += s.A[R.rb(h) + e] * s.rhs[R.rc(h, e)];
+      _Pragma("unroll") for (int e = 0; e < FQ_RMAX; ++e) adx += s.A[R.rb(h) + e] * s.rhs[R.rc(h, e)];
       test(adx / s.E[R.rr[h]], R.ur(h), R.ur(h));
     }
     if (R.vok[h]) test((0.0 + R.Ab[h] * R.dx[h]) / s.E[FQ_MD + R.vj[h]], R.lb[h], R.ub[h]);
@@ -477,6 +516,10 @@ __device__ __forceinline__ QPResult fq_solve(const QPPattern &pt, FleetSmem &s, 
     R.lb[h] = fmax(R.lb[h], -QP_OSQP_INFTY); R.ub[h] = fmin(R.ub[h], QP_OSQP_INFTY);
     if (R.rok[h]) R.ur(h) = fmin(fmax(R.ur(h), -QP_OSQP_INFTY), QP_OSQP_INFTY);
   }
+  if (tid == 0) {  // the zero pads the padded column patterns point at (fq_init_pattern)
+    s.A[FQ_NNZD] = 0.0;
+    s.zt[FQ_MD] = 0.0;
+  }
   if (st.scaling) fq_scale(pt, s, R, st.scaling);
   else {
 #pragma unroll
@@ -504,7 +547,7 @@ __device__ __forceinline__ QPResult fq_solve(const QPPattern &pt, FleetSmem &s, 
     for (int h = 0; h < 2; ++h) {  // z = A x
       if (R.rok[h]) {
         double acc = 0.0;
-        _Pragma("unroll") for (int e = 0; e < FQ_RMAX; ++e) if (e < R.rn(h)) acc += s.A[R.rb(h) + e] * s.rhs[R.rc(h, e)];
+        _Pragma("unroll") for (int e = 0; e < FQ_RMAX; ++e) acc += s.A[R.rb(h) + e] * s.rhs[R.rc(h, e)];
         R.zr(h) = acc;
       }
       if (R.vok[h]) R.zb[h] = 0.0 + R.Ab[h] * R.x[h];
@@ -526,11 +569,11 @@ __device__ __forceinline__ QPResult fq_solve(const QPPattern &pt, FleetSmem &s, 
 #pragma unroll
     for (int h = 0; h < 2; ++h)
       if (R.vok[h]) {
-        double acc = 0.0;
-        _Pragma("unroll") for (int e = 0; e < FQ_CMAX; ++e) if (e < R.cn[h]) acc += s.A[R.ca(h, e)] * s.zt[R.cr(h, e)];
+        double acc = fq_col_dot(s, R, h);
         acc += R.Ab[h] * R.ztb[h];
         s.rhs[R.vj[h]] = sig * R.x[h] - R.q[h] + acc;
       }
+    T.mark(11);
     __syncthreads();
     T.mark(3);
     blk_solve_dispatch<FQ_FUSED_DIAG>(pt, s, s.rhs, &T, cw);  // x~ (wave cw)
@@ -557,8 +600,7 @@ __device__ __forceinline__ QPResult fq_solve(const QPPattern &pt, FleetSmem &s, 
         R.ztb[h] = rho * zn - yn;
       }
       if (R.rok[h]) {
-        double ztl = 0.0;
-        _Pragma("unroll") for (int e = 0; e < FQ_RMAX; ++e) if (e < R.rn(h)) ztl += s.A[R.rb(h) + e] * s.rhs[R.rc(h, e)];
+        const double ztl = fq_row_dot(s, R, h);
         const double rho = QP_RHO_EQ * rs, zo = R.zr(h), yo = R.yr(h);
         const double zr = al * ztl + (1.0 - al) * zo;
         double zn = zr + yo / rho;
@@ -569,6 +611,7 @@ __device__ __forceinline__ QPResult fq_solve(const QPPattern &pt, FleetSmem &s, 
         s.zt[R.rr[h]] = rho * zn - yn;
       }
     }
+    T.mark(12);
     __syncthreads();
     T.mark(5);
     can_check = st.check_termination && (it % st.check_termination == 0);
@@ -584,8 +627,12 @@ __device__ __forceinline__ QPResult fq_solve(const QPPattern &pt, FleetSmem &s, 
         __syncthreads();
         if (tid == 0) s.rho_s = est;
         __syncthreads();
-        f = fq_factor(pt, s, R, st.sigma, cw);
-        if (f) { res.factor_fail = f; return res; }
+        // at max_iter the loop ends here: rho_s persists and the next solve
+        // factors from scratch, so this factorisation would never be used
+        if (it < st.max_iter) {
+          f = fq_factor(pt, s, R, st.sigma, cw);
+          if (f) { res.factor_fail = f; return res; }
+        }
       }
     }
     if (can_check || adapt) fq_rebuild_zt(s, R);

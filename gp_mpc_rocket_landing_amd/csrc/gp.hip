@@ -231,6 +231,17 @@ static int core_cross(gpmpc_ctx *ctx, const GpCore &g, const double *dXq_raw, in
 }
 
 // ---------------------------------------------------------------------------
+// bump allocator over a persistent scratch slot (gp_append temporaries)
+struct ScratchCarve {
+  double *base;
+  size_t off = 0;
+  double *take(size_t count) { double *p = base + off; off += (count + 31) & ~(size_t)31; return p; }
+};
+struct ScratchPtr {
+  double *p;
+  template <class T> T *as() const { return reinterpret_cast<T *>(p); }
+};
+
 extern "C" int gpmpc_gp_fit_exact(gpmpc_ctx *ctx, int kind, const double *X, int n, int d,
                                   const double *Y, int n_out, const double *ls, double sigma2,
                                   double noise, gpmpc_gp **out, double *y_mean, double *y_std,
@@ -784,16 +795,19 @@ extern "C" int gpmpc_gp_append(gpmpc_ctx *ctx, gpmpc_gp *gp, const double *Xnew,
     return GPMPC_ERR_NOT_PD;
   }
   const int n = g.n, m = n + k, d = g.d, no = g.n_out;
-  DevBuf xr, xs, xn, Kt, Bt, Sm, dinfo, Li, C;
-  GPMPC_HIP(xr.alloc(sizeof(double) * k * d));
-  GPMPC_HIP(xs.alloc(sizeof(double) * k * d));
-  GPMPC_HIP(xn.alloc(sizeof(double) * k));
-  GPMPC_HIP(Kt.alloc(sizeof(double) * (size_t)k * n));
-  GPMPC_HIP(Bt.alloc(sizeof(double) * (size_t)k * n));
-  GPMPC_HIP(Sm.alloc(sizeof(double) * (size_t)k * k));
-  GPMPC_HIP(Li.alloc(sizeof(double) * (size_t)k * k));
-  GPMPC_HIP(C.alloc(sizeof(double) * (size_t)k * n));
-  GPMPC_HIP(dinfo.alloc(sizeof(int)));
+  // temporaries carved from persistent scratch (slot 4): a per-call hipMalloc /
+  // hipFree of each cost more than the O(n^2 k) arithmetic
+  const size_t need = 64 + 32 * 16 + (size_t)k * d * 2 + k + (size_t)k * n * 3 + (size_t)k * k * 2 +
+                      (size_t)m * no * 4 + no;
+  double *scr = (double *)gpmpc_scratch(4, sizeof(double) * need);
+  if (!scr) {
+    gpmpc_set_error("gp_append: out of device memory");
+    return -1;
+  }
+  ScratchCarve cv{scr};
+  ScratchPtr xr{cv.take((size_t)k * d)}, xs{cv.take((size_t)k * d)}, xn{cv.take(k)},
+      Kt{cv.take((size_t)k * n)}, Bt{cv.take((size_t)k * n)}, Sm{cv.take((size_t)k * k)},
+      Li{cv.take((size_t)k * k)}, C{cv.take((size_t)k * n)}, dinfo{cv.take(1)};
   GPMPC_HIP(hipMemcpyAsync(xr.p, Xnew, sizeof(double) * k * d, hipMemcpyHostToDevice, s));
   GPMPC_HIP(launch_scale_rows(s, xr.as<double>(), k, d, g.ls.as<double>(), g.kind == GPMPC_SE_ISO,
                               xs.as<double>(), xn.as<double>()));
@@ -820,17 +834,14 @@ extern "C" int gpmpc_gp_append(gpmpc_ctx *ctx, gpmpc_gp *gp, const double *Xnew,
   GPMPC_HIP(launch_trsm_lower_ex(s, k, k, Sm.as<double>(), k, Li.as<double>(), k, 0, 1, nullptr));
   GPMPC_HIP(launch_gemm_nn(s, k, n, n, Bt.as<double>(), n, g.W.as<double>(), n, C.as<double>(), n,
                            1.0, 0.0));
-  DevBuf L2, W2, Xs2, Xn2, yraw, yn, t, alpha, alphaT, dlml;
+  DevBuf L2, W2, Xs2, Xn2, alphaT;  // kept by the handle
+  ScratchPtr yraw{cv.take((size_t)m * no)}, yn{cv.take((size_t)m * no)}, t{cv.take((size_t)m * no)},
+      alpha{cv.take((size_t)m * no)}, dlml{cv.take(no)};
   GPMPC_HIP(L2.alloc(sizeof(double) * (size_t)m * m));
   GPMPC_HIP(W2.alloc(sizeof(double) * (size_t)(m + no) * m));
   GPMPC_HIP(Xs2.alloc(sizeof(double) * (size_t)m * d));
   GPMPC_HIP(Xn2.alloc(sizeof(double) * m));
-  GPMPC_HIP(yraw.alloc(sizeof(double) * (size_t)m * no));
-  GPMPC_HIP(yn.alloc(sizeof(double) * (size_t)m * no));
-  GPMPC_HIP(t.alloc(sizeof(double) * (size_t)m * no));
-  GPMPC_HIP(alpha.alloc(sizeof(double) * (size_t)m * no));
   GPMPC_HIP(alphaT.alloc(sizeof(double) * (size_t)no * m));
-  GPMPC_HIP(dlml.alloc(sizeof(double) * no));
   GPMPC_HIP(hipMemsetAsync(L2.p, 0, sizeof(double) * (size_t)m * m, s));
   GPMPC_HIP(hipMemsetAsync(W2.p, 0, sizeof(double) * (size_t)(m + no) * m, s));
   const size_t rowb = sizeof(double) * n;

@@ -16,7 +16,8 @@ struct gpmpc_ctx {
 
 void gpmpc_set_error(const char *fmt, ...);
 // persistent per-device scratch (slots: 0 trsm block inverses, 1 potrf 32x32 inverses,
-// 2 potrf 128x128 inverses, 3 batched-LML Gram/factor matrices)
+// 2 potrf 128x128 inverses, 3 batched-LML Gram/factor matrices, 4 gp_append temporaries;
+// slots 0..7)
 void *gpmpc_scratch(int slot, size_t bytes);
 
 #define GPMPC_HIP(call)                                                               \

@@ -111,6 +111,9 @@ __device__ __forceinline__ double dot_bcv(double src, const double *mul, std::in
 #ifndef QP_FAST_RECIP
 #define QP_FAST_RECIP 1
 #endif
+#ifndef QP_CHAIN_ROW0
+#define QP_CHAIN_ROW0 1
+#endif
 #ifndef QP_DOT_ASM
 #define QP_DOT_ASM 1
 #endif
@@ -269,6 +272,10 @@ __device__ __forceinline__ void blk_solve(const QPPattern &pt, S &s, double *b, 
   //      registers on the critical path) and the diagonal products run after
   //      it, four independent blocks per round, one per DPP row.
   if constexpr (!FUSED) {
+    // the chains need one 16-lane row: the other three rows would only
+    // replicate it, and their LDS operand reads would triple the chain's LDS
+    // traffic (the CU's LDS is shared by the four landings' chains)
+    if (!QP_CHAIN_ROW0 || row == 0) {
     double *pb = b + rs;
     const bool cpl = rr < CM;
     const double *pg = cpl ? F + SZ * SZ + rc : s.gzero;
@@ -303,6 +310,7 @@ __device__ __forceinline__ void blk_solve(const QPPattern &pt, S &s, double *b, 
       }
     }
     pb[0] = y;
+    }
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
     if (T) T->mark(8);
     // diagonal: u_k = S_k^-1 y_k, block 4t + row in round t.  Rows past the
@@ -396,7 +404,7 @@ __device__ __forceinline__ void blk_solve(const QPPattern &pt, S &s, double *b, 
   __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
   if (T) T->mark(9);
   // ---- backward: x_k = u_k + (-G_k)^T x_{k+1}
-  {
+  if (!QP_CHAIN_ROW0 || row == 0) {
     double *pb = b + (nblk - 1) * SZ + rs;        // block k+1 of b
     const double *pg = F + (nblk - 2) * BS + SZ * SZ + rs * CM;  // -G_k column rs
     double x = pb[0];

@@ -403,7 +403,7 @@ __device__ void qp_band_solve(const QPPattern &pt, S &s, double *b) {
 // diagnostic phase stamps (s_memtime), thread 0 only, enabled by a non-null pointer
 struct QPStamps {
   unsigned long long *out = nullptr;
-  unsigned long long acc[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+  unsigned long long acc[14] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
   unsigned long long last = 0, first = 0, rt0 = 0;
   __device__ __forceinline__ void start() {
     if (out && threadIdx.x == 0) {
@@ -420,7 +420,7 @@ struct QPStamps {
   }
   __device__ __forceinline__ void flush() {
     if (out && threadIdx.x == 0) {
-      for (int k = 0; k < 12; ++k) out[k] += acc[k];
+      for (int k = 0; k < 14; ++k) out[k] += acc[k];
       out[14] += __builtin_amdgcn_s_memrealtime() - rt0;  // 100 MHz constant clock
       out[15] += last - first;                            // shader clock
     }
@@ -695,8 +695,12 @@ __device__ QPResult qp_solve(const QPPattern &pt, S &s, const QPSettingsDev &st,
         if (tid == 0) s.rho_s = est;
         __syncthreads();
         qp_set_rho(pt, s);
-        f = qp_factor(pt, s, st.sigma);
-        if (f) { res.factor_fail = f; return res; }
+        // at max_iter the loop ends here: the new rho persists (the next solve
+        // factors from scratch), so this factorisation would never be used
+        if (it < st.max_iter) {
+          f = qp_factor(pt, s, st.sigma);
+          if (f) { res.factor_fail = f; return res; }
+        }
       }
     }
     if (can_check || adapt) {  // rebuild rho z - y (scratch reused / rho changed)

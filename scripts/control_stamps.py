@@ -15,11 +15,11 @@ from gp_mpc_rocket_landing_amd import _lib  # noqa: E402
 from gp_mpc_rocket_landing_amd.fleet import Fleet, fit_gp, initial_conditions  # noqa: E402
 
 
-def main(steps=4):
+def main(steps=4, B=1024):
     ctx = _lib.Context(0)
     gp = fit_gp(ctx, n_train=1000)
-    fl = Fleet(ctx, gp, 1024, horizon=20)
-    fl.reset(initial_conditions(1024))
+    fl = Fleet(ctx, gp, B, horizon=20)
+    fl.reset(initial_conditions(B))
     fl.step(3)
     st = torch.zeros(16, dtype=torch.int64, device="cuda")
     torch.cuda.synchronize()
@@ -31,13 +31,13 @@ def main(steps=4):
     s = st.cpu().numpy().astype(np.float64)
     it = rec1[0, 11] - rec0[0, 11]
     names = ["assembly", "scaling", "factor", "rhs", "kkt_solve(rest)", "update", "checks", "tail",
-             "kkt_forward", "kkt_diagonal", "kkt_backward", "slot11", "slot12", "slot13"]
+             "kkt_forward", "kkt_diagonal", "kkt_backward", "rhs_compute", "update_compute", "slot13"]
     tot = s[15]
-    print(f"landing 0: {steps} steps, {it:.0f} ADMM iterations, {tot:.0f} shader cycles "
+    print(f"B={B} landing 0: {steps} steps, {it:.0f} ADMM iterations, {tot:.0f} shader cycles "
           f"({s[14] / 100e6 * 1e6:.1f} us realtime)")
     for i, nm in enumerate(names):
         print(f"  {nm:10s} {s[i]:10.0f} cycles  {s[i] / tot * 100:5.1f}%  {s[i] / max(it, 1):8.0f} per iteration")
 
 
 if __name__ == "__main__":
-    main()
+    main(B=int(sys.argv[1]) if len(sys.argv) > 1 else 1024)
