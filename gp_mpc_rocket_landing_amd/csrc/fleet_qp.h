@@ -283,11 +283,37 @@ __device__ __forceinline__ void fq_scale(const QPPattern &pt, FleetSmem &s, Flee
 // (qp_device.h qp_factor, mode 1).  Diagonal slots are assembled by the owner
 // of their variable (its bound row is the slot's last term); the rest by all.
 __device__ __forceinline__ int fq_factor(const QPPattern &pt, FleetSmem &s, FleetRegs &R, double sigma,
-                                         int cw) {
+                                         int cw, QPStamps *T = nullptr) {
   constexpr int SZ = QP_BLK_SZ, BS = SZ * SZ + SZ * QP_BLK_CM;
   const int tid = threadIdx.x;
   const double rs = s.rho_s;
-  for (int e = tid; e < pt.fac_len; e += FQ_T) {
+  if (pt.n_offd >= 0) {
+    // zero every slot, then the listed non-diagonal slots (<= 3 terms each,
+    // packed in one int4, four items in flight per thread); same terms in the
+    // same order as the walk below
+    for (int e = tid; e < pt.fac_len; e += FQ_T) s.band_store[e] = 0.0;
+    __syncthreads();
+    const double re = QP_RHO_EQ * rs;
+    for (int i0 = tid; i0 < pt.n_offd; i0 += 4 * FQ_T) {
+      int4 it[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int i = i0 + u * FQ_T;
+        it[u] = i < pt.n_offd ? pt.offd[i] : make_int4(-1, 0, 0, 0);
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        if (it[u].x < 0) continue;
+        const int e = it[u].x & 0x7fff, nt = it[u].x >> 16;
+        double v = (it[u].x & 0x8000) ? 1.0 : 0.0;
+        if (nt > 0) v += re * s.A[it[u].y & 0xffff] * s.A[it[u].y >> 16];
+        if (nt > 1) v += re * s.A[it[u].z & 0xffff] * s.A[it[u].z >> 16];
+        if (nt > 2) v += re * s.A[it[u].w & 0xffff] * s.A[it[u].w >> 16];
+        s.band_store[e] = v;
+      }
+    }
+  }
+  for (int e = tid; pt.n_offd < 0 && e < pt.fac_len; e += FQ_T) {
     const int d = pt.facdiag[e];
     if (d >= 0) continue;
     double v = (d == -2) ? 1.0 : 0.0;
@@ -315,6 +341,7 @@ __device__ __forceinline__ int fq_factor(const QPPattern &pt, FleetSmem &s, Flee
   if (tid == 0) s.zslot = 0.0;
   if (tid < 64) s.gzero[tid] = 0.0;
   __syncthreads();
+  if (T) T->mark(13);
   int f = 0;
   if ((tid >> 6) == cw) f = blk_factor_dispatch(pt, s);
   if (tid == 0) s.flag = f;

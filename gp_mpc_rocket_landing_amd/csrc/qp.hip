@@ -121,7 +121,26 @@ int QPPatternHost::build(int n_, int m_, const int *rowptr, const int *colidx, h
     tv[3 * k + 2] = terms[k].b;
   }
   for (int e = 0; e < fac_len; ++e) facptr[e + 1] += facptr[e];
-  // one device block: rowptr | colidx | colptr | csc2csr | cscrow | facptr | facdiag | terms
+  // mode 1: the non-diagonal slots that are not plain zeros, one int4 each
+  // (QPPattern::offd), so the fleet's assembly reads one coalesced item per
+  // slot instead of walking facdiag / facptr / terms for every slot
+  std::vector<int> offd;
+  int n_offd = -1;
+  if (blk && fac_len < (1 << 15) && nnz < (1 << 16)) {
+    n_offd = 0;
+    for (int e = 0; e < fac_len && n_offd >= 0; ++e) {
+      if (facdiag[e] >= 0) continue;
+      const int k0 = facptr[e], k1 = facptr[e + 1], one = facdiag[e] == -2;
+      if (k1 == k0 && !one) continue;
+      if (k1 - k0 > 3) { n_offd = -1; break; }
+      int it[4] = {e | (one << 15) | ((k1 - k0) << 16), 0, 0, 0};
+      for (int k = k0; k < k1; ++k) it[1 + k - k0] = tv[3 * k + 1] | (tv[3 * k + 2] << 16);
+      offd.insert(offd.end(), it, it + 4);
+      ++n_offd;
+    }
+  }
+  if (n_offd < 0) offd.clear();
+  // one device block: rowptr | colidx | colptr | csc2csr | cscrow | facptr | facdiag | terms | offd
   std::vector<int> all;
   auto app = [&](const int *p, size_t k) { all.insert(all.end(), p, p + k); };
   const size_t o_rp = 0;
@@ -140,6 +159,9 @@ int QPPatternHost::build(int n_, int m_, const int *rowptr, const int *colidx, h
   app(facdiag.data(), facdiag.size());
   const size_t o_tv = all.size();
   app(tv.data(), tv.size());
+  while (all.size() % 4) all.push_back(0);  // int4 alignment (the buffer itself is 256-B aligned)
+  const size_t o_od = all.size();
+  app(offd.data(), offd.size());
   if (buf.alloc(sizeof(int) * all.size()) != hipSuccess) return -1;
   if (hipMemcpyAsync(buf.p, all.data(), sizeof(int) * all.size(), hipMemcpyHostToDevice, s) !=
           hipSuccess ||
@@ -150,6 +172,8 @@ int QPPatternHost::build(int n_, int m_, const int *rowptr, const int *colidx, h
   dev.rowptr = d + o_rp; dev.colidx = d + o_ci; dev.colptr = d + o_cp; dev.csc2csr = d + o_cm;
   dev.cscrow = d + o_cr; dev.facptr = d + o_bp; dev.facdiag = d + o_fd; dev.terms = d + o_tv;
   dev.mode = mode; dev.fac_len = fac_len; dev.nblk = nblk; dev.bsz = SZ; dev.bcm = CM;
+  dev.offd = reinterpret_cast<const int4 *>(d + o_od);
+  dev.n_offd = n_offd;
   return 0;
 }
 

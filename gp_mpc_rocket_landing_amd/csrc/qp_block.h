@@ -272,10 +272,10 @@ __device__ __forceinline__ void blk_solve(const QPPattern &pt, S &s, double *b, 
   //      registers on the critical path) and the diagonal products run after
   //      it, four independent blocks per round, one per DPP row.
   if constexpr (!FUSED) {
-    // the chains need one 16-lane row: the other three rows would only
-    // replicate it, and their LDS operand reads would triple the chain's LDS
-    // traffic (the CU's LDS is shared by the four landings' chains)
-    if (!QP_CHAIN_ROW0 || row == 0) {
+    // the chains need the SZ lanes of one 16-lane row: the other lanes would
+    // only replicate them, and their LDS operand reads would multiply the
+    // chain's LDS traffic (the CU's LDS is shared by the four landings' chains)
+    if (!QP_CHAIN_ROW0 || lane < SZ) {
     double *pb = b + rs;
     const bool cpl = rr < CM;
     const double *pg = cpl ? F + SZ * SZ + rc : s.gzero;
@@ -404,7 +404,7 @@ __device__ __forceinline__ void blk_solve(const QPPattern &pt, S &s, double *b, 
   __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
   if (T) T->mark(9);
   // ---- backward: x_k = u_k + (-G_k)^T x_{k+1}
-  if (!QP_CHAIN_ROW0 || row == 0) {
+  if (!QP_CHAIN_ROW0 || lane < SZ) {
     double *pb = b + (nblk - 1) * SZ + rs;        // block k+1 of b
     const double *pg = F + (nblk - 2) * BS + SZ * SZ + rs * CM;  // -G_k column rs
     double x = pb[0];

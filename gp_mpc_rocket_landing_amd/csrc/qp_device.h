@@ -52,6 +52,13 @@ struct QPPattern {
   const int *facptr;   // fac_len+1  slot -> term range
   const int *facdiag;  // fac_len    variable d whose P_d + sigma lands in the slot, -1 none, -2 one
   const int *terms;    // 3*nterms: (row, a, b) value pairs with rho_row*A[a]*A[b]
+  // mode 1, dynamics-row (rho_eq) slots only: one int4 per slot that is not a
+  // variable's diagonal and is either an identity pad or has terms:
+  // x = slot | pad-one << 15 | nterms << 16, y/z/w = its terms as a | b << 16.
+  // Every other non-diagonal slot is zero.  n_offd < 0: not available (a slot
+  // with more than 3 terms, or mode 0).
+  const int4 *offd;
+  int n_offd;
 };
 
 template <int NMAX, int MMAX, int NNZMAX, int W>
