@@ -326,16 +326,22 @@ __device__ __forceinline__ int fq_factor(const QPPattern &pt, FleetSmem &s, Flee
     }
     s.band_store[e] = v;
   }
+  // diagonal slot of variable j: P + sigma, then its terms in row order -- the
+  // dynamics rows of column j (the owner's column pattern; pads add re * 0 * 0)
+  // and last its bound row -- with no pattern reads
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
     if (!R.vok[h]) continue;
     const int j = R.vj[h], e = (j / SZ) * BS + (j % SZ) * (SZ + 1);
+    double a[FQ_CMAX];
+#pragma unroll
+    for (int k = 0; k < FQ_CMAX; ++k) a[k] = s.A[R.ca(h, k)];
+    asm volatile("" : "+v"(a[0]), "+v"(a[1]), "+v"(a[2]), "+v"(a[3]), "+v"(a[4]), "+v"(a[5]));
+    const double re = QP_RHO_EQ * rs;
     double v = R.P[h] + sigma;
-    for (int k = pt.facptr[e]; k < pt.facptr[e + 1]; ++k) {
-      const int r = pt.terms[3 * k], a = pt.terms[3 * k + 1], b = pt.terms[3 * k + 2];
-      if (r >= FQ_MD) v += fq_rho(R.lb[h], R.ub[h], rs) * R.Ab[h] * R.Ab[h];
-      else v += QP_RHO_EQ * rs * s.A[a] * s.A[b];
-    }
+#pragma unroll
+    for (int k = 0; k < FQ_CMAX; ++k) v += re * a[k] * a[k];
+    v += fq_rho(R.lb[h], R.ub[h], rs) * R.Ab[h] * R.Ab[h];
     s.band_store[e] = v;
   }
   if (tid == 0) s.zslot = 0.0;
