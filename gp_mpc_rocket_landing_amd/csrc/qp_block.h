@@ -27,6 +27,14 @@
 // than SZ is padded with identity rows by the host).
 #pragma once
 
+// accumulators of the KKT chains' block products (1, 2 or 4).  Measured on the
+// fleet control kernel: 1 and 2 within 0.3%, 4 is 2.4% slower -- with four
+// landings per CU the chains are bound by VALU issue, not by FMA latency, so
+// the fewest instructions (no closing adds) win
+#ifndef QP_CHAIN_ACC
+#define QP_CHAIN_ACC 1
+#endif
+
 // value of lane J of each 16-lane row, in every lane of that row
 template <int J>
 __device__ __forceinline__ double bc16(double v) {
@@ -76,9 +84,25 @@ __device__ __forceinline__ double dot_bc(double src, const double *mul, std::int
 template <int... J>
 __device__ __forceinline__ double dot_bc_init(double init, double src, const double *mul,
                                               std::integer_sequence<int, J...>) {
+#if QP_CHAIN_ACC == 4
+  // four accumulators: the chain's dependent depth is ceil(K/4) FMAs + 2 adds
+  // instead of ceil(K/2) + 1 (the sum order differs from the generic solver's)
+  double a0 = init, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+  ((J % 4 == 0   ? fmac_bc<J, J == 0>(a0, src, mul[J])
+    : J % 4 == 1 ? fmac_bc<J, false>(a1, src, mul[J])
+    : J % 4 == 2 ? fmac_bc<J, false>(a2, src, mul[J])
+                 : fmac_bc<J, false>(a3, src, mul[J])), ...);
+  return (a0 + a1) + (a2 + a3);
+#elif QP_CHAIN_ACC == 1
+  // one accumulator: K dependent FMAs, no closing add
+  double a0 = init;
+  (fmac_bc<J, J == 0>(a0, src, mul[J]), ...);
+  return a0;
+#else
   double a0 = init, a1 = 0.0;
   ((J % 2 == 0 ? fmac_bc<J, J == 0>(a0, src, mul[J]) : fmac_bc<J, false>(a1, src, mul[J])), ...);
   return a0 + a1;
+#endif
 }
 template <int K>
 __device__ __forceinline__ double dot_bc_init(double init, double src, const double *mul) {
