@@ -609,7 +609,7 @@ __device__ __forceinline__ QPResult fq_solve(const QPPattern &pt, FleetSmem &s, 
     T.mark(11);
     __syncthreads();
     T.mark(3);
-    blk_solve_dispatch<FQ_FUSED_DIAG>(pt, s, s.rhs, &T, cw);  // x~ (wave cw)
+    blk_solve_dispatch<FQ_FUSED_DIAG, FQ_NBLK>(pt, s, s.rhs, &T, cw);  // x~ (wave cw)
     __syncthreads();
     T.mark(4);
     const double rs = s.rho_s;

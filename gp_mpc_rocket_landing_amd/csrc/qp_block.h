@@ -28,11 +28,16 @@
 #pragma once
 
 // accumulators of the KKT chains' block products (1, 2 or 4).  Measured on the
-// fleet control kernel: 1 and 2 within 0.3%, 4 is 2.4% slower -- with four
-// landings per CU the chains are bound by VALU issue, not by FMA latency, so
-// the fewest instructions (no closing adds) win
+// fleet control kernel: 4 is 2.4% slower than 2 (more instructions on the
+// chain); 1 needs an s_nop between dependent DPP FMAs, so 2 it is
 #ifndef QP_CHAIN_ACC
-#define QP_CHAIN_ACC 1
+#define QP_CHAIN_ACC 2
+#endif
+// QP_CHAIN_PF2: operands two blocks ahead in the runtime-count forward chain
+// (measured 2.6% slower on the fleet: the extra index math costs more than the
+// LDS latency it hides)
+#ifndef QP_CHAIN_PF2
+#define QP_CHAIN_PF2 0
 #endif
 
 // value of lane J of each 16-lane row, in every lane of that row
@@ -265,7 +270,10 @@ __device__ __forceinline__ int blk_factor(const QPPattern &pt, S &s) {
 // rr >= SZ (never a broadcast source) read clamped addresses and only the
 // stores are masked.  Per-lane pointers advance by constants; operands sit at
 // immediate offsets.
-template <int SZ, int CM, bool FUSED = true, class S>
+//  NBC > 0: the block count is known at compile time (the fleet's N = 20
+//  MPC); when pt.nblk matches, the !FUSED chains run fully unrolled -- no loop
+//  counter, branch or pointer updates, every operand at an immediate offset.
+template <int SZ, int CM, bool FUSED = true, int NBC = 0, class S>
 __device__ __forceinline__ void blk_solve(const QPPattern &pt, S &s, double *b, QPStamps *T = nullptr, int cw = 0) {
   if ((int)(threadIdx.x >> 6) != cw) return;
   constexpr int BS = SZ * SZ + SZ * CM;
@@ -302,9 +310,60 @@ __device__ __forceinline__ void blk_solve(const QPPattern &pt, S &s, double *b, 
     if (!QP_CHAIN_ROW0 || lane < SZ) {
     double *pb = b + rs;
     const bool cpl = rr < CM;
+    if (NBC > 0 && nblk == NBC) {
+      // every lane reads a real -G row (rc is clamped to CM - 1); the
+      // non-coupled lanes then keep b_{k+1}, which is what their zero row gave
+      const double *pgu = F + SZ * SZ + rc;
+      double y = pb[0];
+      double g0[SZ], g1[SZ], c0, c1 = 0.0;
+#pragma unroll
+      for (int j = 0; j < SZ; ++j) g0[j] = pgu[j * CM];
+      c0 = pb[SZ];
+#pragma unroll
+      for (int k = 0; k < NBC - 1; ++k) {
+        double *gc = (k & 1) ? g1 : g0, *gn = (k & 1) ? g0 : g1;
+        double &cc = (k & 1) ? c1 : c0, &cn = (k & 1) ? c0 : c1;
+        if (k + 1 < NBC - 1) {
+#pragma unroll
+          for (int j = 0; j < SZ; ++j) gn[j] = pgu[(k + 1) * BS + j * CM];
+          cn = pb[(k + 2) * SZ];
+        }
+        const double yn = dot_bc_init<SZ>(cc, y, gc);
+        pb[k * SZ] = y;
+        y = cpl ? yn : cc;
+      }
+      pb[(NBC - 1) * SZ] = y;
+    } else {
     const double *pg = cpl ? F + SZ * SZ + rc : s.gzero;
     const int gstep = cpl ? BS : 0;
     double y = pb[0];
+#if QP_CHAIN_PF2
+    // operands two blocks ahead (three rotating sets): under four landings per
+    // CU an LDS read takes longer than one block product.  Step k reads G_k and
+    // b_{k+1}; the look-ahead index is clamped to the last step (no over-read).
+    double g0[SZ], g1[SZ], g2[SZ], c0, c1, c2;
+    auto ld = [&](double (&g)[SZ], double &c, int kk) {
+      const int kc = min(kk, nblk - 2);
+      const double *p = pg + kc * gstep;
+#pragma unroll
+      for (int j = 0; j < SZ; ++j) g[j] = p[j * CM];
+      c = pb[(kc + 1) * SZ];
+    };
+    ld(g0, c0, 0);
+    ld(g1, c1, 1);
+    for (int k = 0;;) {
+      ld(g2, c2, k + 2);
+      { const double yn = dot_bc_init<SZ>(c0, y, g0); pb[k * SZ] = y; y = yn; }
+      if (++k >= nblk - 1) break;
+      ld(g0, c0, k + 2);
+      { const double yn = dot_bc_init<SZ>(c1, y, g1); pb[k * SZ] = y; y = yn; }
+      if (++k >= nblk - 1) break;
+      ld(g1, c1, k + 2);
+      { const double yn = dot_bc_init<SZ>(c2, y, g2); pb[k * SZ] = y; y = yn; }
+      if (++k >= nblk - 1) break;
+    }
+    pb[(nblk - 1) * SZ] = y;
+#else
     double gA[SZ], gB[SZ];
     double bA = pb[SZ], bB;
 #pragma unroll
@@ -334,6 +393,8 @@ __device__ __forceinline__ void blk_solve(const QPPattern &pt, S &s, double *b, 
       }
     }
     pb[0] = y;
+#endif
+    }
     }
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
     if (T) T->mark(8);
@@ -428,7 +489,31 @@ __device__ __forceinline__ void blk_solve(const QPPattern &pt, S &s, double *b, 
   __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
   if (T) T->mark(9);
   // ---- backward: x_k = u_k + (-G_k)^T x_{k+1}
-  if (!QP_CHAIN_ROW0 || lane < SZ) {
+  if ((!QP_CHAIN_ROW0 || lane < SZ) && NBC > 0 && nblk == NBC && !FUSED) {
+    // fully unrolled (see NBC above): x_k = u_k + (-G_k)^T x_{k+1}, k = NBC-2..0
+    double *pb = b + rs;
+    const double *pgu = F + SZ * SZ + rs * CM;   // column rs of -G_k at k * BS
+    double x = pb[(NBC - 1) * SZ];
+    double g0[CM], g1[CM], u0, u1 = 0.0;
+#pragma unroll
+    for (int i = 0; i < CM; ++i) g0[i] = pgu[(NBC - 2) * BS + i];
+    u0 = pb[(NBC - 2) * SZ];
+#pragma unroll
+    for (int t = 0; t < NBC - 1; ++t) {
+      const int k = NBC - 2 - t;
+      double *gc = (t & 1) ? g1 : g0, *gn = (t & 1) ? g0 : g1;
+      double &uc = (t & 1) ? u1 : u0, &un = (t & 1) ? u0 : u1;
+      if (k > 0) {
+#pragma unroll
+        for (int i = 0; i < CM; ++i) gn[i] = pgu[(k - 1) * BS + i];
+        un = pb[(k - 1) * SZ];
+      }
+      const double xn = dot_bc_init<CM>(uc, x, gc);
+      pb[(k + 1) * SZ] = x;
+      x = xn;
+    }
+    pb[0] = x;
+  } else if (!QP_CHAIN_ROW0 || lane < SZ) {
     double *pb = b + (nblk - 1) * SZ + rs;        // block k+1 of b
     const double *pg = F + (nblk - 2) * BS + SZ * SZ + rs * CM;  // -G_k column rs
     double x = pb[0];
@@ -474,8 +559,8 @@ template <class S>
 __device__ __forceinline__ int blk_factor_dispatch(const QPPattern &pt, S &s) {
   return blk_factor<QP_BLK_SZ, QP_BLK_CM>(pt, s);
 }
-template <bool FUSED = true, class S>
+template <bool FUSED = true, int NBC = 0, class S>
 __device__ __forceinline__ void blk_solve_dispatch(const QPPattern &pt, S &s, double *b, QPStamps *T = nullptr,
                                    int cw = 0) {
-  blk_solve<QP_BLK_SZ, QP_BLK_CM, FUSED>(pt, s, b, T, cw);
+  blk_solve<QP_BLK_SZ, QP_BLK_CM, FUSED, NBC>(pt, s, b, T, cw);
 }
