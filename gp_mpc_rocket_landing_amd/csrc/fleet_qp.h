@@ -35,6 +35,11 @@
 #define FQ_FAC (FQ_NBLK * (QP_BLK_SZ * QP_BLK_SZ + QP_BLK_SZ * QP_BLK_CM) + 16)
 #define FQ_CMAX 6     // dynamics entries per column (<= 5) + 1
 #define FQ_RMAX 5     // entries per dynamics row
+#ifndef FQ_DIAG_SPLIT
+#define FQ_DIAG_SPLIT 1  // the KKT diagonal products on both waves (needs !FQ_FUSED_DIAG)
+#endif
+// LDS-only workgroup barrier (no wait on outstanding global memory operations)
+__device__ __forceinline__ void lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 #ifndef FQ_FUSED_DIAG
 #define FQ_FUSED_DIAG false  // block solve: G chain first, then the diagonal blocks 4 at a time
 #endif
@@ -609,7 +614,17 @@ __device__ __forceinline__ QPResult fq_solve(const QPPattern &pt, FleetSmem &s, 
     T.mark(11);
     __syncthreads();
     T.mark(3);
+#if FQ_DIAG_SPLIT
+    // x~: forward chain (wave cw), diagonal products (both waves, eight blocks
+    // a round), backward chain (wave cw), LDS-only barriers between
+    blk_solve_dispatch<false, FQ_NBLK, 1>(pt, s, s.rhs, &T, cw);
+    lds_sync();
+    blk_solve_dispatch<false, FQ_NBLK, 2>(pt, s, s.rhs, &T, cw);
+    lds_sync();
+    blk_solve_dispatch<false, FQ_NBLK, 4>(pt, s, s.rhs, &T, cw);
+#else
     blk_solve_dispatch<FQ_FUSED_DIAG, FQ_NBLK>(pt, s, s.rhs, &T, cw);  // x~ (wave cw)
+#endif
     __syncthreads();
     T.mark(4);
     const double rs = s.rho_s;

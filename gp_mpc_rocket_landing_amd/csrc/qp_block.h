@@ -273,9 +273,13 @@ __device__ __forceinline__ int blk_factor(const QPPattern &pt, S &s) {
 //  NBC > 0: the block count is known at compile time (the fleet's N = 20
 //  MPC); when pt.nblk matches, the !FUSED chains run fully unrolled -- no loop
 //  counter, branch or pointer updates, every operand at an immediate offset.
-template <int SZ, int CM, bool FUSED = true, int NBC = 0, class S>
+//  PH (!FUSED only): the phases run by this call, 1 forward | 2 diagonal |
+//  4 backward.  A PH == 2 call is made by BOTH waves of the workgroup (caller
+//  barriers around it): eight blocks per round, one per DPP row of either wave.
+template <int SZ, int CM, bool FUSED = true, int NBC = 0, int PH = 7, class S>
 __device__ __forceinline__ void blk_solve(const QPPattern &pt, S &s, double *b, QPStamps *T = nullptr, int cw = 0) {
-  if ((int)(threadIdx.x >> 6) != cw) return;
+  static_assert(!FUSED || PH == 7, "the fused solve runs all phases in one call");
+  if (PH != 2 && (int)(threadIdx.x >> 6) != cw) return;
   constexpr int BS = SZ * SZ + SZ * CM;
   // non-coupled lanes keep pg = gzero (gstep 0) and read gzero[j * CM], j < SZ
   static_assert((SZ - 1) * CM + 1 <= sizeof(s.gzero) / sizeof(double), "gzero too small");
@@ -285,6 +289,7 @@ __device__ __forceinline__ void blk_solve(const QPPattern &pt, S &s, double *b, 
   const int nblk = pt.nblk;
   const double *F = s.band();
   if (nblk == 1) {
+    if (!(PH & 1) || (int)(threadIdx.x >> 6) != cw) return;
     double sv[SZ];
 #pragma unroll
     for (int j = 0; j < SZ; ++j) sv[j] = F[j * SZ + rs];
@@ -304,6 +309,7 @@ __device__ __forceinline__ void blk_solve(const QPPattern &pt, S &s, double *b, 
   //      registers on the critical path) and the diagonal products run after
   //      it, four independent blocks per round, one per DPP row.
   if constexpr (!FUSED) {
+    if constexpr ((PH & 1) != 0) {
     // the chains need the SZ lanes of one 16-lane row: the other lanes would
     // only replicate them, and their LDS operand reads would multiply the
     // chain's LDS traffic (the CU's LDS is shared by the four landings' chains)
@@ -398,10 +404,15 @@ __device__ __forceinline__ void blk_solve(const QPPattern &pt, S &s, double *b, 
     }
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
     if (T) T->mark(8);
-    // diagonal: u_k = S_k^-1 y_k, block 4t + row in round t.  Rows past the
-    // last block read the last block (in bounds) and do not store.
-    const int nr = (nblk + 3) >> 2;
-    auto blk = [&](int t) { return min(4 * t + row, nblk - 1); };
+    }
+    if constexpr ((PH & 2) != 0) {
+    // diagonal: u_k = S_k^-1 y_k, block RB t + q in round t (q: this lane's
+    // DPP row, over both waves when PH == 2).  Rows past the last block read
+    // the last block (in bounds) and do not store.
+    constexpr int RB = PH == 2 ? 8 : 4;
+    const int q = PH == 2 ? (int)(threadIdx.x >> 4) : row;
+    const int nr = (nblk + RB - 1) / RB;
+    auto blk = [&](int t) { return min(RB * t + q, nblk - 1); };
     double sA[SZ], sB[SZ];
     {
       const double *ps = F + blk(0) * BS + rs;
@@ -417,7 +428,7 @@ __device__ __forceinline__ void blk_solve(const QPPattern &pt, S &s, double *b, 
         for (int j = 0; j < SZ; ++j) sB[j] = ps[j * SZ];
         yB = b[kn * SZ + rs];
         const double uv = dot_bc<SZ>(yA, sA);
-        if (4 * t + row < nblk) b[(4 * t + row) * SZ + rs] = uv;
+        if (RB * t + q < nblk) b[(RB * t + q) * SZ + rs] = uv;
         if (++t >= nr) break;
       }
       {
@@ -427,9 +438,10 @@ __device__ __forceinline__ void blk_solve(const QPPattern &pt, S &s, double *b, 
         for (int j = 0; j < SZ; ++j) sA[j] = ps[j * SZ];
         yA = b[kn * SZ + rs];
         const double uv = dot_bc<SZ>(yB, sB);
-        if (4 * t + row < nblk) b[(4 * t + row) * SZ + rs] = uv;
+        if (RB * t + q < nblk) b[(RB * t + q) * SZ + rs] = uv;
         if (++t >= nr) break;
       }
+    }
     }
   } else {
     double *pb = b + rs;                          // block k of b
@@ -488,6 +500,7 @@ __device__ __forceinline__ void blk_solve(const QPPattern &pt, S &s, double *b, 
   }
   __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
   if (T) T->mark(9);
+  if constexpr ((PH & 4) == 0) return;
   // ---- backward: x_k = u_k + (-G_k)^T x_{k+1}
   if ((!QP_CHAIN_ROW0 || lane < SZ) && NBC > 0 && nblk == NBC && !FUSED) {
     // fully unrolled (see NBC above): x_k = u_k + (-G_k)^T x_{k+1}, k = NBC-2..0
@@ -559,8 +572,8 @@ template <class S>
 __device__ __forceinline__ int blk_factor_dispatch(const QPPattern &pt, S &s) {
   return blk_factor<QP_BLK_SZ, QP_BLK_CM>(pt, s);
 }
-template <bool FUSED = true, int NBC = 0, class S>
+template <bool FUSED = true, int NBC = 0, int PH = 7, class S>
 __device__ __forceinline__ void blk_solve_dispatch(const QPPattern &pt, S &s, double *b, QPStamps *T = nullptr,
                                    int cw = 0) {
-  blk_solve<QP_BLK_SZ, QP_BLK_CM, FUSED, NBC>(pt, s, b, T, cw);
+  blk_solve<QP_BLK_SZ, QP_BLK_CM, FUSED, NBC, PH>(pt, s, b, T, cw);
 }
