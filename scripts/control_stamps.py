@@ -2,7 +2,8 @@
 control steps of the 1024-landing fleet (gpmpc_fleet_set_stamps: the stamped
 kernel instance).  Slots: 0 assembly, 1 scaling, 2 factor, 3 rhs, 4 KKT block
 solve (rest), 5 x/z/y update, 6 checks + adaptive rho, 7 plant + tail, 8-10 the
-KKT solve's forward chain / diagonal blocks / backward chain, 14 realtime
+KKT solve's forward chain / diagonal blocks / backward chain, 11/12 the rhs and
+update compute before their barriers, 14 realtime
 (100 MHz), 15 total shader cycles."""
 import os
 import sys
@@ -31,7 +32,7 @@ def main(steps=4, B=1024):
     s = st.cpu().numpy().astype(np.float64)
     it = rec1[0, 11] - rec0[0, 11]
     names = ["assembly", "scaling", "factor", "rhs", "kkt_solve(rest)", "update", "checks", "tail",
-             "kkt_forward", "kkt_diagonal", "kkt_backward", "rhs_compute", "update_compute", "slot13"]
+             "kkt_forward", "kkt_diagonal", "kkt_backward", "rhs_compute", "update_compute", "unused"]
     tot = s[15]
     print(f"B={B} landing 0: {steps} steps, {it:.0f} ADMM iterations, {tot:.0f} shader cycles "
           f"({s[14] / 100e6 * 1e6:.1f} us realtime)")
