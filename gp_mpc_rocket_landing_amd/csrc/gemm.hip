@@ -226,6 +226,15 @@ __global__ __launch_bounds__(256) void k_gemm_nt(int M, int N, int K, const doub
   }
 }
 
+// GPMPC_POST_XCD=1: the posterior GEMM's column-grouped XCD mapping (k_gemm128, tri_grid 2)
+static int post_xcd() {
+  static const int v = [] {
+    const char *e = getenv("GPMPC_POST_XCD");
+    return e ? atoi(e) : 0;
+  }();
+  return v;
+}
+
 // ---------------------------------------------------------------------------
 // Large-tile variant: 128 x 128 per workgroup, each wave a 64 x 64 quadrant
 // (4 x 4 MFMA blocks: 8 fragment reads feed 16 MFMAs), K staged 16 at a time,
@@ -249,7 +258,16 @@ __global__ __launch_bounds__(256, 2) void k_gemm128(int M, int N, int K, const d
   B += bz * sB_;
   C += bz * sC_;
   int by = tri_a ? (int)gridDim.y - 1 - (int)blockIdx.y : (int)blockIdx.y, bx = blockIdx.x;
-  if (tri_grid) tri_tile(blockIdx.x, by, bx);  // 1-D grid over the lower-triangular tiles
+  if (tri_grid == 1) tri_tile(blockIdx.x, by, bx);  // 1-D grid over the lower-triangular tiles
+  if (tri_grid == 2) {
+    // column-grouped: workgroup L runs on XCD L % 8; its m-th workgroup there
+    // takes column tile 8 (m / ny) + L % 8, row tile m % ny (longest first), so
+    // the ny row tiles of one K* column tile run together on one XCD and share
+    // its L2 (as do the W row tiles of the 8 column tiles in flight)
+    const int ny = gridDim.y, L = blockIdx.y * gridDim.x + blockIdx.x, m = L >> 3;
+    bx = (L & 7) + 8 * (m / ny);
+    by = tri_a ? ny - 1 - m % ny : m % ny;
+  }
   const int r0 = by * BT, c0 = bx * BT;
   if (lower_c && c0 > r0 + BT - 1) return;
   int kbeg = 0;
@@ -610,7 +628,8 @@ static hipError_t launch_gemm_impl(hipStream_t s, int epi, int M, int N, int K, 
                          (int)tg);
     else
       hipLaunchKernelGGL(k_gemm128<EPI_SUMSQ>, g, dim3(256), 0, s, M, N, K, A, lda, B, ldb, C, ldc,
-                         alpha, beta, tri_a, 0, sA, sB, sC, msum, Cm, ldm, 1, 0);
+                         alpha, beta, tri_a, 0, sA, sB, sC, msum, Cm, ldm, 1,
+                         (post_xcd() && batch == 1 && tx % 8 == 0) ? 2 : 0);
     return hipGetLastError();
   }
   const int tx = (N + GT - 1) / GT, ty = (M + GT - 1) / GT;
