@@ -92,6 +92,23 @@ __device__ __forceinline__ void fq_sum(double (&v)[K], double (*red)[16]) {
   __syncthreads();
 }
 
+// block-wide sum of a and max of b in one exchange (3 barriers instead of 6);
+// each tree is fq_sum's / fq_max's
+__device__ __forceinline__ void fq_sum_max(double &a, double &b, double (*red)[16]) {
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    a += __shfl_xor(a, o);
+    b = fmax(b, __shfl_xor(b, o));
+  }
+  __syncthreads();
+  if (lane == 0) { red[wv][0] = a; red[wv][1] = b; }
+  __syncthreads();
+  a = red[0][0] + red[1][0];
+  b = fmax(red[0][1], red[1][1]);
+  __syncthreads();
+}
+
 __device__ __forceinline__ double fq_rho(double l, double u, double rs) {
   if (l < -QP_OSQP_INFTY * QP_MIN_SCALING && u > QP_OSQP_INFTY * QP_MIN_SCALING) return QP_RHO_MIN;
   if (u - l < QP_RHO_TOL) return QP_RHO_EQ * rs;
@@ -219,15 +236,19 @@ __device__ __forceinline__ void fq_scale(const QPPattern &pt, FleetSmem &s, Flee
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       if (R.vok[h]) {
-        double v = fabs(R.P[h]);
-        _Pragma("unroll") for (int e = 0; e < FQ_CMAX; ++e) if (e < R.cn[h]) v = fmax(v, fabs(s.A[R.ca(h, e)]));
+        double v = fabs(R.P[h]);  // padded entries read the zero A[FQ_NNZD]: fmax(v, 0) = v
+        _Pragma("unroll") for (int e = 0; e < FQ_CMAX; ++e) v = fmax(v, fabs(s.A[R.ca(h, e)]));
         v = fmax(v, fabs(R.Ab[h]));
         s.rhs[R.vj[h]] = 1.0 / sqrt(qp_limit(v));
         eb[h] = 1.0 / sqrt(qp_limit(fmax(0.0, fabs(R.Ab[h]))));
       }
       if (R.rok[h]) {
-        double v = 0.0;
-        _Pragma("unroll") for (int e = 0; e < FQ_RMAX; ++e) if (e < R.rn(h)) v = fmax(v, fabs(s.A[R.rb(h) + e]));
+        double v = 0.0;  // all FQ_RMAX reads issue at once (in bounds); entries past the row count 0
+        const int rb = R.rb(h), rn = R.rn(h);
+        _Pragma("unroll") for (int e = 0; e < FQ_RMAX; ++e) {
+          const double a = fabs(s.A[rb + e]);
+          v = fmax(v, e < rn ? a : 0.0);
+        }
         s.zt[R.rr[h]] = 1.0 / sqrt(qp_limit(v));
       }
     }
@@ -262,8 +283,7 @@ __device__ __forceinline__ void fq_scale(const QPPattern &pt, FleetSmem &s, Flee
 #pragma unroll
     for (int h = 0; h < 2; ++h)
       if (R.vok[h]) mx[0] = fmax(mx[0], fabs(R.q[h]));
-    fq_sum<1>(v, s.red);  // (its barriers also order the A / rhs updates above)
-    fq_max<1>(mx, s.red);
+    fq_sum_max(v[0], mx[0], s.red);  // (its barriers also order the A / rhs updates above)
     double ct = v[0] / n;
     const double nq = qp_limit(mx[0]);
     ct = qp_limit(fmax(ct, nq));
