@@ -48,6 +48,9 @@ struct gpmpc_fleet {
   bool use_order = true;                     // GPMPC_FLEET_ORDER=0 launches in landing order
   bool use_fq = true;                        // fleet-specialised solver (GPMPC_FLEET_SOLVER=0: generic)
   int alt_wave = 0;                          // GPMPC_FLEET_ALTWAVE=1: alternate the chain wave
+  DevBuf claims;                             // per-CU chain-SIMD claims (k_fleet_control2)
+  unsigned epoch = 0;                        // control launches so far (claim generation)
+  bool simd_pick = true;                     // GPMPC_FLEET_SIMD=0: chain on wave 0 always
 };
 
 extern "C" int gpmpc_fleet_set_stamps(gpmpc_fleet *f, void *dev_u64x16) {
@@ -176,6 +179,8 @@ struct FleetArgs {
   int gp_by_slot;       // gmean rows follow the dispatch slot (order[]) instead of the landing
   const int *order;     // workgroup -> landing (longest predicted first), or null
   int alt_wave;         // fleet solver: odd workgroups run the KKT chain on wave 1
+  unsigned *claims;     // per-CU claimed chain SIMDs, (epoch << 8) | 4-bit mask (or null)
+  unsigned epoch;       // this launch's claim generation (never 0)
   int *lastit;          // ADMM iterations of each landing's last solve
   unsigned long long *stamps;  // diagnostic phase cycles of block 0 (or null)
   unsigned long long *trace;   // diagnostic per-landing placement/timing (or null)
@@ -421,8 +426,35 @@ __global__ __launch_bounds__(FQ_T) __attribute__((amdgpu_waves_per_eu(2, 2))) vo
   double *x = a.x + (int64_t)b * NX;
   double *Xw = a.Xw + (int64_t)b * (N + 1) * NX;
   double *Uw = a.Uw + (int64_t)b * N * NU;
+  // Chain wave: the two waves of a workgroup sit on two SIMDs, and the four
+  // workgroups of a CU fill each SIMD with two waves.  Two KKT chains on one
+  // SIMD slow both (the slowest landings, which set the kernel time, are the
+  // ones sharing), so each workgroup claims a SIMD of its CU for its chain:
+  // wave 0's if no earlier workgroup of this launch took it, else wave 1's.
+  __shared__ int s_simd1, s_cw;
+  if (a.claims && tid == 64) s_simd1 = (__builtin_amdgcn_s_getreg(4 | (31 << 11)) >> 4) & 3;
   if (tid < NX) sx[tid] = x[tid];
   __syncthreads();
+  if (tid == 0) {
+    int cw0 = a.alt_wave ? (int)(blockIdx.x & 1) : 0;
+    if (a.claims) {
+      const unsigned hw = __builtin_amdgcn_s_getreg(4 | (31 << 11));
+      const unsigned xcc = __builtin_amdgcn_s_getreg(20 | (31 << 11)) & 15;
+      const int s0 = (hw >> 4) & 3, s1 = s_simd1;
+      const unsigned key = (xcc << 8) | (((hw >> 13) & 7) << 5) | (((hw >> 12) & 1) << 4) | ((hw >> 8) & 15);
+      unsigned *cl = a.claims + key;
+      unsigned old = __hip_atomic_load(cl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      for (int tries = 0; tries < 16; ++tries) {  // bounded: contention is at most 4 workgroups
+        const unsigned mask = (old >> 8) == a.epoch ? (old & 15u) : 0u;
+        const int pick = !(mask & (1u << s0)) ? s0 : (!(mask & (1u << s1)) ? s1 : s0);
+        const unsigned nv = (a.epoch << 8) | mask | (1u << pick);
+        const unsigned prev = atomicCAS(cl, old, nv);
+        if (prev == old) { cw0 = pick == s0 ? 0 : 1; break; }
+        old = prev;
+      }
+    }
+    s_cw = cw0;
+  }
   if (tid == 0) {  // termination checks (monte_carlo.py:458-488), as k_fleet_control
     int out = 0;
     const double m0 = rec[13];
@@ -539,7 +571,7 @@ __global__ __launch_bounds__(FQ_T) __attribute__((amdgpu_waves_per_eu(2, 2))) vo
     }
   __syncthreads();
   T.mark(0);
-  QPResult res = fq_solve(a.pt, s, R, a.st, &T, a.alt_wave ? (int)(blockIdx.x & 1) : 0);
+  QPResult res = fq_solve(a.pt, s, R, a.st, &T, s_cw);
   T.mark(7);
   const bool has = !res.factor_fail && (res.status == 1 || res.status == 2 || res.status == -2);
   if (has) {
@@ -672,7 +704,8 @@ extern "C" int gpmpc_fleet_create(gpmpc_ctx *ctx, gpmpc_gp *gp, const gpmpc_flee
       f->Qn.alloc(sizeof(double) * P) || f->Ks.alloc(sizeof(double) * P * g.n) ||
       f->part.alloc(sizeof(double) * nrt * P) || f->meanT.alloc(sizeof(double) * 3 * P) ||
       f->mean.alloc(sizeof(double) * P * 3) || f->var.alloc(sizeof(double) * P * 3) ||
-      f->order.alloc(sizeof(int) * B) || f->lastit.alloc(sizeof(int) * B)) {
+      f->order.alloc(sizeof(int) * B) || f->lastit.alloc(sizeof(int) * B) ||
+      f->claims.alloc(sizeof(unsigned) * 4096)) {
     delete f;
     gpmpc_set_error("fleet: out of device memory");
     return -1;
@@ -682,6 +715,7 @@ extern "C" int gpmpc_fleet_create(gpmpc_ctx *ctx, gpmpc_gp *gp, const gpmpc_flee
   for (size_t b = 0; b < B; ++b) r[b * GPMPC_REC_LEN] = -1.0;
   hipMemcpyAsync(f->rec.p, r.data(), sizeof(double) * r.size(), hipMemcpyHostToDevice, ctx->stream);
   hipMemsetAsync(f->lastit.p, 0, sizeof(int) * B, ctx->stream);
+  hipMemsetAsync(f->claims.p, 0, sizeof(unsigned) * 4096, ctx->stream);
   {  // identity dispatch order until the first order kernel (every slot maps in range)
     std::vector<int> id(B);
     for (size_t b = 0; b < B; ++b) id[b] = (int)b;
@@ -692,6 +726,8 @@ extern "C" int gpmpc_fleet_create(gpmpc_ctx *ctx, gpmpc_gp *gp, const gpmpc_flee
   f->use_order = !oe || atoi(oe) != 0;
   const char *aw = getenv("GPMPC_FLEET_ALTWAVE");
   f->alt_wave = aw ? atoi(aw) != 0 : 0;
+  const char *sp = getenv("GPMPC_FLEET_SIMD");
+  f->simd_pick = !sp || atoi(sp) != 0;
   const char *se = getenv("GPMPC_FLEET_SOLVER");
   // the specialised solver assumes the N = 20 stage layout of its LDS caps
   f->use_fq = (!se || atoi(se) != 0) && N == 20 && f->pat.mode == 1 && f->pat.nblk == FQ_NBLK &&
@@ -816,6 +852,10 @@ static FleetArgs fleet_args(gpmpc_fleet *f) {
   a.gp_by_slot = f->use_order && f->cfg.use_gp;
   a.order = f->use_order ? f->order.as<int>() : nullptr;
   a.alt_wave = f->alt_wave;
+  a.claims = f->simd_pick ? f->claims.as<unsigned>() : nullptr;
+  f->epoch = (f->epoch + 1) & 0xffffff;
+  if (f->epoch == 0) f->epoch = 1;
+  a.epoch = f->epoch;
   a.lastit = f->lastit.as<int>();
   a.stamps = f->stamps;
   a.trace = f->trace;

@@ -66,7 +66,8 @@ def main(B=1024):
     for c in sorted(set(crowd)):
         m = (crowd == c) & (its == its.max())
         if m.any():
-            print(f"  chain-sharing {c}: {m.sum()} max-it landings, span {span[m].mean():.1f} us")
+            print(f"  chain-sharing {c}: {m.sum()} max-it landings, span {span[m].mean():.1f} us "
+                  f"(p90 {np.percentile(span[m], 90):.1f}, max {span[m].max():.1f})")
     # what sets the slow long landings apart: co-resident long landings, XCC, SE
     longs = its == its.max()
     cu_long = Counter(cu_key(d) for d, l in zip(w, longs) if l)
