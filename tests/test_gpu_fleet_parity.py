@@ -139,3 +139,26 @@ def test_fleet_full_run_compaction_is_exact(gpu_ctx):
     assert np.all(r1[:, REC_OUTCOME] != 0)                       # all terminated
     assert np.all((r1[:, REC_STEPS] >= 1) & (r1[:, REC_STEPS] <= 300))
     np.testing.assert_allclose(r1[:, REC_FUEL], r1[:, REC_M0] - x_1[:, 0], atol=1e-12)   # fuel = m0 - m
+
+
+def test_fleet_chain_simd_claim_is_exact(gpu_ctx):
+    """The chain-SIMD claim (k_fleet_control2 picks wave 0 or 1 for the KKT chain
+    so that no two chains share a SIMD) moves work between waves, never changes
+    it: records and states are bit-identical to the chain-always-on-wave-0 run."""
+    import os
+    from gp_mpc_rocket_landing_amd.fleet import Fleet, fit_gp, initial_conditions
+    gp = fit_gp(gpu_ctx, n_train=1000)
+    x0 = initial_conditions(1024)
+    out = {}
+    for pick in ("0", "1"):
+        os.environ["GPMPC_FLEET_SIMD"] = pick
+        try:
+            f = Fleet(gpu_ctx, gp, 1024)
+        finally:
+            os.environ.pop("GPMPC_FLEET_SIMD", None)
+        f.reset(x0)
+        f.step(20)
+        out[pick] = f.read()
+        f.close()
+    np.testing.assert_array_equal(out["1"][0], out["0"][0])
+    np.testing.assert_array_equal(out["1"][1], out["0"][1])
