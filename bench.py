@@ -453,11 +453,12 @@ def main():
                                 "gram_Kstar": "8 n P + 8 d (P+n) bytes",
                                 "post_finish": "8 P (row tiles + 9) bytes"}[dom],
                     traffic_source=pmc_traffic(d["kernel"])[1], launches_per_step=1)
+        ctl_limiter = ("latency: serial block-tridiagonal KKT chain, one chain wave per landing "
+                       "(each on its own SIMD), four landings per CU; ~10 KB of state in/out per "
+                       "landing-step, the rest of the measured traffic is register-spill scratch")
+        kern["qp_admm_plant"]["limiter"] = ctl_limiter
         if dom == "qp_admm_plant":
-            roof["limiter"] = ("latency: serial block-tridiagonal KKT chain, one chain wave per "
-                               "landing, four landings per CU; ~10 KB of state in/out per "
-                               "landing-step, the rest of the measured traffic is register-spill "
-                               "scratch")
+            roof["limiter"] = ctl_limiter
         out = {
             "metric": "GP-MPC control steps/sec (N=20, 1000 GP pts)",
             "value": round(steps_all / el_max, 2),
