@@ -51,6 +51,9 @@ struct gpmpc_fleet {
   DevBuf claims;                             // per-CU chain-SIMD claims (k_fleet_control2)
   unsigned epoch = 0;                        // control launches so far (claim generation)
   bool simd_pick = true;                     // GPMPC_FLEET_SIMD=0: chain on wave 0 always
+  bool fuse_post = true;                     // GPMPC_FLEET_FUSE_POST=0: separate k_post_finish
+  int64_t post_P = 0;                        // query rows / partial row tiles of the last
+  int post_nrt = 0;                          //   posterior GEMM (fused finish reads them)
 };
 
 extern "C" int gpmpc_fleet_set_stamps(gpmpc_fleet *f, void *dev_u64x16) {
@@ -179,6 +182,12 @@ struct FleetArgs {
   int gp_by_slot;       // gmean rows follow the dispatch slot (order[]) instead of the landing
   const int *order;     // workgroup -> landing (longest predicted first), or null
   int alt_wave;         // fleet solver: odd workgroups run the KKT chain on wave 1
+  // fused posterior finish (k_fleet_control2 only; null part: k_post_finish ran)
+  const double *part, *meanT, *ymean, *ystd;
+  double *mean_out, *var_out;
+  double sigma2;
+  int nrt;
+  int64_t pld;          // leading dimension of part / meanT (P)
   unsigned *claims;     // per-CU claimed chain SIMDs, (epoch << 8) | 4-bit mask (or null)
   unsigned epoch;       // this launch's claim generation (never 0)
   int *lastit;          // ADMM iterations of each landing's last solve
@@ -554,7 +563,22 @@ __global__ __launch_bounds__(FQ_T) __attribute__((amdgpu_waves_per_eu(2, 2))) vo
     bu[0] = b00 * tx + b01 * ty + b02 * tz;
     bu[1] = bu[2] = bu[3] = 0.0;
     bu[4] = bv * tx; bu[5] = bv * ty; bu[6] = bv * tz;
-    const double *gm = a.gmean + ((int64_t)(a.gp_by_slot ? (int)blockIdx.x : b) * N + k) * 3;
+    const int64_t q = (int64_t)(a.gp_by_slot ? (int)blockIdx.x : b) * N + k;  // query row
+    double gm[3];
+    if (a.part && a.use_gp) {
+      // the posterior finish of this landing's query (k_post_finish, same arithmetic)
+      double ss = 0.0;
+      for (int t = 0; t < a.nrt; ++t) ss += a.part[(int64_t)t * a.pld + q];
+      double lat = a.sigma2 - ss;
+      lat = lat > 1e-10 ? lat : 1e-10;
+      for (int c = 0; c < 3; ++c) {
+        gm[c] = a.meanT[(int64_t)c * a.pld + q] * a.ystd[c] + a.ymean[c];
+        a.mean_out[q * 3 + c] = gm[c];
+        a.var_out[q * 3 + c] = lat * a.ystd[c] * a.ystd[c];
+      }
+    } else {
+      for (int c = 0; c < 3; ++c) gm[c] = a.gmean[q * 3 + c];
+    }
     for (int i = 0; i < NX; ++i) {
       double c = (f[i] - ax[i]) - bu[i];
       if (a.use_gp && i >= 4) c += gm[i - 4] * dt;
@@ -728,6 +752,8 @@ extern "C" int gpmpc_fleet_create(gpmpc_ctx *ctx, gpmpc_gp *gp, const gpmpc_flee
   f->alt_wave = aw ? atoi(aw) != 0 : 0;
   const char *sp = getenv("GPMPC_FLEET_SIMD");
   f->simd_pick = !sp || atoi(sp) != 0;
+  const char *fp = getenv("GPMPC_FLEET_FUSE_POST");
+  f->fuse_post = !fp || atoi(fp) != 0;
   const char *se = getenv("GPMPC_FLEET_SOLVER");
   // the specialised solver assumes the N = 20 stage layout of its LDS caps
   f->use_fq = (!se || atoi(se) != 0) && N == 20 && f->pat.mode == 1 && f->pat.nblk == FQ_NBLK &&
@@ -796,7 +822,12 @@ static hipError_t fleet_gp_posterior(gpmpc_fleet *f, int mask) {
                                  f->meanT.as<double>(), P);
     if (e != hipSuccess) return e;
   }
-  if (mask & 8) {
+  if (mask & 4) {
+    f->post_P = P;
+    f->post_nrt = nrt;
+  }
+  // fused: k_fleet_control2 finishes each landing's own queries as it assembles
+  if ((mask & 8) && !(f->use_fq && f->fuse_post)) {
     e = launch_post_finish(s, P, 3, nrt, f->part.as<double>(), P, f->meanT.as<double>(), P,
                            g.ymean, g.ystd, g.sigma2, f->mean.as<double>(), f->var.as<double>());
   }
@@ -853,6 +884,19 @@ static FleetArgs fleet_args(gpmpc_fleet *f) {
   a.order = f->use_order ? f->order.as<int>() : nullptr;
   a.alt_wave = f->alt_wave;
   a.claims = f->simd_pick ? f->claims.as<unsigned>() : nullptr;
+  a.part = nullptr;
+  if (f->use_fq && f->fuse_post && f->cfg.use_gp && f->post_P > 0) {
+    const GpView g = gp_view(f->gp);
+    a.part = f->part.as<double>();
+    a.meanT = f->meanT.as<double>();
+    a.ymean = g.ymean;
+    a.ystd = g.ystd;
+    a.mean_out = f->mean.as<double>();
+    a.var_out = f->var.as<double>();
+    a.sigma2 = g.sigma2;
+    a.nrt = f->post_nrt;
+    a.pld = f->post_P;
+  }
   f->epoch = (f->epoch + 1) & 0xffffff;
   if (f->epoch == 0) f->epoch = 1;
   a.epoch = f->epoch;
