@@ -852,18 +852,57 @@ __global__ __launch_bounds__(1024) void k_fleet_order(int B, const double *__res
     if (rec[(int64_t)b * GPMPC_REC_LEN] != 0.0) return 0;
     return min(lastit[b], ORDER_BUCKETS - 2) + 1;
   };
-  for (int b = threadIdx.x; b < B; b += blockDim.x) atomicAdd(&cnt[key(b)], 1);
-  __syncthreads();
-  if (threadIdx.x == 0) {  // descending exclusive scan
-    int run = 0;
-    for (int k = ORDER_BUCKETS - 1; k >= 0; --k) {
-      const int c = cnt[k];
-      cnt[k] = run;
-      run += c;
+  // Wave-aggregated LDS atomics: nearly every landing sits in one of two or
+  // three buckets (25 / 50 iterations, terminated), and per-lane atomics on one
+  // LDS word serialise.  Each wave adds once per distinct key it holds; lanes
+  // take base + their rank among the wave's lanes with that key.
+  const int lane = threadIdx.x & 63;
+  auto wave_add = [&](int k, bool active) {
+    int slot = 0;
+    unsigned long long todo = __ballot(active);
+    while (todo) {
+      const int leader = __ffsll((long long)todo) - 1;
+      const int lk = __shfl(k, leader);
+      const unsigned long long same = __ballot(active && k == lk);
+      int base = 0;
+      if (lane == leader) base = atomicAdd(&cnt[lk], __popcll(same));
+      base = __shfl(base, leader);
+      if (active && k == lk) slot = base + __popcll(same & ((1ull << lane) - 1));
+      todo &= ~same;
     }
+    return slot;
+  };
+  for (int b0 = 0; b0 < B; b0 += blockDim.x) {
+    const int b = b0 + threadIdx.x;
+    wave_add(b < B ? key(b) : 0, b < B);
   }
   __syncthreads();
-  for (int b = threadIdx.x; b < B; b += blockDim.x) order[atomicAdd(&cnt[key(b)], 1)] = b;
+  // descending exclusive scan over the buckets, 256 threads (4 waves, shuffles)
+  static_assert(ORDER_BUCKETS == 256, "scan is laid out for 256 buckets");
+  __shared__ int wsum[4];
+  int c = 0, inc = 0;
+  if (threadIdx.x < ORDER_BUCKETS) {
+    c = cnt[ORDER_BUCKETS - 1 - threadIdx.x];
+    inc = c;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int t = __shfl_up(inc, o);
+      if (lane >= o) inc += t;
+    }
+    if (lane == 63) wsum[threadIdx.x >> 6] = inc;
+  }
+  __syncthreads();
+  if (threadIdx.x < ORDER_BUCKETS) {
+    int pre = 0;
+    for (int w = 0; w < (int)(threadIdx.x >> 6); ++w) pre += wsum[w];
+    cnt[ORDER_BUCKETS - 1 - threadIdx.x] = pre + inc - c;
+  }
+  __syncthreads();
+  for (int b0 = 0; b0 < B; b0 += blockDim.x) {
+    const int b = b0 + threadIdx.x;
+    const int slot = wave_add(b < B ? key(b) : 0, b < B);
+    if (b < B) order[slot] = b;
+  }
 }
 
 static FleetArgs fleet_args(gpmpc_fleet *f) {
