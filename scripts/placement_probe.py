@@ -2,7 +2,9 @@
 1024-landing fleet, the HW_ID (SIMD, CU, SE, XCC) of its two waves and its
 start/end realtime, over one control step; prints how many KKT-chain waves
 share a SIMD and how the per-landing span relates to its ADMM iterations.
-GPMPC_FLEET_ALTWAVE=1 runs the chain on wave (workgroup & 1)."""
+GPMPC_FLEET_ALTWAVE=1 runs the chain on wave (workgroup & 1).  The chain-sharing
+lines assume the chain wave is 0 (or alternates): run with GPMPC_FLEET_SIMD=0 for
+them, since by default each workgroup claims its chain SIMD at run time."""
 import os
 import sys
 from collections import Counter
