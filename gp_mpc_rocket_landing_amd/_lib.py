@@ -116,6 +116,7 @@ _sig("gpmpc_syrk_batched_dev", _c, _vp, _c, _c, _c, _vp, _c, ctypes.c_int64, _vp
 _sig("gpmpc_cov_propagate", _c, _vp, _c, _c, _c, _dp, _dp, _vp, ctypes.c_double, _dp)
 _sig("gpmpc_cov_propagate_dev", _c, _vp, _c, _c, _c, _vp, _vp, _vp, ctypes.c_double, _vp)
 _sig("gpmpc_fleet_read", _c, _vp, _dp, _dp)
+_sig("gpmpc_fleet_get_state", _c, _vp, _dp, _dp, _dp, _dp)
 _sig("gpmpc_fleet_records_dev", _vp, _vp)
 _sig("gpmpc_fleet_destroy", _c, _vp)
 
@@ -127,7 +128,7 @@ EXPORTED = ["gpmpc_abi_version", "gpmpc_last_error", "gpmpc_ctx_create", "gpmpc_
             "gpmpc_fitc_fit", "gpmpc_fitc_predict", "gpmpc_fitc_destroy",
             "gpmpc_qp_default_settings", "gpmpc_qp_solve_batched", "gpmpc_fleet_default_config",
             "gpmpc_fleet_create", "gpmpc_fleet_reset", "gpmpc_fleet_step", "gpmpc_fleet_read",
-            "gpmpc_fleet_step_phases", "gpmpc_fleet_set_stamps", "gpmpc_fleet_set_trace",
+            "gpmpc_fleet_step_phases", "gpmpc_fleet_get_state", "gpmpc_fleet_set_stamps", "gpmpc_fleet_set_trace",
             "gpmpc_syrk_batched_dev", "gpmpc_cov_propagate", "gpmpc_cov_propagate_dev",
             "gpmpc_fleet_records_dev", "gpmpc_fleet_destroy"]
 
@@ -367,20 +368,38 @@ class FITCHandle:
             pass
 
 
+def _field_names(struct):
+    return {f[0] for f in struct._fields_}
+
+
+def set_fields(struct, kw, nested=None):
+    """Assign keyword settings to a ctypes struct, refusing names it does not
+    have (ctypes would silently accept a typo such as ``max_iters``).  Keys
+    unknown to ``struct`` go to the ``nested`` member struct when given."""
+    own = _field_names(type(struct))
+    sub = getattr(struct, nested) if nested else None
+    subn = _field_names(type(sub)) if sub is not None else set()
+    for k, v in kw.items():
+        if k in own and k != nested:
+            setattr(struct, k, v)
+        elif k in subn:
+            setattr(sub, k, v)
+        else:
+            raise TypeError(f"unknown setting {k!r} for {type(struct).__name__}")
+    return struct
+
+
 def qp_default_settings(**kw):
     s = QPSettings()
     _L.gpmpc_qp_default_settings(ctypes.byref(s))
-    for k, v in kw.items():
-        setattr(s, k, v)
-    return s
+    return set_fields(s, kw)
 
 
 def fleet_default_config(**kw):
+    """Fleet config; QP settings may be given flat (``max_iter=...``)."""
     c = FleetConfig()
     _L.gpmpc_fleet_default_config(ctypes.byref(c))
-    for k, v in kw.items():
-        setattr(c, k, v)
-    return c
+    return set_fields(c, kw, nested="qp")
 
 
 class QPWorkspace:

@@ -1005,6 +1005,20 @@ extern "C" int gpmpc_fleet_read(gpmpc_fleet *f, double *records, double *x) {
   return 0;
 }
 
+extern "C" int gpmpc_fleet_get_state(gpmpc_fleet *f, double *Xw, double *Uw, double *y_scaled,
+                                     double *rho) {
+  GPMPC_CHECK_ARG(f);
+  hipStream_t s = f->ctx->stream;
+  const size_t B = (size_t)f->B, N = (size_t)f->N;
+  if (Xw) GPMPC_HIP(hipMemcpyAsync(Xw, f->Xw.p, sizeof(double) * B * (N + 1) * NX, hipMemcpyDeviceToHost, s));
+  if (Uw) GPMPC_HIP(hipMemcpyAsync(Uw, f->Uw.p, sizeof(double) * B * N * NU, hipMemcpyDeviceToHost, s));
+  if (y_scaled)
+    GPMPC_HIP(hipMemcpyAsync(y_scaled, f->ysc.p, sizeof(double) * B * f->m, hipMemcpyDeviceToHost, s));
+  if (rho) GPMPC_HIP(hipMemcpyAsync(rho, f->rho.p, sizeof(double) * B, hipMemcpyDeviceToHost, s));
+  GPMPC_HIP(hipStreamSynchronize(s));
+  return 0;
+}
+
 extern "C" double *gpmpc_fleet_records_dev(gpmpc_fleet *f) { return f ? f->rec.as<double>() : nullptr; }
 
 extern "C" int gpmpc_fleet_destroy(gpmpc_fleet *f) {

@@ -35,12 +35,7 @@ class Fleet:
     def __init__(self, ctx, gp, batch, **config):
         self.ctx = ctx
         self.gp = gp  # keep the GP alive: the fleet reads its device factor
-        self.cfg = _lib.fleet_default_config()
-        for k, v in config.items():
-            if hasattr(self.cfg, k):
-                setattr(self.cfg, k, v)
-            else:
-                setattr(self.cfg.qp, k, v)
+        self.cfg = _lib.fleet_default_config(**config)
         self.batch = int(batch)
         h = ctypes.c_void_p()
         _lib._chk(_lib._L.gpmpc_fleet_create(ctx.h, gp.h, ctypes.byref(self.cfg), self.batch,
@@ -61,6 +56,17 @@ class Fleet:
         rec = np.empty((self.batch, _lib.REC_LEN)); x = np.empty((self.batch, 7))
         _lib._chk(_lib._L.gpmpc_fleet_read(self.h, _lib._d(rec), _lib._d(x)), "fleet_read")
         return rec, x
+
+    def state(self):
+        """Every landing's full controller state: x, records, the linearisation /
+        warm-start trajectory Xw, Uw, the ADMM's persistent scaled duals and rho."""
+        rec, x = self.read()
+        B, N = self.batch, int(self.cfg.horizon)
+        m = 7 * (N + 1) + 10 * N + 7
+        Xw = np.empty((B, N + 1, 7)); Uw = np.empty((B, N, 3)); y = np.empty((B, m)); rho = np.empty(B)
+        _lib._chk(_lib._L.gpmpc_fleet_get_state(self.h, _lib._d(Xw), _lib._d(Uw), _lib._d(y),
+                                                _lib._d(rho)), "fleet_get_state")
+        return dict(rec=rec, x=x, Xw=Xw, Uw=Uw, y=y, rho=rho)
 
     @property
     def records_dev(self):

@@ -207,6 +207,11 @@ int gpmpc_fleet_step_phases(gpmpc_fleet *f, int phase_mask);
  * 13 initial mass, 14 last QP status, 15 last rho */
 #define GPMPC_REC_LEN 16
 int gpmpc_fleet_read(gpmpc_fleet *f, double *records, double *x /* batch x 7, may be NULL */);
+/* the rest of every landing's controller state, any pointer may be NULL:
+ * linearisation / warm-start trajectory Xw (batch x (N+1) x 7) and Uw
+ * (batch x N x 3), the ADMM's persistent scaled duals (batch x m) and rho
+ * (batch) -- what OSQP keeps between solves (osqp_rti.py:517-527) */
+int gpmpc_fleet_get_state(gpmpc_fleet *f, double *Xw, double *Uw, double *y_scaled, double *rho);
 /* diagnostic: accumulate s_memtime cycles of landing 0's control kernel per
  * phase into dev_u64x16 (16 x uint64 device buffer; NULL disables):
  * 0 assembly, 1 scaling, 2 factor, 3 A' rhs, 4 KKT solve (band path, or the

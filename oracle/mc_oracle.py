@@ -72,3 +72,102 @@ def incremental_target(x):
     t[4:7] = 0.0
     t[1] = max(0.5, x[1] - 2.0)
     return t
+
+
+
+REC_LEN = 16  # the fleet's record layout (include/gpmpc.h GPMPC_REC_LEN)
+
+
+def new_landing(x0, horizon=20):
+    """Controller + loop state at the start of MonteCarloSimulator.run_single
+    (monte_carlo.py:418-433): the first incremental target, the RTI guess of
+    osqp_rti.py:425-446 and OSQP's fresh rho / y.  Dict keys follow the fleet
+    (Fleet.state()): x, Xw, Uw, y (scaled), rho, rec."""
+    from . import admm_ref, qp_oracle
+    x = np.array(x0, float)
+    Xw, Uw = qp_oracle.initial_guess(x, incremental_target(x), horizon)
+    m = qp_oracle.N_X * (horizon + 1) + qp_oracle.n_vars(horizon)
+    rho0 = admm_ref.default_settings().rho
+    rec = np.zeros(REC_LEN)
+    rec[4:11] = x
+    rec[13] = x[0]
+    return dict(x=x, Xw=Xw, Uw=Uw, y=np.zeros(m), rho=rho0, rec=rec)
+
+
+def landing_step(st, S, max_steps=300, dt=0.1, cfg=RUN_EXPERIMENTS_CFG, use_gp=True,
+                 residual_model=True):
+    """One pass of the run_single loop body (monte_carlo.py:455-537) under the
+    solve protocol (:495-512) with the 3-DoF GPMPC adapter as the controller,
+    from the full state S (new_landing / Fleet.state() layout).  Returns the
+    next state; rec[0] != 0 once the landing has terminated:
+
+    * the loop's ``else`` (:539-542): TIMEOUT once max_steps steps ran;
+    * the checks at the top of the step (:455-488): crash, fuel, divergence,
+      landing check -> SUCCESS / CONSTRAINT_VIOLATION;
+    * the incremental target (:497-500), GP mean at the horizon points of the
+      shifted previous plan (exact_gp.py:213-268), the RTI QP with
+      x+ = A x + B u + c (gp_mpc.py:410-411 sign), the C OSQP-0.6 restatement
+      warm-started from the plan with OSQP's persistent rho / scaled y;
+    * a solve without a solution -> DIVERGENCE (:506-508);
+    * plant step with the pre-step drag residual, plan shifted (X[1:], X[-1]).
+
+    Also returns (iterations, status) of the solve, or None at termination.
+    """
+    from . import admm_ref, gp_oracle, qp_oracle
+
+    x = S["x"].copy(); Xw = S["Xw"].copy(); Uw = S["Uw"].copy(); rec = S["rec"].copy()
+    N = Uw.shape[0]
+    m0 = rec[13]
+    out = dict(x=x, Xw=Xw, Uw=Uw, y=S["y"].copy(), rho=float(S["rho"]), rec=rec)
+    if rec[0] != 0:
+        return out, None
+    o = TIMEOUT if rec[1] >= max_steps else pre_step_outcome(x, m0, cfg)
+    if o:
+        rec[0] = o
+        rec[2] = m0 - x[0]
+        rec[4:11] = x
+        return out, None
+    tgt = incremental_target(x)
+    mean = None
+    if use_gp:
+        mean, _var = gp_oracle.exact_predict(st, gp_oracle.features_3dof(Xw[:-1], Uw))
+    P0, q = qp_oracle.cost(N, np.tile(tgt, (N + 1, 1)))
+    A, l, u = qp_oracle.constraints(Xw, Uw, x, dt, gp_dv=mean, sign=-1.0, filter_small=False)
+    qp = admm_ref.RefQP(len(out["y"]))
+    qp.y = out["y"]; qp.rho = np.array([out["rho"]])
+    try:
+        r = qp.solve(P0.diagonal(), q, A, l, u, qp_oracle.to_vector(Xw, Uw))
+    except RuntimeError:  # reduced KKT not positive definite: the device's factor_fail
+        rec[0] = DIVERGENCE; rec[14] = -100; rec[2] = m0 - x[0]; rec[4:11] = x
+        return out, (0, -100)
+    if r["status"] not in (1, 2, -2):   # MPCSolution.success False -> DIVERGENCE
+        rec[0] = DIVERGENCE; rec[14] = r["status"]; rec[2] = m0 - x[0]; rec[4:11] = x
+        return out, (r["iter"], r["status"])
+    Xo, Uo = qp_oracle.from_vector(r["x"], N)
+    dr = qp_oracle.drag_residual(x) if residual_model else np.zeros(3)
+    xn = qp_oracle.plant_step(x, Uo[0], dt)
+    xn[4:7] += dr * dt
+    out.update(x=xn, Xw=np.vstack([Xo[1:], Xo[-1:]]), Uw=np.vstack([Uo[1:], Uo[-1:]]),
+               y=qp.y, rho=float(qp.rho[0]))
+    rec[1] += 1
+    rec[2] = m0 - xn[0]
+    rec[3] = rec[1] * dt
+    rec[4:11] = xn
+    rec[11] += r["iter"]
+    rec[12] += r["status"] == 1
+    rec[14] = r["status"]
+    rec[15] = qp.rho[0]
+    return out, (r["iter"], r["status"])
+
+
+def closed_loop_landing(st, x0, max_steps=300, horizon=20, **kw):
+    """MonteCarloSimulator.run_single (monte_carlo.py:401-583), flown to
+    termination by repeated landing_step.  Returns (record (16,), final state,
+    per-step list of (iterations, status))."""
+    S = new_landing(x0, horizon)
+    trace = []
+    while S["rec"][0] == 0:
+        S, info = landing_step(st, S, max_steps=max_steps, **kw)
+        if info is not None:
+            trace.append(info)
+    return S["rec"], S["x"], trace
