@@ -116,12 +116,13 @@ _sig("gpmpc_syrk_batched_dev", _c, _vp, _c, _c, _c, _vp, _c, ctypes.c_int64, _vp
 _sig("gpmpc_cov_propagate", _c, _vp, _c, _c, _c, _dp, _dp, _vp, ctypes.c_double, _dp)
 _sig("gpmpc_cov_propagate_dev", _c, _vp, _c, _c, _c, _vp, _vp, _vp, ctypes.c_double, _vp)
 _sig("gpmpc_fleet_read", _c, _vp, _dp, _dp)
+_sig("gpmpc_gram_grad", _c, _vp, _c, _dp, _c, _dp, _c, _c, _dp, ctypes.c_double, _dp, _dp)
 _sig("gpmpc_fleet_get_state", _c, _vp, _dp, _dp, _dp, _dp)
 _sig("gpmpc_fleet_records_dev", _vp, _vp)
 _sig("gpmpc_fleet_destroy", _c, _vp)
 
 EXPORTED = ["gpmpc_abi_version", "gpmpc_last_error", "gpmpc_ctx_create", "gpmpc_ctx_destroy",
-            "gpmpc_ctx_sync", "gpmpc_ctx_stream", "gpmpc_gram", "gpmpc_potrf",
+            "gpmpc_ctx_sync", "gpmpc_ctx_stream", "gpmpc_gram", "gpmpc_gram_grad", "gpmpc_potrf",
             "gpmpc_potrf_batched_dev", "gpmpc_trsm_lower", "gpmpc_potrs", "gpmpc_gp_fit_exact",
             "gpmpc_gp_predict", "gpmpc_gp_predict_cov", "gpmpc_gp_get_state", "gpmpc_gp_destroy",
             "gpmpc_gp_lml_batched", "gpmpc_gp_append",
@@ -215,6 +216,21 @@ def gram(ctx, kind, X1, X2, ls, sigma2):
     K = np.empty((n1, n2))
     _chk(_L.gpmpc_gram(ctx.h, kind, _d(X1), n1, _d(X2), n2, d, _d(ls), float(sigma2), _d(K), n2), "gram")
     return K
+
+
+def gram_grad(ctx, kind, X1, X2, ls, sigma2):
+    """(K, G): the Gram and its log-hyperparameter gradients (gpmpc_gram_grad):
+    G (d, n1, n2) for SE_ARD, (1, n1, n2) for SE_ISO."""
+    X1 = f64(np.atleast_2d(X1)); n1, d = X1.shape
+    ls = f64(np.atleast_1d(ls))
+    if ls.size == 1 and kind != SE_ISO:
+        ls = np.full(d, float(ls[0]))
+    X2a = None if X2 is None else f64(np.atleast_2d(X2))
+    n2 = n1 if X2a is None else X2a.shape[0]
+    K = np.empty((n1, n2)); G = np.empty((1 if kind == SE_ISO else d, n1, n2))
+    _chk(_L.gpmpc_gram_grad(ctx.h, kind, _d(X1), n1, None if X2a is None else _d(X2a), n2, d, _d(ls),
+                            float(sigma2), _d(K), _d(G)), "gram_grad")
+    return K, G
 
 
 def potrf(ctx, A):
@@ -421,14 +437,23 @@ class QPWorkspace:
         self.rho = np.full(self.batch, float(self.settings.rho))
         self.y_scaled = np.zeros((self.batch, self.m))
 
-    def solve(self, Aval, Pdiag, q, l, u, x_ws=None):
+    def solve(self, Aval, Pdiag, q, l, u, x_ws=None, pattern=None):
+        """``pattern`` = (rowptr, colidx) replaces the workspace's pattern for this
+        solve (a value-filtered A whose non-zeros move); the rows, and
+        with them OSQP's persistent y, stay the same."""
         B, n, m = self.batch, self.n, self.m
-        Av = f64(np.reshape(Aval, (B, self.nnz))); Pd = f64(np.reshape(Pdiag, (B, n)))
+        rowptr, colidx = self.rowptr, self.colidx
+        if pattern is not None:
+            rowptr = np.ascontiguousarray(pattern[0], np.int32)
+            colidx = np.ascontiguousarray(pattern[1], np.int32)
+            assert rowptr.size == m + 1
+        nnz = int(rowptr[-1])
+        Av = f64(np.reshape(Aval, (B, nnz))); Pd = f64(np.reshape(Pdiag, (B, n)))
         qv = f64(np.reshape(q, (B, n))); lv = f64(np.reshape(l, (B, m))); uv = f64(np.reshape(u, (B, m)))
         xw = None if x_ws is None else f64(np.reshape(x_ws, (B, n)))
         x = np.empty((B, n)); y = np.empty((B, m)); obj = np.empty(B)
         it = np.zeros(B, np.int32); st = np.zeros(B, np.int32)
-        rc = _L.gpmpc_qp_solve_batched(self.ctx.h, B, n, m, self.nnz, _i(self.rowptr), _i(self.colidx),
+        rc = _L.gpmpc_qp_solve_batched(self.ctx.h, B, n, m, nnz, _i(rowptr), _i(colidx),
                                        _d(Av), _d(Pd), _d(qv), _d(lv), _d(uv), ctypes.byref(self.settings),
                                        None if xw is None else _d(xw), _d(self.rho), _d(self.y_scaled),
                                        _d(x), _d(y), _i(it), _i(st), _d(obj))

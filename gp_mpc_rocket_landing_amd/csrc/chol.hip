@@ -684,7 +684,7 @@ hipError_t launch_potrf_batched(hipStream_t s, int n, int batch, double *A, int6
                                            hipFuncAttributeMaxDynamicSharedMemorySize,
                                            (int)DIAG128_LDS) == hipSuccess;
     if (!attr) return hipErrorInvalidConfiguration;
-    double *Lws = (double *)gpmpc_scratch(2, sizeof(double) * DB * DB * (size_t)batch);
+    double *Lws = (double *)gpmpc_scratch(s, 2, sizeof(double) * DB * DB * (size_t)batch);
     if (!Lws) return hipErrorOutOfMemory;
     hipError_t e = hipMemsetAsync(info, 0, sizeof(int) * batch, s);
     if (e != hipSuccess) return e;
@@ -693,11 +693,11 @@ hipError_t launch_potrf_batched(hipStream_t s, int n, int batch, double *A, int6
     return hipGetLastError();
   }
   if (p128) {
-    double *Linv = (double *)gpmpc_scratch(2, sizeof(double) * DB * DB * (size_t)batch);
+    double *Linv = (double *)gpmpc_scratch(s, 2, sizeof(double) * DB * DB * (size_t)batch);
     if (!Linv) return hipErrorOutOfMemory;
     return launch_potrf_batched128(s, n, batch, A, lda, stride, info, Linv);
   }
-  double *Linv = (double *)gpmpc_scratch(1, sizeof(double) * NB * NB * (size_t)batch);
+  double *Linv = (double *)gpmpc_scratch(s, 1, sizeof(double) * NB * NB * (size_t)batch);
   if (!Linv) return hipErrorOutOfMemory;
   return launch_potrf_batched(s, n, batch, A, lda, stride, info, Linv);
 }
@@ -831,7 +831,7 @@ hipError_t launch_trsm_lower_ex(hipStream_t s, int n, int nrhs, const double *L,
                                 double *Linv_blocks /* may be null */) {
   const int nblk = (n + NB - 1) / NB;
   double *Linv = Linv_blocks;
-  if (!Linv) Linv = (double *)gpmpc_scratch(0, sizeof(double) * NB * NB * (size_t)nblk);
+  if (!Linv) Linv = (double *)gpmpc_scratch(s, 0, sizeof(double) * NB * NB * (size_t)nblk);
   if (!Linv) return hipErrorOutOfMemory;
   hipLaunchKernelGGL(k_tri_inv_blocks, dim3(nblk), dim3(64), 0, s, n, L, ldl, Linv);
   if (n <= TB) {

@@ -12,28 +12,39 @@ void gpmpc_set_error(const char *fmt, ...) {
   va_end(ap);
 }
 
-// Persistent device scratch per (device, slot), grown with hipMalloc after a full
-// device sync.  (Stream-ordered hipMallocAsync scratch returned buffers the next
+// Persistent device scratch per (stream, slot), grown with hipMalloc after the
+// stream has drained.  Every context owns one stream, so two contexts (e.g. on
+// two threads) never share a buffer; gpmpc_ctx_destroy releases its stream's
+// slots.  (Stream-ordered hipMallocAsync scratch returned buffers the next
 // kernel on the same stream did not see written on ROCm 7.2 -- see DESIGN.md.)
+#include <map>
+#include <array>
+struct ScratchSlot { void *p = nullptr; size_t bytes = 0; };
 static std::mutex g_scratch_mu;
-#define GPMPC_SCRATCH_SLOTS 8
-static void *g_scratch[64][GPMPC_SCRATCH_SLOTS];
-static size_t g_scratch_bytes[64][GPMPC_SCRATCH_SLOTS];
+static std::map<hipStream_t, std::array<ScratchSlot, GPMPC_SCRATCH_SLOTS>> g_scratch;
 
-void *gpmpc_scratch(int slot, size_t bytes) {
-  int dev = 0;
-  (void)hipGetDevice(&dev);
+void *gpmpc_scratch(hipStream_t s, int slot, size_t bytes) {
+  if (slot < 0 || slot >= GPMPC_SCRATCH_SLOTS) return nullptr;
   std::lock_guard<std::mutex> lk(g_scratch_mu);
-  if (dev < 0 || dev >= 64 || slot < 0 || slot >= GPMPC_SCRATCH_SLOTS) return nullptr;
-  if (g_scratch_bytes[dev][slot] < bytes) {
-    (void)hipDeviceSynchronize();
-    if (g_scratch[dev][slot]) (void)hipFree(g_scratch[dev][slot]);
-    g_scratch[dev][slot] = nullptr;
-    g_scratch_bytes[dev][slot] = 0;
-    if (hipMalloc(&g_scratch[dev][slot], bytes) != hipSuccess) return nullptr;
-    g_scratch_bytes[dev][slot] = bytes;
+  ScratchSlot &e = g_scratch[s][slot];
+  if (e.bytes < bytes) {
+    (void)hipStreamSynchronize(s);  // earlier work on this stream may still read it
+    if (e.p) (void)hipFree(e.p);
+    e.p = nullptr;
+    e.bytes = 0;
+    if (hipMalloc(&e.p, bytes) != hipSuccess) return nullptr;
+    e.bytes = bytes;
   }
-  return g_scratch[dev][slot];
+  return e.p;
+}
+
+static void scratch_release(hipStream_t s) {
+  std::lock_guard<std::mutex> lk(g_scratch_mu);
+  auto it = g_scratch.find(s);
+  if (it == g_scratch.end()) return;
+  for (ScratchSlot &e : it->second)
+    if (e.p) (void)hipFree(e.p);
+  g_scratch.erase(it);
 }
 
 extern "C" int gpmpc_abi_version(void) { return GPMPC_ABI_VERSION; }
@@ -61,7 +72,7 @@ extern "C" int gpmpc_ctx_destroy(gpmpc_ctx *ctx) {
   if (!ctx) return 0;
   (void)hipSetDevice(ctx->device);
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
-  if (ctx->scratch) (void)hipFree(ctx->scratch);
+  if (ctx->stream) scratch_release(ctx->stream);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx;
   return 0;

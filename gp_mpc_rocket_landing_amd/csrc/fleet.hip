@@ -704,6 +704,14 @@ extern "C" int gpmpc_fleet_create(gpmpc_ctx *ctx, gpmpc_gp *gp, const gpmpc_flee
   GPMPC_CHECK_ARG(ctx && gp && cfg && out && batch > 0);
   const GpView g = gp_view(gp);
   GPMPC_CHECK_ARG(g.d == NFEAT && g.n_out == 3);
+  // the fleet runs MonteCarloSimulator's solve protocol (monte_carlo.py:495-512)
+  // with the GPMPC adapter; FastRTI3DoF's step protocol (unshifted linearisation,
+  // D2 sign, fallback to the shifted plan) is the host mirror mpc/osqp_rti.py
+  if (cfg->target_mode != 1) {
+    gpmpc_set_error("fleet: target_mode must be 1 (solve protocol); the step protocol of "
+                    "FastRTI3DoF runs on the host mirror");
+    return -2;
+  }
   const int N = cfg->horizon;
   const int n = (N + 1) * NX + N * NU, m = NX * (N + 1) + n;
   GPMPC_CHECK_ARG(N >= 1 && n <= QP_NMAX && m <= QP_MMAX && NX + N * DYN_NNZ + n <= QP_NNZMAX);

@@ -205,7 +205,8 @@ static int core_setup(gpmpc_ctx *ctx, GpCore &g, int kind, const double *X, int 
   GPMPC_HIP(g.Xs.alloc(sizeof(double) * n * d));
   GPMPC_HIP(g.Xn.alloc(sizeof(double) * n));
   GPMPC_HIP(hipMemcpyAsync(dX.p, X, sizeof(double) * n * d, hipMemcpyHostToDevice, s));
-  GPMPC_HIP(hipMemcpyAsync(g.ls.p, ls, sizeof(double) * d, hipMemcpyHostToDevice, s));
+  // SE_ISO reads one lengthscale (ls[0]); the host array may hold just that one
+  GPMPC_HIP(hipMemcpyAsync(g.ls.p, ls, sizeof(double) * (iso ? 1 : d), hipMemcpyHostToDevice, s));
   GPMPC_HIP(launch_scale_rows(s, dX.as<double>(), n, d, g.ls.as<double>(), iso, g.Xs.as<double>(),
                               g.Xn.as<double>()));
   GPMPC_HIP(hipStreamSynchronize(s));
@@ -701,7 +702,7 @@ extern "C" int gpmpc_gp_lml_batched(gpmpc_ctx *ctx, int kind, const double *X, i
   // the B Gram / factor matrices live in persistent scratch (slot 3): one
   // optimiser gradient per call, so a per-call hipMalloc of B n^2 doubles
   // (112 MB at n = 1000) would cost more than the factorisations
-  double *Kbuf = (double *)gpmpc_scratch(3, sizeof(double) * nn * B);
+  double *Kbuf = (double *)gpmpc_scratch(ctx->stream, 3, sizeof(double) * nn * B);
   if (!Kbuf) {
     gpmpc_set_error("gp_lml_batched: out of device memory for %d x %d^2 doubles", B, n);
     return -1;
@@ -798,8 +799,8 @@ extern "C" int gpmpc_gp_append(gpmpc_ctx *ctx, gpmpc_gp *gp, const double *Xnew,
   // temporaries carved from persistent scratch (slot 4): a per-call hipMalloc /
   // hipFree of each cost more than the O(n^2 k) arithmetic
   const size_t need = 64 + 32 * 16 + (size_t)k * d * 2 + k + (size_t)k * n * 3 + (size_t)k * k * 2 +
-                      (size_t)m * no * 4 + no;
-  double *scr = (double *)gpmpc_scratch(4, sizeof(double) * need);
+                      (size_t)m * no * 4 + no * 3;
+  double *scr = (double *)gpmpc_scratch(ctx->stream, 4, sizeof(double) * need);
   if (!scr) {
     gpmpc_set_error("gp_append: out of device memory");
     return -1;
@@ -836,7 +837,7 @@ extern "C" int gpmpc_gp_append(gpmpc_ctx *ctx, gpmpc_gp *gp, const double *Xnew,
                            1.0, 0.0));
   DevBuf L2, W2, Xs2, Xn2, alphaT;  // kept by the handle
   ScratchPtr yraw{cv.take((size_t)m * no)}, yn{cv.take((size_t)m * no)}, t{cv.take((size_t)m * no)},
-      alpha{cv.take((size_t)m * no)}, dlml{cv.take(no)};
+      alpha{cv.take((size_t)m * no)}, dlml{cv.take(no)}, ym{cv.take(no)}, ys{cv.take(no)};
   GPMPC_HIP(L2.alloc(sizeof(double) * (size_t)m * m));
   GPMPC_HIP(W2.alloc(sizeof(double) * (size_t)(m + no) * m));
   GPMPC_HIP(Xs2.alloc(sizeof(double) * (size_t)m * d));
@@ -863,10 +864,11 @@ extern "C" int gpmpc_gp_append(gpmpc_ctx *ctx, gpmpc_gp *gp, const double *Xnew,
                            hipMemcpyDeviceToDevice, s));
   GPMPC_HIP(hipMemcpyAsync(Xn2.p, g.Xn.p, sizeof(double) * n, hipMemcpyDeviceToDevice, s));
   GPMPC_HIP(hipMemcpyAsync(Xn2.as<double>() + n, xn.p, sizeof(double) * k, hipMemcpyDeviceToDevice, s));
-  // all targets renormalised; alpha = W^T (W y); lml
+  // all targets renormalised (into scratch: the handle's mean / std change only
+  // at the commit below); alpha = W^T (W y); lml
   GPMPC_HIP(hipMemcpyAsync(yraw.p, Yall, sizeof(double) * (size_t)m * no, hipMemcpyHostToDevice, s));
   hipLaunchKernelGGL(k_normalise, dim3(no), dim3(256), 0, s, m, no, yraw.as<double>(),
-                     yn.as<double>(), g.ymean.as<double>(), g.ystd.as<double>());
+                     yn.as<double>(), ym.as<double>(), ys.as<double>());
   GPMPC_HIP(launch_gemm_nn(s, m, no, m, W2.as<double>(), m, yn.as<double>(), no, t.as<double>(), no,
                            1.0, 0.0));
   GPMPC_HIP(launch_gemm_tn(s, m, no, m, W2.as<double>(), m, t.as<double>(), no, alpha.as<double>(),
@@ -875,14 +877,18 @@ extern "C" int gpmpc_gp_append(gpmpc_ctx *ctx, gpmpc_gp *gp, const double *Xnew,
                      alpha.as<double>(), alphaT.as<double>(), dlml.as<double>());
   GPMPC_HIP(hipMemcpyAsync(W2.as<double>() + (size_t)m * m, alphaT.p, sizeof(double) * (size_t)no * m,
                            hipMemcpyDeviceToDevice, s));
-  std::vector<double> hl(no);
-  g.h_ymean.resize(no);
-  g.h_ystd.resize(no);
-  GPMPC_HIP(hipMemcpyAsync(g.h_ymean.data(), g.ymean.p, sizeof(double) * no, hipMemcpyDeviceToHost, s));
-  GPMPC_HIP(hipMemcpyAsync(g.h_ystd.data(), g.ystd.p, sizeof(double) * no, hipMemcpyDeviceToHost, s));
+  std::vector<double> hl(no), hm(no), hs(no);
+  GPMPC_HIP(hipMemcpyAsync(hm.data(), ym.p, sizeof(double) * no, hipMemcpyDeviceToHost, s));
+  GPMPC_HIP(hipMemcpyAsync(hs.data(), ys.p, sizeof(double) * no, hipMemcpyDeviceToHost, s));
   GPMPC_HIP(hipMemcpyAsync(hl.data(), dlml.p, sizeof(double) * no, hipMemcpyDeviceToHost, s));
   GPMPC_HIP(hipStreamSynchronize(s));
-  // commit: swap the grown buffers into the handle
+  // commit: the new normalisation, then swap the grown buffers into the handle
+  // (nothing below can fail half-way: the copies are of buffers already sized)
+  GPMPC_HIP(hipMemcpyAsync(g.ymean.p, ym.p, sizeof(double) * no, hipMemcpyDeviceToDevice, s));
+  GPMPC_HIP(hipMemcpyAsync(g.ystd.p, ys.p, sizeof(double) * no, hipMemcpyDeviceToDevice, s));
+  GPMPC_HIP(hipStreamSynchronize(s));
+  g.h_ymean = hm;
+  g.h_ystd = hs;
   std::swap(gp->L.p, L2.p); std::swap(gp->L.bytes, L2.bytes);
   std::swap(g.W.p, W2.p); std::swap(g.W.bytes, W2.bytes);
   std::swap(g.alphaT.p, alphaT.p); std::swap(g.alphaT.bytes, alphaT.bytes);

@@ -207,7 +207,8 @@ extern "C" int gpmpc_gram(gpmpc_ctx *ctx, int kind, const double *X1, int n1, co
   GPMPC_HIP(dna.alloc(sizeof(double) * n1));
   GPMPC_HIP(dK.alloc(sizeof(double) * (size_t)n1 * n2));
   GPMPC_HIP(hipMemcpyAsync(dX1.p, X1, sizeof(double) * n1 * d, hipMemcpyHostToDevice, s));
-  GPMPC_HIP(hipMemcpyAsync(dls.p, ls, sizeof(double) * d, hipMemcpyHostToDevice, s));
+  // SE_ISO reads one lengthscale (ls[0]); the host array may hold just that one
+  GPMPC_HIP(hipMemcpyAsync(dls.p, ls, sizeof(double) * (iso ? 1 : d), hipMemcpyHostToDevice, s));
   GPMPC_HIP(launch_scale_rows(s, dX1.as<double>(), n1, d, dls.as<double>(), iso, da.as<double>(),
                               dna.as<double>()));
   const double *pb = da.as<double>(), *pnb = dna.as<double>();
@@ -225,6 +226,86 @@ extern "C" int gpmpc_gram(gpmpc_ctx *ctx, int kind, const double *X1, int n1, co
                         iso_scale, dK.as<double>(), n2, 0));
   GPMPC_HIP(hipMemcpy2DAsync(K, sizeof(double) * ldk, dK.p, sizeof(double) * n2,
                              sizeof(double) * n2, n1, hipMemcpyDeviceToHost, s));
+  GPMPC_HIP(hipStreamSynchronize(s));
+  return 0;
+}
+
+// ---------------------------------------------------------------------------
+// Hyperparameter gradients of the Gram (kernels.py:279-318 SE-ARD, 438-456
+// isotropic SE): from K (already formed by launch_gram, so the same bits) and
+//   SE-ARD: G_i = K (x1_i - x2_i)^2 / l_i^2   (direct differences, d matrices)
+//   SE iso: G   = K r^2 / l^2                  (r^2 of the expansion form)
+// one thread per (row, column); every matrix row-major n1 x n2, stacked.
+__global__ __launch_bounds__(256) void k_gram_grad(int kind, const double *__restrict__ X1,
+                                                   int n1, const double *__restrict__ X2, int n2,
+                                                   int d, const double *__restrict__ ls,
+                                                   const double *__restrict__ na,
+                                                   const double *__restrict__ nb,
+                                                   const double *__restrict__ K,
+                                                   double *__restrict__ G) {
+  const int col = blockIdx.x * blockDim.x + threadIdx.x, row = blockIdx.y;
+  if (col >= n2) return;
+  const int64_t e = (int64_t)row * n2 + col, plane = (int64_t)n1 * n2;
+  const double k = K[e];
+  const double *a = X1 + (int64_t)row * d, *b = X2 + (int64_t)col * d;
+  if (kind == GPMPC_SE_ARD) {
+    for (int i = 0; i < d; ++i) {
+      const double df = a[i] - b[i];
+      G[i * plane + e] = k * ((df * df) / (ls[i] * ls[i]));
+    }
+  } else {  // isotropic: rows unscaled, r^2 as k_gram forms it
+    double dot = 0.0;
+    for (int i = 0; i < d; ++i) dot = fma(a[i], b[i], dot);
+    double d2 = (na[row] + nb[col]) - 2.0 * dot;
+    d2 = d2 > 0.0 ? d2 : 0.0;
+    G[e] = (k * d2) / (ls[0] * ls[0]);
+  }
+}
+
+extern "C" int gpmpc_gram_grad(gpmpc_ctx *ctx, int kind, const double *X1, int n1, const double *X2,
+                               int n2, int d, const double *ls, double sigma2, double *K, double *G) {
+  GPMPC_CHECK_ARG(ctx && X1 && ls && G);
+  GPMPC_CHECK_ARG(kind == GPMPC_SE_ARD || kind == GPMPC_SE_ISO);
+  GPMPC_CHECK_ARG(d >= 1 && d <= GRAM_MAXD && n1 >= 0);
+  if (!X2) n2 = n1;
+  GPMPC_CHECK_ARG(n2 >= 0);
+  if (n1 == 0 || n2 == 0) return 0;
+  GPMPC_HIP(hipSetDevice(ctx->device));
+  hipStream_t s = ctx->stream;
+  const int iso = (kind == GPMPC_SE_ISO);
+  const double iso_scale = iso ? 1.0 / (2.0 * ls[0] * ls[0]) : 0.0;
+  const int ng = iso ? 1 : d;
+  const size_t nn = (size_t)n1 * n2;
+  DevBuf dX1, dX2, dls, da, db, dna, dnb, dK, dG;
+  GPMPC_HIP(dX1.alloc(sizeof(double) * n1 * d));
+  GPMPC_HIP(dls.alloc(sizeof(double) * d));
+  GPMPC_HIP(da.alloc(sizeof(double) * n1 * d));
+  GPMPC_HIP(dna.alloc(sizeof(double) * n1));
+  GPMPC_HIP(dK.alloc(sizeof(double) * nn));
+  GPMPC_HIP(dG.alloc(sizeof(double) * nn * ng));
+  GPMPC_HIP(hipMemcpyAsync(dX1.p, X1, sizeof(double) * n1 * d, hipMemcpyHostToDevice, s));
+  // SE_ISO reads one lengthscale (ls[0]); the host array may hold just that one
+  GPMPC_HIP(hipMemcpyAsync(dls.p, ls, sizeof(double) * (iso ? 1 : d), hipMemcpyHostToDevice, s));
+  GPMPC_HIP(launch_scale_rows(s, dX1.as<double>(), n1, d, dls.as<double>(), iso, da.as<double>(),
+                              dna.as<double>()));
+  const double *pX2 = dX1.as<double>(), *pb = da.as<double>(), *pnb = dna.as<double>();
+  if (X2) {
+    GPMPC_HIP(dX2.alloc(sizeof(double) * n2 * d));
+    GPMPC_HIP(db.alloc(sizeof(double) * n2 * d));
+    GPMPC_HIP(dnb.alloc(sizeof(double) * n2));
+    GPMPC_HIP(hipMemcpyAsync(dX2.p, X2, sizeof(double) * n2 * d, hipMemcpyHostToDevice, s));
+    GPMPC_HIP(launch_scale_rows(s, dX2.as<double>(), n2, d, dls.as<double>(), iso,
+                                db.as<double>(), dnb.as<double>()));
+    pX2 = dX2.as<double>(); pb = db.as<double>(); pnb = dnb.as<double>();
+  }
+  GPMPC_HIP(launch_gram(s, kind, da.as<double>(), dna.as<double>(), n1, pb, pnb, n2, d, sigma2,
+                        iso_scale, dK.as<double>(), n2, 0));
+  hipLaunchKernelGGL(k_gram_grad, dim3((n2 + 255) / 256, n1), dim3(256), 0, s, kind,
+                     dX1.as<double>(), n1, pX2, n2, d, dls.as<double>(), dna.as<double>(), pnb,
+                     dK.as<double>(), dG.as<double>());
+  GPMPC_HIP(hipGetLastError());
+  if (K) GPMPC_HIP(hipMemcpyAsync(K, dK.p, sizeof(double) * nn, hipMemcpyDeviceToHost, s));
+  GPMPC_HIP(hipMemcpyAsync(G, dG.p, sizeof(double) * nn * ng, hipMemcpyDeviceToHost, s));
   GPMPC_HIP(hipStreamSynchronize(s));
   return 0;
 }

@@ -9,16 +9,15 @@
 struct gpmpc_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
-  // scratch that grows on demand (device)
-  void *scratch = nullptr;
-  size_t scratch_bytes = 0;
 };
 
 void gpmpc_set_error(const char *fmt, ...);
-// persistent per-device scratch (slots: 0 trsm block inverses, 1 potrf 32x32 inverses,
-// 2 potrf 128x128 inverses, 3 batched-LML Gram/factor matrices, 4 gp_append temporaries;
-// slots 0..7)
-void *gpmpc_scratch(int slot, size_t bytes);
+// persistent scratch per stream (= per context; slots: 0 trsm block inverses,
+// 1 potrf 32x32 inverses, 2 potrf 128x128 inverses, 3 batched-LML Gram/factor
+// matrices, 4 gp_append temporaries; slots 0..7).  Valid until the next call
+// on the same stream that asks the slot for more bytes.
+#define GPMPC_SCRATCH_SLOTS 8
+void *gpmpc_scratch(hipStream_t s, int slot, size_t bytes);
 
 #define GPMPC_HIP(call)                                                               \
   do {                                                                                \

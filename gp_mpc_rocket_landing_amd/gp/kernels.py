@@ -5,8 +5,10 @@ through gpmpc_gram (csrc/gram.hip: expansion-form scaled distance, clamped at
 0, kernels.py:205-236).  Hyperparameters are exposed in log space exactly as
 get_params/set_params/n_params/param_names define them (kernels.py:320-371).
 Sum/product kernels combine device Grams elementwise; WhiteNoise is diagonal.
-Gradient methods (hyperparameter fitting) are not part of this
-path.
+``gradients`` (kernels.py:279-318 and the per-kernel variants) returns the
+same dictionaries as the reference: SE-ARD / isotropic SE gradient matrices
+come from the device (gpmpc_gram_grad), the Matern kernels give only the
+log-signal-variance gradient K, as the reference's do.
 """
 from __future__ import annotations
 
@@ -101,6 +103,11 @@ class _StationaryARD(Kernel):
     def diagonal(self, X) -> np.ndarray:
         return np.full(np.atleast_2d(X).shape[0], self._signal_variance)
 
+    def gradients(self, X1, X2=None) -> dict:
+        """Matern32/52.gradients (kernels.py:551-558, 644-650): the reference
+        returns only d K / d log(sigma2) = K for these kernels."""
+        return {"log_signal_variance": self(X1, X2)}
+
     @property
     def n_params(self) -> int:
         return int(self.learn_signal_variance) + (self.input_dim if self.learn_lengthscales else 0)
@@ -133,6 +140,18 @@ class _StationaryARD(Kernel):
 class SquaredExponentialARD(_StationaryARD):
     """kernels.py:130-384: sigma2 exp(-r^2/2), r^2 = |x/l - x'/l|^2."""
     KIND = _lib.SE_ARD
+
+    def gradients(self, X1, X2=None) -> dict:
+        """kernels.py:279-318: d K / d log(sigma2) = K and, per input dimension,
+        d K / d log(l_i) = K (x1_i - x2_i)^2 / l_i^2 (device)."""
+        K, G = _lib.gram_grad(_ctx(), _lib.SE_ARD, X1, X2, self._lengthscales, self._signal_variance)
+        grads = {}
+        if self.learn_signal_variance:
+            grads["log_signal_variance"] = K.copy()
+        if self.learn_lengthscales:
+            for i in range(self.input_dim):
+                grads[f"log_lengthscale_{i}"] = G[i]
+        return grads
 
 
 class Matern32(_StationaryARD):
@@ -174,6 +193,12 @@ class SquaredExponential(Kernel):
 
     def diagonal(self, X) -> np.ndarray:
         return np.full(np.atleast_2d(X).shape[0], self._signal_variance)
+
+    def gradients(self, X1, X2=None) -> dict:
+        """kernels.py:438-456: K and K r^2 / l^2 (device)."""
+        K, G = _lib.gram_grad(_ctx(), _lib.SE_ISO, X1, X2, np.array([self._lengthscale]),
+                              self._signal_variance)
+        return {"log_signal_variance": K, "log_lengthscale": G[0]}
 
     @property
     def n_params(self) -> int:
@@ -218,12 +243,25 @@ class SumKernel(Kernel):
         self.k1.set_params(params[:self.k1.n_params])
         self.k2.set_params(params[self.k1.n_params:])
 
+    def gradients(self, X1, X2=None) -> dict:
+        """kernels.py:697-707."""
+        grads = {f"k1_{n}": g for n, g in self.k1.gradients(X1, X2).items()}
+        grads.update({f"k2_{n}": g for n, g in self.k2.gradients(X1, X2).items()})
+        return grads
+
 
 class ProductKernel(SumKernel):
     """kernels.py:729-782."""
 
     def __call__(self, X1, X2=None):
         return self.k1(X1, X2) * self.k2(X1, X2)
+
+    def gradients(self, X1, X2=None) -> dict:
+        """kernels.py:750-763: product rule."""
+        K1, K2 = self.k1(X1, X2), self.k2(X1, X2)
+        grads = {f"k1_{n}": g * K2 for n, g in self.k1.gradients(X1, X2).items()}
+        grads.update({f"k2_{n}": K1 * g for n, g in self.k2.gradients(X1, X2).items()})
+        return grads
 
     def diagonal(self, X):
         return self.k1.diagonal(X) * self.k2.diagonal(X)
@@ -261,6 +299,10 @@ class WhiteNoise(Kernel):
 
     def set_params(self, params):
         self._noise_variance = float(np.exp(np.asarray(params)[0]))
+
+    def gradients(self, X1, X2=None) -> dict:
+        """kernels.py:822-827."""
+        return {"log_noise_variance": self(X1, X2)}
 
 
 # aliases (kernels.py:383-384)

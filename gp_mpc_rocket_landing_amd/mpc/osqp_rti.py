@@ -12,9 +12,18 @@ solve calls are replaced by the batched device ADMM (gpmpc_qp_solve_batched,
 OSQP-0.6 semantics, rho and scaled y carried between solves as OSQP's
 workspace does).
 
+c_k = f(x_k, u_k) - A_k x_k - B_k u_k evaluates f with the caller's plant,
+``dynamics.step`` (osqp_rti.py:339).  OSQPRTIMPC linearises by forward
+differences through that plant (osqp_rti.py:374-401, eps 1e-6) and keeps,
+like the reference, the entries of A_k, B_k with |a| > 1e-10
+(osqp_rti.py:299-312): the pattern is re-derived at every solve (the
+reference's update(Ax=...) assumes it does not move).
+FastRTI3DoF uses the analytic 3-DoF Jacobians (osqp_rti.py:656-710) on
+their structural pattern, explicit zeros included.
+
 ``rhs_sign`` (default +1) reproduces the reference's equality right-hand side
-l = u = +c_k; -1 gives x+ = A x + B u + c.  The QP's sparsity
-pattern is the structural one; polishing is not supported.
+l = u = +c_k; -1 gives x+ = A x + B u + c.  Structural zeros are
+stored explicitly; polishing is not supported.
 """
 from __future__ import annotations
 
@@ -73,6 +82,8 @@ def qp_settings_from(cfg) -> "_lib.QPSettings":
 class OSQPRTIMPC:
     """osqp_rti.py:89-639."""
 
+    _DENSE_PATTERN = True   # finite-difference Jacobians: any entry may be non-zero
+
     def __init__(self, dynamics, config: Optional[OSQPRTIConfig] = None, ctx=None):
         self.dynamics = dynamics
         self.config = config or OSQPRTIConfig()
@@ -83,13 +94,15 @@ class OSQPRTIMPC:
         p = getattr(dynamics, "params", None)
         alpha = getattr(p, "alpha", 1.0 / 30.0)
         g_vec = getattr(p, "g_vec", np.array([-1.0, 0.0, 0.0]))
-        self._qp = RTIQPBuilder(self.N, self.config.dt, alpha=alpha, g_vec=g_vec)
+        self._qp = RTIQPBuilder(self.N, self.config.dt, alpha=alpha, g_vec=g_vec,
+                                dense=self._DENSE_PATTERN)
         self._ctx = ctx or _lib.default_context()
         self._solver: Optional[_lib.QPWorkspace] = None
         self._x_ref = self._u_ref = None
         self._X_prev = self._U_prev = None
         self._X_lin = self._U_lin = None
         self._q = None
+        self._pattern = None
 
     def initialize(self, x0, x_target, X_init=None, U_init=None) -> None:
         """osqp_rti.py:403-452."""
@@ -117,8 +130,46 @@ class OSQPRTIMPC:
                                         settings=qp_settings_from(self.config))
         _, self._q = b.cost(self._x_ref)
 
+    def _linearize(self, x, u, eps: float = 1e-6):
+        """osqp_rti.py:374-401: forward differences through dynamics.step."""
+        dt = self.config.dt
+        x = np.asarray(x, float); u = np.asarray(u, float)
+        A = np.zeros((self.n_x, self.n_x)); B = np.zeros((self.n_x, self.n_u))
+        x_next_nom = np.asarray(self.dynamics.step(x, u, dt), float)
+        for i in range(self.n_x):
+            xp = x.copy(); xp[i] += eps
+            A[:, i] = (np.asarray(self.dynamics.step(xp, u, dt), float) - x_next_nom) / eps
+        for i in range(self.n_u):
+            up = u.copy(); up[i] += eps
+            B[:, i] = (np.asarray(self.dynamics.step(x, up, dt), float) - x_next_nom) / eps
+        return A, B
+
+    def _stage_jacobians(self):
+        AB = [self._linearize(self._X_lin[k], self._U_lin[k]) for k in range(self.N)]
+        return np.array([a for a, _ in AB]), np.array([b for _, b in AB])
+
     def _constraints(self, x_current) -> Tuple[np.ndarray, np.ndarray, np.ndarray]:
-        return self._qp.constraints(self._X_lin, self._U_lin, x_current, sign=self.config.rhs_sign)
+        """osqp_rti.py:260-372: Jacobians per stage, c_k from the caller's plant.
+        Sets ``self._pattern`` (rowptr, colidx) of the returned A values."""
+        dt = self.config.dt
+        f_next = np.array([self.dynamics.step(self._X_lin[k], self._U_lin[k], dt) for k in range(self.N)],
+                          dtype=float)
+        Aval, l, u = self._qp.constraints(self._X_lin, self._U_lin, x_current, sign=self.config.rhs_sign,
+                                          jac=self._stage_jacobians(), f_next=f_next)
+        b = self._qp
+        if not b.dense:
+            self._pattern = (b.rowptr, b.colidx)
+            return Aval, l, u
+        # |a| > 1e-10 on the A_k / B_k entries (osqp_rti.py:299-312); the x0 and
+        # bound identities and the -I of x_{k+1} always stay
+        keep = np.ones(Aval.size, bool)
+        dyn = slice(self.n_x, self.n_x + self.N * self.n_x * (self.n_x + self.n_u + 1))
+        blk = keep[dyn].reshape(self.N, self.n_x, self.n_x + self.n_u + 1)
+        blk[:, :, :-1] = np.abs(Aval[dyn].reshape(blk.shape)[:, :, :-1]) > 1e-10
+        rows = np.repeat(np.arange(b.m), np.diff(b.rowptr))
+        rowptr = np.concatenate([[0], np.cumsum(np.bincount(rows[keep], minlength=b.m))]).astype(np.int32)
+        self._pattern = (rowptr, b.colidx[keep])
+        return Aval[keep], l, u
 
     def prepare(self) -> float:
         """osqp_rti.py:480-499."""
@@ -136,7 +187,7 @@ class OSQPRTIMPC:
         xw = None
         if self._X_prev is not None and self.config.osqp_warm_start:
             xw = solution_to_vector(self._X_prev, self._U_prev)
-        r = self._solver.solve(Aval, self._qp.P_diag, self._q, l, u, xw)
+        r = self._solver.solve(Aval, self._qp.P_diag, self._q, l, u, xw, pattern=self._pattern)
         t_solve = time.perf_counter()
         status = int(r["status"][0])
         if status in (1, 2):
@@ -175,6 +226,8 @@ class OSQPRTIMPC:
 class FastRTI3DoF(OSQPRTIMPC):
     """osqp_rti.py:642-710: 3-DoF RTI with analytic Jacobians."""
 
+    _DENSE_PATTERN = False
+
     def __init__(self, dynamics, config: Optional[OSQPRTIConfig] = None, ctx=None):
         config = config or OSQPRTIConfig()
         config.n_x = 7
@@ -184,3 +237,6 @@ class FastRTI3DoF(OSQPRTIMPC):
     def _linearize(self, x, u, eps: float = 1e-6):  # noqa: ARG002
         A, B = self._qp.jacobians(np.asarray(x, float)[None], np.asarray(u, float)[None])
         return A[0], B[0]
+
+    def _stage_jacobians(self):
+        return self._qp.jacobians(self._X_lin, self._U_lin)

@@ -12,7 +12,14 @@ Same QP as OSQPRTIMPC._build_cost_matrix / _build_constraint_matrix
 The sparsity pattern is the structural pattern of the analytic Jacobians
 (26 entries per stage block) and is fixed for a given N, so one pattern serves
 every solve and every landing; the reference filters |a| > 1e-10,
-which stores the same QP with a value-dependent pattern.  s = +1 reproduces
+which stores the same QP with a value-dependent pattern.  ``dense=True``
+stores every entry of A_k and B_k (77 per stage block) -- the pattern for
+OSQPRTIMPC's finite-difference Jacobians of an arbitrary plant
+(osqp_rti.py:374-401), whose non-zeros are not known in advance.
+
+c_k = f(x_k, u_k) - A_k x_k - B_k u_k takes f from the caller's plant when
+``f_next`` (the plant's dynamics.step at every stage, osqp_rti.py:339) is
+given, else from the Euler 3-DoF model restated here (nominal_mpc.py:585-605).  s = +1 reproduces
 the reference's right-hand side; the GP-MPC adapter uses s = -1
 (x+ = A x + B u + c, gp_mpc.py:410-411) with the GP mean dt*d_v added to the
 velocity rows of c_k (gp_mpc.py:309-314).
@@ -72,8 +79,11 @@ class RTIQPBuilder:
     """Pattern + per-solve values of the RTI QP for horizon N."""
 
     def __init__(self, N: int, dt: float, alpha: float = 1.0 / 30.0,
-                 g_vec=(-1.0, 0.0, 0.0)):
+                 g_vec=(-1.0, 0.0, 0.0), dense: bool = False):
         self.N, self.dt, self.alpha = int(N), float(dt), float(alpha)
+        self.dense = bool(dense)
+        block = ([list(range(N_X + N_U)) + [N_X + N_U + i] for i in range(N_X)] if self.dense
+                 else _BLOCK_COLS)
         self.g_vec = np.asarray(g_vec, float)
         N = self.N
         self.n = n_vars(N)
@@ -84,7 +94,7 @@ class RTIQPBuilder:
         for k in range(N):
             c0 = k * (N_X + N_U)
             for i in range(N_X):
-                cols.append([c0 + c for c in _BLOCK_COLS[i]]); rowlen.append(len(_BLOCK_COLS[i]))
+                cols.append([c0 + c for c in block[i]]); rowlen.append(len(block[i]))
         for j in range(self.n):                   # bound rows
             cols.append([j]); rowlen.append(1)
         self.rowptr = np.concatenate([[0], np.cumsum(rowlen)]).astype(np.int32)
@@ -128,26 +138,37 @@ class RTIQPBuilder:
         B[:, 4, 0] = B[:, 5, 1] = B[:, 6, 2] = dt / m
         return A, B
 
-    def constraints(self, X_lin, U_lin, x_init, gp_dv=None, sign: float = 1.0):
-        """(A values in pattern order, l, u) around the linearisation (X_lin, U_lin)."""
+    def constraints(self, X_lin, U_lin, x_init, gp_dv=None, sign: float = 1.0, jac=None,
+                    f_next=None):
+        """(A values in pattern order, l, u) around the linearisation (X_lin, U_lin).
+
+        ``jac`` = (A (N,7,7), B (N,7,3)) overrides the analytic Jacobians; with
+        the structural pattern it must keep that pattern's zeros.  ``f_next``
+        (N,7) = the plant's step at (X_lin[k], U_lin[k]) for c_k."""
         N, dt = self.N, self.dt
         X = np.asarray(X_lin, float); U = np.asarray(U_lin, float)
-        A, B = self.jacobians(X, U)
-        v = np.empty((N, DYN_NNZ))
-        v[:, 0] = A[:, 0, 0]; v[:, 1:4] = B[:, 0, :]; v[:, 4] = -1.0
-        for i in range(1, 4):
-            o = 5 + 3 * (i - 1)
-            v[:, o] = A[:, i, i]; v[:, o + 1] = A[:, i, i + 3]; v[:, o + 2] = -1.0
-        for i in range(4, 7):
-            o = 14 + 4 * (i - 4)
-            v[:, o] = A[:, i, 0]; v[:, o + 1] = A[:, i, i]; v[:, o + 2] = B[:, i, i - 4]; v[:, o + 3] = -1.0
+        A, B = self.jacobians(X, U) if jac is None else (np.asarray(jac[0], float), np.asarray(jac[1], float))
+        if self.dense:
+            v = np.concatenate([A, B, np.broadcast_to(-1.0, (N, N_X, 1))], axis=2)
+        else:
+            v = np.empty((N, DYN_NNZ))
+            v[:, 0] = A[:, 0, 0]; v[:, 1:4] = B[:, 0, :]; v[:, 4] = -1.0
+            for i in range(1, 4):
+                o = 5 + 3 * (i - 1)
+                v[:, o] = A[:, i, i]; v[:, o + 1] = A[:, i, i + 3]; v[:, o + 2] = -1.0
+            for i in range(4, 7):
+                o = 14 + 4 * (i - 4)
+                v[:, o] = A[:, i, 0]; v[:, o + 1] = A[:, i, i]; v[:, o + 2] = B[:, i, i - 4]; v[:, o + 3] = -1.0
         Aval = np.concatenate([np.ones(N_X), v.reshape(-1), np.ones(self.n)])
         # c_k = f(x_k, u_k) - A_k x_k - B_k u_k   (+ dt d_v on the velocity rows)
         Xk, Uk = X[:N], U[:N]
-        f = np.empty((N, N_X))
-        f[:, 0] = Xk[:, 0] - dt * self.alpha * np.sqrt(np.sum(Uk * Uk, axis=1))
-        f[:, 1:4] = Xk[:, 1:4] + dt * Xk[:, 4:7]
-        f[:, 4:7] = Xk[:, 4:7] + dt * (Uk / Xk[:, :1] + self.g_vec)
+        if f_next is not None:
+            f = np.asarray(f_next, float).reshape(N, N_X)
+        else:
+            f = np.empty((N, N_X))
+            f[:, 0] = Xk[:, 0] - dt * self.alpha * np.sqrt(np.sum(Uk * Uk, axis=1))
+            f[:, 1:4] = Xk[:, 1:4] + dt * Xk[:, 4:7]
+            f[:, 4:7] = Xk[:, 4:7] + dt * (Uk / Xk[:, :1] + self.g_vec)
         c = f - np.einsum("kij,kj->ki", A, Xk) - np.einsum("kij,kj->ki", B, Uk)
         if gp_dv is not None:
             c[:, 4:7] += np.asarray(gp_dv, float)[:N] * dt

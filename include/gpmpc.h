@@ -61,6 +61,15 @@ void *gpmpc_ctx_stream(gpmpc_ctx *ctx);
  * ls: d lengthscales (SE_ISO reads ls[0]). */
 int gpmpc_gram(gpmpc_ctx *ctx, int kind, const double *X1, int n1, const double *X2, int n2,
                int d, const double *ls, double sigma2, double *K, int ldk);
+/* Hyperparameter gradients of the Gram, d K / d(log theta)
+ * (SquaredExponentialARD.gradients kernels.py:279-318: K (x1_i - x2_i)^2 / l_i^2
+ * for every input dimension i; SquaredExponential.gradients :438-456:
+ * K r^2 / l^2).  kind SE_ARD writes d matrices, SE_ISO one, each n1 x n2
+ * row-major, stacked in G; K (n1 x n2) is written too unless NULL.  The
+ * log-signal-variance gradient is K itself (and the only one the reference's
+ * Matern kernels define). */
+int gpmpc_gram_grad(gpmpc_ctx *ctx, int kind, const double *X1, int n1, const double *X2, int n2,
+                    int d, const double *ls, double sigma2, double *K, double *G);
 
 /* ---- Cholesky factor / solve -------------------------------------------
  * Replaces np.linalg.cholesky (exact_gp.py:164,170; sparse_gp.py:187,205).
@@ -181,8 +190,9 @@ int gpmpc_qp_solve_batched(gpmpc_ctx *ctx, int batch, int n, int m, int nnz, con
 typedef struct {
   int horizon;           /* N (osqp_rti.py OSQPRTIConfig.N / MPCConfig.N) */
   double dt;             /* control period */
-  int target_mode;       /* 0: fixed x_target (controller.step protocol);
-                            1: incremental target of monte_carlo.py:497-500 (solve protocol) */
+  int target_mode;       /* must be 1: the solve protocol of monte_carlo.py:495-512 with its
+                            incremental target (:497-500); the step protocol of
+                            FastRTI3DoF is the host mirror (mpc/osqp_rti.py) */
   int use_gp;            /* add GP mean to c_k */
   int residual_model;    /* 1: plant gets the aero-drag residual (dispersion.py:349-360) */
   int max_steps;         /* max_time / dt */

@@ -54,6 +54,25 @@ def gram(kind, X1, X2, sigma2, ls):
     raise ValueError(kind)
 
 
+def gram_gradients(kind, X1, X2, sigma2, ls):
+    """Hyperparameter gradients d K / d log(theta) as ordered lists.
+
+    se_ard   kernels.py:279-318   [K, K (x1_i - x2_i)^2 / l_i^2 for each i]
+    se_iso   kernels.py:438-456   [K, K r^2 / l^2]  (r^2 on raw inputs, clamped)
+    matern*  kernels.py:551-558, 644-650   [K]
+    """
+    X1 = np.atleast_2d(X1)
+    X2 = X1 if X2 is None else np.atleast_2d(X2)
+    K = gram(kind, X1, X2, sigma2, ls)
+    if kind == "se_ard":
+        ls = np.asarray(ls, float)
+        return [K] + [K * ((X1[:, i:i + 1] - X2[:, i:i + 1].T) ** 2 / ls[i] ** 2) for i in range(X1.shape[1])]
+    if kind == "se_iso":
+        l = float(np.asarray(ls).ravel()[0])
+        return [K, K * scaled_sqdist(X1, X2, 1.0) / l ** 2]
+    return [K]
+
+
 # --------------------------------------------------------------------------
 # features (src/gp/features.py)
 # --------------------------------------------------------------------------

@@ -8,6 +8,8 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 if REPO not in sys.path:
     sys.path.insert(0, REPO)
 GOLDEN = os.path.join(REPO, "tests", "golden")
+if GOLDEN not in sys.path:  # the stand-in plants of the fixtures (toy_dynamics)
+    sys.path.insert(1, GOLDEN)
 
 
 def pytest_configure(config):

@@ -1,4 +1,4 @@
-"""Generate the golden fixtures F1-F9 from the reference itself.
+"""Generate the golden fixtures F1-F11 from the reference itself.
 
 Container-only: it imports /root/reference/src/{gp,mpc,experiments} through a
 namespace shim that bypasses src/__init__.py (which needs the absent simdyn /
@@ -141,6 +141,33 @@ def f3():
     save("f3_kernels.npz", **out)
 
 
+# ---------------------------------------------------------------- F11
+def f11():
+    """Kernel hyperparameter gradients (kernels.py:279-318, 438-456, 551-558,
+    644-650, 697-707, 750-763, WhiteNoise), same inputs as F3."""
+    rs = np.random.RandomState(9)
+    X1 = rs.normal(0, 1, (32, 11)); X2 = rs.normal(0, 1, (48, 11))
+    ls = rs.uniform(0.5, 2.0, 11); s2 = 0.7
+    X1, X2 = X1[:16], X2[:24]
+    out = dict(X1=X1, X2=X2, ls=ls, sigma2=s2, iso_l=1.3)
+    cases = {
+        "se_ard": kernels.SquaredExponentialARD(11, s2, ls),
+        "se_iso": kernels.SquaredExponential(s2, 1.3),
+        "matern32": kernels.Matern32(11, s2, ls),
+        "matern52": kernels.Matern52(11, s2, ls),
+        "white": kernels.WhiteNoise(0.05),
+        "sum_se_m32": kernels.SquaredExponentialARD(11, s2, ls) + kernels.Matern32(11, 0.3, ls),
+        "prod_se_m52": kernels.SquaredExponentialARD(11, s2, ls) * kernels.Matern52(11, 0.5, ls),
+    }
+    for name, k in cases.items():
+        for tag, args in (("x12", (X1, X2)),) + ((("x11", (X1,)),) if name == "se_ard" else ()):
+            g = k.gradients(*args)
+            out[f"{name}_{tag}_names"] = np.array(list(g.keys()))
+            for j, v in enumerate(g.values()):
+                out[f"{name}_{tag}_{j}"] = v
+    save("f11_kernel_gradients.npz", **out)
+
+
 # ---------------------------------------------------------------- F4
 def f4():
     X, U, D = synthetic_training_data(1000, seed=0)
@@ -238,6 +265,33 @@ def f6():
                     f"c{i}_B0": Bk, f"c{i}_zvec": mpc._solution_to_vector(Xl, Ul)})
     out["ncases"] = len(cases)
     save("f6_qp_assembly.npz", **out)
+
+
+# ---------------------------------------------------------------- F6b
+def f6b():
+    """The caller's-plant hooks of the RTI QP: reference OSQPRTIMPC (forward-
+    difference Jacobians through dynamics.step, osqp_rti.py:374-401) and
+    FastRTI3DoF (analytic Jacobians, c_k from dynamics.step, :339) driven by a
+    plant with drag (toy_dynamics.DragRocket3DoF)."""
+    from toy_dynamics import DragRocket3DoF
+    osqp_rti.HAS_OSQP = True
+    rs = np.random.RandomState(23)
+    out = {}
+    for name, cls in (("fd", osqp_rti.OSQPRTIMPC), ("fast", osqp_rti.FastRTI3DoF)):
+        cfg = osqp_rti.OSQPRTIConfig(N=20, dt=0.1)
+        mpc = cls(DragRocket3DoF(), cfg)
+        for i in range(2):
+            x0 = np.array([2.0, 30.0, 1.0, -1.0, -3.0, 0.2, 0.1]) + rs.normal(0, 1, 7) * [0.1, 5, 2, 2, 0.5, 0.3, 0.3]
+            xt = np.zeros(7); xt[0] = x0[0]
+            X = np.linspace(x0, xt, 21) + rs.normal(0, 0.1, (21, 7))
+            U = np.stack([rs.uniform(0.5, 4.5, 20), rs.normal(0, 0.5, 20), rs.normal(0, 0.5, 20)], 1)
+            A, l, u = mpc._build_constraint_matrix(X, U, x0)
+            Ak, Bk = mpc._linearize(X[3], U[3])
+            out.update({f"{name}{i}_x0": x0, f"{name}{i}_X": X, f"{name}{i}_U": U,
+                        f"{name}{i}_A_data": A.data, f"{name}{i}_A_indices": A.indices,
+                        f"{name}{i}_A_indptr": A.indptr, f"{name}{i}_l": l, f"{name}{i}_u": u,
+                        f"{name}{i}_A3": Ak, f"{name}{i}_B3": Bk})
+    save("f6b_rti_plant_hooks.npz", **out)
 
 
 # ---------------------------------------------------------------- F7 / F8
@@ -342,6 +396,6 @@ def f10():
 
 
 if __name__ == "__main__":
-    which = sys.argv[1:] or ["f1", "f2", "f3", "f4", "f5", "f6", "f7_f8", "f9", "f10"]
+    which = sys.argv[1:] or ["f1", "f2", "f3", "f4", "f5", "f6", "f6b", "f7_f8", "f9", "f10", "f11"]
     for w in which:
         globals()[w]()

@@ -63,3 +63,31 @@ def toy_case(seed=9, N=10):
     x0 = np.concatenate([[2.0], [20.0, 1.5, -1.0], [-2.0, 0.3, 0.1], q, [0.02, -0.01, 0.03]])
     U = np.array([2.2, 0.0, 0.0]) + 0.1 * rs.randn(N, 3)
     return x0, U
+
+
+class _P3:
+    g0 = 1.0
+    alpha = 1.0 / 30.0
+    g_vec = np.array([-1.0, 0.0, 0.0])
+
+
+class DragRocket3DoF:
+    """3-DoF Euler plant (nominal_mpc.py:585-605) plus the aero drag of
+    experiments/dispersion.py:349-360 (rho 0.02, Cd = A = 1) -- a caller's
+    plant whose step differs from the RTI's built-in model and whose
+    Jacobian is not on the analytic Jacobian's pattern (drag couples every
+    velocity component with mass and the other components).  F6b drives the
+    reference OSQPRTIMPC / FastRTI3DoF with it; the tests drive the mirror."""
+    n_state = 7
+    n_control = 3
+    params = _P3()
+
+    def step(self, x, u, dt):
+        x = np.asarray(x, float); u = np.asarray(u, float)
+        out = np.empty(7)
+        out[0] = x[0] - dt * self.params.alpha * np.sqrt(u @ u)
+        out[1:4] = x[1:4] + dt * x[4:7]
+        v = x[4:7]; s = np.sqrt(v @ v)
+        drag = -(0.5 * 0.02 * s * s) / x[0] * (v / s) if s > 1.0 else np.zeros(3)
+        out[4:7] = v + dt * (u / x[0] + self.params.g_vec + drag)
+        return out

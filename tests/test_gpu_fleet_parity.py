@@ -296,3 +296,29 @@ def test_fleet_mc1024_matches_oracle_monte_carlo(gpu_ctx):
     differ = np.nonzero(rec[:, 11] != R[:, 11])[0]
     assert len(differ) <= 8, differ
     assert np.all(np.mod(rec[differ, 11] - R[differ, 11], 25) == 0)
+
+
+def test_fleet_shards_reproduce_the_whole_fleet(gpu_ctx):
+    """Sharding invariance: the landings of BASELINE configs[3] flown
+    as two shard fleets, [0, 512) and [512, 1024) (initial conditions by global
+    index, as each rank of run_monte_carlo builds its shard), give records and
+    states bit-identical to one 1024-landing fleet -- and a ragged 3-way split
+    of the first 100 landings, fleets of 34 / 33 / 33, to one 100-landing fleet."""
+    from gp_mpc_rocket_landing_amd.fleet import Fleet, fit_gp, initial_conditions
+    from gp_mpc_rocket_landing_amd.sharding import shard_range
+    gp = fit_gp(gpu_ctx, n_train=1000)
+
+    def fly(first, count, steps=60):
+        f = Fleet(gpu_ctx, gp, count, max_steps=300)
+        try:
+            f.reset(initial_conditions(count, first=first))
+            f.step(steps)
+            return f.read()
+        finally:
+            f.close()
+
+    for total, world in ((1024, 2), (100, 3)):
+        whole_r, whole_x = fly(0, total)
+        parts = [fly(*shard_range(total, r, world)) for r in range(world)]
+        np.testing.assert_array_equal(np.concatenate([p[0] for p in parts]), whole_r)
+        np.testing.assert_array_equal(np.concatenate([p[1] for p in parts]), whole_x)

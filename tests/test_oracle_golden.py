@@ -210,3 +210,18 @@ def test_oracle_lml_and_optimiser_vs_f10():
     assert r["success"] and bool(f["ref_success"])
     assert abs(r["log_marginal_likelihood"] - float(f["ref_lml"])) < 1e-8 * abs(float(f["ref_lml"]))
     assert np.max(np.abs(p - f["ref_params"])) < 1e-2
+
+
+def test_f11_kernel_gradients():
+    """Oracle gradient restatement vs the reference's gradients (F11)."""
+    f = golden("f11_kernel_gradients.npz")
+    X1, X2, ls, s2 = f["X1"], f["X2"], f["ls"], float(f["sigma2"])
+    for name, kind, l in (("se_ard", "se_ard", ls), ("se_iso", "se_iso", f["iso_l"]),
+                          ("matern32", "matern32", ls), ("matern52", "matern52", ls)):
+        g = gp_oracle.gram_gradients(kind, X1, X2, s2, l)
+        assert len(g) == len(f[f"{name}_x12_names"])
+        for j, gj in enumerate(g):
+            np.testing.assert_allclose(gj, f[f"{name}_x12_{j}"], rtol=1e-12, atol=1e-14)
+    g = gp_oracle.gram_gradients("se_ard", X1, None, s2, ls)
+    for j, gj in enumerate(g):
+        np.testing.assert_allclose(gj, f[f"se_ard_x11_{j}"], rtol=1e-12, atol=1e-14)

@@ -65,3 +65,46 @@ def test_gather_records_world2_gloo(total):
         p.join(timeout=120)
         assert p.exitcode == 0
     np.testing.assert_array_equal(out, _records_for(0, total))
+
+
+def _fleet_records_worker(rank, world, total, port, q):
+    """A rank's shard of real landings, flown by the CPU closed loop (the fleet's
+    oracle, monte_carlo.py:401-583 restated), then the one gather."""
+    import torch.distributed as dist
+    from threadpoolctl import threadpool_limits
+    from gp_mpc_rocket_landing_amd.data import synthetic_training_data
+    from gp_mpc_rocket_landing_amd.fleet import initial_conditions
+    from gp_mpc_rocket_landing_amd.sharding import gather_records
+    from oracle import gp_oracle, mc_oracle
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    first, count = shard_range(total, rank, world)
+    with threadpool_limits(1):
+        X, U, D = synthetic_training_data(1000, seed=0)
+        st = gp_oracle.exact_fit(gp_oracle.features_3dof(X, U), D)
+        x0 = initial_conditions(count, first=first)
+        rec = np.array([mc_oracle.closed_loop_landing(st, x)[0] for x in x0]).reshape(count, 16)
+    out = gather_records(rec, total)
+    if rank == 0:
+        q.put(out)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_gather_real_landing_records_world2_gloo():
+    """Two ranks each fly their contiguous (ragged: 4 + 3) shard of BASELINE
+    configs[3] landings to termination and gather the records: rank 0 holds
+    exactly the single-process Monte-Carlo's records (mc_oracle_1024.npz)."""
+    from conftest import golden
+    total = 7
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_fleet_records_worker, args=(r, 2, total, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    out = q.get(timeout=240)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    np.testing.assert_array_equal(out, golden("mc_oracle_1024.npz")["records"][:total])
