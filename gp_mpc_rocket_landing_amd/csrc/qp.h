@@ -9,7 +9,7 @@
 // 80 KB and two workgroups share a CU
 #define QP_NMAX 216
 #define QP_MMAX 360
-#define QP_NNZMAX 736
+#define QP_NNZMAX 896
 #define QP_W 16
 typedef QPSmem<QP_NMAX, QP_MMAX, QP_NNZMAX, QP_W> QPSmemStd;
 // factor slots available in QPSmem (its factor area minus the 4 zero columns)
