@@ -134,6 +134,10 @@ def cpu_baseline(seconds, n_train=1000, horizon=20, workers=None):
     st1, el1 = _cpu_landing_loop(min(5.0, seconds), n_train, horizon, 42, workers)
     return dict(value=steps / el, unit="control steps/s", cores=workers, kind="port",
                 per_core=round(per_core, 3),
+                # the box grants this job a 16-core share of its CPUs, so a whole
+                # socket cannot be run here; landings are independent single-
+                # threaded processes, so per-core x cores is its upper bound
+                socket_64c_extrapolated=round(per_core * 64, 1),
                 single_landing_all_cores=round(st1 / el1, 3),
                 sample=f"{workers} processes x 1 landing closed loop, {steps} control steps in "
                        f"{el:.1f} s (numpy/scipy GP N={n_train}, P={horizon}; numpy QP assembly; "
@@ -252,9 +256,9 @@ def lml_bench(ctx, n=1000, sets=14, reps=3, cpu=True):
     (the reference's per-set ExactGP.fit, one host core)."""
     from gp_mpc_rocket_landing_amd import _lib
     from gp_mpc_rocket_landing_amd.data import synthetic_training_data
-    from oracle import gp_oracle
+    from gp_mpc_rocket_landing_amd.gp.features import Simple3DoFFeatureExtractor
     X, U, D = synthetic_training_data(n, seed=0)
-    Z = gp_oracle.features_3dof(X, U)
+    Z = Simple3DoFFeatureExtractor().extract_batch(X, U)
     rs = np.random.RandomState(2)
     P = np.concatenate([np.zeros(12), [np.log(1e-4)]]) + 0.2 * rs.normal(size=(sets, 13))
     ts = []
@@ -267,6 +271,7 @@ def lml_bench(ctx, n=1000, sets=14, reps=3, cpu=True):
            "ms": round(min(ts) * 1e3, 3), "gradients_per_s": round(1.0 / min(ts), 2)}
     if cpu:
         from threadpoolctl import threadpool_limits
+        from oracle import gp_oracle   # the CPU leg: the restatement, timed as the baseline
         with threadpool_limits(1):
             t0 = time.perf_counter()
             ref = [gp_oracle.lml_at(Z, D[:, 1], np.exp(p[0]), np.exp(p[1:-1]), np.exp(p[-1]))[0] for p in P]
@@ -282,9 +287,9 @@ def append_bench(ctx, n=1000, k=10, reps=3):
     device refit of the n + k rows it is equivalent to (host-boundary times)."""
     from gp_mpc_rocket_landing_amd import _lib
     from gp_mpc_rocket_landing_amd.data import synthetic_training_data
-    from oracle import gp_oracle
+    from gp_mpc_rocket_landing_amd.gp.features import Simple3DoFFeatureExtractor
     X, U, D = synthetic_training_data(n + k, seed=0)
-    Z = gp_oracle.features_3dof(X, U)
+    Z = Simple3DoFFeatureExtractor().extract_batch(X, U)
     ta, tf = [], []
     for _ in range(reps):
         h = _lib.ExactGPHandle(ctx, _lib.SE_ARD, Z[:n], D[:n], np.ones(11), 1.0, 1e-4)
@@ -299,6 +304,98 @@ def append_bench(ctx, n=1000, k=10, reps=3):
     return {"workload": f"append {k} rows to the n = {n} exact GP (3 outputs)",
             "append_ms": round(min(ta) * 1e3, 3), "refit_ms": round(min(tf) * 1e3, 3),
             "speedup": round(min(tf) / min(ta), 2)}
+
+
+def simple3dof_gp_bench(ctx, n=1000, p=20, reps=5, cpu=True):
+    """BASELINE configs[1] / SURVEY 8d C2: the Simple3DoFGP(use_sparse=False)
+    surface -- add_data(N = 1000) + fit() (features, Gram, Cholesky with the
+    jitter ladder, alpha, W = L^-1, LML; 3 outputs, one shared factor) and
+    predict_batch of the P = 20 horizon points -- on the GPU (host-boundary
+    times: H2D inputs and D2H results included), next to the CPU restatement
+    (numpy/scipy with the reference's LAPACK calls) on all the box's BLAS
+    threads.  Best of ``reps``."""
+    from threadpoolctl import threadpool_limits
+    from gp_mpc_rocket_landing_amd.data import query_points, synthetic_training_data
+    from gp_mpc_rocket_landing_amd.gp import Simple3DoFGP
+    X, U, D = synthetic_training_data(n, seed=0)
+    Xq, Uq = query_points(X, U, p, seed=7)
+    tf, tp = [], []
+    for _ in range(reps):
+        gp = Simple3DoFGP(use_sparse=False)
+        gp.add_data(X, U, D)
+        t0 = time.perf_counter(); gp.fit(); tf.append(time.perf_counter() - t0)
+        t0 = time.perf_counter(); m, v = gp.predict_batch(Xq, Uq); tp.append(time.perf_counter() - t0)
+    out = {"workload": f"Simple3DoFGP(use_sparse=False) fit N={n} + predict {p} points (3 outputs)",
+           "fit_ms": round(min(tf) * 1e3, 3), "predict_ms": round(min(tp) * 1e3, 3)}
+    if cpu:
+        from oracle import gp_oracle   # the CPU leg: the restatement, timed as the baseline
+        threads = max(1, min(16, len(os.sched_getaffinity(0))))
+        cf, cp = [], []
+        with threadpool_limits(threads):
+            for _ in range(max(2, reps // 2)):
+                t0 = time.perf_counter()
+                st = gp_oracle.exact_fit(gp_oracle.features_3dof(X, U), D)
+                cf.append(time.perf_counter() - t0)
+                t0 = time.perf_counter()
+                mo, vo = gp_oracle.exact_predict(st, gp_oracle.features_3dof(Xq, Uq))
+                cp.append(time.perf_counter() - t0)
+        out.update(cpu_fit_ms=round(min(cf) * 1e3, 3), cpu_predict_ms=round(min(cp) * 1e3, 3),
+                   cpu_threads=threads, fit_speedup=round(min(cf) / min(tf), 2),
+                   predict_speedup=round(min(cp) / min(tp), 2),
+                   max_rel_mean_diff=float(np.max(np.abs(m - mo) / np.maximum(np.abs(mo), st["y_std"]))))
+    return out
+
+
+def single_landing_bench(ctx, gp, steps=100, reps=3):
+    """BASELINE configs[2] / SURVEY 8d C3: ONE closed-loop landing (seed 42,
+    108 control steps to touchdown) on one MI355X -- the fleet with B = 1, every
+    control step = features + K* Gram, variance/mean GEMM, QP + ADMM + plant
+    (the 1024-landing step's kernels at batch 1).  Times ``steps`` steps from
+    the initial state (device-resident, one sync at the end)."""
+    from gp_mpc_rocket_landing_amd.fleet import Fleet, initial_conditions
+    f = Fleet(ctx, gp, 1)
+    ts = []
+    try:
+        x0 = initial_conditions(1)
+        for _ in range(reps):
+            f.reset(x0)
+            ctx.sync()
+            t0 = time.perf_counter()
+            f.step(steps)
+            ctx.sync()
+            ts.append(time.perf_counter() - t0)
+        rec, _ = f.read()
+    finally:
+        f.close()
+    t = min(ts)
+    return {"workload": "1 landing (seed 42), GP N=1000 + RTI QP per step, fleet B=1",
+            "steps": int(rec[0, 1]), "us_per_step": round(t / steps * 1e6, 2),
+            "steps_per_s": round(steps / t, 1)}
+
+
+def qp_status_histogram(fl, steps=10):
+    """Status of every landing's QP over ``steps`` further control steps of the
+    bench fleet (untimed): solved / solved inaccurate / maximum iterations
+    reached, and the ADMM iteration counts (25 or 50: termination is checked
+    every 25 iterations, max_iter 50)."""
+    from gp_mpc_rocket_landing_amd.fleet import REC_ADMM_ITERS, REC_LAST_STATUS, REC_OUTCOME
+    names = {1: "solved", 2: "solved_inaccurate", -2: "max_iter_reached"}
+    hist, iters = {}, {}
+    rec0, _ = fl.read()
+    for _ in range(steps):
+        fl.step(1)
+        rec1, _ = fl.read()
+        run = (rec0[:, REC_OUTCOME] == 0) & (rec1[:, 1] > rec0[:, 1])
+        for s_, c in zip(*np.unique(rec1[run, REC_LAST_STATUS].astype(int), return_counts=True)):
+            k = names.get(int(s_), str(int(s_)))
+            hist[k] = hist.get(k, 0) + int(c)
+        d = (rec1[run, REC_ADMM_ITERS] - rec0[run, REC_ADMM_ITERS]).astype(int)
+        for s_, c in zip(*np.unique(d, return_counts=True)):
+            iters[str(int(s_))] = iters.get(str(int(s_)), 0) + int(c)
+        rec0 = rec1
+    tot = max(1, sum(hist.values()))
+    return {"solves": tot, "status": hist, "status_frac": {k: round(v / tot, 4) for k, v in hist.items()},
+            "admm_iterations": iters}
 
 
 def structured_fitc_bench(ctx, reps=2):
@@ -488,8 +585,11 @@ def main():
         if all_rec is not None:
             oc = all_rec[:, 0]
             out["outcomes"] = {str(int(c)): int(np.sum(oc == c)) for c in np.unique(oc)}
+        out["qp_status"] = qp_status_histogram(fl)
         if not args.no_chol:
             try:
+                out["single_landing"] = single_landing_bench(ctx, gp)
+                out["simple3dof_gp"] = simple3dof_gp_bench(ctx, cpu=not args.no_cpu)
                 out["cholesky"] = cholesky_bench(ctx, torch)
                 out["structured_fitc"] = structured_fitc_bench(ctx)
                 out["lml_batched"] = lml_bench(ctx, cpu=not args.no_cpu)
