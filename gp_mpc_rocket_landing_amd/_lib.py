@@ -67,7 +67,8 @@ class QPSettings(ctypes.Structure):
 class FleetConfig(ctypes.Structure):
     _fields_ = [("horizon", ctypes.c_int), ("dt", ctypes.c_double), ("target_mode", ctypes.c_int),
                 ("use_gp", ctypes.c_int), ("residual_model", ctypes.c_int),
-                ("max_steps", ctypes.c_int), ("qp", QPSettings)]
+                ("max_steps", ctypes.c_int), ("qp", QPSettings),
+                ("sqp_iters", ctypes.c_int), ("sqp_tol", ctypes.c_double)]
 
 
 def _sig(name, res, *args):

@@ -49,6 +49,8 @@ struct gpmpc_fleet {
   bool use_fq = true;                        // fleet-specialised solver (GPMPC_FLEET_SOLVER=0: generic)
   int alt_wave = 0;                          // GPMPC_FLEET_ALTWAVE=1: alternate the chain wave
   DevBuf claims;                             // per-CU chain-SIMD claims (k_fleet_control2)
+  DevBuf sqp_done;                           // SQP mode: landing converged this control step
+  int sqp_it = 0;                            // SQP mode: pass of the current control step
   unsigned epoch = 0;                        // control launches so far (claim generation)
   bool simd_pick = true;                     // GPMPC_FLEET_SIMD=0: chain on wave 0 always
   bool fuse_post = true;                     // GPMPC_FLEET_FUSE_POST=0: separate k_post_finish
@@ -76,6 +78,8 @@ extern "C" void gpmpc_fleet_default_config(gpmpc_fleet_config *c) {
   c->residual_model = 1;
   c->max_steps = 300;        // run_experiments.py SimulationConfig max_time 30 s / dt
   gpmpc_qp_default_settings(&c->qp);
+  c->sqp_iters = 1;          // RTI; > 1: GPMPC.solve's loop (gp_mpc.py:296-345)
+  c->sqp_tol = 1e-4;         // gp_mpc.py:343
 }
 
 // ---------------------------------------------------------------------------
@@ -193,6 +197,10 @@ struct FleetArgs {
   int *lastit;          // ADMM iterations of each landing's last solve
   unsigned long long *stamps;  // diagnostic phase cycles of block 0 (or null)
   unsigned long long *trace;   // diagnostic per-landing placement/timing (or null)
+  // SQP pass of GPMPC.solve's loop (gp_mpc.py:296-345; sqp = 0: RTI)
+  int sqp, sqp_first, sqp_last;
+  double sqp_tol;
+  int *sqp_done;               // landing converged in an earlier pass of this control step
 };
 
 __global__ __launch_bounds__(256) void k_fleet_control(FleetArgs a) {
@@ -422,6 +430,7 @@ __global__ __launch_bounds__(FQ_T) __attribute__((amdgpu_waves_per_eu(2, 2))) vo
   const double dt = a.dt;
   double *rec = a.rec + (int64_t)b * GPMPC_REC_LEN;
   if (rec[0] != 0.0) return;  // terminated landing
+  if (a.sqp && !a.sqp_first && a.sqp_done[b]) return;  // converged in an earlier SQP pass
   QPStamps T;
   T.out = (STAMPS && b == 0) ? a.stamps : nullptr;
   T.start();
@@ -469,11 +478,13 @@ __global__ __launch_bounds__(FQ_T) __attribute__((amdgpu_waves_per_eu(2, 2))) vo
     const double m0 = rec[13];
     bool div = false;
     for (int i = 0; i < NX; ++i) div = div || !(fabs(sx[i]) <= 1e6);
-    if ((int)rec[1] >= a.max_steps) out = 5;
+    if (a.sqp && !a.sqp_first) out = 0;  // later SQP passes: same state, checks done
+    else if ((int)rec[1] >= a.max_steps) out = 5;
     else if (sx[1] < 0.0) out = 2;
     else if (sx[0] <= 1.0 + 0.01) out = 3;
     else if (div) out = 6;
     else if (sx[1] < 1.0 && fabs(sx[4]) < 5.0) out = landing_ok(sx, m0) ? 1 : 4;
+    if (a.sqp && a.sqp_first) a.sqp_done[b] = 0;
     s_out = out;
     for (int i = 0; i < NX; ++i) st_tgt[i] = a.target_mode ? sx[i] : a.xt[(int64_t)b * NX + i];
     if (a.target_mode) {
@@ -613,6 +624,64 @@ __global__ __launch_bounds__(FQ_T) __attribute__((amdgpu_waves_per_eu(2, 2))) vo
     }
     return;
   }
+  if (a.sqp) {
+    // GPMPC.solve's loop (gp_mpc.py:336-353): the change of the trajectory,
+    // X_pred <- X_new (no shift), stop below sqp_tol
+    double dm[1] = {0.0};
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+      if (R.vok[h]) {
+        const int j = R.vj[h], i = (j >= Nv) ? j - Nv : j % (NX + NU), k = j / (NX + NU);
+        const double old = (j >= Nv) ? Xw[N * NX + i] : (i < NX ? Xw[k * NX + i] : Uw[k * NU + i - NX]);
+        dm[0] = fmax(dm[0], fabs(s.rhs[j] - old));
+      }
+    fq_max<1>(dm, s.red);  // (its barriers order the reads of Xw / Uw before the writes)
+    for (int e = tid; e < (N + 1) * NX; e += FQ_T) {
+      const int k = e / NX, i = e - k * NX;
+      Xw[e] = s.rhs[(k == N) ? Nv + i : k * (NX + NU) + i];
+    }
+    for (int e = tid; e < N * NU; e += FQ_T) {
+      const int k = e / NU, i = e - k * NU;
+      Uw[e] = s.rhs[k * (NX + NU) + NX + i];
+    }
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      if (R.rok[h]) a.ysc[(int64_t)b * m + R.rr[h]] = R.yr(h);
+      if (R.vok[h]) a.ysc[(int64_t)b * m + MD + R.vj[h]] = R.yb[h];
+    }
+    if (tid == 0) {
+      const bool conv = dm[0] < a.sqp_tol;
+      a.rho[b] = s.rho_s;
+      rec[11] += res.iter;
+      a.lastit[b] = res.iter;
+      rec[12] += (res.status == 1) ? 1.0 : 0.0;
+      rec[14] = res.status;
+      rec[15] = s.rho_s;
+      if (conv) {
+        const double u0[NU] = {s.rhs[NX], s.rhs[NX + 1], s.rhs[NX + 2]};
+        double xn[NX], dr[3];
+        plant_euler(sx, u0, dt, xn);
+        if (a.residual_model) {
+          drag_residual(sx, dr);
+          xn[4] += dr[0] * dt; xn[5] += dr[1] * dt; xn[6] += dr[2] * dt;
+        }
+        for (int i = 0; i < NX; ++i) x[i] = xn[i];
+        rec[1] += 1.0;
+        rec[3] = rec[1] * dt;
+        rec[2] = rec[13] - xn[0];
+        for (int i = 0; i < NX; ++i) rec[4 + i] = xn[i];
+        a.sqp_done[b] = 1;
+      } else if (a.sqp_last) {  // MPCSolution.success False -> DIVERGENCE (monte_carlo.py:506-508)
+        rec[0] = 6;
+        rec[2] = rec[13] - sx[0];
+        for (int i = 0; i < NX; ++i) rec[4 + i] = sx[i];
+      }
+    }
+    T.mark(7);
+    T.flush();
+    if (a.trace && tid == 0) a.trace[(int64_t)b * 4 + 1] = __builtin_amdgcn_s_memrealtime();
+    return;
+  }
   if (has) {
     for (int e = tid; e < (N + 1) * NX; e += FQ_T) {
       const int k = e / NX, i = e - k * NX;
@@ -737,7 +806,7 @@ extern "C" int gpmpc_fleet_create(gpmpc_ctx *ctx, gpmpc_gp *gp, const gpmpc_flee
       f->part.alloc(sizeof(double) * nrt * P) || f->meanT.alloc(sizeof(double) * 3 * P) ||
       f->mean.alloc(sizeof(double) * P * 3) || f->var.alloc(sizeof(double) * P * 3) ||
       f->order.alloc(sizeof(int) * B) || f->lastit.alloc(sizeof(int) * B) ||
-      f->claims.alloc(sizeof(unsigned) * 4096)) {
+      f->claims.alloc(sizeof(unsigned) * 4096) || f->sqp_done.alloc(sizeof(int) * B)) {
     delete f;
     gpmpc_set_error("fleet: out of device memory");
     return -1;
@@ -748,6 +817,7 @@ extern "C" int gpmpc_fleet_create(gpmpc_ctx *ctx, gpmpc_gp *gp, const gpmpc_flee
   hipMemcpyAsync(f->rec.p, r.data(), sizeof(double) * r.size(), hipMemcpyHostToDevice, ctx->stream);
   hipMemsetAsync(f->lastit.p, 0, sizeof(int) * B, ctx->stream);
   hipMemsetAsync(f->claims.p, 0, sizeof(unsigned) * 4096, ctx->stream);
+  hipMemsetAsync(f->sqp_done.p, 0, sizeof(int) * B, ctx->stream);
   {  // identity dispatch order until the first order kernel (every slot maps in range)
     std::vector<int> id(B);
     for (size_t b = 0; b < B; ++b) id[b] = (int)b;
@@ -766,6 +836,11 @@ extern "C" int gpmpc_fleet_create(gpmpc_ctx *ctx, gpmpc_gp *gp, const gpmpc_flee
   // the specialised solver assumes the N = 20 stage layout of its LDS caps
   f->use_fq = (!se || atoi(se) != 0) && N == 20 && f->pat.mode == 1 && f->pat.nblk == FQ_NBLK &&
               m - n == FQ_MD && f->pat.nnz - n == FQ_NNZD;
+  if (cfg->sqp_iters > 1 && !f->use_fq) {  // the SQP pass is implemented in k_fleet_control2
+    delete f;
+    gpmpc_set_error("fleet: sqp_iters > 1 needs the fleet solver (N = 20, GPMPC_FLEET_SOLVER != 0)");
+    return -2;
+  }
   GPMPC_HIP(hipStreamSynchronize(ctx->stream));
   *out = f;
   return 0;
@@ -950,6 +1025,11 @@ static FleetArgs fleet_args(gpmpc_fleet *f) {
   a.lastit = f->lastit.as<int>();
   a.stamps = f->stamps;
   a.trace = f->trace;
+  a.sqp = f->cfg.sqp_iters > 1;
+  a.sqp_first = f->sqp_it == 0;
+  a.sqp_last = f->sqp_it >= f->cfg.sqp_iters - 1;
+  a.sqp_tol = f->cfg.sqp_tol;
+  a.sqp_done = f->sqp_done.as<int>();
   return a;
 }
 
@@ -963,8 +1043,8 @@ extern "C" int gpmpc_fleet_step_phases(gpmpc_fleet *f, int phase_mask) {
   GPMPC_HIP(hipSetDevice(f->ctx->device));
   // the dispatch order of this step, before the GP phase when there is one:
   // the posterior rows then follow the same slots as the control workgroups
-  const bool order_now = f->use_order && ((f->cfg.use_gp && (phase_mask & 1)) ||
-                                          (!f->cfg.use_gp && (phase_mask & 2)));
+  const bool order_now = f->use_order && f->sqp_it == 0 &&
+                         ((f->cfg.use_gp && (phase_mask & 1)) || (!f->cfg.use_gp && (phase_mask & 2)));
   if (order_now)
     hipLaunchKernelGGL(k_fleet_order, dim3(1), dim3(1024), 0, f->ctx->stream, f->B,
                        f->rec.as<double>(), f->lastit.as<int>(), f->order.as<int>());
@@ -990,9 +1070,17 @@ extern "C" int gpmpc_fleet_step_phases(gpmpc_fleet *f, int phase_mask) {
 
 extern "C" int gpmpc_fleet_step(gpmpc_fleet *f, int nsteps) {
   GPMPC_CHECK_ARG(f && nsteps >= 0);
+  const int passes = f->cfg.sqp_iters > 1 ? f->cfg.sqp_iters : 1;
   for (int it = 0; it < nsteps; ++it) {
-    const int rc = gpmpc_fleet_step_phases(f, 15);
-    if (rc) return rc;
+    // SQP mode: every pass re-linearises around the last QP solution (GP
+    // posterior at the new horizon points, QP); landings that converged skip
+    // the later passes' control launches
+    for (int p = 0; p < passes; ++p) {
+      f->sqp_it = p;
+      const int rc = gpmpc_fleet_step_phases(f, 15);
+      if (rc) { f->sqp_it = 0; return rc; }
+    }
+    f->sqp_it = 0;
   }
   return 0;
 }

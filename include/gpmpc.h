@@ -197,6 +197,14 @@ typedef struct {
   int residual_model;    /* 1: plant gets the aero-drag residual (dispersion.py:349-360) */
   int max_steps;         /* max_time / dt */
   gpmpc_qp_settings qp;
+  int sqp_iters;         /* 1: RTI, one QP per control step (the bench metric).
+                            > 1: GPMPC.solve's loop (gp_mpc.py:296-345): up to sqp_iters
+                            re-linearise -> GP posterior -> QP passes around the last QP
+                            solution, stop when max|dX|, max|dU| < sqp_tol; not converged
+                            -> MPCSolution.success False -> DIVERGENCE (monte_carlo.py
+                            :506-508).  The warm start is the unshifted plan (gp_mpc.py
+                            :358-359). */
+  double sqp_tol;        /* 1e-4 (gp_mpc.py:343) */
 } gpmpc_fleet_config;
 void gpmpc_fleet_default_config(gpmpc_fleet_config *c);
 int gpmpc_fleet_create(gpmpc_ctx *ctx, gpmpc_gp *gp, const gpmpc_fleet_config *cfg, int batch,

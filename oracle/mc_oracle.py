@@ -95,7 +95,7 @@ def new_landing(x0, horizon=20):
 
 
 def landing_step(st, S, max_steps=300, dt=0.1, cfg=RUN_EXPERIMENTS_CFG, use_gp=True,
-                 residual_model=True):
+                 residual_model=True, sqp_iters=1, sqp_tol=1e-4, qp_settings=None):
     """One pass of the run_single loop body (monte_carlo.py:455-537) under the
     solve protocol (:495-512) with the 3-DoF GPMPC adapter as the controller,
     from the full state S (new_landing / Fleet.state() layout).  Returns the
@@ -111,8 +111,18 @@ def landing_step(st, S, max_steps=300, dt=0.1, cfg=RUN_EXPERIMENTS_CFG, use_gp=T
     * a solve without a solution -> DIVERGENCE (:506-508);
     * plant step with the pre-step drag residual, plan shifted (X[1:], X[-1]).
 
-    Also returns (iterations, status) of the solve, or None at termination.
+    ``sqp_iters`` > 1: GPMPC.solve's loop (gp_mpc.py:296-353) instead of the RTI
+    step -- up to sqp_iters passes of GP mean at the current plan, QP linearised
+    around it (warm start = the plan, persistent rho / y), plan <- QP solution
+    (no shift); stop when max|dX| and max|dU| < sqp_tol, then the plant takes
+    U[0]; not converged -> success False -> DIVERGENCE.  Every pass's ADMM
+    iterations go to rec[11].
+
+    Also returns (iterations, status) of the (last) solve, or None at termination.
     """
+    if sqp_iters > 1:
+        return _sqp_landing_step(st, S, max_steps, dt, cfg, use_gp, residual_model, sqp_iters, sqp_tol,
+                                 qp_settings)
     from . import admm_ref, gp_oracle, qp_oracle
 
     x = S["x"].copy(); Xw = S["Xw"].copy(); Uw = S["Uw"].copy(); rec = S["rec"].copy()
@@ -133,7 +143,7 @@ def landing_step(st, S, max_steps=300, dt=0.1, cfg=RUN_EXPERIMENTS_CFG, use_gp=T
         mean, _var = gp_oracle.exact_predict(st, gp_oracle.features_3dof(Xw[:-1], Uw))
     P0, q = qp_oracle.cost(N, np.tile(tgt, (N + 1, 1)))
     A, l, u = qp_oracle.constraints(Xw, Uw, x, dt, gp_dv=mean, sign=-1.0, filter_small=False)
-    qp = admm_ref.RefQP(len(out["y"]))
+    qp = admm_ref.RefQP(len(out["y"]), settings=qp_settings)
     qp.y = out["y"]; qp.rho = np.array([out["rho"]])
     try:
         r = qp.solve(P0.diagonal(), q, A, l, u, qp_oracle.to_vector(Xw, Uw))
@@ -158,6 +168,68 @@ def landing_step(st, S, max_steps=300, dt=0.1, cfg=RUN_EXPERIMENTS_CFG, use_gp=T
     rec[14] = r["status"]
     rec[15] = qp.rho[0]
     return out, (r["iter"], r["status"])
+
+
+def _sqp_landing_step(st, S, max_steps, dt, cfg, use_gp, residual_model, sqp_iters, sqp_tol,
+                      qp_settings=None):
+    """The sqp_iters > 1 branch of landing_step (gp_mpc.py:296-353)."""
+    from . import admm_ref, gp_oracle, qp_oracle
+
+    x = S["x"].copy(); Xw = S["Xw"].copy(); Uw = S["Uw"].copy(); rec = S["rec"].copy()
+    N = Uw.shape[0]
+    m0 = rec[13]
+    out = dict(x=x, Xw=Xw, Uw=Uw, y=S["y"].copy(), rho=float(S["rho"]), rec=rec)
+    if rec[0] != 0:
+        return out, None
+    o = TIMEOUT if rec[1] >= max_steps else pre_step_outcome(x, m0, cfg)
+    if o:
+        rec[0] = o
+        rec[2] = m0 - x[0]
+        rec[4:11] = x
+        return out, None
+    tgt = incremental_target(x)
+    P0, q = qp_oracle.cost(N, np.tile(tgt, (N + 1, 1)))
+    qp = admm_ref.RefQP(len(out["y"]), settings=qp_settings)
+    qp.y = out["y"]; qp.rho = np.array([out["rho"]])
+    info = None
+    for it in range(sqp_iters):
+        mean = None
+        if use_gp:
+            mean, _var = gp_oracle.exact_predict(st, gp_oracle.features_3dof(Xw[:-1], Uw))
+        A, l, u = qp_oracle.constraints(Xw, Uw, x, dt, gp_dv=mean, sign=-1.0, filter_small=False)
+        try:
+            r = qp.solve(P0.diagonal(), q, A, l, u, qp_oracle.to_vector(Xw, Uw))
+        except RuntimeError:
+            rec[0] = DIVERGENCE; rec[14] = -100; rec[2] = m0 - x[0]; rec[4:11] = x
+            out.update(Xw=Xw, Uw=Uw, y=qp.y, rho=float(qp.rho[0]))
+            return out, (0, -100)
+        info = (r["iter"], r["status"])
+        if r["status"] not in (1, 2, -2):
+            rec[0] = DIVERGENCE; rec[14] = r["status"]; rec[2] = m0 - x[0]; rec[4:11] = x
+            out.update(Xw=Xw, Uw=Uw, y=qp.y, rho=float(qp.rho[0]))
+            return out, info
+        Xo, Uo = qp_oracle.from_vector(r["x"], N)
+        conv = max(np.max(np.abs(Xo - Xw)), np.max(np.abs(Uo - Uw))) < sqp_tol
+        Xw, Uw = Xo, Uo
+        rec[11] += r["iter"]
+        rec[12] += r["status"] == 1
+        rec[14] = r["status"]
+        rec[15] = qp.rho[0]
+        if conv:
+            dr = qp_oracle.drag_residual(x) if residual_model else np.zeros(3)
+            xn = qp_oracle.plant_step(x, Uo[0], dt)
+            xn[4:7] += dr * dt
+            rec[1] += 1
+            rec[2] = m0 - xn[0]
+            rec[3] = rec[1] * dt
+            rec[4:11] = xn
+            out.update(x=xn, Xw=Xw, Uw=Uw, y=qp.y, rho=float(qp.rho[0]))
+            return out, info
+    rec[0] = DIVERGENCE              # MPCSolution.success False (monte_carlo.py:506-508)
+    rec[2] = m0 - x[0]
+    rec[4:11] = x
+    out.update(Xw=Xw, Uw=Uw, y=qp.y, rho=float(qp.rho[0]))
+    return out, info
 
 
 def closed_loop_landing(st, x0, max_steps=300, horizon=20, **kw):

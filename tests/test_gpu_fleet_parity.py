@@ -322,3 +322,57 @@ def test_fleet_shards_reproduce_the_whole_fleet(gpu_ctx):
         parts = [fly(*shard_range(total, r, world)) for r in range(world)]
         np.testing.assert_array_equal(np.concatenate([p[0] for p in parts]), whole_r)
         np.testing.assert_array_equal(np.concatenate([p[1] for p in parts]), whole_x)
+
+
+def test_fleet_sqp_mode_matches_oracle(gpu_ctx):
+    """GPMPC.solve's loop on the fleet (sqp_iters > 1; gp_mpc.py:296-353): per
+    pass, GP mean at the current plan, QP linearised around it, plan <- QP
+    solution (no shift), stop when max|dX|, max|dU| < sqp_tol; the plant takes
+    U[0] of the converged plan; not converged after sqp_iters passes ->
+    DIVERGENCE.  Every control step of 8 landings against mc_oracle.landing_step
+    with the same loop, from the device's own previous state: outcome, steps,
+    ADMM iteration totals over all passes, solved count and last status exact;
+    state, plan, rho and duals within the tolerance spec.  sqp_tol = 1.0 lets
+    the loop converge after a few passes (the plant branch); with the
+    reference's 1e-4 the 1e-4 ADMM never converges the loop in 10 passes (the
+    lateral thrust of consecutive plans moves by ~0.3), so every landing ends
+    DIVERGENCE at its first step -- on both sides."""
+    from gp_mpc_rocket_landing_amd.data import synthetic_training_data
+    from gp_mpc_rocket_landing_amd.fleet import Fleet, fit_gp, initial_conditions
+    from oracle import gp_oracle, mc_oracle
+
+    X, U, D = synthetic_training_data(1000, seed=0)
+    st = gp_oracle.exact_fit(gp_oracle.features_3dof(X, U), D)
+    nb = 8
+    x0 = initial_conditions(nb)
+    gp = fit_gp(gpu_ctx, n_train=1000)
+    for tol, steps in ((1.0, 25), (1e-4, 2)):
+        fl = Fleet(gpu_ctx, gp, nb, max_steps=300, sqp_iters=10, sqp_tol=tol)
+        moved = 0
+        try:
+            fl.reset(x0)
+            S = fl.state()
+            for k in range(steps):
+                if np.all(S["rec"][:, 0] != 0):
+                    break
+                fl.step(1)
+                T = fl.state()
+                for b in np.nonzero(S["rec"][:, 0] == 0)[0]:
+                    want, info = mc_oracle.landing_step(st, _landing(S, b), sqp_iters=10, sqp_tol=tol)
+                    got = _landing(T, b)
+                    tag = (tol, k, int(b))
+                    np.testing.assert_array_equal(got["rec"][[0, 1, 11, 12, 13, 14]],
+                                                  want["rec"][[0, 1, 11, 12, 13, 14]], err_msg=str(tag))
+                    moved += int(got["rec"][1] > S["rec"][b, 1])
+                    for key in ("x", "Xw", "Uw"):
+                        ok, worst = close(got[key], want[key], 1.0)
+                        assert ok, (tag, key, worst)
+                    ok, worst = close(got["rho"], want["rho"], 0.0); assert ok, (tag, "rho", worst)
+                    ok, worst = close(got["y"], want["y"], np.abs(want["y"]).max()); assert ok, (tag, "y", worst)
+                S = T
+        finally:
+            fl.close()
+        if tol == 1e-4:
+            assert np.all(S["rec"][:, 0] == 6) and np.all(S["rec"][:, 1] == 0)
+        else:
+            assert moved > nb, moved   # the converged branch (plant step) ran
