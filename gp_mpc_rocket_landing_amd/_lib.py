@@ -64,6 +64,11 @@ class QPSettings(ctypes.Structure):
                 ("warm_start", ctypes.c_int)]
 
 
+class Rollout6Config(ctypes.Structure):
+    _fields_ = [("horizon", ctypes.c_int), ("dt", ctypes.c_double), ("max_steps", ctypes.c_int),
+                ("qp", QPSettings)]
+
+
 class FleetConfig(ctypes.Structure):
     _fields_ = [("horizon", ctypes.c_int), ("dt", ctypes.c_double), ("target_mode", ctypes.c_int),
                 ("use_gp", ctypes.c_int), ("residual_model", ctypes.c_int),
@@ -121,6 +126,13 @@ _sig("gpmpc_gram_grad", _c, _vp, _c, _dp, _c, _dp, _c, _c, _dp, ctypes.c_double,
 _sig("gpmpc_fleet_get_state", _c, _vp, _dp, _dp, _dp, _dp)
 _sig("gpmpc_fleet_records_dev", _vp, _vp)
 _sig("gpmpc_fleet_destroy", _c, _vp)
+_sig("gpmpc_rollout6_default_config", None, ctypes.POINTER(Rollout6Config))
+_sig("gpmpc_rollout6_create", _c, _vp, _vp, _vp, ctypes.POINTER(Rollout6Config), _c, ctypes.POINTER(_vp))
+_sig("gpmpc_rollout6_reset", _c, _vp, _c, _c, _dp)
+_sig("gpmpc_rollout6_step", _c, _vp, _c)
+_sig("gpmpc_rollout6_read", _c, _vp, _dp, _dp)
+_sig("gpmpc_rollout6_get_state", _c, _vp, _dp, _dp, _dp, _dp, _dp, _dp)
+_sig("gpmpc_rollout6_destroy", _c, _vp)
 
 EXPORTED = ["gpmpc_abi_version", "gpmpc_last_error", "gpmpc_ctx_create", "gpmpc_ctx_destroy",
             "gpmpc_ctx_sync", "gpmpc_ctx_stream", "gpmpc_gram", "gpmpc_gram_grad", "gpmpc_potrf",
@@ -132,7 +144,9 @@ EXPORTED = ["gpmpc_abi_version", "gpmpc_last_error", "gpmpc_ctx_create", "gpmpc_
             "gpmpc_fleet_create", "gpmpc_fleet_reset", "gpmpc_fleet_step", "gpmpc_fleet_read",
             "gpmpc_fleet_step_phases", "gpmpc_fleet_get_state", "gpmpc_fleet_set_stamps", "gpmpc_fleet_set_trace",
             "gpmpc_syrk_batched_dev", "gpmpc_cov_propagate", "gpmpc_cov_propagate_dev",
-            "gpmpc_fleet_records_dev", "gpmpc_fleet_destroy"]
+            "gpmpc_fleet_records_dev", "gpmpc_fleet_destroy", "gpmpc_rollout6_default_config",
+            "gpmpc_rollout6_create", "gpmpc_rollout6_reset", "gpmpc_rollout6_step", "gpmpc_rollout6_read",
+            "gpmpc_rollout6_get_state", "gpmpc_rollout6_destroy"]
 
 
 class HIPError(RuntimeError):
@@ -410,6 +424,13 @@ def qp_default_settings(**kw):
     s = QPSettings()
     _L.gpmpc_qp_default_settings(ctypes.byref(s))
     return set_fields(s, kw)
+
+
+def rollout6_default_config(**kw):
+    """6-DoF rollout config; QP settings may be given flat (``max_iter=...``)."""
+    c = Rollout6Config()
+    _L.gpmpc_rollout6_default_config(ctypes.byref(c))
+    return set_fields(c, kw, nested="qp")
 
 
 def fleet_default_config(**kw):

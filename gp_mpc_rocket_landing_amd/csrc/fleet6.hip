@@ -1,0 +1,1254 @@
+// fleet6.hip -- BASELINE configs[4]: a batch of closed-loop 6-DoF GP-MPC rollouts
+// (N = 30, 14 states, the StructuredRocketGP FITC residuals), device-resident.
+//
+// One control step of rollout b (oracle/sixdof_oracle.py restates it):
+//   1. k_r6_predict  (256 threads / rollout): Monte-Carlo termination rules
+//      (monte_carlo.py:455-488 on the first seven states), then GPMPC.solve's
+//      forward simulation (gp_mpc.py:258-281): X[k+1] = RK4(X[k], U[k])
+//      (discretization.py:229-252, quaternion normalised, rocket_6dof.py:371-387)
+//      + [.., d_v dt, .., d_w dt] with the FITC means of the two GPs at
+//      (X[k], U[k]) (structured_gp.py:225-268; sparse_gp.py:255-305 mean as
+//      written, K*u alpha) -- the 2 x M kernel rows of a point are spread over
+//      the workgroup and reduced; the 30 points are sequential.
+//   2. k_r6_control  (1024 threads / rollout): the QP subproblem of
+//      gp_mpc.py:394-460 in deviation variables z = [dx_0, du_0, .., dx_30]
+//      (n = 524): x0 + dynamics equalities with A_d = I + A_c dt, B_d = B_c dt
+//      (rocket_6dof.py:427-459, analytic Jacobians) and c_k = GP mean dt; the
+//      QCQP rows made linear (thrust box, |u| >= T_min at U_nom, glideslope
+//      half-planes, trust-region boxes; m = 1104); OSQP-0.6 ADMM (Ruiz scaling,
+//      rho vector, adaptive rho, termination every 25) on the reduced KKT
+//      matrix, which is block tridiagonal in the 31 stage blocks [x_k, u_k]:
+//      S_0 = D_0, S_k+1 = D_k+1 - C_k S_k^-1 C_k^T with S_k^-1 formed by
+//      Gauss-Jordan in LDS; each iteration's solve is a forward chain
+//      (y_k+1 -= G_k y_k, G_k = C_k S_k^-1, 14 lanes), the 31 diagonal products
+//      u_k = S_k^-1 y_k in parallel, and a backward chain (x_k = u_k -
+//      G_k^T x_k+1, 17 lanes).  Then the plan X + dX, U + dU (kept unshifted
+//      as the next warm start, gp_mpc.py:358-359), the truth plant step (RK4
+//      + the drag dispersion of dispersion.py:349-360 and the -0.05 w rate
+//      damping the config-5 GP is trained on) and the records.
+// Ownership: thread j < 524 owns variable j (+ its bound row, and general row
+// j < 146); thread 524 + r owns equality row r < 434.  The 14 x 17 dynamics
+// block of each equality row lives in its owner's registers, a column copy in
+// the variable owner's; only the factor and the cross-thread vectors are LDS.
+#include "internal.h"
+#include "qp.h"
+#include <vector>
+
+#define R6_NX 14
+#define R6_NU 3
+#define R6_SZ 17
+#define R6_N 30
+#define R6_NBLK (R6_N + 1)
+#define R6_NV (R6_N * R6_SZ + R6_NX)          // 524 variables
+#define R6_MD (R6_NX * (R6_N + 1))            // 434 equality rows
+#define R6_MT R6_N                            // 30 thrust rows
+#define R6_MG (4 * (R6_N - 1))                // 116 glideslope rows
+#define R6_MGEN (R6_MT + R6_MG)               // 146 general rows
+#define R6_M (R6_MD + R6_NV + R6_MGEN)        // 1104 rows
+#define R6_T 1024
+#define R6_TRI 153                            // packed lower 17 x 17
+#define R6_PT 256                             // predict threads
+
+// Rocket6DoFConfig (rocket_6dof.py:36-84), ConstraintParams (constraints.py:35-50),
+// CostWeights (cost_functions.py:39-98), gp_mpc.py trust regions (:432-435)
+#define R6_ALPHA (1.0 / 30.0)
+#define R6_T_MIN 0.5
+#define R6_T_MAX 5.0
+
+__device__ __constant__ double r6_J[3] = {0.02 * 0.168, 1.0 * 0.168, 1.0 * 0.168};
+__device__ __constant__ double r6_Q[R6_NX] = {0.0, 10, 10, 10, 1, 1, 1, 0, 5, 5, 0, 0.1, 0.1, 0.1};
+
+struct gpmpc_rollout6 {
+  gpmpc_ctx *ctx = nullptr;
+  gpmpc_fitc *gpv = nullptr, *gpw = nullptr;
+  gpmpc_rollout6_config cfg{};
+  int B = 0;
+  DevBuf x, U, Xp, gm, Xo, ysc, rho, rec, lin, pending;
+};
+
+extern "C" void gpmpc_rollout6_default_config(gpmpc_rollout6_config *c) {
+  c->horizon = R6_N;   // BASELINE configs[4]: N = 30
+  c->dt = 0.1;
+  c->max_steps = 300;
+  gpmpc_qp_default_settings(&c->qp);   // osqp_rti.py:54-60 settings, as the 3-DoF path
+}
+
+// ---------------------------------------------------------------------------
+// dynamics (nominal_mpc.py:163-203)
+__device__ __forceinline__ void r6_dcm(const double *q, double C[3][3]) {
+  const double w = q[0], x = q[1], y = q[2], z = q[3];
+  C[0][0] = 1 - 2 * (y * y + z * z); C[0][1] = 2 * (x * y - w * z); C[0][2] = 2 * (x * z + w * y);
+  C[1][0] = 2 * (x * y + w * z); C[1][1] = 1 - 2 * (x * x + z * z); C[1][2] = 2 * (y * z - w * x);
+  C[2][0] = 2 * (x * z - w * y); C[2][1] = 2 * (y * z + w * x); C[2][2] = 1 - 2 * (x * x + y * y);
+}
+
+__device__ void r6_f(const double *x, const double *u, double *o) {
+  const double m = x[0];
+  const double tm = sqrt(u[0] * u[0] + u[1] * u[1] + u[2] * u[2]);
+  double C[3][3];
+  r6_dcm(x + 7, C);
+  o[0] = -R6_ALPHA * tm;
+  o[1] = x[4]; o[2] = x[5]; o[3] = x[6];
+  const double gI[3] = {-1.0, 0.0, 0.0};
+  for (int i = 0; i < 3; ++i) o[4 + i] = (C[i][0] * u[0] + C[i][1] * u[1] + C[i][2] * u[2]) / m + gI[i];
+  const double qw = x[7], qx = x[8], qy = x[9], qz = x[10], wx = x[11], wy = x[12], wz = x[13];
+  o[7] = 0.5 * -((wx * qx + wy * qy) + wz * qz);
+  o[8] = 0.5 * (qw * wx + (wy * qz - wz * qy));
+  o[9] = 0.5 * (qw * wy + (wz * qx - wx * qz));
+  o[10] = 0.5 * (qw * wz + (wx * qy - wy * qx));
+  // r_T x u with r_T = (-0.25, 0, 0); w x J w
+  const double tq[3] = {0.0 * u[2] - 0.0 * u[1], 0.0 * u[0] - (-0.25) * u[2], (-0.25) * u[1] - 0.0 * u[0]};
+  const double jw[3] = {r6_J[0] * wx, r6_J[1] * wy, r6_J[2] * wz};
+  const double cx[3] = {wy * jw[2] - wz * jw[1], wz * jw[0] - wx * jw[2], wx * jw[1] - wy * jw[0]};
+  for (int i = 0; i < 3; ++i) o[11 + i] = (tq[i] - cx[i]) / r6_J[i];
+}
+
+// RK4 (discretization.py:229-252) + quaternion normalisation (rocket_6dof.py:371-387)
+__device__ void r6_step(const double *x, const double *u, double dt, double *xn) {
+  double k1[R6_NX], k2[R6_NX], k3[R6_NX], k4[R6_NX], t[R6_NX];
+  r6_f(x, u, k1);
+  for (int i = 0; i < R6_NX; ++i) t[i] = x[i] + dt * k1[i] / 2;
+  r6_f(t, u, k2);
+  for (int i = 0; i < R6_NX; ++i) t[i] = x[i] + dt * k2[i] / 2;
+  r6_f(t, u, k3);
+  for (int i = 0; i < R6_NX; ++i) t[i] = x[i] + dt * k3[i];
+  r6_f(t, u, k4);
+  for (int i = 0; i < R6_NX; ++i) xn[i] = x[i] + (dt / 6) * (k1[i] + 2 * k2[i] + 2 * k3[i] + k4[i]);
+  const double nq = sqrt(xn[7] * xn[7] + xn[8] * xn[8] + xn[9] * xn[9] + xn[10] * xn[10]);
+  for (int i = 7; i < 11; ++i) xn[i] = xn[i] / nq;
+}
+
+// -[A_d | B_d] (A_d = I + A_c dt, B_d = B_c dt) into a zeroed 14 x 17 row-major block
+__device__ void r6_neg_lin(const double *x, const double *u, double dt, double *blk) {
+  auto set = [&](int i, int j, double v) { blk[i * R6_SZ + j] = v; };
+  const double m = x[0], qw = x[7], qx = x[8], qy = x[9], qz = x[10], wx = x[11], wy = x[12], wz = x[13];
+  const double u0 = u[0], u1 = u[1], u2 = u[2];
+  const double tm = sqrt(u0 * u0 + u1 * u1 + u2 * u2);
+  double C[3][3];
+  r6_dcm(x + 7, C);
+  for (int i = 0; i < R6_NX; ++i) set(i, i, -(1.0 + 0.0 * dt));
+  set(0, 14, -(-R6_ALPHA * u0 / tm * dt)); set(0, 15, -(-R6_ALPHA * u1 / tm * dt));
+  set(0, 16, -(-R6_ALPHA * u2 / tm * dt));
+  for (int i = 0; i < 3; ++i) set(1 + i, 4 + i, -(1.0 * dt));
+  for (int i = 0; i < 3; ++i) {
+    const double cu = C[i][0] * u0 + C[i][1] * u1 + C[i][2] * u2;
+    set(4 + i, 0, -(-cu / (m * m) * dt));
+    for (int j = 0; j < 3; ++j) set(4 + i, 14 + j, -(C[i][j] / m * dt));
+  }
+  const double dCu[3][4] = {
+      {-2 * qz * u1 + 2 * qy * u2, 2 * qy * u1 + 2 * qz * u2, -4 * qy * u0 + 2 * qx * u1 + 2 * qw * u2,
+       -4 * qz * u0 - 2 * qw * u1 + 2 * qx * u2},
+      {2 * qz * u0 - 2 * qx * u2, 2 * qy * u0 - 4 * qx * u1 - 2 * qw * u2, 2 * qx * u0 + 2 * qz * u2,
+       2 * qw * u0 - 4 * qz * u1 + 2 * qy * u2},
+      {-2 * qy * u0 + 2 * qx * u1, 2 * qz * u0 + 2 * qw * u1 - 4 * qx * u2,
+       -2 * qw * u0 + 2 * qz * u1 - 4 * qy * u2, 2 * qx * u0 + 2 * qy * u1}};
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 4; ++j) set(4 + i, 7 + j, -(dCu[i][j] / m * dt));
+  const double Om[4][4] = {{0, -wx, -wy, -wz}, {wx, 0, -wz, wy}, {wy, wz, 0, -wx}, {wz, -wy, wx, 0}};
+  for (int i = 0; i < 4; ++i)
+    for (int j = 0; j < 4; ++j) set(7 + i, 7 + j, -((i == j ? 1.0 : 0.0) + 0.5 * Om[i][j] * dt));
+  const double Qw[4][3] = {{-qx, -qy, -qz}, {qw, qz, -qy}, {-qz, qw, qx}, {qy, -qx, qw}};
+  for (int i = 0; i < 4; ++i)
+    for (int j = 0; j < 3; ++j) set(7 + i, 11 + j, -(0.5 * Qw[i][j] * dt));
+  const double j1 = r6_J[0], j2 = r6_J[1], j3 = r6_J[2];
+  const double Aw[3][3] = {{0, wz, wy}, {wz, 0, wx}, {wy, wx, 0}};
+  const double cw[3] = {-(j3 - j2) / j1, -(j1 - j3) / j2, -(j2 - j1) / j3};
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) set(11 + i, 11 + j, -((i == j ? 1.0 : 0.0) + cw[i] * Aw[i][j] * dt));
+  // B_c omega rows: J^-1 [r_T]x, r_T = (-0.25, 0, 0)
+  const double rx = -0.25, ry = 0.0, rz = 0.0;
+  const double Rx[3][3] = {{0, -rz, ry}, {rz, 0, -rx}, {-ry, rx, 0}};
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) set(11 + i, 14 + j, -(Rx[i][j] / r6_J[i] * dt));
+}
+
+// ---------------------------------------------------------------------------
+// StructuredRocketGP features (features.py:196-263, :304-356), scaled by the GP's
+// lengthscales, and their squared norm (the k_scale_rows arithmetic)
+__device__ void r6_features(const double *x, const double *u, const double *lsv, const double *lsw,
+                            double *zv, double *zw, double *nv, double *nw) {
+  const double alt = x[1], vx = x[4], vy = x[5], vz = x[6];
+  const double speed = sqrt((vx * vx + vy * vy) + vz * vz);
+  const double rho = 1.225 * exp(-alt / 8500.0);
+  const double qd = 0.5 * rho * speed * speed;
+  // body-from-inertial DCM (features.py:265-270)
+  const double w = x[7], qx = x[8], qy = x[9], qz = x[10];
+  const double Cb[3][3] = {{1 - 2 * (qy * qy + qz * qz), 2 * (qx * qy + w * qz), 2 * (qx * qz - w * qy)},
+                           {2 * (qx * qy - w * qz), 1 - 2 * (qx * qx + qz * qz), 2 * (qy * qz + w * qx)},
+                           {2 * (qx * qz + w * qy), 2 * (qy * qz - w * qx), 1 - 2 * (qx * qx + qy * qy)}};
+  double vb[3];
+  for (int i = 0; i < 3; ++i) vb[i] = (Cb[i][0] * vx + Cb[i][1] * vy) + Cb[i][2] * vz;
+  const bool moving = speed > 1e-3;
+  const double safe = moving ? speed : 1.0;
+  double sb = vb[1] / safe;
+  sb = fmin(fmax(sb, -1.0), 1.0);
+  const double aoa = moving ? atan2(-vb[2], vb[0]) : 0.0;
+  const double beta = moving ? asin(sb) : 0.0;
+  const double tm = sqrt((u[0] * u[0] + u[1] * u[1]) + u[2] * u[2]);
+  const double qn = 0.5 * 1.225 * 100.0;
+  const double fv[13] = {vx / 10.0, vy / 10.0, vz / 10.0, speed / 10.0, qd / qn, aoa, beta,
+                         u[0] / 10.0, u[1] / 10.0, u[2] / 10.0, tm / 10.0, alt / 100.0, rho / 1.225};
+  const double wxx = x[11], wyy = x[12], wzz = x[13];
+  const double wm = sqrt((wxx * wxx + wyy * wyy) + wzz * wzz);
+  const double fw[12] = {wxx, wyy, wzz, wm, u[0] / 10.0, u[1] / 10.0, u[2] / 10.0,
+                         vb[0] / 10.0, vb[1] / 10.0, vb[2] / 10.0, speed / 10.0, qd / qn};
+  double s = 0.0;
+  for (int k = 0; k < 13; ++k) { zv[k] = fv[k] / lsv[k]; s += zv[k] * zv[k]; }
+  *nv = s;
+  s = 0.0;
+  for (int k = 0; k < 12; ++k) { zw[k] = fw[k] / lsw[k]; s += zw[k] * zw[k]; }
+  *nw = s;
+}
+
+__device__ __forceinline__ bool r6_landing_ok(const double *x, double m0) {
+  // LandingConstraints.check_landing (monte_carlo.py:54-104), run_experiments tolerances
+  if (fabs(x[1]) > 1.0) return false;
+  if (fabs(x[2]) > 5.0 || fabs(x[3]) > 5.0) return false;
+  if (fabs(x[4]) > 3.0) return false;
+  if (fabs(x[5]) > 1.0 || fabs(x[6]) > 1.0) return false;
+  if (1.0 - x[0] / m0 > 1.0 - 0.05) return false;
+  return true;
+}
+
+struct R6Args {
+  QPSettingsDev st;
+  double dt;
+  int max_steps;
+  double *x, *U, *Xp, *gm, *Xo, *ysc, *rho, *rec;
+  double *lin;   // per rollout and stage: -[A_d | B_d] (14 x 17), from k_r6_predict
+  int *pending;  // the control kernel solved: k_r6_plant applies U[0]
+  // the two FITC GPs (d_v: 13 features, d_w: 12)
+  GpView gv, gw;
+  int Mv, Mw;
+};
+
+// ---------------------------------------------------------------------------
+// 1. termination rules + forward simulation with the GP mean
+__global__ __launch_bounds__(R6_PT) void k_r6_predict(R6Args a) {
+  const int b = blockIdx.x, tid = threadIdx.x;
+  double *rec = a.rec + (int64_t)b * GPMPC_REC_LEN;
+  if (rec[0] != 0.0) return;
+  __shared__ double X[R6_N + 1][R6_NX];
+  __shared__ double zq[2][16], zn[2];
+  __shared__ double red[R6_PT / 64][6];
+  __shared__ int s_out;
+  const double dt = a.dt;
+  if (tid < R6_NX) X[0][tid] = a.x[(int64_t)b * R6_NX + tid];
+  __syncthreads();
+  if (tid == 0) {  // monte_carlo.py:458-488 on [m, r, v]; then any non-finite 6-DoF state
+    const double *x = X[0];
+    const double m0 = rec[13];
+    bool div7 = false, div = false;
+    for (int i = 0; i < 7; ++i) div7 = div7 || !(fabs(x[i]) <= 1e6);
+    for (int i = 0; i < R6_NX; ++i) div = div || !(fabs(x[i]) <= 1e6);
+    int out = 0;
+    if ((int)rec[1] >= a.max_steps) out = 5;
+    else if (x[1] < 0.0) out = 2;
+    else if (x[0] <= 1.0 + 0.01) out = 3;
+    else if (div7) out = 6;
+    else if (x[1] < 1.0 && fabs(x[4]) < 5.0) out = r6_landing_ok(x, m0) ? 1 : 4;
+    else if (div) out = 6;
+    if (out) {
+      rec[0] = out;
+      rec[2] = m0 - x[0];
+      for (int i = 0; i < 7; ++i) rec[4 + i] = x[i];
+    }
+    s_out = out;
+  }
+  __syncthreads();
+  if (s_out) return;
+  const double *Ub = a.U + (int64_t)b * R6_N * R6_NU;
+  for (int k = 0; k < R6_N; ++k) {
+    if (tid == 0)
+      r6_features(X[k], Ub + k * R6_NU, a.gv.ls, a.gw.ls, zq[0], zq[1], &zn[0], &zn[1]);
+    __syncthreads();
+    // K*u alpha of both GPs: the expansion form of the gram kernel (same bits
+    // per kernel value); 3 outputs each
+    double acc[6] = {0, 0, 0, 0, 0, 0};
+    for (int g = 0; g < 2; ++g) {
+      const GpView &v = g ? a.gw : a.gv;
+      const int M = g ? a.Mw : a.Mv, d = g ? 12 : 13;
+      for (int i = tid; i < M; i += R6_PT) {
+        double dot = 0.0;
+        for (int f = 0; f < d; ++f) dot = fma(zq[g][f], v.Xs[(int64_t)i * d + f], dot);
+        const double d2 = (zn[g] + v.Xn[i]) - 2.0 * dot;
+        const double kv = kernel_epilogue(GPMPC_SE_ARD, d2, v.sigma2, 0.0);
+        for (int c = 0; c < 3; ++c) acc[3 * g + c] += kv * v.alphaT[(int64_t)c * M + i];
+      }
+    }
+    for (int c = 0; c < 6; ++c)
+      for (int o = 32; o > 0; o >>= 1) acc[c] += __shfl_xor(acc[c], o);
+    if ((tid & 63) == 0)
+      for (int c = 0; c < 6; ++c) red[tid >> 6][c] = acc[c];
+    __syncthreads();
+    if (tid == 0) {
+      double gmk[6];
+      for (int c = 0; c < 6; ++c) {
+        double s = 0.0;
+        for (int w = 0; w < R6_PT / 64; ++w) s += red[w][c];
+        const GpView &v = c < 3 ? a.gv : a.gw;
+        gmk[c] = s * v.ystd[c % 3] + v.ymean[c % 3];
+        a.gm[((int64_t)b * R6_N + k) * 6 + c] = gmk[c];
+      }
+      double xn[R6_NX];
+      r6_step(X[k], Ub + k * R6_NU, dt, xn);
+      for (int i = 0; i < 3; ++i) { xn[4 + i] += gmk[i] * dt; xn[11 + i] += gmk[3 + i] * dt; }
+      for (int i = 0; i < R6_NX; ++i) X[k + 1][i] = xn[i];
+    }
+    __syncthreads();
+  }
+  for (int e = tid; e < (R6_N + 1) * R6_NX; e += R6_PT)
+    a.Xp[(int64_t)b * (R6_N + 1) * R6_NX + e] = (&X[0][0])[e];
+  // linearisation at the simulated points (gp_mpc.py:303-304): -[A_d | B_d] per stage
+  double *lin = a.lin + (int64_t)b * R6_N * R6_NX * R6_SZ;
+  for (int e = tid; e < R6_N * R6_NX * R6_SZ; e += R6_PT) lin[e] = 0.0;
+  __syncthreads();
+  if (tid < R6_N) r6_neg_lin(X[tid], Ub + tid * R6_NU, dt, lin + tid * R6_NX * R6_SZ);
+}
+
+// ---------------------------------------------------------------------------
+// 2. QP + ADMM + plant
+struct R6Smem {
+  double Sinv[R6_NBLK * R6_TRI];      // packed lower S_k^-1 (D_k during the assembly)
+  double G[R6_N * R6_NX * R6_SZ];     // staged dynamics rows (scaled), then G_k = C_k S_k^-1
+  double rhs[R6_NBLK * R6_SZ];        // x~ right-hand side, forward chain y
+  double xs[R6_NBLK * R6_SZ];         // diagonal products u, backward chain x = x~
+  double w[R6_MD + R6_MGEN];          // rho z - y of equality + general rows (scratch at checks)
+  double E[R6_M];                     // row scaling
+  double dsc[R6_NV];                  // per-pass column scaling / factor scratch
+  double dpl[R6_MD];                  // each equality row's identity entry (scaled)
+  double gen[R6_MGEN * 3];            // general rows' values (scaled)
+  double T[R6_SZ * R6_SZ];            // Gauss-Jordan block
+  double Gt[R6_NX * R6_SZ];           // G_k before it replaces C_k
+  double Sch[R6_NX * R6_NX];          // G_k C_k^T
+  double red[16][12];
+  double c, rho_s;
+  int flag;
+};
+
+__device__ __forceinline__ int r6_tri(int a, int b) { return a >= b ? a * (a + 1) / 2 + b : b * (b + 1) / 2 + a; }
+
+template <int K>
+__device__ __forceinline__ void r6_max(double (&v)[K], double (*red)[12]) {
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+#pragma unroll
+  for (int k = 0; k < K; ++k)
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v[k] = fmax(v[k], __shfl_xor(v[k], o));
+  __syncthreads();
+  if (lane == 0)
+#pragma unroll
+    for (int k = 0; k < K; ++k) red[wv][k] = v[k];
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    double m = red[0][k];
+    for (int w = 1; w < R6_T / 64; ++w) m = fmax(m, red[w][k]);
+    v[k] = m;
+  }
+  __syncthreads();
+}
+
+template <int K>
+__device__ __forceinline__ void r6_sum(double (&v)[K], double (*red)[12]) {
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+#pragma unroll
+  for (int k = 0; k < K; ++k)
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v[k] += __shfl_xor(v[k], o);
+  __syncthreads();
+  if (lane == 0)
+#pragma unroll
+    for (int k = 0; k < K; ++k) red[wv][k] = v[k];
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    double s = red[0][k];
+    for (int w = 1; w < R6_T / 64; ++w) s += red[w][k];
+    v[k] = s;
+  }
+  __syncthreads();
+}
+
+__device__ __forceinline__ double r6_rho(double l, double u, double rs) {
+  if (l < -QP_OSQP_INFTY * QP_MIN_SCALING && u > QP_OSQP_INFTY * QP_MIN_SCALING) return QP_RHO_MIN;
+  if (u - l < QP_RHO_TOL) return QP_RHO_EQ * rs;
+  return rs;
+}
+
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// general row g: its entries (count, variables, value slots)
+__device__ __forceinline__ int r6_gen_cols(int g, int *col) {
+  if (g < R6_MT) {
+    const int o = g * R6_SZ + R6_NX;
+    col[0] = o; col[1] = o + 1; col[2] = o + 2;
+    return 3;
+  }
+  const int gg = g - R6_MT, k = 1 + gg / 4, c = gg % 4;
+  col[0] = k * R6_SZ + 1;
+  col[1] = k * R6_SZ + (c < 2 ? 2 : 3);
+  return 2;
+}
+
+// the e-th general-row entry (e < 4) of variable (k, i) in row order: its
+// general row g and value slot sl; false past the variable's entries
+__device__ __forceinline__ bool r6_gen_slot(int k, int i, int e, int &g, int &sl) {
+  if (k < R6_N && i >= R6_NX) {  // thrust row k
+    g = k; sl = i - R6_NX;
+    return e == 0;
+  }
+  if (k >= 1 && k < R6_N && i >= 1 && i <= 3) {  // glideslope rows of stage k
+    const int g0 = R6_MT + 4 * (k - 1);
+    g = g0 + (i == 3 ? 2 : 0) + e;
+    sl = (i == 1) ? 0 : 1;
+    return e < (i == 1 ? 4 : 2);
+  }
+  g = 0; sl = 0;
+  return false;
+}
+
+struct R6Var {  // variable j and its bound row MD + j; general row j (< 146)
+  bool ok;
+  int j, k, i;
+  double x, dx, P, q, D, Ab, lb, ub, yb, zb, dyb, ztb;
+  // colA[0..13]: -A_d[:, i] / -B_d[:, i-14] of the dynamics rows of block k
+  // (scaled).  An equality-row thread (no variable) keeps its row here instead.
+  double colA[R6_SZ + 1];
+  bool gok;
+  int gn;
+  double gA[3], gl, gu, gy, gz, gdy;
+};
+// equality row r (x0 row r < 14, else dynamics row (k, i)).  Rows and variables
+// live on different threads, so the row's registers alias the variable slots.
+struct R6Row {
+  bool ok;
+  int r, k, i;
+  double (&A)[R6_SZ + 1];
+  double &ur, &yr, &zr, &dyr;
+  __device__ explicit R6Row(R6Var &V) : A(V.colA), ur(V.lb), yr(V.yb), zr(V.zb), dyr(V.dyb) {}
+};
+
+__device__ __forceinline__ int r6_eqid_row(int k, int i) { return k == 0 ? i : R6_NX + R6_NX * (k - 1) + i; }
+
+// (A' w)_j in row order: equality identity row, dynamics rows of block k, bound row, general rows
+__device__ __forceinline__ double r6_col_dot(const R6Smem &s, const R6Var &V, const double *wv, double wb,
+                                             const double *wg) {
+  double acc = 0.0;
+  if (V.i < R6_NX) {
+    const int r = r6_eqid_row(V.k, V.i);
+    acc += s.dpl[r] * wv[r];
+  }
+  if (V.k < R6_N) {
+    const double *wr = wv + R6_NX + R6_NX * V.k;
+#pragma unroll
+    for (int e = 0; e < R6_NX; ++e) acc += V.colA[e] * wr[e];
+  }
+  acc += V.Ab * wb;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    int g, sl;
+    if (r6_gen_slot(V.k, V.i, e, g, sl)) acc += s.gen[g * 3 + sl] * wg[g];
+  }
+  return acc;
+}
+
+__device__ __forceinline__ double r6_row_dot(const R6Row &R, const double *v) {
+  if (R.r < R6_NX) return 0.0 + R.A[0] * v[R.r];
+  const double *vb = v + R.k * R6_SZ;
+  double acc = 0.0;
+#pragma unroll
+  for (int e = 0; e < R6_SZ; ++e) acc += R.A[e] * vb[e];
+  acc += R.A[R6_SZ] * v[(R.k + 1) * R6_SZ + R.i];
+  return acc;
+}
+__device__ __forceinline__ double r6_gen_dot(const R6Var &V, const double *v) {
+  int col[3];
+  const int n = r6_gen_cols(V.j, col);
+  double acc = 0.0;
+#pragma unroll
+  for (int e = 0; e < 3; ++e)
+    if (e < n) acc += V.gA[e] * v[col[e]];
+  return acc;
+}
+
+// assemble the block tridiagonal M = P + sigma I + A' R A and factor it:
+// returns 0 or a failing block + 1
+__device__ __forceinline__ int r6_factor(R6Smem &s, R6Var &V, R6Row &R, double sigma) {
+  const int tid = threadIdx.x;
+  const double rs = s.rho_s, re = QP_RHO_EQ * rs;
+  // stage: dynamics rows' block values, per-variable P + sigma and bound terms
+  if (R.ok && R.r >= R6_NX)
+#pragma unroll
+    for (int e = 0; e < R6_SZ; ++e) s.G[(R.k * R6_NX + R.i) * R6_SZ + e] = R.A[e];
+  if (V.ok) {
+    s.dsc[V.j] = V.P + sigma;
+    s.xs[V.j] = r6_rho(V.lb, V.ub, rs) * V.Ab * V.Ab;
+  }
+  __syncthreads();
+  // D_k, lower packed, row order of the terms as the banded oracle
+  for (int e = tid; e < R6_NBLK * R6_TRI; e += R6_T) {
+    const int k = e / R6_TRI, t = e - k * R6_TRI;
+    int a = (int)((sqrt(8.0 * t + 1.0) - 1.0) * 0.5);
+    while (a * (a + 1) / 2 > t) --a;
+    while ((a + 1) * (a + 2) / 2 <= t) ++a;
+    const int bb = t - a * (a + 1) / 2;
+    const int nb = (k == R6_N) ? R6_NX : R6_SZ;
+    double v = 0.0;
+    if (a < nb) {
+      const int ja = k * R6_SZ + a, jb = k * R6_SZ + bb;
+      if (a == bb) {
+        v = s.dsc[ja];
+        if (a < R6_NX) {
+          const int r = r6_eqid_row(k, a);
+          v += re * s.dpl[r] * s.dpl[r];
+        }
+      }
+      if (k < R6_N) {
+        const double *g = s.G + k * R6_NX * R6_SZ;
+        for (int i = 0; i < R6_NX; ++i) v += re * g[i * R6_SZ + a] * g[i * R6_SZ + bb];
+      }
+      if (a == bb) v += s.xs[ja];
+#pragma unroll
+      for (int p = 0; p < 4; ++p) {
+        int g1, s1;
+        if (!r6_gen_slot(k, a, p, g1, s1)) continue;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          int g2, s2;
+          if (r6_gen_slot(k, bb, q, g2, s2) && g1 == g2) v += rs * s.gen[g1 * 3 + s1] * s.gen[g2 * 3 + s2];
+        }
+      }
+      (void)jb;
+    } else if (a == bb) {
+      v = 1.0;  // unused tail of the last block
+    }
+    s.Sinv[e] = v;
+  }
+  __syncthreads();
+  // the sweep
+  const int ti = tid / R6_SZ, tj = tid - ti * R6_SZ;
+  const bool tok = tid < R6_SZ * R6_SZ;
+  for (int k = 0; k <= R6_N; ++k) {
+    const int nb = (k == R6_N) ? R6_NX : R6_SZ;
+    if (tok) {
+      double v = s.Sinv[k * R6_TRI + r6_tri(ti, tj)];
+      if (k > 0 && ti < R6_NX && tj < R6_NX) v -= s.Sch[ti * R6_NX + tj];
+      s.T[tid] = v;
+    }
+    __syncthreads();
+    for (int p = 0; p < nb; ++p) {
+      double piv = 0.0, tip = 0.0, tpj = 0.0, tij = 0.0;
+      if (tok) {
+        piv = s.T[p * R6_SZ + p];
+        tip = s.T[ti * R6_SZ + p];
+        tpj = s.T[p * R6_SZ + tj];
+        tij = s.T[tid];
+      } else {
+        piv = s.T[p * R6_SZ + p];
+      }
+      __syncthreads();
+      if (!(piv > 0.0)) return k + 1;  // uniform: every thread read the same pivot
+      if (tok && ti < nb && tj < nb) {
+        double nv;
+        if (ti == p && tj == p) nv = 1.0 / piv;
+        else if (ti == p) nv = tpj / piv;
+        else if (tj == p) nv = -tip / piv;
+        else nv = tij - (tip / piv) * tpj;
+        s.T[tid] = nv;
+      }
+      __syncthreads();
+    }
+    if (tok && ti >= tj) s.Sinv[k * R6_TRI + r6_tri(ti, tj)] = (ti < nb && tj < nb) ? s.T[tid] : 0.0;
+    if (k == R6_N) break;
+    // G_k = C_k S_k^-1, C_k[i][:] = rho_eq dpl(k, i) (staged row (k, i))
+    const double *g = s.G + k * R6_NX * R6_SZ;
+    if (tid < R6_NX * R6_SZ) {
+      const int i = tid / R6_SZ, c = tid - i * R6_SZ;
+      const double sc = re * s.dpl[R6_NX + R6_NX * k + i];
+      double acc = 0.0;
+      for (int e = 0; e < R6_SZ; ++e) acc += (sc * g[i * R6_SZ + e]) * s.T[e * R6_SZ + c];
+      s.Gt[tid] = acc;
+    }
+    __syncthreads();
+    if (tid < R6_NX * R6_NX) {  // G_k C_k^T (14 x 14)
+      const int i = tid / R6_NX, i2 = tid - i * R6_NX;
+      const double sc = re * s.dpl[R6_NX + R6_NX * k + i2];
+      double acc = 0.0;
+      for (int e = 0; e < R6_SZ; ++e) acc += s.Gt[i * R6_SZ + e] * (sc * g[i2 * R6_SZ + e]);
+      s.Sch[tid] = acc;
+    }
+    __syncthreads();
+    if (tid < R6_NX * R6_SZ) s.G[k * R6_NX * R6_SZ + tid] = s.Gt[tid];
+    __syncthreads();
+  }
+  __syncthreads();
+  return 0;
+}
+
+// x~ = M^-1 rhs: forward chain (wave 0), diagonal products, backward chain (wave 0)
+__device__ __forceinline__ void r6_solve(R6Smem &s) {
+  const int tid = threadIdx.x;
+  if (tid < 64) {
+    const int i = tid;
+    for (int k = 0; k < R6_N; ++k) {
+      double acc0 = 0.0, acc1 = 0.0;
+      if (i < R6_NX) {
+        const double *g = s.G + (k * R6_NX + i) * R6_SZ;
+        const double *y = s.rhs + k * R6_SZ;
+#pragma unroll
+        for (int e = 0; e < 16; e += 2) {
+          acc0 = fma(g[e], y[e], acc0);
+          acc1 = fma(g[e + 1], y[e + 1], acc1);
+        }
+        acc0 = fma(g[16], y[16], acc0);
+        s.rhs[(k + 1) * R6_SZ + i] -= acc0 + acc1;
+      }
+      wave_sync();
+    }
+  }
+  __syncthreads();
+  if (tid < R6_NBLK * R6_SZ) {
+    const int k = tid / R6_SZ, a = tid - k * R6_SZ;
+    const int nb = (k == R6_N) ? R6_NX : R6_SZ;
+    if (a < nb) {
+      const double *S = s.Sinv + k * R6_TRI;
+      const double *y = s.rhs + k * R6_SZ;
+      double acc0 = 0.0, acc1 = 0.0;
+      for (int bb = 0; bb + 1 < nb; bb += 2) {
+        acc0 = fma(S[r6_tri(a, bb)], y[bb], acc0);
+        acc1 = fma(S[r6_tri(a, bb + 1)], y[bb + 1], acc1);
+      }
+      if (nb & 1) acc0 = fma(S[r6_tri(a, nb - 1)], y[nb - 1], acc0);
+      s.xs[tid] = acc0 + acc1;
+    }
+  }
+  __syncthreads();
+  if (tid < 64) {
+    const int a = tid;
+    for (int k = R6_N - 1; k >= 0; --k) {
+      if (a < R6_SZ) {
+        const double *g = s.G + k * R6_NX * R6_SZ;
+        const double *xn = s.xs + (k + 1) * R6_SZ;
+        double acc0 = 0.0, acc1 = 0.0;
+#pragma unroll
+        for (int i = 0; i < R6_NX; i += 2) {
+          acc0 = fma(g[i * R6_SZ + a], xn[i], acc0);
+          acc1 = fma(g[(i + 1) * R6_SZ + a], xn[i + 1], acc1);
+        }
+        s.xs[k * R6_SZ + a] -= acc0 + acc1;
+      }
+      wave_sync();
+    }
+  }
+  __syncthreads();
+}
+
+// residual norms (auxil.c update_info) + the rho-estimate quantities (as fq_update_info)
+__device__ __forceinline__ void r6_update_info(R6Smem &s, R6Var &V, R6Row &R, double (&o)[8], double (&re_)[4]) {
+  if (V.ok) s.rhs[V.j] = V.x;
+  if (R.ok) s.w[R.r] = R.yr;
+  if (V.gok) s.w[R6_MD + V.j] = V.gy;
+  __syncthreads();
+  double v[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+  auto row = [&](double ax, double z, double e) {
+    v[0] = fmax(v[0], fabs((ax - z) / e));
+    v[1] = fmax(v[1], fabs(z / e));
+    v[2] = fmax(v[2], fabs(ax / e));
+    v[8] = fmax(v[8], fabs(ax - z));
+    v[9] = fmax(v[9], fmax(fabs(z), fabs(ax)));
+  };
+  if (R.ok) row(r6_row_dot(R, s.rhs), R.zr, s.E[R.r]);
+  if (V.ok) {
+    row(0.0 + V.Ab * V.x, V.zb, s.E[R6_MD + V.j]);
+    const double aty = r6_col_dot(s, V, s.w, V.yb, s.w + R6_MD);
+    const double px = V.P * V.x, d = V.D, q = V.q;
+    v[3] = fmax(v[3], fabs((q + px + aty) / d));
+    v[4] = fmax(v[4], fabs(q / d));
+    v[5] = fmax(v[5], fabs(aty / d));
+    v[6] = fmax(v[6], fabs(px / d));
+    v[10] = fmax(v[10], fabs(q + px + aty));
+    v[11] = fmax(v[11], fmax(fmax(fabs(q), fabs(aty)), fabs(px)));
+  }
+  if (V.gok) row(r6_gen_dot(V, s.rhs), V.gz, s.E[R6_MD + R6_NV + V.j]);
+  r6_max<12>(v, s.red);
+#pragma unroll
+  for (int k = 0; k < 8; ++k) o[k] = v[k];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) re_[k] = v[8 + k];
+}
+
+__device__ __forceinline__ double r6_proj(double d, double l, double u) {
+  const bool bu = u > QP_OSQP_INFTY * QP_MIN_SCALING, bl = l < -QP_OSQP_INFTY * QP_MIN_SCALING;
+  if (bu && bl) return 0.0;
+  if (bu) return fmin(d, 0.0);
+  if (bl) return fmax(d, 0.0);
+  return d;
+}
+
+__device__ __forceinline__ bool r6_primal_infeasible(R6Smem &s, R6Var &V, R6Row &R, double eps) {
+  double v[1] = {0.0};
+  if (R.ok) { R.dyr = r6_proj(R.dyr, R.ur, R.ur); v[0] = fmax(v[0], fabs(s.E[R.r] * R.dyr)); }
+  if (V.ok) { V.dyb = r6_proj(V.dyb, V.lb, V.ub); v[0] = fmax(v[0], fabs(s.E[R6_MD + V.j] * V.dyb)); }
+  if (V.gok) { V.gdy = r6_proj(V.gdy, V.gl, V.gu); v[0] = fmax(v[0], fabs(s.E[R6_MD + R6_NV + V.j] * V.gdy)); }
+  r6_max<1>(v, s.red);
+  const double nrm = v[0];
+  if (!(nrm > QP_DIV_TOL)) return false;
+  double sm[1] = {0.0};
+  if (R.ok) sm[0] += R.ur * fmax(R.dyr, 0.0) + R.ur * fmin(R.dyr, 0.0);
+  if (V.ok) sm[0] += V.ub * fmax(V.dyb, 0.0) + V.lb * fmin(V.dyb, 0.0);
+  if (V.gok) sm[0] += V.gu * fmax(V.gdy, 0.0) + V.gl * fmin(V.gdy, 0.0);
+  r6_sum<1>(sm, s.red);
+  if (!(sm[0] < -eps * nrm)) return false;
+  if (R.ok) s.w[R.r] = R.dyr;
+  if (V.gok) s.w[R6_MD + V.j] = V.gdy;
+  __syncthreads();
+  double mx[1] = {0.0};
+  if (V.ok) mx[0] = fabs(r6_col_dot(s, V, s.w, V.dyb, s.w + R6_MD) / V.D);
+  r6_max<1>(mx, s.red);
+  return mx[0] < eps * nrm;
+}
+
+__device__ __forceinline__ bool r6_dual_infeasible(R6Smem &s, R6Var &V, R6Row &R, double eps) {
+  double v[1] = {0.0};
+  if (V.ok) v[0] = fabs(V.D * V.dx);
+  r6_max<1>(v, s.red);
+  const double nrm = v[0];
+  if (!(nrm > QP_DIV_TOL)) return false;
+  double a[1] = {0.0}, pm[1] = {0.0};
+  if (V.ok) { a[0] = V.q * V.dx; pm[0] = fabs(V.P * V.dx / V.D); }
+  r6_sum<1>(a, s.red);
+  r6_max<1>(pm, s.red);
+  if (!(a[0] < s.c * eps * nrm)) return false;
+  if (!(pm[0] < s.c * eps * nrm)) return false;
+  if (V.ok) s.rhs[V.j] = V.dx;
+  __syncthreads();
+  double bad[1] = {0.0};
+  auto test = [&](double vv, double l, double u) {
+    if ((u < QP_OSQP_INFTY * QP_MIN_SCALING && vv > eps * nrm) ||
+        (l > -QP_OSQP_INFTY * QP_MIN_SCALING && vv < -eps * nrm))
+      bad[0] = 1.0;
+  };
+  if (R.ok) test(r6_row_dot(R, s.rhs) / s.E[R.r], R.ur, R.ur);
+  if (V.ok) test((0.0 + V.Ab * V.dx) / s.E[R6_MD + V.j], V.lb, V.ub);
+  if (V.gok) test(r6_gen_dot(V, s.rhs) / s.E[R6_MD + R6_NV + V.j], V.gl, V.gu);
+  r6_max<1>(bad, s.red);
+  return bad[0] == 0.0;
+}
+
+__device__ __forceinline__ bool r6_check(R6Smem &s, R6Var &V, R6Row &R, const QPSettingsDev &st, const double (&o)[8],
+                         bool approx, int &status) {
+  const double pri = o[0], dua = o[3] / s.c;
+  double ea = st.eps_abs, er = st.eps_rel, epi = st.eps_prim_inf, edi = st.eps_dual_inf;
+  if (pri > QP_OSQP_INFTY || dua > QP_OSQP_INFTY) { status = -7; return true; }
+  if (approx) { ea *= 10; er *= 10; epi *= 10; edi *= 10; }
+  bool prim_ok = false, prim_inf = false, dual_ok = false, dual_inf = false;
+  if (pri < ea + er * fmax(o[1], o[2])) prim_ok = true;
+  else prim_inf = r6_primal_infeasible(s, V, R, epi);
+  if (dua < ea + er * fmax(fmax(o[4], o[5]), o[6]) / s.c) dual_ok = true;
+  else dual_inf = r6_dual_infeasible(s, V, R, edi);
+  if (prim_ok && dual_ok) { status = approx ? 2 : 1; return true; }
+  if (prim_inf) { status = approx ? 3 : -3; return true; }
+  if (dual_inf) { status = approx ? 4 : -4; return true; }
+  return false;
+}
+
+__device__ __forceinline__ void r6_rebuild_w(R6Smem &s, R6Var &V, R6Row &R) {
+  const double rs = s.rho_s;
+  if (R.ok) s.w[R.r] = QP_RHO_EQ * rs * R.zr - R.yr;
+  if (V.ok) V.ztb = r6_rho(V.lb, V.ub, rs) * V.zb - V.yb;
+  if (V.gok) s.w[R6_MD + V.j] = r6_rho(V.gl, V.gu, rs) * V.gz - V.gy;
+  __syncthreads();
+}
+
+__global__ __launch_bounds__(R6_T) void k_r6_control(R6Args a) {
+  const int b = blockIdx.x, tid = threadIdx.x;
+  double *rec = a.rec + (int64_t)b * GPMPC_REC_LEN;
+  if (rec[0] != 0.0) return;
+  extern __shared__ double smem_raw[];
+  R6Smem &s = *reinterpret_cast<R6Smem *>(smem_raw);
+  const double dt = a.dt;
+  const QPSettingsDev &st = a.st;
+  const double *Xb = a.Xp + (int64_t)b * (R6_N + 1) * R6_NX;
+  const double *Ub = a.U + (int64_t)b * R6_N * R6_NU;
+  const double *gmb = a.gm + (int64_t)b * R6_N * 6;
+  double *ysc = a.ysc + (int64_t)b * R6_M;
+  const double *x0 = a.x + (int64_t)b * R6_NX;
+  // incremental target (monte_carlo.py:497-500), upright and at rest
+  double xr[R6_NX];
+  for (int i = 0; i < R6_NX; ++i) xr[i] = x0[i];
+  xr[4] = xr[5] = xr[6] = 0.0;
+  xr[1] = fmax(0.5, x0[1] - 2.0);
+  xr[7] = 1.0; xr[8] = xr[9] = xr[10] = 0.0;
+  xr[11] = xr[12] = xr[13] = 0.0;
+  // ---- the linearisation (-[A_d | B_d] per stage, k_r6_predict) into the staging area
+  {
+    const double *lin = a.lin + (int64_t)b * R6_N * R6_NX * R6_SZ;
+    for (int e = tid; e < R6_N * R6_NX * R6_SZ; e += R6_T) s.G[e] = lin[e];
+  }
+  __syncthreads();
+  R6Var V;
+  R6Row R(V);
+  V.j = tid; V.ok = tid < R6_NV;
+  V.k = tid / R6_SZ; V.i = tid - V.k * R6_SZ;
+  V.gok = tid < R6_MGEN;
+  R.r = tid - R6_NV; R.ok = tid >= R6_NV && R.r < R6_MD;
+  R.k = R.r >= R6_NX ? (R.r - R6_NX) / R6_NX : 0;
+  R.i = R.r >= R6_NX ? (R.r - R6_NX) - R.k * R6_NX : R.r;
+  if (V.ok) {
+    const int k = V.k, i = V.i;
+    double xw, wq;
+    if (i < R6_NX) {
+      xw = Xb[k * R6_NX + i];
+      wq = r6_Q[i] * (k == R6_N ? 10.0 : 1.0);
+      V.P = wq; V.q = wq * (xw - xr[i]);
+      V.lb = -sqrt(10.0); V.ub = sqrt(10.0);
+    } else {
+      const double ub = Ub[k * R6_NU + i - R6_NX];
+      V.P = 0.01; V.q = 0.01 * ub;
+      V.lb = fmax(-sqrt(5.0), -R6_T_MAX - ub);
+      V.ub = fmin(sqrt(5.0), R6_T_MAX - ub);
+    }
+    V.Ab = 1.0;
+    V.x = 0.0;  // warm start dz = 0
+    V.yb = ysc[R6_MD + V.j];
+    if (k < R6_N)
+#pragma unroll
+      for (int e = 0; e < R6_NX; ++e) V.colA[e] = s.G[(k * R6_NX + e) * R6_SZ + i];
+    else
+#pragma unroll
+      for (int e = 0; e < R6_NX; ++e) V.colA[e] = 0.0;
+  }
+  if (V.gok) {
+    const int g = V.j;
+    if (g < R6_MT) {
+      const double *u = Ub + g * R6_NU;
+      const double tm = sqrt((u[0] * u[0] + u[1] * u[1]) + u[2] * u[2]);
+      V.gA[0] = u[0] / tm; V.gA[1] = u[1] / tm; V.gA[2] = u[2] / tm;
+      V.gl = R6_T_MIN - tm; V.gu = INFINITY; V.gn = 3;
+    } else {
+      const int gg = g - R6_MT, k = 1 + gg / 4, c = gg % 4;
+      const double tg = 0.5773502691896257;  // np.tan(np.deg2rad(30.0)), gamma_gs
+      const double rx = Xb[k * R6_NX + 1], rc = Xb[k * R6_NX + (c < 2 ? 2 : 3)];
+      const double sg = (c & 1) ? 1.0 : -1.0;
+      V.gA[0] = tg; V.gA[1] = sg; V.gA[2] = 0.0;
+      V.gl = -(tg * rx + sg * rc); V.gu = INFINITY; V.gn = 2;
+    }
+    V.gy = ysc[R6_MD + R6_NV + g];
+  }
+  if (R.ok) {
+    if (R.r < R6_NX) {
+      R.A[0] = 1.0;
+#pragma unroll
+      for (int e = 1; e <= R6_SZ; ++e) R.A[e] = 0.0;
+      R.ur = 0.0;
+    } else {
+#pragma unroll
+      for (int e = 0; e < R6_SZ; ++e) R.A[e] = s.G[(R.k * R6_NX + R.i) * R6_SZ + e];
+      R.A[R6_SZ] = 1.0;
+      const int i = R.i;
+      R.ur = (i >= 4 && i < 7) ? gmb[R.k * 6 + i - 4] * dt : ((i >= 11) ? gmb[R.k * 6 + 3 + i - 11] * dt : 0.0);
+    }
+    R.yr = ysc[R.r];
+  }
+  // ---- OSQP solve (qp_device.h order): clip bounds, Ruiz scaling, rho, factor
+  if (V.ok) { V.lb = fmax(V.lb, -QP_OSQP_INFTY); V.ub = fmin(V.ub, QP_OSQP_INFTY); }
+  if (V.gok) { V.gl = fmax(V.gl, -QP_OSQP_INFTY); V.gu = fmin(V.gu, QP_OSQP_INFTY); }
+  if (R.ok) R.ur = fmin(fmax(R.ur, -QP_OSQP_INFTY), QP_OSQP_INFTY);
+  for (int r = tid; r < R6_M; r += R6_T) s.E[r] = 1.0;
+  if (R.ok) s.dpl[R.r] = R.r < R6_NX ? R.A[0] : R.A[R6_SZ];
+  if (V.gok)
+#pragma unroll
+    for (int e = 0; e < 3; ++e) s.gen[V.j * 3 + e] = V.gA[e];
+  if (V.ok) V.D = 1.0;
+  if (tid == 0) { s.c = 1.0; s.rho_s = fmin(fmax(a.rho[b], QP_RHO_MIN), QP_RHO_MAX); }
+  __syncthreads();
+  for (int it = 0; it < st.scaling; ++it) {
+    // column factors -> dsc, row factors -> w (equality: [0, MD), general: MD + g)
+    double eb = 1.0;
+    if (V.ok) {
+      double v = fabs(V.P);
+      if (V.i < R6_NX) v = fmax(v, fabs(s.dpl[r6_eqid_row(V.k, V.i)]));
+      if (V.k < R6_N)
+#pragma unroll
+        for (int e = 0; e < R6_NX; ++e) v = fmax(v, fabs(V.colA[e]));
+      v = fmax(v, fabs(V.Ab));
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        int g, sl;
+        if (r6_gen_slot(V.k, V.i, e, g, sl)) v = fmax(v, fabs(s.gen[g * 3 + sl]));
+      }
+      s.dsc[V.j] = 1.0 / sqrt(qp_limit(v));
+      eb = 1.0 / sqrt(qp_limit(fmax(0.0, fabs(V.Ab))));
+    }
+    if (R.ok) {
+      double v = 0.0;
+      const int ne = R.r < R6_NX ? 1 : R6_SZ + 1;
+#pragma unroll
+      for (int e = 0; e < R6_SZ + 1; ++e)
+        if (e < ne) v = fmax(v, fabs(R.A[e]));
+      s.w[R.r] = 1.0 / sqrt(qp_limit(v));
+    }
+    if (V.gok) {
+      double v = 0.0;
+#pragma unroll
+      for (int e = 0; e < 3; ++e)
+        if (e < V.gn) v = fmax(v, fabs(V.gA[e]));
+      s.w[R6_MD + V.j] = 1.0 / sqrt(qp_limit(v));
+    }
+    __syncthreads();
+    if (R.ok) {
+      const double e = s.w[R.r];
+      if (R.r < R6_NX) {
+        R.A[0] = e * R.A[0] * s.dsc[R.r];
+        s.dpl[R.r] = R.A[0];
+      } else {
+        const int o = R.k * R6_SZ;
+#pragma unroll
+        for (int c = 0; c < R6_SZ; ++c) R.A[c] = e * R.A[c] * s.dsc[o + c];
+        R.A[R6_SZ] = e * R.A[R6_SZ] * s.dsc[(R.k + 1) * R6_SZ + R.i];
+        s.dpl[R.r] = R.A[R6_SZ];
+      }
+      s.E[R.r] *= e;
+    }
+    if (V.gok) {
+      const double e = s.w[R6_MD + V.j];
+      int col[3];
+      r6_gen_cols(V.j, col);
+#pragma unroll
+      for (int c = 0; c < 3; ++c)
+        if (c < V.gn) {
+          V.gA[c] = e * V.gA[c] * s.dsc[col[c]];
+          s.gen[V.j * 3 + c] = V.gA[c];
+        }
+      s.E[R6_MD + R6_NV + V.j] *= e;
+    }
+    double v[1] = {0.0}, mx[1] = {0.0};
+    if (V.ok) {
+      const double d = s.dsc[V.j];
+      if (V.k < R6_N)
+#pragma unroll
+        for (int e = 0; e < R6_NX; ++e) V.colA[e] = s.w[R6_NX + R6_NX * V.k + e] * V.colA[e] * d;
+      V.Ab = eb * V.Ab * d;
+      s.E[R6_MD + V.j] *= eb;
+      V.P = d * V.P * d;
+      V.q = d * V.q;
+      V.D *= d;
+      v[0] = fabs(V.P);
+      mx[0] = fabs(V.q);
+    }
+    r6_sum<1>(v, s.red);
+    r6_max<1>(mx, s.red);
+    double ct = v[0] / R6_NV;
+    const double nq = qp_limit(mx[0]);
+    ct = qp_limit(fmax(ct, nq));
+    ct = 1.0 / ct;
+    if (V.ok) { V.P *= ct; V.q *= ct; }
+    if (tid == 0) s.c *= ct;
+    __syncthreads();
+  }
+  if (V.ok) { const double e = s.E[R6_MD + V.j]; V.lb = e * V.lb; V.ub = e * V.ub; }
+  if (V.gok) { const double e = s.E[R6_MD + R6_NV + V.j]; V.gl = e * V.gl; V.gu = e * V.gu; }
+  if (R.ok) R.ur = s.E[R.r] * R.ur;
+  int f = r6_factor(s, V, R, st.sigma);
+  QPResult res{-10, 0, 0.0, 0};
+  if (f) res.factor_fail = f;
+  if (!f) {
+    // warm start x = 0 / D = 0, z = A x = 0; y persisted (osqp_rti.py:521-524)
+    V.x = 0.0; V.zb = 0.0; R.zr = 0.0; V.gz = 0.0;
+    if (V.ok) V.zb = 0.0 + V.Ab * V.x;
+    r6_rebuild_w(s, V, R);
+    const double sig = st.sigma, al = st.alpha;
+    bool can_check = false;
+    int it;
+    double o[8], re_[4];
+    for (it = 1; it <= st.max_iter; ++it) {
+      if (V.ok) s.rhs[V.j] = sig * V.x - V.q + r6_col_dot(s, V, s.w, V.ztb, s.w + R6_MD);
+      __syncthreads();
+      r6_solve(s);
+      const double rs = s.rho_s;
+      if (V.ok) {
+        const double xt = s.xs[V.j], xo = V.x;
+        const double xn = al * xt + (1.0 - al) * xo;
+        V.dx = xn - xo;
+        V.x = xn;
+        const double ztl = 0.0 + V.Ab * xt;
+        const double rho = r6_rho(V.lb, V.ub, rs), zo = V.zb, yo = V.yb;
+        const double zr = al * ztl + (1.0 - al) * zo;
+        double zn = zr + yo / rho;
+        zn = fmin(fmax(zn, V.lb), V.ub);
+        const double d = rho * (zr - zn);
+        V.dyb = d; V.yb = yo + d; V.zb = zn;
+        V.ztb = rho * zn - V.yb;
+      }
+      if (V.gok) {
+        const double ztl = r6_gen_dot(V, s.xs);
+        const double rho = r6_rho(V.gl, V.gu, rs), zo = V.gz, yo = V.gy;
+        const double zr = al * ztl + (1.0 - al) * zo;
+        double zn = zr + yo / rho;
+        zn = fmin(fmax(zn, V.gl), V.gu);
+        const double d = rho * (zr - zn);
+        V.gdy = d; V.gy = yo + d; V.gz = zn;
+      }
+      if (R.ok) {
+        const double ztl = r6_row_dot(R, s.xs);
+        const double rho = QP_RHO_EQ * rs, zo = R.zr, yo = R.yr;
+        const double zr = al * ztl + (1.0 - al) * zo;
+        double zn = zr + yo / rho;
+        zn = fmin(fmax(zn, R.ur), R.ur);
+        const double d = rho * (zr - zn);
+        R.dyr = d; R.yr = yo + d; R.zr = zn;
+      }
+      __syncthreads();  // every read of s.w / s.xs of this iteration is done
+      if (R.ok) s.w[R.r] = QP_RHO_EQ * rs * R.zr - R.yr;
+      if (V.gok) s.w[R6_MD + V.j] = r6_rho(V.gl, V.gu, rs) * V.gz - V.gy;
+      __syncthreads();
+      can_check = st.check_termination && (it % st.check_termination == 0);
+      const bool adapt = st.adaptive_rho && st.adaptive_rho_interval && (it % st.adaptive_rho_interval == 0);
+      if (can_check || adapt) {
+        res.iter = it;
+        r6_update_info(s, V, R, o, re_);
+      }
+      if (can_check && r6_check(s, V, R, st, o, false, res.status)) break;
+      if (adapt) {
+        const double pr = re_[0] / (re_[1] + 1e-10);
+        const double du = re_[2] / (re_[3] + 1e-10);
+        double est = s.rho_s * sqrt(pr / (du + 1e-10));
+        est = fmin(fmax(est, QP_RHO_MIN), QP_RHO_MAX);
+        if (est > s.rho_s * st.adaptive_rho_tolerance || est < s.rho_s / st.adaptive_rho_tolerance) {
+          __syncthreads();
+          if (tid == 0) s.rho_s = est;
+          __syncthreads();
+          if (it < st.max_iter) {
+            f = r6_factor(s, V, R, st.sigma);
+            if (f) { res.factor_fail = f; break; }
+          }
+        }
+      }
+      if (can_check || adapt) r6_rebuild_w(s, V, R);
+    }
+    if (!res.factor_fail) {
+      if (!can_check) {
+        res.iter = it - 1;
+        r6_update_info(s, V, R, o, re_);
+        r6_check(s, V, R, st, o, false, res.status);
+      }
+      if (res.status == -10) {
+        if (!r6_check(s, V, R, st, o, true, res.status)) res.status = -2;
+      }
+    }
+  }
+  const bool has = !res.factor_fail && (res.status == 1 || res.status == 2 || res.status == -2);
+  // ---- solution: the unscaled deviations onto the plan, kept unshifted (gp_mpc.py:358-359)
+  if (has && V.ok) s.xs[V.j] = V.D * V.x;
+  __syncthreads();
+  double *Xo = a.Xo + (int64_t)b * (R6_N + 1) * R6_NX;
+  double *Uw = a.U + (int64_t)b * R6_N * R6_NU;
+  if (has) {
+    for (int e = tid; e < (R6_N + 1) * R6_NX; e += R6_T) {
+      const int k = e / R6_NX, i = e - k * R6_NX;
+      Xo[e] = Xb[e] + s.xs[k * R6_SZ + i];
+    }
+    double un = 0.0;
+    if (tid < R6_N * R6_NU) {
+      const int k = tid / R6_NU, i = tid - k * R6_NU;
+      un = Ub[tid] + s.xs[k * R6_SZ + R6_NX + i];
+    }
+    __syncthreads();  // every thread read U before it is overwritten
+    if (tid < R6_N * R6_NU) Uw[tid] = un;
+    if (R.ok) ysc[R.r] = R.yr;
+    if (V.ok) ysc[R6_MD + V.j] = V.yb;
+    if (V.gok) ysc[R6_MD + R6_NV + V.j] = V.gy;
+    __syncthreads();
+  }
+  if (tid == 0) {
+    if (!has) {  // MPCSolution without a solution -> DIVERGENCE
+      const double *x = a.x + (int64_t)b * R6_NX;
+      rec[0] = 6;
+      rec[14] = res.factor_fail ? -100 : res.status;
+      rec[2] = rec[13] - x[0];
+      for (int i = 0; i < 7; ++i) rec[4 + i] = x[i];
+    } else {
+      a.rho[b] = s.rho_s;
+      rec[11] += res.iter;
+      rec[12] += (res.status == 1) ? 1.0 : 0.0;
+      rec[14] = res.status;
+      rec[15] = s.rho_s;
+      a.pending[b] = 1;
+    }
+  }
+}
+
+// 3. the truth plant step with the plan's first control: RK4 + the drag
+// dispersion at the pre-step state (dispersion.py:349-360) + the -0.05 w rate
+// damping the config-5 GP is trained on (data.synthetic_6dof_training_data)
+__global__ __launch_bounds__(64) void k_r6_plant(R6Args a, int B) {
+  const int b = blockIdx.x * 64 + threadIdx.x;
+  if (b >= B || !a.pending[b]) return;
+  a.pending[b] = 0;
+  double *rec = a.rec + (int64_t)b * GPMPC_REC_LEN;
+  double *x = a.x + (int64_t)b * R6_NX;
+  const double dt = a.dt;
+  double xc[R6_NX], xn[R6_NX];
+  for (int i = 0; i < R6_NX; ++i) xc[i] = x[i];
+  const double *u0 = a.U + (int64_t)b * R6_N * R6_NU;
+  r6_step(xc, u0, dt, xn);
+  const double vx = xc[4], vy = xc[5], vz = xc[6];
+  const double sp = sqrt((vx * vx + vy * vy) + vz * vz);
+  if (sp > 1.0) {
+    const double ac = (0.5 * 0.02 * sp * sp) / xc[0];
+    xn[4] += -ac * (vx / sp) * dt; xn[5] += -ac * (vy / sp) * dt; xn[6] += -ac * (vz / sp) * dt;
+  }
+  for (int i = 11; i < 14; ++i) xn[i] += -0.05 * xc[i] * dt;
+  for (int i = 0; i < R6_NX; ++i) x[i] = xn[i];
+  rec[1] += 1.0;
+  rec[2] = rec[13] - xn[0];
+  rec[3] = rec[1] * dt;
+  for (int i = 0; i < 7; ++i) rec[4 + i] = xn[i];
+}
+
+__global__ void k_r6_reset(int first, int count, const double *__restrict__ x0, double *x, double *U,
+                           double *ysc, double *rho, double rho0, double *rec) {
+  const int i = blockIdx.x;
+  if (i >= count) return;
+  const int b = first + i;
+  const double *xi = x0 + (int64_t)i * R6_NX;
+  for (int e = threadIdx.x; e < R6_N * R6_NU; e += blockDim.x)  // hover guess as written (gp_mpc.py:271-275)
+    U[(int64_t)b * R6_N * R6_NU + e] = (e % R6_NU == 2) ? xi[0] * 1.0 : 0.0;
+  for (int r = threadIdx.x; r < R6_M; r += blockDim.x) ysc[(int64_t)b * R6_M + r] = 0.0;
+  if (threadIdx.x < GPMPC_REC_LEN) rec[(int64_t)b * GPMPC_REC_LEN + threadIdx.x] = 0.0;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int c = 0; c < R6_NX; ++c) x[(int64_t)b * R6_NX + c] = xi[c];
+    for (int c = 0; c < 7; ++c) rec[(int64_t)b * GPMPC_REC_LEN + 4 + c] = xi[c];
+    rec[(int64_t)b * GPMPC_REC_LEN + 13] = xi[0];
+    rho[b] = rho0;
+  }
+}
+
+// ---------------------------------------------------------------------------
+extern "C" int gpmpc_rollout6_create(gpmpc_ctx *ctx, gpmpc_fitc *gp_v, gpmpc_fitc *gp_w,
+                                     const gpmpc_rollout6_config *cfg, int batch, gpmpc_rollout6 **out) {
+  GPMPC_CHECK_ARG(ctx && gp_v && gp_w && cfg && out && batch > 0);
+  const GpView gv = fitc_view(gp_v), gw = fitc_view(gp_w);
+  if (gv.d != 13 || gw.d != 12 || gv.n_out != 3 || gw.n_out != 3 || gv.kind != GPMPC_SE_ARD ||
+      gw.kind != GPMPC_SE_ARD) {
+    gpmpc_set_error("rollout6: expects the StructuredRocketGP FITC pair (13 / 12 features, 3 outputs, SE-ARD)");
+    return -2;
+  }
+  if (cfg->horizon != R6_N) {
+    gpmpc_set_error("rollout6: horizon must be %d (BASELINE configs[4])", R6_N);
+    return -2;
+  }
+  GPMPC_HIP(hipSetDevice(ctx->device));
+  auto *r = new gpmpc_rollout6();
+  r->ctx = ctx; r->gpv = gp_v; r->gpw = gp_w; r->cfg = *cfg; r->B = batch;
+  const size_t B = batch;
+  if (r->x.alloc(sizeof(double) * B * R6_NX) || r->U.alloc(sizeof(double) * B * R6_N * R6_NU) ||
+      r->Xp.alloc(sizeof(double) * B * (R6_N + 1) * R6_NX) || r->gm.alloc(sizeof(double) * B * R6_N * 6) ||
+      r->Xo.alloc(sizeof(double) * B * (R6_N + 1) * R6_NX) || r->ysc.alloc(sizeof(double) * B * R6_M) ||
+      r->rho.alloc(sizeof(double) * B) || r->rec.alloc(sizeof(double) * B * GPMPC_REC_LEN) ||
+      r->lin.alloc(sizeof(double) * B * R6_N * R6_NX * R6_SZ) || r->pending.alloc(sizeof(int) * B)) {
+    delete r;
+    gpmpc_set_error("rollout6: out of device memory");
+    return -1;
+  }
+  std::vector<double> rc(B * GPMPC_REC_LEN, 0.0);
+  for (size_t i = 0; i < B; ++i) rc[i * GPMPC_REC_LEN] = -1.0;  // not started until reset
+  hipMemcpyAsync(r->rec.p, rc.data(), sizeof(double) * rc.size(), hipMemcpyHostToDevice, ctx->stream);
+  hipMemsetAsync(r->Xo.p, 0, sizeof(double) * B * (R6_N + 1) * R6_NX, ctx->stream);
+  hipMemsetAsync(r->pending.p, 0, sizeof(int) * B, ctx->stream);
+  static bool attr = [] {
+    return hipFuncSetAttribute((const void *)k_r6_control, hipFuncAttributeMaxDynamicSharedMemorySize,
+                               (int)sizeof(R6Smem)) == hipSuccess;
+  }();
+  if (!attr) {
+    delete r;
+    gpmpc_set_error("rollout6: %zu B of LDS not available", sizeof(R6Smem));
+    return -1;
+  }
+  GPMPC_HIP(hipStreamSynchronize(ctx->stream));
+  *out = r;
+  return 0;
+}
+
+extern "C" int gpmpc_rollout6_reset(gpmpc_rollout6 *r, int first, int count, const double *x0) {
+  GPMPC_CHECK_ARG(r && x0 && first >= 0 && count >= 0 && first + count <= r->B);
+  if (count == 0) return 0;
+  hipStream_t s = r->ctx->stream;
+  DevBuf d;
+  GPMPC_HIP(d.alloc(sizeof(double) * count * R6_NX));
+  GPMPC_HIP(hipMemcpyAsync(d.p, x0, sizeof(double) * count * R6_NX, hipMemcpyHostToDevice, s));
+  hipLaunchKernelGGL(k_r6_reset, dim3(count), dim3(256), 0, s, first, count, d.as<double>(),
+                     r->x.as<double>(), r->U.as<double>(), r->ysc.as<double>(), r->rho.as<double>(),
+                     r->cfg.qp.rho, r->rec.as<double>());
+  GPMPC_HIP(hipGetLastError());
+  GPMPC_HIP(hipStreamSynchronize(s));
+  return 0;
+}
+
+static R6Args r6_args(gpmpc_rollout6 *r) {
+  R6Args a;
+  a.st = to_dev(r->cfg.qp);
+  a.dt = r->cfg.dt;
+  a.max_steps = r->cfg.max_steps;
+  a.x = r->x.as<double>(); a.U = r->U.as<double>(); a.Xp = r->Xp.as<double>();
+  a.gm = r->gm.as<double>(); a.Xo = r->Xo.as<double>(); a.ysc = r->ysc.as<double>();
+  a.rho = r->rho.as<double>(); a.rec = r->rec.as<double>();
+  a.lin = r->lin.as<double>(); a.pending = r->pending.as<int>();
+  a.gv = fitc_view(r->gpv); a.gw = fitc_view(r->gpw);
+  a.Mv = a.gv.n; a.Mw = a.gw.n;
+  return a;
+}
+
+extern "C" int gpmpc_rollout6_step(gpmpc_rollout6 *r, int nsteps) {
+  GPMPC_CHECK_ARG(r && nsteps >= 0);
+  GPMPC_HIP(hipSetDevice(r->ctx->device));
+  hipStream_t s = r->ctx->stream;
+  const R6Args a = r6_args(r);
+  for (int it = 0; it < nsteps; ++it) {
+    hipLaunchKernelGGL(k_r6_predict, dim3(r->B), dim3(R6_PT), 0, s, a);
+    hipLaunchKernelGGL(k_r6_control, dim3(r->B), dim3(R6_T), sizeof(R6Smem), s, a);
+    hipLaunchKernelGGL(k_r6_plant, dim3((r->B + 63) / 64), dim3(64), 0, s, a, r->B);
+    GPMPC_HIP(hipGetLastError());
+  }
+  return 0;
+}
+
+extern "C" int gpmpc_rollout6_read(gpmpc_rollout6 *r, double *records, double *x) {
+  GPMPC_CHECK_ARG(r);
+  hipStream_t s = r->ctx->stream;
+  if (records)
+    GPMPC_HIP(hipMemcpyAsync(records, r->rec.p, sizeof(double) * r->B * GPMPC_REC_LEN,
+                             hipMemcpyDeviceToHost, s));
+  if (x) GPMPC_HIP(hipMemcpyAsync(x, r->x.p, sizeof(double) * r->B * R6_NX, hipMemcpyDeviceToHost, s));
+  GPMPC_HIP(hipStreamSynchronize(s));
+  return 0;
+}
+
+extern "C" int gpmpc_rollout6_get_state(gpmpc_rollout6 *r, double *U, double *X_plan, double *X_pred,
+                                        double *gp_mean, double *y_scaled, double *rho) {
+  GPMPC_CHECK_ARG(r);
+  hipStream_t s = r->ctx->stream;
+  const size_t B = r->B;
+  if (U) GPMPC_HIP(hipMemcpyAsync(U, r->U.p, sizeof(double) * B * R6_N * R6_NU, hipMemcpyDeviceToHost, s));
+  if (X_plan)
+    GPMPC_HIP(hipMemcpyAsync(X_plan, r->Xo.p, sizeof(double) * B * (R6_N + 1) * R6_NX, hipMemcpyDeviceToHost, s));
+  if (X_pred)
+    GPMPC_HIP(hipMemcpyAsync(X_pred, r->Xp.p, sizeof(double) * B * (R6_N + 1) * R6_NX, hipMemcpyDeviceToHost, s));
+  if (gp_mean) GPMPC_HIP(hipMemcpyAsync(gp_mean, r->gm.p, sizeof(double) * B * R6_N * 6, hipMemcpyDeviceToHost, s));
+  if (y_scaled) GPMPC_HIP(hipMemcpyAsync(y_scaled, r->ysc.p, sizeof(double) * B * R6_M, hipMemcpyDeviceToHost, s));
+  if (rho) GPMPC_HIP(hipMemcpyAsync(rho, r->rho.p, sizeof(double) * B, hipMemcpyDeviceToHost, s));
+  GPMPC_HIP(hipStreamSynchronize(s));
+  return 0;
+}
+
+extern "C" int gpmpc_rollout6_destroy(gpmpc_rollout6 *r) {
+  if (r && r->ctx) (void)hipStreamSynchronize(r->ctx->stream);
+  delete r;
+  return 0;
+}

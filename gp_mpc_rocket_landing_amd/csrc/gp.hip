@@ -450,6 +450,13 @@ GpView gp_view(const gpmpc_gp *gp) {
                 g.ymean.as<double>(), g.ystd.as<double>()};
 }
 
+GpView fitc_view(const gpmpc_fitc *gp) {
+  const GpCore &g = gp->core;
+  return GpView{g.kind, g.n, g.d, g.n_out, g.sigma2, g.iso_scale, g.ls.as<double>(),
+                g.Xs.as<double>(), g.Xn.as<double>(), g.W.as<double>(), g.alphaT.as<double>(),
+                g.ymean.as<double>(), g.ystd.as<double>()};
+}
+
 // ---------------------------------------------------------------------------
 // FITC (sparse_gp.py:150-219 fit, :255-305 predict)
 extern "C" int gpmpc_fitc_fit(gpmpc_ctx *ctx, const double *Z, int m, const double *X, int n,

@@ -99,6 +99,8 @@ struct GpView {
   const double *ls, *Xs, *Xn, *W, *alphaT, *ymean, *ystd;
 };
 GpView gp_view(const gpmpc_gp *gp);
+// the same view of a FITC GP: n = inducing points, Xs / Xn their scaled rows, alphaT
+GpView fitc_view(const gpmpc_fitc *gp);
 // posterior finish: var/mean (P x n_out) from SUMSQ partials and K* alpha (gp.hip)
 hipError_t launch_post_finish(hipStream_t s, int P, int n_out, int nrt, const double *part,
                               int64_t ldp, const double *meanT, int64_t ldm, const double *ymean,

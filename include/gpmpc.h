@@ -255,6 +255,43 @@ int gpmpc_cov_propagate(gpmpc_ctx *ctx, int batch, int N, int nx, const double *
 int gpmpc_cov_propagate_dev(gpmpc_ctx *ctx, int batch, int N, int nx, const double *dA,
                             const double *dq, const double *dS0, double s0_diag, double *dout);
 
+/* ---- BASELINE configs[4]: batched 6-DoF GP-MPC rollouts --------------------
+ * gpmpc_rollout_batched of SURVEY 8b.  One step = for every running rollout:
+ * the Monte-Carlo termination rules (monte_carlo.py:455-488 on [m, r, v]),
+ * GPMPC.solve's forward simulation with the StructuredRocketGP FITC means
+ * (gp_mpc.py:258-281; RK4 of nominal_mpc.py:163-203), the QP subproblem of
+ * gp_mpc.py:394-460 in deviation variables with its QCQP rows made linear
+ * (DESIGN.md section 9), the OSQP-0.6 ADMM on the block-tridiagonal reduced
+ * KKT matrix, the truth plant step (RK4 + the dispersion.py:349-360 drag) and
+ * the plan kept unshifted as the next warm start.  State 14 = [m, r_I, v_I,
+ * q_BI (w, x, y, z), omega_B]; horizon fixed at 30. */
+typedef struct gpmpc_rollout6 gpmpc_rollout6;
+typedef struct {
+  int horizon;           /* must be 30 */
+  double dt;
+  int max_steps;
+  gpmpc_qp_settings qp;  /* osqp_rti.py:54-60 defaults */
+} gpmpc_rollout6_config;
+void gpmpc_rollout6_default_config(gpmpc_rollout6_config *c);
+/* gp_v: FITC on the 13 translational features, gp_w: on the 12 rotational
+ * ones (features.py:149-365), 3 outputs each; both must outlive the batch */
+int gpmpc_rollout6_create(gpmpc_ctx *ctx, gpmpc_fitc *gp_v, gpmpc_fitc *gp_w,
+                          const gpmpc_rollout6_config *cfg, int batch, gpmpc_rollout6 **out);
+/* (re)start rollouts [first, first+count) at x0 (count x 14) */
+int gpmpc_rollout6_reset(gpmpc_rollout6 *r, int first, int count, const double *x0);
+/* nsteps control steps of every running rollout (async on the ctx stream) */
+int gpmpc_rollout6_step(gpmpc_rollout6 *r, int nsteps);
+/* records (batch x GPMPC_REC_LEN, the fleet layout; state slots hold [m, r, v])
+ * and the full states (batch x 14, may be NULL) */
+int gpmpc_rollout6_read(gpmpc_rollout6 *r, double *records, double *x);
+/* controller state, any pointer may be NULL: warm-start controls U (batch x 30
+ * x 3), last QP plan X (batch x 31 x 14), forward-simulated X_pred (batch x 31
+ * x 14), its GP means (batch x 30 x 6: d_v, d_omega), the ADMM's persistent
+ * scaled duals (batch x 1104) and rho (batch) */
+int gpmpc_rollout6_get_state(gpmpc_rollout6 *r, double *U, double *X_plan, double *X_pred,
+                             double *gp_mean, double *y_scaled, double *rho);
+int gpmpc_rollout6_destroy(gpmpc_rollout6 *r);
+
 /* device pointer of the record array (for collectives) */
 double *gpmpc_fleet_records_dev(gpmpc_fleet *f);
 int gpmpc_fleet_destroy(gpmpc_fleet *f);

@@ -1,0 +1,320 @@
+"""6-DoF GP-MPC rollout restatement (TEST INFRASTRUCTURE ONLY) -- BASELINE configs[4].
+
+The reference's 6-DoF closed loop is ``GPMPC.solve`` (src/mpc/gp_mpc.py:229-369)
+over the 14-state rocket of src/dynamics/rocket_6dof.py, whose physics lives in
+the absent ``simdyn``.  This module restates what the reference spells out and
+pins the rest as documented choices:
+
+* dynamics f(x, u): nominal_mpc.py:163-203 (state [m, r_I, v_I, q_BI (w,x,y,z),
+  w_B]; C_IB of :176-181; m' = -alpha |u|; v' = C_IB u / m + g_I; q' =
+  0.5 Omega(w) q; w' = J^-1 (r_T x u - w x J w)), parameters of
+  Rocket6DoFConfig (rocket_6dof.py:36-84: J = diag(0.02, 1, 1) 0.168,
+  r_T = (-0.25, 0, 0), g_I = (-1, 0, 0), alpha = 1 / (I_sp g0) = 1/30);
+* plant step: RK4 (discretization.py:229-252) + quaternion normalisation
+  (rocket_6dof.py:371-387); linearisation A_d = I + A_c dt, B_d = B_c dt with
+  the analytic continuous Jacobians (rocket_6dof.py:427-459);
+* truth = plant + the aero-drag dispersion on the velocity
+  (dispersion.py:349-360) and a -0.05 w rate damping (the residuals of the
+  config-5 training generator), evaluated at the pre-step state;
+* one control step = one pass of GPMPC.solve: forward simulation of the
+  warm-start controls with the GP mean (gp_mpc.py:258-281, hover guess
+  [0, 0, m g0] of :271-275 on the first call), linearisation and
+  c_k = [.., d_v dt, .., d_w dt] at the simulated points (:299-320), the QP
+  subproblem in deviation variables (:394-460) with its QCQP constraints made
+  linear -- thrust ball -> box [-T_max, T_max]^3, |u| >= T_min linearised at
+  U_nom, glideslope cone -> 4 half-planes (stages 1..N-1), trust balls -> boxes
+  sqrt(10) / sqrt(5) -- solved by the OSQP-0.6 restatement (admm_ref) with
+  osqp_rti.py's settings, warm start dz = 0 with OSQP's persistent rho / y;
+  X_pred + dX, U_pred + dU returned; the plan is kept unshifted as the next
+  warm start (:358-359); a solve without a solution -> DIVERGENCE.
+"""
+from __future__ import annotations
+
+import numpy as np
+import scipy.sparse as sp
+
+NX, NU = 14, 3
+ALPHA = 1.0 / 30.0
+J_DIAG = np.array([0.02, 1.0, 1.0]) * 0.168
+R_T = np.array([-0.25, 0.0, 0.0])
+G_I = np.array([-1.0, 0.0, 0.0])
+G0 = 1.0
+T_MIN, T_MAX = 0.5, 5.0                 # ConstraintParams (constraints.py:35-50)
+TAN_GS = np.tan(np.deg2rad(30.0))       # gamma_gs 30 deg
+TRUST_X, TRUST_U = np.sqrt(10.0), np.sqrt(5.0)   # gp_mpc.py:432-435
+Q_DIAG = np.array([0.0, 10, 10, 10, 1, 1, 1, 0, 5, 5, 0, 0.1, 0.1, 0.1])  # CostWeights (cost_functions.py:75-98)
+R_DIAG = np.full(3, 0.01)
+P_SCALE = 10.0
+
+
+def dcm_ib(q):
+    """C_IB of nominal_mpc.py:176-181 (body -> inertial)."""
+    w, x, y, z = q
+    return np.array([[1 - 2 * (y * y + z * z), 2 * (x * y - w * z), 2 * (x * z + w * y)],
+                     [2 * (x * y + w * z), 1 - 2 * (x * x + z * z), 2 * (y * z - w * x)],
+                     [2 * (x * z - w * y), 2 * (y * z + w * x), 1 - 2 * (x * x + y * y)]])
+
+
+def f(x, u):
+    """nominal_mpc.py:163-203."""
+    m, v, q, w = x[0], x[4:7], x[7:11], x[11:14]
+    tm = np.sqrt(u @ u)
+    out = np.empty(NX)
+    out[0] = -ALPHA * tm
+    out[1:4] = v
+    out[4:7] = dcm_ib(q) @ u / m + G_I
+    qv = q[1:4]
+    out[7] = 0.5 * -(w @ qv)
+    out[8:11] = 0.5 * (q[0] * w + np.cross(w, qv))
+    torque = np.cross(R_T, u)
+    jw = J_DIAG * w
+    out[11:14] = (torque - np.cross(w, jw)) / J_DIAG
+    return out
+
+
+def step(x, u, dt):
+    """RK4 (discretization.py:229-252) + quaternion normalisation (rocket_6dof.py:371-387)."""
+    k1 = f(x, u)
+    k2 = f(x + dt * k1 / 2, u)
+    k3 = f(x + dt * k2 / 2, u)
+    k4 = f(x + dt * k3, u)
+    xn = x + (dt / 6) * (k1 + 2 * k2 + 2 * k3 + k4)
+    xn[7:11] = xn[7:11] / np.sqrt(xn[7:11] @ xn[7:11])
+    return xn
+
+
+def jacobians(x, u):
+    """Analytic A_c = df/dx (14 x 14), B_c = df/du (14 x 3) of f."""
+    m, q, w = x[0], x[7:11], x[11:14]
+    qw, qx, qy, qz = q
+    u0, u1, u2 = u
+    A = np.zeros((NX, NX)); B = np.zeros((NX, NU))
+    tm = np.sqrt(u @ u)
+    B[0] = -ALPHA * u / tm
+    A[1:4, 4:7] = np.eye(3)
+    C = dcm_ib(q)
+    A[4:7, 0] = -(C @ u) / (m * m)
+    dCu = np.array([  # d(C u)/d(w, x, y, z)
+        [-2 * qz * u1 + 2 * qy * u2, 2 * qy * u1 + 2 * qz * u2, -4 * qy * u0 + 2 * qx * u1 + 2 * qw * u2,
+         -4 * qz * u0 - 2 * qw * u1 + 2 * qx * u2],
+        [2 * qz * u0 - 2 * qx * u2, 2 * qy * u0 - 4 * qx * u1 - 2 * qw * u2, 2 * qx * u0 + 2 * qz * u2,
+         2 * qw * u0 - 4 * qz * u1 + 2 * qy * u2],
+        [-2 * qy * u0 + 2 * qx * u1, 2 * qz * u0 + 2 * qw * u1 - 4 * qx * u2, -2 * qw * u0 + 2 * qz * u1 - 4 * qy * u2,
+         2 * qx * u0 + 2 * qy * u1]])
+    A[4:7, 7:11] = dCu / m
+    B[4:7] = C / m
+    wx, wy, wz = w
+    A[7:11, 7:11] = 0.5 * np.array([[0, -wx, -wy, -wz], [wx, 0, -wz, wy], [wy, wz, 0, -wx], [wz, -wy, wx, 0]])
+    A[7, 11:14] = -0.5 * q[1:4]
+    A[8:11, 11:14] = 0.5 * np.array([[qw, qz, -qy], [-qz, qw, qx], [qy, -qx, qw]])
+    j1, j2, j3 = J_DIAG
+    A[11, 11:14] = -(j3 - j2) / j1 * np.array([0, wz, wy])
+    A[12, 11:14] = -(j1 - j3) / j2 * np.array([wz, 0, wx])
+    A[13, 11:14] = -(j2 - j1) / j3 * np.array([wy, wx, 0])
+    rx, ry, rz = R_T
+    B[11:14] = np.array([[0, -rz, ry], [rz, 0, -rx], [-ry, rx, 0]]) / J_DIAG[:, None]
+    return A, B
+
+
+def linearize(x, u, dt):
+    """rocket_6dof.py:451-457."""
+    A, B = jacobians(x, u)
+    return np.eye(NX) + A * dt, B * dt
+
+
+def drag(x):
+    """dispersion.py:349-360: rho 0.02, Cd = A = 1, applied when |v| > 1."""
+    v = x[4:7]
+    sp_ = np.sqrt(v @ v)
+    if sp_ > 1.0:
+        return -(0.5 * 0.02 * sp_ ** 2) / x[0] * (v / sp_)
+    return np.zeros(3)
+
+
+def truth_step(x, u, dt):
+    """The rollout plant: nominal step + the residual the config-5 GP is trained on
+    (data.synthetic_6dof_training_data): the drag dispersion on v and a rate
+    damping -0.05 w on w-dot, both at the pre-step state."""
+    xn = step(x, u, dt)
+    xn[4:7] += drag(x) * dt
+    xn[11:14] += -0.05 * x[11:14] * dt
+    return xn
+
+
+def gp_mean(gpv, gpw, x, u):
+    """StructuredRocketGP.predict means (structured_gp.py:225-268) via the FITC oracle."""
+    from . import gp_oracle
+    mv, _ = gp_oracle.fitc_predict(gpv, gp_oracle.features_translational(x[None], u[None]))
+    mw, _ = gp_oracle.fitc_predict(gpw, gp_oracle.features_rotational(x[None], u[None]))
+    return mv[0], mw[0]
+
+
+def qp_pattern(N):
+    """CSR pattern of the 6-DoF QP (row order: x0, dynamics, bounds, thrust, glideslope)."""
+    n = N * (NX + NU) + NX
+    rows = []
+    for i in range(NX):
+        rows.append([i])
+    for k in range(N):
+        o, on = k * (NX + NU), (k + 1) * (NX + NU)
+        for i in range(NX):
+            rows.append(list(range(o, o + NX + NU)) + [on + i])
+    for j in range(n):
+        rows.append([j])
+    for k in range(N):
+        o = k * (NX + NU) + NX
+        rows.append([o, o + 1, o + 2])
+    for k in range(1, N):
+        o = k * (NX + NU)
+        for c in (2, 3):
+            rows.append([o + 1, o + c])
+            rows.append([o + 1, o + c])
+    rp = np.cumsum([0] + [len(r) for r in rows])
+    ci = np.concatenate(rows)
+    return n, len(rows), rp.astype(np.int32), ci.astype(np.int32)
+
+
+def build_qp(Xn, Un, gm, x_ref, dt):
+    """QP of gp_mpc.py:394-460 around (Xn, Un) with c_k = GP mean dt (gp_mpc.py:309-314)
+    in deviation variables z = [dx_0, du_0, ..., dx_N].  Returns Pdiag, q, A (CSR), l, u."""
+    N = Un.shape[0]
+    n, m, rp, ci = qp_pattern(N)
+    val = np.zeros(rp[-1]); l = np.zeros(m); u = np.zeros(m)
+    Pd = np.zeros(n); q = np.zeros(n)
+    for k in range(N + 1):
+        o = k * (NX + NU)
+        w = Q_DIAG * (P_SCALE if k == N else 1.0)
+        Pd[o:o + NX] = w
+        q[o:o + NX] = w * (Xn[k] - x_ref)
+        if k < N:
+            Pd[o + NX:o + NX + NU] = R_DIAG
+            q[o + NX:o + NX + NU] = R_DIAG * Un[k]
+    r = 0
+    for i in range(NX):
+        val[rp[r]] = 1.0; r += 1      # dx_0 = x0 - X_nom[0] = 0
+    for k in range(N):
+        Ad, Bd = linearize(Xn[k], Un[k], dt)
+        c = np.zeros(NX)
+        c[4:7] = gm[k, :3] * dt
+        c[11:14] = gm[k, 3:] * dt
+        for i in range(NX):
+            a = rp[r]
+            val[a:a + NX] = -Ad[i]
+            val[a + NX:a + NX + NU] = -Bd[i]
+            val[a + NX + NU] = 1.0
+            l[r] = u[r] = c[i]
+            r += 1
+    for j in range(n):
+        k, i = divmod(j, NX + NU)
+        val[rp[r]] = 1.0
+        if i < NX:
+            l[r], u[r] = -TRUST_X, TRUST_X
+        else:
+            ub = Un[k, i - NX]
+            l[r] = max(-TRUST_U, -T_MAX - ub)
+            u[r] = min(TRUST_U, T_MAX - ub)
+        r += 1
+    for k in range(N):
+        ub = Un[k]
+        tm = np.sqrt(ub @ ub)
+        val[rp[r]:rp[r] + 3] = ub / tm
+        l[r], u[r] = T_MIN - tm, np.inf
+        r += 1
+    for k in range(1, N):
+        rx, ry, rz = Xn[k, 1:4]
+        for c, rc in ((2, ry), (3, rz)):
+            a = rp[r]
+            val[a:a + 2] = (TAN_GS, -1.0); l[r], u[r] = -(TAN_GS * rx - rc), np.inf; r += 1
+            a = rp[r]
+            val[a:a + 2] = (TAN_GS, 1.0); l[r], u[r] = -(TAN_GS * rx + rc), np.inf; r += 1
+    A = sp.csr_matrix((val, ci, rp), shape=(m, n))
+    return Pd, q, A, l, u
+
+
+def incremental_target(x):
+    """monte_carlo.py:497-500 on the 14-state layout, upright and at rest."""
+    t = x.copy()
+    t[4:7] = 0.0
+    t[1] = max(0.5, x[1] - 2.0)
+    t[7:11] = (1.0, 0.0, 0.0, 0.0)
+    t[11:14] = 0.0
+    return t
+
+
+def hover_guess(x, N):
+    """gp_mpc.py:271-275 (as written: thrust on the body z axis)."""
+    U = np.zeros((N, NU))
+    U[:, 2] = x[0] * G0
+    return U
+
+
+def new_rollout(x0, N=30):
+    from . import admm_ref
+    n, m, _, _ = qp_pattern(N)
+    rec = np.zeros(16)
+    rec[4:11] = x0[:7]
+    rec[13] = x0[0]
+    return dict(x=np.array(x0, float), U=hover_guess(x0, N), y=np.zeros(m),
+                rho=admm_ref.default_settings().rho, rec=rec, X=None)
+
+
+def rollout_step(gpv, gpw, S, dt=0.1, max_steps=300, qp_settings=None):
+    """One control step of the 6-DoF rollout (monte_carlo.py:455-537 termination
+    rules on the first seven states; one GPMPC.solve pass as the module header)."""
+    from . import admm_ref, mc_oracle
+    x = S["x"].copy(); U = S["U"].copy(); rec = S["rec"].copy()
+    N = U.shape[0]
+    out = dict(S, x=x, U=U, rec=rec, y=S["y"].copy())
+    if rec[0] != 0:
+        return out, None
+    m0 = rec[13]
+    o = mc_oracle.TIMEOUT if rec[1] >= max_steps else mc_oracle.pre_step_outcome(x[:7], m0)
+    if o == 0 and (np.any(np.abs(x) > 1e6) or np.any(np.isnan(x))):
+        o = mc_oracle.DIVERGENCE
+    if o:
+        rec[0] = o; rec[2] = m0 - x[0]; rec[4:11] = x[:7]
+        return out, None
+    # forward simulation with the GP mean (gp_mpc.py:258-281)
+    X = np.zeros((N + 1, NX)); X[0] = x
+    gm = np.zeros((N, 6))
+    for k in range(N):
+        dv, dw = gp_mean(gpv, gpw, X[k], U[k])
+        gm[k, :3], gm[k, 3:] = dv, dw
+        X[k + 1] = step(X[k], U[k], dt)
+        X[k + 1, 4:7] += dv * dt
+        X[k + 1, 11:14] += dw * dt
+    Pd, q, A, l, u = build_qp(X, U, gm, incremental_target(x), dt)
+    qp = admm_ref.RefQP(len(out["y"]), settings=qp_settings)
+    qp.y = out["y"]; qp.rho = np.array([out["rho"]])
+    try:
+        r = qp.solve(Pd, q, A, l, u, np.zeros(Pd.size))
+    except RuntimeError:
+        rec[0] = mc_oracle.DIVERGENCE; rec[14] = -100; rec[2] = m0 - x[0]; rec[4:11] = x[:7]
+        return out, (0, -100)
+    if r["status"] not in (1, 2, -2):
+        rec[0] = mc_oracle.DIVERGENCE; rec[14] = r["status"]; rec[2] = m0 - x[0]; rec[4:11] = x[:7]
+        return out, (r["iter"], r["status"])
+    z = r["x"]
+    Xo = X + np.array([z[k * (NX + NU):k * (NX + NU) + NX] for k in range(N + 1)])
+    Uo = U + np.array([z[k * (NX + NU) + NX:(k + 1) * (NX + NU)] for k in range(N)])
+    xn = truth_step(x, Uo[0], dt)
+    out.update(x=xn, U=Uo, X=Xo, X_pred=X, y=qp.y, rho=float(qp.rho[0]), gm=gm)
+    rec[1] += 1; rec[2] = m0 - xn[0]; rec[3] = rec[1] * dt; rec[4:11] = xn[:7]
+    rec[11] += r["iter"]; rec[12] += r["status"] == 1; rec[14] = r["status"]; rec[15] = qp.rho[0]
+    return out, (r["iter"], r["status"])
+
+
+def initial_condition(seed):
+    """6-DoF rollout start: the run_experiments 3-DoF draw (mc_oracle) for
+    [m, r, v], then a tilt of N(0, 5 deg) about a random horizontal body axis,
+    at rest in rotation."""
+    from . import mc_oracle
+    x7 = mc_oracle.sample_initial_condition(seed)
+    rs = np.random.RandomState(seed + 7919)
+    ang = np.deg2rad(5.0) * rs.randn()
+    phi = 2 * np.pi * rs.rand()
+    ax = np.array([0.0, np.cos(phi), np.sin(phi)])
+    x = np.zeros(NX)
+    x[:7] = x7
+    x[7] = np.cos(ang / 2); x[8:11] = ax * np.sin(ang / 2)
+    return x

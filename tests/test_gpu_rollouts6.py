@@ -1,0 +1,84 @@
+"""BASELINE configs[4] on the device: 6-DoF GP-MPC rollouts (csrc/fleet6.hip)
+against the CPU restatement (oracle/sixdof_oracle.py: RK4 of nominal_mpc.py
+:163-203, GPMPC.solve's forward simulation with the StructuredRocketGP FITC
+means, the QP subproblem of gp_mpc.py:394-460 made linear, the C OSQP-0.6
+restatement, the truth plant).
+
+Every control step is checked from the device's own previous state (x, the
+warm-start controls U, OSQP's persistent scaled y and rho, the record), so the
+inputs are identical: ADMM iterations, status, outcome and step count exact;
+the forward-simulated X_pred, its GP means, the QP plan X, the new U, the next
+state, rho and the duals within the SURVEY 8c tolerance (1e-6 relative, unit
+floor; duals floored at max |y|)."""
+import numpy as np
+import pytest
+
+from conftest import close
+
+pytestmark = pytest.mark.gpu
+
+
+def _oracle_gps(n_train, n_inducing, seed=0):
+    from gp_mpc_rocket_landing_amd.data import synthetic_6dof_training_data
+    from oracle import gp_oracle
+    X, U, Dv, Dw = synthetic_6dof_training_data(n_train, seed=seed)
+    Zv = gp_oracle.features_translational(X, U); Zw = gp_oracle.features_rotational(X, U)
+    idx = np.sort(np.random.RandomState(seed + 3).choice(n_train, min(n_inducing, n_train), replace=False))
+    return gp_oracle.fitc_fit(Zv[idx], Zv, Dv), gp_oracle.fitc_fit(Zw[idx], Zw, Dw)
+
+
+def _one(S, b):
+    return {k: (v[b] if k != "rho" else float(v[b])) for k, v in S.items()}
+
+
+def _run(gpu_ctx, n_train, n_inducing, nb, steps, tol=1e-6):
+    from gp_mpc_rocket_landing_amd.rollouts6 import Rollouts6, fit_structured_fitc, initial_conditions_6dof
+    from oracle import sixdof_oracle as so
+    gv, gw = fit_structured_fitc(gpu_ctx, n_train=n_train, n_inducing=n_inducing)
+    ov, ow = _oracle_gps(n_train, n_inducing)
+    x0 = initial_conditions_6dof(nb)
+    ro = Rollouts6(gpu_ctx, gv, gw, nb)
+    seen = 0
+    try:
+        ro.reset(x0)
+        S = ro.state()
+        for k in range(steps):
+            if np.all(S["rec"][:, 0] != 0):
+                break
+            ro.step(1)
+            T = ro.state()
+            for b in np.nonzero(S["rec"][:, 0] == 0)[0]:
+                st = dict(x=S["x"][b], U=S["U"][b], y=S["y"][b], rho=float(S["rho"][b]), rec=S["rec"][b], X=None)
+                want, info = so.rollout_step(ov, ow, st)
+                got = _one(T, b)
+                tag = (k, int(b))
+                np.testing.assert_array_equal(got["rec"][[0, 1, 11, 12, 13, 14]],
+                                              want["rec"][[0, 1, 11, 12, 13, 14]], err_msg=str(tag))
+                if info is None or want["rec"][0] != 0:
+                    continue
+                seen += 1
+                ok, worst = close(got["X_pred"], want["X_pred"], 1.0, rtol=tol); assert ok, (tag, "X_pred", worst)
+                ok, worst = close(got["gm"], want["gm"], 1.0, rtol=tol); assert ok, (tag, "gm", worst)
+                for key in ("X", "U", "x"):
+                    ok, worst = close(got[key], want[key], 1.0, rtol=tol)
+                    assert ok, (tag, key, worst)
+                ok, worst = close(got["rho"], want["rho"], 0.0, rtol=tol); assert ok, (tag, "rho", worst)
+                ok, worst = close(got["y"], want["y"], np.abs(want["y"]).max(), rtol=tol)
+                assert ok, (tag, "y", worst)
+            S = T
+    finally:
+        ro.close()
+    return seen, S
+
+
+def test_rollouts6_match_oracle_small_gp(gpu_ctx):
+    """4 rollouts x 40 control steps on a FITC pair with M = 50, N = 300."""
+    seen, S = _run(gpu_ctx, 300, 50, 4, 40)
+    assert seen >= 40, seen
+
+
+def test_rollouts6_match_oracle_config5_gp(gpu_ctx):
+    """The config-5 GP size (M = 2000 inducing, N = 4000 training rows, two GPs):
+    4 rollouts x 4 control steps."""
+    seen, S = _run(gpu_ctx, 4000, 2000, 4, 4)
+    assert seen >= 8, seen
