@@ -429,6 +429,47 @@ def gpmpc_loop_bench(ctx, gp, batch=1024, reps=3, sqp_iters=10):
             "outcomes": {str(int(c)): int(np.sum(rec[:, 0] == c)) for c in np.unique(rec[:, 0])}}
 
 
+def rollouts6_bench(ctx, batches=(64, 512), max_steps=300):
+    """BASELINE configs[4]: 6-DoF GP-MPC rollouts, N = 30, the StructuredRocketGP
+    FITC pair at M = 2000 inducing / N = 4000 training rows (csrc/fleet6.hip).
+    Every rollout flies to termination (run_experiments initial conditions + a
+    random tilt); 64 = one GPU's share of the config's 512 over 8 GPUs, 512 =
+    the whole config on one GPU.  The GP fit is outside the timed region."""
+    from gp_mpc_rocket_landing_amd.rollouts6 import Rollouts6, fit_structured_fitc, initial_conditions_6dof
+    t0 = time.perf_counter()
+    gv, gw = fit_structured_fitc(ctx, n_train=4000, n_inducing=2000)
+    fit_s = time.perf_counter() - t0
+    out = {"workload": "6-DoF GPMPC rollouts, N=30, FITC M=2000 / N_train=4000 x 2 GPs, to termination",
+           "gp_fit_ms": round(fit_s * 1e3, 1)}
+    for B in batches:
+        ro = Rollouts6(ctx, gv, gw, B, max_steps=max_steps)
+        try:
+            ro.reset(initial_conditions_6dof(B))
+            ro.step(1)          # warm-up: first launch of each kernel
+            ctx.sync()
+            ro.reset(initial_conditions_6dof(B))
+            ctx.sync()
+            t0 = time.perf_counter()
+            steps = 0
+            while steps < max_steps + 1:
+                ro.step(10)
+                steps += 10
+                rec, _ = ro.read()
+                if np.all(rec[:, 0] != 0):
+                    break
+            el = time.perf_counter() - t0
+        finally:
+            ro.close()
+        ctrl = float(rec[:, 1].sum())
+        out[str(B)] = {"s": round(el, 4), "rollouts_per_s": round(B / el, 1),
+                       "control_steps_per_s": round(ctrl / el, 1), "launched_steps": steps,
+                       "ms_per_step": round(el / steps * 1e3, 3),
+                       "mean_steps_per_rollout": round(ctrl / B, 1),
+                       "admm_iters_per_solve": round(float(rec[:, 11].sum()) / max(ctrl, 1.0), 2),
+                       "outcomes": {str(int(c)): int(np.sum(rec[:, 0] == c)) for c in np.unique(rec[:, 0])}}
+    return out
+
+
 def structured_fitc_bench(ctx, reps=2):
     """BASELINE config 5 GP: StructuredRocketGP with FITC M = 2000, N_train = 4000
     (two 3-output GPs, D = 13 translational / 12 rotational features), and one
@@ -624,6 +665,7 @@ def main():
                 out["simple3dof_gp"] = simple3dof_gp_bench(ctx, cpu=not args.no_cpu)
                 out["cholesky"] = cholesky_bench(ctx, torch)
                 out["structured_fitc"] = structured_fitc_bench(ctx)
+                out["rollouts6"] = rollouts6_bench(ctx)
                 out["lml_batched"] = lml_bench(ctx, cpu=not args.no_cpu)
                 out["gp_append"] = append_bench(ctx)
             except Exception as e:  # noqa: BLE001

@@ -66,7 +66,7 @@ class QPSettings(ctypes.Structure):
 
 class Rollout6Config(ctypes.Structure):
     _fields_ = [("horizon", ctypes.c_int), ("dt", ctypes.c_double), ("max_steps", ctypes.c_int),
-                ("qp", QPSettings)]
+                ("qp", QPSettings), ("fitc_mean_as_written", ctypes.c_int)]
 
 
 class FleetConfig(ctypes.Structure):

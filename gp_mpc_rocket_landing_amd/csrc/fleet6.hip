@@ -9,7 +9,9 @@
 //      + [.., d_v dt, .., d_w dt] with the FITC means of the two GPs at
 //      (X[k], U[k]) (structured_gp.py:225-268; sparse_gp.py:255-305 mean as
 //      written, K*u alpha) -- the 2 x M kernel rows of a point are spread over
-//      the workgroup and reduced; the 30 points are sequential.
+//      the workgroup and reduced; the 30 points are sequential.  The mean is the
+//      FITC posterior mean K*u L_uu^-T alpha (SURVEY D1 fixed; the reference's
+//      K*u alpha behind fitc_mean_as_written).
 //   2. k_r6_control  (1024 threads / rollout): the QP subproblem of
 //      gp_mpc.py:394-460 in deviation variables z = [dx_0, du_0, .., dx_30]
 //      (n = 524): x0 + dynamics equalities with A_d = I + A_c dt, B_d = B_c dt
@@ -64,6 +66,7 @@ struct gpmpc_rollout6 {
   gpmpc_rollout6_config cfg{};
   int B = 0;
   DevBuf x, U, Xp, gm, Xo, ysc, rho, rec, lin, pending;
+  DevBuf betav, betaw;  // (L_uu^-T alpha)^T of each GP, 3 x M
 };
 
 extern "C" void gpmpc_rollout6_default_config(gpmpc_rollout6_config *c) {
@@ -71,6 +74,18 @@ extern "C" void gpmpc_rollout6_default_config(gpmpc_rollout6_config *c) {
   c->dt = 0.1;
   c->max_steps = 300;
   gpmpc_qp_default_settings(&c->qp);   // osqp_rti.py:54-60 settings, as the 3-DoF path
+  c->fitc_mean_as_written = 0;         // FITC posterior mean (SURVEY D1 fixed, flag 1 = as written)
+}
+
+// beta^T = alpha^T L_uu^-1 (3 x M): the FITC posterior mean is K*u beta.
+// W = L_uu^-1 (lower, row-major, ld M) is the fit's first M rows of core.W.
+__global__ void k_fitc_beta(int M, const double *__restrict__ W, const double *__restrict__ alphaT,
+                            double *__restrict__ betaT) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x, c = blockIdx.y;
+  if (i >= M) return;
+  double acc = 0.0;
+  for (int j = i; j < M; ++j) acc = fma(alphaT[(int64_t)c * M + j], W[(int64_t)j * M + i], acc);
+  betaT[(int64_t)c * M + i] = acc;
 }
 
 // ---------------------------------------------------------------------------
@@ -220,6 +235,7 @@ struct R6Args {
   // the two FITC GPs (d_v: 13 features, d_w: 12)
   GpView gv, gw;
   int Mv, Mw;
+  const double *cv, *cw;  // mean coefficients (3 x M): beta^T, or alpha^T as written
 };
 
 // ---------------------------------------------------------------------------
@@ -273,7 +289,8 @@ __global__ __launch_bounds__(R6_PT) void k_r6_predict(R6Args a) {
         for (int f = 0; f < d; ++f) dot = fma(zq[g][f], v.Xs[(int64_t)i * d + f], dot);
         const double d2 = (zn[g] + v.Xn[i]) - 2.0 * dot;
         const double kv = kernel_epilogue(GPMPC_SE_ARD, d2, v.sigma2, 0.0);
-        for (int c = 0; c < 3; ++c) acc[3 * g + c] += kv * v.alphaT[(int64_t)c * M + i];
+        const double *cf = g ? a.cw : a.cv;
+        for (int c = 0; c < 3; ++c) acc[3 * g + c] += kv * cf[(int64_t)c * M + i];
       }
     }
     for (int c = 0; c < 6; ++c)
@@ -1152,7 +1169,8 @@ extern "C" int gpmpc_rollout6_create(gpmpc_ctx *ctx, gpmpc_fitc *gp_v, gpmpc_fit
       r->Xp.alloc(sizeof(double) * B * (R6_N + 1) * R6_NX) || r->gm.alloc(sizeof(double) * B * R6_N * 6) ||
       r->Xo.alloc(sizeof(double) * B * (R6_N + 1) * R6_NX) || r->ysc.alloc(sizeof(double) * B * R6_M) ||
       r->rho.alloc(sizeof(double) * B) || r->rec.alloc(sizeof(double) * B * GPMPC_REC_LEN) ||
-      r->lin.alloc(sizeof(double) * B * R6_N * R6_NX * R6_SZ) || r->pending.alloc(sizeof(int) * B)) {
+      r->lin.alloc(sizeof(double) * B * R6_N * R6_NX * R6_SZ) || r->pending.alloc(sizeof(int) * B) ||
+      r->betav.alloc(sizeof(double) * 3 * gv.n) || r->betaw.alloc(sizeof(double) * 3 * gw.n)) {
     delete r;
     gpmpc_set_error("rollout6: out of device memory");
     return -1;
@@ -1162,6 +1180,10 @@ extern "C" int gpmpc_rollout6_create(gpmpc_ctx *ctx, gpmpc_fitc *gp_v, gpmpc_fit
   hipMemcpyAsync(r->rec.p, rc.data(), sizeof(double) * rc.size(), hipMemcpyHostToDevice, ctx->stream);
   hipMemsetAsync(r->Xo.p, 0, sizeof(double) * B * (R6_N + 1) * R6_NX, ctx->stream);
   hipMemsetAsync(r->pending.p, 0, sizeof(int) * B, ctx->stream);
+  hipLaunchKernelGGL(k_fitc_beta, dim3((gv.n + 255) / 256, 3), dim3(256), 0, ctx->stream, gv.n, gv.W,
+                     gv.alphaT, r->betav.as<double>());
+  hipLaunchKernelGGL(k_fitc_beta, dim3((gw.n + 255) / 256, 3), dim3(256), 0, ctx->stream, gw.n, gw.W,
+                     gw.alphaT, r->betaw.as<double>());
   static bool attr = [] {
     return hipFuncSetAttribute((const void *)k_r6_control, hipFuncAttributeMaxDynamicSharedMemorySize,
                                (int)sizeof(R6Smem)) == hipSuccess;
@@ -1202,6 +1224,8 @@ static R6Args r6_args(gpmpc_rollout6 *r) {
   a.lin = r->lin.as<double>(); a.pending = r->pending.as<int>();
   a.gv = fitc_view(r->gpv); a.gw = fitc_view(r->gpw);
   a.Mv = a.gv.n; a.Mw = a.gw.n;
+  a.cv = r->cfg.fitc_mean_as_written ? a.gv.alphaT : r->betav.as<double>();
+  a.cw = r->cfg.fitc_mean_as_written ? a.gw.alphaT : r->betaw.as<double>();
   return a;
 }
 

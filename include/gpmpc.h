@@ -271,6 +271,8 @@ typedef struct {
   double dt;
   int max_steps;
   gpmpc_qp_settings qp;  /* osqp_rti.py:54-60 defaults */
+  int fitc_mean_as_written;  /* 0: the FITC posterior mean K*u L_uu^-T alpha; 1: the
+                                reference's K*u alpha (sparse_gp.py:280-283) */
 } gpmpc_rollout6_config;
 void gpmpc_rollout6_default_config(gpmpc_rollout6_config *c);
 /* gp_v: FITC on the 13 translational features, gp_w: on the 12 rotational

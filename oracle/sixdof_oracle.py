@@ -16,6 +16,10 @@ pins the rest as documented choices:
 * truth = plant + the aero-drag dispersion on the velocity
   (dispersion.py:349-360) and a -0.05 w rate damping (the residuals of the
   config-5 training generator), evaluated at the pre-step state;
+* GP means: the FITC posterior mean K*u L_uu^-T alpha by default; the
+  reference's as-written K*u alpha (sparse_gp.py:280-283) is the
+  ``corrected=False`` flag -- its magnitudes off the training data (|d_w| ~ 10
+  at the hover guess) make the first QP primal infeasible for most rollouts;
 * one control step = one pass of GPMPC.solve: forward simulation of the
   warm-start controls with the GP mean (gp_mpc.py:258-281, hover guess
   [0, 0, m g0] of :271-275 on the first call), linearisation and
@@ -141,11 +145,27 @@ def truth_step(x, u, dt):
     return xn
 
 
-def gp_mean(gpv, gpw, x, u):
-    """StructuredRocketGP.predict means (structured_gp.py:225-268) via the FITC oracle."""
+def fitc_mean(st, Zq, corrected=True):
+    """FITC predictive mean.  As written (sparse_gp.py:280-283) it is
+    K*u alpha; the FITC posterior mean is K*u L_uu^-T alpha (alpha = L_B^-T L_B^-1
+    A Lambda^-1 y in the whitened basis of sparse_gp.py:200-210)."""
+    from scipy.linalg import solve_triangular
     from . import gp_oracle
-    mv, _ = gp_oracle.fitc_predict(gpv, gp_oracle.features_translational(x[None], u[None]))
-    mw, _ = gp_oracle.fitc_predict(gpw, gp_oracle.features_rotational(x[None], u[None]))
+    Ksu = gp_oracle.gram("se_ard", np.atleast_2d(Zq), st["Zi"], st["sigma2"], st["ls"])
+    if corrected:
+        if "beta" not in st:
+            st["beta"] = solve_triangular(st["Luu"].T, st["alpha"], lower=False)
+        a = st["beta"]
+    else:
+        a = st["alpha"]
+    return (Ksu @ a) * st["y_std"] + st["y_mean"]
+
+
+def gp_mean(gpv, gpw, x, u, corrected=True):
+    """StructuredRocketGP.predict means (structured_gp.py:225-268) of the FITC pair."""
+    from . import gp_oracle
+    mv = fitc_mean(gpv, gp_oracle.features_translational(x[None], u[None]), corrected)
+    mw = fitc_mean(gpw, gp_oracle.features_rotational(x[None], u[None]), corrected)
     return mv[0], mw[0]
 
 
@@ -258,7 +278,7 @@ def new_rollout(x0, N=30):
                 rho=admm_ref.default_settings().rho, rec=rec, X=None)
 
 
-def rollout_step(gpv, gpw, S, dt=0.1, max_steps=300, qp_settings=None):
+def rollout_step(gpv, gpw, S, dt=0.1, max_steps=300, qp_settings=None, corrected=True):
     """One control step of the 6-DoF rollout (monte_carlo.py:455-537 termination
     rules on the first seven states; one GPMPC.solve pass as the module header)."""
     from . import admm_ref, mc_oracle
@@ -278,7 +298,7 @@ def rollout_step(gpv, gpw, S, dt=0.1, max_steps=300, qp_settings=None):
     X = np.zeros((N + 1, NX)); X[0] = x
     gm = np.zeros((N, 6))
     for k in range(N):
-        dv, dw = gp_mean(gpv, gpw, X[k], U[k])
+        dv, dw = gp_mean(gpv, gpw, X[k], U[k], corrected)
         gm[k, :3], gm[k, 3:] = dv, dw
         X[k + 1] = step(X[k], U[k], dt)
         X[k + 1, 4:7] += dv * dt
