@@ -43,6 +43,11 @@ __device__ __forceinline__ void lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)\
 #ifndef FQ_FUSED_DIAG
 #define FQ_FUSED_DIAG false  // block solve: G chain first, then the diagonal blocks 4 at a time
 #endif
+// FQ_TWIST: the two-ended factor / solve of fleet_twist.h (10-block chains instead of 20)
+#ifndef FQ_TWIST
+#define FQ_TWIST 1
+#endif
+#include "fleet_twist.h"
 
 struct FleetSmem {
   double A[FQ_NNZD + 1];
@@ -374,8 +379,12 @@ __device__ __forceinline__ int fq_factor(const QPPattern &pt, FleetSmem &s, Flee
   __syncthreads();
   if (T) T->mark(13);
   int f = 0;
+#if FQ_TWIST && !defined(FT_OLD_FACTOR)
+  f = ft_factor(s, cw);
+#else
   if ((tid >> 6) == cw) f = blk_factor_dispatch(pt, s);
-  if (tid == 0) s.flag = f;
+#endif
+  if ((tid & 63) == 0 && (tid >> 6) == cw) s.flag = f;  // the chain wave's lane 0 reports
   __syncthreads();
   return s.flag;
 }
@@ -634,7 +643,18 @@ __device__ __forceinline__ QPResult fq_solve(const QPPattern &pt, FleetSmem &s, 
     T.mark(11);
     __syncthreads();
     T.mark(3);
-#if FQ_DIAG_SPLIT
+#if FQ_TWIST
+    // x~: two-ended forward chains (wave cw), diagonal products (both waves),
+    // two-ended backward chains (wave cw), LDS-only barriers between
+    ft_solve<1>(s, s.rhs, cw);
+    T.mark(8);
+    lds_sync();
+    ft_solve<2>(s, s.rhs, cw);
+    T.mark(9);
+    lds_sync();
+    ft_solve<4>(s, s.rhs, cw);
+    T.mark(10);
+#elif FQ_DIAG_SPLIT
     // x~: forward chain (wave cw), diagonal products (both waves, eight blocks
     // a round), backward chain (wave cw), LDS-only barriers between
     blk_solve_dispatch<false, FQ_NBLK, 1>(pt, s, s.rhs, &T, cw);
