@@ -126,7 +126,7 @@ struct FleetRegs {
   int vj[2], rr[2];
   // variable j and bound row MD + j
   double x[2], dx[2], P[2], q[2], D[2];
-  double Ab[2], lb[2], ub[2], yb[2], zb[2], dyb[2], ztb[2];
+  double Ab[2], lb[2], ub[2], yb[2], zb[2], dyb[2];  // (rho z - y of the bound row: recomputed)
   // dynamics row 0 (l = u = ur).  No thread owns both a second variable and a
   // second dynamics row (t < 79: 2 variables + 1 row; t >= 109: 1 + 2), so row
   // slot 1 lives in variable slot 1's registers: ur <- P, yr <- yb, zr <- zb,
@@ -564,7 +564,6 @@ __device__ __forceinline__ void fq_rebuild_zt(FleetSmem &s, FleetRegs &R) {
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
     if (R.rok[h]) s.zt[R.rr[h]] = QP_RHO_EQ * rs * R.zr(h) - R.yr(h);
-    if (R.vok[h]) R.ztb[h] = fq_rho(R.lb[h], R.ub[h], rs) * R.zb[h] - R.yb[h];
   }
   __syncthreads();
 }
@@ -637,7 +636,7 @@ __device__ __forceinline__ QPResult fq_solve(const QPPattern &pt, FleetSmem &s, 
     for (int h = 0; h < 2; ++h)
       if (R.vok[h]) {
         double acc = fq_col_dot(s, R, h);
-        acc += R.Ab[h] * R.ztb[h];
+        acc += R.Ab[h] * (fq_rho(R.lb[h], R.ub[h], s.rho_s) * R.zb[h] - R.yb[h]);
         s.rhs[R.vj[h]] = sig * R.x[h] - R.q[h] + acc;
       }
     T.mark(11);
@@ -685,7 +684,6 @@ __device__ __forceinline__ QPResult fq_solve(const QPPattern &pt, FleetSmem &s, 
         const double d = rho * (zr - zn);
         const double yn = yo + d;
         R.dyb[h] = d; R.yb[h] = yn; R.zb[h] = zn;
-        R.ztb[h] = rho * zn - yn;
       }
       if (R.rok[h]) {
         const double ztl = fq_row_dot(s, R, h);
@@ -732,6 +730,10 @@ __device__ __forceinline__ QPResult fq_solve(const QPPattern &pt, FleetSmem &s, 
     fq_check(s, R, st, o, false, res.status);
   }
   if (res.status == -10) {
+    // the residuals of the last check iteration, recomputed from the unchanged
+    // iterates (rebuilding rho z - y touches none of them) so that o[] is not
+    // live across the iteration loop (register pressure)
+    if (can_check) fq_update_info(s, R, o, re);
     if (!fq_check(s, R, st, o, true, res.status)) res.status = -2;
   }
   double ob[1] = {0.0};

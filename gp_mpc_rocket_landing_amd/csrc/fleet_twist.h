@@ -218,16 +218,15 @@ __device__ __forceinline__ void ft_solve(S &s, double *b, int cw) {
     // either wave); rows past the last block read the last block and do not store
     const int q = (int)(threadIdx.x >> 4);
     constexpr int RB = 8, NR = (FT_NB + RB - 1) / RB;
-    int off[FT_SZ];
-#pragma unroll
-    for (int j = 0; j < FT_SZ; ++j) off[j] = ft_tri(rs, j);
-#pragma unroll
+#pragma unroll 1
     for (int t = 0; t < NR; ++t) {
       const int kk = RB * t + q, k = kk < FT_NB ? kk : FT_NB - 1;
       const double *Sk = F + k * FT_BS;
+      // packed row rs: (rs, j) at rs (rs + 1) / 2 + j for j <= rs, else j (j + 1) / 2 + rs
+      const double *pr = Sk + rs * (rs + 1) / 2, *pc = Sk + rs;
       double sv[FT_SZ];
 #pragma unroll
-      for (int j = 0; j < FT_SZ; ++j) sv[j] = Sk[off[j]];
+      for (int j = 0; j < FT_SZ; ++j) sv[j] = j <= rs ? pr[j] : pc[j * (j + 1) / 2];
       double y = b[k * FT_SZ + rs];
       if (k == FT_MID) y += b[FT_ZS + rs];
       const double v = dot_bc<FT_SZ>(y, sv);
