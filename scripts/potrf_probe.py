@@ -12,7 +12,10 @@ from gp_mpc_rocket_landing_amd import _lib  # noqa: E402
 def main():
     ctx = _lib.Context(0)
     stream = torch.cuda.ExternalStream(ctx.stream)
-    for n, batch in [(1000, 1), (1000, 14), (1000, 64), (1000, 256), (2000, 1), (2000, 8)]:
+    shapes = [(1000, 1), (1000, 14), (1000, 64), (1000, 256), (2000, 1), (2000, 8)]
+    if os.environ.get("PROBE_SHAPES"):   # e.g. "1000x1,1000x64"
+        shapes = [tuple(int(v) for v in t.split("x")) for t in os.environ["PROBE_SHAPES"].split(",")]
+    for n, batch in shapes:
         g = torch.Generator(device="cuda").manual_seed(0)
         G = torch.randn(batch, n, n, dtype=torch.float64, device="cuda", generator=g) / n ** 0.5
         base = G @ G.transpose(1, 2) + torch.eye(n, dtype=torch.float64, device="cuda")
