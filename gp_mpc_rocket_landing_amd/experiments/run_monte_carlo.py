@@ -10,6 +10,13 @@ Each rank flies its contiguous shard of landings (initial conditions of seeds
 ADMM, plant and the MonteCarloSimulator termination rules all device-resident
 -- then the 16-double records are gathered to rank 0 with one collective and
 summarised like MonteCarloSimulator's statistics (monte_carlo.py:186-272).
+
+``--six-dof`` runs BASELINE configs[4] instead: 6-DoF GP-MPC rollouts (N = 30,
+the StructuredRocketGP FITC pair at M = 2000 / N = 4000, every rank fitting it
+deterministically), default 512 rollouts sharded the same way:
+
+    python -m torch.distributed.run --nproc-per-node 8 --master-addr 127.0.0.1 \
+        -m gp_mpc_rocket_landing_amd.experiments.run_monte_carlo --six-dof
 """
 from __future__ import annotations
 
@@ -47,7 +54,13 @@ def main(argv=None):
     ap.add_argument("--train", type=int, default=1000)
     ap.add_argument("--seed0", type=int, default=42)
     ap.add_argument("--out", default="")
+    ap.add_argument("--six-dof", action="store_true", help="BASELINE configs[4]: 6-DoF rollouts")
+    ap.add_argument("--inducing", type=int, default=2000, help="--six-dof: FITC inducing points")
     args = ap.parse_args(argv)
+    if args.six_dof and args.landings == 1024:
+        args.landings = 512
+    if args.six_dof and args.train == 1000:
+        args.train = 4000
 
     import torch
     import torch.distributed as dist
@@ -63,12 +76,19 @@ def main(argv=None):
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     first, count = shard_range(args.landings, rank, world)
     ctx = _lib.Context(local)
-    gp = fit_gp(ctx, n_train=args.train)          # every rank fits the same GP deterministically
-    fl = Fleet(ctx, gp, max(count, 1), max_steps=args.max_steps)
+    if args.six_dof:
+        from ..rollouts6 import Rollouts6, fit_structured_fitc, initial_conditions_6dof
+        gps = fit_structured_fitc(ctx, n_train=args.train, n_inducing=args.inducing)  # same on every rank
+        fl = Rollouts6(ctx, *gps, max(count, 1), max_steps=args.max_steps)
+        x0 = initial_conditions_6dof(count, args.seed0, first) if count else None
+    else:
+        gp = fit_gp(ctx, n_train=args.train)          # every rank fits the same GP deterministically
+        fl = Fleet(ctx, gp, max(count, 1), max_steps=args.max_steps)
+        x0 = initial_conditions(count, args.seed0, first) if count else None
     t0 = time.perf_counter()
     rec = np.zeros((0, _lib.REC_LEN))
     if count:
-        fl.reset(initial_conditions(count, args.seed0, first))
+        fl.reset(x0)
         done = 0
         while done < args.max_steps + 1:
             fl.step(args.chunk)
@@ -88,6 +108,8 @@ def main(argv=None):
     if rank == 0:
         s = summarise(allrec)
         s.update(n_gpus=world, wall_s=round(el, 3), control_steps_per_s=round(s["control_steps"] / el, 1))
+        if args.six_dof:
+            s.update(config="configs[4] 6-DoF rollouts", rollouts_per_s=round(s["n_landings"] / el, 1))
         print(json.dumps(s), flush=True)
         if args.out:
             np.savez(args.out, records=allrec)

@@ -94,3 +94,27 @@ def test_rollouts6_match_oracle_config5_gp(gpu_ctx):
     1e-6 spec."""
     seen, S = _run(gpu_ctx, 4000, 2000, 4, 4)
     assert seen >= 8, seen
+
+
+def test_rollouts6_shards_reproduce_the_whole_batch(gpu_ctx):
+    """Sharding invariance for configs[4]: 64 rollouts flown as one
+    batch and as two shards [0, 32), [32, 64) (initial conditions by global
+    index, as each rank of run_monte_carlo --six-dof builds its shard) give
+    bit-identical records and states."""
+    from gp_mpc_rocket_landing_amd.rollouts6 import Rollouts6, fit_structured_fitc, initial_conditions_6dof
+    from gp_mpc_rocket_landing_amd.sharding import shard_range
+    gv, gw = fit_structured_fitc(gpu_ctx, n_train=300, n_inducing=50)
+
+    def fly(first, count, steps=30):
+        r = Rollouts6(gpu_ctx, gv, gw, count)
+        try:
+            r.reset(initial_conditions_6dof(count, first=first))
+            r.step(steps)
+            return r.read()
+        finally:
+            r.close()
+
+    whole_r, whole_x = fly(0, 64)
+    parts = [fly(*shard_range(64, rk, 2)) for rk in range(2)]
+    np.testing.assert_array_equal(np.concatenate([p[0] for p in parts]), whole_r)
+    np.testing.assert_array_equal(np.concatenate([p[1] for p in parts]), whole_x)
