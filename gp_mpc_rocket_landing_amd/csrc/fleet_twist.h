@@ -157,59 +157,67 @@ __device__ __forceinline__ void ft_solve(S &s, double *b, int cw) {
   if constexpr (PH == 1 || PH == 4) {
     if ((int)(threadIdx.x >> 6) != cw || lane >= 32 || rr >= FT_SZ) return;
     const bool top = lane < 16;
+    // Block offsets are element indices advanced step by step behind an empty asm:
+    // the two rows walk in opposite directions, so a step's address is not an
+    // immediate offset from one base, and left alone the compiler hoists all
+    // twenty of them out of the ADMM loop as live registers (spilled elsewhere).
     if constexpr (PH == 1) {
       // top: y over blocks 0..10;  bottom: z over blocks 20..11, then z'_10
-      double *pb = b + (top ? 0 : (FT_NB - 1) * FT_SZ) + rs;
+      int ib = (top ? 0 : (FT_NB - 1) * FT_SZ) + rs;
       const int db = top ? FT_SZ : -FT_SZ;
-      const double *pg = F + (top ? 0 : (FT_NB - 1) * FT_BS) + FT_GO + rs;
+      int ig = (top ? 0 : (FT_NB - 1) * FT_BS) + FT_GO + rs;
       const int dg = top ? FT_BS : -FT_BS;
-      double y = pb[0];
+      double y = b[ib];
       double gA[FT_SZ], gB[FT_SZ], cA, cB;
 #pragma unroll
-      for (int j = 0; j < FT_SZ; ++j) gA[j] = pg[j * FT_SZ];
-      cA = pb[db];
+      for (int j = 0; j < FT_SZ; ++j) gA[j] = F[ig + j * FT_SZ];
+      cA = b[ib + db];
 #pragma unroll
       for (int t = 0; t < FT_MID; ++t) {
         double *gc = (t & 1) ? gB : gA, *gn = (t & 1) ? gA : gB;
         double &cc = (t & 1) ? cB : cA, &cn = (t & 1) ? cA : cB;
         if (t + 1 < FT_MID) {
+          const int ign = ig + dg;
 #pragma unroll
-          for (int j = 0; j < FT_SZ; ++j) gn[j] = pg[dg + j * FT_SZ];
-          cn = pb[2 * db];
+          for (int j = 0; j < FT_SZ; ++j) gn[j] = F[ign + j * FT_SZ];
+          cn = b[ib + 2 * db];
         }
         const double init = (t == FT_MID - 1 && !top) ? 0.0 : cc;  // z'_10 = -K_11^T z_11
         const double yn = dot_bc_init<FT_SZ>(init, y, gc);
-        pb[0] = y;
+        b[ib] = y;
         y = yn;
-        pb += db;
-        pg += dg;
+        ib += db;
+        ig += dg;
+        asm volatile("" : "+v"(ib), "+v"(ig));
       }
-      if (top) pb[0] = y;            // y_10 over b_10
+      if (top) b[ib] = y;            // y_10 over b_10
       else b[FT_ZS + rs] = y;        // z'_10
     } else {
       // top: x_9 .. x_0 from x_10;  bottom: x_11 .. x_20
       double x = b[FT_MID * FT_SZ + rs];
-      double *pu = b + (top ? (FT_MID - 1) : (FT_MID + 1)) * FT_SZ + rs;
+      int iu = (top ? (FT_MID - 1) : (FT_MID + 1)) * FT_SZ + rs;
       const int du = top ? -FT_SZ : FT_SZ;
-      const double *pg = F + (top ? (FT_MID - 1) : (FT_MID + 1)) * FT_BS + FT_GO + rs * FT_SZ;
+      int ig = (top ? (FT_MID - 1) : (FT_MID + 1)) * FT_BS + FT_GO + rs * FT_SZ;
       const int dg = top ? -FT_BS : FT_BS;
       double gA[FT_SZ], gB[FT_SZ], cA, cB;
 #pragma unroll
-      for (int j = 0; j < FT_SZ; ++j) gA[j] = pg[j];
-      cA = pu[0];
+      for (int j = 0; j < FT_SZ; ++j) gA[j] = F[ig + j];
+      cA = b[iu];
 #pragma unroll
       for (int t = 0; t < FT_MID; ++t) {
         double *gc = (t & 1) ? gB : gA, *gn = (t & 1) ? gA : gB;
         double &cc = (t & 1) ? cB : cA, &cn = (t & 1) ? cA : cB;
         if (t + 1 < FT_MID) {
+          const int ign = ig + dg;
 #pragma unroll
-          for (int j = 0; j < FT_SZ; ++j) gn[j] = pg[dg + j];
-          cn = pu[du];
+          for (int j = 0; j < FT_SZ; ++j) gn[j] = F[ign + j];
+          cn = b[iu + du];
         }
         x = dot_bc_init<FT_SZ>(cc, x, gc);
-        pu[0] = x;
-        pu += du;
-        pg += dg;
+        b[iu] = x;
+        iu += du;
+        ig += dg;
+        asm volatile("" : "+v"(iu), "+v"(ig));
       }
     }
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
