@@ -12,7 +12,7 @@
 //      the workgroup and reduced; the 30 points are sequential.  The mean is the
 //      FITC posterior mean K*u L_uu^-T alpha (SURVEY D1 fixed; the reference's
 //      K*u alpha behind fitc_mean_as_written).
-//   2. k_r6_control  (1024 threads / rollout): the QP subproblem of
+//   2. k_r6_control  (512 threads / rollout): the QP subproblem of
 //      gp_mpc.py:394-460 in deviation variables z = [dx_0, du_0, .., dx_30]
 //      (n = 524): x0 + dynamics equalities with A_d = I + A_c dt, B_d = B_c dt
 //      (rocket_6dof.py:427-459, analytic Jacobians) and c_k = GP mean dt; the
@@ -22,14 +22,18 @@
 //      matrix, which is block tridiagonal in the 31 stage blocks [x_k, u_k]:
 //      S_0 = D_0, S_k+1 = D_k+1 - C_k S_k^-1 C_k^T with S_k^-1 formed by
 //      Gauss-Jordan in LDS; each iteration's solve is a forward chain
-//      (y_k+1 -= G_k y_k, G_k = C_k S_k^-1, 14 lanes), the 31 diagonal products
-//      u_k = S_k^-1 y_k in parallel, and a backward chain (x_k = u_k -
-//      G_k^T x_k+1, 17 lanes).  Then the plan X + dX, U + dU (kept unshifted
+//      (y_k+1 -= G_k y_k, G_k = C_k S_k^-1, one DPP row), the 31 diagonal
+//      products u_k = S_k^-1 y_k in parallel, and a backward chain (x_k = u_k -
+//      G_k^T x_k+1, two DPP rows); the chains keep their vector in registers
+//      (r6_solve).  Then the plan X + dX, U + dU (kept unshifted
 //      as the next warm start, gp_mpc.py:358-359), the truth plant step (RK4
 //      + the drag dispersion of dispersion.py:349-360 and the -0.05 w rate
 //      damping the config-5 GP is trained on) and the records.
-// Ownership: thread j < 524 owns variable j (+ its bound row, and general row
-// j < 146); thread 524 + r owns equality row r < 434.  The 14 x 17 dynamics
+// Ownership: item j = tid + 512 h (h = 0, 1) of thread tid: variable j < 524
+// (+ its bound row; general row tid < 146 rides on slot 0), else equality row
+// j - 524 < 434.  At 1024 threads (one item each) a lane had 128 VGPRs and the
+// ADMM loop reloaded 222 spilled registers from scratch; two items per lane at
+// 256 VGPRs is the same register file without them.  The 14 x 17 dynamics
 // block of each equality row lives in its owner's registers, a column copy in
 // the variable owner's; only the factor and the cross-thread vectors are LDS.
 #include "internal.h"
@@ -47,9 +51,10 @@
 #define R6_MG (4 * (R6_N - 1))                // 116 glideslope rows
 #define R6_MGEN (R6_MT + R6_MG)               // 146 general rows
 #define R6_M (R6_MD + R6_NV + R6_MGEN)        // 1104 rows
-#define R6_T 1024
+#define R6_T 512                              // two items (variables / rows) per thread
 #define R6_TRI 153                            // packed lower 17 x 17
 #define R6_PT 256                             // predict threads
+#define R6_FOR_H _Pragma("unroll") for (int h = 0; h < 2; ++h)
 
 // Rocket6DoFConfig (rocket_6dof.py:36-84), ConstraintParams (constraints.py:35-50),
 // CostWeights (cost_functions.py:39-98), gp_mpc.py trust regions (:432-435)
@@ -339,6 +344,7 @@ struct R6Smem {
   double Gt[R6_NX * R6_SZ];           // G_k before it replaces C_k
   double Sch[R6_NX * R6_NX];          // G_k C_k^T
   double red[16][12];
+  double zero[R6_SZ];                 // the forward chain's operand row for its pass-through lanes
   double c, rho_s;
   int flag;
 };
@@ -495,16 +501,19 @@ __device__ __forceinline__ double r6_gen_dot(const R6Var &V, const double *v) {
 
 // assemble the block tridiagonal M = P + sigma I + A' R A and factor it:
 // returns 0 or a failing block + 1
-__device__ __forceinline__ int r6_factor(R6Smem &s, R6Var &V, R6Row &R, double sigma) {
+template <class MK>
+__device__ __forceinline__ int r6_factor(R6Smem &s, R6Var (&V)[2], R6Row (&R)[2], double sigma, MK &mark) {
   const int tid = threadIdx.x;
   const double rs = s.rho_s, re = QP_RHO_EQ * rs;
   // stage: dynamics rows' block values, per-variable P + sigma and bound terms
-  if (R.ok && R.r >= R6_NX)
+  R6_FOR_H {
+    if (R[h].ok && R[h].r >= R6_NX)
 #pragma unroll
-    for (int e = 0; e < R6_SZ; ++e) s.G[(R.k * R6_NX + R.i) * R6_SZ + e] = R.A[e];
-  if (V.ok) {
-    s.dsc[V.j] = V.P + sigma;
-    s.xs[V.j] = r6_rho(V.lb, V.ub, rs) * V.Ab * V.Ab;
+      for (int e = 0; e < R6_SZ; ++e) s.G[(R[h].k * R6_NX + R[h].i) * R6_SZ + e] = R[h].A[e];
+    if (V[h].ok) {
+      s.dsc[V[h].j] = V[h].P + sigma;
+      s.xs[V[h].j] = r6_rho(V[h].lb, V[h].ub, rs) * V[h].Ab * V[h].Ab;
+    }
   }
   __syncthreads();
   // D_k, lower packed, row order of the terms as the banded oracle
@@ -547,6 +556,7 @@ __device__ __forceinline__ int r6_factor(R6Smem &s, R6Var &V, R6Row &R, double s
     s.Sinv[e] = v;
   }
   __syncthreads();
+  mark(2);  // (stamps: the assembly)
   // the sweep
   const int ti = tid / R6_SZ, tj = tid - ti * R6_SZ;
   const bool tok = tid < R6_SZ * R6_SZ;
@@ -581,6 +591,7 @@ __device__ __forceinline__ int r6_factor(R6Smem &s, R6Var &V, R6Row &R, double s
       __syncthreads();
     }
     if (tok && ti >= tj) s.Sinv[k * R6_TRI + r6_tri(ti, tj)] = (ti < nb && tj < nb) ? s.T[tid] : 0.0;
+    mark(10);
     if (k == R6_N) break;
     // G_k = C_k S_k^-1, C_k[i][:] = rho_eq dpl(k, i) (staged row (k, i))
     const double *g = s.G + k * R6_NX * R6_SZ;
@@ -600,37 +611,73 @@ __device__ __forceinline__ int r6_factor(R6Smem &s, R6Var &V, R6Row &R, double s
       s.Sch[tid] = acc;
     }
     __syncthreads();
-    if (tid < R6_NX * R6_SZ) s.G[k * R6_NX * R6_SZ + tid] = s.Gt[tid];
+    if (tid < R6_NX * R6_SZ) s.G[k * R6_NX * R6_SZ + tid] = -s.Gt[tid];  // stored negated: the chains accumulate
     __syncthreads();
+    mark(11);
   }
   __syncthreads();
   return 0;
 }
 
-// x~ = M^-1 rhs: forward chain (wave 0), diagonal products, backward chain (wave 0)
-__device__ __forceinline__ void r6_solve(R6Smem &s) {
+// x~ = M^-1 rhs: forward chain (wave 0), diagonal products, backward chain
+// (wave 0).  The chains carry their vector in registers and broadcast it with
+// DPP row_newbcast inside the FMA (qp_block.h fmac_bc), as the 3-DoF fleet does;
+// blocks are 17 wide and a DPP row is 16:
+//   forward  y_k+1 = b_k+1 + (-G_k) y_k on row 0 (lane i: row i < 14; lanes 14,
+//            15 carry b_k+1[14, 15] through zero operands).  y_k[16] = b_k[16]
+//            (no G row reaches it), so its term goes into the init off the chain.
+//   backward x_k = u_k + (-G_k)^T x_k+1 over the 14 coupled entries: lanes 0-15
+//            compute entries 0-15, lanes 16-29 replicate entries 0-13 (so row 1
+//            broadcasts the same x_k+1) and lane 30 computes entry 16.
+template <class MK>
+__device__ __forceinline__ void r6_solve(R6Smem &s, MK &mark) {
   const int tid = threadIdx.x;
   if (tid < 64) {
-    const int i = tid;
-    for (int k = 0; k < R6_N; ++k) {
-      double acc0 = 0.0, acc1 = 0.0;
-      if (i < R6_NX) {
-        const double *g = s.G + (k * R6_NX + i) * R6_SZ;
-        const double *y = s.rhs + k * R6_SZ;
+    // every term's operand for the NEXT step loads right after the term's FMA,
+    // into the register it frees: one buffer, the loads a step ahead
+    const int lane = tid, rr = lane & 15;
+    const double *F = s.G;
+    const bool pass = rr >= R6_NX;  // lanes 14, 15 carry b[14, 15]: zero operands
+    int go = pass ? (int)(s.zero - s.G) : rr * R6_SZ;
+    const int gs = pass ? 0 : R6_NX * R6_SZ;
+    double g[R6_SZ];
 #pragma unroll
-        for (int e = 0; e < 16; e += 2) {
-          acc0 = fma(g[e], y[e], acc0);
-          acc1 = fma(g[e + 1], y[e + 1], acc1);
-        }
-        acc0 = fma(g[16], y[16], acc0);
-        s.rhs[(k + 1) * R6_SZ + i] -= acc0 + acc1;
-      }
-      wave_sync();
+    for (int e = 0; e < R6_SZ; ++e) g[e] = F[go + e];
+    double y = s.rhs[rr];
+    double b16 = s.rhs[R6_SZ - 1], bn = s.rhs[R6_SZ + rr];
+#pragma unroll 1
+    for (int k = 0; k < R6_N; ++k) {
+      const int gn = go + gs;
+      const double init = fma(g[R6_SZ - 1], b16, bn);
+      b16 = s.rhs[(k + 1) * R6_SZ + R6_SZ - 1];
+      bn = s.rhs[min(k + 2, R6_N) * R6_SZ + rr];
+      g[R6_SZ - 1] = F[gn + R6_SZ - 1];
+      double a0 = init, a1 = 0.0;
+      fmac_bc<0, true>(a0, y, g[0]);   g[0] = F[gn + 0];
+      fmac_bc<1, false>(a1, y, g[1]);  g[1] = F[gn + 1];
+      fmac_bc<2, false>(a0, y, g[2]);  g[2] = F[gn + 2];
+      fmac_bc<3, false>(a1, y, g[3]);  g[3] = F[gn + 3];
+      fmac_bc<4, false>(a0, y, g[4]);  g[4] = F[gn + 4];
+      fmac_bc<5, false>(a1, y, g[5]);  g[5] = F[gn + 5];
+      fmac_bc<6, false>(a0, y, g[6]);  g[6] = F[gn + 6];
+      fmac_bc<7, false>(a1, y, g[7]);  g[7] = F[gn + 7];
+      fmac_bc<8, false>(a0, y, g[8]);  g[8] = F[gn + 8];
+      fmac_bc<9, false>(a1, y, g[9]);  g[9] = F[gn + 9];
+      fmac_bc<10, false>(a0, y, g[10]); g[10] = F[gn + 10];
+      fmac_bc<11, false>(a1, y, g[11]); g[11] = F[gn + 11];
+      fmac_bc<12, false>(a0, y, g[12]); g[12] = F[gn + 12];
+      fmac_bc<13, false>(a1, y, g[13]); g[13] = F[gn + 13];
+      fmac_bc<14, false>(a0, y, g[14]); g[14] = F[gn + 14];
+      fmac_bc<15, false>(a1, y, g[15]); g[15] = F[gn + 15];
+      y = a0 + a1;
+      if (lane < 16) s.rhs[(k + 1) * R6_SZ + rr] = y;
+      go = gn;
     }
   }
   __syncthreads();
-  if (tid < R6_NBLK * R6_SZ) {
-    const int k = tid / R6_SZ, a = tid - k * R6_SZ;
+  mark(4);
+  for (int e = tid; e < R6_NBLK * R6_SZ; e += R6_T) {
+    const int k = e / R6_SZ, a = e - k * R6_SZ;
     const int nb = (k == R6_N) ? R6_NX : R6_SZ;
     if (a < nb) {
       const double *S = s.Sinv + k * R6_TRI;
@@ -641,35 +688,60 @@ __device__ __forceinline__ void r6_solve(R6Smem &s) {
         acc1 = fma(S[r6_tri(a, bb + 1)], y[bb + 1], acc1);
       }
       if (nb & 1) acc0 = fma(S[r6_tri(a, nb - 1)], y[nb - 1], acc0);
-      s.xs[tid] = acc0 + acc1;
+      s.xs[e] = acc0 + acc1;
     }
   }
   __syncthreads();
+  mark(5);
   if (tid < 64) {
-    const int a = tid;
-    for (int k = R6_N - 1; k >= 0; --k) {
-      if (a < R6_SZ) {
-        const double *g = s.G + k * R6_NX * R6_SZ;
-        const double *xn = s.xs + (k + 1) * R6_SZ;
-        double acc0 = 0.0, acc1 = 0.0;
+    const int lane = tid;
+    // entry a of lane (0-15: a = lane, 16-29: a = lane - 16, 30: 16); lanes >= 31
+    // compute entry 16 too and drop it
+    const int a = lane < 16 ? lane : (lane < 30 ? lane - 16 : R6_SZ - 1);
+    const bool st = lane < 16 || lane == 30;
+    const double *F = s.G;
+    int go = (R6_N - 1) * R6_NX * R6_SZ + a;
+    double g[R6_NX];
 #pragma unroll
-        for (int i = 0; i < R6_NX; i += 2) {
-          acc0 = fma(g[i * R6_SZ + a], xn[i], acc0);
-          acc1 = fma(g[(i + 1) * R6_SZ + a], xn[i + 1], acc1);
-        }
-        s.xs[k * R6_SZ + a] -= acc0 + acc1;
-      }
-      wave_sync();
+    for (int i = 0; i < R6_NX; ++i) g[i] = F[go + i * R6_SZ];
+    double x = a < R6_NX ? s.xs[R6_N * R6_SZ + a] : 0.0;
+    double u = s.xs[(R6_N - 1) * R6_SZ + a];
+#pragma unroll 1
+    for (int k = R6_N - 1; k >= 0; --k) {
+      const int gn = max(go - R6_NX * R6_SZ, 0);
+      double a0 = u, a1 = 0.0;
+      u = s.xs[max(k - 1, 0) * R6_SZ + a];
+      fmac_bc<0, true>(a0, x, g[0]);   g[0] = F[gn + 0 * R6_SZ];
+      fmac_bc<1, false>(a1, x, g[1]);  g[1] = F[gn + 1 * R6_SZ];
+      fmac_bc<2, false>(a0, x, g[2]);  g[2] = F[gn + 2 * R6_SZ];
+      fmac_bc<3, false>(a1, x, g[3]);  g[3] = F[gn + 3 * R6_SZ];
+      fmac_bc<4, false>(a0, x, g[4]);  g[4] = F[gn + 4 * R6_SZ];
+      fmac_bc<5, false>(a1, x, g[5]);  g[5] = F[gn + 5 * R6_SZ];
+      fmac_bc<6, false>(a0, x, g[6]);  g[6] = F[gn + 6 * R6_SZ];
+      fmac_bc<7, false>(a1, x, g[7]);  g[7] = F[gn + 7 * R6_SZ];
+      fmac_bc<8, false>(a0, x, g[8]);  g[8] = F[gn + 8 * R6_SZ];
+      fmac_bc<9, false>(a1, x, g[9]);  g[9] = F[gn + 9 * R6_SZ];
+      fmac_bc<10, false>(a0, x, g[10]); g[10] = F[gn + 10 * R6_SZ];
+      fmac_bc<11, false>(a1, x, g[11]); g[11] = F[gn + 11 * R6_SZ];
+      fmac_bc<12, false>(a0, x, g[12]); g[12] = F[gn + 12 * R6_SZ];
+      fmac_bc<13, false>(a1, x, g[13]); g[13] = F[gn + 13 * R6_SZ];
+      x = a0 + a1;
+      if (st) s.xs[k * R6_SZ + a] = x;
+      go = gn;
     }
   }
   __syncthreads();
+  mark(6);
 }
 
 // residual norms (auxil.c update_info) + the rho-estimate quantities (as fq_update_info)
-__device__ __forceinline__ void r6_update_info(R6Smem &s, R6Var &V, R6Row &R, double (&o)[8], double (&re_)[4]) {
-  if (V.ok) s.rhs[V.j] = V.x;
-  if (R.ok) s.w[R.r] = R.yr;
-  if (V.gok) s.w[R6_MD + V.j] = V.gy;
+__device__ __forceinline__ void r6_update_info(R6Smem &s, R6Var (&V)[2], R6Row (&R)[2], double (&o)[8],
+                                               double (&re_)[4]) {
+  R6_FOR_H {
+    if (V[h].ok) s.rhs[V[h].j] = V[h].x;
+    if (R[h].ok) s.w[R[h].r] = R[h].yr;
+    if (V[h].gok) s.w[R6_MD + V[h].j] = V[h].gy;
+  }
   __syncthreads();
   double v[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
   auto row = [&](double ax, double z, double e) {
@@ -679,19 +751,22 @@ __device__ __forceinline__ void r6_update_info(R6Smem &s, R6Var &V, R6Row &R, do
     v[8] = fmax(v[8], fabs(ax - z));
     v[9] = fmax(v[9], fmax(fabs(z), fabs(ax)));
   };
-  if (R.ok) row(r6_row_dot(R, s.rhs), R.zr, s.E[R.r]);
-  if (V.ok) {
-    row(0.0 + V.Ab * V.x, V.zb, s.E[R6_MD + V.j]);
-    const double aty = r6_col_dot(s, V, s.w, V.yb, s.w + R6_MD);
-    const double px = V.P * V.x, d = V.D, q = V.q;
-    v[3] = fmax(v[3], fabs((q + px + aty) / d));
-    v[4] = fmax(v[4], fabs(q / d));
-    v[5] = fmax(v[5], fabs(aty / d));
-    v[6] = fmax(v[6], fabs(px / d));
-    v[10] = fmax(v[10], fabs(q + px + aty));
-    v[11] = fmax(v[11], fmax(fmax(fabs(q), fabs(aty)), fabs(px)));
+  R6_FOR_H {
+    R6Var &W = V[h];
+    if (R[h].ok) row(r6_row_dot(R[h], s.rhs), R[h].zr, s.E[R[h].r]);
+    if (W.ok) {
+      row(0.0 + W.Ab * W.x, W.zb, s.E[R6_MD + W.j]);
+      const double aty = r6_col_dot(s, W, s.w, W.yb, s.w + R6_MD);
+      const double px = W.P * W.x, d = W.D, q = W.q;
+      v[3] = fmax(v[3], fabs((q + px + aty) / d));
+      v[4] = fmax(v[4], fabs(q / d));
+      v[5] = fmax(v[5], fabs(aty / d));
+      v[6] = fmax(v[6], fabs(px / d));
+      v[10] = fmax(v[10], fabs(q + px + aty));
+      v[11] = fmax(v[11], fmax(fmax(fabs(q), fabs(aty)), fabs(px)));
+    }
+    if (W.gok) row(r6_gen_dot(W, s.rhs), W.gz, s.E[R6_MD + R6_NV + W.j]);
   }
-  if (V.gok) row(r6_gen_dot(V, s.rhs), V.gz, s.E[R6_MD + R6_NV + V.j]);
   r6_max<12>(v, s.red);
 #pragma unroll
   for (int k = 0; k < 8; ++k) o[k] = v[k];
@@ -707,42 +782,60 @@ __device__ __forceinline__ double r6_proj(double d, double l, double u) {
   return d;
 }
 
-__device__ __forceinline__ bool r6_primal_infeasible(R6Smem &s, R6Var &V, R6Row &R, double eps) {
+__device__ __forceinline__ bool r6_primal_infeasible(R6Smem &s, R6Var (&V)[2], R6Row (&R)[2], double eps) {
   double v[1] = {0.0};
-  if (R.ok) { R.dyr = r6_proj(R.dyr, R.ur, R.ur); v[0] = fmax(v[0], fabs(s.E[R.r] * R.dyr)); }
-  if (V.ok) { V.dyb = r6_proj(V.dyb, V.lb, V.ub); v[0] = fmax(v[0], fabs(s.E[R6_MD + V.j] * V.dyb)); }
-  if (V.gok) { V.gdy = r6_proj(V.gdy, V.gl, V.gu); v[0] = fmax(v[0], fabs(s.E[R6_MD + R6_NV + V.j] * V.gdy)); }
+  R6_FOR_H {
+    R6Var &W = V[h];
+    R6Row &Q = R[h];
+    if (Q.ok) { Q.dyr = r6_proj(Q.dyr, Q.ur, Q.ur); v[0] = fmax(v[0], fabs(s.E[Q.r] * Q.dyr)); }
+    if (W.ok) { W.dyb = r6_proj(W.dyb, W.lb, W.ub); v[0] = fmax(v[0], fabs(s.E[R6_MD + W.j] * W.dyb)); }
+    if (W.gok) { W.gdy = r6_proj(W.gdy, W.gl, W.gu); v[0] = fmax(v[0], fabs(s.E[R6_MD + R6_NV + W.j] * W.gdy)); }
+  }
   r6_max<1>(v, s.red);
   const double nrm = v[0];
   if (!(nrm > QP_DIV_TOL)) return false;
   double sm[1] = {0.0};
-  if (R.ok) sm[0] += R.ur * fmax(R.dyr, 0.0) + R.ur * fmin(R.dyr, 0.0);
-  if (V.ok) sm[0] += V.ub * fmax(V.dyb, 0.0) + V.lb * fmin(V.dyb, 0.0);
-  if (V.gok) sm[0] += V.gu * fmax(V.gdy, 0.0) + V.gl * fmin(V.gdy, 0.0);
+  R6_FOR_H {
+    R6Var &W = V[h];
+    R6Row &Q = R[h];
+    if (Q.ok) sm[0] += Q.ur * fmax(Q.dyr, 0.0) + Q.ur * fmin(Q.dyr, 0.0);
+    if (W.ok) sm[0] += W.ub * fmax(W.dyb, 0.0) + W.lb * fmin(W.dyb, 0.0);
+    if (W.gok) sm[0] += W.gu * fmax(W.gdy, 0.0) + W.gl * fmin(W.gdy, 0.0);
+  }
   r6_sum<1>(sm, s.red);
   if (!(sm[0] < -eps * nrm)) return false;
-  if (R.ok) s.w[R.r] = R.dyr;
-  if (V.gok) s.w[R6_MD + V.j] = V.gdy;
+  R6_FOR_H {
+    if (R[h].ok) s.w[R[h].r] = R[h].dyr;
+    if (V[h].gok) s.w[R6_MD + V[h].j] = V[h].gdy;
+  }
   __syncthreads();
   double mx[1] = {0.0};
-  if (V.ok) mx[0] = fabs(r6_col_dot(s, V, s.w, V.dyb, s.w + R6_MD) / V.D);
+  R6_FOR_H {
+    if (V[h].ok) mx[0] = fmax(mx[0], fabs(r6_col_dot(s, V[h], s.w, V[h].dyb, s.w + R6_MD) / V[h].D));
+  }
   r6_max<1>(mx, s.red);
   return mx[0] < eps * nrm;
 }
 
-__device__ __forceinline__ bool r6_dual_infeasible(R6Smem &s, R6Var &V, R6Row &R, double eps) {
+__device__ __forceinline__ bool r6_dual_infeasible(R6Smem &s, R6Var (&V)[2], R6Row (&R)[2], double eps) {
   double v[1] = {0.0};
-  if (V.ok) v[0] = fabs(V.D * V.dx);
+  R6_FOR_H {
+    if (V[h].ok) v[0] = fmax(v[0], fabs(V[h].D * V[h].dx));
+  }
   r6_max<1>(v, s.red);
   const double nrm = v[0];
   if (!(nrm > QP_DIV_TOL)) return false;
   double a[1] = {0.0}, pm[1] = {0.0};
-  if (V.ok) { a[0] = V.q * V.dx; pm[0] = fabs(V.P * V.dx / V.D); }
+  R6_FOR_H {
+    if (V[h].ok) { a[0] += V[h].q * V[h].dx; pm[0] = fmax(pm[0], fabs(V[h].P * V[h].dx / V[h].D)); }
+  }
   r6_sum<1>(a, s.red);
   r6_max<1>(pm, s.red);
   if (!(a[0] < s.c * eps * nrm)) return false;
   if (!(pm[0] < s.c * eps * nrm)) return false;
-  if (V.ok) s.rhs[V.j] = V.dx;
+  R6_FOR_H {
+    if (V[h].ok) s.rhs[V[h].j] = V[h].dx;
+  }
   __syncthreads();
   double bad[1] = {0.0};
   auto test = [&](double vv, double l, double u) {
@@ -750,15 +843,18 @@ __device__ __forceinline__ bool r6_dual_infeasible(R6Smem &s, R6Var &V, R6Row &R
         (l > -QP_OSQP_INFTY * QP_MIN_SCALING && vv < -eps * nrm))
       bad[0] = 1.0;
   };
-  if (R.ok) test(r6_row_dot(R, s.rhs) / s.E[R.r], R.ur, R.ur);
-  if (V.ok) test((0.0 + V.Ab * V.dx) / s.E[R6_MD + V.j], V.lb, V.ub);
-  if (V.gok) test(r6_gen_dot(V, s.rhs) / s.E[R6_MD + R6_NV + V.j], V.gl, V.gu);
+  R6_FOR_H {
+    R6Var &W = V[h];
+    if (R[h].ok) test(r6_row_dot(R[h], s.rhs) / s.E[R[h].r], R[h].ur, R[h].ur);
+    if (W.ok) test((0.0 + W.Ab * W.dx) / s.E[R6_MD + W.j], W.lb, W.ub);
+    if (W.gok) test(r6_gen_dot(W, s.rhs) / s.E[R6_MD + R6_NV + W.j], W.gl, W.gu);
+  }
   r6_max<1>(bad, s.red);
   return bad[0] == 0.0;
 }
 
-__device__ __forceinline__ bool r6_check(R6Smem &s, R6Var &V, R6Row &R, const QPSettingsDev &st, const double (&o)[8],
-                         bool approx, int &status) {
+__device__ __forceinline__ bool r6_check(R6Smem &s, R6Var (&V)[2], R6Row (&R)[2], const QPSettingsDev &st,
+                                         const double (&o)[8], bool approx, int &status) {
   const double pri = o[0], dua = o[3] / s.c;
   double ea = st.eps_abs, er = st.eps_rel, epi = st.eps_prim_inf, edi = st.eps_dual_inf;
   if (pri > QP_OSQP_INFTY || dua > QP_OSQP_INFTY) { status = -7; return true; }
@@ -774,16 +870,31 @@ __device__ __forceinline__ bool r6_check(R6Smem &s, R6Var &V, R6Row &R, const QP
   return false;
 }
 
-__device__ __forceinline__ void r6_rebuild_w(R6Smem &s, R6Var &V, R6Row &R) {
+__device__ __forceinline__ void r6_rebuild_w(R6Smem &s, R6Var (&V)[2], R6Row (&R)[2]) {
   const double rs = s.rho_s;
-  if (R.ok) s.w[R.r] = QP_RHO_EQ * rs * R.zr - R.yr;
-  if (V.ok) V.ztb = r6_rho(V.lb, V.ub, rs) * V.zb - V.yb;
-  if (V.gok) s.w[R6_MD + V.j] = r6_rho(V.gl, V.gu, rs) * V.gz - V.gy;
+  R6_FOR_H {
+    if (R[h].ok) s.w[R[h].r] = QP_RHO_EQ * rs * R[h].zr - R[h].yr;
+    if (V[h].ok) V[h].ztb = r6_rho(V[h].lb, V[h].ub, rs) * V[h].zb - V[h].yb;
+    if (V[h].gok) s.w[R6_MD + V[h].j] = r6_rho(V[h].gl, V[h].gu, rs) * V[h].gz - V[h].gy;
+  }
   __syncthreads();
 }
 
+// diagnostic phase cycles of workgroup 0 (GPMPC_R6_STAMPS=1 launches the <true> instance)
+__device__ unsigned long long g_r6_stamps[12];
+
+template <bool ST>
 __global__ __launch_bounds__(R6_T) void k_r6_control(R6Args a) {
   const int b = blockIdx.x, tid = threadIdx.x;
+  unsigned long long tl = 0;
+  auto mark = [&](int k) {
+    if (ST && b == 0 && tid == 0) {
+      const unsigned long long t = __builtin_amdgcn_s_memtime();
+      if (k >= 0) g_r6_stamps[k] += t - tl;
+      tl = t;
+    }
+  };
+  mark(-1);
   double *rec = a.rec + (int64_t)b * GPMPC_REC_LEN;
   if (rec[0] != 0.0) return;
   extern __shared__ double smem_raw[];
@@ -806,157 +917,176 @@ __global__ __launch_bounds__(R6_T) void k_r6_control(R6Args a) {
   {
     const double *lin = a.lin + (int64_t)b * R6_N * R6_NX * R6_SZ;
     for (int e = tid; e < R6_N * R6_NX * R6_SZ; e += R6_T) s.G[e] = lin[e];
+    if (tid < R6_SZ) s.zero[tid] = 0.0;
   }
   __syncthreads();
-  R6Var V;
-  R6Row R(V);
-  V.j = tid; V.ok = tid < R6_NV;
-  V.k = tid / R6_SZ; V.i = tid - V.k * R6_SZ;
-  V.gok = tid < R6_MGEN;
-  R.r = tid - R6_NV; R.ok = tid >= R6_NV && R.r < R6_MD;
-  R.k = R.r >= R6_NX ? (R.r - R6_NX) / R6_NX : 0;
-  R.i = R.r >= R6_NX ? (R.r - R6_NX) - R.k * R6_NX : R.r;
-  if (V.ok) {
-    const int k = V.k, i = V.i;
-    double xw, wq;
-    if (i < R6_NX) {
-      xw = Xb[k * R6_NX + i];
-      wq = r6_Q[i] * (k == R6_N ? 10.0 : 1.0);
-      V.P = wq; V.q = wq * (xw - xr[i]);
-      V.lb = -sqrt(10.0); V.ub = sqrt(10.0);
-    } else {
-      const double ub = Ub[k * R6_NU + i - R6_NX];
-      V.P = 0.01; V.q = 0.01 * ub;
-      V.lb = fmax(-sqrt(5.0), -R6_T_MAX - ub);
-      V.ub = fmin(sqrt(5.0), R6_T_MAX - ub);
+  // item tid + 512 h: variable j < 524 (h = 0: all of them below 512), else
+  // equality row r = item - 524; general row g = tid < 146 rides on slot 0
+  R6Var V[2];
+  R6Row R[2] = {R6Row(V[0]), R6Row(V[1])};
+  R6_FOR_H {
+    const int idx = tid + h * R6_T;
+    R6Var &W = V[h];
+    R6Row &Q = R[h];
+    W.j = idx; W.ok = idx < R6_NV;
+    W.k = idx / R6_SZ; W.i = idx - W.k * R6_SZ;
+    W.gok = h == 0 && tid < R6_MGEN;
+    Q.r = idx - R6_NV; Q.ok = h == 1 && idx >= R6_NV && Q.r < R6_MD;
+    Q.k = Q.r >= R6_NX ? (Q.r - R6_NX) / R6_NX : 0;
+    Q.i = Q.r >= R6_NX ? (Q.r - R6_NX) - Q.k * R6_NX : Q.r;
+    if (W.ok) {
+      const int k = W.k, i = W.i;
+      double xw, wq;
+      if (i < R6_NX) {
+        xw = Xb[k * R6_NX + i];
+        wq = r6_Q[i] * (k == R6_N ? 10.0 : 1.0);
+        W.P = wq; W.q = wq * (xw - xr[i]);
+        W.lb = -sqrt(10.0); W.ub = sqrt(10.0);
+      } else {
+        const double ub = Ub[k * R6_NU + i - R6_NX];
+        W.P = 0.01; W.q = 0.01 * ub;
+        W.lb = fmax(-sqrt(5.0), -R6_T_MAX - ub);
+        W.ub = fmin(sqrt(5.0), R6_T_MAX - ub);
+      }
+      W.Ab = 1.0;
+      W.x = 0.0;  // warm start dz = 0
+      W.yb = ysc[R6_MD + W.j];
+      if (k < R6_N)
+#pragma unroll
+        for (int e = 0; e < R6_NX; ++e) W.colA[e] = s.G[(k * R6_NX + e) * R6_SZ + i];
+      else
+#pragma unroll
+        for (int e = 0; e < R6_NX; ++e) W.colA[e] = 0.0;
     }
-    V.Ab = 1.0;
-    V.x = 0.0;  // warm start dz = 0
-    V.yb = ysc[R6_MD + V.j];
-    if (k < R6_N)
-#pragma unroll
-      for (int e = 0; e < R6_NX; ++e) V.colA[e] = s.G[(k * R6_NX + e) * R6_SZ + i];
-    else
-#pragma unroll
-      for (int e = 0; e < R6_NX; ++e) V.colA[e] = 0.0;
-  }
-  if (V.gok) {
-    const int g = V.j;
-    if (g < R6_MT) {
-      const double *u = Ub + g * R6_NU;
-      const double tm = sqrt((u[0] * u[0] + u[1] * u[1]) + u[2] * u[2]);
-      V.gA[0] = u[0] / tm; V.gA[1] = u[1] / tm; V.gA[2] = u[2] / tm;
-      V.gl = R6_T_MIN - tm; V.gu = INFINITY; V.gn = 3;
-    } else {
-      const int gg = g - R6_MT, k = 1 + gg / 4, c = gg % 4;
-      const double tg = 0.5773502691896257;  // np.tan(np.deg2rad(30.0)), gamma_gs
-      const double rx = Xb[k * R6_NX + 1], rc = Xb[k * R6_NX + (c < 2 ? 2 : 3)];
-      const double sg = (c & 1) ? 1.0 : -1.0;
-      V.gA[0] = tg; V.gA[1] = sg; V.gA[2] = 0.0;
-      V.gl = -(tg * rx + sg * rc); V.gu = INFINITY; V.gn = 2;
+    if (W.gok) {
+      const int g = W.j;
+      if (g < R6_MT) {
+        const double *u = Ub + g * R6_NU;
+        const double tm = sqrt((u[0] * u[0] + u[1] * u[1]) + u[2] * u[2]);
+        W.gA[0] = u[0] / tm; W.gA[1] = u[1] / tm; W.gA[2] = u[2] / tm;
+        W.gl = R6_T_MIN - tm; W.gu = INFINITY; W.gn = 3;
+      } else {
+        const int gg = g - R6_MT, k = 1 + gg / 4, c = gg % 4;
+        const double tg = 0.5773502691896257;  // np.tan(np.deg2rad(30.0)), gamma_gs
+        const double rx = Xb[k * R6_NX + 1], rc = Xb[k * R6_NX + (c < 2 ? 2 : 3)];
+        const double sg = (c & 1) ? 1.0 : -1.0;
+        W.gA[0] = tg; W.gA[1] = sg; W.gA[2] = 0.0;
+        W.gl = -(tg * rx + sg * rc); W.gu = INFINITY; W.gn = 2;
+      }
+      W.gy = ysc[R6_MD + R6_NV + g];
     }
-    V.gy = ysc[R6_MD + R6_NV + g];
-  }
-  if (R.ok) {
-    if (R.r < R6_NX) {
-      R.A[0] = 1.0;
+    if (Q.ok) {
+      if (Q.r < R6_NX) {
+        Q.A[0] = 1.0;
 #pragma unroll
-      for (int e = 1; e <= R6_SZ; ++e) R.A[e] = 0.0;
-      R.ur = 0.0;
-    } else {
+        for (int e = 1; e <= R6_SZ; ++e) Q.A[e] = 0.0;
+        Q.ur = 0.0;
+      } else {
 #pragma unroll
-      for (int e = 0; e < R6_SZ; ++e) R.A[e] = s.G[(R.k * R6_NX + R.i) * R6_SZ + e];
-      R.A[R6_SZ] = 1.0;
-      const int i = R.i;
-      R.ur = (i >= 4 && i < 7) ? gmb[R.k * 6 + i - 4] * dt : ((i >= 11) ? gmb[R.k * 6 + 3 + i - 11] * dt : 0.0);
+        for (int e = 0; e < R6_SZ; ++e) Q.A[e] = s.G[(Q.k * R6_NX + Q.i) * R6_SZ + e];
+        Q.A[R6_SZ] = 1.0;
+        const int i = Q.i;
+        Q.ur = (i >= 4 && i < 7) ? gmb[Q.k * 6 + i - 4] * dt : ((i >= 11) ? gmb[Q.k * 6 + 3 + i - 11] * dt : 0.0);
+      }
+      Q.yr = ysc[Q.r];
     }
-    R.yr = ysc[R.r];
+    // ---- OSQP solve (qp_device.h order): clip bounds, Ruiz scaling, rho, factor
+    if (W.ok) { W.lb = fmax(W.lb, -QP_OSQP_INFTY); W.ub = fmin(W.ub, QP_OSQP_INFTY); }
+    if (W.gok) { W.gl = fmax(W.gl, -QP_OSQP_INFTY); W.gu = fmin(W.gu, QP_OSQP_INFTY); }
+    if (Q.ok) Q.ur = fmin(fmax(Q.ur, -QP_OSQP_INFTY), QP_OSQP_INFTY);
   }
-  // ---- OSQP solve (qp_device.h order): clip bounds, Ruiz scaling, rho, factor
-  if (V.ok) { V.lb = fmax(V.lb, -QP_OSQP_INFTY); V.ub = fmin(V.ub, QP_OSQP_INFTY); }
-  if (V.gok) { V.gl = fmax(V.gl, -QP_OSQP_INFTY); V.gu = fmin(V.gu, QP_OSQP_INFTY); }
-  if (R.ok) R.ur = fmin(fmax(R.ur, -QP_OSQP_INFTY), QP_OSQP_INFTY);
+  mark(0);
   for (int r = tid; r < R6_M; r += R6_T) s.E[r] = 1.0;
-  if (R.ok) s.dpl[R.r] = R.r < R6_NX ? R.A[0] : R.A[R6_SZ];
-  if (V.gok)
+  R6_FOR_H {
+    if (R[h].ok) s.dpl[R[h].r] = R[h].r < R6_NX ? R[h].A[0] : R[h].A[R6_SZ];
+    if (V[h].gok)
 #pragma unroll
-    for (int e = 0; e < 3; ++e) s.gen[V.j * 3 + e] = V.gA[e];
-  if (V.ok) V.D = 1.0;
+      for (int e = 0; e < 3; ++e) s.gen[V[h].j * 3 + e] = V[h].gA[e];
+    if (V[h].ok) V[h].D = 1.0;
+  }
   if (tid == 0) { s.c = 1.0; s.rho_s = fmin(fmax(a.rho[b], QP_RHO_MIN), QP_RHO_MAX); }
   __syncthreads();
   for (int it = 0; it < st.scaling; ++it) {
     // column factors -> dsc, row factors -> w (equality: [0, MD), general: MD + g)
-    double eb = 1.0;
-    if (V.ok) {
-      double v = fabs(V.P);
-      if (V.i < R6_NX) v = fmax(v, fabs(s.dpl[r6_eqid_row(V.k, V.i)]));
-      if (V.k < R6_N)
+    double eb[2] = {1.0, 1.0};
+    R6_FOR_H {
+      R6Var &W = V[h];
+      R6Row &Q = R[h];
+      if (W.ok) {
+        double v = fabs(W.P);
+        if (W.i < R6_NX) v = fmax(v, fabs(s.dpl[r6_eqid_row(W.k, W.i)]));
+        if (W.k < R6_N)
 #pragma unroll
-        for (int e = 0; e < R6_NX; ++e) v = fmax(v, fabs(V.colA[e]));
-      v = fmax(v, fabs(V.Ab));
+          for (int e = 0; e < R6_NX; ++e) v = fmax(v, fabs(W.colA[e]));
+        v = fmax(v, fabs(W.Ab));
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        int g, sl;
-        if (r6_gen_slot(V.k, V.i, e, g, sl)) v = fmax(v, fabs(s.gen[g * 3 + sl]));
+        for (int e = 0; e < 4; ++e) {
+          int g, sl;
+          if (r6_gen_slot(W.k, W.i, e, g, sl)) v = fmax(v, fabs(s.gen[g * 3 + sl]));
+        }
+        s.dsc[W.j] = 1.0 / sqrt(qp_limit(v));
+        eb[h] = 1.0 / sqrt(qp_limit(fmax(0.0, fabs(W.Ab))));
       }
-      s.dsc[V.j] = 1.0 / sqrt(qp_limit(v));
-      eb = 1.0 / sqrt(qp_limit(fmax(0.0, fabs(V.Ab))));
-    }
-    if (R.ok) {
-      double v = 0.0;
-      const int ne = R.r < R6_NX ? 1 : R6_SZ + 1;
+      if (Q.ok) {
+        double v = 0.0;
+        const int ne = Q.r < R6_NX ? 1 : R6_SZ + 1;
 #pragma unroll
-      for (int e = 0; e < R6_SZ + 1; ++e)
-        if (e < ne) v = fmax(v, fabs(R.A[e]));
-      s.w[R.r] = 1.0 / sqrt(qp_limit(v));
-    }
-    if (V.gok) {
-      double v = 0.0;
+        for (int e = 0; e < R6_SZ + 1; ++e)
+          if (e < ne) v = fmax(v, fabs(Q.A[e]));
+        s.w[Q.r] = 1.0 / sqrt(qp_limit(v));
+      }
+      if (W.gok) {
+        double v = 0.0;
 #pragma unroll
-      for (int e = 0; e < 3; ++e)
-        if (e < V.gn) v = fmax(v, fabs(V.gA[e]));
-      s.w[R6_MD + V.j] = 1.0 / sqrt(qp_limit(v));
+        for (int e = 0; e < 3; ++e)
+          if (e < W.gn) v = fmax(v, fabs(W.gA[e]));
+        s.w[R6_MD + W.j] = 1.0 / sqrt(qp_limit(v));
+      }
     }
     __syncthreads();
-    if (R.ok) {
-      const double e = s.w[R.r];
-      if (R.r < R6_NX) {
-        R.A[0] = e * R.A[0] * s.dsc[R.r];
-        s.dpl[R.r] = R.A[0];
-      } else {
-        const int o = R.k * R6_SZ;
-#pragma unroll
-        for (int c = 0; c < R6_SZ; ++c) R.A[c] = e * R.A[c] * s.dsc[o + c];
-        R.A[R6_SZ] = e * R.A[R6_SZ] * s.dsc[(R.k + 1) * R6_SZ + R.i];
-        s.dpl[R.r] = R.A[R6_SZ];
-      }
-      s.E[R.r] *= e;
-    }
-    if (V.gok) {
-      const double e = s.w[R6_MD + V.j];
-      int col[3];
-      r6_gen_cols(V.j, col);
-#pragma unroll
-      for (int c = 0; c < 3; ++c)
-        if (c < V.gn) {
-          V.gA[c] = e * V.gA[c] * s.dsc[col[c]];
-          s.gen[V.j * 3 + c] = V.gA[c];
-        }
-      s.E[R6_MD + R6_NV + V.j] *= e;
-    }
     double v[1] = {0.0}, mx[1] = {0.0};
-    if (V.ok) {
-      const double d = s.dsc[V.j];
-      if (V.k < R6_N)
+    R6_FOR_H {
+      R6Var &W = V[h];
+      R6Row &Q = R[h];
+      if (Q.ok) {
+        const double e = s.w[Q.r];
+        if (Q.r < R6_NX) {
+          Q.A[0] = e * Q.A[0] * s.dsc[Q.r];
+          s.dpl[Q.r] = Q.A[0];
+        } else {
+          const int o = Q.k * R6_SZ;
 #pragma unroll
-        for (int e = 0; e < R6_NX; ++e) V.colA[e] = s.w[R6_NX + R6_NX * V.k + e] * V.colA[e] * d;
-      V.Ab = eb * V.Ab * d;
-      s.E[R6_MD + V.j] *= eb;
-      V.P = d * V.P * d;
-      V.q = d * V.q;
-      V.D *= d;
-      v[0] = fabs(V.P);
-      mx[0] = fabs(V.q);
+          for (int c = 0; c < R6_SZ; ++c) Q.A[c] = e * Q.A[c] * s.dsc[o + c];
+          Q.A[R6_SZ] = e * Q.A[R6_SZ] * s.dsc[(Q.k + 1) * R6_SZ + Q.i];
+          s.dpl[Q.r] = Q.A[R6_SZ];
+        }
+        s.E[Q.r] *= e;
+      }
+      if (W.gok) {
+        const double e = s.w[R6_MD + W.j];
+        int col[3];
+        r6_gen_cols(W.j, col);
+#pragma unroll
+        for (int c = 0; c < 3; ++c)
+          if (c < W.gn) {
+            W.gA[c] = e * W.gA[c] * s.dsc[col[c]];
+            s.gen[W.j * 3 + c] = W.gA[c];
+          }
+        s.E[R6_MD + R6_NV + W.j] *= e;
+      }
+      if (W.ok) {
+        const double d = s.dsc[W.j];
+        if (W.k < R6_N)
+#pragma unroll
+          for (int e = 0; e < R6_NX; ++e) W.colA[e] = s.w[R6_NX + R6_NX * W.k + e] * W.colA[e] * d;
+        W.Ab = eb[h] * W.Ab * d;
+        s.E[R6_MD + W.j] *= eb[h];
+        W.P = d * W.P * d;
+        W.q = d * W.q;
+        W.D *= d;
+        v[0] += fabs(W.P);
+        mx[0] = fmax(mx[0], fabs(W.q));
+      }
     }
     r6_sum<1>(v, s.red);
     r6_max<1>(mx, s.red);
@@ -964,66 +1094,85 @@ __global__ __launch_bounds__(R6_T) void k_r6_control(R6Args a) {
     const double nq = qp_limit(mx[0]);
     ct = qp_limit(fmax(ct, nq));
     ct = 1.0 / ct;
-    if (V.ok) { V.P *= ct; V.q *= ct; }
+    R6_FOR_H {
+      if (V[h].ok) { V[h].P *= ct; V[h].q *= ct; }
+    }
     if (tid == 0) s.c *= ct;
     __syncthreads();
   }
-  if (V.ok) { const double e = s.E[R6_MD + V.j]; V.lb = e * V.lb; V.ub = e * V.ub; }
-  if (V.gok) { const double e = s.E[R6_MD + R6_NV + V.j]; V.gl = e * V.gl; V.gu = e * V.gu; }
-  if (R.ok) R.ur = s.E[R.r] * R.ur;
-  int f = r6_factor(s, V, R, st.sigma);
+  R6_FOR_H {
+    R6Var &W = V[h];
+    if (W.ok) { const double e = s.E[R6_MD + W.j]; W.lb = e * W.lb; W.ub = e * W.ub; }
+    if (W.gok) { const double e = s.E[R6_MD + R6_NV + W.j]; W.gl = e * W.gl; W.gu = e * W.gu; }
+    if (R[h].ok) R[h].ur = s.E[R[h].r] * R[h].ur;
+  }
+  mark(1);
+  int f = r6_factor(s, V, R, st.sigma, mark);
+  mark(2);
   QPResult res{-10, 0, 0.0, 0};
   if (f) res.factor_fail = f;
   if (!f) {
     // warm start x = 0 / D = 0, z = A x = 0; y persisted (osqp_rti.py:521-524)
-    V.x = 0.0; V.zb = 0.0; R.zr = 0.0; V.gz = 0.0;
-    if (V.ok) V.zb = 0.0 + V.Ab * V.x;
+    R6_FOR_H {
+      V[h].x = 0.0; V[h].zb = 0.0; R[h].zr = 0.0; V[h].gz = 0.0;
+      if (V[h].ok) V[h].zb = 0.0 + V[h].Ab * V[h].x;
+    }
     r6_rebuild_w(s, V, R);
     const double sig = st.sigma, al = st.alpha;
     bool can_check = false;
     int it;
     double o[8], re_[4];
     for (it = 1; it <= st.max_iter; ++it) {
-      if (V.ok) s.rhs[V.j] = sig * V.x - V.q + r6_col_dot(s, V, s.w, V.ztb, s.w + R6_MD);
+      R6_FOR_H {
+        if (V[h].ok) s.rhs[V[h].j] = sig * V[h].x - V[h].q + r6_col_dot(s, V[h], s.w, V[h].ztb, s.w + R6_MD);
+      }
       __syncthreads();
-      r6_solve(s);
+      mark(3);
+      r6_solve(s, mark);
       const double rs = s.rho_s;
-      if (V.ok) {
-        const double xt = s.xs[V.j], xo = V.x;
-        const double xn = al * xt + (1.0 - al) * xo;
-        V.dx = xn - xo;
-        V.x = xn;
-        const double ztl = 0.0 + V.Ab * xt;
-        const double rho = r6_rho(V.lb, V.ub, rs), zo = V.zb, yo = V.yb;
-        const double zr = al * ztl + (1.0 - al) * zo;
-        double zn = zr + yo / rho;
-        zn = fmin(fmax(zn, V.lb), V.ub);
-        const double d = rho * (zr - zn);
-        V.dyb = d; V.yb = yo + d; V.zb = zn;
-        V.ztb = rho * zn - V.yb;
-      }
-      if (V.gok) {
-        const double ztl = r6_gen_dot(V, s.xs);
-        const double rho = r6_rho(V.gl, V.gu, rs), zo = V.gz, yo = V.gy;
-        const double zr = al * ztl + (1.0 - al) * zo;
-        double zn = zr + yo / rho;
-        zn = fmin(fmax(zn, V.gl), V.gu);
-        const double d = rho * (zr - zn);
-        V.gdy = d; V.gy = yo + d; V.gz = zn;
-      }
-      if (R.ok) {
-        const double ztl = r6_row_dot(R, s.xs);
-        const double rho = QP_RHO_EQ * rs, zo = R.zr, yo = R.yr;
-        const double zr = al * ztl + (1.0 - al) * zo;
-        double zn = zr + yo / rho;
-        zn = fmin(fmax(zn, R.ur), R.ur);
-        const double d = rho * (zr - zn);
-        R.dyr = d; R.yr = yo + d; R.zr = zn;
+      R6_FOR_H {
+        R6Var &W = V[h];
+        R6Row &Q = R[h];
+        if (W.ok) {
+          const double xt = s.xs[W.j], xo = W.x;
+          const double xn = al * xt + (1.0 - al) * xo;
+          W.dx = xn - xo;
+          W.x = xn;
+          const double ztl = 0.0 + W.Ab * xt;
+          const double rho = r6_rho(W.lb, W.ub, rs), zo = W.zb, yo = W.yb;
+          const double zr = al * ztl + (1.0 - al) * zo;
+          double zn = zr + yo / rho;
+          zn = fmin(fmax(zn, W.lb), W.ub);
+          const double d = rho * (zr - zn);
+          W.dyb = d; W.yb = yo + d; W.zb = zn;
+          W.ztb = rho * zn - W.yb;
+        }
+        if (W.gok) {
+          const double ztl = r6_gen_dot(W, s.xs);
+          const double rho = r6_rho(W.gl, W.gu, rs), zo = W.gz, yo = W.gy;
+          const double zr = al * ztl + (1.0 - al) * zo;
+          double zn = zr + yo / rho;
+          zn = fmin(fmax(zn, W.gl), W.gu);
+          const double d = rho * (zr - zn);
+          W.gdy = d; W.gy = yo + d; W.gz = zn;
+        }
+        if (Q.ok) {
+          const double ztl = r6_row_dot(Q, s.xs);
+          const double rho = QP_RHO_EQ * rs, zo = Q.zr, yo = Q.yr;
+          const double zr = al * ztl + (1.0 - al) * zo;
+          double zn = zr + yo / rho;
+          zn = fmin(fmax(zn, Q.ur), Q.ur);
+          const double d = rho * (zr - zn);
+          Q.dyr = d; Q.yr = yo + d; Q.zr = zn;
+        }
       }
       __syncthreads();  // every read of s.w / s.xs of this iteration is done
-      if (R.ok) s.w[R.r] = QP_RHO_EQ * rs * R.zr - R.yr;
-      if (V.gok) s.w[R6_MD + V.j] = r6_rho(V.gl, V.gu, rs) * V.gz - V.gy;
+      R6_FOR_H {
+        if (R[h].ok) s.w[R[h].r] = QP_RHO_EQ * rs * R[h].zr - R[h].yr;
+        if (V[h].gok) s.w[R6_MD + V[h].j] = r6_rho(V[h].gl, V[h].gu, rs) * V[h].gz - V[h].gy;
+      }
       __syncthreads();
+      mark(7);
       can_check = st.check_termination && (it % st.check_termination == 0);
       const bool adapt = st.adaptive_rho && st.adaptive_rho_interval && (it % st.adaptive_rho_interval == 0);
       if (can_check || adapt) {
@@ -1041,12 +1190,13 @@ __global__ __launch_bounds__(R6_T) void k_r6_control(R6Args a) {
           if (tid == 0) s.rho_s = est;
           __syncthreads();
           if (it < st.max_iter) {
-            f = r6_factor(s, V, R, st.sigma);
+            f = r6_factor(s, V, R, st.sigma, mark);
             if (f) { res.factor_fail = f; break; }
           }
         }
       }
       if (can_check || adapt) r6_rebuild_w(s, V, R);
+      mark(8);
     }
     if (!res.factor_fail) {
       if (!can_check) {
@@ -1061,7 +1211,9 @@ __global__ __launch_bounds__(R6_T) void k_r6_control(R6Args a) {
   }
   const bool has = !res.factor_fail && (res.status == 1 || res.status == 2 || res.status == -2);
   // ---- solution: the unscaled deviations onto the plan, kept unshifted (gp_mpc.py:358-359)
-  if (has && V.ok) s.xs[V.j] = V.D * V.x;
+  R6_FOR_H {
+    if (has && V[h].ok) s.xs[V[h].j] = V[h].D * V[h].x;
+  }
   __syncthreads();
   double *Xo = a.Xo + (int64_t)b * (R6_N + 1) * R6_NX;
   double *Uw = a.U + (int64_t)b * R6_N * R6_NU;
@@ -1077,9 +1229,11 @@ __global__ __launch_bounds__(R6_T) void k_r6_control(R6Args a) {
     }
     __syncthreads();  // every thread read U before it is overwritten
     if (tid < R6_N * R6_NU) Uw[tid] = un;
-    if (R.ok) ysc[R.r] = R.yr;
-    if (V.ok) ysc[R6_MD + V.j] = V.yb;
-    if (V.gok) ysc[R6_MD + R6_NV + V.j] = V.gy;
+    R6_FOR_H {
+      if (R[h].ok) ysc[R[h].r] = R[h].yr;
+      if (V[h].ok) ysc[R6_MD + V[h].j] = V[h].yb;
+      if (V[h].gok) ysc[R6_MD + R6_NV + V[h].j] = V[h].gy;
+    }
     __syncthreads();
   }
   if (tid == 0) {
@@ -1098,6 +1252,7 @@ __global__ __launch_bounds__(R6_T) void k_r6_control(R6Args a) {
       a.pending[b] = 1;
     }
   }
+  mark(9);
 }
 
 // 3. the truth plant step with the plan's first control: RK4 + the drag
@@ -1185,7 +1340,9 @@ extern "C" int gpmpc_rollout6_create(gpmpc_ctx *ctx, gpmpc_fitc *gp_v, gpmpc_fit
   hipLaunchKernelGGL(k_fitc_beta, dim3((gw.n + 255) / 256, 3), dim3(256), 0, ctx->stream, gw.n, gw.W,
                      gw.alphaT, r->betaw.as<double>());
   static bool attr = [] {
-    return hipFuncSetAttribute((const void *)k_r6_control, hipFuncAttributeMaxDynamicSharedMemorySize,
+    (void)hipFuncSetAttribute((const void *)k_r6_control<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              sizeof(R6Smem));
+    return hipFuncSetAttribute((const void *)k_r6_control<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                (int)sizeof(R6Smem)) == hipSuccess;
   }();
   if (!attr) {
@@ -1229,6 +1386,14 @@ static R6Args r6_args(gpmpc_rollout6 *r) {
   return a;
 }
 
+static bool r6_stamps_on() {
+  static const bool on = [] {
+    const char *e = getenv("GPMPC_R6_STAMPS");
+    return e && atoi(e) > 0;
+  }();
+  return on;
+}
+
 extern "C" int gpmpc_rollout6_step(gpmpc_rollout6 *r, int nsteps) {
   GPMPC_CHECK_ARG(r && nsteps >= 0);
   GPMPC_HIP(hipSetDevice(r->ctx->device));
@@ -1236,7 +1401,8 @@ extern "C" int gpmpc_rollout6_step(gpmpc_rollout6 *r, int nsteps) {
   const R6Args a = r6_args(r);
   for (int it = 0; it < nsteps; ++it) {
     hipLaunchKernelGGL(k_r6_predict, dim3(r->B), dim3(R6_PT), 0, s, a);
-    hipLaunchKernelGGL(k_r6_control, dim3(r->B), dim3(R6_T), sizeof(R6Smem), s, a);
+    if (r6_stamps_on()) hipLaunchKernelGGL(k_r6_control<true>, dim3(r->B), dim3(R6_T), sizeof(R6Smem), s, a);
+    else hipLaunchKernelGGL(k_r6_control<false>, dim3(r->B), dim3(R6_T), sizeof(R6Smem), s, a);
     hipLaunchKernelGGL(k_r6_plant, dim3((r->B + 63) / 64), dim3(64), 0, s, a, r->B);
     GPMPC_HIP(hipGetLastError());
   }
@@ -1273,6 +1439,17 @@ extern "C" int gpmpc_rollout6_get_state(gpmpc_rollout6 *r, double *U, double *X_
 
 extern "C" int gpmpc_rollout6_destroy(gpmpc_rollout6 *r) {
   if (r && r->ctx) (void)hipStreamSynchronize(r->ctx->stream);
+  if (r && r6_stamps_on()) {  // diagnostic: phase cycles of rollout 0, summed over the steps
+    static const char *nm[12] = {"setup", "scaling", "factor0", "rhs", "kkt_forward", "kkt_diagonal",
+                                 "kkt_backward", "update", "checks_adapt", "tail", "factor_gj", "factor_prod"};
+    unsigned long long h[12] = {0};
+    if (hipMemcpyFromSymbol(h, HIP_SYMBOL(g_r6_stamps), sizeof(h)) == hipSuccess) {
+      unsigned long long tot = 0;
+      for (int k = 0; k < 12; ++k) tot += h[k];
+      for (int k = 0; k < 12; ++k)
+        fprintf(stderr, "r6 stamps %-14s %12llu cycles %5.1f%%\n", nm[k], h[k], tot ? 100.0 * h[k] / tot : 0.0);
+    }
+  }
   delete r;
   return 0;
 }
