@@ -147,6 +147,28 @@ __device__ __forceinline__ int ft_factor(S &s, int cw) {
   return __shfl(bad, __ffsll((long long)m) - 1);
 }
 
+// FT_PF2 1: chain operands two block steps ahead (measured 318 us against 314 us
+// for the one-step form at 1024 landings: spills 3 -> 9 VGPRs, nothing gained)
+#ifndef FT_PF2
+#define FT_PF2 0
+#endif
+
+// init + sum_j g[j] bcast_j(src) (two accumulators, as dot_bc_init), reloading
+// g[j] from nx[j * ST] right after its FMA when rl
+template <int ST, int... J>
+__device__ __forceinline__ double ft_dot_reload(double init, double src, double (&g)[FT_SZ], const double *nx,
+                                                bool rl, std::integer_sequence<int, J...>) {
+  double a0 = init, a1 = 0.0;
+  (((J % 2 == 0 ? fmac_bc<J, J == 0>(a0, src, g[J]) : fmac_bc<J, false>(a1, src, g[J])),
+    (rl ? (void)(g[J] = nx[J * ST]) : (void)0)), ...);
+  return a0 + a1;
+}
+template <int ST>
+__device__ __forceinline__ double ft_dot_reload(double init, double src, double (&g)[FT_SZ], const double *nx,
+                                                bool rl) {
+  return ft_dot_reload<ST>(init, src, g, nx, rl, std::make_integer_sequence<int, FT_SZ>{});
+}
+
 // b <- M^-1 b, by phases (PH: 1 forward | 2 diagonal | 4 backward).  PH 1 / 4 run
 // on the chain wave only; PH 2 on both waves of the workgroup (caller barriers).
 template <int PH, class S>
@@ -161,6 +183,65 @@ __device__ __forceinline__ void ft_solve(S &s, double *b, int cw) {
     // the two rows walk in opposite directions, so a step's address is not an
     // immediate offset from one base, and left alone the compiler hoists all
     // twenty of them out of the ADMM loop as live registers (spilled elsewhere).
+#if FT_PF2
+    // Two steps ahead: each term's operand for step t + 2 loads right after the
+    // term's FMA of step t, into the register it frees (two buffers, as the
+    // one-step-ahead form, but twice the latency cover for the LDS reads).
+    if constexpr (PH == 1) {
+      // top: y over blocks 0..10;  bottom: z over blocks 20..11, then z'_10
+      int ib = (top ? 0 : (FT_NB - 1) * FT_SZ) + rs;
+      const int db = top ? FT_SZ : -FT_SZ;
+      int ig = (top ? 0 : (FT_NB - 1) * FT_BS) + FT_GO + rs;
+      const int dg = top ? FT_BS : -FT_BS;
+      double y = b[ib];
+      double gA[FT_SZ], gB[FT_SZ], cA, cB;
+#pragma unroll
+      for (int j = 0; j < FT_SZ; ++j) { gA[j] = F[ig + j * FT_SZ]; gB[j] = F[ig + dg + j * FT_SZ]; }
+      cA = b[ib + db];
+      cB = b[ib + 2 * db];
+#pragma unroll
+      for (int t = 0; t < FT_MID; ++t) {
+        double (&g)[FT_SZ] = (t & 1) ? gB : gA;
+        double &c = (t & 1) ? cB : cA;
+        const double init = (t == FT_MID - 1 && !top) ? 0.0 : c;  // z'_10 = -K_11^T z_11
+        const bool rl = t + 2 < FT_MID;
+        if (rl) c = b[ib + 3 * db];
+        const double yn = ft_dot_reload<FT_SZ>(init, y, g, F + ig + 2 * dg, rl);
+        b[ib] = y;
+        y = yn;
+        ib += db;
+        ig += dg;
+        asm volatile("" : "+v"(ib), "+v"(ig));
+      }
+      if (top) b[ib] = y;            // y_10 over b_10
+      else b[FT_ZS + rs] = y;        // z'_10
+    } else {
+      // top: x_9 .. x_0 from x_10;  bottom: x_11 .. x_20
+      double x = b[FT_MID * FT_SZ + rs];
+      int iu = (top ? (FT_MID - 1) : (FT_MID + 1)) * FT_SZ + rs;
+      const int du = top ? -FT_SZ : FT_SZ;
+      int ig = (top ? (FT_MID - 1) : (FT_MID + 1)) * FT_BS + FT_GO + rs * FT_SZ;
+      const int dg = top ? -FT_BS : FT_BS;
+      double gA[FT_SZ], gB[FT_SZ], cA, cB;
+#pragma unroll
+      for (int j = 0; j < FT_SZ; ++j) { gA[j] = F[ig + j]; gB[j] = F[ig + dg + j]; }
+      cA = b[iu];
+      cB = b[iu + du];
+#pragma unroll
+      for (int t = 0; t < FT_MID; ++t) {
+        double (&g)[FT_SZ] = (t & 1) ? gB : gA;
+        double &c = (t & 1) ? cB : cA;
+        const double init = c;
+        const bool rl = t + 2 < FT_MID;
+        if (rl) c = b[iu + 2 * du];
+        x = ft_dot_reload<1>(init, x, g, F + ig + 2 * dg, rl);
+        b[iu] = x;
+        iu += du;
+        ig += dg;
+        asm volatile("" : "+v"(iu), "+v"(ig));
+      }
+    }
+#else
     if constexpr (PH == 1) {
       // top: y over blocks 0..10;  bottom: z over blocks 20..11, then z'_10
       int ib = (top ? 0 : (FT_NB - 1) * FT_SZ) + rs;
@@ -220,6 +301,7 @@ __device__ __forceinline__ void ft_solve(S &s, double *b, int cw) {
         asm volatile("" : "+v"(iu), "+v"(ig));
       }
     }
+#endif
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
   } else {
     // diagonal: u_k / x_10 / w_k, eight blocks a round (one per DPP row of
