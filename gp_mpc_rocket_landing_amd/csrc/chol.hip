@@ -183,6 +183,7 @@ __device__ __forceinline__ int diag128_core(double (*S)[DP], double *col, int &s
       if (wave == 0) {
         for (int t = 0; t < 3; ++t) trail_tile(t, c0, c0 - NB);
         wave_lds_sync();
+        mark(3);
       } else {
         for (int t = 3 + wave - 1; t < ntile; t += 3) trail_tile(t, c0, c0 - NB);
       }
@@ -246,6 +247,7 @@ __device__ __forceinline__ int diag128_core(double (*S)[DP], double *col, int &s
           wave_lds_sync();
         }
       }
+      mark(7);
       if (fail) {
         if (lane == 0) {
           *infob = K0 + c0 + fail;
@@ -657,8 +659,8 @@ static hipError_t launch_potrf_batched128(hipStream_t s, int n, int batch, doubl
     unsigned long long h[8];
     (void)hipStreamSynchronize(s);
     (void)hipMemcpyFromSymbol(h, HIP_SYMBOL(g_d128_stamps), sizeof(h));
-    fprintf(stderr, "diag128 cycles: load %llu diag %llu panel %llu trail %llu lout %llu inv %llu "
-                    "linvout %llu\n", h[0], h[1], h[2], h[3], h[4], h[5], h[6]);
+    fprintf(stderr, "diag128 cycles: load %llu diag %llu panel %llu trail0 %llu lout %llu inv %llu "
+                    "linvout %llu fac4 %llu\n", h[0], h[1], h[2], h[3], h[4], h[5], h[6], h[7]);
     const unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     (void)hipMemcpyToSymbol(HIP_SYMBOL(g_d128_stamps), z, sizeof(z));
   }
