@@ -230,7 +230,9 @@ __device__ __forceinline__ int diag128_core(double (*S)[DP], double *col, int &s
               if (c0 + lane < pw) M[(int64_t)(c0 + lane) * lda + c0 + j + q] = p[q];
             }
         }
-        wave_lds_sync();
+        // only wave 0 touches this block now and one wave's LDS operations execute
+        // in order, so no lgkmcnt wait: a compiler fence is enough
+        asm volatile("" ::: "memory");
         const int j4 = j + 4;
         if (j4 < NB) {
           // lower 16 x 16 tiles meeting rows/cols >= j4: (1,1) always, (1,0) and (0,0) while j4 < 16
@@ -244,7 +246,7 @@ __device__ __forceinline__ int diag128_core(double (*S)[DP], double *col, int &s
 #pragma unroll
             for (int r = 0; r < 4; ++r) S[c0 + rb + mf_row(lane, r)][c0 + cb + li] -= acc[r];
           }
-          wave_lds_sync();
+          asm volatile("" ::: "memory");
         }
       }
       mark(7);
