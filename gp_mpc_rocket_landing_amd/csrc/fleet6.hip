@@ -340,7 +340,7 @@ struct R6Smem {
   double dsc[R6_NV];                  // per-pass column scaling / factor scratch
   double dpl[R6_MD];                  // each equality row's identity entry (scaled)
   double gen[R6_MGEN * 3];            // general rows' values (scaled)
-  double T[R6_SZ * R6_SZ];            // Gauss-Jordan block
+  double T[2][R6_SZ * R6_SZ];         // Gauss-Jordan block (ping-pong: one barrier per pivot)
   double Gt[R6_NX * R6_SZ];           // G_k before it replaces C_k
   double Sch[R6_NX * R6_NX];          // G_k C_k^T
   double red[16][12];
@@ -557,40 +557,42 @@ __device__ __forceinline__ int r6_factor(R6Smem &s, R6Var (&V)[2], R6Row (&R)[2]
   }
   __syncthreads();
   mark(2);  // (stamps: the assembly)
-  // the sweep
+  // the sweep; the Gauss-Jordan pivots read one copy of the block and write the
+  // other, so a pivot needs one workgroup barrier instead of two
   const int ti = tid / R6_SZ, tj = tid - ti * R6_SZ;
   const bool tok = tid < R6_SZ * R6_SZ;
+  int cb = 0;
   for (int k = 0; k <= R6_N; ++k) {
     const int nb = (k == R6_N) ? R6_NX : R6_SZ;
+    cb = 0;
     if (tok) {
       double v = s.Sinv[k * R6_TRI + r6_tri(ti, tj)];
       if (k > 0 && ti < R6_NX && tj < R6_NX) v -= s.Sch[ti * R6_NX + tj];
-      s.T[tid] = v;
+      s.T[0][tid] = v;
     }
     __syncthreads();
     for (int p = 0; p < nb; ++p) {
-      double piv = 0.0, tip = 0.0, tpj = 0.0, tij = 0.0;
-      if (tok) {
-        piv = s.T[p * R6_SZ + p];
-        tip = s.T[ti * R6_SZ + p];
-        tpj = s.T[p * R6_SZ + tj];
-        tij = s.T[tid];
-      } else {
-        piv = s.T[p * R6_SZ + p];
-      }
-      __syncthreads();
+      const double *Tc = s.T[cb];
+      const double piv = Tc[p * R6_SZ + p];
       if (!(piv > 0.0)) return k + 1;  // uniform: every thread read the same pivot
-      if (tok && ti < nb && tj < nb) {
-        double nv;
-        if (ti == p && tj == p) nv = 1.0 / piv;
-        else if (ti == p) nv = tpj / piv;
-        else if (tj == p) nv = -tip / piv;
-        else nv = tij - (tip / piv) * tpj;
-        s.T[tid] = nv;
+      if (tok) {
+        const double tip = Tc[ti * R6_SZ + p], tpj = Tc[p * R6_SZ + tj], tij = Tc[tid];
+        // 1/piv by v_rcp_f64 + two Newton steps (blk_recip, within an ulp of the
+        // division) instead of an IEEE division per entry on every pivot's path
+        const double inv = blk_recip(piv), q = tip * inv;
+        double nv = tij;
+        if (ti < nb && tj < nb) {
+          if (ti == p && tj == p) nv = inv;
+          else if (ti == p) nv = tpj * inv;
+          else if (tj == p) nv = -q;
+          else nv = tij - q * tpj;
+        }
+        s.T[cb ^ 1][tid] = nv;
       }
+      cb ^= 1;
       __syncthreads();
     }
-    if (tok && ti >= tj) s.Sinv[k * R6_TRI + r6_tri(ti, tj)] = (ti < nb && tj < nb) ? s.T[tid] : 0.0;
+    if (tok && ti >= tj) s.Sinv[k * R6_TRI + r6_tri(ti, tj)] = (ti < nb && tj < nb) ? s.T[cb][tid] : 0.0;
     mark(10);
     if (k == R6_N) break;
     // G_k = C_k S_k^-1, C_k[i][:] = rho_eq dpl(k, i) (staged row (k, i))
@@ -599,7 +601,7 @@ __device__ __forceinline__ int r6_factor(R6Smem &s, R6Var (&V)[2], R6Row (&R)[2]
       const int i = tid / R6_SZ, c = tid - i * R6_SZ;
       const double sc = re * s.dpl[R6_NX + R6_NX * k + i];
       double acc = 0.0;
-      for (int e = 0; e < R6_SZ; ++e) acc += (sc * g[i * R6_SZ + e]) * s.T[e * R6_SZ + c];
+      for (int e = 0; e < R6_SZ; ++e) acc += (sc * g[i * R6_SZ + e]) * s.T[cb][e * R6_SZ + c];
       s.Gt[tid] = acc;
     }
     __syncthreads();
