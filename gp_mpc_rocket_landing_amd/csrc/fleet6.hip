@@ -684,12 +684,28 @@ __device__ __forceinline__ void r6_solve(R6Smem &s, MK &mark) {
     if (a < nb) {
       const double *S = s.Sinv + k * R6_TRI;
       const double *y = s.rhs + k * R6_SZ;
+      // unrolled over the 17 entries (the last block's 3 masked) in three chunks
+      // of loads in flight (a runtime-count loop waited on each pair; all 17 at
+      // once spilled the items' registers)
       double acc0 = 0.0, acc1 = 0.0;
-      for (int bb = 0; bb + 1 < nb; bb += 2) {
-        acc0 = fma(S[r6_tri(a, bb)], y[bb], acc0);
-        acc1 = fma(S[r6_tri(a, bb + 1)], y[bb + 1], acc1);
+#pragma unroll
+      for (int c0 = 0; c0 < R6_SZ; c0 += 6) {
+        double sv[6], yv[6];
+#pragma unroll
+        for (int q = 0; q < 6; ++q) {
+          const int bb = c0 + q < R6_SZ ? c0 + q : R6_SZ - 1;
+          sv[q] = S[r6_tri(a, bb)];
+          yv[q] = y[bb];
+        }
+#pragma unroll
+        for (int q = 0; q < 6; ++q) {
+          const int bb = c0 + q;
+          if (bb >= R6_SZ) continue;
+          if (bb & 1) acc1 = bb < nb ? fma(sv[q], yv[q], acc1) : acc1;
+          else acc0 = bb < nb ? fma(sv[q], yv[q], acc0) : acc0;
+        }
+        asm volatile("" ::: "memory");
       }
-      if (nb & 1) acc0 = fma(S[r6_tri(a, nb - 1)], y[nb - 1], acc0);
       s.xs[e] = acc0 + acc1;
     }
   }
