@@ -345,6 +345,7 @@ struct R6Smem {
   double Sch[R6_NX * R6_NX];          // G_k C_k^T
   double red[16][12];
   double zero[R6_SZ];                 // the forward chain's operand row for its pass-through lanes
+  double dump[64];                    // the chains' store target for lanes that keep no result
   double c, rho_s;
   int flag;
 };
@@ -647,7 +648,7 @@ __device__ __forceinline__ void r6_solve(R6Smem &s, MK &mark) {
     for (int e = 0; e < R6_SZ; ++e) g[e] = F[go + e];
     double y = s.rhs[rr];
     double b16 = s.rhs[R6_SZ - 1], bn = s.rhs[R6_SZ + rr];
-#pragma unroll 1
+#pragma unroll 2
     for (int k = 0; k < R6_N; ++k) {
       const int gn = go + gs;
       const double init = fma(g[R6_SZ - 1], b16, bn);
@@ -672,7 +673,9 @@ __device__ __forceinline__ void r6_solve(R6Smem &s, MK &mark) {
       fmac_bc<14, false>(a0, y, g[14]); g[14] = F[gn + 14];
       fmac_bc<15, false>(a1, y, g[15]); g[15] = F[gn + 15];
       y = a0 + a1;
-      if (lane < 16) s.rhs[(k + 1) * R6_SZ + rr] = y;
+      // unconditional store (idle rows to the dump): no exec-mask branch in the
+      // loop, so the compiler's LDS wait at the next step is exact, not lgkmcnt(0)
+      *(lane < 16 ? &s.rhs[(k + 1) * R6_SZ + rr] : &s.dump[lane]) = y;
       go = gn;
     }
   }
@@ -724,7 +727,7 @@ __device__ __forceinline__ void r6_solve(R6Smem &s, MK &mark) {
     for (int i = 0; i < R6_NX; ++i) g[i] = F[go + i * R6_SZ];
     double x = a < R6_NX ? s.xs[R6_N * R6_SZ + a] : 0.0;
     double u = s.xs[(R6_N - 1) * R6_SZ + a];
-#pragma unroll 1
+#pragma unroll 2
     for (int k = R6_N - 1; k >= 0; --k) {
       const int gn = max(go - R6_NX * R6_SZ, 0);
       double a0 = u, a1 = 0.0;
@@ -744,7 +747,7 @@ __device__ __forceinline__ void r6_solve(R6Smem &s, MK &mark) {
       fmac_bc<12, false>(a0, x, g[12]); g[12] = F[gn + 12 * R6_SZ];
       fmac_bc<13, false>(a1, x, g[13]); g[13] = F[gn + 13 * R6_SZ];
       x = a0 + a1;
-      if (st) s.xs[k * R6_SZ + a] = x;
+      *(st ? &s.xs[k * R6_SZ + a] : &s.dump[lane]) = x;
       go = gn;
     }
   }
