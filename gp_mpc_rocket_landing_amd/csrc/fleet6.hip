@@ -245,8 +245,20 @@ struct R6Args {
 
 // ---------------------------------------------------------------------------
 // 1. termination rules + forward simulation with the GP mean
+// diagnostic phase cycles of the predict kernel's rollout 0 (GPMPC_R6_STAMPS=1)
+__device__ unsigned long long g_r6p_stamps[4];
+
+template <bool ST>
 __global__ __launch_bounds__(R6_PT) void k_r6_predict(R6Args a) {
   const int b = blockIdx.x, tid = threadIdx.x;
+  unsigned long long tl = 0;
+  auto mark = [&](int k) {
+    if (ST && b == 0 && tid == 0) {
+      const unsigned long long t = __builtin_amdgcn_s_memtime();
+      if (k >= 0) g_r6p_stamps[k] += t - tl;
+      tl = t;
+    }
+  };
   double *rec = a.rec + (int64_t)b * GPMPC_REC_LEN;
   if (rec[0] != 0.0) return;
   __shared__ double X[R6_N + 1][R6_NX];
@@ -279,10 +291,12 @@ __global__ __launch_bounds__(R6_PT) void k_r6_predict(R6Args a) {
   __syncthreads();
   if (s_out) return;
   const double *Ub = a.U + (int64_t)b * R6_N * R6_NU;
+  mark(-1);
   for (int k = 0; k < R6_N; ++k) {
     if (tid == 0)
       r6_features(X[k], Ub + k * R6_NU, a.gv.ls, a.gw.ls, zq[0], zq[1], &zn[0], &zn[1]);
     __syncthreads();
+    mark(0);
     // K*u alpha of both GPs: the expansion form of the gram kernel (same bits
     // per kernel value); 3 outputs each
     double acc[6] = {0, 0, 0, 0, 0, 0};
@@ -298,11 +312,13 @@ __global__ __launch_bounds__(R6_PT) void k_r6_predict(R6Args a) {
         for (int c = 0; c < 3; ++c) acc[3 * g + c] += kv * cf[(int64_t)c * M + i];
       }
     }
+    mark(1);
     for (int c = 0; c < 6; ++c)
       for (int o = 32; o > 0; o >>= 1) acc[c] += __shfl_xor(acc[c], o);
     if ((tid & 63) == 0)
       for (int c = 0; c < 6; ++c) red[tid >> 6][c] = acc[c];
     __syncthreads();
+    mark(2);
     if (tid == 0) {
       double gmk[6];
       for (int c = 0; c < 6; ++c) {
@@ -318,6 +334,7 @@ __global__ __launch_bounds__(R6_PT) void k_r6_predict(R6Args a) {
       for (int i = 0; i < R6_NX; ++i) X[k + 1][i] = xn[i];
     }
     __syncthreads();
+    mark(3);
   }
   for (int e = tid; e < (R6_N + 1) * R6_NX; e += R6_PT)
     a.Xp[(int64_t)b * (R6_N + 1) * R6_NX + e] = (&X[0][0])[e];
@@ -1421,7 +1438,8 @@ extern "C" int gpmpc_rollout6_step(gpmpc_rollout6 *r, int nsteps) {
   hipStream_t s = r->ctx->stream;
   const R6Args a = r6_args(r);
   for (int it = 0; it < nsteps; ++it) {
-    hipLaunchKernelGGL(k_r6_predict, dim3(r->B), dim3(R6_PT), 0, s, a);
+    if (r6_stamps_on()) hipLaunchKernelGGL(k_r6_predict<true>, dim3(r->B), dim3(R6_PT), 0, s, a);
+    else hipLaunchKernelGGL(k_r6_predict<false>, dim3(r->B), dim3(R6_PT), 0, s, a);
     if (r6_stamps_on()) hipLaunchKernelGGL(k_r6_control<true>, dim3(r->B), dim3(R6_T), sizeof(R6Smem), s, a);
     else hipLaunchKernelGGL(k_r6_control<false>, dim3(r->B), dim3(R6_T), sizeof(R6Smem), s, a);
     hipLaunchKernelGGL(k_r6_plant, dim3((r->B + 63) / 64), dim3(64), 0, s, a, r->B);
@@ -1470,6 +1488,10 @@ extern "C" int gpmpc_rollout6_destroy(gpmpc_rollout6 *r) {
       for (int k = 0; k < 12; ++k)
         fprintf(stderr, "r6 stamps %-14s %12llu cycles %5.1f%%\n", nm[k], h[k], tot ? 100.0 * h[k] / tot : 0.0);
     }
+    unsigned long long hp[4] = {0};
+    if (hipMemcpyFromSymbol(hp, HIP_SYMBOL(g_r6p_stamps), sizeof(hp)) == hipSuccess)
+      fprintf(stderr, "r6 predict stamps: features %llu kernel_rows %llu reduce %llu rk4 %llu\n", hp[0], hp[1],
+              hp[2], hp[3]);
   }
   delete r;
   return 0;
