@@ -658,7 +658,7 @@ def main():
             oc = all_rec[:, 0]
             out["outcomes"] = {str(int(c)): int(np.sum(oc == c)) for c in np.unique(oc)}
         out["qp_status"] = qp_status_histogram(fl)
-        if not args.no_chol:
+        if not args.no_chol and world == 1:  # single-GPU legs: the N > 1 runs keep to the metric
             try:
                 out["single_landing"] = single_landing_bench(ctx, gp)
                 out["gpmpc_loop"] = gpmpc_loop_bench(ctx, gp)
