@@ -66,7 +66,11 @@ class QPSettings(ctypes.Structure):
 
 class Rollout6Config(ctypes.Structure):
     _fields_ = [("horizon", ctypes.c_int), ("dt", ctypes.c_double), ("max_steps", ctypes.c_int),
-                ("qp", QPSettings), ("fitc_mean_as_written", ctypes.c_int)]
+                ("qp", QPSettings), ("fitc_mean_as_written", ctypes.c_int),
+                ("q_diag", ctypes.c_double * 14), ("p_diag", ctypes.c_double * 14),
+                ("r_diag", ctypes.c_double * 3), ("t_min", ctypes.c_double), ("t_max", ctypes.c_double),
+                ("tan_gamma_gs", ctypes.c_double), ("trust_x2", ctypes.c_double),
+                ("trust_u2", ctypes.c_double), ("use_gp_mean", ctypes.c_int), ("upright_target", ctypes.c_int)]
 
 
 class FleetConfig(ctypes.Structure):
@@ -107,6 +111,7 @@ _sig("gpmpc_fitc_fit", _c, _vp, _dp, _c, _dp, _c, _c, _dp, _c, _dp, ctypes.c_dou
      ctypes.c_double, ctypes.c_double, ctypes.POINTER(_vp), _dp, _dp, _dp, _dp)
 _sig("gpmpc_fitc_predict", _c, _vp, _vp, _dp, _c, _dp, _dp)
 _sig("gpmpc_fitc_destroy", _c, _vp)
+_sig("gpmpc_fitc_get_state", _c, _vp, _vp, _dp)
 _sig("gpmpc_qp_default_settings", None, ctypes.POINTER(QPSettings))
 _sig("gpmpc_qp_solve_batched", _c, _vp, _c, _c, _c, _c, _ip, _ip, _dp, _dp, _dp, _dp, _dp,
      ctypes.POINTER(QPSettings), _dp, _dp, _dp, _dp, _dp, _ip, _ip, _dp)
@@ -128,6 +133,9 @@ _sig("gpmpc_fleet_records_dev", _vp, _vp)
 _sig("gpmpc_fleet_destroy", _c, _vp)
 _sig("gpmpc_rollout6_default_config", None, ctypes.POINTER(Rollout6Config))
 _sig("gpmpc_rollout6_create", _c, _vp, _vp, _vp, ctypes.POINTER(Rollout6Config), _c, ctypes.POINTER(_vp))
+_sig("gpmpc_rollout6_create_exact", _c, _vp, _vp, _vp, ctypes.POINTER(Rollout6Config), _c, ctypes.POINTER(_vp))
+_sig("gpmpc_rollout6_solve", _c, _vp, _dp, _dp, _c, _c, ctypes.c_double, _dp, _dp, _ip, _ip, _ip, _ip)
+_sig("gpmpc_rollout6_set_state", _c, _vp, _dp, _dp, _dp)
 _sig("gpmpc_rollout6_reset", _c, _vp, _c, _c, _dp)
 _sig("gpmpc_rollout6_step", _c, _vp, _c)
 _sig("gpmpc_rollout6_read", _c, _vp, _dp, _dp)
@@ -146,7 +154,8 @@ EXPORTED = ["gpmpc_abi_version", "gpmpc_last_error", "gpmpc_ctx_create", "gpmpc_
             "gpmpc_syrk_batched_dev", "gpmpc_cov_propagate", "gpmpc_cov_propagate_dev",
             "gpmpc_fleet_records_dev", "gpmpc_fleet_destroy", "gpmpc_rollout6_default_config",
             "gpmpc_rollout6_create", "gpmpc_rollout6_reset", "gpmpc_rollout6_step", "gpmpc_rollout6_read",
-            "gpmpc_rollout6_get_state", "gpmpc_rollout6_destroy"]
+            "gpmpc_rollout6_get_state", "gpmpc_rollout6_destroy", "gpmpc_rollout6_create_exact",
+            "gpmpc_rollout6_solve", "gpmpc_rollout6_set_state", "gpmpc_fitc_get_state"]
 
 
 class HIPError(RuntimeError):
@@ -390,6 +399,12 @@ class FITCHandle:
         _chk(_L.gpmpc_fitc_predict(self.ctx.h, self.h, _d(Xq), p, _d(mean), _d(var)), "fitc_predict")
         return mean, var
 
+    def alpha(self):
+        """The fitted alpha (m x n_out), gpmpc_fitc_get_state."""
+        a = np.empty((self.m, self.n_out))
+        _chk(_L.gpmpc_fitc_get_state(self.ctx.h, self.h, _d(a)), "fitc_get_state")
+        return a
+
     def __del__(self):
         try:
             if getattr(self, "h", None):
@@ -412,6 +427,12 @@ def set_fields(struct, kw, nested=None):
     subn = _field_names(type(sub)) if sub is not None else set()
     for k, v in kw.items():
         if k in own and k != nested:
+            cur = getattr(struct, k)
+            if isinstance(cur, ctypes.Array):  # fixed-size array fields take a sequence
+                v = np.ravel(np.asarray(v, dtype=np.float64))
+                if v.size != len(cur):
+                    raise ValueError(f"{k} needs {len(cur)} values, got {v.size}")
+                v = type(cur)(*v.tolist())
             setattr(struct, k, v)
         elif k in subn:
             setattr(sub, k, v)

@@ -63,16 +63,31 @@
 #define R6_T_MAX 5.0
 
 __device__ __constant__ double r6_J[3] = {0.02 * 0.168, 1.0 * 0.168, 1.0 * 0.168};
-__device__ __constant__ double r6_Q[R6_NX] = {0.0, 10, 10, 10, 1, 1, 1, 0, 5, 5, 0, 0.1, 0.1, 0.1};
 
 struct gpmpc_rollout6 {
   gpmpc_ctx *ctx = nullptr;
-  gpmpc_fitc *gpv = nullptr, *gpw = nullptr;
+  GpView gv{}, gw{};
+  bool exact = false;  // the GP pair is exact (mean K* alpha over the training rows)
   gpmpc_rollout6_config cfg{};
   int B = 0;
   DevBuf x, U, Xp, gm, Xo, ysc, rho, rec, lin, pending;
   DevBuf betav, betaw;  // (L_uu^-T alpha)^T of each GP, 3 x M
+  DevBuf prm;           // problem data (R6_PRM doubles, r6_prm layout)
+  DevBuf xt, done, passes, qit, qst, xin;  // GPMPC.solve mode (gpmpc_rollout6_solve)
 };
+
+// problem data in device memory (read per thread with a dynamic index, so not a
+// by-value kernel argument): Q (14), P (14), R (3), T_min, T_max, tan gamma_gs,
+// trust x / u radii
+#define R6_PQ 0
+#define R6_PP 14
+#define R6_PR 28
+#define R6_PTMIN 31
+#define R6_PTMAX 32
+#define R6_PTAN 33
+#define R6_PTRX 34
+#define R6_PTRU 35
+#define R6_PRM 36
 
 extern "C" void gpmpc_rollout6_default_config(gpmpc_rollout6_config *c) {
   c->horizon = R6_N;   // BASELINE configs[4]: N = 30
@@ -80,6 +95,18 @@ extern "C" void gpmpc_rollout6_default_config(gpmpc_rollout6_config *c) {
   c->max_steps = 300;
   gpmpc_qp_default_settings(&c->qp);   // osqp_rti.py:54-60 settings, as the 3-DoF path
   c->fitc_mean_as_written = 0;         // FITC posterior mean (SURVEY D1 fixed, flag 1 = as written)
+  // CostWeights (cost_functions.py:39-98): Q = diag(w_mass, w_pos x3, w_vel x3, 0, w_att x2, 0,
+  // w_omega x3), R = w_thrust I, P = terminal_weight Q
+  const double q[R6_NX] = {0.0, 10, 10, 10, 1, 1, 1, 0, 5, 5, 0, 0.1, 0.1, 0.1};
+  for (int i = 0; i < R6_NX; ++i) { c->q_diag[i] = q[i]; c->p_diag[i] = 10.0 * q[i]; }
+  for (int i = 0; i < R6_NU; ++i) c->r_diag[i] = 0.01;
+  c->t_min = R6_T_MIN;                 // ConstraintParams (constraints.py:35-50)
+  c->t_max = R6_T_MAX;
+  c->tan_gamma_gs = 0.5773502691896257;  // np.tan(np.deg2rad(30.0))
+  c->trust_x2 = 10.0;                  // gp_mpc.py:432-435
+  c->trust_u2 = 5.0;
+  c->use_gp_mean = 1;
+  c->upright_target = 0;
 }
 
 // beta^T = alpha^T L_uu^-1 (3 x M): the FITC posterior mean is K*u beta.
@@ -241,6 +268,14 @@ struct R6Args {
   GpView gv, gw;
   int Mv, Mw;
   const double *cv, *cw;  // mean coefficients (3 x M): beta^T, or alpha^T as written
+  const double *prm;      // problem data (R6_PRM, r6 layout above)
+  int use_gp, upright;
+  // GPMPC.solve mode (gpmpc_rollout6_solve): 0 = Monte-Carlo rollout step; 1 = first
+  // pass (forward simulation of U); 2 = later pass (GP means and Jacobians at the plan)
+  int mode;
+  double sqp_tol;
+  const double *xt;       // per-rollout target (B x 14)
+  int *done, *passes, *qit, *qst;
 };
 
 // ---------------------------------------------------------------------------
@@ -260,15 +295,22 @@ __global__ __launch_bounds__(R6_PT) void k_r6_predict(R6Args a) {
     }
   };
   double *rec = a.rec + (int64_t)b * GPMPC_REC_LEN;
-  if (rec[0] != 0.0) return;
+  if (a.mode == 0 ? rec[0] != 0.0 : a.done[b] != 0) return;
   __shared__ double X[R6_N + 1][R6_NX];
   __shared__ double zq[2][16], zn[2];
   __shared__ double red[R6_PT / 64][6];
   __shared__ int s_out;
   const double dt = a.dt;
-  if (tid < R6_NX) X[0][tid] = a.x[(int64_t)b * R6_NX + tid];
+  const bool relin = a.mode == 2;  // a later GPMPC.solve pass: X_pred = the last plan
+  if (relin) {
+    for (int e = tid; e < (R6_N + 1) * R6_NX; e += R6_PT)
+      (&X[0][0])[e] = a.Xo[(int64_t)b * (R6_N + 1) * R6_NX + e];
+  } else if (tid < R6_NX) {
+    X[0][tid] = a.x[(int64_t)b * R6_NX + tid];
+  }
+  if (tid == 0) s_out = 0;
   __syncthreads();
-  if (tid == 0) {  // monte_carlo.py:458-488 on [m, r, v]; then any non-finite 6-DoF state
+  if (a.mode == 0 && tid == 0) {  // monte_carlo.py:458-488 on [m, r, v]; then any non-finite 6-DoF state
     const double *x = X[0];
     const double m0 = rec[13];
     bool div7 = false, div = false;
@@ -293,14 +335,14 @@ __global__ __launch_bounds__(R6_PT) void k_r6_predict(R6Args a) {
   const double *Ub = a.U + (int64_t)b * R6_N * R6_NU;
   mark(-1);
   for (int k = 0; k < R6_N; ++k) {
-    if (tid == 0)
+    if (tid == 0 && a.use_gp)
       r6_features(X[k], Ub + k * R6_NU, a.gv.ls, a.gw.ls, zq[0], zq[1], &zn[0], &zn[1]);
     __syncthreads();
     mark(0);
     // K*u alpha of both GPs: the expansion form of the gram kernel (same bits
     // per kernel value); 3 outputs each
     double acc[6] = {0, 0, 0, 0, 0, 0};
-    for (int g = 0; g < 2; ++g) {
+    for (int g = 0; g < (a.use_gp ? 2 : 0); ++g) {
       const GpView &v = g ? a.gw : a.gv;
       const int M = g ? a.Mw : a.Mv, d = g ? 12 : 13;
       for (int i = tid; i < M; i += R6_PT) {
@@ -325,13 +367,15 @@ __global__ __launch_bounds__(R6_PT) void k_r6_predict(R6Args a) {
         double s = 0.0;
         for (int w = 0; w < R6_PT / 64; ++w) s += red[w][c];
         const GpView &v = c < 3 ? a.gv : a.gw;
-        gmk[c] = s * v.ystd[c % 3] + v.ymean[c % 3];
+        gmk[c] = a.use_gp ? s * v.ystd[c % 3] + v.ymean[c % 3] : 0.0;
         a.gm[((int64_t)b * R6_N + k) * 6 + c] = gmk[c];
       }
-      double xn[R6_NX];
-      r6_step(X[k], Ub + k * R6_NU, dt, xn);
-      for (int i = 0; i < 3; ++i) { xn[4 + i] += gmk[i] * dt; xn[11 + i] += gmk[3 + i] * dt; }
-      for (int i = 0; i < R6_NX; ++i) X[k + 1][i] = xn[i];
+      if (!relin) {  // _predict_with_gp (gp_mpc.py:139-175)
+        double xn[R6_NX];
+        r6_step(X[k], Ub + k * R6_NU, dt, xn);
+        for (int i = 0; i < 3; ++i) { xn[4 + i] += gmk[i] * dt; xn[11 + i] += gmk[3 + i] * dt; }
+        for (int i = 0; i < R6_NX; ++i) X[k + 1][i] = xn[i];
+      }
     }
     __syncthreads();
     mark(3);
@@ -934,7 +978,7 @@ __global__ __launch_bounds__(R6_T) void k_r6_control(R6Args a) {
   };
   mark(-1);
   double *rec = a.rec + (int64_t)b * GPMPC_REC_LEN;
-  if (rec[0] != 0.0) return;
+  if (a.mode == 0 ? rec[0] != 0.0 : a.done[b] != 0) return;
   extern __shared__ double smem_raw[];
   R6Smem &s = *reinterpret_cast<R6Smem *>(smem_raw);
   const double dt = a.dt;
@@ -944,13 +988,22 @@ __global__ __launch_bounds__(R6_T) void k_r6_control(R6Args a) {
   const double *gmb = a.gm + (int64_t)b * R6_N * 6;
   double *ysc = a.ysc + (int64_t)b * R6_M;
   const double *x0 = a.x + (int64_t)b * R6_NX;
-  // incremental target (monte_carlo.py:497-500), upright and at rest
+  const double *prm = a.prm;
+  // the target: GPMPC.solve's x_target, or in a rollout step the incremental
+  // target of monte_carlo.py:497-500 (x copied, v = 0, altitude - 2 m, floor
+  // 0.5 m; optionally upright and at rest)
   double xr[R6_NX];
-  for (int i = 0; i < R6_NX; ++i) xr[i] = x0[i];
-  xr[4] = xr[5] = xr[6] = 0.0;
-  xr[1] = fmax(0.5, x0[1] - 2.0);
-  xr[7] = 1.0; xr[8] = xr[9] = xr[10] = 0.0;
-  xr[11] = xr[12] = xr[13] = 0.0;
+  if (a.mode) {
+    for (int i = 0; i < R6_NX; ++i) xr[i] = a.xt[(int64_t)b * R6_NX + i];
+  } else {
+    for (int i = 0; i < R6_NX; ++i) xr[i] = x0[i];
+    xr[4] = xr[5] = xr[6] = 0.0;
+    xr[1] = fmax(0.5, x0[1] - 2.0);
+    if (a.upright) {
+      xr[7] = 1.0; xr[8] = xr[9] = xr[10] = 0.0;
+      xr[11] = xr[12] = xr[13] = 0.0;
+    }
+  }
   // ---- the linearisation (-[A_d | B_d] per stage, k_r6_predict) into the staging area
   {
     const double *lin = a.lin + (int64_t)b * R6_N * R6_NX * R6_SZ;
@@ -977,14 +1030,16 @@ __global__ __launch_bounds__(R6_T) void k_r6_control(R6Args a) {
       double xw, wq;
       if (i < R6_NX) {
         xw = Xb[k * R6_NX + i];
-        wq = r6_Q[i] * (k == R6_N ? 10.0 : 1.0);
+        wq = prm[(k == R6_N ? R6_PP : R6_PQ) + i];
         W.P = wq; W.q = wq * (xw - xr[i]);
-        W.lb = -sqrt(10.0); W.ub = sqrt(10.0);
+        const double tr = sqrt(prm[R6_PTRX]);
+        W.lb = -tr; W.ub = tr;
       } else {
         const double ub = Ub[k * R6_NU + i - R6_NX];
-        W.P = 0.01; W.q = 0.01 * ub;
-        W.lb = fmax(-sqrt(5.0), -R6_T_MAX - ub);
-        W.ub = fmin(sqrt(5.0), R6_T_MAX - ub);
+        const double rr = prm[R6_PR + i - R6_NX], tr = sqrt(prm[R6_PTRU]), tmax = prm[R6_PTMAX];
+        W.P = rr; W.q = rr * ub;
+        W.lb = fmax(-tr, -tmax - ub);
+        W.ub = fmin(tr, tmax - ub);
       }
       W.Ab = 1.0;
       W.x = 0.0;  // warm start dz = 0
@@ -1002,10 +1057,10 @@ __global__ __launch_bounds__(R6_T) void k_r6_control(R6Args a) {
         const double *u = Ub + g * R6_NU;
         const double tm = sqrt((u[0] * u[0] + u[1] * u[1]) + u[2] * u[2]);
         W.gA[0] = u[0] / tm; W.gA[1] = u[1] / tm; W.gA[2] = u[2] / tm;
-        W.gl = R6_T_MIN - tm; W.gu = INFINITY; W.gn = 3;
+        W.gl = prm[R6_PTMIN] - tm; W.gu = INFINITY; W.gn = 3;
       } else {
         const int gg = g - R6_MT, k = 1 + gg / 4, c = gg % 4;
-        const double tg = 0.5773502691896257;  // np.tan(np.deg2rad(30.0)), gamma_gs
+        const double tg = prm[R6_PTAN];  // np.tan(gamma_gs)
         const double rx = Xb[k * R6_NX + 1], rc = Xb[k * R6_NX + (c < 2 ? 2 : 3)];
         const double sg = (c & 1) ? 1.0 : -1.0;
         W.gA[0] = tg; W.gA[1] = sg; W.gA[2] = 0.0;
@@ -1018,7 +1073,7 @@ __global__ __launch_bounds__(R6_T) void k_r6_control(R6Args a) {
         Q.A[0] = 1.0;
 #pragma unroll
         for (int e = 1; e <= R6_SZ; ++e) Q.A[e] = 0.0;
-        Q.ur = 0.0;
+        Q.ur = x0[Q.r] - Xb[Q.r];  // dX_0 = x0 - X_nom[0] (gp_mpc.py:402)
       } else {
 #pragma unroll
         for (int e = 0; e < R6_SZ; ++e) Q.A[e] = s.G[(Q.k * R6_NX + Q.i) * R6_SZ + e];
@@ -1255,15 +1310,21 @@ __global__ __launch_bounds__(R6_T) void k_r6_control(R6Args a) {
   __syncthreads();
   double *Xo = a.Xo + (int64_t)b * (R6_N + 1) * R6_NX;
   double *Uw = a.U + (int64_t)b * R6_N * R6_NU;
+  double chg[2] = {0.0, 0.0};  // max |X_new - X_pred|, max |U_new - U_pred| (gp_mpc.py:337-338)
   if (has) {
     for (int e = tid; e < (R6_N + 1) * R6_NX; e += R6_T) {
       const int k = e / R6_NX, i = e - k * R6_NX;
-      Xo[e] = Xb[e] + s.xs[k * R6_SZ + i];
+      const double xo = Xb[e] + s.xs[k * R6_SZ + i];
+      Xo[e] = xo;
+      const double d = fabs(xo - Xb[e]);
+      if (!(d <= chg[0])) chg[0] = d != d ? INFINITY : d;  // a NaN never converges
     }
     double un = 0.0;
     if (tid < R6_N * R6_NU) {
       const int k = tid / R6_NU, i = tid - k * R6_NU;
       un = Ub[tid] + s.xs[k * R6_SZ + R6_NX + i];
+      const double d = fabs(un - Ub[tid]);
+      chg[1] = d != d ? INFINITY : d;
     }
     __syncthreads();  // every thread read U before it is overwritten
     if (tid < R6_N * R6_NU) Uw[tid] = un;
@@ -1273,8 +1334,21 @@ __global__ __launch_bounds__(R6_T) void k_r6_control(R6Args a) {
       if (V[h].gok) ysc[R6_MD + R6_NV + V[h].j] = V[h].gy;
     }
     __syncthreads();
+  } else if (a.mode) {
+    // _solve_qp's fallback (gp_mpc.py:478-482): the nominal trajectory
+    for (int e = tid; e < (R6_N + 1) * R6_NX; e += R6_T) Xo[e] = Xb[e];
   }
-  if (tid == 0) {
+  if (a.mode) r6_max<2>(chg, s.red);  // a.mode is uniform over the launch
+  if (tid == 0 && a.mode) {  // GPMPC.solve pass bookkeeping
+    a.passes[b] += 1;
+    a.qit[b] += res.iter;
+    a.qst[b] = res.factor_fail ? -100 : res.status;
+    a.done[b] = (chg[0] < a.sqp_tol && chg[1] < a.sqp_tol) ? 1 : 0;  // a failed QP: X_new = X_pred
+    rec[11] += res.iter;
+    rec[12] += (res.status == 1 && !res.factor_fail) ? 1.0 : 0.0;
+    rec[14] = res.factor_fail ? -100 : res.status;
+    if (has) { a.rho[b] = s.rho_s; rec[15] = s.rho_s; }
+  } else if (tid == 0) {
     if (!has) {  // MPCSolution without a solution -> DIVERGENCE
       const double *x = a.x + (int64_t)b * R6_NX;
       rec[0] = 6;
@@ -1341,42 +1415,62 @@ __global__ void k_r6_reset(int first, int count, const double *__restrict__ x0, 
 }
 
 // ---------------------------------------------------------------------------
-extern "C" int gpmpc_rollout6_create(gpmpc_ctx *ctx, gpmpc_fitc *gp_v, gpmpc_fitc *gp_w,
-                                     const gpmpc_rollout6_config *cfg, int batch, gpmpc_rollout6 **out) {
-  GPMPC_CHECK_ARG(ctx && gp_v && gp_w && cfg && out && batch > 0);
-  const GpView gv = fitc_view(gp_v), gw = fitc_view(gp_w);
+static int r6_create(gpmpc_ctx *ctx, const GpView &gv, const GpView &gw, bool exact,
+                     const gpmpc_rollout6_config *cfg, int batch, gpmpc_rollout6 **out) {
+  GPMPC_CHECK_ARG(ctx && cfg && out && batch > 0);
   if (gv.d != 13 || gw.d != 12 || gv.n_out != 3 || gw.n_out != 3 || gv.kind != GPMPC_SE_ARD ||
       gw.kind != GPMPC_SE_ARD) {
-    gpmpc_set_error("rollout6: expects the StructuredRocketGP FITC pair (13 / 12 features, 3 outputs, SE-ARD)");
+    gpmpc_set_error("rollout6: expects the StructuredRocketGP pair (13 / 12 features, 3 outputs, SE-ARD)");
     return -2;
   }
   if (cfg->horizon != R6_N) {
     gpmpc_set_error("rollout6: horizon must be %d (BASELINE configs[4])", R6_N);
     return -2;
   }
+  for (int i = 0; i < R6_NX; ++i)
+    if (!(cfg->q_diag[i] >= 0.0) || !(cfg->p_diag[i] >= 0.0)) {
+      gpmpc_set_error("rollout6: cost weights must be non-negative");
+      return -2;
+    }
+  if (!(cfg->t_max > 0.0) || !(cfg->trust_x2 > 0.0) || !(cfg->trust_u2 > 0.0)) {
+    gpmpc_set_error("rollout6: t_max and the trust radii must be positive");
+    return -2;
+  }
   GPMPC_HIP(hipSetDevice(ctx->device));
   auto *r = new gpmpc_rollout6();
-  r->ctx = ctx; r->gpv = gp_v; r->gpw = gp_w; r->cfg = *cfg; r->B = batch;
+  r->ctx = ctx; r->gv = gv; r->gw = gw; r->exact = exact; r->cfg = *cfg; r->B = batch;
   const size_t B = batch;
   if (r->x.alloc(sizeof(double) * B * R6_NX) || r->U.alloc(sizeof(double) * B * R6_N * R6_NU) ||
       r->Xp.alloc(sizeof(double) * B * (R6_N + 1) * R6_NX) || r->gm.alloc(sizeof(double) * B * R6_N * 6) ||
       r->Xo.alloc(sizeof(double) * B * (R6_N + 1) * R6_NX) || r->ysc.alloc(sizeof(double) * B * R6_M) ||
       r->rho.alloc(sizeof(double) * B) || r->rec.alloc(sizeof(double) * B * GPMPC_REC_LEN) ||
       r->lin.alloc(sizeof(double) * B * R6_N * R6_NX * R6_SZ) || r->pending.alloc(sizeof(int) * B) ||
-      r->betav.alloc(sizeof(double) * 3 * gv.n) || r->betaw.alloc(sizeof(double) * 3 * gw.n)) {
+      r->betav.alloc(sizeof(double) * 3 * gv.n) || r->betaw.alloc(sizeof(double) * 3 * gw.n) ||
+      r->prm.alloc(sizeof(double) * R6_PRM) || r->xt.alloc(sizeof(double) * B * R6_NX) ||
+      r->xin.alloc(sizeof(double) * B * R6_NX) || r->done.alloc(sizeof(int) * B) ||
+      r->passes.alloc(sizeof(int) * B) || r->qit.alloc(sizeof(int) * B) || r->qst.alloc(sizeof(int) * B)) {
     delete r;
     gpmpc_set_error("rollout6: out of device memory");
     return -1;
   }
+  double prm[R6_PRM];
+  for (int i = 0; i < R6_NX; ++i) { prm[R6_PQ + i] = cfg->q_diag[i]; prm[R6_PP + i] = cfg->p_diag[i]; }
+  for (int i = 0; i < R6_NU; ++i) prm[R6_PR + i] = cfg->r_diag[i];
+  prm[R6_PTMIN] = cfg->t_min; prm[R6_PTMAX] = cfg->t_max; prm[R6_PTAN] = cfg->tan_gamma_gs;
+  prm[R6_PTRX] = cfg->trust_x2; prm[R6_PTRU] = cfg->trust_u2;
+  hipMemcpyAsync(r->prm.p, prm, sizeof(prm), hipMemcpyHostToDevice, ctx->stream);
   std::vector<double> rc(B * GPMPC_REC_LEN, 0.0);
   for (size_t i = 0; i < B; ++i) rc[i * GPMPC_REC_LEN] = -1.0;  // not started until reset
   hipMemcpyAsync(r->rec.p, rc.data(), sizeof(double) * rc.size(), hipMemcpyHostToDevice, ctx->stream);
   hipMemsetAsync(r->Xo.p, 0, sizeof(double) * B * (R6_N + 1) * R6_NX, ctx->stream);
   hipMemsetAsync(r->pending.p, 0, sizeof(int) * B, ctx->stream);
-  hipLaunchKernelGGL(k_fitc_beta, dim3((gv.n + 255) / 256, 3), dim3(256), 0, ctx->stream, gv.n, gv.W,
-                     gv.alphaT, r->betav.as<double>());
-  hipLaunchKernelGGL(k_fitc_beta, dim3((gw.n + 255) / 256, 3), dim3(256), 0, ctx->stream, gw.n, gw.W,
-                     gw.alphaT, r->betaw.as<double>());
+  hipMemsetAsync(r->done.p, 0, sizeof(int) * B, ctx->stream);
+  if (!exact) {  // beta^T = alpha^T L_uu^-1: the FITC posterior mean's coefficients
+    hipLaunchKernelGGL(k_fitc_beta, dim3((gv.n + 255) / 256, 3), dim3(256), 0, ctx->stream, gv.n, gv.W,
+                       gv.alphaT, r->betav.as<double>());
+    hipLaunchKernelGGL(k_fitc_beta, dim3((gw.n + 255) / 256, 3), dim3(256), 0, ctx->stream, gw.n, gw.W,
+                       gw.alphaT, r->betaw.as<double>());
+  }
   static bool attr = [] {
     (void)hipFuncSetAttribute((const void *)k_r6_control<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               sizeof(R6Smem));
@@ -1391,6 +1485,18 @@ extern "C" int gpmpc_rollout6_create(gpmpc_ctx *ctx, gpmpc_fitc *gp_v, gpmpc_fit
   GPMPC_HIP(hipStreamSynchronize(ctx->stream));
   *out = r;
   return 0;
+}
+
+extern "C" int gpmpc_rollout6_create(gpmpc_ctx *ctx, gpmpc_fitc *gp_v, gpmpc_fitc *gp_w,
+                                     const gpmpc_rollout6_config *cfg, int batch, gpmpc_rollout6 **out) {
+  GPMPC_CHECK_ARG(gp_v && gp_w);
+  return r6_create(ctx, fitc_view(gp_v), fitc_view(gp_w), false, cfg, batch, out);
+}
+
+extern "C" int gpmpc_rollout6_create_exact(gpmpc_ctx *ctx, gpmpc_gp *gp_v, gpmpc_gp *gp_w,
+                                           const gpmpc_rollout6_config *cfg, int batch, gpmpc_rollout6 **out) {
+  GPMPC_CHECK_ARG(gp_v && gp_w);
+  return r6_create(ctx, gp_view(gp_v), gp_view(gp_w), true, cfg, batch, out);
 }
 
 extern "C" int gpmpc_rollout6_reset(gpmpc_rollout6 *r, int first, int count, const double *x0) {
@@ -1408,6 +1514,27 @@ extern "C" int gpmpc_rollout6_reset(gpmpc_rollout6 *r, int first, int count, con
   return 0;
 }
 
+// GPMPC.solve: x0 / x_target already in x / xt; cold = hover guess + fresh ADMM state
+__global__ void k_r6_solve_begin(R6Args a, int cold, double rho0) {
+  const int b = blockIdx.x;
+  const double m0 = a.x[(int64_t)b * R6_NX];
+  if (cold == 1) {
+    // gp_mpc.py:271-275 as intended: [0, 0, m0 g0] at every stage (as written it reads
+    // X_pred[k, 0] before the simulation has filled it, i.e. zero thrust for k >= 1,
+    // whose thrust-magnitude rows have no linearisation)
+    for (int e = threadIdx.x; e < R6_N * R6_NU; e += blockDim.x)
+      a.U[(int64_t)b * R6_N * R6_NU + e] = (e % R6_NU == 2) ? m0 * 1.0 : 0.0;
+  }
+  if (cold)
+    for (int r = threadIdx.x; r < R6_M; r += blockDim.x) a.ysc[(int64_t)b * R6_M + r] = 0.0;
+  if (threadIdx.x == 0) {
+    if (cold) a.rho[b] = rho0;
+    a.done[b] = 0; a.passes[b] = 0; a.qit[b] = 0; a.qst[b] = -10;
+    double *rec = a.rec + (int64_t)b * GPMPC_REC_LEN;
+    rec[11] = 0.0; rec[12] = 0.0;
+  }
+}
+
 static R6Args r6_args(gpmpc_rollout6 *r) {
   R6Args a;
   a.st = to_dev(r->cfg.qp);
@@ -1417,10 +1544,19 @@ static R6Args r6_args(gpmpc_rollout6 *r) {
   a.gm = r->gm.as<double>(); a.Xo = r->Xo.as<double>(); a.ysc = r->ysc.as<double>();
   a.rho = r->rho.as<double>(); a.rec = r->rec.as<double>();
   a.lin = r->lin.as<double>(); a.pending = r->pending.as<int>();
-  a.gv = fitc_view(r->gpv); a.gw = fitc_view(r->gpw);
+  a.gv = r->gv; a.gw = r->gw;
   a.Mv = a.gv.n; a.Mw = a.gw.n;
-  a.cv = r->cfg.fitc_mean_as_written ? a.gv.alphaT : r->betav.as<double>();
-  a.cw = r->cfg.fitc_mean_as_written ? a.gw.alphaT : r->betaw.as<double>();
+  const bool as_written = r->exact || r->cfg.fitc_mean_as_written;
+  a.cv = as_written ? a.gv.alphaT : r->betav.as<double>();
+  a.cw = as_written ? a.gw.alphaT : r->betaw.as<double>();
+  a.prm = r->prm.as<double>();
+  a.use_gp = r->cfg.use_gp_mean != 0;
+  a.upright = r->cfg.upright_target != 0;
+  a.mode = 0;
+  a.sqp_tol = 0.0;
+  a.xt = r->xt.as<double>();
+  a.done = r->done.as<int>(); a.passes = r->passes.as<int>();
+  a.qit = r->qit.as<int>(); a.qst = r->qst.as<int>();
   return a;
 }
 
@@ -1448,6 +1584,34 @@ extern "C" int gpmpc_rollout6_step(gpmpc_rollout6 *r, int nsteps) {
   return 0;
 }
 
+extern "C" int gpmpc_rollout6_solve(gpmpc_rollout6 *r, const double *x0, const double *x_target, int cold,
+                                    int max_sqp_iter, double sqp_tol, double *X, double *U, int *passes,
+                                    int *converged, int *qp_status, int *qp_iters) {
+  GPMPC_CHECK_ARG(r && x0 && x_target && max_sqp_iter >= 1 && sqp_tol >= 0.0 && cold >= 0 && cold <= 2);
+  GPMPC_HIP(hipSetDevice(r->ctx->device));
+  hipStream_t s = r->ctx->stream;
+  const size_t B = r->B;
+  GPMPC_HIP(hipMemcpyAsync(r->x.p, x0, sizeof(double) * B * R6_NX, hipMemcpyHostToDevice, s));
+  GPMPC_HIP(hipMemcpyAsync(r->xt.p, x_target, sizeof(double) * B * R6_NX, hipMemcpyHostToDevice, s));
+  R6Args a = r6_args(r);
+  a.sqp_tol = sqp_tol;
+  hipLaunchKernelGGL(k_r6_solve_begin, dim3(r->B), dim3(256), 0, s, a, cold, r->cfg.qp.rho);
+  for (int p = 1; p <= max_sqp_iter; ++p) {  // passes of converged rollouts exit at once
+    a.mode = p == 1 ? 1 : 2;
+    hipLaunchKernelGGL(k_r6_predict<false>, dim3(r->B), dim3(R6_PT), 0, s, a);
+    hipLaunchKernelGGL(k_r6_control<false>, dim3(r->B), dim3(R6_T), sizeof(R6Smem), s, a);
+  }
+  GPMPC_HIP(hipGetLastError());
+  if (X) GPMPC_HIP(hipMemcpyAsync(X, r->Xo.p, sizeof(double) * B * (R6_N + 1) * R6_NX, hipMemcpyDeviceToHost, s));
+  if (U) GPMPC_HIP(hipMemcpyAsync(U, r->U.p, sizeof(double) * B * R6_N * R6_NU, hipMemcpyDeviceToHost, s));
+  if (passes) GPMPC_HIP(hipMemcpyAsync(passes, r->passes.p, sizeof(int) * B, hipMemcpyDeviceToHost, s));
+  if (converged) GPMPC_HIP(hipMemcpyAsync(converged, r->done.p, sizeof(int) * B, hipMemcpyDeviceToHost, s));
+  if (qp_status) GPMPC_HIP(hipMemcpyAsync(qp_status, r->qst.p, sizeof(int) * B, hipMemcpyDeviceToHost, s));
+  if (qp_iters) GPMPC_HIP(hipMemcpyAsync(qp_iters, r->qit.p, sizeof(int) * B, hipMemcpyDeviceToHost, s));
+  GPMPC_HIP(hipStreamSynchronize(s));
+  return 0;
+}
+
 extern "C" int gpmpc_rollout6_read(gpmpc_rollout6 *r, double *records, double *x) {
   GPMPC_CHECK_ARG(r);
   hipStream_t s = r->ctx->stream;
@@ -1472,6 +1636,18 @@ extern "C" int gpmpc_rollout6_get_state(gpmpc_rollout6 *r, double *U, double *X_
   if (gp_mean) GPMPC_HIP(hipMemcpyAsync(gp_mean, r->gm.p, sizeof(double) * B * R6_N * 6, hipMemcpyDeviceToHost, s));
   if (y_scaled) GPMPC_HIP(hipMemcpyAsync(y_scaled, r->ysc.p, sizeof(double) * B * R6_M, hipMemcpyDeviceToHost, s));
   if (rho) GPMPC_HIP(hipMemcpyAsync(rho, r->rho.p, sizeof(double) * B, hipMemcpyDeviceToHost, s));
+  GPMPC_HIP(hipStreamSynchronize(s));
+  return 0;
+}
+
+extern "C" int gpmpc_rollout6_set_state(gpmpc_rollout6 *r, const double *U, const double *y_scaled,
+                                        const double *rho) {
+  GPMPC_CHECK_ARG(r);
+  hipStream_t s = r->ctx->stream;
+  const size_t B = r->B;
+  if (U) GPMPC_HIP(hipMemcpyAsync(r->U.p, U, sizeof(double) * B * R6_N * R6_NU, hipMemcpyHostToDevice, s));
+  if (y_scaled) GPMPC_HIP(hipMemcpyAsync(r->ysc.p, y_scaled, sizeof(double) * B * R6_M, hipMemcpyHostToDevice, s));
+  if (rho) GPMPC_HIP(hipMemcpyAsync(r->rho.p, rho, sizeof(double) * B, hipMemcpyHostToDevice, s));
   GPMPC_HIP(hipStreamSynchronize(s));
   return 0;
 }

@@ -443,6 +443,19 @@ extern "C" int gpmpc_gp_destroy(gpmpc_gp *gp) {
 }
 
 // ---- internal accessor for the fleet ----------------------------------------
+extern "C" int gpmpc_fitc_get_state(gpmpc_ctx *ctx, gpmpc_fitc *gp, double *alpha) {
+  GPMPC_CHECK_ARG(ctx && gp && alpha);
+  GPMPC_HIP(hipSetDevice(ctx->device));
+  const int m = gp->core.n, no = gp->core.n_out;
+  std::vector<double> aT((size_t)no * m);
+  GPMPC_HIP(hipMemcpyAsync(aT.data(), gp->core.alphaT.p, sizeof(double) * no * m, hipMemcpyDeviceToHost,
+                           ctx->stream));
+  GPMPC_HIP(hipStreamSynchronize(ctx->stream));
+  for (int i = 0; i < m; ++i)
+    for (int c = 0; c < no; ++c) alpha[(size_t)i * no + c] = aT[(size_t)c * m + i];
+  return 0;
+}
+
 GpView gp_view(const gpmpc_gp *gp) {
   const GpCore &g = gp->core;
   return GpView{g.kind, g.n, g.d, g.n_out, g.sigma2, g.iso_scale, g.ls.as<double>(),

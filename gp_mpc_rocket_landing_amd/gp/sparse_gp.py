@@ -184,6 +184,12 @@ class MultiOutputSparseGP:
     def predict_f(self, X):
         return self.predict(X)
 
+    @property
+    def device_handle(self):
+        """The shared device FITC GP (None before fit or with share_inducing=False)."""
+        d = self.gps[0]._dev
+        return d.h if isinstance(d, _SharedFITC) and all(g._dev is d for g in self.gps) else None
+
     def update(self, X_new, Y_new) -> "MultiOutputSparseGP":
         Y_new = np.atleast_2d(Y_new)
         if Y_new.shape[1] != self.output_dim:

@@ -35,6 +35,7 @@ from typing import Optional
 import numpy as np
 
 from .. import _lib
+from .. import rollouts6 as _r6
 from .constraints import ConstraintParams, TightenedConstraints
 from .cost_functions import CostWeights
 from .nominal_mpc import MPCConfig, MPCSolution, _SQPBase, trajectory_cost
@@ -54,11 +55,22 @@ class GPMPCConfig(MPCConfig):
 
 
 class GPMPC(_SQPBase):
+    """``GPMPC(dynamics, gp_model, config, constraint_params, cost_weights)``.
+
+    A 14-state plant (``dynamics.n_state == 14``, the reference's own use with
+    StructuredRocketGP) constructs the 6-DoF device controller, GPMPC6DoF; a
+    7-state plant the 3-DoF adapter below."""
+
+    def __new__(cls, dynamics=None, *args, **kwargs):
+        if cls is GPMPC and getattr(dynamics, "n_state", 7) == 14:
+            return super().__new__(GPMPC6DoF)
+        return super().__new__(cls)
+
     def __init__(self, dynamics, gp_model, config: Optional[GPMPCConfig] = None,
                  constraint_params=None, cost_weights=None, ctx=None):
         n_state = getattr(dynamics, "n_state", 7)
         if n_state != 7:
-            raise NotImplementedError("this GPMPC runs the 3-DoF model (n_x = 7)")
+            raise NotImplementedError("the 3-DoF adapter runs n_x = 7; 14 states go to GPMPC6DoF")
         super().__init__(dynamics, config or GPMPCConfig(), ctx=ctx)
         self.gp = gp_model
         self.constraint_params = constraint_params or ConstraintParams()
@@ -154,6 +166,157 @@ class GPMPC(_SQPBase):
         if k is None:
             return None if self._last_var is None else self._last_var.copy()
         return None if self.last_uncertainty is None else self.last_uncertainty.covariances[k].copy()
+
+
+class GPMPC6DoF(GPMPC):
+    """The reference's own GPMPC: the 14-state rocket with StructuredRocketGP
+    (gp_mpc.py:66-497), one control solve on the device (csrc/fleet6.hip
+    through gpmpc_rollout6_solve, a batch of one).
+
+    ``solve(x0, x_target)`` = gp_mpc.py:229-369: forward simulation of the
+    warm-start controls with the GP mean (RK4 of nominal_mpc.py:163-203 +
+    [.., d_v dt, .., d_w dt]), then up to ``max_sqp_iter`` passes of
+    linearise (A_d = I + A_c dt, B_d = B_c dt) -> c_k = GP mean dt -> QP
+    subproblem (:394-460) -> plan, stopping when max|dX|, max|dU| < sqp_tol.
+    The QP subproblem is the reference's with its quadratic constraints made
+    linear (thrust ball -> box, |u| >= T_min linearised at
+    U_nom, glide-slope cone -> 4 half-planes, trust balls -> boxes), solved by
+    the OSQP-0.6 ADMM (osqp_rti.py settings: the reference's IPOPT/CasADi are
+    absent) with OSQP's persistent rho / duals across passes and calls.
+
+    Defaults and semantics as the 3-DoF adapter (D14): ``max_sqp_iter = 1``
+    (the RTI control step; success = the ADMM returned a solution); ``> 1``
+    runs the reference loop (success = converged, status "Converged" / "Max
+    iterations"; a QP without a solution returns the nominal, which the
+    reference's loop counts as converged, gp_mpc.py:478-482 + :343).
+
+    The GP must be a fitted StructuredRocketGP (FITC or exact); its means are
+    what ``gp.predict`` returns (FITC: K*u alpha as written).
+    Cost weights must be diagonal (CostWeights builds them so); X_ref must be
+    x_target on every stage and U_ref zero in the cost (the reference's
+    defaults, :442-445).  The device model is the Rocket6DoFConfig default
+    rocket and N = 30 (BASELINE configs[4]); ``GPMPCConfig()`` without an N
+    gets N = 30 here.
+    """
+    n_x, n_u = 14, 3
+
+    def __init__(self, dynamics, gp_model, config: Optional[GPMPCConfig] = None,
+                 constraint_params=None, cost_weights=None, ctx=None):
+        if config is None:
+            config = GPMPCConfig(N=30)
+        if config.N != 30:
+            raise NotImplementedError("the 6-DoF device controller is compiled for N = 30 (BASELINE configs[4])")
+        matches = getattr(dynamics, "matches_device_model", None)
+        if matches is None or not matches():
+            raise NotImplementedError("the 6-DoF device controller runs the Rocket6DoFConfig default rocket "
+                                      "(dynamics.Rocket6DoFDynamics)")
+        self.dynamics = dynamics
+        self.config = config
+        self.gp = gp_model
+        self.constraint_params = constraint_params or ConstraintParams()
+        self.cost_weights = cost_weights or CostWeights()
+        self._ctx = ctx   # the device context is taken at the first solve
+        self._tightened_constraints = TightenedConstraints(base_params=self.constraint_params,
+                                                           confidence_level=self.config.confidence_level)
+        self._uncertainty_prop = UncertaintyPropagator(dynamics, gp_model, ctx=ctx)
+        self.last_uncertainty: Optional[PropagatedUncertainty] = None
+        self.last_tightened_params: Optional[ConstraintParams] = None
+        self._last_var = None
+        self._X_warm = self._U_warm = None
+        self._ro = None
+        self._ro_key = None
+        self._is_setup = False
+        self.last_status, self.last_iterations, self.last_passes = -10, 0, 0
+        self._cfg_kw = self._device_problem()
+
+    def _device_problem(self):
+        cw, cp = self.cost_weights, self.constraint_params
+        Q, R, P = (np.asarray(M, float) for M in (cw.Q, cw.R, cw.P))
+        for M in (Q, R, P):
+            if np.any(M - np.diag(np.diag(M))):
+                raise NotImplementedError("the device QP takes diagonal cost weights (CostWeights' own)")
+        return dict(q_diag=np.diag(Q), p_diag=np.diag(P), r_diag=np.diag(R), t_min=float(cp.T_min),
+                    t_max=float(cp.T_max), tan_gamma_gs=float(np.tan(cp.gamma_gs_rad)),
+                    dt=float(self.config.dt), use_gp_mean=int(bool(self.config.use_gp_mean)),
+                    fitc_mean_as_written=1,   # gp.predict's mean (sparse_gp.py:280-283, D1)
+                    max_iter=int(self.config.qp_max_iter), eps_abs=float(self.config.qp_eps),
+                    eps_rel=float(self.config.qp_eps))
+
+    def _rollout(self):
+        """The batch-of-one device controller over the GP's current device pair;
+        rebuilt (carrying U, duals and rho) when the GP has been refitted."""
+        hv, hw, _ = _r6.device_handles(self.gp)
+        key = (id(hv), id(hw))
+        if self._ro is not None and key == self._ro_key:
+            return self._ro
+        old = self._ro.state() if self._ro is not None else None
+        if self._ctx is None:
+            self._ctx = _lib.default_context()
+        ro = _r6.Rollouts6(self._ctx, hv, hw, 1, **self._cfg_kw)
+        if old is not None:
+            ro.set_state(U=old["U"], y=old["y"], rho=old["rho"])
+            self._ro.close()
+        self._ro, self._ro_key = ro, key
+        return ro
+
+    def reset_warm_start(self) -> None:
+        """gp_mpc.py:494-497 (+ the ADMM's persistent duals / rho)."""
+        self._X_warm = self._U_warm = None
+
+    def solve(self, x0, x_target, X_ref=None, U_ref=None) -> MPCSolution:
+        if not self._is_setup:
+            self.setup()
+        t0 = time.perf_counter()
+        N = self.config.N
+        x0 = np.asarray(x0, float).reshape(14); x_target = np.asarray(x_target, float).reshape(14)
+        if X_ref is not None and not np.array_equal(np.asarray(X_ref, float)[:N + 1],
+                                                    np.tile(x_target, (N + 1, 1))):
+            raise NotImplementedError("the device QP tracks x_target on every stage (X_ref=None)")
+        ro = self._rollout()
+        if self._U_warm is not None:
+            cold = 0
+        elif U_ref is not None:  # gp_mpc.py:268-269: U_ref as the first guess
+            ro.set_state(U=np.asarray(U_ref, float)[:N].reshape(1, N, 3))
+            cold = 2
+        else:
+            cold = 1
+        max_sqp = max(1, int(self.config.max_sqp_iter))
+        r = ro.solve(x0[None], x_target[None], cold, max_sqp_iter=max_sqp, sqp_tol=float(self.config.sqp_tol))
+        X, U = r["X"][0], r["U"][0]
+        st, passes = int(r["qp_status"][0]), int(r["passes"][0])
+        has = st in (1, 2, -2)
+        self.last_status, self.last_iterations, self.last_passes = st, int(r["qp_iters"][0]), passes
+        self._X_warm, self._U_warm = X.copy(), U.copy()
+        self._propagate(x0, U)
+        cost = self._cost(X, U, x_target) if has else np.inf
+        if max_sqp <= 1:
+            return MPCSolution(success=has, X_opt=X, U_opt=U, cost=cost, solve_time=time.perf_counter() - t0,
+                               iterations=self.last_iterations, status=_lib.QP_STATUS_TEXT.get(st, str(st)))
+        conv = bool(r["converged"][0])
+        return MPCSolution(success=conv, X_opt=X, U_opt=U, cost=cost, solve_time=time.perf_counter() - t0,
+                           iterations=passes, status="Converged" if conv else "Max iterations")
+
+    def _cost(self, X, U, x_target):
+        """gp_mpc.py:447-458 at the returned plan (X_ref = x_target, U_ref = 0)."""
+        cw = self.cost_weights
+        e = X - x_target
+        return float(np.einsum("ki,ij,kj->", e[:-1], cw.Q, e[:-1]) + np.einsum("ki,ij,kj->", U, cw.R, U)
+                     + e[-1] @ cw.P @ e[-1])
+
+    def _get_tightened_params(self, unc: PropagatedUncertainty, k: int) -> ConstraintParams:
+        return GPMPC._get_tightened_params(self, unc, k)
+
+    def _propagate(self, x0, U):
+        """gp_mpc.py:284-290 with the returned controls.  The re-propagations
+        of :347-353 are not repeated per pass: their only consumer,
+        _get_tightened_params(uncertainty, 0) (:414), reads covariances[0] =
+        Sigma_0 and tightens none of the rows the QP has (D14)."""
+        GPMPC._propagate(self, x0, U)
+
+    def close(self):
+        if self._ro is not None:
+            self._ro.close()
+            self._ro = None
 
 
 class SimpleGPPredictor:

@@ -21,21 +21,43 @@ from .gp.features import CombinedFeatureExtractor
 NX6 = 14
 
 
-def fit_structured_fitc(ctx, n_train=4000, n_inducing=2000, seed=0):
-    """The config-5 StructuredRocketGP pair as device FITC handles: d_v on the 13
-    translational, d_w on the 12 rotational features of generator-G6 data
-    (data.synthetic_6dof_training_data), unit SE-ARD kernels and noise 1e-4 as
-    StructuredRocketGP builds them; the inducing points are a seeded random
-    subset of the training rows (kmeans2's, sparse_gp.py:122-148, is host work
-    outside the hot path)."""
+def fit_structured_gp(n_train=4000, n_inducing=2000, seed=0, use_sparse=True):
+    """The config-5 ``StructuredRocketGP`` (structured_gp.py:66-411) fitted on
+    generator-G6 data (data.synthetic_6dof_training_data): d_v on the 13
+    translational, d_w on the 12 rotational features, unit SE-ARD kernels and
+    noise 1e-4 as the surface builds them, ``max_data_points = n_train`` (else
+    add_data keeps only the newest 1000).  The inducing points are
+    the surface's own: scipy kmeans2 on the global RNG (sparse_gp.py:122-148),
+    seeded here by ``np.random.seed(seed)``."""
+    from .gp.structured_gp import StructuredGPConfig, StructuredRocketGP
     X, U, Dv, Dw = synthetic_6dof_training_data(n_train, seed=seed)
-    fe = CombinedFeatureExtractor()
-    Zv = fe.extract_batch_translational(X, U)
-    Zw = fe.extract_batch_rotational(X, U)
-    idx = np.sort(np.random.RandomState(seed + 3).choice(n_train, min(n_inducing, n_train), replace=False))
-    gv = _lib.FITCHandle(ctx, Zv[idx], Zv, Dv, np.ones(Zv.shape[1]), 1.0, 1e-4)
-    gw = _lib.FITCHandle(ctx, Zw[idx], Zw, Dw, np.ones(Zw.shape[1]), 1.0, 1e-4)
-    return gv, gw
+    gp = StructuredRocketGP(StructuredGPConfig(n_inducing=n_inducing, max_data_points=n_train,
+                                               use_sparse=use_sparse))
+    gp.add_data(X, U, Dv, Dw)
+    np.random.seed(seed)
+    gp.fit()
+    return gp
+
+
+def device_handles(gp):
+    """The fitted StructuredRocketGP's device GP pair (FITCHandle or
+    ExactGPHandle each) and whether it is exact."""
+    if not gp._is_fitted:
+        gp.fit()
+    hv, hw = gp.gp_v.device_handle, gp.gp_omega.device_handle
+    if hv is None or hw is None:
+        raise ValueError("the StructuredRocketGP's outputs must share one device GP per residual group")
+    return hv, hw, not gp.config.use_sparse
+
+
+def fit_structured_fitc(ctx=None, n_train=4000, n_inducing=2000, seed=0):
+    """The config-5 FITC pair as device handles, through the StructuredRocketGP
+    surface (fit_structured_gp).  Returns (gp_v handle, gp_w handle); the
+    surface object stays alive on the first handle (``.surface``)."""
+    gp = fit_structured_gp(n_train, n_inducing, seed)
+    hv, hw, _ = device_handles(gp)
+    hv.surface = gp
+    return hv, hw
 
 
 def initial_conditions_6dof(count, seed0=42, first=0):
@@ -57,7 +79,8 @@ def initial_conditions_6dof(count, seed0=42, first=0):
 
 
 class Rollouts6:
-    """B rollouts on one device.  ``gp_v`` / ``gp_w``: FITCHandles (13 / 12 features)."""
+    """B rollouts on one device.  ``gp_v`` / ``gp_w``: FITCHandles (13 / 12
+    features), or ExactGPHandles (the exact StructuredRocketGP)."""
 
     def __init__(self, ctx, gp_v, gp_w, batch, **config):
         self.ctx = ctx
@@ -65,8 +88,12 @@ class Rollouts6:
         self.cfg = _lib.rollout6_default_config(**config)
         self.batch = int(batch)
         h = ctypes.c_void_p()
-        _lib._chk(_lib._L.gpmpc_rollout6_create(ctx.h, gp_v.h, gp_w.h, ctypes.byref(self.cfg), self.batch,
-                                                ctypes.byref(h)), "rollout6_create")
+        exact = isinstance(gp_v, _lib.ExactGPHandle)
+        if exact != isinstance(gp_w, _lib.ExactGPHandle):
+            raise TypeError("gp_v and gp_w must both be FITC or both exact")
+        create = _lib._L.gpmpc_rollout6_create_exact if exact else _lib._L.gpmpc_rollout6_create
+        _lib._chk(create(ctx.h, gp_v.h, gp_w.h, ctypes.byref(self.cfg), self.batch, ctypes.byref(h)),
+                  "rollout6_create")
         self.h = h
 
     def reset(self, x0, first=0):
@@ -91,6 +118,28 @@ class Rollouts6:
         _lib._chk(_lib._L.gpmpc_rollout6_get_state(self.h, _lib._d(U), _lib._d(X), _lib._d(Xp), _lib._d(gm),
                                                    _lib._d(y), _lib._d(rho)), "rollout6_get_state")
         return dict(rec=rec, x=x, U=U, X=X, X_pred=Xp, gm=gm, y=y, rho=rho)
+
+    def set_state(self, U=None, y=None, rho=None):
+        """gpmpc_rollout6_set_state (None leaves a part unchanged)."""
+        B, N = self.batch, int(self.cfg.horizon)
+        a = [None if v is None else _lib.f64(np.reshape(v, shape))
+             for v, shape in ((U, (B, N, 3)), (y, (B, 1104)), (rho, (B,)))]
+        _lib._chk(_lib._L.gpmpc_rollout6_set_state(self.h, *[None if v is None else _lib._d(v) for v in a]),
+                  "rollout6_set_state")
+
+    def solve(self, x0, x_target, cold, max_sqp_iter=10, sqp_tol=1e-4):
+        """GPMPC.solve (gp_mpc.py:229-369) for every rollout (gpmpc_rollout6_solve).
+        Returns dict(X (B, N+1, 14), U (B, N, 3), passes, converged, qp_status,
+        qp_iters) of int arrays (B,)."""
+        B, N = self.batch, int(self.cfg.horizon)
+        x0 = _lib.f64(np.reshape(x0, (B, NX6))); xt = _lib.f64(np.reshape(x_target, (B, NX6)))
+        X = np.empty((B, N + 1, NX6)); U = np.empty((B, N, 3))
+        ps, cv, qs, qi = (np.zeros(B, np.int32) for _ in range(4))
+        _lib._chk(_lib._L.gpmpc_rollout6_solve(self.h, _lib._d(x0), _lib._d(xt), int(cold),
+                                               int(max_sqp_iter), float(sqp_tol), _lib._d(X), _lib._d(U),
+                                               _lib._i(ps), _lib._i(cv), _lib._i(qs), _lib._i(qi)),
+                  "rollout6_solve")
+        return dict(X=X, U=U, passes=ps, converged=cv.astype(bool), qp_status=qs, qp_iters=qi)
 
     def close(self):
         if getattr(self, "h", None):

@@ -26,7 +26,9 @@
 extern "C" {
 #endif
 
-#define GPMPC_ABI_VERSION 1
+/* 2: gpmpc_fleet_config gained sqp_iters / sqp_tol (round 2) and
+ * gpmpc_rollout6_config the GPMPC problem data (round 3) */
+#define GPMPC_ABI_VERSION 2
 
 typedef struct gpmpc_ctx gpmpc_ctx;
 typedef struct gpmpc_gp gpmpc_gp;
@@ -150,6 +152,9 @@ int gpmpc_fitc_fit(gpmpc_ctx *ctx, const double *Z, int m, const double *X, int 
 /* SparseGP.predict (sparse_gp.py:255-305), mean as written. */
 int gpmpc_fitc_predict(gpmpc_ctx *ctx, gpmpc_fitc *gp, const double *Xq, int p, double *mean,
                        double *var);
+/* copy of the fitted alpha (m x n_out: L_B^-T L_B^-1 A Lambda^-1 y per output,
+ * sparse_gp.py:208-210) */
+int gpmpc_fitc_get_state(gpmpc_ctx *ctx, gpmpc_fitc *gp, double *alpha);
 int gpmpc_fitc_destroy(gpmpc_fitc *gp);
 
 /* ---- a15: batched OSQP-style ADMM ------------------------------------------
@@ -273,12 +278,48 @@ typedef struct {
   gpmpc_qp_settings qp;  /* osqp_rti.py:54-60 defaults */
   int fitc_mean_as_written;  /* 0: the FITC posterior mean K*u L_uu^-T alpha; 1: the
                                 reference's K*u alpha (sparse_gp.py:280-283) */
+  /* GPMPC's problem data (ABI 2).  Defaults: CostWeights (cost_functions.py:39-98),
+   * ConstraintParams (constraints.py:35-50), gp_mpc.py:432-435. */
+  double q_diag[14];     /* stage cost Q (diagonal) */
+  double p_diag[14];     /* terminal cost P (diagonal; 10 Q) */
+  double r_diag[3];      /* control cost R (diagonal) */
+  double t_min, t_max;   /* thrust magnitude bounds */
+  double tan_gamma_gs;   /* tan of the glide-slope angle, np.tan(np.deg2rad(30)) */
+  double trust_x2, trust_u2;  /* squared trust radii 10, 5 */
+  int use_gp_mean;       /* GPMPCConfig.use_gp_mean: 0 drops the GP from the simulation and c_k */
+  int upright_target;    /* rollouts: 0 = monte_carlo.py:497-500 as written (x copied, v = 0,
+                            altitude - 2); 1 = also q = (1, 0, 0, 0), omega = 0 */
 } gpmpc_rollout6_config;
 void gpmpc_rollout6_default_config(gpmpc_rollout6_config *c);
 /* gp_v: FITC on the 13 translational features, gp_w: on the 12 rotational
  * ones (features.py:149-365), 3 outputs each; both must outlive the batch */
 int gpmpc_rollout6_create(gpmpc_ctx *ctx, gpmpc_fitc *gp_v, gpmpc_fitc *gp_w,
                           const gpmpc_rollout6_config *cfg, int batch, gpmpc_rollout6 **out);
+/* the same over a pair of exact GPs (StructuredRocketGP(use_sparse=False),
+ * exact_gp.py:213-268: mean K* alpha over the training rows) */
+int gpmpc_rollout6_create_exact(gpmpc_ctx *ctx, gpmpc_gp *gp_v, gpmpc_gp *gp_w,
+                                const gpmpc_rollout6_config *cfg, int batch, gpmpc_rollout6 **out);
+/* GPMPC.solve (gp_mpc.py:229-369) for every rollout b of the batch at x0[b]
+ * (batch x 14) with target x_target[b] (batch x 14), X_ref = x_target, U_ref = 0:
+ *   pass 1: forward simulation of the warm-start controls with the GP mean
+ *           (gp_mpc.py:258-281), the QP around it (:394-460, made linear as the
+ *           rollouts), plan <- X_pred + dX, U_pred + dU;
+ *   pass p > 1: GP means and Jacobians at the last plan (:299-320), QP, plan;
+ *   stop after max_sqp_iter passes or when max|X_new - X_pred| and
+ *   max|U_new - U_pred| are both < sqp_tol (:336-345).
+ * A QP without a solution returns the nominal trajectory (:478-482: X_new =
+ * X_pred, so the loop stops as converged) with qp_status < 0 (not -2).
+ * cold = 1: the hover guess [0, 0, m0 g0] at every stage and fresh ADMM duals /
+ * rho (first call, GPMPC.reset_warm_start); cold = 2: fresh duals / rho, the
+ * controls already set (gpmpc_rollout6_set_state: U_ref, :268-269); cold = 0:
+ * the previous call's plan U, unshifted (:266-267, :358-359).  The batch's Monte-Carlo records are not
+ * touched except rec[11] (ADMM iterations of this call), rec[12] (solves with
+ * status solved), rec[14] (last QP status), rec[15] (rho).
+ * Outputs (any may be NULL): X (batch x 31 x 14), U (batch x 30 x 3), passes,
+ * converged (0 / 1), qp_status of the last pass, qp_iters summed over passes. */
+int gpmpc_rollout6_solve(gpmpc_rollout6 *r, const double *x0, const double *x_target, int cold,
+                         int max_sqp_iter, double sqp_tol, double *X, double *U, int *passes,
+                         int *converged, int *qp_status, int *qp_iters);
 /* (re)start rollouts [first, first+count) at x0 (count x 14) */
 int gpmpc_rollout6_reset(gpmpc_rollout6 *r, int first, int count, const double *x0);
 /* nsteps control steps of every running rollout (async on the ctx stream) */
@@ -292,6 +333,10 @@ int gpmpc_rollout6_read(gpmpc_rollout6 *r, double *records, double *x);
  * scaled duals (batch x 1104) and rho (batch) */
 int gpmpc_rollout6_get_state(gpmpc_rollout6 *r, double *U, double *X_plan, double *X_pred,
                              double *gp_mean, double *y_scaled, double *rho);
+/* set controller state (any pointer may be NULL): U (batch x 30 x 3), scaled
+ * duals (batch x 1104), rho (batch) -- e.g. to carry a warm start across a GP
+ * refit, or to start GPMPC.solve from caller-given controls */
+int gpmpc_rollout6_set_state(gpmpc_rollout6 *r, const double *U, const double *y_scaled, const double *rho);
 int gpmpc_rollout6_destroy(gpmpc_rollout6 *r);
 
 /* device pointer of the record array (for collectives) */

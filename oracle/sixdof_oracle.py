@@ -194,24 +194,38 @@ def qp_pattern(N):
     return n, len(rows), rp.astype(np.int32), ci.astype(np.int32)
 
 
-def build_qp(Xn, Un, gm, x_ref, dt):
+def default_problem():
+    """GPMPC's problem data with the reference defaults: CostWeights Q / R / P
+    (cost_functions.py:39-105), ConstraintParams T_min, T_max, gamma_gs
+    (constraints.py:35-50), trust radii^2 10 / 5 (gp_mpc.py:432-435)."""
+    return dict(Q=Q_DIAG.copy(), P=Q_DIAG * P_SCALE, R=R_DIAG.copy(), t_min=T_MIN, t_max=T_MAX,
+                tan_gs=TAN_GS, trust_x2=10.0, trust_u2=5.0)
+
+
+def build_qp(Xn, Un, gm, x_ref, dt, x0=None, prob=None):
     """QP of gp_mpc.py:394-460 around (Xn, Un) with c_k = GP mean dt (gp_mpc.py:309-314)
-    in deviation variables z = [dx_0, du_0, ..., dx_N].  Returns Pdiag, q, A (CSR), l, u."""
+    in deviation variables z = [dx_0, du_0, ..., dx_N], X_ref = x_ref, U_ref = 0.
+    x0 rows: dx_0 = x0 - X_nom[0] (gp_mpc.py:402; 0 when X_nom[0] = x0).
+    Returns Pdiag, q, A (CSR), l, u."""
+    pr = prob or default_problem()
     N = Un.shape[0]
     n, m, rp, ci = qp_pattern(N)
     val = np.zeros(rp[-1]); l = np.zeros(m); u = np.zeros(m)
     Pd = np.zeros(n); q = np.zeros(n)
+    tr_x, tr_u = np.sqrt(pr["trust_x2"]), np.sqrt(pr["trust_u2"])
     for k in range(N + 1):
         o = k * (NX + NU)
-        w = Q_DIAG * (P_SCALE if k == N else 1.0)
+        w = pr["P"] if k == N else pr["Q"]
         Pd[o:o + NX] = w
         q[o:o + NX] = w * (Xn[k] - x_ref)
         if k < N:
-            Pd[o + NX:o + NX + NU] = R_DIAG
-            q[o + NX:o + NX + NU] = R_DIAG * Un[k]
+            Pd[o + NX:o + NX + NU] = pr["R"]
+            q[o + NX:o + NX + NU] = pr["R"] * Un[k]
     r = 0
     for i in range(NX):
-        val[rp[r]] = 1.0; r += 1      # dx_0 = x0 - X_nom[0] = 0
+        val[rp[r]] = 1.0
+        l[r] = u[r] = 0.0 if x0 is None else x0[i] - Xn[0, i]
+        r += 1
     for k in range(N):
         Ad, Bd = linearize(Xn[k], Un[k], dt)
         c = np.zeros(NX)
@@ -228,41 +242,49 @@ def build_qp(Xn, Un, gm, x_ref, dt):
         k, i = divmod(j, NX + NU)
         val[rp[r]] = 1.0
         if i < NX:
-            l[r], u[r] = -TRUST_X, TRUST_X
+            l[r], u[r] = -tr_x, tr_x
         else:
             ub = Un[k, i - NX]
-            l[r] = max(-TRUST_U, -T_MAX - ub)
-            u[r] = min(TRUST_U, T_MAX - ub)
+            l[r] = max(-tr_u, -pr["t_max"] - ub)
+            u[r] = min(tr_u, pr["t_max"] - ub)
         r += 1
     for k in range(N):
         ub = Un[k]
         tm = np.sqrt(ub @ ub)
         val[rp[r]:rp[r] + 3] = ub / tm
-        l[r], u[r] = T_MIN - tm, np.inf
+        l[r], u[r] = pr["t_min"] - tm, np.inf
         r += 1
+    tg = pr["tan_gs"]
     for k in range(1, N):
         rx, ry, rz = Xn[k, 1:4]
         for c, rc in ((2, ry), (3, rz)):
             a = rp[r]
-            val[a:a + 2] = (TAN_GS, -1.0); l[r], u[r] = -(TAN_GS * rx - rc), np.inf; r += 1
+            val[a:a + 2] = (tg, -1.0); l[r], u[r] = -(tg * rx - rc), np.inf; r += 1
             a = rp[r]
-            val[a:a + 2] = (TAN_GS, 1.0); l[r], u[r] = -(TAN_GS * rx + rc), np.inf; r += 1
+            val[a:a + 2] = (tg, 1.0); l[r], u[r] = -(tg * rx + rc), np.inf; r += 1
     A = sp.csr_matrix((val, ci, rp), shape=(m, n))
     return Pd, q, A, l, u
 
 
-def incremental_target(x):
-    """monte_carlo.py:497-500 on the 14-state layout, upright and at rest."""
+def incremental_target(x, upright=False):
+    """monte_carlo.py:497-500 on the 14-state layout: x copied (attitude and rates
+    kept), v = 0, altitude - 2 m with a 0.5 m floor; ``upright`` also sets
+    q = (1, 0, 0, 0), omega = 0 (the fleet6 ``upright_target`` option)."""
     t = x.copy()
     t[4:7] = 0.0
     t[1] = max(0.5, x[1] - 2.0)
-    t[7:11] = (1.0, 0.0, 0.0, 0.0)
-    t[11:14] = 0.0
+    if upright:
+        t[7:11] = (1.0, 0.0, 0.0, 0.0)
+        t[11:14] = 0.0
     return t
 
 
 def hover_guess(x, N):
-    """gp_mpc.py:271-275 (as written: thrust on the body z axis)."""
+    """gp_mpc.py:271-275: [0, 0, m g0] (thrust on the body z axis, as written) at
+    every stage.  As written the loop reads X_pred[k, 0] before the forward
+    simulation has filled it, so stages k >= 1 get zero thrust; zero thrust has
+    no linearisation of the thrust-magnitude rows (u / |u|), so the evident
+    intent m0 g0 is used at every stage."""
     U = np.zeros((N, NU))
     U[:, 2] = x[0] * G0
     return U
@@ -278,7 +300,7 @@ def new_rollout(x0, N=30):
                 rho=admm_ref.default_settings().rho, rec=rec, X=None)
 
 
-def rollout_step(gpv, gpw, S, dt=0.1, max_steps=300, qp_settings=None, corrected=True):
+def rollout_step(gpv, gpw, S, dt=0.1, max_steps=300, qp_settings=None, corrected=True, upright=False):
     """One control step of the 6-DoF rollout (monte_carlo.py:455-537 termination
     rules on the first seven states; one GPMPC.solve pass as the module header)."""
     from . import admm_ref, mc_oracle
@@ -303,7 +325,7 @@ def rollout_step(gpv, gpw, S, dt=0.1, max_steps=300, qp_settings=None, corrected
         X[k + 1] = step(X[k], U[k], dt)
         X[k + 1, 4:7] += dv * dt
         X[k + 1, 11:14] += dw * dt
-    Pd, q, A, l, u = build_qp(X, U, gm, incremental_target(x), dt)
+    Pd, q, A, l, u = build_qp(X, U, gm, incremental_target(x, upright), dt)
     qp = admm_ref.RefQP(len(out["y"]), settings=qp_settings)
     qp.y = out["y"]; qp.rho = np.array([out["rho"]])
     try:
@@ -338,3 +360,82 @@ def initial_condition(seed):
     x[:7] = x7
     x[7] = np.cos(ang / 2); x[8:11] = ax * np.sin(ang / 2)
     return x
+
+
+def gpmpc_solve(gpv, gpw, S, x0, x_target, max_sqp_iter=10, sqp_tol=1e-4, dt=0.1, qp_settings=None,
+                corrected=True, use_gp=True, prob=None):
+    """GPMPC.solve (gp_mpc.py:229-369) on the 14-state rocket with the QP made
+    linear as in build_qp and solved by the OSQP-0.6 restatement:
+
+    * X_pred[0] = x0; the controls are the warm start S["U"] (the previous
+      plan, unshifted, :266-267 / :358-359; the caller puts hover_guess there on
+      the first call); forward simulation with the GP mean (:277-281);
+    * up to max_sqp_iter passes (:299-353): GP means and Jacobians at
+      (X_pred[k], U_pred[k]) (the first pass reuses the simulation's means,
+      which are the same calls), QP around (X_pred, U_pred), plan = X_pred +
+      dX, U_pred + dU; a QP without a solution returns the nominal (:478-482),
+      so that pass changes nothing and the loop stops as converged; stop when
+      max|X_new - X_pred| and max|U_new - U_pred| are both < sqp_tol;
+    * the ADMM keeps OSQP's persistent rho / scaled y across passes and calls;
+      a failed pass leaves them as they were (the device writes them back only
+      with a solution).
+
+    S: dict(U (N, 3), y (m,), rho).  Returns dict(X, U, y, rho, passes,
+    converged, qp_status, qp_iters, n_solved, X_pred (of the first pass), gm)."""
+    from . import admm_ref
+    U = np.array(S["U"], float)
+    N = U.shape[0]
+    x0 = np.asarray(x0, float)
+    X = np.zeros((N + 1, NX)); X[0] = x0
+    gm = np.zeros((N, 6))
+    for k in range(N):
+        if use_gp:
+            dv, dw = gp_mean(gpv, gpw, X[k], U[k], corrected)
+            gm[k, :3], gm[k, 3:] = dv, dw
+        X[k + 1] = step(X[k], U[k], dt)
+        X[k + 1, 4:7] += gm[k, :3] * dt
+        X[k + 1, 11:14] += gm[k, 3:] * dt
+    X_first = X.copy()
+    n, m, _, _ = qp_pattern(N)
+    qp = admm_ref.RefQP(m, settings=qp_settings)
+    qp.y = np.array(S["y"], float); qp.rho = np.array([float(S["rho"])])
+    passes, qit, qst, conv, nsolved = 0, 0, -10, False, 0
+    for it in range(max_sqp_iter):
+        if it > 0:
+            gm = np.zeros((N, 6))
+            if use_gp:
+                for k in range(N):
+                    dv, dw = gp_mean(gpv, gpw, X[k], U[k], corrected)
+                    gm[k, :3], gm[k, 3:] = dv, dw
+        Pd, q, A, l, u = build_qp(X, U, gm, x_target, dt, x0=x0, prob=prob)
+        y_keep, rho_keep = qp.y.copy(), qp.rho.copy()
+        try:
+            r = qp.solve(Pd, q, A, l, u, np.zeros(Pd.size))
+            st, nit = r["status"], r["iter"]
+        except RuntimeError:
+            r, st, nit = None, -100, 0
+        passes += 1; qit += nit; qst = st
+        nsolved += st == 1
+        if st in (1, 2, -2):
+            z = r["x"]
+            Xn = X + np.array([z[k * (NX + NU):k * (NX + NU) + NX] for k in range(N + 1)])
+            Un = U + np.array([z[k * (NX + NU) + NX:(k + 1) * (NX + NU)] for k in range(N)])
+        else:
+            qp.y, qp.rho = y_keep, rho_keep
+            Xn, Un = X, U
+        dx, du = np.max(np.abs(Xn - X)), np.max(np.abs(Un - U))
+        X, U = Xn, Un
+        if dx < sqp_tol and du < sqp_tol:
+            conv = True
+            break
+    return dict(X=X, U=U, y=qp.y, rho=float(qp.rho[0]), passes=passes, converged=conv, qp_status=qst,
+                qp_iters=qit, n_solved=nsolved, X_pred=X_first, gm=gm)
+
+
+def solution_cost(X, U, x_target, prob=None):
+    """The QP subproblem's objective at the returned plan (gp_mpc.py:447-458,
+    X_ref = x_target, U_ref = 0)."""
+    pr = prob or default_problem()
+    e = np.asarray(X) - np.asarray(x_target)
+    return float(np.sum(e[:-1] ** 2 * pr["Q"]) + np.sum(np.asarray(U) ** 2 * pr["R"])
+                 + np.sum(e[-1] ** 2 * pr["P"]))
