@@ -17,6 +17,8 @@ LIB_PATH = os.path.join(_HERE, "libgpmpc_hip.so")
 SE_ARD, SE_ISO, MATERN32, MATERN52 = 0, 1, 2, 3
 ERR_NOT_PD = -100
 REC_LEN = 16
+# caps of the generic device QP (csrc/qp.h QP_NMAX, QP_MMAX, QP_NNZMAX)
+QP_NMAX, QP_MMAX, QP_NNZMAX = 216, 360, 896
 
 QP_STATUS = {1: "solved", 2: "solved inaccurate", -2: "maximum iterations reached",
              -3: "primal infeasible", 3: "primal infeasible inaccurate", -4: "dual infeasible",

@@ -48,19 +48,19 @@ def summarise(records: np.ndarray) -> dict:
 
 def main(argv=None):
     ap = argparse.ArgumentParser()
-    ap.add_argument("--landings", type=int, default=1024)
+    ap.add_argument("--landings", type=int, default=None, help="default 1024 (512 with --six-dof)")
     ap.add_argument("--max-steps", type=int, default=300)
     ap.add_argument("--chunk", type=int, default=25, help="control steps between termination polls")
-    ap.add_argument("--train", type=int, default=1000)
+    ap.add_argument("--train", type=int, default=None, help="GP training rows, default 1000 (4000 with --six-dof)")
     ap.add_argument("--seed0", type=int, default=42)
     ap.add_argument("--out", default="")
     ap.add_argument("--six-dof", action="store_true", help="BASELINE configs[4]: 6-DoF rollouts")
     ap.add_argument("--inducing", type=int, default=2000, help="--six-dof: FITC inducing points")
     args = ap.parse_args(argv)
-    if args.six_dof and args.landings == 1024:
-        args.landings = 512
-    if args.six_dof and args.train == 1000:
-        args.train = 4000
+    if args.landings is None:
+        args.landings = 512 if args.six_dof else 1024
+    if args.train is None:
+        args.train = 4000 if args.six_dof else 1000
 
     import torch
     import torch.distributed as dist

@@ -82,7 +82,12 @@ def qp_settings_from(cfg) -> "_lib.QPSettings":
 class OSQPRTIMPC:
     """osqp_rti.py:89-639."""
 
-    _DENSE_PATTERN = True   # finite-difference Jacobians: any entry may be non-zero
+    # finite-difference Jacobians: any entry may be non-zero.  The filtered
+    # pattern must fit the device QP's caps (_lib.QP_NNZMAX = 896 non-zeros,
+    # n <= 216, m <= 360): the drag Euler plant at N = 20 has 854; a plant whose
+    # Jacobians are dense (e.g. an RK4 step, ~44 non-zeros per stage) exceeds the
+    # cap from N ~ 16 on, and the first solve then raises ValueError.
+    _DENSE_PATTERN = True
 
     def __init__(self, dynamics, config: Optional[OSQPRTIConfig] = None, ctx=None):
         self.dynamics = dynamics
@@ -168,6 +173,9 @@ class OSQPRTIMPC:
         blk[:, :, :-1] = np.abs(Aval[dyn].reshape(blk.shape)[:, :, :-1]) > 1e-10
         rows = np.repeat(np.arange(b.m), np.diff(b.rowptr))
         rowptr = np.concatenate([[0], np.cumsum(np.bincount(rows[keep], minlength=b.m))]).astype(np.int32)
+        if int(rowptr[-1]) > _lib.QP_NNZMAX:
+            raise ValueError(f"the plant's Jacobians give {int(rowptr[-1])} constraint non-zeros at N = {self.N}; "
+                             f"the device QP holds at most {_lib.QP_NNZMAX} (QP_NNZMAX, csrc/qp.h)")
         self._pattern = (rowptr, b.colidx[keep])
         return Aval[keep], l, u
 

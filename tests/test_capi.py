@@ -52,3 +52,11 @@ def test_settings_reject_unknown_keys():
         _lib.fleet_default_config(eps=1e-5)
     with pytest.raises(TypeError):
         _lib.fleet_default_config(qp=None)
+
+
+def test_qp_caps_match_the_header():
+    """_lib's QP caps (used for the OSQPRTIMPC pattern check) are csrc/qp.h's."""
+    from gp_mpc_rocket_landing_amd import _lib
+    src = open(os.path.join(REPO, "gp_mpc_rocket_landing_amd", "csrc", "qp.h")).read()
+    caps = {k: int(v) for k, v in re.findall(r"#define (QP_NMAX|QP_MMAX|QP_NNZMAX) (\d+)", src)}
+    assert caps == {"QP_NMAX": _lib.QP_NMAX, "QP_MMAX": _lib.QP_MMAX, "QP_NNZMAX": _lib.QP_NNZMAX}
