@@ -79,7 +79,7 @@ class FleetConfig(ctypes.Structure):
     _fields_ = [("horizon", ctypes.c_int), ("dt", ctypes.c_double), ("target_mode", ctypes.c_int),
                 ("use_gp", ctypes.c_int), ("residual_model", ctypes.c_int),
                 ("max_steps", ctypes.c_int), ("qp", QPSettings),
-                ("sqp_iters", ctypes.c_int), ("sqp_tol", ctypes.c_double)]
+                ("sqp_iters", ctypes.c_int), ("sqp_tol", ctypes.c_double), ("sqp_qp", QPSettings)]
 
 
 def _sig(name, res, *args):
@@ -430,6 +430,9 @@ def set_fields(struct, kw, nested=None):
     for k, v in kw.items():
         if k in own and k != nested:
             cur = getattr(struct, k)
+            if isinstance(cur, ctypes.Structure) and isinstance(v, dict):  # a nested settings struct
+                set_fields(cur, v)
+                continue
             if isinstance(cur, ctypes.Array):  # fixed-size array fields take a sequence
                 v = np.ravel(np.asarray(v, dtype=np.float64))
                 if v.size != len(cur):
@@ -457,10 +460,16 @@ def rollout6_default_config(**kw):
 
 
 def fleet_default_config(**kw):
-    """Fleet config; QP settings may be given flat (``max_iter=...``)."""
+    """Fleet config; QP settings may be given flat (``max_iter=...``); the SQP
+    passes' settings as ``sqp_qp=dict(...)`` on top of the (final) ``qp``."""
     c = FleetConfig()
     _L.gpmpc_fleet_default_config(ctypes.byref(c))
-    return set_fields(c, kw, nested="qp")
+    sq = kw.pop("sqp_qp", None)
+    set_fields(c, kw, nested="qp")
+    c.sqp_qp = c.qp
+    if sq:
+        set_fields(c.sqp_qp, sq)
+    return c
 
 
 class QPWorkspace:

@@ -80,6 +80,7 @@ extern "C" void gpmpc_fleet_default_config(gpmpc_fleet_config *c) {
   gpmpc_qp_default_settings(&c->qp);
   c->sqp_iters = 1;          // RTI; > 1: GPMPC.solve's loop (gp_mpc.py:296-345)
   c->sqp_tol = 1e-4;         // gp_mpc.py:343
+  c->sqp_qp = c->qp;         // the SQP passes' QP settings (the same unless set)
 }
 
 // ---------------------------------------------------------------------------
@@ -500,6 +501,11 @@ __global__ __launch_bounds__(FQ_T) __attribute__((amdgpu_waves_per_eu(2, 2))) vo
       for (int i = 0; i < NX; ++i) rec[4 + i] = sx[i];
     }
     return;
+  }
+  if (a.sqp && a.sqp_first) {
+    // X_pred[0] = x0 (gp_mpc.py:263): the unshifted plan starts at the last state
+    if (tid < NX) Xw[tid] = sx[tid];
+    __syncthreads();
   }
   FleetRegs R;
   fq_init_pattern(a.pt, R, n);
@@ -991,7 +997,7 @@ __global__ __launch_bounds__(1024) void k_fleet_order(int B, const double *__res
 static FleetArgs fleet_args(gpmpc_fleet *f) {
   FleetArgs a;
   a.pt = f->pat.dev;
-  a.st = to_dev(f->cfg.qp);
+  a.st = to_dev(f->cfg.sqp_iters > 1 ? f->cfg.sqp_qp : f->cfg.qp);
   a.N = f->N;
   a.target_mode = f->cfg.target_mode;
   a.use_gp = f->cfg.use_gp;

@@ -28,6 +28,7 @@ uses the propagator's default dt = 0.1 like the reference (D6).
 """
 from __future__ import annotations
 
+import dataclasses
 import time
 from dataclasses import dataclass
 from typing import Optional
@@ -52,6 +53,17 @@ class GPMPCConfig(MPCConfig):
     max_variance_for_constraint: float = 1.0
     robust_horizon: int = -1
     max_sqp_iter: int = 1
+    # QP settings of the loop's passes (max_sqp_iter > 1); None = qp_max_iter / qp_eps.
+    # The reference solves this subproblem with IPOPT (gp_mpc.py:462-470).
+    sqp_qp_max_iter: Optional[int] = None
+    sqp_qp_eps: Optional[float] = None
+
+    def qp_settings(self):
+        """(max_iter, eps) of the QP solves this configuration runs."""
+        if self.max_sqp_iter > 1:
+            return (self.qp_max_iter if self.sqp_qp_max_iter is None else self.sqp_qp_max_iter,
+                    self.qp_eps if self.sqp_qp_eps is None else self.sqp_qp_eps)
+        return self.qp_max_iter, self.qp_eps
 
 
 class GPMPC(_SQPBase):
@@ -71,7 +83,10 @@ class GPMPC(_SQPBase):
         n_state = getattr(dynamics, "n_state", 7)
         if n_state != 7:
             raise NotImplementedError("the 3-DoF adapter runs n_x = 7; 14 states go to GPMPC6DoF")
-        super().__init__(dynamics, config or GPMPCConfig(), ctx=ctx)
+        config = config or GPMPCConfig()
+        mi, eps = config.qp_settings()
+        super().__init__(dynamics, dataclasses.replace(config, qp_max_iter=mi, qp_eps=eps), ctx=ctx)
+        self.config = config
         self.gp = gp_model
         self.constraint_params = constraint_params or ConstraintParams()
         self.cost_weights = cost_weights or CostWeights()
@@ -154,6 +169,7 @@ class GPMPC(_SQPBase):
                                cost=trajectory_cost(X, U, x_target) if ok else np.inf,
                                solve_time=time.perf_counter() - t0, iterations=int(r["iter"][0]),
                                status=_lib.QP_STATUS_TEXT.get(st, str(st)))
+        X[0] = x0   # X_pred[0] = x0 (gp_mpc.py:263)
         X, U, conv, it, st, dt = self._sqp(x0, x_target, X, U, self.config.max_sqp_iter, -1.0)
         self._X_warm, self._U_warm = X.copy(), U.copy()
         return MPCSolution(success=conv, X_opt=X, U_opt=U, cost=trajectory_cost(X, U, x_target),
@@ -239,8 +255,8 @@ class GPMPC6DoF(GPMPC):
                     t_max=float(cp.T_max), tan_gamma_gs=float(np.tan(cp.gamma_gs_rad)),
                     dt=float(self.config.dt), use_gp_mean=int(bool(self.config.use_gp_mean)),
                     fitc_mean_as_written=1,   # gp.predict's mean (sparse_gp.py:280-283, D1)
-                    max_iter=int(self.config.qp_max_iter), eps_abs=float(self.config.qp_eps),
-                    eps_rel=float(self.config.qp_eps))
+                    max_iter=int(self.config.qp_settings()[0]), eps_abs=float(self.config.qp_settings()[1]),
+                    eps_rel=float(self.config.qp_settings()[1]))
 
     def _rollout(self):
         """The batch-of-one device controller over the GP's current device pair;

@@ -210,6 +210,8 @@ typedef struct {
                             :506-508).  The warm start is the unshifted plan (gp_mpc.py
                             :358-359). */
   double sqp_tol;        /* 1e-4 (gp_mpc.py:343) */
+  gpmpc_qp_settings sqp_qp;  /* QP settings of the SQP passes (sqp_iters > 1); default = qp.
+                                The reference solves this subproblem with IPOPT (gp_mpc.py:462-470) */
 } gpmpc_fleet_config;
 void gpmpc_fleet_default_config(gpmpc_fleet_config *c);
 int gpmpc_fleet_create(gpmpc_ctx *ctx, gpmpc_gp *gp, const gpmpc_fleet_config *cfg, int batch,

@@ -192,6 +192,7 @@ def _sqp_landing_step(st, S, max_steps, dt, cfg, use_gp, residual_model, sqp_ite
     qp = admm_ref.RefQP(len(out["y"]), settings=qp_settings)
     qp.y = out["y"]; qp.rho = np.array([out["rho"]])
     info = None
+    Xw[0] = x          # X_pred[0] = x0 (gp_mpc.py:263): the unshifted plan starts at the last state
     for it in range(sqp_iters):
         mean = None
         if use_gp:
