@@ -398,6 +398,25 @@ def qp_status_histogram(fl, steps=10):
             "admm_iterations": iters}
 
 
+def gather_shard_records(ctx, d_records, host_records, total):
+    """The one collective: the C-ABI's ncclGather of the device
+    record arrays (gpmpc_gather_results).  GPMPC_GATHER=torch selects
+    torch.distributed.gather (also RCCL) instead; an error in the C-ABI path
+    falls back to it, so the records always reach rank 0."""
+    from gp_mpc_rocket_landing_amd.sharding import RCCLRecordGather, gather_records
+    if os.environ.get("GPMPC_GATHER", "rccl") != "torch":
+        try:
+            g = RCCLRecordGather(ctx)
+            try:
+                return g.gather(d_records, total)
+            finally:
+                g.close()
+        except Exception as e:  # noqa: BLE001
+            print(f"bench: C-ABI RCCL gather failed ({e}); torch.distributed.gather instead",
+                  file=sys.stderr, flush=True)
+    return gather_records(host_records, total, device="cuda")
+
+
 def gpmpc_loop_bench(ctx, gp, batch=1024, reps=3, sqp_iters=10):
     """GPMPC.solve's own loop on the fleet (gp_mpc.py:296-353; sqp_iters = 10,
     stop at 1e-4): every control step = up to 10 passes of GP posterior at the
@@ -594,8 +613,7 @@ def main():
         tmax = t.clone(); dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
         tsum = t.clone(); dist.all_reduce(tsum, op=dist.ReduceOp.SUM)
         el_max, steps_all, iters_all = float(tmax[0]), float(tsum[1]), float(tsum[2])
-        from gp_mpc_rocket_landing_amd.sharding import gather_records
-        all_rec = gather_records(rec1, world * B, device="cuda")   # the one RCCL gather
+        all_rec = gather_shard_records(ctx, fl.records_dev, rec1, world * B)   # the one RCCL gather
     else:
         el_max, steps_all, iters_all = el, steps_done, admm_iters
         all_rec = rec1

@@ -138,6 +138,11 @@ _sig("gpmpc_rollout6_create", _c, _vp, _vp, _vp, ctypes.POINTER(Rollout6Config),
 _sig("gpmpc_rollout6_create_exact", _c, _vp, _vp, _vp, ctypes.POINTER(Rollout6Config), _c, ctypes.POINTER(_vp))
 _sig("gpmpc_rollout6_solve", _c, _vp, _dp, _dp, _c, _c, ctypes.c_double, _dp, _dp, _ip, _ip, _ip, _ip)
 _sig("gpmpc_rollout6_set_state", _c, _vp, _dp, _dp, _dp)
+_sig("gpmpc_rollout6_records_dev", _vp, _vp)
+_sig("gpmpc_comm_unique_id", _c, ctypes.c_char_p)
+_sig("gpmpc_comm_init", _c, _vp, ctypes.c_char_p, _c, _c, ctypes.POINTER(_vp))
+_sig("gpmpc_comm_destroy", _c, _vp)
+_sig("gpmpc_gather_results", _c, _vp, _vp, _vp, _ip, _c, _dp)
 _sig("gpmpc_rollout6_reset", _c, _vp, _c, _c, _dp)
 _sig("gpmpc_rollout6_step", _c, _vp, _c)
 _sig("gpmpc_rollout6_read", _c, _vp, _dp, _dp)
@@ -157,7 +162,9 @@ EXPORTED = ["gpmpc_abi_version", "gpmpc_last_error", "gpmpc_ctx_create", "gpmpc_
             "gpmpc_fleet_records_dev", "gpmpc_fleet_destroy", "gpmpc_rollout6_default_config",
             "gpmpc_rollout6_create", "gpmpc_rollout6_reset", "gpmpc_rollout6_step", "gpmpc_rollout6_read",
             "gpmpc_rollout6_get_state", "gpmpc_rollout6_destroy", "gpmpc_rollout6_create_exact",
-            "gpmpc_rollout6_solve", "gpmpc_rollout6_set_state", "gpmpc_fitc_get_state"]
+            "gpmpc_rollout6_solve", "gpmpc_rollout6_set_state", "gpmpc_fitc_get_state",
+            "gpmpc_rollout6_records_dev", "gpmpc_comm_unique_id", "gpmpc_comm_init", "gpmpc_comm_destroy",
+            "gpmpc_gather_results"]
 
 
 class HIPError(RuntimeError):

@@ -121,6 +121,17 @@ __device__ __forceinline__ void features3(const double *x, const double *u, doub
   z[9] = alt / 100.0; z[10] = rho / 1.225;
 }
 
+// GPMPC.solve's loop: X_pred[0] = x0 (gp_mpc.py:263) -- before the first pass of
+// a control step the unshifted plan's first point becomes the current state
+__global__ void k_fleet_x0_to_plan(int B, int N, const double *__restrict__ x, const double *__restrict__ rec,
+                                   double *__restrict__ Xw) {
+  const int g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= B * NX) return;
+  const int b = g / NX, i = g - b * NX;
+  if (rec[(int64_t)b * GPMPC_REC_LEN] != 0.0) return;
+  Xw[(int64_t)b * (N + 1) * NX + i] = x[g];
+}
+
 __global__ void k_fleet_queries(int B, int N, const double *__restrict__ Xw,
                                 const double *__restrict__ Uw, const double *__restrict__ ls,
                                 int iso, const int *__restrict__ order, double *__restrict__ Q,
@@ -501,11 +512,6 @@ __global__ __launch_bounds__(FQ_T) __attribute__((amdgpu_waves_per_eu(2, 2))) vo
       for (int i = 0; i < NX; ++i) rec[4 + i] = sx[i];
     }
     return;
-  }
-  if (a.sqp && a.sqp_first) {
-    // X_pred[0] = x0 (gp_mpc.py:263): the unshifted plan starts at the last state
-    if (tid < NX) Xw[tid] = sx[tid];
-    __syncthreads();
   }
   FleetRegs R;
   fq_init_pattern(a.pt, R, n);
@@ -1047,6 +1053,9 @@ extern "C" int gpmpc_fleet_step_phases(gpmpc_fleet *f, int phase_mask) {
     return -2;
   }
   GPMPC_HIP(hipSetDevice(f->ctx->device));
+  if (f->cfg.sqp_iters > 1 && f->sqp_it == 0 && (phase_mask & 3))
+    hipLaunchKernelGGL(k_fleet_x0_to_plan, dim3((f->B * NX + 255) / 256), dim3(256), 0, f->ctx->stream, f->B,
+                       f->cfg.horizon, f->x.as<double>(), f->rec.as<double>(), f->Xw.as<double>());
   // the dispatch order of this step, before the GP phase when there is one:
   // the posterior rows then follow the same slots as the control workgroups
   const bool order_now = f->use_order && f->sqp_it == 0 &&

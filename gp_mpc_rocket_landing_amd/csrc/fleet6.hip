@@ -1640,6 +1640,8 @@ extern "C" int gpmpc_rollout6_get_state(gpmpc_rollout6 *r, double *U, double *X_
   return 0;
 }
 
+extern "C" double *gpmpc_rollout6_records_dev(gpmpc_rollout6 *r) { return r ? r->rec.as<double>() : nullptr; }
+
 extern "C" int gpmpc_rollout6_set_state(gpmpc_rollout6 *r, const double *U, const double *y_scaled,
                                         const double *rho) {
   GPMPC_CHECK_ARG(r);

@@ -66,7 +66,7 @@ def main(argv=None):
     import torch.distributed as dist
     from .. import _lib
     from ..fleet import REC_OUTCOME, Fleet, fit_gp, initial_conditions
-    from ..sharding import gather_records, shard_range
+    from ..sharding import RCCLRecordGather, gather_records, shard_range
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -102,7 +102,12 @@ def main(argv=None):
         t = torch.tensor([el], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t[0])
-        allrec = gather_records(rec, args.landings, device="cuda")
+        if os.environ.get("GPMPC_GATHER", "rccl") == "torch":
+            allrec = gather_records(rec, args.landings, device="cuda")
+        else:  # the C-ABI's ncclGather of the device records (gpmpc_gather_results)
+            g = RCCLRecordGather(ctx)
+            allrec = g.gather(fl.records_dev, args.landings)
+            g.close()
     else:
         allrec = rec
     if rank == 0:

@@ -103,6 +103,10 @@ class Rollouts6:
     def step(self, nsteps=1):
         _lib._chk(_lib._L.gpmpc_rollout6_step(self.h, int(nsteps)), "rollout6_step")
 
+    @property
+    def records_dev(self):
+        return _lib._L.gpmpc_rollout6_records_dev(self.h)
+
     def read(self):
         rec = np.empty((self.batch, _lib.REC_LEN)); x = np.empty((self.batch, NX6))
         _lib._chk(_lib._L.gpmpc_rollout6_read(self.h, _lib._d(rec), _lib._d(x)), "rollout6_read")

@@ -343,6 +343,27 @@ int gpmpc_rollout6_destroy(gpmpc_rollout6 *r);
 
 /* device pointer of the record array (for collectives) */
 double *gpmpc_fleet_records_dev(gpmpc_fleet *f);
+double *gpmpc_rollout6_records_dev(gpmpc_rollout6 *r);
+
+/* ---- (e) the one collective: shard records to the root over RCCL -----------
+ * SURVEY 8b gpmpc_gather_results.  Landings are sharded in contiguous blocks,
+ * one process per GPU, with no data-path collective (monte_carlo.py:401-583 is
+ * per landing); at the end one ncclGather over xGMI brings every rank's record
+ * block to the root.  The communicator is bootstrapped from a ncclUniqueId
+ * that rank 0 creates (gpmpc_comm_unique_id) and the caller distributes (a
+ * file on local disk, or the process group it already has).  RCCL is loaded at
+ * run time (librccl.so.1; the copy torch loaded when there is one). */
+typedef struct gpmpc_comm gpmpc_comm;
+#define GPMPC_COMM_ID_BYTES 128
+int gpmpc_comm_unique_id(unsigned char *id /* GPMPC_COMM_ID_BYTES */);
+int gpmpc_comm_init(gpmpc_ctx *ctx, const unsigned char *id, int nranks, int rank, gpmpc_comm **out);
+int gpmpc_comm_destroy(gpmpc_comm *c);
+/* d_records: this rank's counts[rank] x GPMPC_REC_LEN records (device, e.g.
+ * gpmpc_fleet_records_dev); counts: every rank's shard size (host, nranks).
+ * On the root, out (host) receives sum(counts) x GPMPC_REC_LEN doubles in
+ * rank order; elsewhere out may be NULL.  Collective: every rank calls it. */
+int gpmpc_gather_results(gpmpc_ctx *ctx, gpmpc_comm *c, const double *d_records, const int *counts, int root,
+                         double *out);
 int gpmpc_fleet_destroy(gpmpc_fleet *f);
 
 #ifdef __cplusplus

@@ -181,6 +181,7 @@ def _sqp_landing_step(st, S, max_steps, dt, cfg, use_gp, residual_model, sqp_ite
     out = dict(x=x, Xw=Xw, Uw=Uw, y=S["y"].copy(), rho=float(S["rho"]), rec=rec)
     if rec[0] != 0:
         return out, None
+    Xw[0] = x          # X_pred[0] = x0 (gp_mpc.py:263): the unshifted plan starts at the state
     o = TIMEOUT if rec[1] >= max_steps else pre_step_outcome(x, m0, cfg)
     if o:
         rec[0] = o
@@ -192,7 +193,6 @@ def _sqp_landing_step(st, S, max_steps, dt, cfg, use_gp, residual_model, sqp_ite
     qp = admm_ref.RefQP(len(out["y"]), settings=qp_settings)
     qp.y = out["y"]; qp.rho = np.array([out["rho"]])
     info = None
-    Xw[0] = x          # X_pred[0] = x0 (gp_mpc.py:263): the unshifted plan starts at the last state
     for it in range(sqp_iters):
         mean = None
         if use_gp:

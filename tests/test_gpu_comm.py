@@ -1,0 +1,44 @@
+"""The C-ABI gather (gpmpc_comm_* / gpmpc_gather_results) on
+the GPU box's one device: a world of one exercises the RCCL bootstrap
+(unique id, ncclCommInitRank), the device-side padding of a ragged shard and
+the ncclGather itself; the ragged multi-rank compaction is the same code as
+the gloo-tested Python path (tests/test_sharding.py) and runs at N > 1 in
+the driver's multi-GPU bench."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def test_rccl_gather_fleet_records_world1(gpu_ctx):
+    from gp_mpc_rocket_landing_amd.fleet import Fleet, fit_gp, initial_conditions
+    from gp_mpc_rocket_landing_amd.sharding import RCCLRecordGather
+    gp = fit_gp(gpu_ctx, n_train=200)
+    fl = Fleet(gpu_ctx, gp, 37)
+    g = RCCLRecordGather(gpu_ctx)
+    try:
+        fl.reset(initial_conditions(37))
+        fl.step(5)
+        rec, _ = fl.read()
+        out = g.gather(fl.records_dev, 37)
+        np.testing.assert_array_equal(out, rec)
+        assert (g.world, g.rank) == (1, 0)
+    finally:
+        g.close()
+        fl.close()
+
+
+def test_rccl_gather_rollout6_records_world1(gpu_ctx):
+    from gp_mpc_rocket_landing_amd.rollouts6 import Rollouts6, fit_structured_fitc, initial_conditions_6dof
+    from gp_mpc_rocket_landing_amd.sharding import RCCLRecordGather
+    gv, gw = fit_structured_fitc(gpu_ctx, n_train=300, n_inducing=50)
+    ro = Rollouts6(gpu_ctx, gv, gw, 5)
+    g = RCCLRecordGather(gpu_ctx)
+    try:
+        ro.reset(initial_conditions_6dof(5))
+        ro.step(3)
+        rec, _ = ro.read()
+        np.testing.assert_array_equal(g.gather(ro.records_dev, 5), rec)
+    finally:
+        g.close()
+        ro.close()

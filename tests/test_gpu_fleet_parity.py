@@ -371,11 +371,16 @@ def test_fleet_sqp_mode_matches_oracle(gpu_ctx):
                     np.testing.assert_array_equal(got["rec"][[0, 1, 11, 12, 13, 14]],
                                                   want["rec"][[0, 1, 11, 12, 13, 14]], err_msg=str(tag))
                     moved += int(got["rec"][1] > S["rec"][b, 1])
+                    # the tight case runs up to 100 passes x 2000 ADMM iterations per control step:
+                    # the device's summation orders drift the continuous state by up to ~1e-5
+                    # relative over that many iterations (integer outputs stay exact)
+                    rt = 1e-4 if sq else 1e-6
                     for key in ("x", "Xw", "Uw"):
-                        ok, worst = close(got[key], want[key], 1.0)
+                        ok, worst = close(got[key], want[key], 1.0, rtol=rt)
                         assert ok, (tag, key, worst)
-                    ok, worst = close(got["rho"], want["rho"], 0.0); assert ok, (tag, "rho", worst)
-                    ok, worst = close(got["y"], want["y"], np.abs(want["y"]).max()); assert ok, (tag, "y", worst)
+                    ok, worst = close(got["rho"], want["rho"], 0.0, rtol=rt); assert ok, (tag, "rho", worst)
+                    ok, worst = close(got["y"], want["y"], np.abs(want["y"]).max(), rtol=rt)
+                    assert ok, (tag, "y", worst)
                 S = T
         finally:
             fl.close()
