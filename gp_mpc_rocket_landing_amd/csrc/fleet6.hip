@@ -37,6 +37,7 @@
 // block of each equality row lives in its owner's registers, a column copy in
 // the variable owner's; only the factor and the cross-thread vectors are LDS.
 #include "internal.h"
+#include "gemm.h"
 #include "qp.h"
 #include <vector>
 
@@ -53,7 +54,7 @@
 #define R6_M (R6_MD + R6_NV + R6_MGEN)        // 1104 rows
 #define R6_T 512                              // two items (variables / rows) per thread
 #define R6_TRI 153                            // packed lower 17 x 17
-#define R6_PT 256                             // predict threads
+#define R6_PT 512                             // predict threads (7 kernel-row waves + the RK4 wave)
 #define R6_FOR_H _Pragma("unroll") for (int h = 0; h < 2; ++h)
 
 // Rocket6DoFConfig (rocket_6dof.py:36-84), ConstraintParams (constraints.py:35-50),
@@ -110,15 +111,8 @@ extern "C" void gpmpc_rollout6_default_config(gpmpc_rollout6_config *c) {
 }
 
 // beta^T = alpha^T L_uu^-1 (3 x M): the FITC posterior mean is K*u beta.
-// W = L_uu^-1 (lower, row-major, ld M) is the fit's first M rows of core.W.
-__global__ void k_fitc_beta(int M, const double *__restrict__ W, const double *__restrict__ alphaT,
-                            double *__restrict__ betaT) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x, c = blockIdx.y;
-  if (i >= M) return;
-  double acc = 0.0;
-  for (int j = i; j < M; ++j) acc = fma(alphaT[(int64_t)c * M + j], W[(int64_t)j * M + i], acc);
-  betaT[(int64_t)c * M + i] = acc;
-}
+// W = L_uu^-1 (lower, row-major, ld M) is the fit's first M rows of core.W; the
+// product is one FP64-MFMA NN GEMM (a thread-per-column loop took 614 us at M = 2000)
 
 // ---------------------------------------------------------------------------
 // dynamics (nominal_mpc.py:163-203)
@@ -211,20 +205,26 @@ __device__ void r6_neg_lin(const double *x, const double *u, double dt, double *
 
 // ---------------------------------------------------------------------------
 // StructuredRocketGP features (features.py:196-263, :304-356), scaled by the GP's
-// lengthscales, and their squared norm (the k_scale_rows arithmetic)
-__device__ void r6_features(const double *x, const double *u, const double *lsv, const double *lsw,
-                            double *zv, double *zw, double *nv, double *nw) {
-  const double alt = x[1], vx = x[4], vy = x[5], vz = x[6];
-  const double speed = sqrt((vx * vx + vy * vy) + vz * vz);
-  const double rho = 1.225 * exp(-alt / 8500.0);
-  const double qd = 0.5 * rho * speed * speed;
+// lengthscales, and their squared norm (the k_scale_rows arithmetic).  The two
+// sets are separate functions so that two waves compute them side by side.
+__device__ __forceinline__ void r6_body_velocity(const double *x, double *vb, double &speed) {
+  const double vx = x[4], vy = x[5], vz = x[6];
+  speed = sqrt((vx * vx + vy * vy) + vz * vz);
   // body-from-inertial DCM (features.py:265-270)
   const double w = x[7], qx = x[8], qy = x[9], qz = x[10];
   const double Cb[3][3] = {{1 - 2 * (qy * qy + qz * qz), 2 * (qx * qy + w * qz), 2 * (qx * qz - w * qy)},
                            {2 * (qx * qy - w * qz), 1 - 2 * (qx * qx + qz * qz), 2 * (qy * qz + w * qx)},
                            {2 * (qx * qz + w * qy), 2 * (qy * qz - w * qx), 1 - 2 * (qx * qx + qy * qy)}};
-  double vb[3];
   for (int i = 0; i < 3; ++i) vb[i] = (Cb[i][0] * vx + Cb[i][1] * vy) + Cb[i][2] * vz;
+}
+
+// translational features (13)
+__device__ void r6_features_v(const double *x, const double *u, const double *lsv, double *zv, double *nv) {
+  double vb[3], speed;
+  r6_body_velocity(x, vb, speed);
+  const double alt = x[1], vx = x[4], vy = x[5], vz = x[6];
+  const double rho = 1.225 * exp(-alt / 8500.0);
+  const double qd = 0.5 * rho * speed * speed;
   const bool moving = speed > 1e-3;
   const double safe = moving ? speed : 1.0;
   double sb = vb[1] / safe;
@@ -235,14 +235,23 @@ __device__ void r6_features(const double *x, const double *u, const double *lsv,
   const double qn = 0.5 * 1.225 * 100.0;
   const double fv[13] = {vx / 10.0, vy / 10.0, vz / 10.0, speed / 10.0, qd / qn, aoa, beta,
                          u[0] / 10.0, u[1] / 10.0, u[2] / 10.0, tm / 10.0, alt / 100.0, rho / 1.225};
+  double s = 0.0;
+  for (int k = 0; k < 13; ++k) { zv[k] = fv[k] / lsv[k]; s += zv[k] * zv[k]; }
+  *nv = s;
+}
+
+// rotational features (12)
+__device__ void r6_features_w(const double *x, const double *u, const double *lsw, double *zw, double *nw) {
+  double vb[3], speed;
+  r6_body_velocity(x, vb, speed);
+  const double rho = 1.225 * exp(-x[1] / 8500.0);
+  const double qd = 0.5 * rho * speed * speed;
+  const double qn = 0.5 * 1.225 * 100.0;
   const double wxx = x[11], wyy = x[12], wzz = x[13];
   const double wm = sqrt((wxx * wxx + wyy * wyy) + wzz * wzz);
   const double fw[12] = {wxx, wyy, wzz, wm, u[0] / 10.0, u[1] / 10.0, u[2] / 10.0,
                          vb[0] / 10.0, vb[1] / 10.0, vb[2] / 10.0, speed / 10.0, qd / qn};
   double s = 0.0;
-  for (int k = 0; k < 13; ++k) { zv[k] = fv[k] / lsv[k]; s += zv[k] * zv[k]; }
-  *nv = s;
-  s = 0.0;
   for (int k = 0; k < 12; ++k) { zw[k] = fw[k] / lsw[k]; s += zw[k] * zw[k]; }
   *nw = s;
 }
@@ -280,12 +289,56 @@ struct R6Args {
 
 // ---------------------------------------------------------------------------
 // 1. termination rules + forward simulation with the GP mean
+// sum over the inducing rows i = t0, t0 + stride, .. of k(z, x_i) coef[c][i] (c < 3),
+// two rows per trip with all their loads issued before either is used
+template <int D>
+__device__ __forceinline__ void r6_kernel_rows(const GpView &v, int M, const double *__restrict__ cf,
+                                               const double *zs, double zn, int t0, int stride, double *acc) {
+  double z[D];
+#pragma unroll
+  for (int f = 0; f < D; ++f) z[f] = zs[f];
+  const double *__restrict__ Xs = v.Xs;
+  const double *__restrict__ Xn = v.Xn;
+  int i = t0;
+  for (; i + stride < M; i += 2 * stride) {
+    const int j = i + stride;
+    double xa[D], xb[D], ca[3], cb[3];
+#pragma unroll
+    for (int f = 0; f < D; ++f) { xa[f] = Xs[(int64_t)i * D + f]; xb[f] = Xs[(int64_t)j * D + f]; }
+    const double na = Xn[i], nb = Xn[j];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) { ca[c] = cf[(int64_t)c * M + i]; cb[c] = cf[(int64_t)c * M + j]; }
+    double da = 0.0, db = 0.0;
+#pragma unroll
+    for (int f = 0; f < D; ++f) { da = fma(z[f], xa[f], da); db = fma(z[f], xb[f], db); }
+    const double ka = kernel_epilogue(GPMPC_SE_ARD, (zn + na) - 2.0 * da, v.sigma2, 0.0);
+    const double kb = kernel_epilogue(GPMPC_SE_ARD, (zn + nb) - 2.0 * db, v.sigma2, 0.0);
+#pragma unroll
+    for (int c = 0; c < 3; ++c) { acc[c] += ka * ca[c]; acc[c] += kb * cb[c]; }
+  }
+  if (i < M) {
+    double dot = 0.0;
+#pragma unroll
+    for (int f = 0; f < D; ++f) dot = fma(z[f], Xs[(int64_t)i * D + f], dot);
+    const double kv = kernel_epilogue(GPMPC_SE_ARD, (zn + Xn[i]) - 2.0 * dot, v.sigma2, 0.0);
+#pragma unroll
+    for (int c = 0; c < 3; ++c) acc[c] += kv * cf[(int64_t)c * M + i];
+  }
+}
+
 // diagnostic phase cycles of the predict kernel's rollout 0 (GPMPC_R6_STAMPS=1)
 __device__ unsigned long long g_r6p_stamps[4];
 
+// Per horizon point k (the points are sequential: X[k+1] needs the GP mean at X[k]):
+//   waves 0 .. R6_PT/64 - 2: the 2 x M kernel rows of both GPs (K*u . coefficients);
+//   the last wave, lane 0, meanwhile: RK4(X[k], U[k]) (the GP mean is added after);
+//   barrier; lanes 0 of waves 0 and 1: the means, X[k+1] = RK4 + [.., d_v dt, .., d_w dt],
+//   then the translational (wave 0) and rotational (wave 1) features of point k+1;
+//   barrier.
 template <bool ST>
 __global__ __launch_bounds__(R6_PT) void k_r6_predict(R6Args a) {
-  const int b = blockIdx.x, tid = threadIdx.x;
+  const int b = blockIdx.x, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  constexpr int NW = R6_PT / 64, NRT = R6_PT - 64;  // waves; kernel-row threads
   unsigned long long tl = 0;
   auto mark = [&](int k) {
     if (ST && b == 0 && tid == 0) {
@@ -298,7 +351,8 @@ __global__ __launch_bounds__(R6_PT) void k_r6_predict(R6Args a) {
   if (a.mode == 0 ? rec[0] != 0.0 : a.done[b] != 0) return;
   __shared__ double X[R6_N + 1][R6_NX];
   __shared__ double zq[2][16], zn[2];
-  __shared__ double red[R6_PT / 64][6];
+  __shared__ double red[NW][6];
+  __shared__ double xrk[R6_NX];
   __shared__ int s_out;
   const double dt = a.dt;
   const bool relin = a.mode == 2;  // a later GPMPC.solve pass: X_pred = the last plan
@@ -333,52 +387,64 @@ __global__ __launch_bounds__(R6_PT) void k_r6_predict(R6Args a) {
   __syncthreads();
   if (s_out) return;
   const double *Ub = a.U + (int64_t)b * R6_N * R6_NU;
+  const bool feat_lane = lane == 0 && wave < 2;
+  // features of point 0
+  if (a.use_gp && feat_lane) {
+    if (wave == 0) r6_features_v(X[0], Ub, a.gv.ls, zq[0], &zn[0]);
+    else r6_features_w(X[0], Ub, a.gw.ls, zq[1], &zn[1]);
+  }
+  __syncthreads();
   mark(-1);
   for (int k = 0; k < R6_N; ++k) {
-    if (tid == 0 && a.use_gp)
-      r6_features(X[k], Ub + k * R6_NU, a.gv.ls, a.gw.ls, zq[0], zq[1], &zn[0], &zn[1]);
-    __syncthreads();
-    mark(0);
-    // K*u alpha of both GPs: the expansion form of the gram kernel (same bits
-    // per kernel value); 3 outputs each
+    // K*u . coefficients of both GPs: the expansion form of the gram kernel (same
+    // bits per kernel value); 3 outputs each
     double acc[6] = {0, 0, 0, 0, 0, 0};
-    for (int g = 0; g < (a.use_gp ? 2 : 0); ++g) {
-      const GpView &v = g ? a.gw : a.gv;
-      const int M = g ? a.Mw : a.Mv, d = g ? 12 : 13;
-      for (int i = tid; i < M; i += R6_PT) {
-        double dot = 0.0;
-        for (int f = 0; f < d; ++f) dot = fma(zq[g][f], v.Xs[(int64_t)i * d + f], dot);
-        const double d2 = (zn[g] + v.Xn[i]) - 2.0 * dot;
-        const double kv = kernel_epilogue(GPMPC_SE_ARD, d2, v.sigma2, 0.0);
-        const double *cf = g ? a.cw : a.cv;
-        for (int c = 0; c < 3; ++c) acc[3 * g + c] += kv * cf[(int64_t)c * M + i];
+    if (tid < NRT) {
+      if (a.use_gp) {
+        r6_kernel_rows<13>(a.gv, a.Mv, a.cv, zq[0], zn[0], tid, NRT, acc);
+        r6_kernel_rows<12>(a.gw, a.Mw, a.cw, zq[1], zn[1], tid, NRT, acc + 3);
       }
+#pragma unroll
+      for (int c = 0; c < 6; ++c)
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) acc[c] += __shfl_xor(acc[c], o);
+      if (lane == 0)
+#pragma unroll
+        for (int c = 0; c < 6; ++c) red[wave][c] = acc[c];
+    } else if (!relin && lane == 0) {  // _predict_with_gp's nominal step (gp_mpc.py:156)
+      double xn[R6_NX];
+      r6_step(X[k], Ub + k * R6_NU, dt, xn);
+      for (int i = 0; i < R6_NX; ++i) xrk[i] = xn[i];
     }
-    mark(1);
-    for (int c = 0; c < 6; ++c)
-      for (int o = 32; o > 0; o >>= 1) acc[c] += __shfl_xor(acc[c], o);
-    if ((tid & 63) == 0)
-      for (int c = 0; c < 6; ++c) red[tid >> 6][c] = acc[c];
     __syncthreads();
-    mark(2);
-    if (tid == 0) {
+    mark(1);
+    if (feat_lane) {
       double gmk[6];
       for (int c = 0; c < 6; ++c) {
-        double s = 0.0;
-        for (int w = 0; w < R6_PT / 64; ++w) s += red[w][c];
+        double sm = 0.0;
+        for (int w = 0; w < NW - 1; ++w) sm += red[w][c];
         const GpView &v = c < 3 ? a.gv : a.gw;
-        gmk[c] = a.use_gp ? s * v.ystd[c % 3] + v.ymean[c % 3] : 0.0;
-        a.gm[((int64_t)b * R6_N + k) * 6 + c] = gmk[c];
+        gmk[c] = a.use_gp ? sm * v.ystd[c % 3] + v.ymean[c % 3] : 0.0;
       }
-      if (!relin) {  // _predict_with_gp (gp_mpc.py:139-175)
-        double xn[R6_NX];
-        r6_step(X[k], Ub + k * R6_NU, dt, xn);
+      double xn[R6_NX];
+      if (relin) {
+        for (int i = 0; i < R6_NX; ++i) xn[i] = X[k + 1][i];
+      } else {  // gp_mpc.py:166-168
+        for (int i = 0; i < R6_NX; ++i) xn[i] = xrk[i];
         for (int i = 0; i < 3; ++i) { xn[4 + i] += gmk[i] * dt; xn[11 + i] += gmk[3 + i] * dt; }
-        for (int i = 0; i < R6_NX; ++i) X[k + 1][i] = xn[i];
+      }
+      if (wave == 0) {
+        for (int c = 0; c < 6; ++c) a.gm[((int64_t)b * R6_N + k) * 6 + c] = gmk[c];
+        if (!relin)
+          for (int i = 0; i < R6_NX; ++i) X[k + 1][i] = xn[i];
+      }
+      if (a.use_gp && k + 1 < R6_N) {  // the next point's features, from this lane's own copy of X[k+1]
+        if (wave == 0) r6_features_v(xn, Ub + (k + 1) * R6_NU, a.gv.ls, zq[0], &zn[0]);
+        else r6_features_w(xn, Ub + (k + 1) * R6_NU, a.gw.ls, zq[1], &zn[1]);
       }
     }
     __syncthreads();
-    mark(3);
+    mark(0);
   }
   for (int e = tid; e < (R6_N + 1) * R6_NX; e += R6_PT)
     a.Xp[(int64_t)b * (R6_N + 1) * R6_NX + e] = (&X[0][0])[e];
@@ -1466,10 +1532,14 @@ static int r6_create(gpmpc_ctx *ctx, const GpView &gv, const GpView &gw, bool ex
   hipMemsetAsync(r->pending.p, 0, sizeof(int) * B, ctx->stream);
   hipMemsetAsync(r->done.p, 0, sizeof(int) * B, ctx->stream);
   if (!exact) {  // beta^T = alpha^T L_uu^-1: the FITC posterior mean's coefficients
-    hipLaunchKernelGGL(k_fitc_beta, dim3((gv.n + 255) / 256, 3), dim3(256), 0, ctx->stream, gv.n, gv.W,
-                       gv.alphaT, r->betav.as<double>());
-    hipLaunchKernelGGL(k_fitc_beta, dim3((gw.n + 255) / 256, 3), dim3(256), 0, ctx->stream, gw.n, gw.W,
-                       gw.alphaT, r->betaw.as<double>());
+    if (launch_gemm_nn(ctx->stream, 3, gv.n, gv.n, gv.alphaT, gv.n, gv.W, gv.n, r->betav.as<double>(), gv.n, 1.0,
+                       0.0) != hipSuccess ||
+        launch_gemm_nn(ctx->stream, 3, gw.n, gw.n, gw.alphaT, gw.n, gw.W, gw.n, r->betaw.as<double>(), gw.n, 1.0,
+                       0.0) != hipSuccess) {
+      delete r;
+      gpmpc_set_error("rollout6: beta GEMM launch failed");
+      return -1;
+    }
   }
   static bool attr = [] {
     (void)hipFuncSetAttribute((const void *)k_r6_control<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -1668,8 +1738,7 @@ extern "C" int gpmpc_rollout6_destroy(gpmpc_rollout6 *r) {
     }
     unsigned long long hp[4] = {0};
     if (hipMemcpyFromSymbol(hp, HIP_SYMBOL(g_r6p_stamps), sizeof(hp)) == hipSuccess)
-      fprintf(stderr, "r6 predict stamps: features %llu kernel_rows %llu reduce %llu rk4 %llu\n", hp[0], hp[1],
-              hp[2], hp[3]);
+      fprintf(stderr, "r6 predict stamps: kernel rows + rk4 %llu means + next features %llu\n", hp[1], hp[0]);
   }
   delete r;
   return 0;
