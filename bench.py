@@ -471,12 +471,31 @@ def gpmpc_loop_bench(ctx, gp, batch=1024, reps=3, sqp_iters=10):
     return out
 
 
-def rollouts6_bench(ctx, batches=(64, 512), max_steps=300):
+def r6_admm_flops(N=30, nx=14, nu=3):
+    """Algorithmic fp64 flop of the 6-DoF QP (csrc/fleet6.hip; FMA = 2): per ADMM
+    iteration (A'(rho z - y) and A x~ over the constraint non-zeros, the block-
+    tridiagonal KKT solve: forward G products, 31 diagonal S^-1 products,
+    backward G^T products, ~10 vector ops per variable and row), and per
+    factorisation (assembly of P + sigma I + A'RA per stage block, Gauss-Jordan
+    S^-1, G = C S^-1, the Schur update)."""
+    sz = nx + nu
+    n, m = N * sz + nx, nx * (N + 1) + (N * sz + nx) + N + 4 * (N - 1)
+    nnz = nx + N * nx * (sz + 1) + n + 3 * N + 2 * 4 * (N - 1)
+    kkt = 2 * (N * nx * sz) + 2 * ((N + 1) * sz * sz) + 2 * (N * sz * nx)
+    it = 2 * 2 * nnz + kkt + 10 * (n + m)
+    fac = (N + 1) * (2 * sz ** 3 + 2 * nx * sz * sz + 2 * nx * nx * sz + 2 * nx * sz * sz)
+    return it, fac
+
+
+def rollouts6_bench(ctx, torch=None, batches=(64, 512), max_steps=300):
     """BASELINE configs[4]: 6-DoF GP-MPC rollouts, N = 30, the StructuredRocketGP
     FITC pair at M = 2000 inducing / N = 4000 training rows (csrc/fleet6.hip).
     Every rollout flies to termination (run_experiments initial conditions + a
     random tilt); 64 = one GPU's share of the config's 512 over 8 GPUs, 512 =
-    the whole config on one GPU.  The GP fit is outside the timed region."""
+    the whole config on one GPU.  The GP fit (host kmeans2 + two device FITC
+    fits) is outside the timed region.  Then, untimed: per-kernel times of the
+    64-rollout batch (HIP events around each phase on the context stream) with
+    the control kernel's roofline object, and the QP status of every solve."""
     from gp_mpc_rocket_landing_amd.rollouts6 import Rollouts6, fit_structured_fitc, initial_conditions_6dof
     t0 = time.perf_counter()
     gv, gw = fit_structured_fitc(ctx, n_train=4000, n_inducing=2000)
@@ -509,6 +528,60 @@ def rollouts6_bench(ctx, batches=(64, 512), max_steps=300):
                        "mean_steps_per_rollout": round(ctrl / B, 1),
                        "admm_iters_per_solve": round(float(rec[:, 11].sum()) / max(ctrl, 1.0), 2),
                        "outcomes": {str(int(c)): int(np.sum(rec[:, 0] == c)) for c in np.unique(rec[:, 0])}}
+    # per-kernel times (first 20 steps of 64 rollouts) and the QP status of every solve
+    B = batches[0]
+    ro = Rollouts6(ctx, gv, gw, B, max_steps=max_steps)
+    names = {1: "solved", 2: "solved_inaccurate", -2: "max_iter_reached", -3: "primal_infeasible",
+             3: "primal_infeasible_inaccurate", -4: "dual_infeasible", 4: "dual_infeasible_inaccurate",
+             -100: "kkt_factor_failed"}
+    hist = {}
+    try:
+        ro.reset(initial_conditions_6dof(B))
+        ph = []
+        if torch is not None:
+            stream = torch.cuda.ExternalStream(ctx.stream)
+            ev = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(20)]
+            for k in range(20):
+                ev[k][0].record(stream); ro.phases(1)
+                ev[k][1].record(stream); ro.phases(2)
+                ev[k][2].record(stream); ro.phases(4)
+                ev[k][3].record(stream)
+            ctx.sync()
+            ph = np.array([[ev[k][i].elapsed_time(ev[k][i + 1]) for i in range(3)] for k in range(20)]) * 1e-3
+        ro.reset(initial_conditions_6dof(B))
+        rec0, _ = ro.read()
+        for _ in range(max_steps + 1):
+            ro.step(1)
+            rec1, _ = ro.read()
+            failed = (rec1[:, 0] == 6) & ~np.isin(rec1[:, 14], (1, 2, -2))   # a solve without a solution
+            adv = (rec0[:, 0] == 0) & ((rec1[:, 1] > rec0[:, 1]) | failed)
+            for s_, c in zip(*np.unique(rec1[adv, 14].astype(int), return_counts=True)):
+                k = names.get(int(s_), str(int(s_)))
+                hist[k] = hist.get(k, 0) + int(c)
+            rec0 = rec1
+            if np.all(rec1[:, 0] != 0):
+                break
+    finally:
+        ro.close()
+    tot = max(1, sum(hist.values()))
+    out["qp_status"] = {"rollouts": B, "solves": tot, "status": hist,
+                        "status_frac": {k: round(v / tot, 4) for k, v in hist.items()}}
+    if len(ph):
+        pm = ph.mean(axis=0)
+        it_f, fac_f = r6_admm_flops()
+        iters = float(out[str(B)]["admm_iters_per_solve"])
+        # per control launch: B solves x (iterations x per-iteration flop + ~2 factorisations)
+        ctl_flop = B * (iters * it_f + 2.0 * fac_f)
+        tr, tr_src = pmc_traffic("k_r6_control")
+        out["kernels"] = {"predict": {"kernel": "k_r6_predict<false>", "ms": round(pm[0] * 1e3, 4)},
+                          "control": {"kernel": "k_r6_control<false>", "ms": round(pm[1] * 1e3, 4)},
+                          "plant": {"kernel": "k_r6_plant", "ms": round(pm[2] * 1e3, 4)}}
+        out["roofline"] = {"kernel": "k_r6_control<false>", "bound": "mfma", "achieved": round(ctl_flop / pm[1] / 1e12, 5),
+                           "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+                           "frac": round(ctl_flop / pm[1] / 1e12 / FP64_PEAK_TFLOPS, 5),
+                           "traffic": tr, "traffic_source": tr_src,
+                           "per_launch": f"{B} solves x (iterations x {it_f} + 2 x {fac_f}) fp64 flop",
+                           "limiter": "latency: serial block-tridiagonal KKT chains (31 stage blocks), one rollout per CU"}
     return out
 
 
@@ -706,7 +779,7 @@ def main():
                 out["simple3dof_gp"] = simple3dof_gp_bench(ctx, cpu=not args.no_cpu)
                 out["cholesky"] = cholesky_bench(ctx, torch)
                 out["structured_fitc"] = structured_fitc_bench(ctx)
-                out["rollouts6"] = rollouts6_bench(ctx)
+                out["rollouts6"] = rollouts6_bench(ctx, torch)
                 out["lml_batched"] = lml_bench(ctx, cpu=not args.no_cpu)
                 out["gp_append"] = append_bench(ctx)
             except Exception as e:  # noqa: BLE001

@@ -145,6 +145,7 @@ _sig("gpmpc_comm_destroy", _c, _vp)
 _sig("gpmpc_gather_results", _c, _vp, _vp, _vp, _ip, _c, _dp)
 _sig("gpmpc_rollout6_reset", _c, _vp, _c, _c, _dp)
 _sig("gpmpc_rollout6_step", _c, _vp, _c)
+_sig("gpmpc_rollout6_step_phases", _c, _vp, _c)
 _sig("gpmpc_rollout6_read", _c, _vp, _dp, _dp)
 _sig("gpmpc_rollout6_get_state", _c, _vp, _dp, _dp, _dp, _dp, _dp, _dp)
 _sig("gpmpc_rollout6_destroy", _c, _vp)
@@ -164,7 +165,7 @@ EXPORTED = ["gpmpc_abi_version", "gpmpc_last_error", "gpmpc_ctx_create", "gpmpc_
             "gpmpc_rollout6_get_state", "gpmpc_rollout6_destroy", "gpmpc_rollout6_create_exact",
             "gpmpc_rollout6_solve", "gpmpc_rollout6_set_state", "gpmpc_fitc_get_state",
             "gpmpc_rollout6_records_dev", "gpmpc_comm_unique_id", "gpmpc_comm_init", "gpmpc_comm_destroy",
-            "gpmpc_gather_results"]
+            "gpmpc_gather_results", "gpmpc_rollout6_step_phases"]
 
 
 class HIPError(RuntimeError):

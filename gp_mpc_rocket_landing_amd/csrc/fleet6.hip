@@ -1638,18 +1638,29 @@ static bool r6_stamps_on() {
   return on;
 }
 
-extern "C" int gpmpc_rollout6_step(gpmpc_rollout6 *r, int nsteps) {
-  GPMPC_CHECK_ARG(r && nsteps >= 0);
+extern "C" int gpmpc_rollout6_step_phases(gpmpc_rollout6 *r, int mask) {
+  GPMPC_CHECK_ARG(r);
   GPMPC_HIP(hipSetDevice(r->ctx->device));
   hipStream_t s = r->ctx->stream;
   const R6Args a = r6_args(r);
-  for (int it = 0; it < nsteps; ++it) {
+  if (mask & 1) {
     if (r6_stamps_on()) hipLaunchKernelGGL(k_r6_predict<true>, dim3(r->B), dim3(R6_PT), 0, s, a);
     else hipLaunchKernelGGL(k_r6_predict<false>, dim3(r->B), dim3(R6_PT), 0, s, a);
+  }
+  if (mask & 2) {
     if (r6_stamps_on()) hipLaunchKernelGGL(k_r6_control<true>, dim3(r->B), dim3(R6_T), sizeof(R6Smem), s, a);
     else hipLaunchKernelGGL(k_r6_control<false>, dim3(r->B), dim3(R6_T), sizeof(R6Smem), s, a);
-    hipLaunchKernelGGL(k_r6_plant, dim3((r->B + 63) / 64), dim3(64), 0, s, a, r->B);
-    GPMPC_HIP(hipGetLastError());
+  }
+  if (mask & 4) hipLaunchKernelGGL(k_r6_plant, dim3((r->B + 63) / 64), dim3(64), 0, s, a, r->B);
+  GPMPC_HIP(hipGetLastError());
+  return 0;
+}
+
+extern "C" int gpmpc_rollout6_step(gpmpc_rollout6 *r, int nsteps) {
+  GPMPC_CHECK_ARG(r && nsteps >= 0);
+  for (int it = 0; it < nsteps; ++it) {
+    const int rc = gpmpc_rollout6_step_phases(r, 7);
+    if (rc) return rc;
   }
   return 0;
 }

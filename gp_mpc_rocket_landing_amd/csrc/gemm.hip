@@ -85,6 +85,23 @@ __global__ __launch_bounds__(256) void k_gemm_nt(int M, int N, int K, const doub
   for (int x = 0; x < 2; ++x)
 #pragma unroll
     for (int y = 0; y < 2; ++y) acc[x][y] = (d4_t){0.0, 0.0, 0.0, 0.0};
+  // beta != 0: C is loaded here, before the K loop, so that its latency hides under
+  // the loop instead of following it (the K = 128 Cholesky updates spent much of
+  // their epilogue waiting for it); the epilogue arithmetic is unchanged
+  const bool prec = EPI == EPI_STORE && beta != 0.0;
+  d4_t cpre[2][2];
+  if (prec) {
+#pragma unroll
+    for (int x = 0; x < 2; ++x)
+#pragma unroll
+      for (int y = 0; y < 2; ++y)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = r0 + qi + x * 16 + mf_row(lane, r);
+          const int col = c0 + qj + y * 16 + mf_col(lane);
+          cpre[x][y][r] = (row < M && col < N && (!lower_c || col <= row)) ? C[(int64_t)row * ldc + col] : 0.0;
+        }
+  }
   // each thread moves 4 consecutive k of one row of A and of B per K-step:
   // row = tid/4, k = (tid%4)*4..+3.  The next step's operands are loaded into
   // registers while the current step's MFMAs run (LDS double buffer, one
@@ -185,7 +202,7 @@ __global__ __launch_bounds__(256) void k_gemm_nt(int M, int N, int K, const doub
           const int col = c0 + qj + y * 16 + mf_col(lane);
           if (row < M && col < N && (!lower_c || col <= row)) {
             double *p = C + (int64_t)row * ldc + col;
-            *p = (beta == 0.0) ? alpha * acc[x][y][r] : alpha * acc[x][y][r] + beta * *p;
+            *p = prec ? alpha * acc[x][y][r] + beta * cpre[x][y][r] : alpha * acc[x][y][r];
           }
         }
   } else {

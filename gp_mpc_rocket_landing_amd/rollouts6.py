@@ -103,6 +103,10 @@ class Rollouts6:
     def step(self, nsteps=1):
         _lib._chk(_lib._L.gpmpc_rollout6_step(self.h, int(nsteps)), "rollout6_step")
 
+    def phases(self, mask):
+        """gpmpc_rollout6_step_phases: 1 predict, 2 control, 4 plant (7 = a step)."""
+        _lib._chk(_lib._L.gpmpc_rollout6_step_phases(self.h, int(mask)), "rollout6_step_phases")
+
     @property
     def records_dev(self):
         return _lib._L.gpmpc_rollout6_records_dev(self.h)

@@ -326,6 +326,10 @@ int gpmpc_rollout6_solve(gpmpc_rollout6 *r, const double *x0, const double *x_ta
 int gpmpc_rollout6_reset(gpmpc_rollout6 *r, int first, int count, const double *x0);
 /* nsteps control steps of every running rollout (async on the ctx stream) */
 int gpmpc_rollout6_step(gpmpc_rollout6 *r, int nsteps);
+/* one step split in its kernels, launched in order: bit 0 termination rules +
+ * forward simulation + GP means + Jacobians (k_r6_predict), bit 1 QP + ADMM +
+ * plan (k_r6_control), bit 2 truth plant step (k_r6_plant); a full step = 7 */
+int gpmpc_rollout6_step_phases(gpmpc_rollout6 *r, int mask);
 /* records (batch x GPMPC_REC_LEN, the fleet layout; state slots hold [m, r, v])
  * and the full states (batch x 14, may be NULL) */
 int gpmpc_rollout6_read(gpmpc_rollout6 *r, double *records, double *x);

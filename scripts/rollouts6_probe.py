@@ -10,4 +10,5 @@ from gp_mpc_rocket_landing_amd import _lib  # noqa: E402
 
 if __name__ == "__main__":
     batches = tuple(int(v) for v in os.environ.get("BATCHES", "64,512").split(","))
-    print(json.dumps(bench.rollouts6_bench(_lib.Context(0), batches=batches)), flush=True)
+    import torch
+    print(json.dumps(bench.rollouts6_bench(_lib.Context(0), torch, batches=batches)), flush=True)
