@@ -12,7 +12,7 @@ import os
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libgpmpc_hip.so")
+LIB_PATH = os.environ.get("GPMPC_LIB") or os.path.join(_HERE, "libgpmpc_hip.so")  # GPMPC_LIB: A/B builds
 
 SE_ARD, SE_ISO, MATERN32, MATERN52 = 0, 1, 2, 3
 ERR_NOT_PD = -100

@@ -467,14 +467,16 @@ struct R6Smem {
   double dsc[R6_NV];                  // per-pass column scaling / factor scratch
   double dpl[R6_MD];                  // each equality row's identity entry (scaled)
   double gen[R6_MGEN * 3];            // general rows' values (scaled)
-  double T[2][R6_SZ * R6_SZ];         // Gauss-Jordan block (ping-pong: one barrier per pivot)
-  double Gt[R6_NX * R6_SZ];           // G_k before it replaces C_k
-  double Sch[R6_NX * R6_NX];          // G_k C_k^T
+  // per end of the twisted sweep (0 top, 1 bottom):
+  double T[2][2][R6_SZ * R6_SZ];      // Gauss-Jordan block (ping-pong: one barrier per pivot)
+  double Ct[2][R6_NX * R6_SZ];        // the coupling C_k (top) / E_k (bottom), 14 x 17
+  double Sch[2][R6_NX * R6_NX];       // G_k C_k^T / H_k E_k^T, the next block's update
   double red[16][12];
   double zero[R6_SZ];                 // the forward chain's operand row for its pass-through lanes
+  double zmid[16];                    // the bottom chain's z'_15 = -H_15 z_16
   double dump[64];                    // the chains' store target for lanes that keep no result
   double c, rho_s;
-  int flag;
+  int flag, bad[2];
 };
 
 __device__ __forceinline__ int r6_tri(int a, int b) { return a >= b ? a * (a + 1) / 2 + b : b * (b + 1) / 2 + a; }
@@ -627,8 +629,126 @@ __device__ __forceinline__ double r6_gen_dot(const R6Var &V, const double *v) {
   return acc;
 }
 
-// assemble the block tridiagonal M = P + sigma I + A' R A and factor it:
-// returns 0 or a failing block + 1
+// The reduced KKT matrix M = P + sigma I + A' R A is block tridiagonal.  It is
+// factored from both ends at once (the 3-DoF fleet's twist, fleet_twist.h), in
+// 31 factor blocks of natural variables (r6_nat):
+//   top     k = 0..14:  the stage block [x_k, u_k], coupled to x_k+1 through
+//                       C_k (14 x 17: rho_eq dpl(k, i) g_k[i][:], stage k's dynamics rows);
+//   middle  k = 15:     x_15 alone (14 x 14);
+//   bottom  k = 16..30: [x_k, u_k-1], coupled to x_k-1 through E_k-1 (14 x 17:
+//                       x_k columns from stage k-1's dynamics rows, u_k-1
+//                       columns from stage k-1's x-u block).
+// Neither end's coupling reaches a block's entries 14-16 (u_k on top, u_k-1 at the
+// bottom), so the two ends are the same recursion, 15 block steps each:
+//   top     S_0 = D_0,   S_k+1 = D_k+1 - G_k C_k^T,      G_k = C_k S_k^-1
+//   bottom  T_30 = D_30, T_k-1 = D_k-1 - H_k-1 E_k-1^T,  H_k-1 = E_k-1 T_k^-1
+//   middle  Z = D_15 - G_14 C_14^T - H_15 E_15^T
+// -G_k goes to slot k (k < 15) and -H_k to slot k (k = 15..29) of s.G, over the
+// staged dynamics rows of its own stage once their last reader is done.
+#define R6_MID 15
+// Gauss-Jordan two pivots per barrier (0: one)
+#ifndef R6_GJ2
+#define R6_GJ2 1
+#endif
+
+__device__ __forceinline__ int r6_nat(int k, int e) {
+  return k * R6_SZ + e - ((k > R6_MID && e >= R6_NX) ? R6_SZ : 0);
+}
+
+// M entry of variables (k, a) and (k, bb) of one stage, the terms in the banded oracle's row order
+__device__ __forceinline__ double r6_m_stage(const R6Smem &s, int k, int a, int bb, double re, double rs) {
+  double v = 0.0;
+  if (a == bb) {
+    v = s.dsc[k * R6_SZ + a];
+    if (a < R6_NX) {
+      const int r = r6_eqid_row(k, a);
+      v += re * s.dpl[r] * s.dpl[r];
+    }
+  }
+  if (k < R6_N) {
+    const double *g = s.G + k * R6_NX * R6_SZ;
+    for (int i = 0; i < R6_NX; ++i) v += re * g[i * R6_SZ + a] * g[i * R6_SZ + bb];
+  }
+  if (a == bb) v += s.xs[k * R6_SZ + a];
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    int g1, s1;
+    if (!r6_gen_slot(k, a, p, g1, s1)) continue;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      int g2, s2;
+      if (r6_gen_slot(k, bb, q, g2, s2) && g1 == g2) v += rs * s.gen[g1 * 3 + s1] * s.gen[g2 * 3 + s2];
+    }
+  }
+  return v;
+}
+// M entry of x_k+1[i] and (k, e): dynamics row (k, i) alone
+__device__ __forceinline__ double r6_m_next(const R6Smem &s, int k, int i, int e, double re) {
+  return (re * s.dpl[R6_NX + R6_NX * k + i]) * s.G[(k * R6_NX + i) * R6_SZ + e];
+}
+
+// one Gauss-Jordan pivot step of entry q of a block of width nb (pivot p)
+__device__ __forceinline__ double r6_gj_entry(const double *Tc, int q, int p, int nb, double inv) {
+  const int ti = q / R6_SZ, tj = q - ti * R6_SZ;
+  const double tip = Tc[ti * R6_SZ + p], tpj = Tc[p * R6_SZ + tj], tij = Tc[q];
+  const double f = tip * inv;
+  if (ti >= nb || tj >= nb) return tij;
+  if (ti == p && tj == p) return inv;
+  if (ti == p) return tpj * inv;
+  if (tj == p) return -f;
+  return tij - f * tpj;
+}
+
+// two pivot steps at once (p, p + 1; ai = the inverse of T[P][P], row-major):
+// half the barriers of single steps, one more operand read per entry
+__device__ __forceinline__ double r6_gj2_entry(const double *Tc, int q, int p, int nb, const double (&ai)[4]) {
+  const int ti = q / R6_SZ, tj = q - ti * R6_SZ;
+  const double tij = Tc[q];
+  const double r0 = Tc[ti * R6_SZ + p], r1 = Tc[ti * R6_SZ + p + 1];    // T[ti][P]
+  const double c0 = Tc[p * R6_SZ + tj], c1 = Tc[(p + 1) * R6_SZ + tj];  // T[P][tj]
+  if (ti >= nb || tj >= nb) return tij;
+  const int di = ti - p, dj = tj - p;
+  const bool ip = di == 0 || di == 1, jp = dj == 0 || dj == 1;
+  if (ip && jp) return di == 0 ? (dj == 0 ? ai[0] : ai[1]) : (dj == 0 ? ai[2] : ai[3]);
+  if (ip) return di == 0 ? ai[0] * c0 + ai[1] * c1 : ai[2] * c0 + ai[3] * c1;
+  const double f0 = r0 * ai[0] + r1 * ai[2], f1 = r0 * ai[1] + r1 * ai[3];  // T[ti][P] A^-1
+  if (jp) return -(dj == 0 ? f0 : f1);
+  return tij - (f0 * c0 + f1 * c1);
+}
+
+// the Gauss-Jordan inverse of the block in T[0] (width nb) on threads lt (of nt);
+// the result lands in T[return value]
+__device__ __forceinline__ int r6_gj(double (*T)[R6_SZ * R6_SZ], int lt, int nt, int nb, int kfail, int &bad) {
+  int cb = 0;
+  for (int p = 0; p < nb; p += 2) {
+    const double *Tc = T[cb];
+    if (R6_GJ2 && p + 1 < nb) {
+      const double a = Tc[p * R6_SZ + p], b = Tc[p * R6_SZ + p + 1];
+      const double c = Tc[(p + 1) * R6_SZ + p], d = Tc[(p + 1) * R6_SZ + p + 1];
+      const double det = fma(a, d, -(b * c));
+      if (!(a > 0.0 && det > 0.0) && !bad) bad = kfail;  // both pivots positive
+      const double rd = blk_recip(det);
+      const double ai[4] = {d * rd, -b * rd, -c * rd, a * rd};
+      for (int q = lt; q < R6_SZ * R6_SZ; q += nt) T[cb ^ 1][q] = r6_gj2_entry(Tc, q, p, nb, ai);
+    } else {
+      for (int pp = p; pp < p + 2 && pp < nb; ++pp) {
+        const double *Tp = T[cb];
+        const double piv = Tp[pp * R6_SZ + pp];
+        if (!(piv > 0.0) && !bad) bad = kfail;
+        // 1/piv by v_rcp_f64 + two Newton steps (blk_recip, within an ulp of the
+        // division) instead of an IEEE division per entry on every pivot's path
+        const double inv = blk_recip(piv);
+        for (int q = lt; q < R6_SZ * R6_SZ; q += nt) T[cb ^ 1][q] = r6_gj_entry(Tp, q, pp, nb, inv);
+        if (pp + 1 < p + 2 && pp + 1 < nb) { cb ^= 1; __syncthreads(); }
+      }
+    }
+    cb ^= 1;
+    __syncthreads();
+  }
+  return cb;
+}
+
+// assemble M and factor it: returns 0 or a failing block + 1
 template <class MK>
 __device__ __forceinline__ int r6_factor(R6Smem &s, R6Var (&V)[2], R6Row (&R)[2], double sigma, MK &mark) {
   const int tid = threadIdx.x;
@@ -644,143 +764,172 @@ __device__ __forceinline__ int r6_factor(R6Smem &s, R6Var (&V)[2], R6Row (&R)[2]
     }
   }
   __syncthreads();
-  // D_k, lower packed, row order of the terms as the banded oracle
+  // the 31 diagonal blocks, packed lower
   for (int e = tid; e < R6_NBLK * R6_TRI; e += R6_T) {
     const int k = e / R6_TRI, t = e - k * R6_TRI;
     int a = (int)((sqrt(8.0 * t + 1.0) - 1.0) * 0.5);
     while (a * (a + 1) / 2 > t) --a;
     while ((a + 1) * (a + 2) / 2 <= t) ++a;
     const int bb = t - a * (a + 1) / 2;
-    const int nb = (k == R6_N) ? R6_NX : R6_SZ;
+    const int nb = (k == R6_MID) ? R6_NX : R6_SZ;
     double v = 0.0;
     if (a < nb) {
-      const int ja = k * R6_SZ + a, jb = k * R6_SZ + bb;
-      if (a == bb) {
-        v = s.dsc[ja];
-        if (a < R6_NX) {
-          const int r = r6_eqid_row(k, a);
-          v += re * s.dpl[r] * s.dpl[r];
-        }
-      }
-      if (k < R6_N) {
-        const double *g = s.G + k * R6_NX * R6_SZ;
-        for (int i = 0; i < R6_NX; ++i) v += re * g[i * R6_SZ + a] * g[i * R6_SZ + bb];
-      }
-      if (a == bb) v += s.xs[ja];
-#pragma unroll
-      for (int p = 0; p < 4; ++p) {
-        int g1, s1;
-        if (!r6_gen_slot(k, a, p, g1, s1)) continue;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          int g2, s2;
-          if (r6_gen_slot(k, bb, q, g2, s2) && g1 == g2) v += rs * s.gen[g1 * 3 + s1] * s.gen[g2 * 3 + s2];
-        }
-      }
-      (void)jb;
+      if (k <= R6_MID || a < R6_NX) v = r6_m_stage(s, k, a, bb, re, rs);  // bb <= a
+      else if (bb >= R6_NX) v = r6_m_stage(s, k - 1, a, bb, re, rs);      // u_k-1 with u_k-1
+      else v = r6_m_next(s, k - 1, bb, a, re);                             // x_k[bb] with u_k-1
     } else if (a == bb) {
-      v = 1.0;  // unused tail of the last block
+      v = 1.0;  // unused tail of the middle block
     }
     s.Sinv[e] = v;
   }
   __syncthreads();
   mark(2);  // (stamps: the assembly)
-  // the sweep; the Gauss-Jordan pivots read one copy of the block and write the
-  // other, so a pivot needs one workgroup barrier instead of two
-  const int ti = tid / R6_SZ, tj = tid - ti * R6_SZ;
-  const bool tok = tid < R6_SZ * R6_SZ;
-  int cb = 0;
-  for (int k = 0; k <= R6_N; ++k) {
-    const int nb = (k == R6_N) ? R6_NX : R6_SZ;
-    cb = 0;
-    if (tok) {
+  // the sweep: threads 0-255 the top end, 256-511 the bottom end.  The
+  // Gauss-Jordan pivots read one copy of the block and write the other, so a
+  // pivot needs one workgroup barrier instead of two.
+  const int half = tid >> 8, lt = tid & 255;
+  constexpr int BB = R6_SZ * R6_SZ;
+  int bad = 0;
+  for (int t = 0; t < R6_MID; ++t) {
+    const int k = half ? R6_N - t : t;    // factor block
+    const int kc = half ? k - 1 : k;      // its coupling's slot
+    double (*T)[BB] = s.T[half];
+    for (int q = lt; q < BB; q += 256) {
+      const int ti = q / R6_SZ, tj = q - ti * R6_SZ;
       double v = s.Sinv[k * R6_TRI + r6_tri(ti, tj)];
-      if (k > 0 && ti < R6_NX && tj < R6_NX) v -= s.Sch[ti * R6_NX + tj];
-      s.T[0][tid] = v;
+      if (t > 0 && ti < R6_NX && tj < R6_NX) v -= s.Sch[half][ti * R6_NX + tj];
+      T[0][q] = v;
+    }
+    if (lt < R6_NX * R6_SZ) {  // top C_k[i][c]: x_k+1[i] with (k, c); bottom E_k-1[i][c]: x_k-1[i] with entry c of block k
+      const int i = lt / R6_SZ, c = lt - i * R6_SZ;
+      double v;
+      if (!half) v = r6_m_next(s, k, i, c, re);
+      else if (c < R6_NX) v = r6_m_next(s, k - 1, c, i, re);
+      else v = r6_m_stage(s, k - 1, i, c, re, rs);
+      s.Ct[half][lt] = v;
     }
     __syncthreads();
-    for (int p = 0; p < nb; ++p) {
-      const double *Tc = s.T[cb];
-      const double piv = Tc[p * R6_SZ + p];
-      if (!(piv > 0.0)) return k + 1;  // uniform: every thread read the same pivot
-      if (tok) {
-        const double tip = Tc[ti * R6_SZ + p], tpj = Tc[p * R6_SZ + tj], tij = Tc[tid];
-        // 1/piv by v_rcp_f64 + two Newton steps (blk_recip, within an ulp of the
-        // division) instead of an IEEE division per entry on every pivot's path
-        const double inv = blk_recip(piv), q = tip * inv;
-        double nv = tij;
-        if (ti < nb && tj < nb) {
-          if (ti == p && tj == p) nv = inv;
-          else if (ti == p) nv = tpj * inv;
-          else if (tj == p) nv = -q;
-          else nv = tij - q * tpj;
-        }
-        s.T[cb ^ 1][tid] = nv;
-      }
-      cb ^= 1;
-      __syncthreads();
+    const int cb = r6_gj(T, lt, 256, R6_SZ, k + 1, bad);  // bad: uniform over the half
+    for (int q = lt; q < BB; q += 256) {
+      const int ti = q / R6_SZ, tj = q - ti * R6_SZ;
+      if (ti >= tj) s.Sinv[k * R6_TRI + r6_tri(ti, tj)] = T[cb][q];
     }
-    if (tok && ti >= tj) s.Sinv[k * R6_TRI + r6_tri(ti, tj)] = (ti < nb && tj < nb) ? s.T[cb][tid] : 0.0;
     mark(10);
-    if (k == R6_N) break;
-    // G_k = C_k S_k^-1, C_k[i][:] = rho_eq dpl(k, i) (staged row (k, i))
-    const double *g = s.G + k * R6_NX * R6_SZ;
-    if (tid < R6_NX * R6_SZ) {
-      const int i = tid / R6_SZ, c = tid - i * R6_SZ;
-      const double sc = re * s.dpl[R6_NX + R6_NX * k + i];
+    // -G_k = -C_k S_k^-1 / -H_k-1 = -E_k-1 T_k^-1 over the staged rows of its slot
+    double *Gs = s.G + kc * R6_NX * R6_SZ;
+    if (lt < R6_NX * R6_SZ) {
+      const int i = lt / R6_SZ, c = lt - i * R6_SZ;
       double acc = 0.0;
-      for (int e = 0; e < R6_SZ; ++e) acc += (sc * g[i * R6_SZ + e]) * s.T[cb][e * R6_SZ + c];
-      s.Gt[tid] = acc;
+      for (int e = 0; e < R6_SZ; ++e) acc += s.Ct[half][i * R6_SZ + e] * T[cb][e * R6_SZ + c];
+      Gs[lt] = -acc;  // stored negated: the chains accumulate
     }
     __syncthreads();
-    if (tid < R6_NX * R6_NX) {  // G_k C_k^T (14 x 14)
-      const int i = tid / R6_NX, i2 = tid - i * R6_NX;
-      const double sc = re * s.dpl[R6_NX + R6_NX * k + i2];
+    if (lt < R6_NX * R6_NX) {  // the next block's update G_k C_k^T / H_k-1 E_k-1^T (14 x 14)
+      const int i = lt / R6_NX, i2 = lt - i * R6_NX;
       double acc = 0.0;
-      for (int e = 0; e < R6_SZ; ++e) acc += s.Gt[i * R6_SZ + e] * (sc * g[i2 * R6_SZ + e]);
-      s.Sch[tid] = acc;
+      for (int e = 0; e < R6_SZ; ++e) acc += Gs[i * R6_SZ + e] * s.Ct[half][i2 * R6_SZ + e];
+      s.Sch[half][lt] = -acc;
     }
-    __syncthreads();
-    if (tid < R6_NX * R6_SZ) s.G[k * R6_NX * R6_SZ + tid] = -s.Gt[tid];  // stored negated: the chains accumulate
     __syncthreads();
     mark(11);
   }
+  // the middle block Z = D_15 - G_14 C_14^T - H_15 E_15^T, 14 wide
+  double (*T)[BB] = s.T[0];
+  if (tid < BB) {
+    const int ti = tid / R6_SZ, tj = tid - ti * R6_SZ;
+    double v = s.Sinv[R6_MID * R6_TRI + r6_tri(ti, tj)];
+    if (ti < R6_NX && tj < R6_NX) v = (v - s.Sch[0][ti * R6_NX + tj]) - s.Sch[1][ti * R6_NX + tj];
+    T[0][tid] = v;
+  }
   __syncthreads();
-  return 0;
+  const int cb = r6_gj(T, tid, R6_T, R6_NX, R6_MID + 1, bad);
+  if (tid < BB) {
+    const int ti = tid / R6_SZ, tj = tid - ti * R6_SZ;
+    if (ti >= tj) s.Sinv[R6_MID * R6_TRI + r6_tri(ti, tj)] = (ti < R6_NX && tj < R6_NX) ? T[cb][tid] : 0.0;
+  }
+  if (lt == 0) s.bad[half] = bad;
+  __syncthreads();
+  mark(10);
+  return s.bad[0] ? s.bad[0] : s.bad[1];
 }
 
-// x~ = M^-1 rhs: forward chain (wave 0), diagonal products, backward chain
-// (wave 0).  The chains carry their vector in registers and broadcast it with
-// DPP row_newbcast inside the FMA (qp_block.h fmac_bc), as the 3-DoF fleet does;
-// blocks are 17 wide and a DPP row is 16:
-//   forward  y_k+1 = b_k+1 + (-G_k) y_k on row 0 (lane i: row i < 14; lanes 14,
-//            15 carry b_k+1[14, 15] through zero operands).  y_k[16] = b_k[16]
-//            (no G row reaches it), so its term goes into the init off the chain.
-//   backward x_k = u_k + (-G_k)^T x_k+1 over the 14 coupled entries: lanes 0-15
-//            compute entries 0-15, lanes 16-29 replicate entries 0-13 (so row 1
-//            broadcasts the same x_k+1) and lane 30 computes entry 16.
+// u = S_k^-1 y_k, row a of factor block k (the middle block on y_15 + z'_15)
+__device__ __forceinline__ void r6_diag_row(R6Smem &s, int k, int a) {
+  const int e = k * R6_SZ + a;
+  const int nb = (k == R6_MID) ? R6_NX : R6_SZ;
+  if (a < nb) {
+    const double *S = s.Sinv + k * R6_TRI;
+    const double *y = s.rhs + k * R6_SZ;
+    const int lo = k > R6_MID ? R6_SZ : 0;   // a bottom block's u_k-1 one block down
+    const bool mid = k == R6_MID;
+    // unrolled over the 17 entries (the middle block's 3 masked) in three chunks
+    // of loads in flight (a runtime-count loop waited on each pair; all 17 at
+    // once spilled the items' registers)
+    double acc0 = 0.0, acc1 = 0.0;
+#pragma unroll
+    for (int c0 = 0; c0 < R6_SZ; c0 += 6) {
+      double sv[6], yv[6];
+#pragma unroll
+      for (int q = 0; q < 6; ++q) {
+        const int bb = c0 + q < R6_SZ ? c0 + q : R6_SZ - 1;
+        sv[q] = S[r6_tri(a, bb)];
+        yv[q] = y[bb >= R6_NX ? bb - lo : bb];
+        if (bb < R6_NX && mid) yv[q] += s.zmid[bb];
+      }
+#pragma unroll
+      for (int q = 0; q < 6; ++q) {
+        const int bb = c0 + q;
+        if (bb >= R6_SZ) continue;
+        if (bb & 1) acc1 = bb < nb ? fma(sv[q], yv[q], acc1) : acc1;
+        else acc0 = bb < nb ? fma(sv[q], yv[q], acc0) : acc0;
+      }
+      asm volatile("" ::: "memory");
+    }
+    s.xs[a >= R6_NX ? e - lo : e] = acc0 + acc1;
+  }
+}
+
+// x~ = M^-1 rhs, twisted: the forward chains (wave 0: y down the top blocks to
+// y_15; wave 1: z up the bottom blocks, then z'_15 = -H_15 z_16), the 31 diagonal
+// products (the middle on y_15 + z'_15), the backward chains (wave 0: x_14 .. x_0
+// from x_15; wave 1: blocks 16 .. 30 from x_15).  The chains carry their vector
+// in registers and broadcast it with DPP row_newbcast inside the FMA (qp_block.h
+// fmac_bc), as the 3-DoF fleet does; blocks are 17 wide and a DPP row 16:
+//   forward  row 0, lane i < 14: entry i of the next block; lanes 14, 15 carry
+//            the block's entries 14, 15 (which no coupling reaches) through zero
+//            operands, and entry 16's term goes into the init off the chain.
+//   backward lanes 0-15 compute entries 0-15, lanes 16-29 replicate entries
+//            0-13 (so row 1 broadcasts the same x) and lane 30 computes entry 16.
+// Both ends run the same instruction stream; a bottom block's entries 14-16
+// (u_k-1) sit 17 below its x_k in the natural order (offsets rr - 17).
 template <class MK>
 __device__ __forceinline__ void r6_solve(R6Smem &s, MK &mark) {
-  const int tid = threadIdx.x;
-  if (tid < 64) {
+  const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
+  if (wv < 2) {
     // every term's operand for the NEXT step loads right after the term's FMA,
     // into the register it frees: one buffer, the loads a step ahead
-    const int lane = tid, rr = lane & 15;
+    const bool bot = wv == 1;
+    const int rr = lane & 15;
+    const bool pass = rr >= R6_NX;
+    const int off = (bot && pass) ? rr - R6_SZ : rr;
+    const int o16 = bot ? -1 : R6_SZ - 1;
+    const int db = bot ? -R6_SZ : R6_SZ;
+    const int gs = pass ? 0 : (bot ? -R6_NX * R6_SZ : R6_NX * R6_SZ);
     const double *F = s.G;
-    const bool pass = rr >= R6_NX;  // lanes 14, 15 carry b[14, 15]: zero operands
-    int go = pass ? (int)(s.zero - s.G) : rr * R6_SZ;
-    const int gs = pass ? 0 : R6_NX * R6_SZ;
+    int go = pass ? (int)(s.zero - s.G) : (bot ? R6_N - 1 : 0) * R6_NX * R6_SZ + rr * R6_SZ;
+    int ib = bot ? R6_N * R6_SZ : 0;
     double g[R6_SZ];
 #pragma unroll
     for (int e = 0; e < R6_SZ; ++e) g[e] = F[go + e];
-    double y = s.rhs[rr];
-    double b16 = s.rhs[R6_SZ - 1], bn = s.rhs[R6_SZ + rr];
-#pragma unroll 2
-    for (int k = 0; k < R6_N; ++k) {
+    double y = s.rhs[ib + off];
+    double b16 = s.rhs[ib + o16], bn = s.rhs[ib + db + off];
+#pragma unroll 3
+    for (int t = 0; t < R6_MID; ++t) {
+      const bool last = t == R6_MID - 1;
       const int gn = go + gs;
-      const double init = fma(g[R6_SZ - 1], b16, bn);
-      b16 = s.rhs[(k + 1) * R6_SZ + R6_SZ - 1];
-      bn = s.rhs[min(k + 2, R6_N) * R6_SZ + rr];
+      const double init = fma(g[R6_SZ - 1], b16, (bot && last) ? 0.0 : bn);
+      b16 = s.rhs[ib + db + o16];
+      bn = s.rhs[ib + 2 * db + off];
       g[R6_SZ - 1] = F[gn + R6_SZ - 1];
       double a0 = init, a1 = 0.0;
       fmac_bc<0, true>(a0, y, g[0]);   g[0] = F[gn + 0];
@@ -800,65 +949,46 @@ __device__ __forceinline__ void r6_solve(R6Smem &s, MK &mark) {
       fmac_bc<14, false>(a0, y, g[14]); g[14] = F[gn + 14];
       fmac_bc<15, false>(a1, y, g[15]); g[15] = F[gn + 15];
       y = a0 + a1;
-      // unconditional store (idle rows to the dump): no exec-mask branch in the
-      // loop, so the compiler's LDS wait at the next step is exact, not lgkmcnt(0)
-      *(lane < 16 ? &s.rhs[(k + 1) * R6_SZ + rr] : &s.dump[lane]) = y;
+      // unconditional store (pass-through and idle lanes to the dump): no
+      // exec-mask branch in the loop, so the LDS wait at the next step is exact
+      double *dst = (!pass && lane < 16) ? ((bot && last) ? &s.zmid[rr] : &s.rhs[ib + db + rr]) : &s.dump[lane];
+      *dst = y;
       go = gn;
+      ib += db;
+      // the two ends walk in opposite directions, so a step's address is no
+      // immediate offset from one base; left visible, the compiler hoists every
+      // step's address out of the ADMM loop as a live register
+      asm volatile("" : "+v"(ib), "+v"(go));
     }
   }
   __syncthreads();
   mark(4);
-  for (int e = tid; e < R6_NBLK * R6_SZ; e += R6_T) {
-    const int k = e / R6_SZ, a = e - k * R6_SZ;
-    const int nb = (k == R6_N) ? R6_NX : R6_SZ;
-    if (a < nb) {
-      const double *S = s.Sinv + k * R6_TRI;
-      const double *y = s.rhs + k * R6_SZ;
-      // unrolled over the 17 entries (the last block's 3 masked) in three chunks
-      // of loads in flight (a runtime-count loop waited on each pair; all 17 at
-      // once spilled the items' registers)
-      double acc0 = 0.0, acc1 = 0.0;
-#pragma unroll
-      for (int c0 = 0; c0 < R6_SZ; c0 += 6) {
-        double sv[6], yv[6];
-#pragma unroll
-        for (int q = 0; q < 6; ++q) {
-          const int bb = c0 + q < R6_SZ ? c0 + q : R6_SZ - 1;
-          sv[q] = S[r6_tri(a, bb)];
-          yv[q] = y[bb];
-        }
-#pragma unroll
-        for (int q = 0; q < 6; ++q) {
-          const int bb = c0 + q;
-          if (bb >= R6_SZ) continue;
-          if (bb & 1) acc1 = bb < nb ? fma(sv[q], yv[q], acc1) : acc1;
-          else acc0 = bb < nb ? fma(sv[q], yv[q], acc0) : acc0;
-        }
-        asm volatile("" ::: "memory");
-      }
-      s.xs[e] = acc0 + acc1;
-    }
-  }
+  for (int e = tid; e < R6_NBLK * R6_SZ; e += R6_T) r6_diag_row(s, e / R6_SZ, e % R6_SZ);
   __syncthreads();
   mark(5);
-  if (tid < 64) {
-    const int lane = tid;
+  if (wv < 2) {
+    const bool bot = wv == 1;
     // entry a of lane (0-15: a = lane, 16-29: a = lane - 16, 30: 16); lanes >= 31
     // compute entry 16 too and drop it
     const int a = lane < 16 ? lane : (lane < 30 ? lane - 16 : R6_SZ - 1);
     const bool st = lane < 16 || lane == 30;
+    const int off = (bot && a >= R6_NX) ? a - R6_SZ : a;
+    // top: blocks 14 .. 0 (slots 14 .. 0); bottom: blocks 16 .. 30 (slots 15 .. 29)
+    const int gs = bot ? R6_NX * R6_SZ : -R6_NX * R6_SZ;
+    const int db = bot ? R6_SZ : -R6_SZ;
     const double *F = s.G;
-    int go = (R6_N - 1) * R6_NX * R6_SZ + a;
+    int go = (R6_MID - (bot ? 0 : 1)) * R6_NX * R6_SZ + a;
+    int ib = (bot ? R6_MID + 1 : R6_MID - 1) * R6_SZ;
     double g[R6_NX];
 #pragma unroll
     for (int i = 0; i < R6_NX; ++i) g[i] = F[go + i * R6_SZ];
-    double x = a < R6_NX ? s.xs[R6_N * R6_SZ + a] : 0.0;
-    double u = s.xs[(R6_N - 1) * R6_SZ + a];
-#pragma unroll 2
-    for (int k = R6_N - 1; k >= 0; --k) {
-      const int gn = max(go - R6_NX * R6_SZ, 0);
+    double x = a < R6_NX ? s.xs[R6_MID * R6_SZ + a] : 0.0;
+    double u = s.xs[ib + off];
+#pragma unroll 3
+    for (int t = 0; t < R6_MID; ++t) {
+      const int gn = min(max(go + gs, a), (R6_N - 1) * R6_NX * R6_SZ + a);
       double a0 = u, a1 = 0.0;
-      u = s.xs[max(k - 1, 0) * R6_SZ + a];
+      u = s.xs[min(max(ib + db, 0), R6_N * R6_SZ) + off];
       fmac_bc<0, true>(a0, x, g[0]);   g[0] = F[gn + 0 * R6_SZ];
       fmac_bc<1, false>(a1, x, g[1]);  g[1] = F[gn + 1 * R6_SZ];
       fmac_bc<2, false>(a0, x, g[2]);  g[2] = F[gn + 2 * R6_SZ];
@@ -874,8 +1004,10 @@ __device__ __forceinline__ void r6_solve(R6Smem &s, MK &mark) {
       fmac_bc<12, false>(a0, x, g[12]); g[12] = F[gn + 12 * R6_SZ];
       fmac_bc<13, false>(a1, x, g[13]); g[13] = F[gn + 13 * R6_SZ];
       x = a0 + a1;
-      *(st ? &s.xs[k * R6_SZ + a] : &s.dump[lane]) = x;
+      *(st ? &s.xs[ib + off] : &s.dump[lane]) = x;
       go = gn;
+      ib += db;
+      asm volatile("" : "+v"(ib), "+v"(go));
     }
   }
   __syncthreads();
