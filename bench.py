@@ -572,7 +572,7 @@ def rollouts6_bench(ctx, torch=None, batches=(64, 512), max_steps=300):
         iters = float(out[str(B)]["admm_iters_per_solve"])
         # per control launch: B solves x (iterations x per-iteration flop + ~2 factorisations)
         ctl_flop = B * (iters * it_f + 2.0 * fac_f)
-        tr, tr_src = pmc_traffic("k_r6_control")
+        tr, tr_src = pmc_traffic("k_r6_control<false>")
         out["kernels"] = {"predict": {"kernel": "k_r6_predict<false>", "ms": round(pm[0] * 1e3, 4)},
                           "control": {"kernel": "k_r6_control<false>", "ms": round(pm[1] * 1e3, 4)},
                           "plant": {"kernel": "k_r6_plant", "ms": round(pm[2] * 1e3, 4)}}
@@ -581,7 +581,7 @@ def rollouts6_bench(ctx, torch=None, batches=(64, 512), max_steps=300):
                            "frac": round(ctl_flop / pm[1] / 1e12 / FP64_PEAK_TFLOPS, 5),
                            "traffic": tr, "traffic_source": tr_src,
                            "per_launch": f"{B} solves x (iterations x {it_f} + 2 x {fac_f}) fp64 flop",
-                           "limiter": "latency: serial block-tridiagonal KKT chains (31 stage blocks), one rollout per CU"}
+                           "limiter": "latency: the block-tridiagonal KKT chains (twisted, 15 block steps per end) and the factor sweep, one rollout per CU"}
     return out
 
 

@@ -932,22 +932,22 @@ __device__ __forceinline__ void r6_solve(R6Smem &s, MK &mark) {
       bn = s.rhs[ib + 2 * db + off];
       g[R6_SZ - 1] = F[gn + R6_SZ - 1];
       double a0 = init, a1 = 0.0;
-      fmac_bc<0, true>(a0, y, g[0]);   g[0] = F[gn + 0];
-      fmac_bc<1, false>(a1, y, g[1]);  g[1] = F[gn + 1];
-      fmac_bc<2, false>(a0, y, g[2]);  g[2] = F[gn + 2];
-      fmac_bc<3, false>(a1, y, g[3]);  g[3] = F[gn + 3];
-      fmac_bc<4, false>(a0, y, g[4]);  g[4] = F[gn + 4];
-      fmac_bc<5, false>(a1, y, g[5]);  g[5] = F[gn + 5];
-      fmac_bc<6, false>(a0, y, g[6]);  g[6] = F[gn + 6];
-      fmac_bc<7, false>(a1, y, g[7]);  g[7] = F[gn + 7];
-      fmac_bc<8, false>(a0, y, g[8]);  g[8] = F[gn + 8];
-      fmac_bc<9, false>(a1, y, g[9]);  g[9] = F[gn + 9];
-      fmac_bc<10, false>(a0, y, g[10]); g[10] = F[gn + 10];
-      fmac_bc<11, false>(a1, y, g[11]); g[11] = F[gn + 11];
-      fmac_bc<12, false>(a0, y, g[12]); g[12] = F[gn + 12];
-      fmac_bc<13, false>(a1, y, g[13]); g[13] = F[gn + 13];
-      fmac_bc<14, false>(a0, y, g[14]); g[14] = F[gn + 14];
-      fmac_bc<15, false>(a1, y, g[15]); g[15] = F[gn + 15];
+      fmac_bc<0, true>(a0, y, g[0]); fmac_bc<1, false>(a1, y, g[1]);
+      g[0] = F[gn + 0]; g[1] = F[gn + 1];
+      fmac_bc<2, false>(a0, y, g[2]); fmac_bc<3, false>(a1, y, g[3]);
+      g[2] = F[gn + 2]; g[3] = F[gn + 3];
+      fmac_bc<4, false>(a0, y, g[4]); fmac_bc<5, false>(a1, y, g[5]);
+      g[4] = F[gn + 4]; g[5] = F[gn + 5];
+      fmac_bc<6, false>(a0, y, g[6]); fmac_bc<7, false>(a1, y, g[7]);
+      g[6] = F[gn + 6]; g[7] = F[gn + 7];
+      fmac_bc<8, false>(a0, y, g[8]); fmac_bc<9, false>(a1, y, g[9]);
+      g[8] = F[gn + 8]; g[9] = F[gn + 9];
+      fmac_bc<10, false>(a0, y, g[10]); fmac_bc<11, false>(a1, y, g[11]);
+      g[10] = F[gn + 10]; g[11] = F[gn + 11];
+      fmac_bc<12, false>(a0, y, g[12]); fmac_bc<13, false>(a1, y, g[13]);
+      g[12] = F[gn + 12]; g[13] = F[gn + 13];
+      fmac_bc<14, false>(a0, y, g[14]); fmac_bc<15, false>(a1, y, g[15]);
+      g[14] = F[gn + 14]; g[15] = F[gn + 15];
       y = a0 + a1;
       // unconditional store (pass-through and idle lanes to the dump): no
       // exec-mask branch in the loop, so the LDS wait at the next step is exact
@@ -989,20 +989,20 @@ __device__ __forceinline__ void r6_solve(R6Smem &s, MK &mark) {
       const int gn = min(max(go + gs, a), (R6_N - 1) * R6_NX * R6_SZ + a);
       double a0 = u, a1 = 0.0;
       u = s.xs[min(max(ib + db, 0), R6_N * R6_SZ) + off];
-      fmac_bc<0, true>(a0, x, g[0]);   g[0] = F[gn + 0 * R6_SZ];
-      fmac_bc<1, false>(a1, x, g[1]);  g[1] = F[gn + 1 * R6_SZ];
-      fmac_bc<2, false>(a0, x, g[2]);  g[2] = F[gn + 2 * R6_SZ];
-      fmac_bc<3, false>(a1, x, g[3]);  g[3] = F[gn + 3 * R6_SZ];
-      fmac_bc<4, false>(a0, x, g[4]);  g[4] = F[gn + 4 * R6_SZ];
-      fmac_bc<5, false>(a1, x, g[5]);  g[5] = F[gn + 5 * R6_SZ];
-      fmac_bc<6, false>(a0, x, g[6]);  g[6] = F[gn + 6 * R6_SZ];
-      fmac_bc<7, false>(a1, x, g[7]);  g[7] = F[gn + 7 * R6_SZ];
-      fmac_bc<8, false>(a0, x, g[8]);  g[8] = F[gn + 8 * R6_SZ];
-      fmac_bc<9, false>(a1, x, g[9]);  g[9] = F[gn + 9 * R6_SZ];
-      fmac_bc<10, false>(a0, x, g[10]); g[10] = F[gn + 10 * R6_SZ];
-      fmac_bc<11, false>(a1, x, g[11]); g[11] = F[gn + 11 * R6_SZ];
-      fmac_bc<12, false>(a0, x, g[12]); g[12] = F[gn + 12 * R6_SZ];
-      fmac_bc<13, false>(a1, x, g[13]); g[13] = F[gn + 13 * R6_SZ];
+      fmac_bc<0, true>(a0, x, g[0]); fmac_bc<1, false>(a1, x, g[1]);
+      g[0] = F[gn + 0 * R6_SZ]; g[1] = F[gn + 1 * R6_SZ];
+      fmac_bc<2, false>(a0, x, g[2]); fmac_bc<3, false>(a1, x, g[3]);
+      g[2] = F[gn + 2 * R6_SZ]; g[3] = F[gn + 3 * R6_SZ];
+      fmac_bc<4, false>(a0, x, g[4]); fmac_bc<5, false>(a1, x, g[5]);
+      g[4] = F[gn + 4 * R6_SZ]; g[5] = F[gn + 5 * R6_SZ];
+      fmac_bc<6, false>(a0, x, g[6]); fmac_bc<7, false>(a1, x, g[7]);
+      g[6] = F[gn + 6 * R6_SZ]; g[7] = F[gn + 7 * R6_SZ];
+      fmac_bc<8, false>(a0, x, g[8]); fmac_bc<9, false>(a1, x, g[9]);
+      g[8] = F[gn + 8 * R6_SZ]; g[9] = F[gn + 9 * R6_SZ];
+      fmac_bc<10, false>(a0, x, g[10]); fmac_bc<11, false>(a1, x, g[11]);
+      g[10] = F[gn + 10 * R6_SZ]; g[11] = F[gn + 11 * R6_SZ];
+      fmac_bc<12, false>(a0, x, g[12]); fmac_bc<13, false>(a1, x, g[13]);
+      g[12] = F[gn + 12 * R6_SZ]; g[13] = F[gn + 13 * R6_SZ];
       x = a0 + a1;
       *(st ? &s.xs[ib + off] : &s.dump[lane]) = x;
       go = gn;
