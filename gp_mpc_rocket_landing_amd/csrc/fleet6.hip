@@ -205,11 +205,21 @@ __device__ void r6_neg_lin(const double *x, const double *u, double dt, double *
 
 // ---------------------------------------------------------------------------
 // StructuredRocketGP features (features.py:196-263, :304-356), scaled by the GP's
-// lengthscales, and their squared norm (the k_scale_rows arithmetic).  The two
-// sets are separate functions so that two waves compute them side by side.
-__device__ __forceinline__ void r6_body_velocity(const double *x, double *vb, double &speed) {
+// lengthscales (the k_scale_rows arithmetic).  The formulas are split over six
+// wave-uniform roles, one lane each, so the transcendental chains of a point run
+// side by side instead of one after another on one lane:
+//   0: v 0-2, 7-11 (velocity, thrust, altitude)    1: v 3, w 0-6, 10 (speeds, rates, thrust)
+//   2: v 4, 12, w 11 (density: exp)                3: v 5 (angle of attack: atan2)
+//   4: v 6 (sideslip: asin)                        5: w 7-9 (body-frame velocity)
+// Each role evaluates its features with the same expressions as the whole set
+// would, so the scaled features are the same bits.
+#define R6_FEAT_ROLES 6
+__device__ __forceinline__ double r6_speed(const double *x) {
   const double vx = x[4], vy = x[5], vz = x[6];
-  speed = sqrt((vx * vx + vy * vy) + vz * vz);
+  return sqrt((vx * vx + vy * vy) + vz * vz);
+}
+__device__ __forceinline__ void r6_body_velocity(const double *x, double *vb) {
+  const double vx = x[4], vy = x[5], vz = x[6];
   // body-from-inertial DCM (features.py:265-270)
   const double w = x[7], qx = x[8], qy = x[9], qz = x[10];
   const double Cb[3][3] = {{1 - 2 * (qy * qy + qz * qz), 2 * (qx * qy + w * qz), 2 * (qx * qz - w * qy)},
@@ -218,42 +228,59 @@ __device__ __forceinline__ void r6_body_velocity(const double *x, double *vb, do
   for (int i = 0; i < 3; ++i) vb[i] = (Cb[i][0] * vx + Cb[i][1] * vy) + Cb[i][2] * vz;
 }
 
-// translational features (13)
-__device__ void r6_features_v(const double *x, const double *u, const double *lsv, double *zv, double *nv) {
-  double vb[3], speed;
-  r6_body_velocity(x, vb, speed);
-  const double alt = x[1], vx = x[4], vy = x[5], vz = x[6];
-  const double rho = 1.225 * exp(-alt / 8500.0);
-  const double qd = 0.5 * rho * speed * speed;
-  const bool moving = speed > 1e-3;
-  const double safe = moving ? speed : 1.0;
-  double sb = vb[1] / safe;
-  sb = fmin(fmax(sb, -1.0), 1.0);
-  const double aoa = moving ? atan2(-vb[2], vb[0]) : 0.0;
-  const double beta = moving ? asin(sb) : 0.0;
-  const double tm = sqrt((u[0] * u[0] + u[1] * u[1]) + u[2] * u[2]);
+__device__ void r6_features_role(int role, const double *x, const double *u, const double *lsv,
+                                 const double *lsw, double *zv, double *zw) {
   const double qn = 0.5 * 1.225 * 100.0;
-  const double fv[13] = {vx / 10.0, vy / 10.0, vz / 10.0, speed / 10.0, qd / qn, aoa, beta,
-                         u[0] / 10.0, u[1] / 10.0, u[2] / 10.0, tm / 10.0, alt / 100.0, rho / 1.225};
-  double s = 0.0;
-  for (int k = 0; k < 13; ++k) { zv[k] = fv[k] / lsv[k]; s += zv[k] * zv[k]; }
-  *nv = s;
-}
-
-// rotational features (12)
-__device__ void r6_features_w(const double *x, const double *u, const double *lsw, double *zw, double *nw) {
-  double vb[3], speed;
-  r6_body_velocity(x, vb, speed);
-  const double rho = 1.225 * exp(-x[1] / 8500.0);
-  const double qd = 0.5 * rho * speed * speed;
-  const double qn = 0.5 * 1.225 * 100.0;
-  const double wxx = x[11], wyy = x[12], wzz = x[13];
-  const double wm = sqrt((wxx * wxx + wyy * wyy) + wzz * wzz);
-  const double fw[12] = {wxx, wyy, wzz, wm, u[0] / 10.0, u[1] / 10.0, u[2] / 10.0,
-                         vb[0] / 10.0, vb[1] / 10.0, vb[2] / 10.0, speed / 10.0, qd / qn};
-  double s = 0.0;
-  for (int k = 0; k < 12; ++k) { zw[k] = fw[k] / lsw[k]; s += zw[k] * zw[k]; }
-  *nw = s;
+  switch (role) {
+    case 0: {
+      const double tm = sqrt((u[0] * u[0] + u[1] * u[1]) + u[2] * u[2]);
+      zv[0] = (x[4] / 10.0) / lsv[0]; zv[1] = (x[5] / 10.0) / lsv[1]; zv[2] = (x[6] / 10.0) / lsv[2];
+      zv[7] = (u[0] / 10.0) / lsv[7]; zv[8] = (u[1] / 10.0) / lsv[8]; zv[9] = (u[2] / 10.0) / lsv[9];
+      zv[10] = (tm / 10.0) / lsv[10]; zv[11] = (x[1] / 100.0) / lsv[11];
+      break;
+    }
+    case 1: {
+      const double speed = r6_speed(x);
+      const double wxx = x[11], wyy = x[12], wzz = x[13];
+      const double wm = sqrt((wxx * wxx + wyy * wyy) + wzz * wzz);
+      zv[3] = (speed / 10.0) / lsv[3];
+      zw[0] = wxx / lsw[0]; zw[1] = wyy / lsw[1]; zw[2] = wzz / lsw[2]; zw[3] = wm / lsw[3];
+      zw[4] = (u[0] / 10.0) / lsw[4]; zw[5] = (u[1] / 10.0) / lsw[5]; zw[6] = (u[2] / 10.0) / lsw[6];
+      zw[10] = (speed / 10.0) / lsw[10];
+      break;
+    }
+    case 2: {
+      const double speed = r6_speed(x);
+      const double rho = 1.225 * exp(-x[1] / 8500.0);
+      const double qd = 0.5 * rho * speed * speed;
+      zv[4] = (qd / qn) / lsv[4]; zv[12] = (rho / 1.225) / lsv[12];
+      zw[11] = (qd / qn) / lsw[11];
+      break;
+    }
+    case 3: {
+      const double speed = r6_speed(x);
+      double vb[3];
+      r6_body_velocity(x, vb);
+      zv[5] = (speed > 1e-3 ? atan2(-vb[2], vb[0]) : 0.0) / lsv[5];
+      break;
+    }
+    case 4: {
+      const double speed = r6_speed(x);
+      double vb[3];
+      r6_body_velocity(x, vb);
+      const bool moving = speed > 1e-3;
+      double sb = vb[1] / (moving ? speed : 1.0);
+      sb = fmin(fmax(sb, -1.0), 1.0);
+      zv[6] = (moving ? asin(sb) : 0.0) / lsv[6];
+      break;
+    }
+    default: {
+      double vb[3];
+      r6_body_velocity(x, vb);
+      zw[7] = (vb[0] / 10.0) / lsw[7]; zw[8] = (vb[1] / 10.0) / lsw[8]; zw[9] = (vb[2] / 10.0) / lsw[9];
+      break;
+    }
+  }
 }
 
 __device__ __forceinline__ bool r6_landing_ok(const double *x, double m0) {
@@ -293,10 +320,10 @@ struct R6Args {
 // two rows per trip with all their loads issued before either is used
 template <int D>
 __device__ __forceinline__ void r6_kernel_rows(const GpView &v, int M, const double *__restrict__ cf,
-                                               const double *zs, double zn, int t0, int stride, double *acc) {
-  double z[D];
+                                               const double *zs, int t0, int stride, double *acc) {
+  double z[D], zn = 0.0;
 #pragma unroll
-  for (int f = 0; f < D; ++f) z[f] = zs[f];
+  for (int f = 0; f < D; ++f) { z[f] = zs[f]; zn += z[f] * z[f]; }  // |z|^2 in the feature order
   const double *__restrict__ Xs = v.Xs;
   const double *__restrict__ Xn = v.Xn;
   int i = t0;
@@ -332,8 +359,8 @@ __device__ unsigned long long g_r6p_stamps[4];
 // Per horizon point k (the points are sequential: X[k+1] needs the GP mean at X[k]):
 //   waves 0 .. R6_PT/64 - 2: the 2 x M kernel rows of both GPs (K*u . coefficients);
 //   the last wave, lane 0, meanwhile: RK4(X[k], U[k]) (the GP mean is added after);
-//   barrier; lanes 0 of waves 0 and 1: the means, X[k+1] = RK4 + [.., d_v dt, .., d_w dt],
-//   then the translational (wave 0) and rotational (wave 1) features of point k+1;
+//   barrier; lanes 0 of waves 0 .. 5: the means, X[k+1] = RK4 + [.., d_v dt, .., d_w dt],
+//   then the six roles of point k+1's features (r6_features_role);
 //   barrier.
 template <bool ST>
 __global__ __launch_bounds__(R6_PT) void k_r6_predict(R6Args a) {
@@ -350,7 +377,7 @@ __global__ __launch_bounds__(R6_PT) void k_r6_predict(R6Args a) {
   double *rec = a.rec + (int64_t)b * GPMPC_REC_LEN;
   if (a.mode == 0 ? rec[0] != 0.0 : a.done[b] != 0) return;
   __shared__ double X[R6_N + 1][R6_NX];
-  __shared__ double zq[2][16], zn[2];
+  __shared__ double zq[2][16];
   __shared__ double red[NW][6];
   __shared__ double xrk[R6_NX];
   __shared__ int s_out;
@@ -387,12 +414,9 @@ __global__ __launch_bounds__(R6_PT) void k_r6_predict(R6Args a) {
   __syncthreads();
   if (s_out) return;
   const double *Ub = a.U + (int64_t)b * R6_N * R6_NU;
-  const bool feat_lane = lane == 0 && wave < 2;
+  const bool feat_lane = lane == 0 && wave < R6_FEAT_ROLES;
   // features of point 0
-  if (a.use_gp && feat_lane) {
-    if (wave == 0) r6_features_v(X[0], Ub, a.gv.ls, zq[0], &zn[0]);
-    else r6_features_w(X[0], Ub, a.gw.ls, zq[1], &zn[1]);
-  }
+  if (a.use_gp && feat_lane) r6_features_role(wave, X[0], Ub, a.gv.ls, a.gw.ls, zq[0], zq[1]);
   __syncthreads();
   mark(-1);
   for (int k = 0; k < R6_N; ++k) {
@@ -401,8 +425,8 @@ __global__ __launch_bounds__(R6_PT) void k_r6_predict(R6Args a) {
     double acc[6] = {0, 0, 0, 0, 0, 0};
     if (tid < NRT) {
       if (a.use_gp) {
-        r6_kernel_rows<13>(a.gv, a.Mv, a.cv, zq[0], zn[0], tid, NRT, acc);
-        r6_kernel_rows<12>(a.gw, a.Mw, a.cw, zq[1], zn[1], tid, NRT, acc + 3);
+        r6_kernel_rows<13>(a.gv, a.Mv, a.cv, zq[0], tid, NRT, acc);
+        r6_kernel_rows<12>(a.gw, a.Mw, a.cw, zq[1], tid, NRT, acc + 3);
       }
 #pragma unroll
       for (int c = 0; c < 6; ++c)
@@ -438,10 +462,8 @@ __global__ __launch_bounds__(R6_PT) void k_r6_predict(R6Args a) {
         if (!relin)
           for (int i = 0; i < R6_NX; ++i) X[k + 1][i] = xn[i];
       }
-      if (a.use_gp && k + 1 < R6_N) {  // the next point's features, from this lane's own copy of X[k+1]
-        if (wave == 0) r6_features_v(xn, Ub + (k + 1) * R6_NU, a.gv.ls, zq[0], &zn[0]);
-        else r6_features_w(xn, Ub + (k + 1) * R6_NU, a.gw.ls, zq[1], &zn[1]);
-      }
+      if (a.use_gp && k + 1 < R6_N)  // the next point's features, from this lane's own copy of X[k+1]
+        r6_features_role(wave, xn, Ub + (k + 1) * R6_NU, a.gv.ls, a.gw.ls, zq[0], zq[1]);
     }
     __syncthreads();
     mark(0);
