@@ -303,7 +303,9 @@ __global__ __launch_bounds__(256, 2) void k_gemm128(int M, int N, int K, const d
   int kend = K;
   if (tri_a) kend = min(K, r0 + BT);
   d4_t acc[4][4];
-  mma128_tile(A, lda, B, ldb, M, N, r0, c0, 0, kend, sA, sB, acc);
+  // triangular rows: all of W for a store, the W rows above the alpha rows for SUMSQ
+  const int tri_rows = (tri_a && ksplit == 1) ? (EPI == EPI_SUMSQ ? msum : M) : -1;
+  mma128_tile<true>(A, lda, B, ldb, M, N, r0, c0, 0, kend, sA, sB, acc, tri_rows);
   if (EPI == EPI_STORE) {
 #pragma unroll
     for (int x = 0; x < 4; ++x)
@@ -311,7 +313,7 @@ __global__ __launch_bounds__(256, 2) void k_gemm128(int M, int N, int K, const d
       for (int y = 0; y < 4; ++y)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const int row = r0 + qi + x * 16 + mf_row(lane, r);
+          const int row = r0 + mma128_row(wave, x, true) + mf_row(lane, r);
           const int col = c0 + qj + y * 16 + mf_col(lane);
           if (row < M && col < N && (!lower_c || col <= row)) {
             double *p = C + (int64_t)row * ldc + col;
@@ -326,7 +328,7 @@ __global__ __launch_bounds__(256, 2) void k_gemm128(int M, int N, int K, const d
     for (int x = 0; x < 4; ++x)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int row = r0 + qi + x * 16 + mf_row(lane, r);
+        const int row = r0 + mma128_row(wave, x, true) + mf_row(lane, r);
         if (row < msum) {
 #pragma unroll
           for (int y = 0; y < 4; ++y) sq[y] = fma(acc[x][y][r], acc[x][y][r], sq[y]);

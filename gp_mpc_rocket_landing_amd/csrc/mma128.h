@@ -15,12 +15,26 @@
 // acc = A[r0.., k_lo:k_hi] B[c0.., k_lo:k_hi]^T for one 128 x 128 tile (wave w
 // owns quadrant (w/2, w%2)); k_lo must be a multiple of GK.  Ends on a barrier,
 // so the LDS can be reused by the caller straight away.
+// tri_rows >= 0: rows r < tri_rows of A are lower triangular (A[r][k] = 0 for
+// k > r) and rows >= M are padding, so a 16-row MFMA block whose rows are all
+// above the step's k, or all padding, multiplies exact zeros: it is skipped (the
+// diagonal K block of a triangular row tile, the padded last tile).  Same bits.
+// IL: wave w's four 16-row blocks interleaved with its partner's (rows 16 (w/2 + 2x),
+// mma128_row) instead of a contiguous 64-row half, so the two row halves of a
+// triangular tile carry the same mix of early- and late-dying blocks
+__device__ __forceinline__ int mma128_row(int wave, int x, bool il) {
+  return il ? 16 * ((wave >> 1) + 2 * x) : (wave >> 1) * 64 + 16 * x;
+}
+
+template <bool IL = false>
 __device__ __forceinline__ void mma128_tile(const double *__restrict__ A, int64_t lda,
                                             const double *__restrict__ B, int64_t ldb, int M, int N,
                                             int r0, int c0, int k_lo, int k_hi,
                                             double (*sA)[BT][GP], double (*sB)[BT][GP],
-                                            d4_t (&acc)[4][4]) {
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+                                            d4_t (&acc)[4][4], int tri_rows = -1) {
+  // the wave index through readfirstlane: the compiler then knows every per-wave
+  // quantity (and the triangular skips below) is uniform
+  const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
   const int qi = (wave >> 1) * 64, qj = (wave & 1) * 64;
 #pragma unroll
   for (int x = 0; x < 4; ++x)
@@ -61,23 +75,49 @@ __device__ __forceinline__ void mma128_tile(const double *__restrict__ A, int64_
   lstore(0);
   __syncthreads();
   int cur = 0;
-  for (int k0 = k_lo; k0 < k_hi; k0 += GK) {
+  // Skipped MFMA blocks (tri_rows >= 0).  A 16-row block x of this wave (rows
+  // R_x = r0 + mma128_row(x), increasing in x) multiplies exact zeros from the K step
+  // on whose first k is past R_x + 15 when all its rows are triangular, and always
+  // when all are padding.  The live blocks of a step are then a range [XF, XL); each
+  // range runs as a loop of its own over the steps it covers (a branch around the
+  // MFMAs, even a uniform one, made the compiler spill the accumulators), and every
+  // wave takes every step's barrier.
+  const int R0 = r0 + mma128_row(wave, 0, IL), R1 = r0 + mma128_row(wave, 1, IL);
+  const int R2 = r0 + mma128_row(wave, 2, IL), R3 = r0 + mma128_row(wave, 3, IL);
+  int k0 = k_lo;
+#define MMA_PHASE(XF, XL, KEND)                                                         \
+  for (const int ke_ = (KEND); k0 < ke_; k0 += GK) {                                     \
+    const bool more = k0 + GK < k_hi;                                                    \
+    if (more) gload(k0 + GK);                                                            \
+    _Pragma("unroll") for (int kk = 0; kk < GK; kk += 4) {                               \
+      const int kc = kk + (lane >> 4);                                                   \
+      double a[4], b[4];                                                                 \
+      _Pragma("unroll") for (int x = XF; x < XL; ++x) a[x] = sA[cur][mma128_row(wave, x, IL) + (lane & 15)][kc]; \
+      _Pragma("unroll") for (int y = 0; y < 4; ++y) b[y] = sB[cur][qj + 16 * y + (lane & 15)][kc];   \
+      _Pragma("unroll") for (int x = XF; x < XL; ++x)                                    \
+        _Pragma("unroll") for (int y = 0; y < 4; ++y) acc[x][y] = mfma_f64(a[x], b[y], acc[x][y]); \
+    }                                                                                    \
+    if (more) lstore(cur ^ 1);                                                           \
+    __syncthreads();                                                                     \
+    cur ^= 1;                                                                            \
+  }
+  if (tri_rows >= 0 && R3 + 15 < tri_rows) {  // all rows triangular: blocks die one by one
+    MMA_PHASE(0, 4, min(k_hi, R0 + 16))
+    MMA_PHASE(1, 4, min(k_hi, R1 + 16))
+    MMA_PHASE(2, 4, min(k_hi, R2 + 16))
+    MMA_PHASE(3, 4, min(k_hi, R3 + 16))
+  } else if (tri_rows >= 0 && R2 < M && R3 >= M) {  // the last block all padding
+    MMA_PHASE(0, 3, k_hi)
+  } else if (!(tri_rows >= 0 && R0 >= M)) {
+    MMA_PHASE(0, 4, k_hi)
+  }
+#undef MMA_PHASE
+  for (; k0 < k_hi; k0 += GK) {  // dead steps: staging only
     const bool more = k0 + GK < k_hi;
-    if (more) gload(k0 + GK);
-#pragma unroll
-    for (int kk = 0; kk < GK; kk += 4) {
-      const int kc = kk + (lane >> 4);
-      double a[4], b[4];
-#pragma unroll
-      for (int x = 0; x < 4; ++x) a[x] = sA[cur][qi + 16 * x + (lane & 15)][kc];
-#pragma unroll
-      for (int y = 0; y < 4; ++y) b[y] = sB[cur][qj + 16 * y + (lane & 15)][kc];
-#pragma unroll
-      for (int x = 0; x < 4; ++x)
-#pragma unroll
-        for (int y = 0; y < 4; ++y) acc[x][y] = mfma_f64(a[x], b[y], acc[x][y]);
+    if (more) {
+      gload(k0 + GK);
+      lstore(cur ^ 1);
     }
-    if (more) lstore(cur ^ 1);
     __syncthreads();
     cur ^= 1;
   }
