@@ -490,7 +490,7 @@ struct R6Smem {
   double dpl[R6_MD];                  // each equality row's identity entry (scaled)
   double gen[R6_MGEN * 3];            // general rows' values (scaled)
   // per end of the twisted sweep (0 top, 1 bottom):
-  double T[2][2][R6_SZ * R6_SZ];      // Gauss-Jordan block (ping-pong: one barrier per pivot)
+  double T[2][2][R6_TRI];             // the swept block, packed lower (ping-pong: one barrier per step)
   double Ct[2][R6_NX * R6_SZ];        // the coupling C_k (top) / E_k (bottom), 14 x 17
   double Sch[2][R6_NX * R6_NX];       // G_k C_k^T / H_k E_k^T, the next block's update
   double red[16][12];
@@ -668,10 +668,6 @@ __device__ __forceinline__ double r6_gen_dot(const R6Var &V, const double *v) {
 // -G_k goes to slot k (k < 15) and -H_k to slot k (k = 15..29) of s.G, over the
 // staged dynamics rows of its own stage once their last reader is done.
 #define R6_MID 15
-// Gauss-Jordan two pivots per barrier (0: one)
-#ifndef R6_GJ2
-#define R6_GJ2 1
-#endif
 
 __device__ __forceinline__ int r6_nat(int k, int e) {
   return k * R6_SZ + e - ((k > R6_MID && e >= R6_NX) ? R6_SZ : 0);
@@ -709,61 +705,59 @@ __device__ __forceinline__ double r6_m_next(const R6Smem &s, int k, int i, int e
   return (re * s.dpl[R6_NX + R6_NX * k + i]) * s.G[(k * R6_NX + i) * R6_SZ + e];
 }
 
-// one Gauss-Jordan pivot step of entry q of a block of width nb (pivot p)
-__device__ __forceinline__ double r6_gj_entry(const double *Tc, int q, int p, int nb, double inv) {
-  const int ti = q / R6_SZ, tj = q - ti * R6_SZ;
-  const double tip = Tc[ti * R6_SZ + p], tpj = Tc[p * R6_SZ + tj], tij = Tc[q];
-  const double f = tip * inv;
-  if (ti >= nb || tj >= nb) return tij;
-  if (ti == p && tj == p) return inv;
-  if (ti == p) return tpj * inv;
-  if (tj == p) return -f;
-  return tij - f * tpj;
+// (row, column) of packed-lower entry t
+__device__ __forceinline__ void r6_untri(int t, int &i, int &j) {
+  i = (int)((sqrt(8.0 * t + 1.0) - 1.0) * 0.5);
+  while (i * (i + 1) / 2 > t) --i;
+  while ((i + 1) * (i + 2) / 2 <= t) ++i;
+  j = t - i * (i + 1) / 2;
 }
 
-// two pivot steps at once (p, p + 1; ai = the inverse of T[P][P], row-major):
-// half the barriers of single steps, one more operand read per entry
-__device__ __forceinline__ double r6_gj2_entry(const double *Tc, int q, int p, int nb, const double (&ai)[4]) {
-  const int ti = q / R6_SZ, tj = q - ti * R6_SZ;
-  const double tij = Tc[q];
-  const double r0 = Tc[ti * R6_SZ + p], r1 = Tc[ti * R6_SZ + p + 1];    // T[ti][P]
-  const double c0 = Tc[p * R6_SZ + tj], c1 = Tc[(p + 1) * R6_SZ + tj];  // T[P][tj]
-  if (ti >= nb || tj >= nb) return tij;
-  const int di = ti - p, dj = tj - p;
-  const bool ip = di == 0 || di == 1, jp = dj == 0 || dj == 1;
-  if (ip && jp) return di == 0 ? (dj == 0 ? ai[0] : ai[1]) : (dj == 0 ? ai[2] : ai[3]);
-  if (ip) return di == 0 ? ai[0] * c0 + ai[1] * c1 : ai[2] * c0 + ai[3] * c1;
-  const double f0 = r0 * ai[0] + r1 * ai[2], f1 = r0 * ai[1] + r1 * ai[3];  // T[ti][P] A^-1
-  if (jp) return -(dj == 0 ? f0 : f1);
-  return tij - (f0 * c0 + f1 * c1);
-}
-
-// the Gauss-Jordan inverse of the block in T[0] (width nb) on threads lt (of nt);
-// the result lands in T[return value]
-__device__ __forceinline__ int r6_gj(double (*T)[R6_SZ * R6_SZ], int lt, int nt, int nb, int kfail, int &bad) {
+// The block inverse by the symmetric sweep operator on the packed lower triangle
+// (153 entries instead of Gauss-Jordan's 289: the block is SPD, so every
+// intermediate is symmetric), two pivots P = {p, p + 1} per barrier:
+//   W'[P][P] = -A^-1,  W'[i][P] = W[i][P] A^-1,  W'[i][j] = W[i][j] - W[i][P] A^-1 W[P][j]
+// with A = W[P][P]; after all pivots W = -S^-1.  Thread lt owns entry lt of T[0]
+// (one entry per thread); the result lands in T[return value].
+__device__ __forceinline__ int r6_sweep(double (*T)[R6_TRI], int lt, int nb, int kfail, int &bad) {
+  const bool own = lt < nb * (nb + 1) / 2;
+  int i = 0, j = 0;  // recomputed per call: kept live across the sweep loop they spilled more
+  if (own) r6_untri(lt, i, j);
   int cb = 0;
   for (int p = 0; p < nb; p += 2) {
-    const double *Tc = T[cb];
-    if (R6_GJ2 && p + 1 < nb) {
-      const double a = Tc[p * R6_SZ + p], b = Tc[p * R6_SZ + p + 1];
-      const double c = Tc[(p + 1) * R6_SZ + p], d = Tc[(p + 1) * R6_SZ + p + 1];
-      const double det = fma(a, d, -(b * c));
-      if (!(a > 0.0 && det > 0.0) && !bad) bad = kfail;  // both pivots positive
+    const double *W = T[cb];
+    double v = 0.0;
+    if (p + 1 < nb) {
+      const double a = W[r6_tri(p, p)], b = W[r6_tri(p + 1, p)], d = W[r6_tri(p + 1, p + 1)];
+      const double det = fma(a, d, -(b * b));
+      if (!(a > 0.0 && det > 0.0) && !bad) bad = kfail;  // both pivots positive (uniform)
+      // 1/det by v_rcp_f64 + two Newton steps (blk_recip, within an ulp of the division)
       const double rd = blk_recip(det);
-      const double ai[4] = {d * rd, -b * rd, -c * rd, a * rd};
-      for (int q = lt; q < R6_SZ * R6_SZ; q += nt) T[cb ^ 1][q] = r6_gj2_entry(Tc, q, p, nb, ai);
+      const double ia = d * rd, ib = -b * rd, id = a * rd;  // A^-1 = [ia ib; ib id]
+      if (own) {
+        const double wij = W[lt];
+        const double wip = W[r6_tri(i, p)], wiq = W[r6_tri(i, p + 1)];
+        const double wjp = W[r6_tri(j, p)], wjq = W[r6_tri(j, p + 1)];
+        const int di = i - p, dj = j - p;  // i >= j
+        const bool ip = di == 0 || di == 1, jp = dj == 0 || dj == 1;
+        if (ip && jp) v = -(di + dj == 0 ? ia : (di + dj == 1 ? ib : id));
+        else if (jp) v = dj == 0 ? wip * ia + wiq * ib : wip * ib + wiq * id;  // W[i][P] A^-1
+        else if (ip) v = di == 0 ? ia * wjp + ib * wjq : ib * wjp + id * wjq;  // A^-1 W[P][j]
+        else v = wij - ((wip * ia + wiq * ib) * wjp + (wip * ib + wiq * id) * wjq);
+      }
     } else {
-      for (int pp = p; pp < p + 2 && pp < nb; ++pp) {
-        const double *Tp = T[cb];
-        const double piv = Tp[pp * R6_SZ + pp];
-        if (!(piv > 0.0) && !bad) bad = kfail;
-        // 1/piv by v_rcp_f64 + two Newton steps (blk_recip, within an ulp of the
-        // division) instead of an IEEE division per entry on every pivot's path
-        const double inv = blk_recip(piv);
-        for (int q = lt; q < R6_SZ * R6_SZ; q += nt) T[cb ^ 1][q] = r6_gj_entry(Tp, q, pp, nb, inv);
-        if (pp + 1 < p + 2 && pp + 1 < nb) { cb ^= 1; __syncthreads(); }
+      const double d = W[r6_tri(p, p)];
+      if (!(d > 0.0) && !bad) bad = kfail;
+      const double inv = blk_recip(d);
+      if (own) {
+        const double wij = W[lt], wip = W[r6_tri(i, p)], wjp = W[r6_tri(j, p)];
+        if (i == p && j == p) v = -inv;
+        else if (j == p) v = wip * inv;
+        else if (i == p) v = wjp * inv;
+        else v = wij - (wip * inv) * wjp;
       }
     }
+    if (own) T[cb ^ 1][lt] = v;
     cb ^= 1;
     __syncthreads();
   }
@@ -806,21 +800,21 @@ __device__ __forceinline__ int r6_factor(R6Smem &s, R6Var (&V)[2], R6Row (&R)[2]
   }
   __syncthreads();
   mark(2);  // (stamps: the assembly)
-  // the sweep: threads 0-255 the top end, 256-511 the bottom end.  The
-  // Gauss-Jordan pivots read one copy of the block and write the other, so a
-  // pivot needs one workgroup barrier instead of two.
+  // the sweep: threads 0-255 the top end, 256-511 the bottom end.  The pivot
+  // steps read one copy of the block and write the other, so a step needs one
+  // workgroup barrier instead of two.
   const int half = tid >> 8, lt = tid & 255;
-  constexpr int BB = R6_SZ * R6_SZ;
   int bad = 0;
   for (int t = 0; t < R6_MID; ++t) {
     const int k = half ? R6_N - t : t;    // factor block
     const int kc = half ? k - 1 : k;      // its coupling's slot
-    double (*T)[BB] = s.T[half];
-    for (int q = lt; q < BB; q += 256) {
-      const int ti = q / R6_SZ, tj = q - ti * R6_SZ;
-      double v = s.Sinv[k * R6_TRI + r6_tri(ti, tj)];
-      if (t > 0 && ti < R6_NX && tj < R6_NX) v -= s.Sch[half][ti * R6_NX + tj];
-      T[0][q] = v;
+    double (*T)[R6_TRI] = s.T[half];
+    if (lt < R6_TRI) {
+      int ti, tj;
+      r6_untri(lt, ti, tj);
+      double v = s.Sinv[k * R6_TRI + lt];
+      if (t > 0 && ti < R6_NX) v -= s.Sch[half][ti * R6_NX + tj];  // tj <= ti
+      T[0][lt] = v;
     }
     if (lt < R6_NX * R6_SZ) {  // top C_k[i][c]: x_k+1[i] with (k, c); bottom E_k-1[i][c]: x_k-1[i] with entry c of block k
       const int i = lt / R6_SZ, c = lt - i * R6_SZ;
@@ -831,19 +825,16 @@ __device__ __forceinline__ int r6_factor(R6Smem &s, R6Var (&V)[2], R6Row (&R)[2]
       s.Ct[half][lt] = v;
     }
     __syncthreads();
-    const int cb = r6_gj(T, lt, 256, R6_SZ, k + 1, bad);  // bad: uniform over the half
-    for (int q = lt; q < BB; q += 256) {
-      const int ti = q / R6_SZ, tj = q - ti * R6_SZ;
-      if (ti >= tj) s.Sinv[k * R6_TRI + r6_tri(ti, tj)] = T[cb][q];
-    }
+    const int cb = r6_sweep(T, lt, R6_SZ, k + 1, bad);  // W = -S_k^-1; bad: uniform over the half
+    if (lt < R6_TRI) s.Sinv[k * R6_TRI + lt] = -T[cb][lt];
     mark(10);
-    // -G_k = -C_k S_k^-1 / -H_k-1 = -E_k-1 T_k^-1 over the staged rows of its slot
+    // -G_k = -C_k S_k^-1 = C_k W / -H_k-1 over the staged rows of its slot
     double *Gs = s.G + kc * R6_NX * R6_SZ;
     if (lt < R6_NX * R6_SZ) {
       const int i = lt / R6_SZ, c = lt - i * R6_SZ;
       double acc = 0.0;
-      for (int e = 0; e < R6_SZ; ++e) acc += s.Ct[half][i * R6_SZ + e] * T[cb][e * R6_SZ + c];
-      Gs[lt] = -acc;  // stored negated: the chains accumulate
+      for (int e = 0; e < R6_SZ; ++e) acc += s.Ct[half][i * R6_SZ + e] * T[cb][r6_tri(e, c)];
+      Gs[lt] = acc;  // stored negated: the chains accumulate
     }
     __syncthreads();
     if (lt < R6_NX * R6_NX) {  // the next block's update G_k C_k^T / H_k-1 E_k-1^T (14 x 14)
@@ -855,20 +846,17 @@ __device__ __forceinline__ int r6_factor(R6Smem &s, R6Var (&V)[2], R6Row (&R)[2]
     __syncthreads();
     mark(11);
   }
-  // the middle block Z = D_15 - G_14 C_14^T - H_15 E_15^T, 14 wide
-  double (*T)[BB] = s.T[0];
-  if (tid < BB) {
-    const int ti = tid / R6_SZ, tj = tid - ti * R6_SZ;
-    double v = s.Sinv[R6_MID * R6_TRI + r6_tri(ti, tj)];
-    if (ti < R6_NX && tj < R6_NX) v = (v - s.Sch[0][ti * R6_NX + tj]) - s.Sch[1][ti * R6_NX + tj];
-    T[0][tid] = v;
+  // the middle block Z = D_15 - G_14 C_14^T - H_15 E_15^T, 14 wide (packed: the first 105)
+  double (*T)[R6_TRI] = s.T[0];
+  constexpr int MT = R6_NX * (R6_NX + 1) / 2;
+  if (tid < MT) {
+    int mi, mj;
+    r6_untri(tid, mi, mj);
+    T[0][tid] = (s.Sinv[R6_MID * R6_TRI + tid] - s.Sch[0][mi * R6_NX + mj]) - s.Sch[1][mi * R6_NX + mj];
   }
   __syncthreads();
-  const int cb = r6_gj(T, tid, R6_T, R6_NX, R6_MID + 1, bad);
-  if (tid < BB) {
-    const int ti = tid / R6_SZ, tj = tid - ti * R6_SZ;
-    if (ti >= tj) s.Sinv[R6_MID * R6_TRI + r6_tri(ti, tj)] = (ti < R6_NX && tj < R6_NX) ? T[cb][tid] : 0.0;
-  }
+  const int cb = r6_sweep(T, tid, R6_NX, R6_MID + 1, bad);
+  if (tid < R6_TRI) s.Sinv[R6_MID * R6_TRI + tid] = tid < MT ? -T[cb][tid] : 0.0;
   if (lt == 0) s.bad[half] = bad;
   __syncthreads();
   mark(10);
