@@ -303,9 +303,10 @@ __global__ __launch_bounds__(256, 2) void k_gemm128(int M, int N, int K, const d
   int kend = K;
   if (tri_a) kend = min(K, r0 + BT);
   d4_t acc[4][4];
-  // triangular rows: all of W for a store, the W rows above the alpha rows for SUMSQ
-  const int tri_rows = (tri_a && ksplit == 1) ? (EPI == EPI_SUMSQ ? msum : M) : -1;
-  mma128_tile<true>(A, lda, B, ldb, M, N, r0, c0, 0, kend, sA, sB, acc, tri_rows);
+  // triangular rows: all of W for a store, the W rows above the alpha rows for SUMSQ,
+  // none for a plain A (0: only its padding rows are skipped)
+  const int tri_rows = ksplit > 1 ? -1 : (tri_a ? (EPI == EPI_SUMSQ ? msum : M) : 0);
+  mma128_tile<true>(A, lda, B, ldb, M, N, r0, c0, 0, kend, sA, sB, acc, tri_rows, lower_c != 0);
   if (EPI == EPI_STORE) {
 #pragma unroll
     for (int x = 0; x < 4; ++x)
@@ -555,7 +556,7 @@ __global__ __launch_bounds__(256, 2) void k_gemm128_sk(int M, int N, int K,
     const int r0 = by * BT, c0 = bx * BT;
     d4_t acc[4][4];
     mma128_tile(A + bz * sA_, lda, B + bz * sB_, ldb, M, N, r0, c0, j0 * GK, min(K, j1 * GK), sA,
-                sB, acc);
+                sB, acc, 0, tri != 0);  // padding rows of the last row tile skipped
     double *Cb = C + bz * sC_;
 #pragma unroll
     for (int x = 0; x < 4; ++x)

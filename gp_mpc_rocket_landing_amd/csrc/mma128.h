@@ -16,9 +16,11 @@
 // owns quadrant (w/2, w%2)); k_lo must be a multiple of GK.  Ends on a barrier,
 // so the LDS can be reused by the caller straight away.
 // tri_rows >= 0: rows r < tri_rows of A are lower triangular (A[r][k] = 0 for
-// k > r) and rows >= M are padding, so a 16-row MFMA block whose rows are all
-// above the step's k, or all padding, multiplies exact zeros: it is skipped (the
-// diagonal K block of a triangular row tile, the padded last tile).  Same bits.
+// k > r; 0: none is) and rows >= M are padding, so a 16-row MFMA block whose rows
+// are all above the step's k, or all padding, multiplies exact zeros: it is
+// skipped (the diagonal K block of a triangular row tile, the padded last tile).
+// lower_out: only the lower triangle of the output is used, so a diagonal tile's
+// blocks wholly above the diagonal are skipped.  Same bits.
 // IL: wave w's four 16-row blocks interleaved with its partner's (rows 16 (w/2 + 2x),
 // mma128_row) instead of a contiguous 64-row half, so the two row halves of a
 // triangular tile carry the same mix of early- and late-dying blocks
@@ -31,7 +33,7 @@ __device__ __forceinline__ void mma128_tile(const double *__restrict__ A, int64_
                                             const double *__restrict__ B, int64_t ldb, int M, int N,
                                             int r0, int c0, int k_lo, int k_hi,
                                             double (*sA)[BT][GP], double (*sB)[BT][GP],
-                                            d4_t (&acc)[4][4], int tri_rows = -1) {
+                                            d4_t (&acc)[4][4], int tri_rows = -1, bool lower_out = false) {
   // the wave index through readfirstlane: the compiler then knows every per-wave
   // quantity (and the triangular skips below) is uniform
   const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
@@ -85,33 +87,57 @@ __device__ __forceinline__ void mma128_tile(const double *__restrict__ A, int64_
   const int R0 = r0 + mma128_row(wave, 0, IL), R1 = r0 + mma128_row(wave, 1, IL);
   const int R2 = r0 + mma128_row(wave, 2, IL), R3 = r0 + mma128_row(wave, 3, IL);
   int k0 = k_lo;
-#define MMA_PHASE(XF, XL, KEND)                                                         \
+// MFMA block (x, y) runs when bit 4 x + y of MASK is set (a literal: the unrolled
+// loops fold the tests away)
+#define MMA_PHASE_M(MASK, KEND)                                                          \
   for (const int ke_ = (KEND); k0 < ke_; k0 += GK) {                                     \
     const bool more = k0 + GK < k_hi;                                                    \
     if (more) gload(k0 + GK);                                                            \
     _Pragma("unroll") for (int kk = 0; kk < GK; kk += 4) {                               \
       const int kc = kk + (lane >> 4);                                                   \
       double a[4], b[4];                                                                 \
-      _Pragma("unroll") for (int x = XF; x < XL; ++x) a[x] = sA[cur][mma128_row(wave, x, IL) + (lane & 15)][kc]; \
+      _Pragma("unroll") for (int x = 0; x < 4; ++x)                                      \
+        if (((MASK) >> (4 * x)) & 15) a[x] = sA[cur][mma128_row(wave, x, IL) + (lane & 15)][kc]; \
       _Pragma("unroll") for (int y = 0; y < 4; ++y) b[y] = sB[cur][qj + 16 * y + (lane & 15)][kc];   \
-      _Pragma("unroll") for (int x = XF; x < XL; ++x)                                    \
-        _Pragma("unroll") for (int y = 0; y < 4; ++y) acc[x][y] = mfma_f64(a[x], b[y], acc[x][y]); \
+      _Pragma("unroll") for (int x = 0; x < 4; ++x)                                      \
+        _Pragma("unroll") for (int y = 0; y < 4; ++y)                                    \
+          if (((MASK) >> (4 * x + y)) & 1) acc[x][y] = mfma_f64(a[x], b[y], acc[x][y]);  \
     }                                                                                    \
     if (more) lstore(cur ^ 1);                                                           \
     __syncthreads();                                                                     \
     cur ^= 1;                                                                            \
   }
-  if (tri_rows >= 0 && R3 + 15 < tri_rows) {  // all rows triangular: blocks die one by one
+#define MMA_PHASE(XF, XL, KEND) MMA_PHASE_M(((0xFFFF << (4 * (XF))) & (0xFFFF >> (4 * (4 - (XL))))), KEND)
+  if (lower_out && r0 == c0) {
+    // a diagonal tile of a lower-triangular output: the blocks wholly above the
+    // diagonal are never stored, so they are not computed (the live pattern of
+    // wave (w/2, w%2) for its row mapping; one wave of the contiguous mapping has none)
+    const int wi = wave >> 1, wj = wave & 1;
+    if (IL) {
+      if (wj == 0 && wi == 0) { MMA_PHASE_M(0xFF71, k_hi) }
+      else if (wj == 0) { MMA_PHASE_M(0xFFF3, k_hi) }
+      else if (wi == 0) { MMA_PHASE_M(0x7100, k_hi) }
+      else { MMA_PHASE_M(0xF300, k_hi) }
+    } else {
+      if (wi == wj) { MMA_PHASE_M(0xF731, k_hi) }
+      else if (wi == 1) { MMA_PHASE_M(0xFFFF, k_hi) }
+    }
+  } else if (tri_rows >= 0 && R3 + 15 < tri_rows) {  // all rows triangular: blocks die one by one
     MMA_PHASE(0, 4, min(k_hi, R0 + 16))
     MMA_PHASE(1, 4, min(k_hi, R1 + 16))
     MMA_PHASE(2, 4, min(k_hi, R2 + 16))
     MMA_PHASE(3, 4, min(k_hi, R3 + 16))
-  } else if (tri_rows >= 0 && R2 < M && R3 >= M) {  // the last block all padding
-    MMA_PHASE(0, 3, k_hi)
-  } else if (!(tri_rows >= 0 && R0 >= M)) {
+  } else if (tri_rows < 0 || R3 < M) {
     MMA_PHASE(0, 4, k_hi)
+  } else if (R2 < M) {  // padding rows (>= M) from block 3, 2 or 1 on
+    MMA_PHASE(0, 3, k_hi)
+  } else if (R1 < M) {
+    MMA_PHASE(0, 2, k_hi)
+  } else if (R0 < M) {
+    MMA_PHASE(0, 1, k_hi)
   }
 #undef MMA_PHASE
+#undef MMA_PHASE_M
   for (; k0 < k_hi; k0 += GK) {  // dead steps: staging only
     const bool more = k0 + GK < k_hi;
     if (more) {

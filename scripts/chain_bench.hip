@@ -17,6 +17,23 @@ __device__ __forceinline__ void fbc(double &acc, double src, double mul) {
                  : "+v"(acc) : "v"(src), "v"(mul), "i"(J));
 }
 
+// the sum of this lane's value and its partner's in the other row of the row pair
+// (rows 0/1, 2/3): v_permlane16_swap on both halves, then one add; both rows get
+// the same bits (the add is commutative)
+__device__ __forceinline__ double pair_sum(double v) {
+  const unsigned lo = __double2loint(v), hi = __double2hiint(v);
+  const auto l = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
+  const auto h = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+  return __hiloint2double(h[0], l[0]) + __hiloint2double(h[1], l[1]);
+}
+// odd rows rotated by 8 lanes (DPP row_ror:8 on both halves, rows 1 and 3 only)
+__device__ __forceinline__ double ror8_odd(double v) {
+  const int lo = __double2loint(v), hi = __double2hiint(v);
+  const int l = __builtin_amdgcn_update_dpp(lo, lo, 0x128, 0xa, 0xf, false);
+  const int h = __builtin_amdgcn_update_dpp(hi, hi, 0x128, 0xa, 0xf, false);
+  return __hiloint2double(h, l);
+}
+
 #define STEPS 15
 template <int MODE>
 __global__ __launch_bounds__(512) void k(double *out, long long *cyc, int reps, int nw) {
@@ -54,6 +71,19 @@ __global__ __launch_bounds__(512) void k(double *out, long long *cyc, int reps, 
           fbc<10>(a0, y, g[10]); g[10] = fn[10]; fbc<11>(a1, y, g[11]); g[11] = fn[11];
           fbc<12>(a0, y, g[12]); g[12] = fn[12]; fbc<13>(a1, y, g[13]); g[13] = fn[13];
           fbc<14>(a0, y, g[14]); g[14] = fn[14]; fbc<15>(a1, y, g[15]); g[15] = fn[15];
+        } else if (MODE == 3) {
+          // two rows: row 0 terms 0..7, row 1 terms 8..15 (its vector rotated by 8),
+          // operands in 16-byte pairs, then the pair sum and the odd rows' rotation
+          const double2 *f2 = reinterpret_cast<const double2 *>(fn + ((lane & 16) ? 8 : 0));
+          double2 p;
+          if (lane & 16) a0 = 0.0;
+          fbc<0>(a0, y, g[0]); fbc<1>(a1, y, g[1]); p = f2[0]; g[0] = p.x; g[1] = p.y;
+          fbc<2>(a0, y, g[2]); fbc<3>(a1, y, g[3]); p = f2[1]; g[2] = p.x; g[3] = p.y;
+          fbc<4>(a0, y, g[4]); fbc<5>(a1, y, g[5]); p = f2[2]; g[4] = p.x; g[5] = p.y;
+          fbc<6>(a0, y, g[6]); fbc<7>(a1, y, g[7]); p = f2[3]; g[6] = p.x; g[7] = p.y;
+          y = ror8_odd(pair_sum(a0 + a1));
+          *(lane < 14 ? &Y[t + 1][rr] : &dump[lane]) = y;
+          continue;
         } else {
           const double2 *f2 = reinterpret_cast<const double2 *>(fn);
           double2 p;
@@ -82,12 +112,13 @@ int main() {
   hipMalloc(&out, sizeof(double) * 512);
   hipMalloc(&cyc, sizeof(long long));
   const int reps = 200;
-  const char *nm[3] = {"registers", "b64 each", "b128 pairs"};
+  const char *nm[4] = {"registers", "b64 each", "b128 pairs", "two rows"};
   for (int nw = 1; nw <= 2; ++nw)
-    for (int m = 0; m < 3; ++m) {
+    for (int m = 0; m < 4; ++m) {
       if (m == 0) hipLaunchKernelGGL(k<0>, dim3(1), dim3(512), 0, 0, out, cyc, reps, nw);
       if (m == 1) hipLaunchKernelGGL(k<1>, dim3(1), dim3(512), 0, 0, out, cyc, reps, nw);
       if (m == 2) hipLaunchKernelGGL(k<2>, dim3(1), dim3(512), 0, 0, out, cyc, reps, nw);
+      if (m == 3) hipLaunchKernelGGL(k<3>, dim3(1), dim3(512), 0, 0, out, cyc, reps, nw);
       long long h = 0;
       hipMemcpy(&h, cyc, sizeof(h), hipMemcpyDeviceToHost);
       printf("%d chain wave(s), %-11s %8.1f ticks per step (incl. the per-pass barrier)\n", nw, nm[m],
