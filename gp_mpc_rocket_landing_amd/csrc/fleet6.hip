@@ -899,6 +899,23 @@ __device__ __forceinline__ void r6_diag_row(R6Smem &s, int k, int a) {
   }
 }
 
+// the sum of a lane's value and its partner's in the other row of its row pair
+// (rows 0/1, 2/3): v_permlane16_swap on both halves, one add; both rows get the
+// same bits (the add commutes)
+__device__ __forceinline__ double pair_sum(double v) {
+  const unsigned lo = __double2loint(v), hi = __double2hiint(v);
+  const auto l = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
+  const auto h = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+  return __hiloint2double(h[0], l[0]) + __hiloint2double(h[1], l[1]);
+}
+// rows 1 and 3 rotated by 8 lanes (DPP row_ror:8 on both halves); rows 0, 2 unchanged
+__device__ __forceinline__ double ror8_odd(double v) {
+  const int lo = __double2loint(v), hi = __double2hiint(v);
+  const int l = __builtin_amdgcn_update_dpp(lo, lo, 0x128, 0xa, 0xf, false);
+  const int h = __builtin_amdgcn_update_dpp(hi, hi, 0x128, 0xa, 0xf, false);
+  return __hiloint2double(h, l);
+}
+
 // x~ = M^-1 rhs, twisted: the forward chains (wave 0: y down the top blocks to
 // y_15; wave 1: z up the bottom blocks, then z'_15 = -H_15 z_16), the 31 diagonal
 // products (the middle on y_15 + z'_15), the backward chains (wave 0: x_14 .. x_0
@@ -916,53 +933,53 @@ template <class MK>
 __device__ __forceinline__ void r6_solve(R6Smem &s, MK &mark) {
   const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
   if (wv < 2) {
-    // every term's operand for the NEXT step loads right after the term's FMA,
-    // into the register it frees: one buffer, the loads a step ahead
+    // Two DPP rows per end: row h = 0 takes terms 0-7 and row 1 terms 8-15 of the
+    // 16 on the chain, row 1 holding the vector rotated by 8 lanes so that its
+    // broadcasts 0-7 reach entries 8-15; the pair sum (v_permlane16_swap) gives both
+    // rows the new entry and row 1 rotates it back.  Half the dependent FMAs and half
+    // the operand reads per block step.  Rows 2 and 3 repeat rows 0 and 1.
+    // Every term's operand pair for the NEXT step loads right after the pair's FMAs.
     const bool bot = wv == 1;
-    const int rr = lane & 15;
-    const bool pass = rr >= R6_NX;
-    const int off = (bot && pass) ? rr - R6_SZ : rr;
+    const int m = lane & 15, h = (lane >> 4) & 1;
+    const int ms = h ? (m + 8) & 15 : m;  // the entry this lane's vector register holds
+    const bool pass = m >= R6_NX;         // output m: a pass-through entry (14, 15)
+    auto offo = [&](int e) { return (bot && e >= R6_NX) ? e - R6_SZ : e; };
     const int o16 = bot ? -1 : R6_SZ - 1;
     const int db = bot ? -R6_SZ : R6_SZ;
     const int gs = pass ? 0 : (bot ? -R6_NX * R6_SZ : R6_NX * R6_SZ);
     const double *F = s.G;
-    int go = pass ? (int)(s.zero - s.G) : (bot ? R6_N - 1 : 0) * R6_NX * R6_SZ + rr * R6_SZ;
+    int go = pass ? (int)(s.zero - s.G) : (bot ? R6_N - 1 : 0) * R6_NX * R6_SZ + m * R6_SZ;
+    const int gh = 8 * h;
     int ib = bot ? R6_N * R6_SZ : 0;
-    double g[R6_SZ];
+    double g[8];
 #pragma unroll
-    for (int e = 0; e < R6_SZ; ++e) g[e] = F[go + e];
-    double y = s.rhs[ib + off];
-    double b16 = s.rhs[ib + o16], bn = s.rhs[ib + db + off];
+    for (int e = 0; e < 8; ++e) g[e] = F[go + gh + e];
+    double g16 = F[go + R6_SZ - 1];
+    double y = s.rhs[ib + offo(ms)];
+    double b16 = s.rhs[ib + o16], bn = s.rhs[ib + db + offo(m)];
 #pragma unroll 3
     for (int t = 0; t < R6_MID; ++t) {
       const bool last = t == R6_MID - 1;
       const int gn = go + gs;
-      const double init = fma(g[R6_SZ - 1], b16, (bot && last) ? 0.0 : bn);
+      const double init = h ? 0.0 : fma(g16, b16, (bot && last) ? 0.0 : bn);
       b16 = s.rhs[ib + db + o16];
-      bn = s.rhs[ib + 2 * db + off];
-      g[R6_SZ - 1] = F[gn + R6_SZ - 1];
+      bn = s.rhs[ib + 2 * db + offo(m)];
+      g16 = F[gn + R6_SZ - 1];
       double a0 = init, a1 = 0.0;
       fmac_bc<0, true>(a0, y, g[0]); fmac_bc<1, false>(a1, y, g[1]);
-      g[0] = F[gn + 0]; g[1] = F[gn + 1];
+      g[0] = F[gn + gh + 0]; g[1] = F[gn + gh + 1];
       fmac_bc<2, false>(a0, y, g[2]); fmac_bc<3, false>(a1, y, g[3]);
-      g[2] = F[gn + 2]; g[3] = F[gn + 3];
+      g[2] = F[gn + gh + 2]; g[3] = F[gn + gh + 3];
       fmac_bc<4, false>(a0, y, g[4]); fmac_bc<5, false>(a1, y, g[5]);
-      g[4] = F[gn + 4]; g[5] = F[gn + 5];
+      g[4] = F[gn + gh + 4]; g[5] = F[gn + gh + 5];
       fmac_bc<6, false>(a0, y, g[6]); fmac_bc<7, false>(a1, y, g[7]);
-      g[6] = F[gn + 6]; g[7] = F[gn + 7];
-      fmac_bc<8, false>(a0, y, g[8]); fmac_bc<9, false>(a1, y, g[9]);
-      g[8] = F[gn + 8]; g[9] = F[gn + 9];
-      fmac_bc<10, false>(a0, y, g[10]); fmac_bc<11, false>(a1, y, g[11]);
-      g[10] = F[gn + 10]; g[11] = F[gn + 11];
-      fmac_bc<12, false>(a0, y, g[12]); fmac_bc<13, false>(a1, y, g[13]);
-      g[12] = F[gn + 12]; g[13] = F[gn + 13];
-      fmac_bc<14, false>(a0, y, g[14]); fmac_bc<15, false>(a1, y, g[15]);
-      g[14] = F[gn + 14]; g[15] = F[gn + 15];
-      y = a0 + a1;
+      g[6] = F[gn + gh + 6]; g[7] = F[gn + gh + 7];
+      const double sum = pair_sum(a0 + a1);  // entry m of the next block, on both rows
+      y = ror8_odd(sum);
       // unconditional store (pass-through and idle lanes to the dump): no
       // exec-mask branch in the loop, so the LDS wait at the next step is exact
-      double *dst = (!pass && lane < 16) ? ((bot && last) ? &s.zmid[rr] : &s.rhs[ib + db + rr]) : &s.dump[lane];
-      *dst = y;
+      double *dst = (!pass && lane < 16) ? ((bot && last) ? &s.zmid[m] : &s.rhs[ib + db + m]) : &s.dump[lane];
+      *dst = sum;
       go = gn;
       ib += db;
       // the two ends walk in opposite directions, so a step's address is no
