@@ -321,27 +321,34 @@ __device__ __forceinline__ int diag128_core(double (*S)[DP], double *col, int &s
         }
       }
       lds_barrier();
+      // X is final L (later steps touch only columns beyond this block): it goes to
+      // global memory from the registers as well (the diagonal blocks went out in step 1)
 #pragma unroll
       for (int q = 0; q < 3; ++q) {
         const int t = wave + 4 * q;
         if (t < nt) {
           const int rb = c0 + NB + (t >> 1) * 16, cb = (t & 1) * 16;
 #pragma unroll
-          for (int r = 0; r < 4; ++r) S[rb + mf_row(lane, r)][c0 + cb + li] = acc[q][r];
+          for (int r = 0; r < 4; ++r) {
+            const int row = rb + mf_row(lane, r);
+            S[row][c0 + cb + li] = acc[q][r];
+            if (row < pw) M[(int64_t)row * lda + c0 + cb + li] = acc[q][r];
+          }
         }
       }
       lds_barrier();
       mark(2);
     }
   }
-  // off-diagonal blocks of L to global memory (diagonal blocks went out in step 1)
+  mark(4);
+  if (pw < DB || !Li) return 0;  // the last panel has no rows below: no inverse needed
+  // Linv's diagonal blocks (T_i, lower; zero above) and zero upper blocks now;
+  // the off-diagonal blocks go out from the registers as they are formed below
 #pragma unroll 4
   for (int e = tid; e < DB * DB; e += 256) {
     const int i = e >> 7, j = e & 127;
-    if ((j >> 5) < (i >> 5) && i < pw) M[(int64_t)i * lda + j] = S[i][j];
+    if ((j >> 5) >= (i >> 5)) Li[e] = (j > i) ? 0.0 : S[i][j];
   }
-  mark(4);
-  if (pw < DB || !Li) return 0;  // the last panel has no rows below: no inverse needed
   // ---- inverse, block row i = 1..3:  Y_j = sum_k L_ik X_kj -> upper block (j, i)
   // transposed; then X_ij = -T_i Y_j in place.  Jobs: (j, 16x16 tile) pairs.
   for (int i = 1; i < DB / NB; ++i) {
@@ -398,17 +405,16 @@ __device__ __forceinline__ int diag128_core(double (*S)[DP], double *col, int &s
       if (jt < njob) {
         const int j = jt >> 2, rb = (jt >> 1 & 1) * 16, cb = (jt & 1) * 16;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) S[j * NB + cb + li][i * NB + rb + mf_row(lane, r)] = -acc[q][r];
+        for (int r = 0; r < 4; ++r) {
+          const int row = i * NB + rb + mf_row(lane, r);
+          S[j * NB + cb + li][row] = -acc[q][r];
+          Li[row * DB + j * NB + cb + li] = -acc[q][r];
+        }
       }
     }
     lds_barrier();
   }
   mark(5);
-#pragma unroll 4
-  for (int e = tid; e < DB * DB; e += 256) {
-    const int i = e >> 7, j = e & 127;
-    Li[e] = (j > i) ? 0.0 : ((i >> 5) == (j >> 5) ? S[i][j] : S[j][i]);
-  }
   mark(6);
   return 0;
 }
@@ -617,9 +623,20 @@ static hipError_t launch_potrf_batched128(hipStream_t s, int n, int batch, doubl
   hipError_t e = hipMemsetAsync(info, 0, sizeof(int) * batch, s);
   if (e != hipSuccess) return e;
   auto at = [&](int r, int c) { return A + (int64_t)r * lda + c; };
+  // few matrices: the panel solve and the trailing SYRK in the latency form
+  // (k_gemm_lat: one memory round trip per launch instead of K / 16);
+  // GPMPC_POTRF_LAT = 0 / 1 forces it off / on, default for batch <= lat_max
+  static const int lat_env = [] {
+    const char *v = getenv("GPMPC_POTRF_LAT");
+    return v ? atoi(v) : -1;
+  }();
+  const bool lat = lat_env >= 0 ? lat_env > 0 : batch <= 16;
   // panel solve A[c+128:n, c:c+128] <- A[c+128:n, c:c+128] Linv^T (in place)
   auto psolve = [&](int c) {
     const int r = c + DB;
+    if (lat)
+      return launch_gemm_lat(s, 0, n - r, DB, DB, at(r, c), lda, Linv, DB, at(r, c), lda, 1.0, 0.0,
+                             1, batch, stride, (int64_t)DB * DB, stride);
     return launch_gemm_nt_rowblock(s, n - r, DB, DB, at(r, c), lda, Linv, DB, at(r, c), lda, 1.0,
                                    0.0, batch, stride, (int64_t)DB * DB, stride);
   };
@@ -652,8 +669,12 @@ static hipError_t launch_potrf_batched128(hipStream_t s, int n, int batch, doubl
     }
     const int t0 = K0 + pw;
     if (t0 < n) {
-      e = launch_gemm_nt(s, EPI_STORE, n - t0, n - t0, pw, at(t0, K0), lda, at(t0, K0), lda,
-                         at(t0, t0), lda, -1.0, 1.0, 0, 1, batch, stride, stride, stride);
+      if (lat && pw <= DB)
+        e = launch_gemm_lat(s, 1, n - t0, n - t0, pw, at(t0, K0), lda, nullptr, lda, at(t0, t0),
+                            lda, -1.0, 1.0, 0, batch, stride, stride, stride);
+      else
+        e = launch_gemm_nt(s, EPI_STORE, n - t0, n - t0, pw, at(t0, K0), lda, at(t0, K0), lda,
+                           at(t0, t0), lda, -1.0, 1.0, 0, 1, batch, stride, stride, stride);
       if (e != hipSuccess) return e;
     }
   }

@@ -573,6 +573,126 @@ __global__ __launch_bounds__(256, 2) void k_gemm128_sk(int M, int N, int K,
   }
 }
 
+// ---------------------------------------------------------------------------
+// Latency form for short products (K <= 128) on few matrices: the Cholesky's
+// panel solve and trailing SYRK at batch 1-16, where the pipelined tile kernels
+// above spend their time in K / 16 dependent global-load round trips (13 us for
+// a K = 128 SYRK of three workgroups, 29 us for a 128 x 128 x 128 panel tile on
+// one CU).  Each wave owns a 16 x 32 block of C and loads its whole operand
+// strip straight into registers -- 16 two-double loads per 16-row fragment,
+// all in flight at once -- then runs the MFMAs: one memory round trip per
+// launch.  Chunk t of 8 k's: lane l holds k = 8t + 2(l >> 4) + {0, 1} of row /
+// column l & 15, used by two MFMAs (.x, .y); A and B share the permutation, so
+// every k is summed once.
+//   MODE 0 (rows, in place): a workgroup owns rows [16 bx, +16) x all N <= 128
+//     columns (wave w: columns 32w..), so C may alias A: every wave's loads are
+//     consumed before the barrier that precedes the stores.  tri_b: B is lower
+//     triangular (B[c][k] = 0 for k > c), column block c0 stops at k < c0 + 32.
+//   MODE 1 (lower): C = alpha A A^T + beta C over the lower 32 x 32 blocks of an
+//     M x M matrix (B = A), two waves per block (row halves).
+#define LAT_CH 16  // 16 chunks of 8 = K <= 128
+template <int MODE>
+__global__ __launch_bounds__(256) void k_gemm_lat(int M, int N, int K, const double *A, int64_t lda,
+                                                  const double *B, int64_t ldb, double *C,
+                                                  int64_t ldc, double alpha, double beta, int tri_b,
+                                                  int64_t sA_, int64_t sB_, int64_t sC_) {
+  const int bz = blockIdx.z;
+  A += bz * sA_;
+  B += bz * sB_;
+  C += bz * sC_;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  int r0, c0, kend = K;
+  bool live = true, upper_half = false;
+  if (MODE == 0) {
+    r0 = blockIdx.x * 16;
+    c0 = wave * 32;
+    live = c0 < N;
+    if (tri_b) kend = min(K, c0 + 32);
+  } else {
+    const int nb = (M + 31) / 32, T = nb * (nb + 1) / 2;
+    const int blk = blockIdx.x * 2 + (wave >> 1);
+    int bi, bj;
+    tri_tile(min(blk, T - 1), bi, bj);
+    live = blk < T;
+    r0 = bi * 32 + (wave & 1) * 16;
+    c0 = bj * 32;
+    upper_half = bi == bj && (wave & 1) == 0;  // its columns 16..31 lie above the diagonal
+  }
+  const int li = lane & 15, kq = (lane >> 4) * 2;
+  const int ra = r0 + li, rb0 = c0 + li, rb1 = c0 + 16 + li;
+  const bool va = live && ra < M, vb0 = live && rb0 < N, vb1 = live && rb1 < N && !upper_half;
+  const double *pa = A + (int64_t)(va ? ra : 0) * lda;
+  const double *pb0 = B + (int64_t)(vb0 ? rb0 : 0) * ldb;
+  const double *pb1 = B + (int64_t)(vb1 ? rb1 : 0) * ldb;
+  const bool vec = ((lda | ldb) & 1) == 0 && ((((uintptr_t)A) | ((uintptr_t)B)) & 15) == 0;
+  auto ld2 = [&](const double *p, bool v, int k) -> double2 {
+    if (!v || k >= kend) return make_double2(0.0, 0.0);
+    if (k + 1 >= kend) return make_double2(p[k], 0.0);
+    if (vec) return *(const double2 *)(p + k);
+    return make_double2(p[k], p[k + 1]);
+  };
+  double2 a[LAT_CH], b0[LAT_CH], b1[LAT_CH];
+#pragma unroll
+  for (int t = 0; t < LAT_CH; ++t) {
+    const int k = 8 * t + kq;
+    a[t] = ld2(pa, va, k);
+    b0[t] = ld2(pb0, vb0, k);
+    b1[t] = ld2(pb1, vb1, k);
+  }
+  d4_t cpre[2];
+  if (MODE == 1 && beta != 0.0) {
+#pragma unroll
+    for (int y = 0; y < 2; ++y)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = r0 + mf_row(lane, r), col = c0 + 16 * y + li;
+        cpre[y][r] = (live && row < M && col <= row) ? C[(int64_t)row * ldc + col] : 0.0;
+      }
+  }
+  d4_t acc0 = d4_t{0.0, 0.0, 0.0, 0.0}, acc1 = acc0;
+#pragma unroll
+  for (int t = 0; t < LAT_CH; ++t) {
+    acc0 = mfma_f64(a[t].x, b0[t].x, acc0);
+    acc1 = mfma_f64(a[t].x, b1[t].x, acc1);
+    acc0 = mfma_f64(a[t].y, b0[t].y, acc0);
+    acc1 = mfma_f64(a[t].y, b1[t].y, acc1);
+  }
+  if (MODE == 0) __syncthreads();  // every wave's operand reads are done: C may alias A
+  if (!live) return;
+#pragma unroll
+  for (int y = 0; y < 2; ++y)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = r0 + mf_row(lane, r), col = c0 + 16 * y + li;
+      const double v = y ? acc1[r] : acc0[r];
+      if (MODE == 0) {
+        if (row < M && col < N) {
+          double *p = C + (int64_t)row * ldc + col;
+          *p = beta == 0.0 ? alpha * v : alpha * v + beta * *p;
+        }
+      } else if (row < M && col <= row) {
+        C[(int64_t)row * ldc + col] = beta == 0.0 ? alpha * v : alpha * v + beta * cpre[y][r];
+      }
+    }
+}
+
+hipError_t launch_gemm_lat(hipStream_t s, int mode, int M, int N, int K, const double *A,
+                           int64_t lda, const double *B, int64_t ldb, double *C, int64_t ldc,
+                           double alpha, double beta, int tri_b, int batch, int64_t sA, int64_t sB,
+                           int64_t sC) {
+  if (M <= 0 || N <= 0 || batch <= 0) return hipSuccess;
+  if (K > 8 * LAT_CH || (mode == 0 && N > 128) || (mode == 1 && N != M)) return hipErrorInvalidValue;
+  if (mode == 0) {
+    hipLaunchKernelGGL(k_gemm_lat<0>, dim3((M + 15) / 16, 1, batch), dim3(256), 0, s, M, N, K, A,
+                       lda, B, ldb, C, ldc, alpha, beta, tri_b, sA, sB, sC);
+  } else {
+    const int nb = (M + 31) / 32, T = nb * (nb + 1) / 2;
+    hipLaunchKernelGGL(k_gemm_lat<1>, dim3((T + 1) / 2, 1, batch), dim3(256), 0, s, M, N, K, A, lda,
+                       A, lda, C, ldc, alpha, beta, 0, sA, sA, sC);
+  }
+  return hipGetLastError();
+}
+
 static hipError_t launch_gemm_impl(hipStream_t s, int epi, int M, int N, int K, const double *A,
                                    int64_t lda, const double *B, int64_t ldb, double *C,
                                    int64_t ldc, double alpha, double beta, int tri_a, int lower_c,
