@@ -114,7 +114,8 @@ __global__ __launch_bounds__(64) void k_potrf_diag(int n, int k0, double *A, int
 // X_ij stored transposed in the (free) upper triangle.
 #define DB 128
 #define DP 130
-#define DIAG128_LDS (sizeof(double) * (DB * DP + NB + 2))
+// S, then 1 / L_jj for the 128 columns, then the fail flag and the sweep's flags
+#define DIAG128_LDS (sizeof(double) * (DB * DP + DB + 4))
 // LDS-only ordering.  A release fence (and __syncthreads, which carries one)
 // waits for every outstanding global store (vmcnt(0)) -- here the L blocks
 // streamed out behind the factor -- which put ~1-2 us of store latency on the
@@ -132,6 +133,146 @@ __device__ __forceinline__ double rdlane(double v, int l) {
 
 // diagnostic phase cycles of workgroup 0 (GPMPC_DIAG128_STAMPS=1 builds the <true> launch)
 __device__ unsigned long long g_d128_stamps[8];
+// sweep timeline of workgroup 0, cycles since the sweep start: per wave, the
+// start and end of its owner block; the per-wave sweep end
+__device__ unsigned long long g_sw_stamps[12];
+
+// T = L^-1 of the 32 x 32 diagonal block at (c0, c0) of S, by the calling wave: T11
+// (lanes 0-15) and T22 (lanes 16-31) by column substitution, T21 = -T22 (L21 T11) by
+// two K = 16 MFMA products; T goes to the block's lower triangle (dinv: 1 / L_jj of
+// the block).  The block's upper-right 16 x 16 is used as scratch.
+__device__ __forceinline__ void tinv32(double (*S)[DP], int c0, const double *dinv) {
+  const int lane = threadIdx.x & 63, li = lane & 15, lk = lane >> 4;
+  // T11 (lanes 0-15) and T22 (lanes 16-31): column c of the half in lane c
+  const int base = lane & 16, c = lane & 15;
+  double x[16];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    double sum = (r == c) ? 1.0 : 0.0;
+#pragma unroll
+    for (int k = 0; k < r; ++k) sum = fma(-S[c0 + base + r][c0 + base + k], x[k], sum);
+    x[r] = (r >= c) ? sum * dinv[base + r] : 0.0;
+  }
+  wave_lds_sync();
+  if (lane < NB) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r)
+      if (r >= c) S[c0 + base + r][c0 + base + c] = x[r];
+  }
+  wave_lds_sync();
+  // Y = L21 T11 -> upper-right 16 x 16 of the block (free space)
+  d4_t y = d4_t{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+  for (int kk = 0; kk < 16; kk += 4) {
+    const int m = kk + lk;
+    y = mfma_f64(S[c0 + 16 + li][c0 + m], (m >= li) ? S[c0 + m][c0 + li] : 0.0, y);
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) S[c0 + mf_row(lane, r)][c0 + 16 + li] = y[r];
+  wave_lds_sync();
+  // T21 = -T22 Y over L21
+  d4_t t21 = d4_t{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+  for (int kk = 0; kk < 16; kk += 4) {
+    const int m = kk + lk;
+    t21 = mfma_f64((m <= li) ? S[c0 + 16 + li][c0 + 16 + m] : 0.0, S[c0 + m][c0 + 16 + li],
+                   t21);
+  }
+  wave_lds_sync();
+#pragma unroll
+  for (int r = 0; r < 4; ++r) S[c0 + 16 + mf_row(lane, r)][c0 + li] = -t21[r];
+}
+
+// Linv = L^-1 of the factored 128 x 128 block in S (diagonal blocks already
+// inverted in place, tinv32) to Li, all four waves.
+__device__ __forceinline__ void inv_assemble(double (*S)[DP], double *Li, bool zero_upper) {
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int li = lane & 15, lk = lane >> 4;
+  // Linv's diagonal blocks (T_i, lower; zero above) now, its zero upper blocks
+  // on the first panel only (the scratch keeps them: later panels write the
+  // same lower part); the off-diagonal blocks go out from the registers as
+  // they are formed below
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    const int e = tid + 256 * q, blk = e >> 10, rr = (e >> 5) & 31, cc = e & 31;
+    const int i = blk * NB + rr, j = blk * NB + cc;
+    Li[i * DB + j] = (cc > rr) ? 0.0 : S[i][j];
+  }
+  if (zero_upper) {
+#pragma unroll 2
+    for (int q = 0; q < 24; ++q) {
+      // upper blocks (bi, bj), bj > bi: (0,1) (0,2) (0,3) (1,2) (1,3) (2,3)
+      const int e = tid + 256 * q, ub = e >> 10, rr = (e >> 5) & 31, cc = e & 31;
+      const int bi = ub < 3 ? 0 : ub < 5 ? 1 : 2, bj = ub < 3 ? ub + 1 : ub < 5 ? ub - 1 : 3;
+      Li[(bi * NB + rr) * DB + bj * NB + cc] = 0.0;
+    }
+  }
+  // ---- inverse, block row i = 1..3:  Y_j = sum_k L_ik X_kj -> upper block (j, i)
+  // transposed; then X_ij = -T_i Y_j in place.  Jobs: (j, 16x16 tile) pairs.
+  for (int i = 1; i < DB / NB; ++i) {
+    const int njob = 4 * i;
+    d4_t acc[3];
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      acc[q] = d4_t{0.0, 0.0, 0.0, 0.0};
+      const int jt = wave + 4 * q;
+      if (jt < njob) {
+        const int j = jt >> 2, rb = (jt >> 1 & 1) * 16, cb = (jt & 1) * 16;
+        for (int k = j; k < i; ++k) {
+#pragma unroll
+          for (int mm = 0; mm < NB; mm += 4) {
+            const int m = mm + lk, cc = cb + li;
+            const double av = S[i * NB + rb + li][k * NB + m];            // L_ik[r][m]
+            double bv;                                                      // X_kj[m][cc]
+            if (k == j) bv = (cc <= m) ? S[j * NB + m][j * NB + cc] : 0.0;  // T_j lower
+            else bv = S[j * NB + cc][k * NB + m];                           // transposed X_kj
+            acc[q] = mfma_f64(av, bv, acc[q]);
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      const int jt = wave + 4 * q;
+      if (jt < njob) {
+        const int j = jt >> 2, rb = (jt >> 1 & 1) * 16, cb = (jt & 1) * 16;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) S[j * NB + cb + li][i * NB + rb + mf_row(lane, r)] = acc[q][r];
+      }
+    }
+    lds_barrier();
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      acc[q] = d4_t{0.0, 0.0, 0.0, 0.0};
+      const int jt = wave + 4 * q;
+      if (jt < njob) {
+        const int j = jt >> 2, rb = (jt >> 1 & 1) * 16, cb = (jt & 1) * 16;
+#pragma unroll
+        for (int mm = 0; mm < NB; mm += 4) {
+          const int m = mm + lk, rr = rb + li;
+          const double av = (m <= rr) ? S[i * NB + rr][i * NB + m] : 0.0;  // T_i[rr][m]
+          const double bv = S[j * NB + cb + li][i * NB + m];                // Y_j[m][cb+li]
+          acc[q] = mfma_f64(av, bv, acc[q]);
+        }
+      }
+    }
+    lds_barrier();
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      const int jt = wave + 4 * q;
+      if (jt < njob) {
+        const int j = jt >> 2, rb = (jt >> 1 & 1) * 16, cb = (jt & 1) * 16;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = i * NB + rb + mf_row(lane, r);
+          S[j * NB + cb + li][row] = -acc[q][r];
+          Li[row * DB + j * NB + cb + li] = -acc[q][r];
+        }
+      }
+    }
+    lds_barrier();
+  }
+}
 
 // The factor + inverse of a 128 x 128 diagonal block already in LDS (S: lower
 // triangle, identity padding beyond pw, zero upper triangle; sfail = 0), for
@@ -141,7 +282,7 @@ __device__ unsigned long long g_d128_stamps[8];
 template <bool ST>
 __device__ __forceinline__ int diag128_core(double (*S)[DP], double *col, int &sfail, double *M,
                                             int64_t lda, int pw, int K0, int *infob, double *Li,
-                                            bool stamp) {
+                                            bool stamp, bool zero_upper) {
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int li = lane & 15, lk = lane >> 4;
   unsigned long long tl = 0;
@@ -235,16 +376,35 @@ __device__ __forceinline__ int diag128_core(double (*S)[DP], double *col, int &s
         asm volatile("" ::: "memory");
         const int j4 = j + 4;
         if (j4 < NB) {
-          // lower 16 x 16 tiles meeting rows/cols >= j4: (1,1) always, (1,0) and (0,0) while j4 < 16
+          // lower 16 x 16 tiles meeting rows/cols >= j4: (1,1) always, (1,0) and (0,0)
+          // while j4 < 16 (j is a compile-time constant here).  The tiles' operands
+          // are the panel columns' two 16-row halves; all reads first, the MFMAs
+          // back to back, then the read-modify-writes: one LDS round trip per stage
+          // instead of one per tile (the columns read and written are disjoint)
+          const bool lo = j4 < 16;
+          const double v16 = S[c0 + 16 + li][c0 + j + lk];
+          const double v0 = lo ? S[c0 + li][c0 + j + lk] : 0.0;
+          const double a16 = (16 + li >= j4) ? v16 : 0.0, a0 = (li >= j4) ? v0 : 0.0;
+          const d4_t z4 = d4_t{0.0, 0.0, 0.0, 0.0};
+          const d4_t t11 = mfma_f64(a16, a16, z4);
+          const d4_t t10 = lo ? mfma_f64(a16, a0, z4) : z4;
+          const d4_t t00 = lo ? mfma_f64(a0, a0, z4) : z4;
+          double o11[4], o10[4], o00[4];
 #pragma unroll
-          for (int t = 0; t < 3; ++t) {
-            const int rb = (t == 2) ? 0 : 16, cb = (t == 0) ? 16 : 0;
-            if (t > 0 && j4 >= 16) continue;
-            const double av = (rb + li >= j4) ? S[c0 + rb + li][c0 + j + lk] : 0.0;
-            const double bv = (cb + li >= j4) ? S[c0 + cb + li][c0 + j + lk] : 0.0;
-            const d4_t acc = mfma_f64(av, bv, d4_t{0.0, 0.0, 0.0, 0.0});
+          for (int r = 0; r < 4; ++r) {
+            o11[r] = S[c0 + 16 + mf_row(lane, r)][c0 + 16 + li];
+            if (lo) {
+              o10[r] = S[c0 + 16 + mf_row(lane, r)][c0 + li];
+              o00[r] = S[c0 + mf_row(lane, r)][c0 + li];
+            }
+          }
 #pragma unroll
-            for (int r = 0; r < 4; ++r) S[c0 + rb + mf_row(lane, r)][c0 + cb + li] -= acc[r];
+          for (int r = 0; r < 4; ++r) {
+            S[c0 + 16 + mf_row(lane, r)][c0 + 16 + li] = o11[r] - t11[r];
+            if (lo) {
+              S[c0 + 16 + mf_row(lane, r)][c0 + li] = o10[r] - t10[r];
+              S[c0 + mf_row(lane, r)][c0 + li] = o00[r] - t00[r];
+            }
           }
           asm volatile("" ::: "memory");
         }
@@ -256,44 +416,7 @@ __device__ __forceinline__ int diag128_core(double (*S)[DP], double *col, int &s
           sfail = 1;
         }
       } else {
-        // T11 (lanes 0-15) and T22 (lanes 16-31): column c of the half in lane c
-        const int base = lane & 16, c = lane & 15;
-        double x[16];
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          double sum = (r == c) ? 1.0 : 0.0;
-#pragma unroll
-          for (int k = 0; k < r; ++k) sum = fma(-S[c0 + base + r][c0 + base + k], x[k], sum);
-          x[r] = (r >= c) ? sum * dinv[base + r] : 0.0;
-        }
-        wave_lds_sync();
-        if (lv) {
-#pragma unroll
-          for (int r = 0; r < 16; ++r)
-            if (r >= c) S[c0 + base + r][c0 + base + c] = x[r];
-        }
-        wave_lds_sync();
-        // Y = L21 T11 -> upper-right 16 x 16 of the block (free space)
-        d4_t y = d4_t{0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-        for (int kk = 0; kk < 16; kk += 4) {
-          const int m = kk + lk;
-          y = mfma_f64(S[c0 + 16 + li][c0 + m], (m >= li) ? S[c0 + m][c0 + li] : 0.0, y);
-        }
-#pragma unroll
-        for (int r = 0; r < 4; ++r) S[c0 + mf_row(lane, r)][c0 + 16 + li] = y[r];
-        wave_lds_sync();
-        // T21 = -T22 Y over L21
-        d4_t t21 = d4_t{0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-        for (int kk = 0; kk < 16; kk += 4) {
-          const int m = kk + lk;
-          t21 = mfma_f64((m <= li) ? S[c0 + 16 + li][c0 + 16 + m] : 0.0, S[c0 + m][c0 + 16 + li],
-                         t21);
-        }
-        wave_lds_sync();
-#pragma unroll
-        for (int r = 0; r < 4; ++r) S[c0 + 16 + mf_row(lane, r)][c0 + li] = -t21[r];
+        tinv32(S, c0, dinv);
       }
     }
     lds_barrier();
@@ -342,93 +465,278 @@ __device__ __forceinline__ int diag128_core(double (*S)[DP], double *col, int &s
   }
   mark(4);
   if (pw < DB || !Li) return 0;  // the last panel has no rows below: no inverse needed
-  // Linv's diagonal blocks (T_i, lower; zero above) and zero upper blocks now;
-  // the off-diagonal blocks go out from the registers as they are formed below
-#pragma unroll 4
-  for (int e = tid; e < DB * DB; e += 256) {
-    const int i = e >> 7, j = e & 127;
-    if ((j >> 5) >= (i >> 5)) Li[e] = (j > i) ? 0.0 : S[i][j];
-  }
-  // ---- inverse, block row i = 1..3:  Y_j = sum_k L_ik X_kj -> upper block (j, i)
-  // transposed; then X_ij = -T_i Y_j in place.  Jobs: (j, 16x16 tile) pairs.
-  for (int i = 1; i < DB / NB; ++i) {
-    const int njob = 4 * i;
-    d4_t acc[3];
-#pragma unroll
-    for (int q = 0; q < 3; ++q) {
-      acc[q] = d4_t{0.0, 0.0, 0.0, 0.0};
-      const int jt = wave + 4 * q;
-      if (jt < njob) {
-        const int j = jt >> 2, rb = (jt >> 1 & 1) * 16, cb = (jt & 1) * 16;
-        for (int k = j; k < i; ++k) {
-#pragma unroll
-          for (int mm = 0; mm < NB; mm += 4) {
-            const int m = mm + lk, cc = cb + li;
-            const double av = S[i * NB + rb + li][k * NB + m];            // L_ik[r][m]
-            double bv;                                                      // X_kj[m][cc]
-            if (k == j) bv = (cc <= m) ? S[j * NB + m][j * NB + cc] : 0.0;  // T_j lower
-            else bv = S[j * NB + cc][k * NB + m];                           // transposed X_kj
-            acc[q] = mfma_f64(av, bv, acc[q]);
-          }
-        }
-      }
-    }
-#pragma unroll
-    for (int q = 0; q < 3; ++q) {
-      const int jt = wave + 4 * q;
-      if (jt < njob) {
-        const int j = jt >> 2, rb = (jt >> 1 & 1) * 16, cb = (jt & 1) * 16;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) S[j * NB + cb + li][i * NB + rb + mf_row(lane, r)] = acc[q][r];
-      }
-    }
-    lds_barrier();
-#pragma unroll
-    for (int q = 0; q < 3; ++q) {
-      acc[q] = d4_t{0.0, 0.0, 0.0, 0.0};
-      const int jt = wave + 4 * q;
-      if (jt < njob) {
-        const int j = jt >> 2, rb = (jt >> 1 & 1) * 16, cb = (jt & 1) * 16;
-#pragma unroll
-        for (int mm = 0; mm < NB; mm += 4) {
-          const int m = mm + lk, rr = rb + li;
-          const double av = (m <= rr) ? S[i * NB + rr][i * NB + m] : 0.0;  // T_i[rr][m]
-          const double bv = S[j * NB + cb + li][i * NB + m];                // Y_j[m][cb+li]
-          acc[q] = mfma_f64(av, bv, acc[q]);
-        }
-      }
-    }
-    lds_barrier();
-#pragma unroll
-    for (int q = 0; q < 3; ++q) {
-      const int jt = wave + 4 * q;
-      if (jt < njob) {
-        const int j = jt >> 2, rb = (jt >> 1 & 1) * 16, cb = (jt & 1) * 16;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int row = i * NB + rb + mf_row(lane, r);
-          S[j * NB + cb + li][row] = -acc[q][r];
-          Li[row * DB + j * NB + cb + li] = -acc[q][r];
-        }
-      }
-    }
-    lds_barrier();
-  }
+  inv_assemble(S, Li, zero_upper);
   mark(5);
   mark(6);
   return 0;
 }
 
+
+// The same factor + inverse as a column sweep with the rows owned by the waves
+// (wave w: rows 32w..32w+31 of the block, one per lane) -- no per-block inverse
+// or panel GEMM on the serial path.  For 32-column block jb, wave jb (the owner)
+// factors its diagonal block in 4-column steps as diag128_core's wave 0 does and
+// publishes each step (LDS flag); every wave below it (followers) applies the
+// step to its own rows -- the 4 x 4 triangular solve with the owner's pivots,
+// then its rows x the block's remaining columns by K = 4 MFMAs -- one step
+// behind.  At the end of the block each follower publishes its panel rows and
+// updates its rows x the column blocks jb+1..w by K = 32 MFMAs (the other waves'
+// panel rows behind their flags).  The owner never waits, and the next owner
+// (wave jb+1) only needs its own rows.  Flags only rise, and a failed pivot
+// raises them all (SW_BIG), so no wave waits forever.  Afterwards each wave
+// inverts its own diagonal block (tinv32) and inv_assemble forms Linv.
+#define SW_BIG (1 << 20)
+template <bool ST>
+__device__ __forceinline__ int diag128_sweep(double (*S)[DP], double *dinv, int &sfail, int *fl,
+                                             double *M, int64_t lda, int pw, int K0, int *infob,
+                                             double *Li, bool stamp, bool zero_upper) {
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int li = lane & 15, lk = lane >> 4;
+  unsigned long long tl = 0;
+  auto mark = [&](int k) {
+    if (ST && stamp && threadIdx.x == 0) {
+      const unsigned long long t = __builtin_amdgcn_s_memtime();
+      if (k >= 0) atomicAdd(&g_d128_stamps[k], t - tl);
+      tl = t;
+    }
+  };
+  volatile int *vfl = fl;
+  volatile int *vfail = &sfail;
+  if (tid < 5) vfl[tid] = 0;
+  lds_barrier();
+  mark(-1);
+  const unsigned long long tsw = ST ? __builtin_amdgcn_s_memtime() : 0;
+  auto swmark = [&](int k) {
+    if (ST && stamp && lane == 0) atomicAdd(&g_sw_stamps[k], __builtin_amdgcn_s_memtime() - tsw);
+  };
+  // bounded: a wait that never ends (a broken invariant) fails the matrix with
+  // info = -1 instead of hanging the device
+  auto wait_ge = [&](int i, int v) {
+    for (int spin = 0; vfl[i] < v; ++spin) {
+      if (spin > (1 << 22)) {
+        if (lane == 0) {
+          *infob = -1;
+          *vfail = 1;
+        }
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+    asm volatile("" ::: "memory");
+  };
+  // LDS operations of one wave execute in order: the data written before a flag
+  // is in place when another wave sees the flag
+  auto publish = [&](int i, int v) {
+    asm volatile("" ::: "memory");
+    if (lane == 0) vfl[i] = v;
+  };
+  const int nblk = (pw + NB - 1) / NB;
+  const bool lv = lane < NB;
+  const int w0 = wave * NB;
+  const int r = w0 + (lane & 31);  // this lane's row of the block
+  const d4_t z4 = d4_t{0.0, 0.0, 0.0, 0.0};
+  bool out = wave >= nblk;
+  for (int jb = 0; jb <= wave && !out; ++jb) {
+    const int cb0 = jb * NB;
+    if (wave == jb) {
+      // ---- owner
+      swmark(wave);
+      int fail = 0;
+#pragma unroll
+      for (int j = 0; j < NB; j += 4) {
+        double p[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) p[q] = (lv && lane >= j) ? S[r][cb0 + j + q] : 0.0;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const double piv = rdlane(p[q], j + q);
+          if (fail == 0 && !(piv > 0.0)) fail = j + q + 1;
+          if (fail) continue;
+          double id = __builtin_amdgcn_rsq(piv);
+          id = id * fma(-0.5 * piv * id, id, 1.5);
+          id = id * fma(-0.5 * piv * id, id, 1.5);
+          const double d = piv * id;
+          if (lane == j + q) dinv[cb0 + j + q] = id;
+          p[q] = (lane < j + q) ? 0.0 : (lane == j + q ? d : p[q] * id);
+#pragma unroll
+          for (int q2 = q + 1; q2 < 4; ++q2) p[q2] = fma(-p[q], rdlane(p[q], j + q2), p[q2]);
+        }
+        if (fail) break;
+        if (lv && lane >= j) {
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+            if (lane >= j + q) {
+              S[r][cb0 + j + q] = p[q];
+              if (r < pw) M[(int64_t)r * lda + cb0 + j + q] = p[q];
+            }
+        }
+        publish(0, jb * 8 + j / 4 + 1);
+        const int j4 = j + 4;
+        if (j4 < NB) {
+          const bool lo = j4 < 16;
+          const double v16 = S[cb0 + 16 + li][cb0 + j + lk];
+          const double v0 = lo ? S[cb0 + li][cb0 + j + lk] : 0.0;
+          const double a16 = (16 + li >= j4) ? v16 : 0.0, a0 = (li >= j4) ? v0 : 0.0;
+          const d4_t t11 = mfma_f64(a16, a16, z4);
+          const d4_t t10 = lo ? mfma_f64(a16, a0, z4) : z4;
+          const d4_t t00 = lo ? mfma_f64(a0, a0, z4) : z4;
+          double o11[4], o10[4], o00[4];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            o11[q] = S[cb0 + 16 + mf_row(lane, q)][cb0 + 16 + li];
+            if (lo) {
+              o10[q] = S[cb0 + 16 + mf_row(lane, q)][cb0 + li];
+              o00[q] = S[cb0 + mf_row(lane, q)][cb0 + li];
+            }
+          }
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            S[cb0 + 16 + mf_row(lane, q)][cb0 + 16 + li] = o11[q] - t11[q];
+            if (lo) {
+              S[cb0 + 16 + mf_row(lane, q)][cb0 + li] = o10[q] - t10[q];
+              S[cb0 + mf_row(lane, q)][cb0 + li] = o00[q] - t00[q];
+            }
+          }
+          asm volatile("" ::: "memory");
+        }
+      }
+      swmark(4 + wave);
+      if (fail) {
+        if (lane == 0) {
+          *infob = K0 + cb0 + fail;
+          *vfail = 1;
+        }
+        publish(0, SW_BIG);
+        out = true;
+      }
+    } else {
+      // ---- follower: the owner's step on this wave's rows
+#pragma unroll
+      for (int j = 0; j < NB; j += 4) {
+        wait_ge(0, jb * 8 + j / 4 + 1);
+        if (*vfail) {
+          out = true;
+          break;
+        }
+        const int c = cb0 + j;
+        double p[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) p[q] = lv ? S[r][c + q] : 0.0;
+        const double l10 = S[c + 1][c], l20 = S[c + 2][c], l30 = S[c + 3][c];
+        const double l21 = S[c + 2][c + 1], l31 = S[c + 3][c + 1], l32 = S[c + 3][c + 2];
+        p[0] *= dinv[c];
+        p[1] = fma(-p[0], l10, p[1]);
+        p[2] = fma(-p[0], l20, p[2]);
+        p[3] = fma(-p[0], l30, p[3]);
+        p[1] *= dinv[c + 1];
+        p[2] = fma(-p[1], l21, p[2]);
+        p[3] = fma(-p[1], l31, p[3]);
+        p[2] *= dinv[c + 2];
+        p[3] = fma(-p[2], l32, p[3]);
+        p[3] *= dinv[c + 3];
+        if (lv) {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            S[r][c + q] = p[q];
+            if (r < pw) M[(int64_t)r * lda + c + q] = p[q];
+          }
+        }
+        asm volatile("" ::: "memory");
+        const int j4 = j + 4;
+        if (j4 < NB) {
+          // own rows (two 16-row tiles) x the block's columns >= j4
+          const bool lo = j4 < 16;
+          const double a0 = S[w0 + li][c + lk], a1 = S[w0 + 16 + li][c + lk];
+          const double b1 = (16 + li >= j4) ? S[cb0 + 16 + li][c + lk] : 0.0;
+          const double b0 = (lo && li >= j4) ? S[cb0 + li][c + lk] : 0.0;
+          const d4_t t01 = mfma_f64(a0, b1, z4), t11 = mfma_f64(a1, b1, z4);
+          const d4_t t00 = lo ? mfma_f64(a0, b0, z4) : z4;
+          const d4_t t10 = lo ? mfma_f64(a1, b0, z4) : z4;
+          double o01[4], o11[4], o00[4], o10[4];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            o01[q] = S[w0 + mf_row(lane, q)][cb0 + 16 + li];
+            o11[q] = S[w0 + 16 + mf_row(lane, q)][cb0 + 16 + li];
+            if (lo) {
+              o00[q] = S[w0 + mf_row(lane, q)][cb0 + li];
+              o10[q] = S[w0 + 16 + mf_row(lane, q)][cb0 + li];
+            }
+          }
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            S[w0 + mf_row(lane, q)][cb0 + 16 + li] = o01[q] - t01[q];
+            S[w0 + 16 + mf_row(lane, q)][cb0 + 16 + li] = o11[q] - t11[q];
+            if (lo) {
+              S[w0 + mf_row(lane, q)][cb0 + li] = o00[q] - t00[q];
+              S[w0 + 16 + mf_row(lane, q)][cb0 + li] = o10[q] - t10[q];
+            }
+          }
+          asm volatile("" ::: "memory");
+        }
+      }
+      if (out) break;
+      publish(1 + wave, jb + 1);
+      // block end: own rows x column blocks v = jb+1..wave, K = 32 over block jb's
+      // columns (block v's rows are wave v's: behind its flag)
+      for (int v = jb + 1; v <= wave; ++v) {
+        if (v < wave) {
+          wait_ge(1 + v, jb + 1);
+          if (*vfail) {
+            out = true;
+            break;
+          }
+        }
+        const int v0 = v * NB;
+        const bool own = v == wave;  // lower half only: no (rows 0-15) x (cols 16-31) tile
+        d4_t t00 = z4, t01 = z4, t10 = z4, t11 = z4;
+#pragma unroll
+        for (int kk = 0; kk < NB; kk += 4) {
+          const int k = cb0 + kk + lk;
+          const double a0 = S[w0 + li][k], a1 = S[w0 + 16 + li][k];
+          const double b0 = S[v0 + li][k], b1 = S[v0 + 16 + li][k];
+          t00 = mfma_f64(a0, b0, t00);
+          t10 = mfma_f64(a1, b0, t10);
+          t11 = mfma_f64(a1, b1, t11);
+          t01 = mfma_f64(a0, own ? 0.0 : b1, t01);
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          S[w0 + mf_row(lane, q)][v0 + li] -= t00[q];
+          S[w0 + 16 + mf_row(lane, q)][v0 + li] -= t10[q];
+          S[w0 + 16 + mf_row(lane, q)][v0 + 16 + li] -= t11[q];
+          if (!own) S[w0 + mf_row(lane, q)][v0 + 16 + li] -= t01[q];
+        }
+        asm volatile("" ::: "memory");
+      }
+    }
+  }
+  if (out && wave < nblk) publish(1 + wave, SW_BIG);
+  swmark(8 + wave);
+  lds_barrier();
+  mark(7);
+  if (sfail) return 1;
+  if (pw < DB || !Li) return 0;  // the last panel has no rows below: no inverse needed
+  tinv32(S, w0, dinv + w0);
+  lds_barrier();
+  mark(1);
+  inv_assemble(S, Li, zero_upper);
+  mark(5);
+  return 0;
+}
+
 template <bool ST>
 __global__ __launch_bounds__(256) void k_potrf_diag128(int n, int K0, double *A, int64_t lda,
-                                                       int64_t stride, int *info, double *Linv) {
+                                                       int64_t stride, int *info, double *Linv,
+                                                       int sweep) {
   const int b = blockIdx.x;
   if (info[b]) return;
   // one dynamic region (no static LDS in front of it): S, then col, then the fail flag
   extern __shared__ double S_[];
   double(*S)[DP] = reinterpret_cast<double(*)[DP]>(S_);
   double *col = S_ + DB * DP;
-  int &sfail = *reinterpret_cast<int *>(S_ + DB * DP + NB);
+  int &sfail = *reinterpret_cast<int *>(S_ + DB * DP + DB);
+  int *sflags = reinterpret_cast<int *>(S_ + DB * DP + DB) + 1;
   double *M = A + (int64_t)b * stride + (int64_t)K0 * lda + K0;
   const int pw = min(DB, n - K0);
   const int tid = threadIdx.x;
@@ -451,8 +759,11 @@ __global__ __launch_bounds__(256) void k_potrf_diag128(int n, int K0, double *A,
   }
   if (tid == 0) sfail = 0;
   lds_barrier();
-  diag128_core<ST>(S, col, sfail, M, lda, pw, K0, info + b, Linv ? Linv + (int64_t)b * DB * DB : nullptr,
-                   b == 0);
+  double *Li = Linv ? Linv + (int64_t)b * DB * DB : nullptr;
+  if (sweep)
+    diag128_sweep<ST>(S, col, sfail, sflags, M, lda, pw, K0, info + b, Li, b == 0, K0 == 0);
+  else
+    diag128_core<ST>(S, col, sfail, M, lda, pw, K0, info + b, Li, b == 0, K0 == 0);
 }
 
 // ---------------------------------------------------------------------------
@@ -480,7 +791,8 @@ __global__ __launch_bounds__(256) void k_potrf_persist(int n, double *A, int64_t
   extern __shared__ double S_[];
   double(*S)[DP] = reinterpret_cast<double(*)[DP]>(S_);
   double *col = S_ + DB * DP;
-  int &sfail = *reinterpret_cast<int *>(S_ + DB * DP + NB);
+  int &sfail = *reinterpret_cast<int *>(S_ + DB * DP + DB);
+  int *sflags = reinterpret_cast<int *>(S_ + DB * DP + DB) + 1;
   double(*sA)[BT][GP] = reinterpret_cast<double(*)[BT][GP]>(S_);
   double(*sB)[BT][GP] = reinterpret_cast<double(*)[BT][GP]>(S_ + 2 * BT * GP);
   double *Mb = A + (int64_t)b * stride;
@@ -535,7 +847,7 @@ __global__ __launch_bounds__(256) void k_potrf_persist(int n, double *A, int64_t
     lds_barrier();
     // 2. diagonal block: L_JJ to the matrix, Linv to the workspace
     if (diag128_core<false>(S, col, sfail, Mb + (int64_t)J * lda + J, lda, pw, J, info + b,
-                            J + DB < n ? Li : nullptr, false))
+                            J + DB < n ? Li : nullptr, false, J == 0))
       return;
     if (J + DB >= n) break;
     wg_global_sync();
@@ -631,6 +943,11 @@ static hipError_t launch_potrf_batched128(hipStream_t s, int n, int batch, doubl
     return v ? atoi(v) : -1;
   }();
   const bool lat = lat_env >= 0 ? lat_env > 0 : batch <= 16;
+  // diagonal kernel: the column sweep (default) or the per-block inverse form
+  static const int sweep = [] {
+    const char *v = getenv("GPMPC_DIAG_SWEEP");
+    return v ? atoi(v) : 1;
+  }();
   // panel solve A[c+128:n, c:c+128] <- A[c+128:n, c:c+128] Linv^T (in place)
   auto psolve = [&](int c) {
     const int r = c + DB;
@@ -661,10 +978,10 @@ static hipError_t launch_potrf_batched128(hipStream_t s, int n, int batch, doubl
       }
       if (st)
         hipLaunchKernelGGL(k_potrf_diag128<true>, dim3(batch), dim3(256), DIAG128_LDS, s, n, c, A,
-                           lda, stride, info, c + DB < n ? Linv : nullptr);
+                           lda, stride, info, c + DB < n ? Linv : nullptr, sweep);
       else
         hipLaunchKernelGGL(k_potrf_diag128<false>, dim3(batch), dim3(256), DIAG128_LDS, s, n, c,
-                           A, lda, stride, info, c + DB < n ? Linv : nullptr);
+                           A, lda, stride, info, c + DB < n ? Linv : nullptr, sweep);
       if (c + DB < n && (e = psolve(c)) != hipSuccess) return e;
     }
     const int t0 = K0 + pw;
@@ -684,8 +1001,14 @@ static hipError_t launch_potrf_batched128(hipStream_t s, int n, int batch, doubl
     (void)hipMemcpyFromSymbol(h, HIP_SYMBOL(g_d128_stamps), sizeof(h));
     fprintf(stderr, "diag128 cycles: load %llu diag %llu panel %llu trail0 %llu lout %llu inv %llu "
                     "linvout %llu fac4 %llu\n", h[0], h[1], h[2], h[3], h[4], h[5], h[6], h[7]);
-    const unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    (void)hipMemcpyToSymbol(HIP_SYMBOL(g_d128_stamps), z, sizeof(z));
+    const unsigned long long z[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(g_d128_stamps), z, sizeof(h));
+    unsigned long long w[12];
+    (void)hipMemcpyFromSymbol(w, HIP_SYMBOL(g_sw_stamps), sizeof(w));
+    fprintf(stderr, "sweep (sum over panels) own start %llu %llu %llu %llu  own end %llu %llu %llu %llu  "
+                    "wave end %llu %llu %llu %llu\n", w[0], w[1], w[2], w[3], w[4], w[5], w[6], w[7],
+            w[8], w[9], w[10], w[11]);
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(g_sw_stamps), z, sizeof(z));
   }
   return hipGetLastError();
 }
