@@ -136,6 +136,8 @@ __device__ unsigned long long g_d128_stamps[8];
 // sweep timeline of workgroup 0, cycles since the sweep start: per wave, the
 // start and end of its owner block; the per-wave sweep end
 __device__ unsigned long long g_sw_stamps[12];
+// owner-step phases of wave 0 (block 0), workgroup 0: pivots, stores, tiles
+__device__ unsigned long long g_sw_step[3];
 
 // T = L^-1 of the 32 x 32 diagonal block at (c0, c0) of S, by the calling wave: T11
 // (lanes 0-15) and T22 (lanes 16-31) by column substitution, T21 = -T22 (L21 T11) by
@@ -501,9 +503,12 @@ __device__ __forceinline__ int diag128_sweep(double (*S)[DP], double *dinv, int 
       tl = t;
     }
   };
-  volatile int *vfl = fl;
-  volatile int *vfail = &sfail;
-  if (tid < 5) vfl[tid] = 0;
+  // flags by relaxed workgroup-scope atomics: unlike volatile accesses they stay
+  // LDS operations (a volatile access goes through a flat address and waits for
+  // every outstanding global store)
+  auto ld_flag = [](int *f) { return __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); };
+  auto st_flag = [](int *f, int v) { __hip_atomic_store(f, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); };
+  if (tid < 5) st_flag(fl + tid, 0);
   lds_barrier();
   mark(-1);
   const unsigned long long tsw = ST ? __builtin_amdgcn_s_memtime() : 0;
@@ -513,11 +518,11 @@ __device__ __forceinline__ int diag128_sweep(double (*S)[DP], double *dinv, int 
   // bounded: a wait that never ends (a broken invariant) fails the matrix with
   // info = -1 instead of hanging the device
   auto wait_ge = [&](int i, int v) {
-    for (int spin = 0; vfl[i] < v; ++spin) {
+    for (int spin = 0; ld_flag(fl + i) < v; ++spin) {
       if (spin > (1 << 22)) {
         if (lane == 0) {
           *infob = -1;
-          *vfail = 1;
+          st_flag(&sfail, 1);
         }
         break;
       }
@@ -529,7 +534,7 @@ __device__ __forceinline__ int diag128_sweep(double (*S)[DP], double *dinv, int 
   // is in place when another wave sees the flag
   auto publish = [&](int i, int v) {
     asm volatile("" ::: "memory");
-    if (lane == 0) vfl[i] = v;
+    if (lane == 0) st_flag(fl + i, v);
   };
   const int nblk = (pw + NB - 1) / NB;
   const bool lv = lane < NB;
@@ -546,32 +551,87 @@ __device__ __forceinline__ int diag128_sweep(double (*S)[DP], double *dinv, int 
 #pragma unroll
       for (int j = 0; j < NB; j += 4) {
         double p[4];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) p[q] = (lv && lane >= j) ? S[r][cb0 + j + q] : 0.0;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const double piv = rdlane(p[q], j + q);
-          if (fail == 0 && !(piv > 0.0)) fail = j + q + 1;
-          if (fail) continue;
+        unsigned long long ts0 = 0;
+        if (ST && stamp && wave == 0 && lane == 0) ts0 = __builtin_amdgcn_s_memtime();
+        // the step's four columns of this lane's row (two 16-byte reads; rows above
+        // the step read as zero)
+        {
+          const double2 *rp = reinterpret_cast<const double2 *>(&S[r][cb0 + j]);
+          const double2 x01 = rp[0], x23 = rp[1];
+          const bool on = lv && lane >= j;
+          p[0] = on ? x01.x : 0.0;
+          p[1] = on ? x01.y : 0.0;
+          p[2] = on ? x23.x : 0.0;
+          p[3] = on ? x23.y : 0.0;
+        }
+        // the 4 x 4 diagonal block by readlane, factored as uniform values: the
+        // pivot chain is rsq + Newton + two ops per column, with the row updates
+        // off it (the same operations, in the same order, as the per-lane form)
+        const double a00 = rdlane(p[0], j), a10 = rdlane(p[0], j + 1), a11 = rdlane(p[1], j + 1);
+        const double a20 = rdlane(p[0], j + 2), a21 = rdlane(p[1], j + 2), a22 = rdlane(p[2], j + 2);
+        const double a30 = rdlane(p[0], j + 3), a31 = rdlane(p[1], j + 3), a32 = rdlane(p[2], j + 3);
+        const double a33 = rdlane(p[3], j + 3);
+        auto rsqn = [](double piv) {
           double id = __builtin_amdgcn_rsq(piv);
           id = id * fma(-0.5 * piv * id, id, 1.5);
-          id = id * fma(-0.5 * piv * id, id, 1.5);
-          const double d = piv * id;
-          if (lane == j + q) dinv[cb0 + j + q] = id;
-          p[q] = (lane < j + q) ? 0.0 : (lane == j + q ? d : p[q] * id);
-#pragma unroll
-          for (int q2 = q + 1; q2 < 4; ++q2) p[q2] = fma(-p[q], rdlane(p[q], j + q2), p[q2]);
+          return id * fma(-0.5 * piv * id, id, 1.5);
+        };
+        int f = !(a00 > 0.0) ? 1 : 0;
+        const double id0 = rsqn(a00);
+        const double l10 = a10 * id0, l20 = a20 * id0, l30 = a30 * id0;
+        const double piv1 = fma(-l10, l10, a11);
+        if (!f && !(piv1 > 0.0)) f = 2;
+        const double b21 = fma(-l20, l10, a21), b31 = fma(-l30, l10, a31);
+        const double b22 = fma(-l20, l20, a22), b32 = fma(-l30, l20, a32), b33 = fma(-l30, l30, a33);
+        const double id1 = rsqn(piv1);
+        const double l21 = b21 * id1, l31 = b31 * id1;
+        const double piv2 = fma(-l21, l21, b22);
+        if (!f && !(piv2 > 0.0)) f = 3;
+        const double c32 = fma(-l31, l21, b32), c33 = fma(-l31, l31, b33);
+        const double id2 = rsqn(piv2);
+        const double l32 = c32 * id2;
+        const double piv3 = fma(-l32, l32, c33);
+        if (!f && !(piv3 > 0.0)) f = 4;
+        const double id3 = rsqn(piv3);
+        if (f) {
+          fail = j + f;
+          break;
         }
-        if (fail) break;
-        if (lv && lane >= j) {
-#pragma unroll
-          for (int q = 0; q < 4; ++q)
-            if (lane >= j + q) {
-              S[r][cb0 + j + q] = p[q];
-              if (r < pw) M[(int64_t)r * lda + cb0 + j + q] = p[q];
-            }
+        // rows: the per-lane form; the pivot rows take sqrt(piv) on the diagonal
+        // and zero above it
+        {
+          const double v0 = p[0] * id0;
+          double q1 = fma(-v0, l10, p[1]);
+          const double v1 = q1 * id1;
+          double q2 = fma(-v0, l20, p[2]);
+          q2 = fma(-v1, l21, q2);
+          const double v2 = q2 * id2;
+          double q3 = fma(-v0, l30, p[3]);
+          q3 = fma(-v1, l31, q3);
+          q3 = fma(-v2, l32, q3);
+          const double v3 = q3 * id3;
+          const int d = lane - j;
+          p[0] = d == 0 ? a00 * id0 : v0;
+          p[1] = d < 1 ? 0.0 : d == 1 ? piv1 * id1 : v1;
+          p[2] = d < 2 ? 0.0 : d == 2 ? piv2 * id2 : v2;
+          p[3] = d < 3 ? 0.0 : d == 3 ? piv3 * id3 : v3;
+        }
+        unsigned long long ts1 = 0;
+        if (ST && stamp && wave == 0 && lane == 0) ts1 = __builtin_amdgcn_s_memtime();
+        // LDS only: the diagonal block goes to global memory at the end of the sweep
+        if (lane == 0) {
+          double2 *dp = reinterpret_cast<double2 *>(&dinv[cb0 + j]);
+          dp[0] = make_double2(id0, id1);
+          dp[1] = make_double2(id2, id3);
+        }
+        if (lv) {
+          double2 *rp = reinterpret_cast<double2 *>(&S[r][cb0 + j]);
+          rp[0] = make_double2(p[0], p[1]);
+          rp[1] = make_double2(p[2], p[3]);
         }
         publish(0, jb * 8 + j / 4 + 1);
+        unsigned long long ts2 = 0;
+        if (ST && stamp && wave == 0 && lane == 0) ts2 = __builtin_amdgcn_s_memtime();
         const int j4 = j + 4;
         if (j4 < NB) {
           const bool lo = j4 < 16;
@@ -600,22 +660,32 @@ __device__ __forceinline__ int diag128_sweep(double (*S)[DP], double *dinv, int 
           }
           asm volatile("" ::: "memory");
         }
+        if (ST && stamp && wave == 0 && lane == 0) {
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+          const unsigned long long ts3 = __builtin_amdgcn_s_memtime();
+          atomicAdd(&g_sw_step[0], ts1 - ts0);
+          atomicAdd(&g_sw_step[1], ts2 - ts1);
+          atomicAdd(&g_sw_step[2], ts3 - ts2);
+        }
       }
       swmark(4 + wave);
       if (fail) {
         if (lane == 0) {
           *infob = K0 + cb0 + fail;
-          *vfail = 1;
+          st_flag(&sfail, 1);
         }
         publish(0, SW_BIG);
         out = true;
       }
     } else {
-      // ---- follower: the owner's step on this wave's rows
+      // ---- follower: the owner's step on this wave's rows.  The panel's update of
+      // this wave's own diagonal block accumulates step by step (K = 4 each), so a
+      // wave that owns the next block starts without a K = 32 product
+      d4_t d00 = z4, d10 = z4, d11 = z4;
 #pragma unroll
       for (int j = 0; j < NB; j += 4) {
         wait_ge(0, jb * 8 + j / 4 + 1);
-        if (*vfail) {
+        if (ld_flag(&sfail)) {
           out = true;
           break;
         }
@@ -643,11 +713,14 @@ __device__ __forceinline__ int diag128_sweep(double (*S)[DP], double *dinv, int 
           }
         }
         asm volatile("" ::: "memory");
+        const double a0 = S[w0 + li][c + lk], a1 = S[w0 + 16 + li][c + lk];
+        d00 = mfma_f64(a0, a0, d00);
+        d10 = mfma_f64(a1, a0, d10);
+        d11 = mfma_f64(a1, a1, d11);
         const int j4 = j + 4;
         if (j4 < NB) {
           // own rows (two 16-row tiles) x the block's columns >= j4
           const bool lo = j4 < 16;
-          const double a0 = S[w0 + li][c + lk], a1 = S[w0 + 16 + li][c + lk];
           const double b1 = (16 + li >= j4) ? S[cb0 + 16 + li][c + lk] : 0.0;
           const double b0 = (lo && li >= j4) ? S[cb0 + li][c + lk] : 0.0;
           const d4_t t01 = mfma_f64(a0, b1, z4), t11 = mfma_f64(a1, b1, z4);
@@ -677,18 +750,23 @@ __device__ __forceinline__ int diag128_sweep(double (*S)[DP], double *dinv, int 
       }
       if (out) break;
       publish(1 + wave, jb + 1);
-      // block end: own rows x column blocks v = jb+1..wave, K = 32 over block jb's
-      // columns (block v's rows are wave v's: behind its flag)
-      for (int v = jb + 1; v <= wave; ++v) {
-        if (v < wave) {
-          wait_ge(1 + v, jb + 1);
-          if (*vfail) {
-            out = true;
-            break;
-          }
+      // block end: the accumulated own diagonal block, then own rows x column blocks
+      // v = jb+1..wave-1, K = 32 over block jb's columns (block v's rows are wave
+      // v's: behind its flag)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        S[w0 + mf_row(lane, q)][w0 + li] -= d00[q];
+        S[w0 + 16 + mf_row(lane, q)][w0 + li] -= d10[q];
+        S[w0 + 16 + mf_row(lane, q)][w0 + 16 + li] -= d11[q];
+      }
+      asm volatile("" ::: "memory");
+      for (int v = jb + 1; v < wave; ++v) {
+        wait_ge(1 + v, jb + 1);
+        if (ld_flag(&sfail)) {
+          out = true;
+          break;
         }
         const int v0 = v * NB;
-        const bool own = v == wave;  // lower half only: no (rows 0-15) x (cols 16-31) tile
         d4_t t00 = z4, t01 = z4, t10 = z4, t11 = z4;
 #pragma unroll
         for (int kk = 0; kk < NB; kk += 4) {
@@ -698,20 +776,28 @@ __device__ __forceinline__ int diag128_sweep(double (*S)[DP], double *dinv, int 
           t00 = mfma_f64(a0, b0, t00);
           t10 = mfma_f64(a1, b0, t10);
           t11 = mfma_f64(a1, b1, t11);
-          t01 = mfma_f64(a0, own ? 0.0 : b1, t01);
+          t01 = mfma_f64(a0, b1, t01);
         }
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           S[w0 + mf_row(lane, q)][v0 + li] -= t00[q];
           S[w0 + 16 + mf_row(lane, q)][v0 + li] -= t10[q];
           S[w0 + 16 + mf_row(lane, q)][v0 + 16 + li] -= t11[q];
-          if (!own) S[w0 + mf_row(lane, q)][v0 + 16 + li] -= t01[q];
+          S[w0 + mf_row(lane, q)][v0 + 16 + li] -= t01[q];
         }
         asm volatile("" ::: "memory");
       }
     }
   }
   if (out && wave < nblk) publish(1 + wave, SW_BIG);
+  // the owned diagonal block's lower triangle (kept in LDS while it was factored)
+  if (!out && wave < nblk) {
+#pragma unroll 4
+    for (int k = 0; k < NB * NB / 64; ++k) {
+      const int e = lane + 64 * k, rr = e >> 5, cc = e & 31;
+      if (cc <= rr && w0 + rr < pw) M[(int64_t)(w0 + rr) * lda + w0 + cc] = S[w0 + rr][w0 + cc];
+    }
+  }
   swmark(8 + wave);
   lds_barrier();
   mark(7);
@@ -1009,6 +1095,9 @@ static hipError_t launch_potrf_batched128(hipStream_t s, int n, int batch, doubl
                     "wave end %llu %llu %llu %llu\n", w[0], w[1], w[2], w[3], w[4], w[5], w[6], w[7],
             w[8], w[9], w[10], w[11]);
     (void)hipMemcpyToSymbol(HIP_SYMBOL(g_sw_stamps), z, sizeof(z));
+    (void)hipMemcpyFromSymbol(w, HIP_SYMBOL(g_sw_step), 3 * sizeof(w[0]));
+    fprintf(stderr, "owner steps of block 0 (sum): pivots %llu stores %llu tiles %llu\n", w[0], w[1], w[2]);
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(g_sw_step), z, 3 * sizeof(z[0]));
   }
   return hipGetLastError();
 }
