@@ -676,6 +676,31 @@ __device__ __forceinline__ int diag128_sweep(double (*S)[DP], double *dinv, int 
         }
         publish(0, SW_BIG);
         out = true;
+        break;
+      }
+      // the factored diagonal blocks go to global memory off the owners' path:
+      // block 0 by wave 0 now, block w+1 by wave w (idle once it has owned block w)
+      // column group by column group behind the owner's step flags
+      if (wave == 0) {
+#pragma unroll 4
+        for (int k = 0; k < NB * NB / 64; ++k) {
+          const int e = lane + 64 * k, rr = e >> 5, cc = e & 31;
+          if (cc <= rr && rr < pw) M[(int64_t)rr * lda + cc] = S[rr][cc];
+        }
+      }
+      if (wave + 1 < nblk) {
+        const int n0 = (wave + 1) * NB, rr = n0 + (lane & 31), ch = (lane >> 5) * 2;
+#pragma unroll 1
+        for (int j = 0; j < NB; j += 4) {
+          wait_ge(0, (wave + 1) * 8 + j / 4 + 1);
+          if (ld_flag(&sfail)) break;
+          const int cc = n0 + j + ch;
+          const double2 v = *reinterpret_cast<const double2 *>(&S[rr][cc]);
+          if (rr < pw) {
+            if (cc <= rr) M[(int64_t)rr * lda + cc] = v.x;
+            if (cc + 1 <= rr) M[(int64_t)rr * lda + cc + 1] = v.y;
+          }
+        }
       }
     } else {
       // ---- follower: the owner's step on this wave's rows.  The panel's update of
@@ -790,14 +815,6 @@ __device__ __forceinline__ int diag128_sweep(double (*S)[DP], double *dinv, int 
     }
   }
   if (out && wave < nblk) publish(1 + wave, SW_BIG);
-  // the owned diagonal block's lower triangle (kept in LDS while it was factored)
-  if (!out && wave < nblk) {
-#pragma unroll 4
-    for (int k = 0; k < NB * NB / 64; ++k) {
-      const int e = lane + 64 * k, rr = e >> 5, cc = e & 31;
-      if (cc <= rr && w0 + rr < pw) M[(int64_t)(w0 + rr) * lda + w0 + cc] = S[w0 + rr][w0 + cc];
-    }
-  }
   swmark(8 + wave);
   lds_barrier();
   mark(7);
