@@ -491,7 +491,7 @@ __device__ __forceinline__ int diag128_core(double (*S)[DP], double *col, int &s
 template <bool ST>
 __device__ __forceinline__ int diag128_sweep(double (*S)[DP], double *dinv, int &sfail, int *fl,
                                              double *M, int64_t lda, int pw, int K0, int *infob,
-                                             double *Li, bool stamp, bool zero_upper) {
+                                             double *Li, bool stamp, bool zero_upper, bool tblk) {
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int li = lane & 15, lk = lane >> 4;
@@ -821,11 +821,109 @@ __device__ __forceinline__ int diag128_sweep(double (*S)[DP], double *dinv, int 
   if (sfail) return 1;
   if (pw < DB || !Li) return 0;  // the last panel has no rows below: no inverse needed
   tinv32(S, w0, dinv + w0);
+  if (tblk) {
+    // the TRSM-form panel solve (k_potrf_psolve_lat) takes the four inverted
+    // diagonal blocks (lower part; it masks the rest) instead of the full inverse
+    wave_lds_sync();
+#pragma unroll
+    for (int q = 0; q < NB * NB / 64; ++q) {
+      const int e = lane + 64 * q;
+      Li[wave * NB * NB + e] = S[w0 + (e >> 5)][w0 + (e & 31)];
+    }
+    mark(1);
+    return 0;
+  }
   lds_barrier();
   mark(1);
   inv_assemble(S, Li, zero_upper);
   mark(5);
   return 0;
+}
+
+// Panel solve X L^T = A (in place) for few matrices, in the TRSM form: with T_w the
+// inverted 32 x 32 diagonal blocks of L (k_potrf_diag128's tblk output),
+//   X_w = (A_w - sum_{k<w} X_k L_wk^T) T_w^T,   w = 0..3 (32-column blocks).
+// A workgroup owns 16 rows; wave w owns column block w and holds A_w in its MFMA
+// accumulators from the start, with its operands of L and T_w prefetched into
+// registers (one memory round trip).  Stage s: wave s forms X_s (accumulator ->
+// LDS -> A operand, times T_s^T) and hands it to the later waves through LDS;
+// after the barrier they subtract X_s L_ws^T.  Replaces the 128 x 128 inverse
+// (its assembly was ~20% of the diagonal kernel) and the full 128 x 128 x 128
+// product with a half-triangular one.
+__global__ __launch_bounds__(256) void k_potrf_psolve_lat(int M, const double *L, int64_t lda,
+                                                          const double *Tb, double *X,
+                                                          int64_t sL, int64_t sT, int64_t sX) {
+  const int bz = blockIdx.z;
+  L += bz * sL;
+  Tb += bz * sT;
+  X += bz * sX;
+  const int lane = threadIdx.x & 63, li = lane & 15, lk = lane >> 4;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int r0 = blockIdx.x * 16, w0 = wave * NB;
+  __shared__ double sx[4][16][NB + 2];  // X_w, row-major (A-operand reads)
+  d4_t acc0, acc1;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int row = r0 + mf_row(lane, q);
+    acc0[q] = row < M ? X[(int64_t)row * lda + w0 + li] : 0.0;
+    acc1[q] = row < M ? X[(int64_t)row * lda + w0 + 16 + li] : 0.0;
+  }
+  // B operands: L_wk^T (k < w) and T_w^T (lower: kk <= c)
+  double lb[3][2][8], tb[2][8];
+#pragma unroll
+  for (int k = 0; k < 3; ++k)
+#pragma unroll
+    for (int y = 0; y < 2; ++y)
+#pragma unroll
+      for (int t = 0; t < 8; ++t)
+        lb[k][y][t] = k < wave ? L[(int64_t)(w0 + 16 * y + li) * lda + k * NB + 4 * t + lk] : 0.0;
+#pragma unroll
+  for (int y = 0; y < 2; ++y)
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+      const int c = 16 * y + li, kk = 4 * t + lk;
+      tb[y][t] = kk <= c ? Tb[wave * NB * NB + c * NB + kk] : 0.0;
+    }
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    if (wave == s) {
+      // R (accumulators) -> LDS, back as the A operand of R T_s^T
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        sx[s][mf_row(lane, q)][li] = acc0[q];
+        sx[s][mf_row(lane, q)][16 + li] = acc1[q];
+      }
+      wave_lds_sync();
+      d4_t x0 = d4_t{0.0, 0.0, 0.0, 0.0}, x1 = x0;
+#pragma unroll
+      for (int t = 0; t < 8; ++t) {
+        const double a = sx[s][li][4 * t + lk];
+        x0 = mfma_f64(a, tb[0][t], x0);
+        x1 = mfma_f64(a, tb[1][t], x1);
+      }
+      wave_lds_sync();
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int row = r0 + mf_row(lane, q);
+        sx[s][mf_row(lane, q)][li] = x0[q];
+        sx[s][mf_row(lane, q)][16 + li] = x1[q];
+        if (row < M) {
+          X[(int64_t)row * lda + w0 + li] = x0[q];
+          X[(int64_t)row * lda + w0 + 16 + li] = x1[q];
+        }
+      }
+    }
+    if (s == 3) break;
+    lds_barrier();
+    if (wave > s) {
+#pragma unroll
+      for (int t = 0; t < 8; ++t) {
+        const double a = -sx[s][li][4 * t + lk];
+        acc0 = mfma_f64(a, lb[s][0][t], acc0);
+        acc1 = mfma_f64(a, lb[s][1][t], acc1);
+      }
+    }
+  }
 }
 
 template <bool ST>
@@ -864,7 +962,8 @@ __global__ __launch_bounds__(256) void k_potrf_diag128(int n, int K0, double *A,
   lds_barrier();
   double *Li = Linv ? Linv + (int64_t)b * DB * DB : nullptr;
   if (sweep)
-    diag128_sweep<ST>(S, col, sfail, sflags, M, lda, pw, K0, info + b, Li, b == 0, K0 == 0);
+    diag128_sweep<ST>(S, col, sfail, sflags, M, lda, pw, K0, info + b, Li, b == 0, K0 == 0,
+                      (sweep & 2) != 0);
   else
     diag128_core<ST>(S, col, sfail, M, lda, pw, K0, info + b, Li, b == 0, K0 == 0);
 }
@@ -1051,9 +1150,23 @@ static hipError_t launch_potrf_batched128(hipStream_t s, int n, int batch, doubl
     const char *v = getenv("GPMPC_DIAG_SWEEP");
     return v ? atoi(v) : 1;
   }();
+  // panel solve in the TRSM form (k_potrf_psolve_lat) with the diagonal kernel's
+  // inverted 32 x 32 blocks, for the latency path (GPMPC_POTRF_TRSM=0: the full
+  // inverse and the latency GEMM)
+  static const int trsm_env = [] {
+    const char *v = getenv("GPMPC_POTRF_TRSM");
+    return v ? atoi(v) : -1;
+  }();
+  // (measured: batch 32 0.99 -> 0.86 ms, 64 1.35 -> 1.28 ms, 256 3.64 -> 3.75 ms)
+  const bool tblk = sweep && (trsm_env >= 0 ? trsm_env > 0 : batch <= 64);
   // panel solve A[c+128:n, c:c+128] <- A[c+128:n, c:c+128] Linv^T (in place)
   auto psolve = [&](int c) {
     const int r = c + DB;
+    if (tblk) {
+      hipLaunchKernelGGL(k_potrf_psolve_lat, dim3((n - r + 15) / 16, 1, batch), dim3(256), 0, s,
+                         n - r, at(c, c), lda, Linv, at(r, c), stride, (int64_t)DB * DB, stride);
+      return hipGetLastError();
+    }
     if (lat)
       return launch_gemm_lat(s, 0, n - r, DB, DB, at(r, c), lda, Linv, DB, at(r, c), lda, 1.0, 0.0,
                              1, batch, stride, (int64_t)DB * DB, stride);
@@ -1081,10 +1194,10 @@ static hipError_t launch_potrf_batched128(hipStream_t s, int n, int batch, doubl
       }
       if (st)
         hipLaunchKernelGGL(k_potrf_diag128<true>, dim3(batch), dim3(256), DIAG128_LDS, s, n, c, A,
-                           lda, stride, info, c + DB < n ? Linv : nullptr, sweep);
+                           lda, stride, info, c + DB < n ? Linv : nullptr, sweep | (tblk ? 2 : 0));
       else
         hipLaunchKernelGGL(k_potrf_diag128<false>, dim3(batch), dim3(256), DIAG128_LDS, s, n, c,
-                           A, lda, stride, info, c + DB < n ? Linv : nullptr, sweep);
+                           A, lda, stride, info, c + DB < n ? Linv : nullptr, sweep | (tblk ? 2 : 0));
       if (c + DB < n && (e = psolve(c)) != hipSuccess) return e;
     }
     const int t0 = K0 + pw;
