@@ -1177,12 +1177,18 @@ static hipError_t launch_potrf_batched128(hipStream_t s, int n, int batch, doubl
   // left-looking (a step's columns take the update of the panel's earlier
   // steps, K = c - K0); across panels, one lower SYRK with K = OB, so the
   // O(n^3) work runs as K = OB products (fewer C read-modify-writes, longer K).
+  // Default: 128 (right-looking, K = 128 SYRKs) up to batch 255, 1024 (left-looking:
+  // each 128-column block takes the update of all earlier columns, K = c, with no
+  // trailing SYRK) from batch 256 on -- measured at n = 1000: 64: 1.34 vs 1.60 ms,
+  // 256: 3.62 vs 3.58 ms, 1024: 13.6 vs 13.2 ms (the long-K updates run at 50-70% of
+  // peak, the K = 128 / 256 ones at 30-38%).  256-512: no better than either.
   static const int ob_env = [] {
     const char *v = getenv("GPMPC_POTRF_OB");
-    const int m = v ? atoi(v) / DB : 1;  // 256 / 384 / 512 measured 5-10% slower at n = 1000
+    if (!v) return 0;
+    const int m = atoi(v) / DB;
     return DB * (m < 1 ? 1 : m > 8 ? 8 : m);
   }();
-  const int OBk = ob_env;
+  const int OBk = ob_env ? ob_env : (batch >= 256 ? 8 * DB : DB);
   for (int K0 = 0; K0 < n; K0 += OBk) {
     const int pw = min(OBk, n - K0);
     for (int c = K0; c < K0 + pw; c += DB) {

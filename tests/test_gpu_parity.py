@@ -54,12 +54,16 @@ def test_blocked_trsm_paths(gpu_ctx, n, nrhs):
     np.testing.assert_allclose(L.potrs(gpu_ctx, Lr, B), np.linalg.solve(A, B), rtol=1e-9, atol=1e-11)
 
 
-@pytest.mark.parametrize("n,batch", [(100, 3), (128, 2), (129, 3), (256, 2), (300, 4), (1000, 3)])
+@pytest.mark.parametrize("n,batch", [(100, 3), (128, 2), (129, 3), (256, 2), (300, 4), (1000, 3),
+                                     (300, 20), (300, 70), (257, 260)])
 def test_potrf_batched_dev(gpu_ctx, n, batch):
-    """Batched device potrf (fused 128 x 128 diagonal factor + inverse, in-place
-    panel GEMM, lower SYRK) vs np.linalg.cholesky per matrix (exact_gp.py:164);
-    the strict upper triangle is left untouched; a matrix with a bad pivot
-    reports its 1-based column without disturbing the others."""
+    """Batched device potrf vs np.linalg.cholesky per matrix (exact_gp.py:164) over
+    the batch regimes of launch_potrf_batched128: <= 16 (column-sweep diagonal
+    kernel, TRSM-form panel solve, latency-form SYRK), 17-64 (TRSM panel solve,
+    tiled SYRK), 65-255 (assembled 128 x 128 inverse, in-place panel GEMM) and
+    >= 256 (left-looking block columns, no trailing SYRK).  The strict upper
+    triangle is left untouched; a matrix with a bad pivot reports its 1-based
+    column without disturbing the others."""
     import torch
     L = _lib()
     rs = np.random.RandomState(7 * n + batch)
