@@ -1189,13 +1189,24 @@ static hipError_t launch_potrf_batched128(hipStream_t s, int n, int batch, doubl
     return DB * (m < 1 ? 1 : m > 8 ? 8 : m);
   }();
   const int OBk = ob_env ? ob_env : (batch >= 256 ? 8 * DB : DB);
+  static const int ksplit_env = [] {
+    const char *v = getenv("GPMPC_POTRF_KSPLIT");
+    return v ? atoi(v) : 0;
+  }();
   for (int K0 = 0; K0 < n; K0 += OBk) {
     const int pw = min(OBk, n - K0);
     for (int c = K0; c < K0 + pw; c += DB) {
       const int w = min(DB, n - c);
       if (c > K0) {
-        e = launch_gemm_nt_rowblock(s, n - c, w, c - K0, at(c, K0), lda, at(c, K0), lda,
-                                    at(c, c), lda, -1.0, 1.0, batch, stride, stride, stride, 1);
+        // the block column's update by all earlier columns of the outer panel; K split
+        // (atomic partial sums) when its row tiles give fewer than ~2 workgroups per CU,
+        // >= 128 of K per split (GPMPC_POTRF_KSPLIT=1: never)
+        const int K = c - K0, tiles = (n - c + DB - 1) / DB * batch;
+        int ks = 1;
+        if (ksplit_env != 1)
+          while (ks < K / DB && tiles * ks < 512) ++ks;
+        e = launch_gemm_nt_rowblock(s, n - c, w, K, at(c, K0), lda, at(c, K0), lda, at(c, c), lda,
+                                    -1.0, 1.0, batch, stride, stride, stride, 1, ks);
         if (e != hipSuccess) return e;
       }
       if (st)

@@ -18,7 +18,7 @@ hipError_t launch_gemm_nt(hipStream_t s, int epi, int M, int N, int K, const dou
 hipError_t launch_gemm_nt_rowblock(hipStream_t s, int M, int N, int K, const double *A,
                                    int64_t lda, const double *B, int64_t ldb, double *C,
                                    int64_t ldc, double alpha, double beta, int batch, int64_t sA,
-                                   int64_t sB, int64_t sC, int lower_c = 0);
+                                   int64_t sB, int64_t sC, int lower_c = 0, int ksplit = 1);
 
 // latency form for K <= 128 (see gemm.hip): mode 0 = rows in place (N <= 128,
 // C may alias A; tri_b: B lower-triangular), mode 1 = lower C += A A^T (M == N)

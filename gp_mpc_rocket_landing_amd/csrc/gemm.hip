@@ -826,12 +826,14 @@ hipError_t launch_gemm_tn(hipStream_t s, int M, int N, int K, const double *A, i
 hipError_t launch_gemm_nt_rowblock(hipStream_t s, int M, int N, int K, const double *A,
                                    int64_t lda, const double *B, int64_t ldb, double *C,
                                    int64_t ldc, double alpha, double beta, int batch, int64_t sA,
-                                   int64_t sB, int64_t sC, int lower_c) {
+                                   int64_t sB, int64_t sC, int lower_c, int ksplit) {
   if (M <= 0 || N <= 0) return hipSuccess;
   if (N > BT) return hipErrorInvalidValue;
-  dim3 g(1, (M + BT - 1) / BT, batch);
+  // split K (partial products added atomically): only with beta = 1 and C apart from A, B
+  if (ksplit < 1 || beta != 1.0) ksplit = 1;
+  dim3 g(1, (M + BT - 1) / BT, batch * ksplit);
   hipLaunchKernelGGL(k_gemm128<EPI_STORE>, g, dim3(256), 0, s, M, N, K, A, lda, B, ldb, C, ldc,
-                     alpha, beta, 0, lower_c, sA, sB, sC, M, nullptr, (int64_t)0, 1, 0);
+                     alpha, beta, 0, lower_c, sA, sB, sC, M, nullptr, (int64_t)0, ksplit, 0);
   return hipGetLastError();
 }
 
