@@ -111,6 +111,8 @@ _sig("gpmpc_gp_append", _c, _vp, _vp, _dp, _c, _dp, _dp, _dp, _dp)
 _sig("gpmpc_gp_lml_batched", _c, _vp, _c, _dp, _c, _c, _dp, _c, _dp, _dp, _dp, _dp, _ip)
 _sig("gpmpc_fitc_fit", _c, _vp, _dp, _c, _dp, _c, _c, _dp, _c, _dp, ctypes.c_double,
      ctypes.c_double, ctypes.c_double, ctypes.POINTER(_vp), _dp, _dp, _dp, _dp)
+_sig("gpmpc_vfe_fit", _c, _vp, _dp, _c, _dp, _c, _c, _dp, _c, _dp, ctypes.c_double,
+     ctypes.c_double, ctypes.c_double, ctypes.POINTER(_vp), _dp, _dp, _dp)
 _sig("gpmpc_fitc_predict", _c, _vp, _vp, _dp, _c, _dp, _dp)
 _sig("gpmpc_fitc_destroy", _c, _vp)
 _sig("gpmpc_fitc_get_state", _c, _vp, _vp, _dp)
@@ -165,7 +167,7 @@ EXPORTED = ["gpmpc_abi_version", "gpmpc_last_error", "gpmpc_ctx_create", "gpmpc_
             "gpmpc_rollout6_get_state", "gpmpc_rollout6_destroy", "gpmpc_rollout6_create_exact",
             "gpmpc_rollout6_solve", "gpmpc_rollout6_set_state", "gpmpc_fitc_get_state",
             "gpmpc_rollout6_records_dev", "gpmpc_comm_unique_id", "gpmpc_comm_init", "gpmpc_comm_destroy",
-            "gpmpc_gather_results", "gpmpc_rollout6_step_phases"]
+            "gpmpc_gather_results", "gpmpc_rollout6_step_phases", "gpmpc_vfe_fit"]
 
 
 class HIPError(RuntimeError):
@@ -383,7 +385,10 @@ class ExactGPHandle:
 
 
 class FITCHandle:
-    def __init__(self, ctx, Z, X, Y, ls, sigma2, noise, jitter=1e-6):
+    """A fitted sparse GP on the device: FITC (gpmpc_fitc_fit) or, with
+    ``method="vfe"``, VFE (gpmpc_vfe_fit; ``lam`` is then None)."""
+
+    def __init__(self, ctx, Z, X, Y, ls, sigma2, noise, jitter=1e-6, method="fitc"):
         Z = f64(np.atleast_2d(Z)); X = f64(np.atleast_2d(X)); Y = f64(Y)
         if Y.ndim == 1:
             Y = Y[:, None]
@@ -393,11 +398,19 @@ class FITCHandle:
             ls = np.full(d, float(ls[0]))
         self.ctx = ctx; self.n_out = no; self.m = m
         self.y_mean = np.empty(no); self.y_std = np.empty(no); self.lml = np.empty(no)
-        self.lam = np.empty(n)
         h = _vp()
-        rc = _L.gpmpc_fitc_fit(ctx.h, _d(Z), m, _d(X), n, d, _d(Y), no, _d(ls), float(sigma2),
-                               float(noise), float(jitter), ctypes.byref(h), _d(self.y_mean),
-                               _d(self.y_std), _d(self.lml), _d(self.lam))
+        if method == "vfe":
+            self.lam = None
+            rc = _L.gpmpc_vfe_fit(ctx.h, _d(Z), m, _d(X), n, d, _d(Y), no, _d(ls), float(sigma2),
+                                  float(noise), float(jitter), ctypes.byref(h), _d(self.y_mean),
+                                  _d(self.y_std), _d(self.lml))
+        elif method == "fitc":
+            self.lam = np.empty(n)
+            rc = _L.gpmpc_fitc_fit(ctx.h, _d(Z), m, _d(X), n, d, _d(Y), no, _d(ls), float(sigma2),
+                                   float(noise), float(jitter), ctypes.byref(h), _d(self.y_mean),
+                                   _d(self.y_std), _d(self.lml), _d(self.lam))
+        else:
+            raise ValueError(f"method must be 'fitc' or 'vfe', got {method!r}")
         if rc > 0:
             raise np.linalg.LinAlgError(_L.gpmpc_last_error().decode())
         _chk(rc, "fitc_fit")

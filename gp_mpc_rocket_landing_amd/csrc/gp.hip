@@ -472,12 +472,153 @@ GpView fitc_view(const gpmpc_fitc *gp) {
 
 // ---------------------------------------------------------------------------
 // FITC (sparse_gp.py:150-219 fit, :255-305 predict)
-extern "C" int gpmpc_fitc_fit(gpmpc_ctx *ctx, const double *Z, int m, const double *X, int n,
-                              int d, const double *Y, int n_out, const double *ls, double sigma2,
-                              double noise, double jitter, gpmpc_fitc **out, double *y_mean,
-                              double *y_std, double *lml, double *lambda_diag) {
+// VFE per-column |A e_j|^2 (A = L_uu^-1 K_uf), the Q_ff diagonal of the trace term
+__global__ void k_colsumsq(int m, int n, const double *A, double *q) {
+  int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= n) return;
+  double s = 0.0;
+  for (int i = 0; i < m; ++i) s += A[(int64_t)i * n + j] * A[(int64_t)i * n + j];
+  q[j] = s;
+}
+
+__global__ void k_fill(int n, double v, double *x) {
+  int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j < n) x[j] = v;
+}
+
+// VFE lower bound (sparse_gp.py:232-249) and alpha^T, one workgroup per output:
+//   -y.y/(2 s2n) + c.alpha - alpha^T K_uu alpha / 2 - (n sigma2 - sum q) / (2 s2n)
+//   - sum log diag L_B + sum log diag L_uu - n/2 log s2n - n/2 log 2 pi
+// with c = K_uf y / s2n, so y^T K_fu alpha / s2n = c.alpha
+__global__ __launch_bounds__(256) void k_lml_vfe(int m, int n, int n_out, const double *LB,
+                                                 const double *Luu, const double *Kuu,
+                                                 const double *yn, const double *q,
+                                                 const double *cvec, const double *alpha,
+                                                 double sigma2, double noise, double *alphaT,
+                                                 double *lml) {
+  __shared__ double red[4];
+  const int c = blockIdx.x;
+  double ldb = 0.0, ldu = 0.0, ca = 0.0, aka = 0.0, yy = 0.0, qs = 0.0;
+  for (int i = threadIdx.x; i < m; i += 256) {
+    ldb += log(LB[(int64_t)i * m + i]);
+    ldu += log(Luu[(int64_t)i * m + i]);
+    const double a = alpha[(int64_t)i * n_out + c];
+    ca += cvec[(int64_t)i * n_out + c] * a;
+    alphaT[(int64_t)c * m + i] = a;
+    double r = 0.0;
+    for (int k = 0; k < m; ++k) r += Kuu[(int64_t)i * m + k] * alpha[(int64_t)k * n_out + c];
+    aka += a * r;
+  }
+  for (int j = threadIdx.x; j < n; j += 256) {
+    const double y = yn[(int64_t)j * n_out + c];
+    yy += y * y;
+    qs += q[j];
+  }
+  ldb = block_sum(ldb, red);
+  ldu = block_sum(ldu, red);
+  ca = block_sum(ca, red);
+  aka = block_sum(aka, red);
+  yy = block_sum(yy, red);
+  qs = block_sum(qs, red);
+  if (threadIdx.x == 0) {
+    const double data_fit = -0.5 / noise * yy + ca - 0.5 * aka;
+    const double trace_term = (n * sigma2 - qs) / noise;
+    const double complexity = -ldb + ldu - 0.5 * n * log(noise);
+    lml[c] = data_fit - 0.5 * trace_term + complexity - 0.5 * n * log(2.0 * M_PI);
+  }
+}
+
+// VFE after L_uu, K_uf and W = L_uu^-1 are formed (sparse_gp.py:221-249): B = K_uu +
+// K_uf K_fu / s2n + jitter I -> L_B, c = K_uf y / s2n, alpha = B^-1 c, the bound
+static int vfe_tail(gpmpc_ctx *ctx, gpmpc_fitc *gp, DevBuf &Luu, DevBuf &Kuf, DevBuf &B,
+                    DevBuf &dinfo, const double *Y, int n, int n_out, double sigma2, double noise,
+                    double jitter, gpmpc_fitc **out, double *y_mean, double *y_std, double *lml) {
+  hipStream_t s = ctx->stream;
+  GpCore &g = gp->core;
+  const int m = gp->m;
+  auto fail = [&](int code) { delete gp; return code; };
+  DevBuf Kuu, q, dYraw, dyn, yl, sig, cvec, alpha, dlml;
+  if (Kuu.alloc(sizeof(double) * (size_t)m * m) || q.alloc(sizeof(double) * n) ||
+      dYraw.alloc(sizeof(double) * n * n_out) || dyn.alloc(sizeof(double) * n * n_out) ||
+      yl.alloc(sizeof(double) * n * n_out) || sig.alloc(sizeof(double) * n) ||
+      cvec.alloc(sizeof(double) * m * n_out) || alpha.alloc(sizeof(double) * m * n_out) ||
+      dlml.alloc(sizeof(double) * n_out) || g.ymean.alloc(sizeof(double) * n_out) ||
+      g.ystd.alloc(sizeof(double) * n_out) || g.alphaT.alloc(sizeof(double) * n_out * m)) {
+    gpmpc_set_error("vfe_fit: out of device memory");
+    return fail(-1);
+  }
+  g.n_out = n_out;
+  // K_uu into B (kept for alpha^T K_uu alpha), then B += K_uf K_fu / s2n (SYRK on
+  // MFMA, lower triangle), then + jitter I in the reference's order
+  launch_gram(s, GPMPC_SE_ARD, g.Xs.as<double>(), g.Xn.as<double>(), m, g.Xs.as<double>(),
+              g.Xn.as<double>(), m, g.d, sigma2, 0.0, B.as<double>(), m, 0);
+  hipMemcpyAsync(Kuu.p, B.p, sizeof(double) * (size_t)m * m, hipMemcpyDeviceToDevice, s);
+  launch_gemm_nt(s, EPI_STORE, m, m, n, Kuf.as<double>(), n, Kuf.as<double>(), n, B.as<double>(), m,
+                 1.0 / noise, 1.0, 0, 1, 1, 0, 0, 0);
+  launch_add_diag(s, m, B.as<double>(), m, jitter, 1, 0);
+  // normalised targets; c = K_uf (y / s2n)  (sparse_gp.py:160-166, 231)
+  hipMemcpyAsync(dYraw.p, Y, sizeof(double) * n * n_out, hipMemcpyHostToDevice, s);
+  hipLaunchKernelGGL(k_normalise, dim3(n_out), dim3(256), 0, s, n, n_out, dYraw.as<double>(),
+                     dyn.as<double>(), g.ymean.as<double>(), g.ystd.as<double>());
+  hipLaunchKernelGGL(k_fill, dim3((n + 255) / 256), dim3(256), 0, s, n, noise, sig.as<double>());
+  hipLaunchKernelGGL(k_fitc_yl, dim3((n + 255) / 256, n_out), dim3(256), 0, s, n, n_out,
+                     dyn.as<double>(), sig.as<double>(), yl.as<double>());
+  launch_gemm_nt(s, EPI_STORE, m, n_out, n, Kuf.as<double>(), n, yl.as<double>(), n,
+                 cvec.as<double>(), n_out, 1.0, 0.0, 0, 0, 1, 0, 0, 0);
+  // Q_ff diagonal for the trace term: colsum((L_uu^-1 K_uf)^2)  (sparse_gp.py:240-242)
+  launch_trsm_lower_ex(s, m, n, Luu.as<double>(), m, Kuf.as<double>(), n, 0, 0, nullptr);
+  hipLaunchKernelGGL(k_colsumsq, dim3((n + 255) / 256), dim3(256), 0, s, m, n, Kuf.as<double>(),
+                     q.as<double>());
+  int info = 0;
+  launch_potrf_batched(s, m, 1, B.as<double>(), m, 0, dinfo.as<int>());
+  hipMemcpyAsync(&info, dinfo.p, sizeof(int), hipMemcpyDeviceToHost, s);
+  GPMPC_HIP(hipStreamSynchronize(s));
+  if (info) {
+    gpmpc_set_error("Matrix is not positive definite (B, column %d)", info);
+    return fail(info);
+  }
+  // W2 = L_B^-1 L_uu^-1: the predict's w = L_B^-1 v as the reference writes it for both
+  // methods (sparse_gp.py:292-296)
+  hipMemcpyAsync(gp->W2.p, g.W.p, sizeof(double) * (size_t)m * m, hipMemcpyDeviceToDevice, s);
+  launch_trsm_lower_ex(s, m, m, B.as<double>(), m, gp->W2.as<double>(), m, 0, 1, nullptr);
+  hipMemcpyAsync(alpha.p, cvec.p, sizeof(double) * m * n_out, hipMemcpyDeviceToDevice, s);
+  launch_trsm_lower_ex(s, m, n_out, B.as<double>(), m, alpha.as<double>(), n_out, 0, 0, nullptr);
+  launch_trsm_lower_ex(s, m, n_out, B.as<double>(), m, alpha.as<double>(), n_out, 1, 0, nullptr);
+  hipLaunchKernelGGL(k_lml_vfe, dim3(n_out), dim3(256), 0, s, m, n, n_out, B.as<double>(),
+                     Luu.as<double>(), Kuu.as<double>(), dyn.as<double>(), q.as<double>(),
+                     cvec.as<double>(), alpha.as<double>(), sigma2, noise, g.alphaT.as<double>(),
+                     dlml.as<double>());
+  hipMemcpyAsync(g.W.as<double>() + (size_t)m * m, g.alphaT.p, sizeof(double) * n_out * m,
+                 hipMemcpyDeviceToDevice, s);
+  g.h_ymean.resize(n_out);
+  g.h_ystd.resize(n_out);
+  std::vector<double> hl(n_out);
+  hipMemcpyAsync(g.h_ymean.data(), g.ymean.p, sizeof(double) * n_out, hipMemcpyDeviceToHost, s);
+  hipMemcpyAsync(g.h_ystd.data(), g.ystd.p, sizeof(double) * n_out, hipMemcpyDeviceToHost, s);
+  hipMemcpyAsync(hl.data(), dlml.p, sizeof(double) * n_out, hipMemcpyDeviceToHost, s);
+  if (hipStreamSynchronize(s) != hipSuccess) {
+    gpmpc_set_error("vfe_fit: %s", hipGetErrorString(hipGetLastError()));
+    return fail(-1);
+  }
+  for (int c = 0; c < n_out; ++c) {
+    if (lml) lml[c] = hl[c];
+    if (y_mean) y_mean[c] = g.h_ymean[c];
+    if (y_std) y_std[c] = g.h_ystd[c];
+  }
+  *out = gp;
+  return 0;
+}
+
+// SparseGP.fit, FITC (vfe = 0, sparse_gp.py:181-219) or VFE (vfe = 1, :181-188 then
+// :221-249).  Both leave the same handle: W = [L_uu^-1; alpha^T], W2 = L_B^-1 L_uu^-1,
+// so gpmpc_fitc_predict serves both (the reference's predict has one body for the two).
+static int sparse_fit(gpmpc_ctx *ctx, const double *Z, int m, const double *X, int n, int d,
+                      const double *Y, int n_out, const double *ls, double sigma2, double noise,
+                      double jitter, gpmpc_fitc **out, double *y_mean, double *y_std, double *lml,
+                      double *lambda_diag, int vfe) {
   GPMPC_CHECK_ARG(ctx && Z && X && Y && ls && out && m >= 1 && n >= 1 && d >= 1 && d <= 32);
   GPMPC_CHECK_ARG(n_out >= 1 && n_out <= 16);
+  GPMPC_CHECK_ARG(!vfe || noise > 0.0);
   GPMPC_HIP(hipSetDevice(ctx->device));
   hipStream_t s = ctx->stream;
   auto *gp = new gpmpc_fitc();
@@ -511,12 +652,14 @@ extern "C" int gpmpc_fitc_fit(gpmpc_ctx *ctx, const double *Z, int m, const doub
     gpmpc_set_error("Matrix is not positive definite (K_uu, column %d)", info);
     return fail(info);
   }
-  // A = L_uu^-1 K_uf  (m x n)
+  // A = L_uu^-1 K_uf  (m x n); VFE forms B and c from K_uf itself first
   launch_gram(s, GPMPC_SE_ARD, g.Xs.as<double>(), g.Xn.as<double>(), m, Xs.as<double>(),
               Xn.as<double>(), n, d, sigma2, 0.0, Kuf.as<double>(), n, 0);
-  launch_trsm_lower_ex(s, m, n, Luu.as<double>(), m, Kuf.as<double>(), n, 0, 0, nullptr);
   hipLaunchKernelGGL(k_eye, dim3((m + 255) / 256, m), dim3(256), 0, s, m, g.W.as<double>());
   launch_trsm_lower_ex(s, m, m, Luu.as<double>(), m, g.W.as<double>(), m, 0, 1, nullptr);
+  if (vfe) return vfe_tail(ctx, gp, Luu, Kuf, B, dinfo, Y, n, n_out, sigma2, noise, jitter, out,
+                           y_mean, y_std, lml);
+  launch_trsm_lower_ex(s, m, n, Luu.as<double>(), m, Kuf.as<double>(), n, 0, 0, nullptr);
   // normalised targets; c = A (y / Lambda) before A is rescaled  (sparse_gp.py:160-166, 204)
   DevBuf isq, dYraw, dyn, yl, cvec, alpha, dlml;
   if (isq.alloc(sizeof(double) * n) || dYraw.alloc(sizeof(double) * n * n_out) ||
@@ -583,6 +726,22 @@ extern "C" int gpmpc_fitc_fit(gpmpc_ctx *ctx, const double *Z, int m, const doub
   }
   *out = gp;
   return 0;
+}
+
+extern "C" int gpmpc_fitc_fit(gpmpc_ctx *ctx, const double *Z, int m, const double *X, int n,
+                              int d, const double *Y, int n_out, const double *ls, double sigma2,
+                              double noise, double jitter, gpmpc_fitc **out, double *y_mean,
+                              double *y_std, double *lml, double *lambda_diag) {
+  return sparse_fit(ctx, Z, m, X, n, d, Y, n_out, ls, sigma2, noise, jitter, out, y_mean, y_std,
+                    lml, lambda_diag, 0);
+}
+
+extern "C" int gpmpc_vfe_fit(gpmpc_ctx *ctx, const double *Z, int m, const double *X, int n,
+                             int d, const double *Y, int n_out, const double *ls, double sigma2,
+                             double noise, double jitter, gpmpc_fitc **out, double *y_mean,
+                             double *y_std, double *lml) {
+  return sparse_fit(ctx, Z, m, X, n, d, Y, n_out, ls, sigma2, noise, jitter, out, y_mean, y_std,
+                    lml, nullptr, 1);
 }
 
 extern "C" int gpmpc_fitc_predict(gpmpc_ctx *ctx, gpmpc_fitc *gp, const double *Xq, int p,

@@ -7,7 +7,9 @@ Lambda = max(sigma2 - colsum(A^2) + sigma_n^2, 1e-10), B = I + A Lambda^-1 A^T
 255-305).  Inducing points are chosen on the host exactly like the reference
 (scipy kmeans2 on the global RNG, random-subset fallback, sparse_gp.py:122-148);
 MultiOutputSparseGP shares them and fits all outputs with one device call.
-The VFE branch (unused by the reference's surfaces) is not on this path.
+method="vfe" -> gpmpc_vfe_fit: B = K_uu + K_uf K_fu / sigma_n^2 + jitter I -> L_B,
+alpha = B^-1 K_uf y / sigma_n^2, the VFE bound (sparse_gp.py:221-249); the
+reference predicts both methods with one body, and so does the device handle.
 """
 from __future__ import annotations
 
@@ -71,15 +73,15 @@ class SparseGP:
         return Z
 
     def fit(self, X, y) -> "SparseGP":
-        if self.method != "fitc":
-            raise NotImplementedError("only the FITC approximation is on the device path")
+        if self.method not in ("fitc", "vfe"):
+            raise ValueError(f"method must be 'fitc' or 'vfe', got {self.method!r}")
         X = np.atleast_2d(X)
         y = np.atleast_1d(y).flatten()
         if self._Z is None:
             self._Z = self._initialize_inducing_points(X)
         _, ls, s2 = _spec(self.kernel)
         h = _lib.FITCHandle(_lib.default_context(), self._Z, X, y[:, None], ls, s2,
-                            self._noise_variance, self.jitter)
+                            self._noise_variance, self.jitter, method=self.method)
         self._attach(X, y, h, 0)
         return self
 

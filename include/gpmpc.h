@@ -149,6 +149,13 @@ int gpmpc_fitc_fit(gpmpc_ctx *ctx, const double *Z, int m, const double *X, int 
                    const double *Y, int n_out, const double *ls, double sigma2, double noise,
                    double jitter, gpmpc_fitc **out, double *y_mean, double *y_std, double *lml,
                    double *lambda_diag);
+/* SparseGP(method="vfe").fit (sparse_gp.py:221-249 after the shared :181-188):
+ * B = K_uu + K_uf K_fu / noise + jitter I, alpha = B^-1 K_uf y / noise, the VFE
+ * lower bound as lml.  Same handle type as gpmpc_fitc_fit: gpmpc_fitc_predict
+ * evaluates it with the reference's one predict body (sparse_gp.py:255-305). */
+int gpmpc_vfe_fit(gpmpc_ctx *ctx, const double *Z, int m, const double *X, int n, int d,
+                  const double *Y, int n_out, const double *ls, double sigma2, double noise,
+                  double jitter, gpmpc_fitc **out, double *y_mean, double *y_std, double *lml);
 /* SparseGP.predict (sparse_gp.py:255-305), mean as written. */
 int gpmpc_fitc_predict(gpmpc_ctx *ctx, gpmpc_fitc *gp, const double *Xq, int p, double *mean,
                        double *var);

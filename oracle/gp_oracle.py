@@ -258,6 +258,39 @@ def fitc_fit(Zi, X, Y, sigma2=1.0, ls=None, noise=1e-4, jitter=1e-6):
     return st
 
 
+def vfe_fit(Zi, X, Y, sigma2=1.0, ls=None, noise=1e-4, jitter=1e-6):
+    """SparseGP.fit, VFE branch (sparse_gp.py:221-249 after the shared :181-188), every
+    column of Y over one inducing set.  Returns the fitc_fit state layout, so
+    fitc_predict evaluates it (the reference's predict has one body for both)."""
+    X = np.atleast_2d(X); Y = np.asarray(Y, float)
+    if Y.ndim == 1:
+        Y = Y[:, None]
+    if ls is None:
+        ls = np.ones(X.shape[1])
+    M = Zi.shape[0]; N = X.shape[0]
+    Kuu = gram("se_ard", Zi, None, sigma2, ls)
+    Kuf = gram("se_ard", Zi, X, sigma2, ls)
+    Luu = np.linalg.cholesky(Kuu + jitter * np.eye(M))
+    A = solve_triangular(Luu, Kuf, lower=True)
+    B = Kuu + (1.0 / noise) * Kuf @ Kuf.T + jitter * np.eye(M)
+    LB = np.linalg.cholesky(B)
+    trace_term = (N * sigma2 - np.sum(A ** 2)) / noise
+    st = dict(Zi=Zi, Luu=Luu, LB=LB, lam=None, sigma2=sigma2, ls=np.asarray(ls, float),
+              alpha=[], y_mean=[], y_std=[], lml=[])
+    for c in range(Y.shape[1]):
+        yn, m, s = normalise(Y[:, c])
+        cv = Kuf @ yn / noise
+        a = cho_solve((LB, True), cv)
+        fit = -0.5 / noise * np.dot(yn, yn) + np.dot(cv, a) - 0.5 * np.dot(a, Kuu @ a)
+        cplx = -np.sum(np.log(np.diag(LB))) + np.sum(np.log(np.diag(Luu))) - 0.5 * N * np.log(noise)
+        st["alpha"].append(a); st["y_mean"].append(m); st["y_std"].append(s)
+        st["lml"].append(fit - 0.5 * trace_term + cplx - 0.5 * N * np.log(2 * np.pi))
+    st["alpha"] = np.stack(st["alpha"], axis=1)
+    for k in ("y_mean", "y_std", "lml"):
+        st[k] = np.array(st[k])
+    return st
+
+
 def fitc_predict(st, Xq):
     """SparseGP.predict (sparse_gp.py:255-305); the mean is K*u @ alpha as written (D1)."""
     Xq = np.atleast_2d(Xq)

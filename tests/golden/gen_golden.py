@@ -395,7 +395,36 @@ def f10():
          opt_success=res["success"])
 
 
+# ---------------------------------------------------------------- F12
+def f12():
+    """Reference SparseGP(method="vfe") (sparse_gp.py:150-188, 221-249; predict
+    :255-305) on the 3-DoF features, two outputs over caller-set inducing points
+    (a random subset, so no kmeans2 draw is involved), non-unit hyperparameters."""
+    X, U, D = synthetic_training_data(600, seed=5)
+    fe = features.Simple3DoFFeatureExtractor()
+    Z = fe.extract_batch(X, U)
+    rs = np.random.RandomState(12)
+    Zi = Z[rs.choice(Z.shape[0], 40, replace=False)].copy()
+    sd = Z.std(0)
+    sd[sd < 1e-6] = 1.0
+    ls = 3.0 * sd * (0.8 + 0.4 * rs.rand(Z.shape[1]))  # well-conditioned B (cond ~1e5)
+    Xq, Uq = query_points(X, U, 25, seed=13)
+    Zq = fe.extract_batch(Xq, Uq)
+    out = dict(Z=Z, Y=D[:, :2], Zi=Zi, ls=ls, Zq=Zq, sigma2=np.array(1.7), noise=np.array(5e-2),
+               jitter=np.array(1e-6))
+    for c in range(2):
+        k = kernels.SquaredExponentialARD(Z.shape[1], signal_variance=1.7, lengthscales=ls.copy())
+        g = sparse_gp.SparseGP(k, n_inducing=40, noise_variance=5e-2, method="vfe",
+                               inducing_points=Zi.copy())
+        g.fit(Z, D[:, c])
+        pr = g.predict(Zq)
+        out[f"mean{c}"] = pr.mean; out[f"var{c}"] = pr.variance
+        out[f"alpha{c}"] = g._alpha; out[f"lml{c}"] = np.array(g.log_marginal_likelihood)
+        out[f"diagLB{c}"] = np.diag(g._L_B).copy()
+    save("f12_vfe_3dof.npz", **out)
+
+
 if __name__ == "__main__":
-    which = sys.argv[1:] or ["f1", "f2", "f3", "f4", "f5", "f6", "f6b", "f7_f8", "f9", "f10", "f11"]
+    which = sys.argv[1:] or ["f1", "f2", "f3", "f4", "f5", "f6", "f6b", "f7_f8", "f9", "f10", "f11", "f12"]
     for w in which:
         globals()[w]()

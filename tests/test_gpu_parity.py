@@ -185,6 +185,54 @@ def test_fitc_vs_golden_f4(gpu_ctx):
     ok, e = close(var, f["var"], f["y_std"] ** 2); assert ok, e
 
 
+def test_vfe_vs_golden_f12(gpu_ctx):
+    """gpmpc_vfe_fit + gpmpc_fitc_predict vs the reference's SparseGP(method="vfe")
+    (F12) and the oracle restatement; through the host SparseGP surface as well."""
+    L = _lib()
+    from oracle import gp_oracle
+    from gp_mpc_rocket_landing_amd.gp.kernels import SquaredExponentialARD
+    from gp_mpc_rocket_landing_amd.gp.sparse_gp import SparseGP
+    f = golden("f12_vfe_3dof.npz")
+    s2, nz, jit = float(f["sigma2"]), float(f["noise"]), float(f["jitter"])
+    gp = L.FITCHandle(gpu_ctx, f["Zi"], f["Z"], f["Y"], f["ls"], s2, nz, jit, method="vfe")
+    assert gp.lam is None
+    st = gp_oracle.vfe_fit(f["Zi"], f["Z"], f["Y"], s2, f["ls"], nz, jit)
+    mean, var = gp.predict(f["Zq"])
+    alpha = gp.alpha()
+    for c in range(2):
+        np.testing.assert_allclose(gp.lml[c], f[f"lml{c}"], rtol=1e-7)
+        np.testing.assert_allclose(alpha[:, c], f[f"alpha{c}"], rtol=1e-6, atol=1e-8)
+        ok, e = close(mean[:, c], f[f"mean{c}"], gp.y_std[c]); assert ok, e
+        ok, e = close(var[:, c], f[f"var{c}"], gp.y_std[c] ** 2); assert ok, e
+    np.testing.assert_allclose(gp.lml, st["lml"], rtol=1e-7)
+    k = SquaredExponentialARD(f["Z"].shape[1], signal_variance=s2, lengthscales=f["ls"].copy())
+    sg = SparseGP(k, n_inducing=40, noise_variance=nz, method="vfe", inducing_points=f["Zi"].copy())
+    sg.fit(f["Z"], f["Y"][:, 1])
+    pr = sg.predict(f["Zq"])
+    ok, e = close(pr.mean, f["mean1"], sg._y_std); assert ok, e
+    ok, e = close(pr.variance, f["var1"], sg._y_std ** 2); assert ok, e
+    np.testing.assert_allclose(sg.log_marginal_likelihood, f["lml1"], rtol=1e-7)
+
+
+def test_vfe_scale_vs_oracle(gpu_ctx):
+    """VFE at M = 600 / N = 2500 (the MFMA SYRK, blocked potrf and TRSM paths) vs the oracle."""
+    L = _lib()
+    from oracle import gp_oracle
+    rs = np.random.RandomState(21)
+    X = rs.randn(2500, 11); Y = np.stack([np.sin(X[:, 0]) + 0.1 * X[:, 1], X[:, 2] * X[:, 3]], 1)
+    Zi = X[rs.choice(2500, 600, replace=False)].copy()
+    ls = 1.5 + rs.rand(11)
+    gp = L.FITCHandle(gpu_ctx, Zi, X, Y, ls, 1.3, 1e-2, 1e-6, method="vfe")
+    st = gp_oracle.vfe_fit(Zi, X, Y, 1.3, ls, 1e-2, 1e-6)
+    Xq = rs.randn(300, 11)
+    mean, var = gp.predict(Xq)
+    m_o, v_o = gp_oracle.fitc_predict(st, Xq)
+    np.testing.assert_allclose(gp.lml, st["lml"], rtol=1e-7)
+    for c in range(2):
+        ok, e = close(mean[:, c], m_o[:, c], st["y_std"][c]); assert ok, e
+        ok, e = close(var[:, c], v_o[:, c], st["y_std"][c] ** 2); assert ok, e
+
+
 def _qp_batch(B, seed=0, N=20):
     from oracle import mc_oracle, qp_oracle
     rs = np.random.RandomState(seed)

@@ -1,4 +1,4 @@
-"""The CPU oracle against the reference's own outputs (golden fixtures F1-F8).
+"""The CPU oracle against the reference's own outputs (golden fixtures F1-F12).
 
 These pin the oracle before it is trusted as the parity checker for the HIP path.
 """
@@ -80,6 +80,20 @@ def test_f4_fitc():
     mean, var = gp_oracle.fitc_predict(st, f["Zq"])
     ok, e = close(mean, f["mean"], f["y_std"]); assert ok, e
     ok, e = close(var, f["var"], f["y_std"] ** 2); assert ok, e
+
+
+def test_f12_vfe():
+    """SparseGP(method="vfe") restated (gp_oracle.vfe_fit) vs the reference's own fit."""
+    f = golden("f12_vfe_3dof.npz")
+    st = gp_oracle.vfe_fit(f["Zi"], f["Z"], f["Y"], float(f["sigma2"]), f["ls"], float(f["noise"]),
+                           float(f["jitter"]))
+    mean, var = gp_oracle.fitc_predict(st, f["Zq"])
+    for c in range(2):
+        np.testing.assert_allclose(np.diag(st["LB"]), f[f"diagLB{c}"], rtol=1e-12)
+        np.testing.assert_allclose(st["alpha"][:, c], f[f"alpha{c}"], rtol=1e-7, atol=1e-9)
+        np.testing.assert_allclose(st["lml"][c], f[f"lml{c}"], rtol=1e-9)
+        ok, e = close(mean[:, c], f[f"mean{c}"], st["y_std"][c]); assert ok, e
+        ok, e = close(var[:, c], f[f"var{c}"], st["y_std"][c] ** 2); assert ok, e
 
 
 def test_f5_structured_features():
