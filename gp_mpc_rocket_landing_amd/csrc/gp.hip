@@ -243,6 +243,106 @@ struct ScratchPtr {
   template <class T> T *as() const { return reinterpret_cast<T *>(p); }
 };
 
+// alpha = L^-T L^-1 y for the few output columns of an exact fit (exact_gp.py:179,
+// cho_solve): one workgroup per column with the vector in LDS, by 32-row blocks.
+// Forward: wave 0 solves the block's triangle in registers (readlane broadcasts),
+// then all 256 threads subtract L[r, blk] x_blk from the rows below (each row's 32
+// block entries contiguous).  Backward (L^T): wave 0 back-substitutes the block with
+// L_bb^T, then x[r] -= sum_j L[r0 + j][r] x_j for the rows above (consecutive threads,
+// consecutive r: coalesced).  The blocked TRSM it replaces walked 2 x 8 panel
+// launches of ~70 us each for 3 columns (fit breakdown).
+#define POTRS_COLS_MAXN 16384
+__global__ __launch_bounds__(256) void k_potrs_cols(int n, const double *__restrict__ L,
+                                                    int64_t ldl, double *__restrict__ Y,
+                                                    int n_out) {
+  const int c = blockIdx.x;
+  extern __shared__ double x[];
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  for (int i = tid; i < n; i += 256) x[i] = Y[(int64_t)i * n_out + c];
+  __syncthreads();
+  for (int r0 = 0; r0 < n; r0 += 32) {
+    const int nb = min(32, n - r0);
+    if (wave == 0) {
+      double a[32];
+#pragma unroll
+      for (int j = 0; j < 32; ++j)
+        a[j] = (lane < nb && j <= lane) ? L[(int64_t)(r0 + lane) * ldl + r0 + j] : 1.0;
+      double sv = lane < nb ? x[r0 + lane] : 0.0;
+#pragma unroll
+      for (int j = 0; j < 32; ++j) {
+        if (j < nb) {
+          if (lane == j) sv = sv / a[j];
+          const double xj = __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(sv), j),
+                                             __builtin_amdgcn_readlane(__double2loint(sv), j));
+          if (lane > j) sv = fma(-a[j], xj, sv);
+        }
+      }
+      if (lane < nb) x[r0 + lane] = sv;
+    }
+    __syncthreads();
+    const int r1 = r0 + nb;
+    if (r1 < n) {
+      double xb[32];
+#pragma unroll
+      for (int j = 0; j < 32; ++j) xb[j] = x[r0 + j];  // nb = 32 whenever rows remain below
+      for (int r = r1 + tid; r < n; r += 256) {
+        const double *row = L + (int64_t)r * ldl + r0;
+        double acc = 0.0;
+#pragma unroll
+        for (int j = 0; j < 32; ++j) acc = fma(row[j], xb[j], acc);
+        x[r] -= acc;
+      }
+    }
+    __syncthreads();
+  }
+  for (int r0 = ((n - 1) / 32) * 32; r0 >= 0; r0 -= 32) {
+    const int nb = min(32, n - r0);
+    if (wave == 0) {
+      double a[32];  // a[j] = (L_bb^T)[lane][j] = L[r0 + j][r0 + lane], j >= lane
+#pragma unroll
+      for (int j = 0; j < 32; ++j)
+        a[j] = (lane < nb && j < nb && j >= lane) ? L[(int64_t)(r0 + j) * ldl + r0 + lane] : 1.0;
+      double sv = lane < nb ? x[r0 + lane] : 0.0;
+#pragma unroll
+      for (int j = 31; j >= 0; --j) {
+        if (j < nb) {
+          if (lane == j) sv = sv / a[j];
+          const double xj = __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(sv), j),
+                                             __builtin_amdgcn_readlane(__double2loint(sv), j));
+          if (lane < j) sv = fma(-a[j], xj, sv);
+        }
+      }
+      if (lane < nb) x[r0 + lane] = sv;
+    }
+    __syncthreads();
+    if (r0 > 0) {
+      double xb[32];
+#pragma unroll
+      for (int j = 0; j < 32; ++j) xb[j] = j < nb ? x[r0 + j] : 0.0;
+      for (int r = tid; r < r0; r += 256) {
+        double acc = 0.0;
+#pragma unroll
+        for (int j = 0; j < 32; ++j)
+          if (j < nb) acc = fma(L[(int64_t)(r0 + j) * ldl + r], xb[j], acc);
+        x[r] -= acc;
+      }
+    }
+    __syncthreads();
+  }
+  for (int i = tid; i < n; i += 256) Y[(int64_t)i * n_out + c] = x[i];
+}
+
+static bool potrs_cols_ok(int n) {
+  static const int env = [] {
+    const char *e = getenv("GPMPC_POTRS_COLS");
+    return e ? atoi(e) : 1;
+  }();
+  static const bool attr = hipFuncSetAttribute((const void *)k_potrs_cols,
+                                               hipFuncAttributeMaxDynamicSharedMemorySize,
+                                               (int)(sizeof(double) * POTRS_COLS_MAXN)) == hipSuccess;
+  return env && attr && n <= POTRS_COLS_MAXN;
+}
+
 extern "C" int gpmpc_gp_fit_exact(gpmpc_ctx *ctx, int kind, const double *X, int n, int d,
                                   const double *Y, int n_out, const double *ls, double sigma2,
                                   double noise, gpmpc_gp **out, double *y_mean, double *y_std,
@@ -311,8 +411,13 @@ extern "C" int gpmpc_gp_fit_exact(gpmpc_ctx *ctx, int kind, const double *X, int
   hipLaunchKernelGGL(k_normalise, dim3(n_out), dim3(256), 0, s, n, n_out, dYraw.as<double>(),
                      dyn.as<double>(), g.ymean.as<double>(), g.ystd.as<double>());
   hipMemcpyAsync(dY.p, dyn.p, sizeof(double) * n * n_out, hipMemcpyDeviceToDevice, s);
-  launch_trsm_lower_ex(s, n, n_out, gp->L.as<double>(), n, dY.as<double>(), n_out, 0, 0, nullptr);
-  launch_trsm_lower_ex(s, n, n_out, gp->L.as<double>(), n, dY.as<double>(), n_out, 1, 0, nullptr);
+  if (potrs_cols_ok(n)) {
+    hipLaunchKernelGGL(k_potrs_cols, dim3(n_out), dim3(256), sizeof(double) * n, s, n,
+                       gp->L.as<double>(), (int64_t)n, dY.as<double>(), n_out);
+  } else {
+    launch_trsm_lower_ex(s, n, n_out, gp->L.as<double>(), n, dY.as<double>(), n_out, 0, 0, nullptr);
+    launch_trsm_lower_ex(s, n, n_out, gp->L.as<double>(), n, dY.as<double>(), n_out, 1, 0, nullptr);
+  }
   // log marginal likelihood per output + alpha^T for the posterior GEMM (exact_gp.py:186-204)
   hipLaunchKernelGGL(k_lml_exact, dim3(n_out), dim3(256), 0, s, n, n_out, gp->L.as<double>(),
                      dyn.as<double>(), dY.as<double>(), g.alphaT.as<double>(), dlml.as<double>());
