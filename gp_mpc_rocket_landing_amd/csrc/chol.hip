@@ -1335,6 +1335,16 @@ __device__ __forceinline__ double ld_l2(const double *p) {
 __global__ __launch_bounds__(256) void k_trsm_panel(int n, int nrhs, const double *L, int64_t ldl,
                                                     const double *Linv, double *X, int64_t ldx,
                                                     int trans, int rhs_lower) {
+  // blockIdx.y: the TB x TB diagonal block solved (launch_tri_inverse solves all the
+  // diagonal blocks of L^-1 side by side; every other launch has gridDim.y = 1, n <= TB)
+  {
+    const int bq = blockIdx.y;
+    L += (int64_t)bq * TB * (ldl + 1);
+    X += (int64_t)bq * TB * (ldx + 1);
+    Linv += (int64_t)bq * (TB / NB) * NB * NB;
+    n = min(TB, n - bq * TB);
+    if (bq) nrhs = n;
+  }
   const int c0 = blockIdx.x * 64;
   const int nblk = (n + NB - 1) / NB;
   __shared__ double sL[NB][TP];
@@ -1453,6 +1463,35 @@ hipError_t launch_trsm_lower_ex(hipStream_t s, int n, int nrhs, const double *L,
     if (r1 < n) {
       hipError_t e = launch_gemm_nn(s, n - r1, cols, nb, L + (int64_t)r1 * ldl + r0, ldl,
                                     X + (int64_t)r0 * ldx, ldx, X + (int64_t)r1 * ldx, ldx, -1.0, 1.0);
+      if (e != hipSuccess) return e;
+    }
+  }
+  return hipGetLastError();
+}
+
+// W = L^-1 (W preset to the identity, ldw >= n): the TB x TB diagonal blocks of W by
+// one k_trsm_panel launch over all of them (blockIdx.y = block), then by doubling,
+// for each pair of solved blocks A (rows s0..s0+b) and C (the next <= b rows):
+//   W_CA = -C^-1 (L_CA A^-1)     (two MFMA GEMMs, tmp >= b x b doubles)
+// 8 serial panel launches of the blocked TRSM (~0.8 ms at n = 1000) become one panel
+// launch and 2 log2(n / TB) levels of GEMMs.
+hipError_t launch_tri_inverse(hipStream_t s, int n, const double *L, int64_t ldl, double *W,
+                              int64_t ldw, double *tmp) {
+  const int nblk = (n + NB - 1) / NB;
+  double *Linv = (double *)gpmpc_scratch(s, 0, sizeof(double) * NB * NB * (size_t)nblk);
+  if (!Linv) return hipErrorOutOfMemory;
+  hipLaunchKernelGGL(k_tri_inv_blocks, dim3(nblk), dim3(64), 0, s, n, L, ldl, Linv);
+  const int nd = (n + TB - 1) / TB;
+  hipLaunchKernelGGL(k_trsm_panel, dim3((std::min(n, TB) + 63) / 64, nd), dim3(256), 0, s, n,
+                     std::min(n, TB), L, ldl, Linv, W, ldw, 0, 1);
+  for (int b = TB; b < n; b *= 2) {
+    for (int s0 = 0; s0 + b < n; s0 += 2 * b) {
+      const int c0 = s0 + b, mc = std::min(n, s0 + 2 * b) - c0;
+      hipError_t e = launch_gemm_nn(s, mc, b, b, L + (int64_t)c0 * ldl + s0, ldl,
+                                    W + (int64_t)s0 * ldw + s0, ldw, tmp, b, 1.0, 0.0);
+      if (e != hipSuccess) return e;
+      e = launch_gemm_nn(s, mc, b, mc, W + (int64_t)c0 * ldw + c0, ldw, tmp, b,
+                         W + (int64_t)c0 * ldw + s0, ldw, -1.0, 0.0);
       if (e != hipSuccess) return e;
     }
   }

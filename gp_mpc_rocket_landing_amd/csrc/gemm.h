@@ -37,6 +37,10 @@ hipError_t launch_gemm_tn(hipStream_t s, int M, int N, int K, const double *A, i
                           const double *B, int64_t ldb, double *C, int64_t ldc, double alpha,
                           double beta);
 
+// W = L^-1 with W preset to the identity; tmp: >= (n/2 rounded up to TB) squared doubles
+hipError_t launch_tri_inverse(hipStream_t s, int n, const double *L, int64_t ldl, double *W,
+                              int64_t ldw, double *tmp);
+
 hipError_t launch_trsm_lower_ex(hipStream_t s, int n, int nrhs, const double *L, int64_t ldl,
                                 double *X, int64_t ldx, int trans, int rhs_lower,
                                 double *Linv_blocks);

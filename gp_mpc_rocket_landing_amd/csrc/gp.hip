@@ -423,7 +423,15 @@ extern "C" int gpmpc_gp_fit_exact(gpmpc_ctx *ctx, int kind, const double *X, int
                      dyn.as<double>(), dY.as<double>(), g.alphaT.as<double>(), dlml.as<double>());
   // W = L^-1 (identity right-hand side, lower-triangular result)
   hipLaunchKernelGGL(k_eye, dim3((n + 255) / 256, n), dim3(256), 0, s, n, g.W.as<double>());
-  launch_trsm_lower_ex(s, n, n, gp->L.as<double>(), n, g.W.as<double>(), n, 0, 1, nullptr);
+  static const int tri_inv_env = [] {
+    const char *e = getenv("GPMPC_TRI_INV");
+    return e ? atoi(e) : 1;
+  }();
+  DevBuf tinv;
+  if (tri_inv_env && n > 128 && tinv.alloc(sizeof(double) * (size_t)n * n) == hipSuccess)
+    launch_tri_inverse(s, n, gp->L.as<double>(), n, g.W.as<double>(), n, tinv.as<double>());
+  else
+    launch_trsm_lower_ex(s, n, n, gp->L.as<double>(), n, g.W.as<double>(), n, 0, 1, nullptr);
   // alpha^T below W: the variance GEMM produces the posterior mean in the same pass
   hipMemcpyAsync(g.W.as<double>() + (size_t)n * n, g.alphaT.p, sizeof(double) * n_out * n,
                  hipMemcpyDeviceToDevice, s);
@@ -687,8 +695,13 @@ static int vfe_tail(gpmpc_ctx *ctx, gpmpc_fitc *gp, DevBuf &Luu, DevBuf &Kuf, De
   hipMemcpyAsync(gp->W2.p, g.W.p, sizeof(double) * (size_t)m * m, hipMemcpyDeviceToDevice, s);
   launch_trsm_lower_ex(s, m, m, B.as<double>(), m, gp->W2.as<double>(), m, 0, 1, nullptr);
   hipMemcpyAsync(alpha.p, cvec.p, sizeof(double) * m * n_out, hipMemcpyDeviceToDevice, s);
-  launch_trsm_lower_ex(s, m, n_out, B.as<double>(), m, alpha.as<double>(), n_out, 0, 0, nullptr);
-  launch_trsm_lower_ex(s, m, n_out, B.as<double>(), m, alpha.as<double>(), n_out, 1, 0, nullptr);
+  if (potrs_cols_ok(m)) {
+    hipLaunchKernelGGL(k_potrs_cols, dim3(n_out), dim3(256), sizeof(double) * m, s, m,
+                       B.as<double>(), (int64_t)m, alpha.as<double>(), n_out);
+  } else {
+    launch_trsm_lower_ex(s, m, n_out, B.as<double>(), m, alpha.as<double>(), n_out, 0, 0, nullptr);
+    launch_trsm_lower_ex(s, m, n_out, B.as<double>(), m, alpha.as<double>(), n_out, 1, 0, nullptr);
+  }
   hipLaunchKernelGGL(k_lml_vfe, dim3(n_out), dim3(256), 0, s, m, n, n_out, B.as<double>(),
                      Luu.as<double>(), Kuu.as<double>(), dyn.as<double>(), q.as<double>(),
                      cvec.as<double>(), alpha.as<double>(), sigma2, noise, g.alphaT.as<double>(),
@@ -804,8 +817,13 @@ static int sparse_fit(gpmpc_ctx *ctx, const double *Z, int m, const double *X, i
   launch_trsm_lower_ex(s, m, m, B.as<double>(), m, gp->W2.as<double>(), m, 0, 1, nullptr);
   // alpha = B^-1 c  and the FITC lml  (sparse_gp.py:207-218)
   hipMemcpyAsync(alpha.p, cvec.p, sizeof(double) * m * n_out, hipMemcpyDeviceToDevice, s);
-  launch_trsm_lower_ex(s, m, n_out, B.as<double>(), m, alpha.as<double>(), n_out, 0, 0, nullptr);
-  launch_trsm_lower_ex(s, m, n_out, B.as<double>(), m, alpha.as<double>(), n_out, 1, 0, nullptr);
+  if (potrs_cols_ok(m)) {
+    hipLaunchKernelGGL(k_potrs_cols, dim3(n_out), dim3(256), sizeof(double) * m, s, m,
+                       B.as<double>(), (int64_t)m, alpha.as<double>(), n_out);
+  } else {
+    launch_trsm_lower_ex(s, m, n_out, B.as<double>(), m, alpha.as<double>(), n_out, 0, 0, nullptr);
+    launch_trsm_lower_ex(s, m, n_out, B.as<double>(), m, alpha.as<double>(), n_out, 1, 0, nullptr);
+  }
   hipLaunchKernelGGL(k_lml_fitc, dim3(n_out), dim3(256), 0, s, m, n, n_out, B.as<double>(),
                      dyn.as<double>(), lam.as<double>(), cvec.as<double>(), alpha.as<double>(),
                      g.alphaT.as<double>(), dlml.as<double>());
