@@ -774,7 +774,13 @@ static int sparse_fit(gpmpc_ctx *ctx, const double *Z, int m, const double *X, i
   launch_gram(s, GPMPC_SE_ARD, g.Xs.as<double>(), g.Xn.as<double>(), m, Xs.as<double>(),
               Xn.as<double>(), n, d, sigma2, 0.0, Kuf.as<double>(), n, 0);
   hipLaunchKernelGGL(k_eye, dim3((m + 255) / 256, m), dim3(256), 0, s, m, g.W.as<double>());
-  launch_trsm_lower_ex(s, m, m, Luu.as<double>(), m, g.W.as<double>(), m, 0, 1, nullptr);
+  {
+    DevBuf tinv;  // W = L_uu^-1 by the doubling inverse (exact fit's W, §10)
+    if (m > 128 && tinv.alloc(sizeof(double) * (size_t)m * m) == hipSuccess)
+      launch_tri_inverse(s, m, Luu.as<double>(), m, g.W.as<double>(), m, tinv.as<double>());
+    else
+      launch_trsm_lower_ex(s, m, m, Luu.as<double>(), m, g.W.as<double>(), m, 0, 1, nullptr);
+  }
   if (vfe) return vfe_tail(ctx, gp, Luu, Kuf, B, dinfo, Y, n, n_out, sigma2, noise, jitter, out,
                            y_mean, y_std, lml);
   launch_trsm_lower_ex(s, m, n, Luu.as<double>(), m, Kuf.as<double>(), n, 0, 0, nullptr);
