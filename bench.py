@@ -11,7 +11,8 @@ GP mean, OSQP-style ADMM (<= 50 iterations), plant step -- all device-resident.
 
 N > 1: one process per GPU (torch.distributed.run), landings sharded (weak
 scaling: a fixed fleet per GPU), no collective on the data path; the fleet
-records are gathered to rank 0 with one RCCL gather after the timed region.
+records are gathered to rank 0 with one RCCL gather after the timed region
+(the JSON's `gather` says which path ran and how many ranks it spanned).
 
 Prints ONE JSON line on rank 0.  ``value`` = landing control steps executed by
 all ranks / max-over-ranks wall time of the timed region.
@@ -398,25 +399,6 @@ def qp_status_histogram(fl, steps=10):
             "admm_iterations": iters}
 
 
-def gather_shard_records(ctx, d_records, host_records, total):
-    """The one collective: the C-ABI's ncclGather of the device
-    record arrays (gpmpc_gather_results).  GPMPC_GATHER=torch selects
-    torch.distributed.gather (also RCCL) instead; an error in the C-ABI path
-    falls back to it, so the records always reach rank 0."""
-    from gp_mpc_rocket_landing_amd.sharding import RCCLRecordGather, gather_records
-    if os.environ.get("GPMPC_GATHER", "rccl") != "torch":
-        try:
-            g = RCCLRecordGather(ctx)
-            try:
-                return g.gather(d_records, total)
-            finally:
-                g.close()
-        except Exception as e:  # noqa: BLE001
-            print(f"bench: C-ABI RCCL gather failed ({e}); torch.distributed.gather instead",
-                  file=sys.stderr, flush=True)
-    return gather_records(host_records, total, device="cuda")
-
-
 def gpmpc_loop_bench(ctx, gp, batch=1024, reps=3, sqp_iters=10):
     """GPMPC.solve's own loop on the fleet (gp_mpc.py:296-353; sqp_iters = 10,
     stop at 1e-4): every control step = up to 10 passes of GP posterior at the
@@ -485,6 +467,37 @@ def r6_admm_flops(N=30, nx=14, nu=3):
     it = 2 * 2 * nnz + kkt + 10 * (n + m)
     fac = (N + 1) * (2 * sz ** 3 + 2 * nx * sz * sz + 2 * nx * nx * sz + 2 * nx * sz * sz)
     return it, fac
+
+
+def rollouts6_qp_status(ctx, gv, gw, B, max_steps=300, **cfg):
+    """Fly B rollouts to termination one step at a time and histogram the status
+    of every QP solve (a solve without a solution ends its rollout)."""
+    from gp_mpc_rocket_landing_amd.rollouts6 import Rollouts6, initial_conditions_6dof
+    names = {1: "solved", 2: "solved_inaccurate", -2: "max_iter_reached", -3: "primal_infeasible",
+             3: "primal_infeasible_inaccurate", -4: "dual_infeasible", 4: "dual_infeasible_inaccurate",
+             -100: "kkt_factor_failed"}
+    ro = Rollouts6(ctx, gv, gw, B, max_steps=max_steps, **cfg)
+    hist = {}
+    try:
+        ro.reset(initial_conditions_6dof(B))
+        rec0, _ = ro.read()
+        for _ in range(max_steps + 1):
+            ro.step(1)
+            rec1, _ = ro.read()
+            failed = (rec1[:, 0] == 6) & ~np.isin(rec1[:, 14], (1, 2, -2))   # a solve without a solution
+            adv = (rec0[:, 0] == 0) & ((rec1[:, 1] > rec0[:, 1]) | failed)
+            for s_, c in zip(*np.unique(rec1[adv, 14].astype(int), return_counts=True)):
+                k = names.get(int(s_), str(int(s_)))
+                hist[k] = hist.get(k, 0) + int(c)
+            rec0 = rec1
+            if np.all(rec1[:, 0] != 0):
+                break
+    finally:
+        ro.close()
+    tot = max(1, sum(hist.values()))
+    return {"rollouts": B, "solves": tot, "status": hist, "status_frac": {k: round(v / tot, 4) for k, v in hist.items()},
+            "outcomes": {str(int(c)): int(np.sum(rec1[:, 0] == c)) for c in np.unique(rec1[:, 0])},
+            "admm_iters_per_solve": round(float(rec1[:, 11].sum()) / max(float(rec1[:, 1].sum()), 1.0), 2)}
 
 
 def rollouts6_bench(ctx, torch=None, batches=(64, 512), max_steps=300):
@@ -686,10 +699,16 @@ def main():
         tmax = t.clone(); dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
         tsum = t.clone(); dist.all_reduce(tsum, op=dist.ReduceOp.SUM)
         el_max, steps_all, iters_all = float(tmax[0]), float(tsum[1]), float(tsum[2])
-        all_rec = gather_shard_records(ctx, fl.records_dev, rec1, world * B)   # the one RCCL gather
     else:
         el_max, steps_all, iters_all = el, steps_done, admm_iters
-        all_rec = rec1
+    # the one collective, after the timed region: the C-ABI's RCCL gather of the device
+    # records (a communicator of one at N = 1).  A set-up failure on any rank is agreed by
+    # every rank and falls back to torch.distributed.gather together; `gather` records
+    # which path ran and how many ranks RCCL's communicator spanned.
+    from gp_mpc_rocket_landing_amd.sharding import gather_shard_records
+    all_rec, gather_info = gather_shard_records(ctx, fl.records_dev, rec1, world * B, device="cuda")
+    if rank == 0 and world == 1 and gather_info["path"] == "rccl" and not np.array_equal(all_rec, rec1):
+        raise RuntimeError("RCCL gather of a world of one does not reproduce the fleet records")
 
     if rank == 0:
         P = B * args.horizon
@@ -768,6 +787,7 @@ def main():
             "admm_iters_per_solve": round(iters_all / max(steps_all, 1.0), 2),
             "landing_steps_per_gpu_step": round(steps_done / K, 1),
         }
+        out["gather"] = gather_info
         if all_rec is not None:
             oc = all_rec[:, 0]
             out["outcomes"] = {str(int(c)): int(np.sum(oc == c)) for c in np.unique(oc)}

@@ -17,6 +17,7 @@ LIB_PATH = os.environ.get("GPMPC_LIB") or os.path.join(_HERE, "libgpmpc_hip.so")
 SE_ARD, SE_ISO, MATERN32, MATERN52 = 0, 1, 2, 3
 ERR_NOT_PD = -100
 REC_LEN = 16
+COMM_ID_BYTES = 128   # GPMPC_COMM_ID_BYTES (sizeof ncclUniqueId)
 # caps of the generic device QP (csrc/qp.h QP_NMAX, QP_MMAX, QP_NNZMAX)
 QP_NMAX, QP_MMAX, QP_NNZMAX = 216, 360, 896
 
@@ -72,7 +73,10 @@ class Rollout6Config(ctypes.Structure):
                 ("q_diag", ctypes.c_double * 14), ("p_diag", ctypes.c_double * 14),
                 ("r_diag", ctypes.c_double * 3), ("t_min", ctypes.c_double), ("t_max", ctypes.c_double),
                 ("tan_gamma_gs", ctypes.c_double), ("trust_x2", ctypes.c_double),
-                ("trust_u2", ctypes.c_double), ("use_gp_mean", ctypes.c_int), ("upright_target", ctypes.c_int)]
+                ("trust_u2", ctypes.c_double), ("use_gp_mean", ctypes.c_int), ("upright_target", ctypes.c_int),
+                ("rocket_j", ctypes.c_double * 3), ("rocket_r_t", ctypes.c_double * 3),
+                ("rocket_g_i", ctypes.c_double * 3), ("rocket_alpha", ctypes.c_double),
+                ("rocket_g0", ctypes.c_double)]
 
 
 class FleetConfig(ctypes.Structure):
@@ -139,11 +143,14 @@ _sig("gpmpc_rollout6_default_config", None, ctypes.POINTER(Rollout6Config))
 _sig("gpmpc_rollout6_create", _c, _vp, _vp, _vp, ctypes.POINTER(Rollout6Config), _c, ctypes.POINTER(_vp))
 _sig("gpmpc_rollout6_create_exact", _c, _vp, _vp, _vp, ctypes.POINTER(Rollout6Config), _c, ctypes.POINTER(_vp))
 _sig("gpmpc_rollout6_solve", _c, _vp, _dp, _dp, _c, _c, ctypes.c_double, _dp, _dp, _ip, _ip, _ip, _ip)
+_sig("gpmpc_rollout6_solve_ref", _c, _vp, _dp, _dp, _dp, _dp, _c, _c, ctypes.c_double, _dp, _dp, _ip, _ip, _ip,
+     _ip)
 _sig("gpmpc_rollout6_set_state", _c, _vp, _dp, _dp, _dp)
 _sig("gpmpc_rollout6_records_dev", _vp, _vp)
 _sig("gpmpc_comm_unique_id", _c, ctypes.c_char_p)
 _sig("gpmpc_comm_init", _c, _vp, ctypes.c_char_p, _c, _c, ctypes.POINTER(_vp))
 _sig("gpmpc_comm_destroy", _c, _vp)
+_sig("gpmpc_comm_count", _c, _vp, _ip)
 _sig("gpmpc_gather_results", _c, _vp, _vp, _vp, _ip, _c, _dp)
 _sig("gpmpc_rollout6_reset", _c, _vp, _c, _c, _dp)
 _sig("gpmpc_rollout6_step", _c, _vp, _c)
@@ -165,9 +172,9 @@ EXPORTED = ["gpmpc_abi_version", "gpmpc_last_error", "gpmpc_ctx_create", "gpmpc_
             "gpmpc_fleet_records_dev", "gpmpc_fleet_destroy", "gpmpc_rollout6_default_config",
             "gpmpc_rollout6_create", "gpmpc_rollout6_reset", "gpmpc_rollout6_step", "gpmpc_rollout6_read",
             "gpmpc_rollout6_get_state", "gpmpc_rollout6_destroy", "gpmpc_rollout6_create_exact",
-            "gpmpc_rollout6_solve", "gpmpc_rollout6_set_state", "gpmpc_fitc_get_state",
+            "gpmpc_rollout6_solve", "gpmpc_rollout6_solve_ref", "gpmpc_rollout6_set_state", "gpmpc_fitc_get_state",
             "gpmpc_rollout6_records_dev", "gpmpc_comm_unique_id", "gpmpc_comm_init", "gpmpc_comm_destroy",
-            "gpmpc_gather_results", "gpmpc_rollout6_step_phases", "gpmpc_vfe_fit"]
+            "gpmpc_comm_count", "gpmpc_gather_results", "gpmpc_rollout6_step_phases", "gpmpc_vfe_fit"]
 
 
 class HIPError(RuntimeError):
@@ -487,8 +494,8 @@ def fleet_default_config(**kw):
     _L.gpmpc_fleet_default_config(ctypes.byref(c))
     sq = kw.pop("sqp_qp", None)
     set_fields(c, kw, nested="qp")
-    c.sqp_qp = c.qp
-    if sq:
+    if sq:   # explicit pass settings on top of qp; otherwise max_iter 0 = "the same as qp"
+        c.sqp_qp = c.qp
         set_fields(c.sqp_qp, sq)
     return c
 

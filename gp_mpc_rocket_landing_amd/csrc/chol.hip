@@ -1512,8 +1512,8 @@ extern "C" int gpmpc_potrf(gpmpc_ctx *ctx, int n, double *A, int lda, int *info)
   GPMPC_HIP(hipSetDevice(ctx->device));
   hipStream_t s = ctx->stream;
   DevBuf dA, dinfo;
-  GPMPC_HIP(dA.alloc(sizeof(double) * (size_t)n * n));
-  GPMPC_HIP(dinfo.alloc(sizeof(int)));
+  GPMPC_HIP(dA.alloc(s, sizeof(double) * (size_t)n * n));
+  GPMPC_HIP(dinfo.alloc(s, sizeof(int)));
   GPMPC_HIP(hipMemcpy2DAsync(dA.p, sizeof(double) * n, A, sizeof(double) * lda,
                              sizeof(double) * n, n, hipMemcpyHostToDevice, s));
   GPMPC_HIP(launch_potrf_batched(s, n, 1, dA.as<double>(), n, 0, dinfo.as<int>()));
@@ -1521,7 +1521,21 @@ extern "C" int gpmpc_potrf(gpmpc_ctx *ctx, int n, double *A, int lda, int *info)
   GPMPC_HIP(hipMemcpy2DAsync(A, sizeof(double) * lda, dA.p, sizeof(double) * n,
                              sizeof(double) * n, n, hipMemcpyDeviceToHost, s));
   GPMPC_HIP(hipStreamSynchronize(s));
+  if (*info < 0) return gpmpc_potrf_info_error(*info, "potrf");
   return *info > 0 ? *info : 0;
+}
+
+// info > 0: the 1-based column of the first non-positive pivot (the reference's
+// LinAlgError); info < 0: the diagonal kernel's sweep timed out -- an error of this
+// library, reported as such and never as a pivot column
+int gpmpc_potrf_info_error(int info, const char *what) {
+  if (info < 0) {
+    gpmpc_set_error("%s: Cholesky diagonal-factor sweep timed out (internal invariant broken, "
+                    "factor unreliable)", what);
+    return -1;
+  }
+  gpmpc_set_error("Matrix is not positive definite (%s, column %d)", what, info);
+  return info;
 }
 
 extern "C" int gpmpc_potrf_batched_dev(gpmpc_ctx *ctx, int n, int batch, double *dA, int lda,
@@ -1540,8 +1554,8 @@ static int trsm_host(gpmpc_ctx *ctx, int n, int nrhs, const double *L, int ldl, 
   GPMPC_HIP(hipSetDevice(ctx->device));
   hipStream_t s = ctx->stream;
   DevBuf dL, dB;
-  GPMPC_HIP(dL.alloc(sizeof(double) * (size_t)n * n));
-  GPMPC_HIP(dB.alloc(sizeof(double) * (size_t)n * nrhs));
+  GPMPC_HIP(dL.alloc(s, sizeof(double) * (size_t)n * n));
+  GPMPC_HIP(dB.alloc(s, sizeof(double) * (size_t)n * nrhs));
   GPMPC_HIP(hipMemcpy2DAsync(dL.p, sizeof(double) * n, L, sizeof(double) * ldl,
                              sizeof(double) * n, n, hipMemcpyHostToDevice, s));
   GPMPC_HIP(hipMemcpy2DAsync(dB.p, sizeof(double) * nrhs, B, sizeof(double) * ldb,

@@ -23,6 +23,7 @@ struct RcclApi {
   ncclResult_t (*getUniqueId)(ncclUniqueId *) = nullptr;
   ncclResult_t (*commInitRank)(ncclComm_t *, int, ncclUniqueId, int) = nullptr;
   ncclResult_t (*commDestroy)(ncclComm_t) = nullptr;
+  ncclResult_t (*commCount)(const ncclComm_t, int *) = nullptr;
   ncclResult_t (*gather)(const void *, void *, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
   const char *(*errorString)(ncclResult_t) = nullptr;
   bool ok = false;
@@ -37,9 +38,10 @@ const RcclApi &rccl() {
     a.getUniqueId = (decltype(a.getUniqueId))dlsym(h, "ncclGetUniqueId");
     a.commInitRank = (decltype(a.commInitRank))dlsym(h, "ncclCommInitRank");
     a.commDestroy = (decltype(a.commDestroy))dlsym(h, "ncclCommDestroy");
+    a.commCount = (decltype(a.commCount))dlsym(h, "ncclCommCount");
     a.gather = (decltype(a.gather))dlsym(h, "ncclGather");
     a.errorString = (decltype(a.errorString))dlsym(h, "ncclGetErrorString");
-    a.ok = a.getUniqueId && a.commInitRank && a.commDestroy && a.gather && a.errorString;
+    a.ok = a.getUniqueId && a.commInitRank && a.commDestroy && a.commCount && a.gather && a.errorString;
     return a;
   }();
   return api;
@@ -101,6 +103,15 @@ extern "C" int gpmpc_comm_destroy(gpmpc_comm *c) {
   if (!c) return 0;
   if (c->comm && rccl().ok) (void)rccl().commDestroy(c->comm);
   delete c;
+  return 0;
+}
+
+// the number of ranks RCCL's communicator spans (ncclCommCount), so a caller can
+// record what the collective actually saw rather than what it asked for
+extern "C" int gpmpc_comm_count(gpmpc_comm *c, int *nranks) {
+  GPMPC_CHECK_ARG(c && c->comm && nranks);
+  GPMPC_RCCL_LOADED();
+  GPMPC_RCCL(rccl().commCount(c->comm, nranks));
   return 0;
 }
 

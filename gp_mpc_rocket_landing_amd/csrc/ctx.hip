@@ -38,6 +38,71 @@ void *gpmpc_scratch(hipStream_t s, int slot, size_t bytes) {
   return e.p;
 }
 
+// ---- per-stream caching pool (internal.h) ------------------------------------
+#include <vector>
+struct StreamPool {
+  std::map<size_t, std::vector<void *>> free;  // size class -> cached blocks
+  size_t cached = 0;
+};
+static std::mutex g_pool_mu;
+static std::map<hipStream_t, StreamPool> g_pool;
+static const size_t kPoolCapBytes = (size_t)8 << 30;  // per stream
+
+static size_t pool_class(size_t b) {
+  if (b <= 256) return 256;
+  size_t p2 = 256;
+  while (p2 < b) p2 <<= 1;
+  const size_t g = p2 >= 2048 ? p2 / 8 : 256;  // eighths of the power of two above
+  return (b + g - 1) / g * g;
+}
+
+void *gpmpc_pool_get(hipStream_t s, size_t bytes, size_t *cls) {
+  const size_t c = pool_class(bytes);
+  *cls = c;
+  {
+    std::lock_guard<std::mutex> lk(g_pool_mu);
+    StreamPool &sp = g_pool[s];
+    auto it = sp.free.find(c);
+    if (it != sp.free.end() && !it->second.empty()) {
+      void *p = it->second.back();
+      it->second.pop_back();
+      sp.cached -= c;
+      return p;
+    }
+  }
+  void *p = nullptr;
+  if (hipMalloc(&p, c) != hipSuccess) return nullptr;
+  return p;
+}
+
+void gpmpc_pool_put(hipStream_t s, void *p, size_t cls) {
+  if (!p) return;
+  bool live = false;
+  {
+    std::lock_guard<std::mutex> lk(g_pool_mu);
+    auto it = g_pool.find(s);
+    live = it != g_pool.end();
+    if (live && it->second.cached + cls <= kPoolCapBytes) {
+      it->second.free[cls].push_back(p);
+      it->second.cached += cls;
+      return;
+    }
+  }
+  // over the cap: let the stream's earlier readers finish first; a stream whose pool is
+  // gone was synchronised and destroyed with its context
+  if (live) (void)hipStreamSynchronize(s);
+  (void)hipFree(p);
+}
+
+static void pool_release(hipStream_t s) {
+  std::lock_guard<std::mutex> lk(g_pool_mu);
+  auto it = g_pool.find(s);
+  if (it == g_pool.end()) return;
+  for (auto &kv : it->second.free)
+    for (void *p : kv.second) (void)hipFree(p);
+  g_pool.erase(it);
+}
+
 static void scratch_release(hipStream_t s) {
   std::lock_guard<std::mutex> lk(g_scratch_mu);
   auto it = g_scratch.find(s);
@@ -73,6 +138,7 @@ extern "C" int gpmpc_ctx_destroy(gpmpc_ctx *ctx) {
   (void)hipSetDevice(ctx->device);
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
   if (ctx->stream) scratch_release(ctx->stream);
+  if (ctx->stream) pool_release(ctx->stream);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx;
   return 0;

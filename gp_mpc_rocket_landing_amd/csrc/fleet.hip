@@ -80,7 +80,8 @@ extern "C" void gpmpc_fleet_default_config(gpmpc_fleet_config *c) {
   gpmpc_qp_default_settings(&c->qp);
   c->sqp_iters = 1;          // RTI; > 1: GPMPC.solve's loop (gp_mpc.py:296-345)
   c->sqp_tol = 1e-4;         // gp_mpc.py:343
-  c->sqp_qp = c->qp;         // the SQP passes' QP settings (the same unless set)
+  c->sqp_qp = c->qp;         // the SQP passes' QP settings: max_iter 0 = "the same as qp",
+  c->sqp_qp.max_iter = 0;    // resolved at launch, so later edits of qp reach the passes too
 }
 
 // ---------------------------------------------------------------------------
@@ -1003,7 +1004,7 @@ __global__ __launch_bounds__(1024) void k_fleet_order(int B, const double *__res
 static FleetArgs fleet_args(gpmpc_fleet *f) {
   FleetArgs a;
   a.pt = f->pat.dev;
-  a.st = to_dev(f->cfg.sqp_iters > 1 ? f->cfg.sqp_qp : f->cfg.qp);
+  a.st = to_dev(f->cfg.sqp_iters > 1 && f->cfg.sqp_qp.max_iter > 0 ? f->cfg.sqp_qp : f->cfg.qp);
   a.N = f->N;
   a.target_mode = f->cfg.target_mode;
   a.use_gp = f->cfg.use_gp;

@@ -44,37 +44,38 @@
 #define R6_NX 14
 #define R6_NU 3
 #define R6_SZ 17
-#define R6_N 30
-#define R6_NBLK (R6_N + 1)
-#define R6_NV (R6_N * R6_SZ + R6_NX)          // 524 variables
-#define R6_MD (R6_NX * (R6_N + 1))            // 434 equality rows
-#define R6_MT R6_N                            // 30 thrust rows
-#define R6_MG (4 * (R6_N - 1))                // 116 glideslope rows
-#define R6_MGEN (R6_MT + R6_MG)               // 146 general rows
-#define R6_M (R6_MD + R6_NV + R6_MGEN)        // 1104 rows
+// the horizon N is a compile-time constant of the kernels (fully unrolled chains,
+// LDS layout): fleet6_n.h is compiled once per supported horizon, in namespaces
+// r6n20 (GPMPCConfig's N = 20, gp_mpc.py:110 / nominal_mpc.py:47) and r6n30
+// (BASELINE configs[4]); the C-ABI dispatches on the config's horizon
 #define R6_T 512                              // two items (variables / rows) per thread
 #define R6_TRI 153                            // packed lower 17 x 17
 #define R6_PT 512                             // predict threads (7 kernel-row waves + the RK4 wave)
 #define R6_FOR_H _Pragma("unroll") for (int h = 0; h < 2; ++h)
 
-// Rocket6DoFConfig (rocket_6dof.py:36-84), ConstraintParams (constraints.py:35-50),
-// CostWeights (cost_functions.py:39-98), gp_mpc.py trust regions (:432-435)
-#define R6_ALPHA (1.0 / 30.0)
+// ConstraintParams (constraints.py:35-50), CostWeights (cost_functions.py:39-98),
+// gp_mpc.py trust regions (:432-435)
 #define R6_T_MIN 0.5
 #define R6_T_MAX 5.0
 
-__device__ __constant__ double r6_J[3] = {0.02 * 0.168, 1.0 * 0.168, 1.0 * 0.168};
+// the rocket (Rocket6DoFConfig, rocket_6dof.py:36-84): diagonal J_B, thrust point
+// r_T_B, gravity g_I, alpha = 1 / (I_sp g0), g0 -- kernel arguments (uniform values)
+struct R6Rocket {
+  double J[3], rT[3], gI[3], alpha, g0;
+};
 
+struct R6Impl;  // the kernels of one horizon (fleet6_n.h), below
 struct gpmpc_rollout6 {
   gpmpc_ctx *ctx = nullptr;
   GpView gv{}, gw{};
   bool exact = false;  // the GP pair is exact (mean K* alpha over the training rows)
   gpmpc_rollout6_config cfg{};
-  int B = 0;
+  const R6Impl *impl = nullptr;
+  int B = 0, N = 0, M = 0;  // batch, horizon, QP rows
   DevBuf x, U, Xp, gm, Xo, ysc, rho, rec, lin, pending;
   DevBuf betav, betaw;  // (L_uu^-T alpha)^T of each GP, 3 x M
   DevBuf prm;           // problem data (R6_PRM doubles, r6_prm layout)
-  DevBuf xt, done, passes, qit, qst, xin;  // GPMPC.solve mode (gpmpc_rollout6_solve)
+  DevBuf xt, ut, done, passes, qit, qst, xin;  // GPMPC.solve mode: X_ref (B x (N+1) x 14), U_ref (B x N x 3)
 };
 
 // problem data in device memory (read per thread with a dynamic index, so not a
@@ -91,7 +92,7 @@ struct gpmpc_rollout6 {
 #define R6_PRM 36
 
 extern "C" void gpmpc_rollout6_default_config(gpmpc_rollout6_config *c) {
-  c->horizon = R6_N;   // BASELINE configs[4]: N = 30
+  c->horizon = 30;     // BASELINE configs[4]: N = 30
   c->dt = 0.1;
   c->max_steps = 300;
   gpmpc_qp_default_settings(&c->qp);   // osqp_rti.py:54-60 settings, as the 3-DoF path
@@ -108,6 +109,12 @@ extern "C" void gpmpc_rollout6_default_config(gpmpc_rollout6_config *c) {
   c->trust_u2 = 5.0;
   c->use_gp_mean = 1;
   c->upright_target = 0;
+  // Rocket6DoFConfig defaults (rocket_6dof.py:36-84)
+  c->rocket_j[0] = 0.02 * 0.168; c->rocket_j[1] = 1.0 * 0.168; c->rocket_j[2] = 1.0 * 0.168;
+  c->rocket_r_t[0] = -0.25; c->rocket_r_t[1] = 0.0; c->rocket_r_t[2] = 0.0;
+  c->rocket_g_i[0] = -1.0; c->rocket_g_i[1] = 0.0; c->rocket_g_i[2] = 0.0;
+  c->rocket_alpha = 1.0 / (30.0 * 1.0);  // I_sp 30, g0 1
+  c->rocket_g0 = 1.0;
 }
 
 // beta^T = alpha^T L_uu^-1 (3 x M): the FITC posterior mean is K*u beta.
@@ -123,44 +130,44 @@ __device__ __forceinline__ void r6_dcm(const double *q, double C[3][3]) {
   C[2][0] = 2 * (x * z - w * y); C[2][1] = 2 * (y * z + w * x); C[2][2] = 1 - 2 * (x * x + y * y);
 }
 
-__device__ void r6_f(const double *x, const double *u, double *o) {
+__device__ void r6_f(const R6Rocket &rk, const double *x, const double *u, double *o) {
   const double m = x[0];
   const double tm = sqrt(u[0] * u[0] + u[1] * u[1] + u[2] * u[2]);
   double C[3][3];
   r6_dcm(x + 7, C);
-  o[0] = -R6_ALPHA * tm;
+  o[0] = -rk.alpha * tm;
   o[1] = x[4]; o[2] = x[5]; o[3] = x[6];
-  const double gI[3] = {-1.0, 0.0, 0.0};
-  for (int i = 0; i < 3; ++i) o[4 + i] = (C[i][0] * u[0] + C[i][1] * u[1] + C[i][2] * u[2]) / m + gI[i];
+  for (int i = 0; i < 3; ++i) o[4 + i] = (C[i][0] * u[0] + C[i][1] * u[1] + C[i][2] * u[2]) / m + rk.gI[i];
   const double qw = x[7], qx = x[8], qy = x[9], qz = x[10], wx = x[11], wy = x[12], wz = x[13];
   o[7] = 0.5 * -((wx * qx + wy * qy) + wz * qz);
   o[8] = 0.5 * (qw * wx + (wy * qz - wz * qy));
   o[9] = 0.5 * (qw * wy + (wz * qx - wx * qz));
   o[10] = 0.5 * (qw * wz + (wx * qy - wy * qx));
-  // r_T x u with r_T = (-0.25, 0, 0); w x J w
-  const double tq[3] = {0.0 * u[2] - 0.0 * u[1], 0.0 * u[0] - (-0.25) * u[2], (-0.25) * u[1] - 0.0 * u[0]};
-  const double jw[3] = {r6_J[0] * wx, r6_J[1] * wy, r6_J[2] * wz};
+  // r_T x u; w x J w
+  const double *rT = rk.rT, *J = rk.J;
+  const double tq[3] = {rT[1] * u[2] - rT[2] * u[1], rT[2] * u[0] - rT[0] * u[2], rT[0] * u[1] - rT[1] * u[0]};
+  const double jw[3] = {J[0] * wx, J[1] * wy, J[2] * wz};
   const double cx[3] = {wy * jw[2] - wz * jw[1], wz * jw[0] - wx * jw[2], wx * jw[1] - wy * jw[0]};
-  for (int i = 0; i < 3; ++i) o[11 + i] = (tq[i] - cx[i]) / r6_J[i];
+  for (int i = 0; i < 3; ++i) o[11 + i] = (tq[i] - cx[i]) / J[i];
 }
 
 // RK4 (discretization.py:229-252) + quaternion normalisation (rocket_6dof.py:371-387)
-__device__ void r6_step(const double *x, const double *u, double dt, double *xn) {
+__device__ void r6_step(const R6Rocket &rk, const double *x, const double *u, double dt, double *xn) {
   double k1[R6_NX], k2[R6_NX], k3[R6_NX], k4[R6_NX], t[R6_NX];
-  r6_f(x, u, k1);
+  r6_f(rk, x, u, k1);
   for (int i = 0; i < R6_NX; ++i) t[i] = x[i] + dt * k1[i] / 2;
-  r6_f(t, u, k2);
+  r6_f(rk, t, u, k2);
   for (int i = 0; i < R6_NX; ++i) t[i] = x[i] + dt * k2[i] / 2;
-  r6_f(t, u, k3);
+  r6_f(rk, t, u, k3);
   for (int i = 0; i < R6_NX; ++i) t[i] = x[i] + dt * k3[i];
-  r6_f(t, u, k4);
+  r6_f(rk, t, u, k4);
   for (int i = 0; i < R6_NX; ++i) xn[i] = x[i] + (dt / 6) * (k1[i] + 2 * k2[i] + 2 * k3[i] + k4[i]);
   const double nq = sqrt(xn[7] * xn[7] + xn[8] * xn[8] + xn[9] * xn[9] + xn[10] * xn[10]);
   for (int i = 7; i < 11; ++i) xn[i] = xn[i] / nq;
 }
 
 // -[A_d | B_d] (A_d = I + A_c dt, B_d = B_c dt) into a zeroed 14 x 17 row-major block
-__device__ void r6_neg_lin(const double *x, const double *u, double dt, double *blk) {
+__device__ void r6_neg_lin(const R6Rocket &rk, const double *x, const double *u, double dt, double *blk) {
   auto set = [&](int i, int j, double v) { blk[i * R6_SZ + j] = v; };
   const double m = x[0], qw = x[7], qx = x[8], qy = x[9], qz = x[10], wx = x[11], wy = x[12], wz = x[13];
   const double u0 = u[0], u1 = u[1], u2 = u[2];
@@ -168,8 +175,8 @@ __device__ void r6_neg_lin(const double *x, const double *u, double dt, double *
   double C[3][3];
   r6_dcm(x + 7, C);
   for (int i = 0; i < R6_NX; ++i) set(i, i, -(1.0 + 0.0 * dt));
-  set(0, 14, -(-R6_ALPHA * u0 / tm * dt)); set(0, 15, -(-R6_ALPHA * u1 / tm * dt));
-  set(0, 16, -(-R6_ALPHA * u2 / tm * dt));
+  set(0, 14, -(-rk.alpha * u0 / tm * dt)); set(0, 15, -(-rk.alpha * u1 / tm * dt));
+  set(0, 16, -(-rk.alpha * u2 / tm * dt));
   for (int i = 0; i < 3; ++i) set(1 + i, 4 + i, -(1.0 * dt));
   for (int i = 0; i < 3; ++i) {
     const double cu = C[i][0] * u0 + C[i][1] * u1 + C[i][2] * u2;
@@ -191,16 +198,16 @@ __device__ void r6_neg_lin(const double *x, const double *u, double dt, double *
   const double Qw[4][3] = {{-qx, -qy, -qz}, {qw, qz, -qy}, {-qz, qw, qx}, {qy, -qx, qw}};
   for (int i = 0; i < 4; ++i)
     for (int j = 0; j < 3; ++j) set(7 + i, 11 + j, -(0.5 * Qw[i][j] * dt));
-  const double j1 = r6_J[0], j2 = r6_J[1], j3 = r6_J[2];
+  const double j1 = rk.J[0], j2 = rk.J[1], j3 = rk.J[2];
   const double Aw[3][3] = {{0, wz, wy}, {wz, 0, wx}, {wy, wx, 0}};
   const double cw[3] = {-(j3 - j2) / j1, -(j1 - j3) / j2, -(j2 - j1) / j3};
   for (int i = 0; i < 3; ++i)
     for (int j = 0; j < 3; ++j) set(11 + i, 11 + j, -((i == j ? 1.0 : 0.0) + cw[i] * Aw[i][j] * dt));
-  // B_c omega rows: J^-1 [r_T]x, r_T = (-0.25, 0, 0)
-  const double rx = -0.25, ry = 0.0, rz = 0.0;
+  // B_c omega rows: J^-1 [r_T]x
+  const double rx = rk.rT[0], ry = rk.rT[1], rz = rk.rT[2];
   const double Rx[3][3] = {{0, -rz, ry}, {rz, 0, -rx}, {-ry, rx, 0}};
   for (int i = 0; i < 3; ++i)
-    for (int j = 0; j < 3; ++j) set(11 + i, 14 + j, -(Rx[i][j] / r6_J[i] * dt));
+    for (int j = 0; j < 3; ++j) set(11 + i, 14 + j, -(Rx[i][j] / rk.J[i] * dt));
 }
 
 // ---------------------------------------------------------------------------
@@ -310,7 +317,9 @@ struct R6Args {
   // pass (forward simulation of U); 2 = later pass (GP means and Jacobians at the plan)
   int mode;
   double sqp_tol;
-  const double *xt;       // per-rollout target (B x 14)
+  const double *xt;       // GPMPC.solve: per-rollout X_ref (B x (N+1) x 14)
+  const double *ut;       // GPMPC.solve: per-rollout U_ref (B x N x 3)
+  R6Rocket rk;
   int *done, *passes, *qit, *qst;
 };
 
@@ -353,1292 +362,38 @@ __device__ __forceinline__ void r6_kernel_rows(const GpView &v, int M, const dou
   }
 }
 
-// diagnostic phase cycles of the predict kernel's rollout 0 (GPMPC_R6_STAMPS=1)
-__device__ unsigned long long g_r6p_stamps[4];
 
-// Per horizon point k (the points are sequential: X[k+1] needs the GP mean at X[k]):
-//   waves 0 .. R6_PT/64 - 2: the 2 x M kernel rows of both GPs (K*u . coefficients);
-//   the last wave, lane 0, meanwhile: RK4(X[k], U[k]) (the GP mean is added after);
-//   barrier; lanes 0 of waves 0 .. 5: the means, X[k+1] = RK4 + [.., d_v dt, .., d_w dt],
-//   then the six roles of point k+1's features (r6_features_role);
-//   barrier.
-template <bool ST>
-__global__ __launch_bounds__(R6_PT) void k_r6_predict(R6Args a) {
-  const int b = blockIdx.x, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  constexpr int NW = R6_PT / 64, NRT = R6_PT - 64;  // waves; kernel-row threads
-  unsigned long long tl = 0;
-  auto mark = [&](int k) {
-    if (ST && b == 0 && tid == 0) {
-      const unsigned long long t = __builtin_amdgcn_s_memtime();
-      if (k >= 0) g_r6p_stamps[k] += t - tl;
-      tl = t;
-    }
-  };
-  double *rec = a.rec + (int64_t)b * GPMPC_REC_LEN;
-  if (a.mode == 0 ? rec[0] != 0.0 : a.done[b] != 0) return;
-  __shared__ double X[R6_N + 1][R6_NX];
-  __shared__ double zq[2][16];
-  __shared__ double red[NW][6];
-  __shared__ double xrk[R6_NX];
-  __shared__ int s_out;
-  const double dt = a.dt;
-  const bool relin = a.mode == 2;  // a later GPMPC.solve pass: X_pred = the last plan
-  if (relin) {
-    for (int e = tid; e < (R6_N + 1) * R6_NX; e += R6_PT)
-      (&X[0][0])[e] = a.Xo[(int64_t)b * (R6_N + 1) * R6_NX + e];
-  } else if (tid < R6_NX) {
-    X[0][tid] = a.x[(int64_t)b * R6_NX + tid];
-  }
-  if (tid == 0) s_out = 0;
-  __syncthreads();
-  if (a.mode == 0 && tid == 0) {  // monte_carlo.py:458-488 on [m, r, v]; then any non-finite 6-DoF state
-    const double *x = X[0];
-    const double m0 = rec[13];
-    bool div7 = false, div = false;
-    for (int i = 0; i < 7; ++i) div7 = div7 || !(fabs(x[i]) <= 1e6);
-    for (int i = 0; i < R6_NX; ++i) div = div || !(fabs(x[i]) <= 1e6);
-    int out = 0;
-    if ((int)rec[1] >= a.max_steps) out = 5;
-    else if (x[1] < 0.0) out = 2;
-    else if (x[0] <= 1.0 + 0.01) out = 3;
-    else if (div7) out = 6;
-    else if (x[1] < 1.0 && fabs(x[4]) < 5.0) out = r6_landing_ok(x, m0) ? 1 : 4;
-    else if (div) out = 6;
-    if (out) {
-      rec[0] = out;
-      rec[2] = m0 - x[0];
-      for (int i = 0; i < 7; ++i) rec[4 + i] = x[i];
-    }
-    s_out = out;
-  }
-  __syncthreads();
-  if (s_out) return;
-  const double *Ub = a.U + (int64_t)b * R6_N * R6_NU;
-  const bool feat_lane = lane == 0 && wave < R6_FEAT_ROLES;
-  // features of point 0
-  if (a.use_gp && feat_lane) r6_features_role(wave, X[0], Ub, a.gv.ls, a.gw.ls, zq[0], zq[1]);
-  __syncthreads();
-  mark(-1);
-  for (int k = 0; k < R6_N; ++k) {
-    // K*u . coefficients of both GPs: the expansion form of the gram kernel (same
-    // bits per kernel value); 3 outputs each
-    double acc[6] = {0, 0, 0, 0, 0, 0};
-    if (tid < NRT) {
-      if (a.use_gp) {
-        r6_kernel_rows<13>(a.gv, a.Mv, a.cv, zq[0], tid, NRT, acc);
-        r6_kernel_rows<12>(a.gw, a.Mw, a.cw, zq[1], tid, NRT, acc + 3);
-      }
-#pragma unroll
-      for (int c = 0; c < 6; ++c)
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) acc[c] += __shfl_xor(acc[c], o);
-      if (lane == 0)
-#pragma unroll
-        for (int c = 0; c < 6; ++c) red[wave][c] = acc[c];
-    } else if (!relin && lane == 0) {  // _predict_with_gp's nominal step (gp_mpc.py:156)
-      double xn[R6_NX];
-      r6_step(X[k], Ub + k * R6_NU, dt, xn);
-      for (int i = 0; i < R6_NX; ++i) xrk[i] = xn[i];
-    }
-    __syncthreads();
-    mark(1);
-    if (feat_lane) {
-      double gmk[6];
-      for (int c = 0; c < 6; ++c) {
-        double sm = 0.0;
-        for (int w = 0; w < NW - 1; ++w) sm += red[w][c];
-        const GpView &v = c < 3 ? a.gv : a.gw;
-        gmk[c] = a.use_gp ? sm * v.ystd[c % 3] + v.ymean[c % 3] : 0.0;
-      }
-      double xn[R6_NX];
-      if (relin) {
-        for (int i = 0; i < R6_NX; ++i) xn[i] = X[k + 1][i];
-      } else {  // gp_mpc.py:166-168
-        for (int i = 0; i < R6_NX; ++i) xn[i] = xrk[i];
-        for (int i = 0; i < 3; ++i) { xn[4 + i] += gmk[i] * dt; xn[11 + i] += gmk[3 + i] * dt; }
-      }
-      if (wave == 0) {
-        for (int c = 0; c < 6; ++c) a.gm[((int64_t)b * R6_N + k) * 6 + c] = gmk[c];
-        if (!relin)
-          for (int i = 0; i < R6_NX; ++i) X[k + 1][i] = xn[i];
-      }
-      if (a.use_gp && k + 1 < R6_N)  // the next point's features, from this lane's own copy of X[k+1]
-        r6_features_role(wave, xn, Ub + (k + 1) * R6_NU, a.gv.ls, a.gw.ls, zq[0], zq[1]);
-    }
-    __syncthreads();
-    mark(0);
-  }
-  for (int e = tid; e < (R6_N + 1) * R6_NX; e += R6_PT)
-    a.Xp[(int64_t)b * (R6_N + 1) * R6_NX + e] = (&X[0][0])[e];
-  // linearisation at the simulated points (gp_mpc.py:303-304): -[A_d | B_d] per stage
-  double *lin = a.lin + (int64_t)b * R6_N * R6_NX * R6_SZ;
-  for (int e = tid; e < R6_N * R6_NX * R6_SZ; e += R6_PT) lin[e] = 0.0;
-  __syncthreads();
-  if (tid < R6_N) r6_neg_lin(X[tid], Ub + tid * R6_NU, dt, lin + tid * R6_NX * R6_SZ);
-}
-
-// ---------------------------------------------------------------------------
-// 2. QP + ADMM + plant
-struct R6Smem {
-  double Sinv[R6_NBLK * R6_TRI];      // packed lower S_k^-1 (D_k during the assembly)
-  double G[R6_N * R6_NX * R6_SZ];     // staged dynamics rows (scaled), then G_k = C_k S_k^-1
-  double rhs[R6_NBLK * R6_SZ];        // x~ right-hand side, forward chain y
-  double xs[R6_NBLK * R6_SZ];         // diagonal products u, backward chain x = x~
-  double w[R6_MD + R6_MGEN];          // rho z - y of equality + general rows (scratch at checks)
-  double E[R6_M];                     // row scaling
-  double dsc[R6_NV];                  // per-pass column scaling / factor scratch
-  double dpl[R6_MD];                  // each equality row's identity entry (scaled)
-  double gen[R6_MGEN * 3];            // general rows' values (scaled)
-  // per end of the twisted sweep (0 top, 1 bottom):
-  double T[2][2][R6_TRI];             // the swept block, packed lower (ping-pong: one barrier per step)
-  double Ct[2][R6_NX * R6_SZ];        // the coupling C_k (top) / E_k (bottom), 14 x 17
-  double Sch[2][R6_NX * R6_NX];       // G_k C_k^T / H_k E_k^T, the next block's update
-  double red[16][12];
-  double zero[R6_SZ];                 // the forward chain's operand row for its pass-through lanes
-  double zmid[16];                    // the bottom chain's z'_15 = -H_15 z_16
-  double dump[64];                    // the chains' store target for lanes that keep no result
-  double c, rho_s;
-  int flag, bad[2];
+// the kernels of one horizon, compiled per supported N (fleet6_n.h)
+struct R6Impl {
+  int N, M;
+  size_t smem;
+  hipError_t (*init)();
+  void (*predict)(hipStream_t, int B, const R6Args &, bool stamps);
+  void (*control)(hipStream_t, int B, const R6Args &, bool stamps);
+  void (*plant)(hipStream_t, int B, const R6Args &);
+  void (*reset)(hipStream_t, int first, int count, const double *x0, const R6Args &, double rho0);
+  void (*solve_begin)(hipStream_t, int B, const R6Args &, int cold, double rho0);
+  void (*print_stamps)();
 };
 
-__device__ __forceinline__ int r6_tri(int a, int b) { return a >= b ? a * (a + 1) / 2 + b : b * (b + 1) / 2 + a; }
+namespace r6n20 {
+#define R6_N 20
+#include "fleet6_n.h"
+#undef R6_N
+}  // namespace r6n20
+namespace r6n30 {
+#define R6_N 30
+#include "fleet6_n.h"
+#undef R6_N
+}  // namespace r6n30
 
-template <int K>
-__device__ __forceinline__ void r6_max(double (&v)[K], double (*red)[12]) {
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-#pragma unroll
-  for (int k = 0; k < K; ++k)
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v[k] = fmax(v[k], __shfl_xor(v[k], o));
-  __syncthreads();
-  if (lane == 0)
-#pragma unroll
-    for (int k = 0; k < K; ++k) red[wv][k] = v[k];
-  __syncthreads();
-#pragma unroll
-  for (int k = 0; k < K; ++k) {
-    double m = red[0][k];
-    for (int w = 1; w < R6_T / 64; ++w) m = fmax(m, red[w][k]);
-    v[k] = m;
-  }
-  __syncthreads();
-}
-
-template <int K>
-__device__ __forceinline__ void r6_sum(double (&v)[K], double (*red)[12]) {
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-#pragma unroll
-  for (int k = 0; k < K; ++k)
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v[k] += __shfl_xor(v[k], o);
-  __syncthreads();
-  if (lane == 0)
-#pragma unroll
-    for (int k = 0; k < K; ++k) red[wv][k] = v[k];
-  __syncthreads();
-#pragma unroll
-  for (int k = 0; k < K; ++k) {
-    double s = red[0][k];
-    for (int w = 1; w < R6_T / 64; ++w) s += red[w][k];
-    v[k] = s;
-  }
-  __syncthreads();
-}
-
-__device__ __forceinline__ double r6_rho(double l, double u, double rs) {
-  if (l < -QP_OSQP_INFTY * QP_MIN_SCALING && u > QP_OSQP_INFTY * QP_MIN_SCALING) return QP_RHO_MIN;
-  if (u - l < QP_RHO_TOL) return QP_RHO_EQ * rs;
-  return rs;
-}
-
-__device__ __forceinline__ void wave_sync() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-
-// general row g: its entries (count, variables, value slots)
-__device__ __forceinline__ int r6_gen_cols(int g, int *col) {
-  if (g < R6_MT) {
-    const int o = g * R6_SZ + R6_NX;
-    col[0] = o; col[1] = o + 1; col[2] = o + 2;
-    return 3;
-  }
-  const int gg = g - R6_MT, k = 1 + gg / 4, c = gg % 4;
-  col[0] = k * R6_SZ + 1;
-  col[1] = k * R6_SZ + (c < 2 ? 2 : 3);
-  return 2;
-}
-
-// the e-th general-row entry (e < 4) of variable (k, i) in row order: its
-// general row g and value slot sl; false past the variable's entries
-__device__ __forceinline__ bool r6_gen_slot(int k, int i, int e, int &g, int &sl) {
-  if (k < R6_N && i >= R6_NX) {  // thrust row k
-    g = k; sl = i - R6_NX;
-    return e == 0;
-  }
-  if (k >= 1 && k < R6_N && i >= 1 && i <= 3) {  // glideslope rows of stage k
-    const int g0 = R6_MT + 4 * (k - 1);
-    g = g0 + (i == 3 ? 2 : 0) + e;
-    sl = (i == 1) ? 0 : 1;
-    return e < (i == 1 ? 4 : 2);
-  }
-  g = 0; sl = 0;
-  return false;
-}
-
-struct R6Var {  // variable j and its bound row MD + j; general row j (< 146)
-  bool ok;
-  int j, k, i;
-  double x, dx, P, q, D, Ab, lb, ub, yb, zb, dyb, ztb;
-  // colA[0..13]: -A_d[:, i] / -B_d[:, i-14] of the dynamics rows of block k
-  // (scaled).  An equality-row thread (no variable) keeps its row here instead.
-  double colA[R6_SZ + 1];
-  bool gok;
-  int gn;
-  double gA[3], gl, gu, gy, gz, gdy;
-};
-// equality row r (x0 row r < 14, else dynamics row (k, i)).  Rows and variables
-// live on different threads, so the row's registers alias the variable slots.
-struct R6Row {
-  bool ok;
-  int r, k, i;
-  double (&A)[R6_SZ + 1];
-  double &ur, &yr, &zr, &dyr;
-  __device__ explicit R6Row(R6Var &V) : A(V.colA), ur(V.lb), yr(V.yb), zr(V.zb), dyr(V.dyb) {}
-};
-
-__device__ __forceinline__ int r6_eqid_row(int k, int i) { return k == 0 ? i : R6_NX + R6_NX * (k - 1) + i; }
-
-// (A' w)_j in row order: equality identity row, dynamics rows of block k, bound row, general rows
-__device__ __forceinline__ double r6_col_dot(const R6Smem &s, const R6Var &V, const double *wv, double wb,
-                                             const double *wg) {
-  double acc = 0.0;
-  if (V.i < R6_NX) {
-    const int r = r6_eqid_row(V.k, V.i);
-    acc += s.dpl[r] * wv[r];
-  }
-  if (V.k < R6_N) {
-    const double *wr = wv + R6_NX + R6_NX * V.k;
-#pragma unroll
-    for (int e = 0; e < R6_NX; ++e) acc += V.colA[e] * wr[e];
-  }
-  acc += V.Ab * wb;
-#pragma unroll
-  for (int e = 0; e < 4; ++e) {
-    int g, sl;
-    if (r6_gen_slot(V.k, V.i, e, g, sl)) acc += s.gen[g * 3 + sl] * wg[g];
-  }
-  return acc;
-}
-
-__device__ __forceinline__ double r6_row_dot(const R6Row &R, const double *v) {
-  if (R.r < R6_NX) return 0.0 + R.A[0] * v[R.r];
-  const double *vb = v + R.k * R6_SZ;
-  double acc = 0.0;
-#pragma unroll
-  for (int e = 0; e < R6_SZ; ++e) acc += R.A[e] * vb[e];
-  acc += R.A[R6_SZ] * v[(R.k + 1) * R6_SZ + R.i];
-  return acc;
-}
-__device__ __forceinline__ double r6_gen_dot(const R6Var &V, const double *v) {
-  int col[3];
-  const int n = r6_gen_cols(V.j, col);
-  double acc = 0.0;
-#pragma unroll
-  for (int e = 0; e < 3; ++e)
-    if (e < n) acc += V.gA[e] * v[col[e]];
-  return acc;
-}
-
-// The reduced KKT matrix M = P + sigma I + A' R A is block tridiagonal.  It is
-// factored from both ends at once (the 3-DoF fleet's twist, fleet_twist.h), in
-// 31 factor blocks of natural variables (r6_nat):
-//   top     k = 0..14:  the stage block [x_k, u_k], coupled to x_k+1 through
-//                       C_k (14 x 17: rho_eq dpl(k, i) g_k[i][:], stage k's dynamics rows);
-//   middle  k = 15:     x_15 alone (14 x 14);
-//   bottom  k = 16..30: [x_k, u_k-1], coupled to x_k-1 through E_k-1 (14 x 17:
-//                       x_k columns from stage k-1's dynamics rows, u_k-1
-//                       columns from stage k-1's x-u block).
-// Neither end's coupling reaches a block's entries 14-16 (u_k on top, u_k-1 at the
-// bottom), so the two ends are the same recursion, 15 block steps each:
-//   top     S_0 = D_0,   S_k+1 = D_k+1 - G_k C_k^T,      G_k = C_k S_k^-1
-//   bottom  T_30 = D_30, T_k-1 = D_k-1 - H_k-1 E_k-1^T,  H_k-1 = E_k-1 T_k^-1
-//   middle  Z = D_15 - G_14 C_14^T - H_15 E_15^T
-// -G_k goes to slot k (k < 15) and -H_k to slot k (k = 15..29) of s.G, over the
-// staged dynamics rows of its own stage once their last reader is done.
-#define R6_MID 15
-
-__device__ __forceinline__ int r6_nat(int k, int e) {
-  return k * R6_SZ + e - ((k > R6_MID && e >= R6_NX) ? R6_SZ : 0);
-}
-
-// M entry of variables (k, a) and (k, bb) of one stage, the terms in the banded oracle's row order
-__device__ __forceinline__ double r6_m_stage(const R6Smem &s, int k, int a, int bb, double re, double rs) {
-  double v = 0.0;
-  if (a == bb) {
-    v = s.dsc[k * R6_SZ + a];
-    if (a < R6_NX) {
-      const int r = r6_eqid_row(k, a);
-      v += re * s.dpl[r] * s.dpl[r];
-    }
-  }
-  if (k < R6_N) {
-    const double *g = s.G + k * R6_NX * R6_SZ;
-    for (int i = 0; i < R6_NX; ++i) v += re * g[i * R6_SZ + a] * g[i * R6_SZ + bb];
-  }
-  if (a == bb) v += s.xs[k * R6_SZ + a];
-#pragma unroll
-  for (int p = 0; p < 4; ++p) {
-    int g1, s1;
-    if (!r6_gen_slot(k, a, p, g1, s1)) continue;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      int g2, s2;
-      if (r6_gen_slot(k, bb, q, g2, s2) && g1 == g2) v += rs * s.gen[g1 * 3 + s1] * s.gen[g2 * 3 + s2];
-    }
-  }
-  return v;
-}
-// M entry of x_k+1[i] and (k, e): dynamics row (k, i) alone
-__device__ __forceinline__ double r6_m_next(const R6Smem &s, int k, int i, int e, double re) {
-  return (re * s.dpl[R6_NX + R6_NX * k + i]) * s.G[(k * R6_NX + i) * R6_SZ + e];
-}
-
-// (row, column) of packed-lower entry t
-__device__ __forceinline__ void r6_untri(int t, int &i, int &j) {
-  i = (int)((sqrt(8.0 * t + 1.0) - 1.0) * 0.5);
-  while (i * (i + 1) / 2 > t) --i;
-  while ((i + 1) * (i + 2) / 2 <= t) ++i;
-  j = t - i * (i + 1) / 2;
-}
-
-// The block inverse by the symmetric sweep operator on the packed lower triangle
-// (153 entries instead of Gauss-Jordan's 289: the block is SPD, so every
-// intermediate is symmetric), two pivots P = {p, p + 1} per barrier:
-//   W'[P][P] = -A^-1,  W'[i][P] = W[i][P] A^-1,  W'[i][j] = W[i][j] - W[i][P] A^-1 W[P][j]
-// with A = W[P][P]; after all pivots W = -S^-1.  Thread lt owns entry lt of T[0]
-// (one entry per thread); the result lands in T[return value].
-__device__ __forceinline__ int r6_sweep(double (*T)[R6_TRI], int lt, int nb, int kfail, int &bad) {
-  const bool own = lt < nb * (nb + 1) / 2;
-  int i = 0, j = 0;  // recomputed per call: kept live across the sweep loop they spilled more
-  if (own) r6_untri(lt, i, j);
-  int cb = 0;
-  for (int p = 0; p < nb; p += 2) {
-    const double *W = T[cb];
-    double v = 0.0;
-    if (p + 1 < nb) {
-      const double a = W[r6_tri(p, p)], b = W[r6_tri(p + 1, p)], d = W[r6_tri(p + 1, p + 1)];
-      const double det = fma(a, d, -(b * b));
-      if (!(a > 0.0 && det > 0.0) && !bad) bad = kfail;  // both pivots positive (uniform)
-      // 1/det by v_rcp_f64 + two Newton steps (blk_recip, within an ulp of the division)
-      const double rd = blk_recip(det);
-      const double ia = d * rd, ib = -b * rd, id = a * rd;  // A^-1 = [ia ib; ib id]
-      if (own) {
-        const double wij = W[lt];
-        const double wip = W[r6_tri(i, p)], wiq = W[r6_tri(i, p + 1)];
-        const double wjp = W[r6_tri(j, p)], wjq = W[r6_tri(j, p + 1)];
-        const int di = i - p, dj = j - p;  // i >= j
-        const bool ip = di == 0 || di == 1, jp = dj == 0 || dj == 1;
-        if (ip && jp) v = -(di + dj == 0 ? ia : (di + dj == 1 ? ib : id));
-        else if (jp) v = dj == 0 ? wip * ia + wiq * ib : wip * ib + wiq * id;  // W[i][P] A^-1
-        else if (ip) v = di == 0 ? ia * wjp + ib * wjq : ib * wjp + id * wjq;  // A^-1 W[P][j]
-        else v = wij - ((wip * ia + wiq * ib) * wjp + (wip * ib + wiq * id) * wjq);
-      }
-    } else {
-      const double d = W[r6_tri(p, p)];
-      if (!(d > 0.0) && !bad) bad = kfail;
-      const double inv = blk_recip(d);
-      if (own) {
-        const double wij = W[lt], wip = W[r6_tri(i, p)], wjp = W[r6_tri(j, p)];
-        if (i == p && j == p) v = -inv;
-        else if (j == p) v = wip * inv;
-        else if (i == p) v = wjp * inv;
-        else v = wij - (wip * inv) * wjp;
-      }
-    }
-    if (own) T[cb ^ 1][lt] = v;
-    cb ^= 1;
-    __syncthreads();
-  }
-  return cb;
-}
-
-// assemble M and factor it: returns 0 or a failing block + 1
-template <class MK>
-__device__ __forceinline__ int r6_factor(R6Smem &s, R6Var (&V)[2], R6Row (&R)[2], double sigma, MK &mark) {
-  const int tid = threadIdx.x;
-  const double rs = s.rho_s, re = QP_RHO_EQ * rs;
-  // stage: dynamics rows' block values, per-variable P + sigma and bound terms
-  R6_FOR_H {
-    if (R[h].ok && R[h].r >= R6_NX)
-#pragma unroll
-      for (int e = 0; e < R6_SZ; ++e) s.G[(R[h].k * R6_NX + R[h].i) * R6_SZ + e] = R[h].A[e];
-    if (V[h].ok) {
-      s.dsc[V[h].j] = V[h].P + sigma;
-      s.xs[V[h].j] = r6_rho(V[h].lb, V[h].ub, rs) * V[h].Ab * V[h].Ab;
-    }
-  }
-  __syncthreads();
-  // the 31 diagonal blocks, packed lower
-  for (int e = tid; e < R6_NBLK * R6_TRI; e += R6_T) {
-    const int k = e / R6_TRI, t = e - k * R6_TRI;
-    int a = (int)((sqrt(8.0 * t + 1.0) - 1.0) * 0.5);
-    while (a * (a + 1) / 2 > t) --a;
-    while ((a + 1) * (a + 2) / 2 <= t) ++a;
-    const int bb = t - a * (a + 1) / 2;
-    const int nb = (k == R6_MID) ? R6_NX : R6_SZ;
-    double v = 0.0;
-    if (a < nb) {
-      if (k <= R6_MID || a < R6_NX) v = r6_m_stage(s, k, a, bb, re, rs);  // bb <= a
-      else if (bb >= R6_NX) v = r6_m_stage(s, k - 1, a, bb, re, rs);      // u_k-1 with u_k-1
-      else v = r6_m_next(s, k - 1, bb, a, re);                             // x_k[bb] with u_k-1
-    } else if (a == bb) {
-      v = 1.0;  // unused tail of the middle block
-    }
-    s.Sinv[e] = v;
-  }
-  __syncthreads();
-  mark(2);  // (stamps: the assembly)
-  // the sweep: threads 0-255 the top end, 256-511 the bottom end.  The pivot
-  // steps read one copy of the block and write the other, so a step needs one
-  // workgroup barrier instead of two.
-  const int half = tid >> 8, lt = tid & 255;
-  int bad = 0;
-  for (int t = 0; t < R6_MID; ++t) {
-    const int k = half ? R6_N - t : t;    // factor block
-    const int kc = half ? k - 1 : k;      // its coupling's slot
-    double (*T)[R6_TRI] = s.T[half];
-    if (lt < R6_TRI) {
-      int ti, tj;
-      r6_untri(lt, ti, tj);
-      double v = s.Sinv[k * R6_TRI + lt];
-      if (t > 0 && ti < R6_NX) v -= s.Sch[half][ti * R6_NX + tj];  // tj <= ti
-      T[0][lt] = v;
-    }
-    if (lt < R6_NX * R6_SZ) {  // top C_k[i][c]: x_k+1[i] with (k, c); bottom E_k-1[i][c]: x_k-1[i] with entry c of block k
-      const int i = lt / R6_SZ, c = lt - i * R6_SZ;
-      double v;
-      if (!half) v = r6_m_next(s, k, i, c, re);
-      else if (c < R6_NX) v = r6_m_next(s, k - 1, c, i, re);
-      else v = r6_m_stage(s, k - 1, i, c, re, rs);
-      s.Ct[half][lt] = v;
-    }
-    __syncthreads();
-    const int cb = r6_sweep(T, lt, R6_SZ, k + 1, bad);  // W = -S_k^-1; bad: uniform over the half
-    if (lt < R6_TRI) s.Sinv[k * R6_TRI + lt] = -T[cb][lt];
-    mark(10);
-    // -G_k = -C_k S_k^-1 = C_k W / -H_k-1 over the staged rows of its slot
-    double *Gs = s.G + kc * R6_NX * R6_SZ;
-    if (lt < R6_NX * R6_SZ) {
-      const int i = lt / R6_SZ, c = lt - i * R6_SZ;
-      double acc = 0.0;
-      for (int e = 0; e < R6_SZ; ++e) acc += s.Ct[half][i * R6_SZ + e] * T[cb][r6_tri(e, c)];
-      Gs[lt] = acc;  // stored negated: the chains accumulate
-    }
-    __syncthreads();
-    if (lt < R6_NX * R6_NX) {  // the next block's update G_k C_k^T / H_k-1 E_k-1^T (14 x 14)
-      const int i = lt / R6_NX, i2 = lt - i * R6_NX;
-      double acc = 0.0;
-      for (int e = 0; e < R6_SZ; ++e) acc += Gs[i * R6_SZ + e] * s.Ct[half][i2 * R6_SZ + e];
-      s.Sch[half][lt] = -acc;
-    }
-    __syncthreads();
-    mark(11);
-  }
-  // the middle block Z = D_15 - G_14 C_14^T - H_15 E_15^T, 14 wide (packed: the first 105)
-  double (*T)[R6_TRI] = s.T[0];
-  constexpr int MT = R6_NX * (R6_NX + 1) / 2;
-  if (tid < MT) {
-    int mi, mj;
-    r6_untri(tid, mi, mj);
-    T[0][tid] = (s.Sinv[R6_MID * R6_TRI + tid] - s.Sch[0][mi * R6_NX + mj]) - s.Sch[1][mi * R6_NX + mj];
-  }
-  __syncthreads();
-  const int cb = r6_sweep(T, tid, R6_NX, R6_MID + 1, bad);
-  if (tid < R6_TRI) s.Sinv[R6_MID * R6_TRI + tid] = tid < MT ? -T[cb][tid] : 0.0;
-  if (lt == 0) s.bad[half] = bad;
-  __syncthreads();
-  mark(10);
-  return s.bad[0] ? s.bad[0] : s.bad[1];
-}
-
-// u = S_k^-1 y_k, row a of factor block k (the middle block on y_15 + z'_15)
-__device__ __forceinline__ void r6_diag_row(R6Smem &s, int k, int a) {
-  const int e = k * R6_SZ + a;
-  const int nb = (k == R6_MID) ? R6_NX : R6_SZ;
-  if (a < nb) {
-    const double *S = s.Sinv + k * R6_TRI;
-    const double *y = s.rhs + k * R6_SZ;
-    const int lo = k > R6_MID ? R6_SZ : 0;   // a bottom block's u_k-1 one block down
-    const bool mid = k == R6_MID;
-    // unrolled over the 17 entries (the middle block's 3 masked) in three chunks
-    // of loads in flight (a runtime-count loop waited on each pair; all 17 at
-    // once spilled the items' registers)
-    double acc0 = 0.0, acc1 = 0.0;
-#pragma unroll
-    for (int c0 = 0; c0 < R6_SZ; c0 += 6) {
-      double sv[6], yv[6];
-#pragma unroll
-      for (int q = 0; q < 6; ++q) {
-        const int bb = c0 + q < R6_SZ ? c0 + q : R6_SZ - 1;
-        sv[q] = S[r6_tri(a, bb)];
-        yv[q] = y[bb >= R6_NX ? bb - lo : bb];
-        if (bb < R6_NX && mid) yv[q] += s.zmid[bb];
-      }
-#pragma unroll
-      for (int q = 0; q < 6; ++q) {
-        const int bb = c0 + q;
-        if (bb >= R6_SZ) continue;
-        if (bb & 1) acc1 = bb < nb ? fma(sv[q], yv[q], acc1) : acc1;
-        else acc0 = bb < nb ? fma(sv[q], yv[q], acc0) : acc0;
-      }
-      asm volatile("" ::: "memory");
-    }
-    s.xs[a >= R6_NX ? e - lo : e] = acc0 + acc1;
+static const R6Impl *r6_impl(int N) {
+  switch (N) {
+    case 20: return &r6n20::impl;
+    case 30: return &r6n30::impl;
+    default: return nullptr;
   }
 }
-
-// the sum of a lane's value and its partner's in the other row of its row pair
-// (rows 0/1, 2/3): v_permlane16_swap on both halves, one add; both rows get the
-// same bits (the add commutes)
-__device__ __forceinline__ double pair_sum(double v) {
-  const unsigned lo = __double2loint(v), hi = __double2hiint(v);
-  const auto l = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
-  const auto h = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
-  return __hiloint2double(h[0], l[0]) + __hiloint2double(h[1], l[1]);
-}
-// rows 1 and 3 rotated by 8 lanes (DPP row_ror:8 on both halves); rows 0, 2 unchanged
-__device__ __forceinline__ double ror8_odd(double v) {
-  const int lo = __double2loint(v), hi = __double2hiint(v);
-  const int l = __builtin_amdgcn_update_dpp(lo, lo, 0x128, 0xa, 0xf, false);
-  const int h = __builtin_amdgcn_update_dpp(hi, hi, 0x128, 0xa, 0xf, false);
-  return __hiloint2double(h, l);
-}
-
-// x~ = M^-1 rhs, twisted: the forward chains (wave 0: y down the top blocks to
-// y_15; wave 1: z up the bottom blocks, then z'_15 = -H_15 z_16), the 31 diagonal
-// products (the middle on y_15 + z'_15), the backward chains (wave 0: x_14 .. x_0
-// from x_15; wave 1: blocks 16 .. 30 from x_15).  The chains carry their vector
-// in registers and broadcast it with DPP row_newbcast inside the FMA (qp_block.h
-// fmac_bc), as the 3-DoF fleet does; blocks are 17 wide and a DPP row 16:
-//   forward  row 0, lane i < 14: entry i of the next block; lanes 14, 15 carry
-//            the block's entries 14, 15 (which no coupling reaches) through zero
-//            operands, and entry 16's term goes into the init off the chain.
-//   backward lanes 0-15 compute entries 0-15, lanes 16-29 replicate entries
-//            0-13 (so row 1 broadcasts the same x) and lane 30 computes entry 16.
-// Both ends run the same instruction stream; a bottom block's entries 14-16
-// (u_k-1) sit 17 below its x_k in the natural order (offsets rr - 17).
-template <class MK>
-__device__ __forceinline__ void r6_solve(R6Smem &s, MK &mark) {
-  const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
-  if (wv < 2) {
-    // Two DPP rows per end: row h = 0 takes terms 0-7 and row 1 terms 8-15 of the
-    // 16 on the chain, row 1 holding the vector rotated by 8 lanes so that its
-    // broadcasts 0-7 reach entries 8-15; the pair sum (v_permlane16_swap) gives both
-    // rows the new entry and row 1 rotates it back.  Half the dependent FMAs and half
-    // the operand reads per block step.  Rows 2 and 3 repeat rows 0 and 1.
-    // Every term's operand pair for the NEXT step loads right after the pair's FMAs.
-    const bool bot = wv == 1;
-    const int m = lane & 15, h = (lane >> 4) & 1;
-    const int ms = h ? (m + 8) & 15 : m;  // the entry this lane's vector register holds
-    const bool pass = m >= R6_NX;         // output m: a pass-through entry (14, 15)
-    auto offo = [&](int e) { return (bot && e >= R6_NX) ? e - R6_SZ : e; };
-    const int o16 = bot ? -1 : R6_SZ - 1;
-    const int db = bot ? -R6_SZ : R6_SZ;
-    const int gs = pass ? 0 : (bot ? -R6_NX * R6_SZ : R6_NX * R6_SZ);
-    const double *F = s.G;
-    int go = pass ? (int)(s.zero - s.G) : (bot ? R6_N - 1 : 0) * R6_NX * R6_SZ + m * R6_SZ;
-    const int gh = 8 * h;
-    int ib = bot ? R6_N * R6_SZ : 0;
-    double g[8];
-#pragma unroll
-    for (int e = 0; e < 8; ++e) g[e] = F[go + gh + e];
-    double g16 = F[go + R6_SZ - 1];
-    double y = s.rhs[ib + offo(ms)];
-    double b16 = s.rhs[ib + o16], bn = s.rhs[ib + db + offo(m)];
-#pragma unroll 3
-    for (int t = 0; t < R6_MID; ++t) {
-      const bool last = t == R6_MID - 1;
-      const int gn = go + gs;
-      const double init = h ? 0.0 : fma(g16, b16, (bot && last) ? 0.0 : bn);
-      b16 = s.rhs[ib + db + o16];
-      bn = s.rhs[ib + 2 * db + offo(m)];
-      g16 = F[gn + R6_SZ - 1];
-      double a0 = init, a1 = 0.0;
-      fmac_bc<0, true>(a0, y, g[0]); fmac_bc<1, false>(a1, y, g[1]);
-      g[0] = F[gn + gh + 0]; g[1] = F[gn + gh + 1];
-      fmac_bc<2, false>(a0, y, g[2]); fmac_bc<3, false>(a1, y, g[3]);
-      g[2] = F[gn + gh + 2]; g[3] = F[gn + gh + 3];
-      fmac_bc<4, false>(a0, y, g[4]); fmac_bc<5, false>(a1, y, g[5]);
-      g[4] = F[gn + gh + 4]; g[5] = F[gn + gh + 5];
-      fmac_bc<6, false>(a0, y, g[6]); fmac_bc<7, false>(a1, y, g[7]);
-      g[6] = F[gn + gh + 6]; g[7] = F[gn + gh + 7];
-      const double sum = pair_sum(a0 + a1);  // entry m of the next block, on both rows
-      y = ror8_odd(sum);
-      // unconditional store (pass-through and idle lanes to the dump): no
-      // exec-mask branch in the loop, so the LDS wait at the next step is exact
-      double *dst = (!pass && lane < 16) ? ((bot && last) ? &s.zmid[m] : &s.rhs[ib + db + m]) : &s.dump[lane];
-      *dst = sum;
-      go = gn;
-      ib += db;
-      // the two ends walk in opposite directions, so a step's address is no
-      // immediate offset from one base; left visible, the compiler hoists every
-      // step's address out of the ADMM loop as a live register
-      asm volatile("" : "+v"(ib), "+v"(go));
-    }
-  }
-  __syncthreads();
-  mark(4);
-  for (int e = tid; e < R6_NBLK * R6_SZ; e += R6_T) r6_diag_row(s, e / R6_SZ, e % R6_SZ);
-  __syncthreads();
-  mark(5);
-  if (wv < 2) {
-    const bool bot = wv == 1;
-    // entry a of lane (0-15: a = lane, 16-29: a = lane - 16, 30: 16); lanes >= 31
-    // compute entry 16 too and drop it
-    const int a = lane < 16 ? lane : (lane < 30 ? lane - 16 : R6_SZ - 1);
-    const bool st = lane < 16 || lane == 30;
-    const int off = (bot && a >= R6_NX) ? a - R6_SZ : a;
-    // top: blocks 14 .. 0 (slots 14 .. 0); bottom: blocks 16 .. 30 (slots 15 .. 29)
-    const int gs = bot ? R6_NX * R6_SZ : -R6_NX * R6_SZ;
-    const int db = bot ? R6_SZ : -R6_SZ;
-    const double *F = s.G;
-    int go = (R6_MID - (bot ? 0 : 1)) * R6_NX * R6_SZ + a;
-    int ib = (bot ? R6_MID + 1 : R6_MID - 1) * R6_SZ;
-    double g[R6_NX];
-#pragma unroll
-    for (int i = 0; i < R6_NX; ++i) g[i] = F[go + i * R6_SZ];
-    double x = a < R6_NX ? s.xs[R6_MID * R6_SZ + a] : 0.0;
-    double u = s.xs[ib + off];
-#pragma unroll 3
-    for (int t = 0; t < R6_MID; ++t) {
-      const int gn = min(max(go + gs, a), (R6_N - 1) * R6_NX * R6_SZ + a);
-      double a0 = u, a1 = 0.0;
-      u = s.xs[min(max(ib + db, 0), R6_N * R6_SZ) + off];
-      fmac_bc<0, true>(a0, x, g[0]); fmac_bc<1, false>(a1, x, g[1]);
-      g[0] = F[gn + 0 * R6_SZ]; g[1] = F[gn + 1 * R6_SZ];
-      fmac_bc<2, false>(a0, x, g[2]); fmac_bc<3, false>(a1, x, g[3]);
-      g[2] = F[gn + 2 * R6_SZ]; g[3] = F[gn + 3 * R6_SZ];
-      fmac_bc<4, false>(a0, x, g[4]); fmac_bc<5, false>(a1, x, g[5]);
-      g[4] = F[gn + 4 * R6_SZ]; g[5] = F[gn + 5 * R6_SZ];
-      fmac_bc<6, false>(a0, x, g[6]); fmac_bc<7, false>(a1, x, g[7]);
-      g[6] = F[gn + 6 * R6_SZ]; g[7] = F[gn + 7 * R6_SZ];
-      fmac_bc<8, false>(a0, x, g[8]); fmac_bc<9, false>(a1, x, g[9]);
-      g[8] = F[gn + 8 * R6_SZ]; g[9] = F[gn + 9 * R6_SZ];
-      fmac_bc<10, false>(a0, x, g[10]); fmac_bc<11, false>(a1, x, g[11]);
-      g[10] = F[gn + 10 * R6_SZ]; g[11] = F[gn + 11 * R6_SZ];
-      fmac_bc<12, false>(a0, x, g[12]); fmac_bc<13, false>(a1, x, g[13]);
-      g[12] = F[gn + 12 * R6_SZ]; g[13] = F[gn + 13 * R6_SZ];
-      x = a0 + a1;
-      *(st ? &s.xs[ib + off] : &s.dump[lane]) = x;
-      go = gn;
-      ib += db;
-      asm volatile("" : "+v"(ib), "+v"(go));
-    }
-  }
-  __syncthreads();
-  mark(6);
-}
-
-// residual norms (auxil.c update_info) + the rho-estimate quantities (as fq_update_info)
-__device__ __forceinline__ void r6_update_info(R6Smem &s, R6Var (&V)[2], R6Row (&R)[2], double (&o)[8],
-                                               double (&re_)[4]) {
-  R6_FOR_H {
-    if (V[h].ok) s.rhs[V[h].j] = V[h].x;
-    if (R[h].ok) s.w[R[h].r] = R[h].yr;
-    if (V[h].gok) s.w[R6_MD + V[h].j] = V[h].gy;
-  }
-  __syncthreads();
-  double v[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-  auto row = [&](double ax, double z, double e) {
-    v[0] = fmax(v[0], fabs((ax - z) / e));
-    v[1] = fmax(v[1], fabs(z / e));
-    v[2] = fmax(v[2], fabs(ax / e));
-    v[8] = fmax(v[8], fabs(ax - z));
-    v[9] = fmax(v[9], fmax(fabs(z), fabs(ax)));
-  };
-  R6_FOR_H {
-    R6Var &W = V[h];
-    if (R[h].ok) row(r6_row_dot(R[h], s.rhs), R[h].zr, s.E[R[h].r]);
-    if (W.ok) {
-      row(0.0 + W.Ab * W.x, W.zb, s.E[R6_MD + W.j]);
-      const double aty = r6_col_dot(s, W, s.w, W.yb, s.w + R6_MD);
-      const double px = W.P * W.x, d = W.D, q = W.q;
-      v[3] = fmax(v[3], fabs((q + px + aty) / d));
-      v[4] = fmax(v[4], fabs(q / d));
-      v[5] = fmax(v[5], fabs(aty / d));
-      v[6] = fmax(v[6], fabs(px / d));
-      v[10] = fmax(v[10], fabs(q + px + aty));
-      v[11] = fmax(v[11], fmax(fmax(fabs(q), fabs(aty)), fabs(px)));
-    }
-    if (W.gok) row(r6_gen_dot(W, s.rhs), W.gz, s.E[R6_MD + R6_NV + W.j]);
-  }
-  r6_max<12>(v, s.red);
-#pragma unroll
-  for (int k = 0; k < 8; ++k) o[k] = v[k];
-#pragma unroll
-  for (int k = 0; k < 4; ++k) re_[k] = v[8 + k];
-}
-
-__device__ __forceinline__ double r6_proj(double d, double l, double u) {
-  const bool bu = u > QP_OSQP_INFTY * QP_MIN_SCALING, bl = l < -QP_OSQP_INFTY * QP_MIN_SCALING;
-  if (bu && bl) return 0.0;
-  if (bu) return fmin(d, 0.0);
-  if (bl) return fmax(d, 0.0);
-  return d;
-}
-
-__device__ __forceinline__ bool r6_primal_infeasible(R6Smem &s, R6Var (&V)[2], R6Row (&R)[2], double eps) {
-  double v[1] = {0.0};
-  R6_FOR_H {
-    R6Var &W = V[h];
-    R6Row &Q = R[h];
-    if (Q.ok) { Q.dyr = r6_proj(Q.dyr, Q.ur, Q.ur); v[0] = fmax(v[0], fabs(s.E[Q.r] * Q.dyr)); }
-    if (W.ok) { W.dyb = r6_proj(W.dyb, W.lb, W.ub); v[0] = fmax(v[0], fabs(s.E[R6_MD + W.j] * W.dyb)); }
-    if (W.gok) { W.gdy = r6_proj(W.gdy, W.gl, W.gu); v[0] = fmax(v[0], fabs(s.E[R6_MD + R6_NV + W.j] * W.gdy)); }
-  }
-  r6_max<1>(v, s.red);
-  const double nrm = v[0];
-  if (!(nrm > QP_DIV_TOL)) return false;
-  double sm[1] = {0.0};
-  R6_FOR_H {
-    R6Var &W = V[h];
-    R6Row &Q = R[h];
-    if (Q.ok) sm[0] += Q.ur * fmax(Q.dyr, 0.0) + Q.ur * fmin(Q.dyr, 0.0);
-    if (W.ok) sm[0] += W.ub * fmax(W.dyb, 0.0) + W.lb * fmin(W.dyb, 0.0);
-    if (W.gok) sm[0] += W.gu * fmax(W.gdy, 0.0) + W.gl * fmin(W.gdy, 0.0);
-  }
-  r6_sum<1>(sm, s.red);
-  if (!(sm[0] < -eps * nrm)) return false;
-  R6_FOR_H {
-    if (R[h].ok) s.w[R[h].r] = R[h].dyr;
-    if (V[h].gok) s.w[R6_MD + V[h].j] = V[h].gdy;
-  }
-  __syncthreads();
-  double mx[1] = {0.0};
-  R6_FOR_H {
-    if (V[h].ok) mx[0] = fmax(mx[0], fabs(r6_col_dot(s, V[h], s.w, V[h].dyb, s.w + R6_MD) / V[h].D));
-  }
-  r6_max<1>(mx, s.red);
-  return mx[0] < eps * nrm;
-}
-
-__device__ __forceinline__ bool r6_dual_infeasible(R6Smem &s, R6Var (&V)[2], R6Row (&R)[2], double eps) {
-  double v[1] = {0.0};
-  R6_FOR_H {
-    if (V[h].ok) v[0] = fmax(v[0], fabs(V[h].D * V[h].dx));
-  }
-  r6_max<1>(v, s.red);
-  const double nrm = v[0];
-  if (!(nrm > QP_DIV_TOL)) return false;
-  double a[1] = {0.0}, pm[1] = {0.0};
-  R6_FOR_H {
-    if (V[h].ok) { a[0] += V[h].q * V[h].dx; pm[0] = fmax(pm[0], fabs(V[h].P * V[h].dx / V[h].D)); }
-  }
-  r6_sum<1>(a, s.red);
-  r6_max<1>(pm, s.red);
-  if (!(a[0] < s.c * eps * nrm)) return false;
-  if (!(pm[0] < s.c * eps * nrm)) return false;
-  R6_FOR_H {
-    if (V[h].ok) s.rhs[V[h].j] = V[h].dx;
-  }
-  __syncthreads();
-  double bad[1] = {0.0};
-  auto test = [&](double vv, double l, double u) {
-    if ((u < QP_OSQP_INFTY * QP_MIN_SCALING && vv > eps * nrm) ||
-        (l > -QP_OSQP_INFTY * QP_MIN_SCALING && vv < -eps * nrm))
-      bad[0] = 1.0;
-  };
-  R6_FOR_H {
-    R6Var &W = V[h];
-    if (R[h].ok) test(r6_row_dot(R[h], s.rhs) / s.E[R[h].r], R[h].ur, R[h].ur);
-    if (W.ok) test((0.0 + W.Ab * W.dx) / s.E[R6_MD + W.j], W.lb, W.ub);
-    if (W.gok) test(r6_gen_dot(W, s.rhs) / s.E[R6_MD + R6_NV + W.j], W.gl, W.gu);
-  }
-  r6_max<1>(bad, s.red);
-  return bad[0] == 0.0;
-}
-
-__device__ __forceinline__ bool r6_check(R6Smem &s, R6Var (&V)[2], R6Row (&R)[2], const QPSettingsDev &st,
-                                         const double (&o)[8], bool approx, int &status) {
-  const double pri = o[0], dua = o[3] / s.c;
-  double ea = st.eps_abs, er = st.eps_rel, epi = st.eps_prim_inf, edi = st.eps_dual_inf;
-  if (pri > QP_OSQP_INFTY || dua > QP_OSQP_INFTY) { status = -7; return true; }
-  if (approx) { ea *= 10; er *= 10; epi *= 10; edi *= 10; }
-  bool prim_ok = false, prim_inf = false, dual_ok = false, dual_inf = false;
-  if (pri < ea + er * fmax(o[1], o[2])) prim_ok = true;
-  else prim_inf = r6_primal_infeasible(s, V, R, epi);
-  if (dua < ea + er * fmax(fmax(o[4], o[5]), o[6]) / s.c) dual_ok = true;
-  else dual_inf = r6_dual_infeasible(s, V, R, edi);
-  if (prim_ok && dual_ok) { status = approx ? 2 : 1; return true; }
-  if (prim_inf) { status = approx ? 3 : -3; return true; }
-  if (dual_inf) { status = approx ? 4 : -4; return true; }
-  return false;
-}
-
-__device__ __forceinline__ void r6_rebuild_w(R6Smem &s, R6Var (&V)[2], R6Row (&R)[2]) {
-  const double rs = s.rho_s;
-  R6_FOR_H {
-    if (R[h].ok) s.w[R[h].r] = QP_RHO_EQ * rs * R[h].zr - R[h].yr;
-    if (V[h].ok) V[h].ztb = r6_rho(V[h].lb, V[h].ub, rs) * V[h].zb - V[h].yb;
-    if (V[h].gok) s.w[R6_MD + V[h].j] = r6_rho(V[h].gl, V[h].gu, rs) * V[h].gz - V[h].gy;
-  }
-  __syncthreads();
-}
-
-// diagnostic phase cycles of workgroup 0 (GPMPC_R6_STAMPS=1 launches the <true> instance)
-__device__ unsigned long long g_r6_stamps[12];
-
-template <bool ST>
-__global__ __launch_bounds__(R6_T) void k_r6_control(R6Args a) {
-  const int b = blockIdx.x, tid = threadIdx.x;
-  unsigned long long tl = 0;
-  auto mark = [&](int k) {
-    if (ST && b == 0 && tid == 0) {
-      const unsigned long long t = __builtin_amdgcn_s_memtime();
-      if (k >= 0) g_r6_stamps[k] += t - tl;
-      tl = t;
-    }
-  };
-  mark(-1);
-  double *rec = a.rec + (int64_t)b * GPMPC_REC_LEN;
-  if (a.mode == 0 ? rec[0] != 0.0 : a.done[b] != 0) return;
-  extern __shared__ double smem_raw[];
-  R6Smem &s = *reinterpret_cast<R6Smem *>(smem_raw);
-  const double dt = a.dt;
-  const QPSettingsDev &st = a.st;
-  const double *Xb = a.Xp + (int64_t)b * (R6_N + 1) * R6_NX;
-  const double *Ub = a.U + (int64_t)b * R6_N * R6_NU;
-  const double *gmb = a.gm + (int64_t)b * R6_N * 6;
-  double *ysc = a.ysc + (int64_t)b * R6_M;
-  const double *x0 = a.x + (int64_t)b * R6_NX;
-  const double *prm = a.prm;
-  // the target: GPMPC.solve's x_target, or in a rollout step the incremental
-  // target of monte_carlo.py:497-500 (x copied, v = 0, altitude - 2 m, floor
-  // 0.5 m; optionally upright and at rest)
-  double xr[R6_NX];
-  if (a.mode) {
-    for (int i = 0; i < R6_NX; ++i) xr[i] = a.xt[(int64_t)b * R6_NX + i];
-  } else {
-    for (int i = 0; i < R6_NX; ++i) xr[i] = x0[i];
-    xr[4] = xr[5] = xr[6] = 0.0;
-    xr[1] = fmax(0.5, x0[1] - 2.0);
-    if (a.upright) {
-      xr[7] = 1.0; xr[8] = xr[9] = xr[10] = 0.0;
-      xr[11] = xr[12] = xr[13] = 0.0;
-    }
-  }
-  // ---- the linearisation (-[A_d | B_d] per stage, k_r6_predict) into the staging area
-  {
-    const double *lin = a.lin + (int64_t)b * R6_N * R6_NX * R6_SZ;
-    for (int e = tid; e < R6_N * R6_NX * R6_SZ; e += R6_T) s.G[e] = lin[e];
-    if (tid < R6_SZ) s.zero[tid] = 0.0;
-  }
-  __syncthreads();
-  // item tid + 512 h: variable j < 524 (h = 0: all of them below 512), else
-  // equality row r = item - 524; general row g = tid < 146 rides on slot 0
-  R6Var V[2];
-  R6Row R[2] = {R6Row(V[0]), R6Row(V[1])};
-  R6_FOR_H {
-    const int idx = tid + h * R6_T;
-    R6Var &W = V[h];
-    R6Row &Q = R[h];
-    W.j = idx; W.ok = idx < R6_NV;
-    W.k = idx / R6_SZ; W.i = idx - W.k * R6_SZ;
-    W.gok = h == 0 && tid < R6_MGEN;
-    Q.r = idx - R6_NV; Q.ok = h == 1 && idx >= R6_NV && Q.r < R6_MD;
-    Q.k = Q.r >= R6_NX ? (Q.r - R6_NX) / R6_NX : 0;
-    Q.i = Q.r >= R6_NX ? (Q.r - R6_NX) - Q.k * R6_NX : Q.r;
-    if (W.ok) {
-      const int k = W.k, i = W.i;
-      double xw, wq;
-      if (i < R6_NX) {
-        xw = Xb[k * R6_NX + i];
-        wq = prm[(k == R6_N ? R6_PP : R6_PQ) + i];
-        W.P = wq; W.q = wq * (xw - xr[i]);
-        const double tr = sqrt(prm[R6_PTRX]);
-        W.lb = -tr; W.ub = tr;
-      } else {
-        const double ub = Ub[k * R6_NU + i - R6_NX];
-        const double rr = prm[R6_PR + i - R6_NX], tr = sqrt(prm[R6_PTRU]), tmax = prm[R6_PTMAX];
-        W.P = rr; W.q = rr * ub;
-        W.lb = fmax(-tr, -tmax - ub);
-        W.ub = fmin(tr, tmax - ub);
-      }
-      W.Ab = 1.0;
-      W.x = 0.0;  // warm start dz = 0
-      W.yb = ysc[R6_MD + W.j];
-      if (k < R6_N)
-#pragma unroll
-        for (int e = 0; e < R6_NX; ++e) W.colA[e] = s.G[(k * R6_NX + e) * R6_SZ + i];
-      else
-#pragma unroll
-        for (int e = 0; e < R6_NX; ++e) W.colA[e] = 0.0;
-    }
-    if (W.gok) {
-      const int g = W.j;
-      if (g < R6_MT) {
-        const double *u = Ub + g * R6_NU;
-        const double tm = sqrt((u[0] * u[0] + u[1] * u[1]) + u[2] * u[2]);
-        W.gA[0] = u[0] / tm; W.gA[1] = u[1] / tm; W.gA[2] = u[2] / tm;
-        W.gl = prm[R6_PTMIN] - tm; W.gu = INFINITY; W.gn = 3;
-      } else {
-        const int gg = g - R6_MT, k = 1 + gg / 4, c = gg % 4;
-        const double tg = prm[R6_PTAN];  // np.tan(gamma_gs)
-        const double rx = Xb[k * R6_NX + 1], rc = Xb[k * R6_NX + (c < 2 ? 2 : 3)];
-        const double sg = (c & 1) ? 1.0 : -1.0;
-        W.gA[0] = tg; W.gA[1] = sg; W.gA[2] = 0.0;
-        W.gl = -(tg * rx + sg * rc); W.gu = INFINITY; W.gn = 2;
-      }
-      W.gy = ysc[R6_MD + R6_NV + g];
-    }
-    if (Q.ok) {
-      if (Q.r < R6_NX) {
-        Q.A[0] = 1.0;
-#pragma unroll
-        for (int e = 1; e <= R6_SZ; ++e) Q.A[e] = 0.0;
-        Q.ur = x0[Q.r] - Xb[Q.r];  // dX_0 = x0 - X_nom[0] (gp_mpc.py:402)
-      } else {
-#pragma unroll
-        for (int e = 0; e < R6_SZ; ++e) Q.A[e] = s.G[(Q.k * R6_NX + Q.i) * R6_SZ + e];
-        Q.A[R6_SZ] = 1.0;
-        const int i = Q.i;
-        Q.ur = (i >= 4 && i < 7) ? gmb[Q.k * 6 + i - 4] * dt : ((i >= 11) ? gmb[Q.k * 6 + 3 + i - 11] * dt : 0.0);
-      }
-      Q.yr = ysc[Q.r];
-    }
-    // ---- OSQP solve (qp_device.h order): clip bounds, Ruiz scaling, rho, factor
-    if (W.ok) { W.lb = fmax(W.lb, -QP_OSQP_INFTY); W.ub = fmin(W.ub, QP_OSQP_INFTY); }
-    if (W.gok) { W.gl = fmax(W.gl, -QP_OSQP_INFTY); W.gu = fmin(W.gu, QP_OSQP_INFTY); }
-    if (Q.ok) Q.ur = fmin(fmax(Q.ur, -QP_OSQP_INFTY), QP_OSQP_INFTY);
-  }
-  mark(0);
-  for (int r = tid; r < R6_M; r += R6_T) s.E[r] = 1.0;
-  R6_FOR_H {
-    if (R[h].ok) s.dpl[R[h].r] = R[h].r < R6_NX ? R[h].A[0] : R[h].A[R6_SZ];
-    if (V[h].gok)
-#pragma unroll
-      for (int e = 0; e < 3; ++e) s.gen[V[h].j * 3 + e] = V[h].gA[e];
-    if (V[h].ok) V[h].D = 1.0;
-  }
-  if (tid == 0) { s.c = 1.0; s.rho_s = fmin(fmax(a.rho[b], QP_RHO_MIN), QP_RHO_MAX); }
-  __syncthreads();
-  for (int it = 0; it < st.scaling; ++it) {
-    // column factors -> dsc, row factors -> w (equality: [0, MD), general: MD + g)
-    double eb[2] = {1.0, 1.0};
-    R6_FOR_H {
-      R6Var &W = V[h];
-      R6Row &Q = R[h];
-      if (W.ok) {
-        double v = fabs(W.P);
-        if (W.i < R6_NX) v = fmax(v, fabs(s.dpl[r6_eqid_row(W.k, W.i)]));
-        if (W.k < R6_N)
-#pragma unroll
-          for (int e = 0; e < R6_NX; ++e) v = fmax(v, fabs(W.colA[e]));
-        v = fmax(v, fabs(W.Ab));
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          int g, sl;
-          if (r6_gen_slot(W.k, W.i, e, g, sl)) v = fmax(v, fabs(s.gen[g * 3 + sl]));
-        }
-        s.dsc[W.j] = 1.0 / sqrt(qp_limit(v));
-        eb[h] = 1.0 / sqrt(qp_limit(fmax(0.0, fabs(W.Ab))));
-      }
-      if (Q.ok) {
-        double v = 0.0;
-        const int ne = Q.r < R6_NX ? 1 : R6_SZ + 1;
-#pragma unroll
-        for (int e = 0; e < R6_SZ + 1; ++e)
-          if (e < ne) v = fmax(v, fabs(Q.A[e]));
-        s.w[Q.r] = 1.0 / sqrt(qp_limit(v));
-      }
-      if (W.gok) {
-        double v = 0.0;
-#pragma unroll
-        for (int e = 0; e < 3; ++e)
-          if (e < W.gn) v = fmax(v, fabs(W.gA[e]));
-        s.w[R6_MD + W.j] = 1.0 / sqrt(qp_limit(v));
-      }
-    }
-    __syncthreads();
-    double v[1] = {0.0}, mx[1] = {0.0};
-    R6_FOR_H {
-      R6Var &W = V[h];
-      R6Row &Q = R[h];
-      if (Q.ok) {
-        const double e = s.w[Q.r];
-        if (Q.r < R6_NX) {
-          Q.A[0] = e * Q.A[0] * s.dsc[Q.r];
-          s.dpl[Q.r] = Q.A[0];
-        } else {
-          const int o = Q.k * R6_SZ;
-#pragma unroll
-          for (int c = 0; c < R6_SZ; ++c) Q.A[c] = e * Q.A[c] * s.dsc[o + c];
-          Q.A[R6_SZ] = e * Q.A[R6_SZ] * s.dsc[(Q.k + 1) * R6_SZ + Q.i];
-          s.dpl[Q.r] = Q.A[R6_SZ];
-        }
-        s.E[Q.r] *= e;
-      }
-      if (W.gok) {
-        const double e = s.w[R6_MD + W.j];
-        int col[3];
-        r6_gen_cols(W.j, col);
-#pragma unroll
-        for (int c = 0; c < 3; ++c)
-          if (c < W.gn) {
-            W.gA[c] = e * W.gA[c] * s.dsc[col[c]];
-            s.gen[W.j * 3 + c] = W.gA[c];
-          }
-        s.E[R6_MD + R6_NV + W.j] *= e;
-      }
-      if (W.ok) {
-        const double d = s.dsc[W.j];
-        if (W.k < R6_N)
-#pragma unroll
-          for (int e = 0; e < R6_NX; ++e) W.colA[e] = s.w[R6_NX + R6_NX * W.k + e] * W.colA[e] * d;
-        W.Ab = eb[h] * W.Ab * d;
-        s.E[R6_MD + W.j] *= eb[h];
-        W.P = d * W.P * d;
-        W.q = d * W.q;
-        W.D *= d;
-        v[0] += fabs(W.P);
-        mx[0] = fmax(mx[0], fabs(W.q));
-      }
-    }
-    r6_sum<1>(v, s.red);
-    r6_max<1>(mx, s.red);
-    double ct = v[0] / R6_NV;
-    const double nq = qp_limit(mx[0]);
-    ct = qp_limit(fmax(ct, nq));
-    ct = 1.0 / ct;
-    R6_FOR_H {
-      if (V[h].ok) { V[h].P *= ct; V[h].q *= ct; }
-    }
-    if (tid == 0) s.c *= ct;
-    __syncthreads();
-  }
-  R6_FOR_H {
-    R6Var &W = V[h];
-    if (W.ok) { const double e = s.E[R6_MD + W.j]; W.lb = e * W.lb; W.ub = e * W.ub; }
-    if (W.gok) { const double e = s.E[R6_MD + R6_NV + W.j]; W.gl = e * W.gl; W.gu = e * W.gu; }
-    if (R[h].ok) R[h].ur = s.E[R[h].r] * R[h].ur;
-  }
-  mark(1);
-  int f = r6_factor(s, V, R, st.sigma, mark);
-  mark(2);
-  QPResult res{-10, 0, 0.0, 0};
-  if (f) res.factor_fail = f;
-  if (!f) {
-    // warm start x = 0 / D = 0, z = A x = 0; y persisted (osqp_rti.py:521-524)
-    R6_FOR_H {
-      V[h].x = 0.0; V[h].zb = 0.0; R[h].zr = 0.0; V[h].gz = 0.0;
-      if (V[h].ok) V[h].zb = 0.0 + V[h].Ab * V[h].x;
-    }
-    r6_rebuild_w(s, V, R);
-    const double sig = st.sigma, al = st.alpha;
-    bool can_check = false;
-    int it;
-    double o[8], re_[4];
-    for (it = 1; it <= st.max_iter; ++it) {
-      R6_FOR_H {
-        if (V[h].ok) s.rhs[V[h].j] = sig * V[h].x - V[h].q + r6_col_dot(s, V[h], s.w, V[h].ztb, s.w + R6_MD);
-      }
-      __syncthreads();
-      mark(3);
-      r6_solve(s, mark);
-      const double rs = s.rho_s;
-      R6_FOR_H {
-        R6Var &W = V[h];
-        R6Row &Q = R[h];
-        if (W.ok) {
-          const double xt = s.xs[W.j], xo = W.x;
-          const double xn = al * xt + (1.0 - al) * xo;
-          W.dx = xn - xo;
-          W.x = xn;
-          const double ztl = 0.0 + W.Ab * xt;
-          const double rho = r6_rho(W.lb, W.ub, rs), zo = W.zb, yo = W.yb;
-          const double zr = al * ztl + (1.0 - al) * zo;
-          double zn = zr + yo / rho;
-          zn = fmin(fmax(zn, W.lb), W.ub);
-          const double d = rho * (zr - zn);
-          W.dyb = d; W.yb = yo + d; W.zb = zn;
-          W.ztb = rho * zn - W.yb;
-        }
-        if (W.gok) {
-          const double ztl = r6_gen_dot(W, s.xs);
-          const double rho = r6_rho(W.gl, W.gu, rs), zo = W.gz, yo = W.gy;
-          const double zr = al * ztl + (1.0 - al) * zo;
-          double zn = zr + yo / rho;
-          zn = fmin(fmax(zn, W.gl), W.gu);
-          const double d = rho * (zr - zn);
-          W.gdy = d; W.gy = yo + d; W.gz = zn;
-        }
-        if (Q.ok) {
-          const double ztl = r6_row_dot(Q, s.xs);
-          const double rho = QP_RHO_EQ * rs, zo = Q.zr, yo = Q.yr;
-          const double zr = al * ztl + (1.0 - al) * zo;
-          double zn = zr + yo / rho;
-          zn = fmin(fmax(zn, Q.ur), Q.ur);
-          const double d = rho * (zr - zn);
-          Q.dyr = d; Q.yr = yo + d; Q.zr = zn;
-        }
-      }
-      __syncthreads();  // every read of s.w / s.xs of this iteration is done
-      R6_FOR_H {
-        if (R[h].ok) s.w[R[h].r] = QP_RHO_EQ * rs * R[h].zr - R[h].yr;
-        if (V[h].gok) s.w[R6_MD + V[h].j] = r6_rho(V[h].gl, V[h].gu, rs) * V[h].gz - V[h].gy;
-      }
-      __syncthreads();
-      mark(7);
-      can_check = st.check_termination && (it % st.check_termination == 0);
-      const bool adapt = st.adaptive_rho && st.adaptive_rho_interval && (it % st.adaptive_rho_interval == 0);
-      if (can_check || adapt) {
-        res.iter = it;
-        r6_update_info(s, V, R, o, re_);
-      }
-      if (can_check && r6_check(s, V, R, st, o, false, res.status)) break;
-      if (adapt) {
-        const double pr = re_[0] / (re_[1] + 1e-10);
-        const double du = re_[2] / (re_[3] + 1e-10);
-        double est = s.rho_s * sqrt(pr / (du + 1e-10));
-        est = fmin(fmax(est, QP_RHO_MIN), QP_RHO_MAX);
-        if (est > s.rho_s * st.adaptive_rho_tolerance || est < s.rho_s / st.adaptive_rho_tolerance) {
-          __syncthreads();
-          if (tid == 0) s.rho_s = est;
-          __syncthreads();
-          if (it < st.max_iter) {
-            f = r6_factor(s, V, R, st.sigma, mark);
-            if (f) { res.factor_fail = f; break; }
-          }
-        }
-      }
-      if (can_check || adapt) r6_rebuild_w(s, V, R);
-      mark(8);
-    }
-    if (!res.factor_fail) {
-      if (!can_check) {
-        res.iter = it - 1;
-        r6_update_info(s, V, R, o, re_);
-        r6_check(s, V, R, st, o, false, res.status);
-      }
-      if (res.status == -10) {
-        if (!r6_check(s, V, R, st, o, true, res.status)) res.status = -2;
-      }
-    }
-  }
-  const bool has = !res.factor_fail && (res.status == 1 || res.status == 2 || res.status == -2);
-  // ---- solution: the unscaled deviations onto the plan, kept unshifted (gp_mpc.py:358-359)
-  R6_FOR_H {
-    if (has && V[h].ok) s.xs[V[h].j] = V[h].D * V[h].x;
-  }
-  __syncthreads();
-  double *Xo = a.Xo + (int64_t)b * (R6_N + 1) * R6_NX;
-  double *Uw = a.U + (int64_t)b * R6_N * R6_NU;
-  double chg[2] = {0.0, 0.0};  // max |X_new - X_pred|, max |U_new - U_pred| (gp_mpc.py:337-338)
-  if (has) {
-    for (int e = tid; e < (R6_N + 1) * R6_NX; e += R6_T) {
-      const int k = e / R6_NX, i = e - k * R6_NX;
-      const double xo = Xb[e] + s.xs[k * R6_SZ + i];
-      Xo[e] = xo;
-      const double d = fabs(xo - Xb[e]);
-      if (!(d <= chg[0])) chg[0] = d != d ? INFINITY : d;  // a NaN never converges
-    }
-    double un = 0.0;
-    if (tid < R6_N * R6_NU) {
-      const int k = tid / R6_NU, i = tid - k * R6_NU;
-      un = Ub[tid] + s.xs[k * R6_SZ + R6_NX + i];
-      const double d = fabs(un - Ub[tid]);
-      chg[1] = d != d ? INFINITY : d;
-    }
-    __syncthreads();  // every thread read U before it is overwritten
-    if (tid < R6_N * R6_NU) Uw[tid] = un;
-    R6_FOR_H {
-      if (R[h].ok) ysc[R[h].r] = R[h].yr;
-      if (V[h].ok) ysc[R6_MD + V[h].j] = V[h].yb;
-      if (V[h].gok) ysc[R6_MD + R6_NV + V[h].j] = V[h].gy;
-    }
-    __syncthreads();
-  } else if (a.mode) {
-    // _solve_qp's fallback (gp_mpc.py:478-482): the nominal trajectory
-    for (int e = tid; e < (R6_N + 1) * R6_NX; e += R6_T) Xo[e] = Xb[e];
-  }
-  if (a.mode) r6_max<2>(chg, s.red);  // a.mode is uniform over the launch
-  if (tid == 0 && a.mode) {  // GPMPC.solve pass bookkeeping
-    a.passes[b] += 1;
-    a.qit[b] += res.iter;
-    a.qst[b] = res.factor_fail ? -100 : res.status;
-    a.done[b] = (chg[0] < a.sqp_tol && chg[1] < a.sqp_tol) ? 1 : 0;  // a failed QP: X_new = X_pred
-    rec[11] += res.iter;
-    rec[12] += (res.status == 1 && !res.factor_fail) ? 1.0 : 0.0;
-    rec[14] = res.factor_fail ? -100 : res.status;
-    if (has) { a.rho[b] = s.rho_s; rec[15] = s.rho_s; }
-  } else if (tid == 0) {
-    if (!has) {  // MPCSolution without a solution -> DIVERGENCE
-      const double *x = a.x + (int64_t)b * R6_NX;
-      rec[0] = 6;
-      rec[14] = res.factor_fail ? -100 : res.status;
-      rec[2] = rec[13] - x[0];
-      for (int i = 0; i < 7; ++i) rec[4 + i] = x[i];
-    } else {
-      a.rho[b] = s.rho_s;
-      rec[11] += res.iter;
-      rec[12] += (res.status == 1) ? 1.0 : 0.0;
-      rec[14] = res.status;
-      rec[15] = s.rho_s;
-      a.pending[b] = 1;
-    }
-  }
-  mark(9);
-}
-
-// 3. the truth plant step with the plan's first control: RK4 + the drag
-// dispersion at the pre-step state (dispersion.py:349-360) + the -0.05 w rate
-// damping the config-5 GP is trained on (data.synthetic_6dof_training_data)
-__global__ __launch_bounds__(64) void k_r6_plant(R6Args a, int B) {
-  const int b = blockIdx.x * 64 + threadIdx.x;
-  if (b >= B || !a.pending[b]) return;
-  a.pending[b] = 0;
-  double *rec = a.rec + (int64_t)b * GPMPC_REC_LEN;
-  double *x = a.x + (int64_t)b * R6_NX;
-  const double dt = a.dt;
-  double xc[R6_NX], xn[R6_NX];
-  for (int i = 0; i < R6_NX; ++i) xc[i] = x[i];
-  const double *u0 = a.U + (int64_t)b * R6_N * R6_NU;
-  r6_step(xc, u0, dt, xn);
-  const double vx = xc[4], vy = xc[5], vz = xc[6];
-  const double sp = sqrt((vx * vx + vy * vy) + vz * vz);
-  if (sp > 1.0) {
-    const double ac = (0.5 * 0.02 * sp * sp) / xc[0];
-    xn[4] += -ac * (vx / sp) * dt; xn[5] += -ac * (vy / sp) * dt; xn[6] += -ac * (vz / sp) * dt;
-  }
-  for (int i = 11; i < 14; ++i) xn[i] += -0.05 * xc[i] * dt;
-  for (int i = 0; i < R6_NX; ++i) x[i] = xn[i];
-  rec[1] += 1.0;
-  rec[2] = rec[13] - xn[0];
-  rec[3] = rec[1] * dt;
-  for (int i = 0; i < 7; ++i) rec[4 + i] = xn[i];
-}
-
-__global__ void k_r6_reset(int first, int count, const double *__restrict__ x0, double *x, double *U,
-                           double *ysc, double *rho, double rho0, double *rec) {
-  const int i = blockIdx.x;
-  if (i >= count) return;
-  const int b = first + i;
-  const double *xi = x0 + (int64_t)i * R6_NX;
-  for (int e = threadIdx.x; e < R6_N * R6_NU; e += blockDim.x)  // hover guess as written (gp_mpc.py:271-275)
-    U[(int64_t)b * R6_N * R6_NU + e] = (e % R6_NU == 2) ? xi[0] * 1.0 : 0.0;
-  for (int r = threadIdx.x; r < R6_M; r += blockDim.x) ysc[(int64_t)b * R6_M + r] = 0.0;
-  if (threadIdx.x < GPMPC_REC_LEN) rec[(int64_t)b * GPMPC_REC_LEN + threadIdx.x] = 0.0;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    for (int c = 0; c < R6_NX; ++c) x[(int64_t)b * R6_NX + c] = xi[c];
-    for (int c = 0; c < 7; ++c) rec[(int64_t)b * GPMPC_REC_LEN + 4 + c] = xi[c];
-    rec[(int64_t)b * GPMPC_REC_LEN + 13] = xi[0];
-    rho[b] = rho0;
-  }
-}
-
 // ---------------------------------------------------------------------------
 static int r6_create(gpmpc_ctx *ctx, const GpView &gv, const GpView &gw, bool exact,
                      const gpmpc_rollout6_config *cfg, int batch, gpmpc_rollout6 **out) {
@@ -1648,8 +403,10 @@ static int r6_create(gpmpc_ctx *ctx, const GpView &gv, const GpView &gw, bool ex
     gpmpc_set_error("rollout6: expects the StructuredRocketGP pair (13 / 12 features, 3 outputs, SE-ARD)");
     return -2;
   }
-  if (cfg->horizon != R6_N) {
-    gpmpc_set_error("rollout6: horizon must be %d (BASELINE configs[4])", R6_N);
+  const R6Impl *impl = r6_impl(cfg->horizon);
+  if (!impl) {
+    gpmpc_set_error("rollout6: horizon %d not compiled (20: GPMPCConfig's N, 30: BASELINE configs[4])",
+                    cfg->horizon);
     return -2;
   }
   for (int i = 0; i < R6_NX; ++i)
@@ -1661,17 +418,28 @@ static int r6_create(gpmpc_ctx *ctx, const GpView &gv, const GpView &gw, bool ex
     gpmpc_set_error("rollout6: t_max and the trust radii must be positive");
     return -2;
   }
+  for (int i = 0; i < 3; ++i)
+    if (!(cfg->rocket_j[i] > 0.0)) {
+      gpmpc_set_error("rollout6: the rocket's J_B diagonal must be positive");
+      return -2;
+    }
+  if (!(cfg->rocket_alpha >= 0.0) || !(cfg->rocket_g0 > 0.0)) {
+    gpmpc_set_error("rollout6: rocket alpha must be >= 0 and g0 > 0");
+    return -2;
+  }
   GPMPC_HIP(hipSetDevice(ctx->device));
   auto *r = new gpmpc_rollout6();
   r->ctx = ctx; r->gv = gv; r->gw = gw; r->exact = exact; r->cfg = *cfg; r->B = batch;
-  const size_t B = batch;
-  if (r->x.alloc(sizeof(double) * B * R6_NX) || r->U.alloc(sizeof(double) * B * R6_N * R6_NU) ||
-      r->Xp.alloc(sizeof(double) * B * (R6_N + 1) * R6_NX) || r->gm.alloc(sizeof(double) * B * R6_N * 6) ||
-      r->Xo.alloc(sizeof(double) * B * (R6_N + 1) * R6_NX) || r->ysc.alloc(sizeof(double) * B * R6_M) ||
+  r->impl = impl; r->N = impl->N; r->M = impl->M;
+  const size_t B = batch, N = r->N;
+  if (r->x.alloc(sizeof(double) * B * R6_NX) || r->U.alloc(sizeof(double) * B * N * R6_NU) ||
+      r->Xp.alloc(sizeof(double) * B * (N + 1) * R6_NX) || r->gm.alloc(sizeof(double) * B * N * 6) ||
+      r->Xo.alloc(sizeof(double) * B * (N + 1) * R6_NX) || r->ysc.alloc(sizeof(double) * B * r->M) ||
       r->rho.alloc(sizeof(double) * B) || r->rec.alloc(sizeof(double) * B * GPMPC_REC_LEN) ||
-      r->lin.alloc(sizeof(double) * B * R6_N * R6_NX * R6_SZ) || r->pending.alloc(sizeof(int) * B) ||
+      r->lin.alloc(sizeof(double) * B * N * R6_NX * R6_SZ) || r->pending.alloc(sizeof(int) * B) ||
       r->betav.alloc(sizeof(double) * 3 * gv.n) || r->betaw.alloc(sizeof(double) * 3 * gw.n) ||
-      r->prm.alloc(sizeof(double) * R6_PRM) || r->xt.alloc(sizeof(double) * B * R6_NX) ||
+      r->prm.alloc(sizeof(double) * R6_PRM) || r->xt.alloc(sizeof(double) * B * (N + 1) * R6_NX) ||
+      r->ut.alloc(sizeof(double) * B * N * R6_NU) ||
       r->xin.alloc(sizeof(double) * B * R6_NX) || r->done.alloc(sizeof(int) * B) ||
       r->passes.alloc(sizeof(int) * B) || r->qit.alloc(sizeof(int) * B) || r->qst.alloc(sizeof(int) * B)) {
     delete r;
@@ -1687,7 +455,8 @@ static int r6_create(gpmpc_ctx *ctx, const GpView &gv, const GpView &gw, bool ex
   std::vector<double> rc(B * GPMPC_REC_LEN, 0.0);
   for (size_t i = 0; i < B; ++i) rc[i * GPMPC_REC_LEN] = -1.0;  // not started until reset
   hipMemcpyAsync(r->rec.p, rc.data(), sizeof(double) * rc.size(), hipMemcpyHostToDevice, ctx->stream);
-  hipMemsetAsync(r->Xo.p, 0, sizeof(double) * B * (R6_N + 1) * R6_NX, ctx->stream);
+  hipMemsetAsync(r->Xo.p, 0, sizeof(double) * B * (N + 1) * R6_NX, ctx->stream);
+  hipMemsetAsync(r->ut.p, 0, sizeof(double) * B * N * R6_NU, ctx->stream);
   hipMemsetAsync(r->pending.p, 0, sizeof(int) * B, ctx->stream);
   hipMemsetAsync(r->done.p, 0, sizeof(int) * B, ctx->stream);
   if (!exact) {  // beta^T = alpha^T L_uu^-1: the FITC posterior mean's coefficients
@@ -1700,15 +469,9 @@ static int r6_create(gpmpc_ctx *ctx, const GpView &gv, const GpView &gw, bool ex
       return -1;
     }
   }
-  static bool attr = [] {
-    (void)hipFuncSetAttribute((const void *)k_r6_control<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              sizeof(R6Smem));
-    return hipFuncSetAttribute((const void *)k_r6_control<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                               (int)sizeof(R6Smem)) == hipSuccess;
-  }();
-  if (!attr) {
+  if (impl->init() != hipSuccess) {
     delete r;
-    gpmpc_set_error("rollout6: %zu B of LDS not available", sizeof(R6Smem));
+    gpmpc_set_error("rollout6: %zu B of LDS not available", impl->smem);
     return -1;
   }
   GPMPC_HIP(hipStreamSynchronize(ctx->stream));
@@ -1726,42 +489,6 @@ extern "C" int gpmpc_rollout6_create_exact(gpmpc_ctx *ctx, gpmpc_gp *gp_v, gpmpc
                                            const gpmpc_rollout6_config *cfg, int batch, gpmpc_rollout6 **out) {
   GPMPC_CHECK_ARG(gp_v && gp_w);
   return r6_create(ctx, gp_view(gp_v), gp_view(gp_w), true, cfg, batch, out);
-}
-
-extern "C" int gpmpc_rollout6_reset(gpmpc_rollout6 *r, int first, int count, const double *x0) {
-  GPMPC_CHECK_ARG(r && x0 && first >= 0 && count >= 0 && first + count <= r->B);
-  if (count == 0) return 0;
-  hipStream_t s = r->ctx->stream;
-  DevBuf d;
-  GPMPC_HIP(d.alloc(sizeof(double) * count * R6_NX));
-  GPMPC_HIP(hipMemcpyAsync(d.p, x0, sizeof(double) * count * R6_NX, hipMemcpyHostToDevice, s));
-  hipLaunchKernelGGL(k_r6_reset, dim3(count), dim3(256), 0, s, first, count, d.as<double>(),
-                     r->x.as<double>(), r->U.as<double>(), r->ysc.as<double>(), r->rho.as<double>(),
-                     r->cfg.qp.rho, r->rec.as<double>());
-  GPMPC_HIP(hipGetLastError());
-  GPMPC_HIP(hipStreamSynchronize(s));
-  return 0;
-}
-
-// GPMPC.solve: x0 / x_target already in x / xt; cold = hover guess + fresh ADMM state
-__global__ void k_r6_solve_begin(R6Args a, int cold, double rho0) {
-  const int b = blockIdx.x;
-  const double m0 = a.x[(int64_t)b * R6_NX];
-  if (cold == 1) {
-    // gp_mpc.py:271-275 as intended: [0, 0, m0 g0] at every stage (as written it reads
-    // X_pred[k, 0] before the simulation has filled it, i.e. zero thrust for k >= 1,
-    // whose thrust-magnitude rows have no linearisation)
-    for (int e = threadIdx.x; e < R6_N * R6_NU; e += blockDim.x)
-      a.U[(int64_t)b * R6_N * R6_NU + e] = (e % R6_NU == 2) ? m0 * 1.0 : 0.0;
-  }
-  if (cold)
-    for (int r = threadIdx.x; r < R6_M; r += blockDim.x) a.ysc[(int64_t)b * R6_M + r] = 0.0;
-  if (threadIdx.x == 0) {
-    if (cold) a.rho[b] = rho0;
-    a.done[b] = 0; a.passes[b] = 0; a.qit[b] = 0; a.qst[b] = -10;
-    double *rec = a.rec + (int64_t)b * GPMPC_REC_LEN;
-    rec[11] = 0.0; rec[12] = 0.0;
-  }
 }
 
 static R6Args r6_args(gpmpc_rollout6 *r) {
@@ -1784,9 +511,27 @@ static R6Args r6_args(gpmpc_rollout6 *r) {
   a.mode = 0;
   a.sqp_tol = 0.0;
   a.xt = r->xt.as<double>();
+  a.ut = r->ut.as<double>();
   a.done = r->done.as<int>(); a.passes = r->passes.as<int>();
   a.qit = r->qit.as<int>(); a.qst = r->qst.as<int>();
+  const gpmpc_rollout6_config &c = r->cfg;
+  for (int i = 0; i < 3; ++i) { a.rk.J[i] = c.rocket_j[i]; a.rk.rT[i] = c.rocket_r_t[i]; a.rk.gI[i] = c.rocket_g_i[i]; }
+  a.rk.alpha = c.rocket_alpha;
+  a.rk.g0 = c.rocket_g0;
   return a;
+}
+
+extern "C" int gpmpc_rollout6_reset(gpmpc_rollout6 *r, int first, int count, const double *x0) {
+  GPMPC_CHECK_ARG(r && x0 && first >= 0 && count >= 0 && first + count <= r->B);
+  if (count == 0) return 0;
+  hipStream_t s = r->ctx->stream;
+  DevBuf d;
+  GPMPC_HIP(d.alloc(s, sizeof(double) * count * R6_NX));
+  GPMPC_HIP(hipMemcpyAsync(d.p, x0, sizeof(double) * count * R6_NX, hipMemcpyHostToDevice, s));
+  r->impl->reset(s, first, count, d.as<double>(), r6_args(r), r->cfg.qp.rho);
+  GPMPC_HIP(hipGetLastError());
+  GPMPC_HIP(hipStreamSynchronize(s));
+  return 0;
 }
 
 static bool r6_stamps_on() {
@@ -1802,15 +547,9 @@ extern "C" int gpmpc_rollout6_step_phases(gpmpc_rollout6 *r, int mask) {
   GPMPC_HIP(hipSetDevice(r->ctx->device));
   hipStream_t s = r->ctx->stream;
   const R6Args a = r6_args(r);
-  if (mask & 1) {
-    if (r6_stamps_on()) hipLaunchKernelGGL(k_r6_predict<true>, dim3(r->B), dim3(R6_PT), 0, s, a);
-    else hipLaunchKernelGGL(k_r6_predict<false>, dim3(r->B), dim3(R6_PT), 0, s, a);
-  }
-  if (mask & 2) {
-    if (r6_stamps_on()) hipLaunchKernelGGL(k_r6_control<true>, dim3(r->B), dim3(R6_T), sizeof(R6Smem), s, a);
-    else hipLaunchKernelGGL(k_r6_control<false>, dim3(r->B), dim3(R6_T), sizeof(R6Smem), s, a);
-  }
-  if (mask & 4) hipLaunchKernelGGL(k_r6_plant, dim3((r->B + 63) / 64), dim3(64), 0, s, a, r->B);
+  if (mask & 1) r->impl->predict(s, r->B, a, r6_stamps_on());
+  if (mask & 2) r->impl->control(s, r->B, a, r6_stamps_on());
+  if (mask & 4) r->impl->plant(s, r->B, a);
   GPMPC_HIP(hipGetLastError());
   return 0;
 }
@@ -1824,32 +563,52 @@ extern "C" int gpmpc_rollout6_step(gpmpc_rollout6 *r, int nsteps) {
   return 0;
 }
 
-extern "C" int gpmpc_rollout6_solve(gpmpc_rollout6 *r, const double *x0, const double *x_target, int cold,
-                                    int max_sqp_iter, double sqp_tol, double *X, double *U, int *passes,
-                                    int *converged, int *qp_status, int *qp_iters) {
+extern "C" int gpmpc_rollout6_solve_ref(gpmpc_rollout6 *r, const double *x0, const double *x_target,
+                                        const double *X_ref, const double *U_ref, int cold, int max_sqp_iter,
+                                        double sqp_tol, double *X, double *U, int *passes, int *converged,
+                                        int *qp_status, int *qp_iters) {
   GPMPC_CHECK_ARG(r && x0 && x_target && max_sqp_iter >= 1 && sqp_tol >= 0.0 && cold >= 0 && cold <= 2);
   GPMPC_HIP(hipSetDevice(r->ctx->device));
   hipStream_t s = r->ctx->stream;
-  const size_t B = r->B;
+  const size_t B = r->B, N = r->N;
   GPMPC_HIP(hipMemcpyAsync(r->x.p, x0, sizeof(double) * B * R6_NX, hipMemcpyHostToDevice, s));
-  GPMPC_HIP(hipMemcpyAsync(r->xt.p, x_target, sizeof(double) * B * R6_NX, hipMemcpyHostToDevice, s));
+  // the QP cost's references (gp_mpc.py:442-445): X_ref = x_target on every stage unless given,
+  // U_ref = 0 unless given
+  std::vector<double> xr;
+  if (!X_ref) {
+    xr.resize(B * (N + 1) * R6_NX);
+    for (size_t b = 0; b < B; ++b)
+      for (size_t k = 0; k <= N; ++k)
+        for (int i = 0; i < R6_NX; ++i) xr[(b * (N + 1) + k) * R6_NX + i] = x_target[b * R6_NX + i];
+    X_ref = xr.data();
+  }
+  GPMPC_HIP(hipMemcpyAsync(r->xt.p, X_ref, sizeof(double) * B * (N + 1) * R6_NX, hipMemcpyHostToDevice, s));
+  if (U_ref) GPMPC_HIP(hipMemcpyAsync(r->ut.p, U_ref, sizeof(double) * B * N * R6_NU, hipMemcpyHostToDevice, s));
+  else GPMPC_HIP(hipMemsetAsync(r->ut.p, 0, sizeof(double) * B * N * R6_NU, s));
   R6Args a = r6_args(r);
   a.sqp_tol = sqp_tol;
-  hipLaunchKernelGGL(k_r6_solve_begin, dim3(r->B), dim3(256), 0, s, a, cold, r->cfg.qp.rho);
+  r->impl->solve_begin(s, r->B, a, cold, r->cfg.qp.rho);
   for (int p = 1; p <= max_sqp_iter; ++p) {  // passes of converged rollouts exit at once
     a.mode = p == 1 ? 1 : 2;
-    hipLaunchKernelGGL(k_r6_predict<false>, dim3(r->B), dim3(R6_PT), 0, s, a);
-    hipLaunchKernelGGL(k_r6_control<false>, dim3(r->B), dim3(R6_T), sizeof(R6Smem), s, a);
+    r->impl->predict(s, r->B, a, false);
+    r->impl->control(s, r->B, a, false);
   }
   GPMPC_HIP(hipGetLastError());
-  if (X) GPMPC_HIP(hipMemcpyAsync(X, r->Xo.p, sizeof(double) * B * (R6_N + 1) * R6_NX, hipMemcpyDeviceToHost, s));
-  if (U) GPMPC_HIP(hipMemcpyAsync(U, r->U.p, sizeof(double) * B * R6_N * R6_NU, hipMemcpyDeviceToHost, s));
+  if (X) GPMPC_HIP(hipMemcpyAsync(X, r->Xo.p, sizeof(double) * B * (N + 1) * R6_NX, hipMemcpyDeviceToHost, s));
+  if (U) GPMPC_HIP(hipMemcpyAsync(U, r->U.p, sizeof(double) * B * N * R6_NU, hipMemcpyDeviceToHost, s));
   if (passes) GPMPC_HIP(hipMemcpyAsync(passes, r->passes.p, sizeof(int) * B, hipMemcpyDeviceToHost, s));
   if (converged) GPMPC_HIP(hipMemcpyAsync(converged, r->done.p, sizeof(int) * B, hipMemcpyDeviceToHost, s));
   if (qp_status) GPMPC_HIP(hipMemcpyAsync(qp_status, r->qst.p, sizeof(int) * B, hipMemcpyDeviceToHost, s));
   if (qp_iters) GPMPC_HIP(hipMemcpyAsync(qp_iters, r->qit.p, sizeof(int) * B, hipMemcpyDeviceToHost, s));
   GPMPC_HIP(hipStreamSynchronize(s));
   return 0;
+}
+
+extern "C" int gpmpc_rollout6_solve(gpmpc_rollout6 *r, const double *x0, const double *x_target, int cold,
+                                    int max_sqp_iter, double sqp_tol, double *X, double *U, int *passes,
+                                    int *converged, int *qp_status, int *qp_iters) {
+  return gpmpc_rollout6_solve_ref(r, x0, x_target, nullptr, nullptr, cold, max_sqp_iter, sqp_tol, X, U, passes,
+                                  converged, qp_status, qp_iters);
 }
 
 extern "C" int gpmpc_rollout6_read(gpmpc_rollout6 *r, double *records, double *x) {
@@ -1867,14 +626,14 @@ extern "C" int gpmpc_rollout6_get_state(gpmpc_rollout6 *r, double *U, double *X_
                                         double *gp_mean, double *y_scaled, double *rho) {
   GPMPC_CHECK_ARG(r);
   hipStream_t s = r->ctx->stream;
-  const size_t B = r->B;
-  if (U) GPMPC_HIP(hipMemcpyAsync(U, r->U.p, sizeof(double) * B * R6_N * R6_NU, hipMemcpyDeviceToHost, s));
+  const size_t B = r->B, N = r->N;
+  if (U) GPMPC_HIP(hipMemcpyAsync(U, r->U.p, sizeof(double) * B * N * R6_NU, hipMemcpyDeviceToHost, s));
   if (X_plan)
-    GPMPC_HIP(hipMemcpyAsync(X_plan, r->Xo.p, sizeof(double) * B * (R6_N + 1) * R6_NX, hipMemcpyDeviceToHost, s));
+    GPMPC_HIP(hipMemcpyAsync(X_plan, r->Xo.p, sizeof(double) * B * (N + 1) * R6_NX, hipMemcpyDeviceToHost, s));
   if (X_pred)
-    GPMPC_HIP(hipMemcpyAsync(X_pred, r->Xp.p, sizeof(double) * B * (R6_N + 1) * R6_NX, hipMemcpyDeviceToHost, s));
-  if (gp_mean) GPMPC_HIP(hipMemcpyAsync(gp_mean, r->gm.p, sizeof(double) * B * R6_N * 6, hipMemcpyDeviceToHost, s));
-  if (y_scaled) GPMPC_HIP(hipMemcpyAsync(y_scaled, r->ysc.p, sizeof(double) * B * R6_M, hipMemcpyDeviceToHost, s));
+    GPMPC_HIP(hipMemcpyAsync(X_pred, r->Xp.p, sizeof(double) * B * (N + 1) * R6_NX, hipMemcpyDeviceToHost, s));
+  if (gp_mean) GPMPC_HIP(hipMemcpyAsync(gp_mean, r->gm.p, sizeof(double) * B * N * 6, hipMemcpyDeviceToHost, s));
+  if (y_scaled) GPMPC_HIP(hipMemcpyAsync(y_scaled, r->ysc.p, sizeof(double) * B * r->M, hipMemcpyDeviceToHost, s));
   if (rho) GPMPC_HIP(hipMemcpyAsync(rho, r->rho.p, sizeof(double) * B, hipMemcpyDeviceToHost, s));
   GPMPC_HIP(hipStreamSynchronize(s));
   return 0;
@@ -1886,9 +645,9 @@ extern "C" int gpmpc_rollout6_set_state(gpmpc_rollout6 *r, const double *U, cons
                                         const double *rho) {
   GPMPC_CHECK_ARG(r);
   hipStream_t s = r->ctx->stream;
-  const size_t B = r->B;
-  if (U) GPMPC_HIP(hipMemcpyAsync(r->U.p, U, sizeof(double) * B * R6_N * R6_NU, hipMemcpyHostToDevice, s));
-  if (y_scaled) GPMPC_HIP(hipMemcpyAsync(r->ysc.p, y_scaled, sizeof(double) * B * R6_M, hipMemcpyHostToDevice, s));
+  const size_t B = r->B, N = r->N;
+  if (U) GPMPC_HIP(hipMemcpyAsync(r->U.p, U, sizeof(double) * B * N * R6_NU, hipMemcpyHostToDevice, s));
+  if (y_scaled) GPMPC_HIP(hipMemcpyAsync(r->ysc.p, y_scaled, sizeof(double) * B * r->M, hipMemcpyHostToDevice, s));
   if (rho) GPMPC_HIP(hipMemcpyAsync(r->rho.p, rho, sizeof(double) * B, hipMemcpyHostToDevice, s));
   GPMPC_HIP(hipStreamSynchronize(s));
   return 0;
@@ -1896,20 +655,7 @@ extern "C" int gpmpc_rollout6_set_state(gpmpc_rollout6 *r, const double *U, cons
 
 extern "C" int gpmpc_rollout6_destroy(gpmpc_rollout6 *r) {
   if (r && r->ctx) (void)hipStreamSynchronize(r->ctx->stream);
-  if (r && r6_stamps_on()) {  // diagnostic: phase cycles of rollout 0, summed over the steps
-    static const char *nm[12] = {"setup", "scaling", "factor0", "rhs", "kkt_forward", "kkt_diagonal",
-                                 "kkt_backward", "update", "checks_adapt", "tail", "factor_gj", "factor_prod"};
-    unsigned long long h[12] = {0};
-    if (hipMemcpyFromSymbol(h, HIP_SYMBOL(g_r6_stamps), sizeof(h)) == hipSuccess) {
-      unsigned long long tot = 0;
-      for (int k = 0; k < 12; ++k) tot += h[k];
-      for (int k = 0; k < 12; ++k)
-        fprintf(stderr, "r6 stamps %-14s %12llu cycles %5.1f%%\n", nm[k], h[k], tot ? 100.0 * h[k] / tot : 0.0);
-    }
-    unsigned long long hp[4] = {0};
-    if (hipMemcpyFromSymbol(hp, HIP_SYMBOL(g_r6p_stamps), sizeof(hp)) == hipSuccess)
-      fprintf(stderr, "r6 predict stamps: kernel rows + rk4 %llu means + next features %llu\n", hp[1], hp[0]);
-  }
+  if (r && r6_stamps_on() && r->impl) r->impl->print_stamps();
   delete r;
   return 0;
 }

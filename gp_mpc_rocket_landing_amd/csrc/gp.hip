@@ -200,7 +200,7 @@ static int core_setup(gpmpc_ctx *ctx, GpCore &g, int kind, const double *X, int 
   const int iso = (kind == GPMPC_SE_ISO);
   g.iso_scale = iso ? 1.0 / (2.0 * ls[0] * ls[0]) : 0.0;
   DevBuf dX;
-  GPMPC_HIP(dX.alloc(sizeof(double) * n * d));
+  GPMPC_HIP(dX.alloc(s, sizeof(double) * n * d));
   GPMPC_HIP(g.ls.alloc(sizeof(double) * d));
   GPMPC_HIP(g.Xs.alloc(sizeof(double) * n * d));
   GPMPC_HIP(g.Xn.alloc(sizeof(double) * n));
@@ -220,11 +220,11 @@ static int core_cross(gpmpc_ctx *ctx, const GpCore &g, const double *dXq_raw, in
   DevBuf a, na;
   DevBuf &A = qs ? *qs : a;
   DevBuf &NA = qn ? *qn : na;
-  GPMPC_HIP(A.alloc(sizeof(double) * p * g.d));
-  GPMPC_HIP(NA.alloc(sizeof(double) * p));
+  GPMPC_HIP(A.alloc(s, sizeof(double) * p * g.d));
+  GPMPC_HIP(NA.alloc(s, sizeof(double) * p));
   GPMPC_HIP(launch_scale_rows(s, dXq_raw, p, g.d, g.ls.as<double>(), g.kind == GPMPC_SE_ISO,
                               A.as<double>(), NA.as<double>()));
-  GPMPC_HIP(Ks.alloc(sizeof(double) * (size_t)p * g.n));
+  GPMPC_HIP(Ks.alloc(s, sizeof(double) * (size_t)p * g.n));
   GPMPC_HIP(launch_gram(s, g.kind, A.as<double>(), NA.as<double>(), p, g.Xs.as<double>(),
                         g.Xn.as<double>(), g.n, g.d, g.sigma2, g.iso_scale, Ks.as<double>(), g.n,
                         0));
@@ -332,6 +332,113 @@ __global__ __launch_bounds__(256) void k_potrs_cols(int n, const double *__restr
   for (int i = tid; i < n; i += 256) Y[(int64_t)i * n_out + c] = x[i];
 }
 
+// ---------------------------------------------------------------------------
+// cho_solve through the inverse the fit forms anyway (exact fits, W = L^-1):
+//   alpha1 = W^T (W y);  r = y - L (L^T alpha1);  alpha = alpha1 + W^T (W r)
+// One step of iterative refinement against the factor makes the explicit-inverse
+// solve as accurate as the two substitutions (exact_gp.py:179, cho_solve); six
+// triangular matrix x (n x nc) products that fill the device instead of one
+// serial substitution per output column on one CU (k_potrs_cols, ~0.77 ms at n = 1000).
+// Both forms sum in a fixed order (no atomics): results are bit-reproducible.
+
+// y = base + sgn * T x   (T lower n x n, row-major; x, y, base n x nc row-major, nc <= 16):
+// one wave per row, lanes striding the row's columns, then a wave reduction
+__global__ __launch_bounds__(256) void k_trmv_n(int n, int nc, const double *__restrict__ T, int64_t ldt,
+                                                const double *__restrict__ x, const double *__restrict__ base,
+                                                double sgn, double *__restrict__ y) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (row >= n) return;
+  double acc[16];
+#pragma unroll
+  for (int c = 0; c < 16; ++c) acc[c] = 0.0;
+  const double *tr = T + (int64_t)row * ldt;
+  for (int j = lane; j <= row; j += 64) {
+    const double t = tr[j];
+#pragma unroll
+    for (int c = 0; c < 16; ++c)
+      if (c < nc) acc[c] = fma(t, x[(int64_t)j * nc + c], acc[c]);
+  }
+#pragma unroll
+  for (int c = 0; c < 16; ++c) {
+    if (c < nc) {
+      double v = acc[c];
+      for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+      acc[c] = v;
+    }
+  }
+  if (lane < nc) {
+    double v = 0.0;
+#pragma unroll
+    for (int c = 0; c < 16; ++c)
+      if (c == lane) v = acc[c];
+    y[(int64_t)row * nc + lane] = (base ? base[(int64_t)row * nc + lane] : 0.0) + sgn * v;
+  }
+}
+
+// partial sums of T^T x over 32-row blocks: part[rb][j][c] = sum_{i in rb, i >= j} T[i][j] x[i][c]
+#define TRMV_T_RB 32
+__global__ __launch_bounds__(256) void k_trmv_t_part(int n, int nc, const double *__restrict__ T, int64_t ldt,
+                                                     const double *__restrict__ x, double *__restrict__ part) {
+  const int j = blockIdx.x * 256 + threadIdx.x, rb = blockIdx.y;
+  const int i0 = rb * TRMV_T_RB, i1 = min(n, i0 + TRMV_T_RB);
+  if (j >= n) return;
+  double acc[16];
+#pragma unroll
+  for (int c = 0; c < 16; ++c) acc[c] = 0.0;
+  for (int i = max(i0, j); i < i1; ++i) {
+    const double t = T[(int64_t)i * ldt + j];
+#pragma unroll
+    for (int c = 0; c < 16; ++c)
+      if (c < nc) acc[c] = fma(t, x[(int64_t)i * nc + c], acc[c]);
+  }
+#pragma unroll
+  for (int c = 0; c < 16; ++c)
+    if (c < nc) part[((int64_t)rb * n + j) * nc + c] = acc[c];
+}
+
+// y = base + sgn * sum_rb part[rb]   (row blocks summed in order)
+__global__ void k_trmv_t_sum(int n, int nc, int nrb, const double *__restrict__ part,
+                             const double *__restrict__ base, double sgn, double *__restrict__ y) {
+  const int e = blockIdx.x * 256 + threadIdx.x;
+  if (e >= n * nc) return;
+  const int j = e / nc;
+  double v = 0.0;
+  for (int rb = j / TRMV_T_RB; rb < nrb; ++rb) v += part[(int64_t)rb * n * nc + e];
+  y[e] = (base ? base[e] : 0.0) + sgn * v;
+}
+
+static hipError_t launch_trmv(hipStream_t s, int trans, int n, int nc, const double *T, int64_t ldt,
+                              const double *x, const double *base, double sgn, double *y, double *part) {
+  if (!trans) {
+    hipLaunchKernelGGL(k_trmv_n, dim3((n + 3) / 4), dim3(256), 0, s, n, nc, T, ldt, x, base, sgn, y);
+  } else {
+    const int nrb = (n + TRMV_T_RB - 1) / TRMV_T_RB;
+    hipLaunchKernelGGL(k_trmv_t_part, dim3((n + 255) / 256, nrb), dim3(256), 0, s, n, nc, T, ldt, x, part);
+    hipLaunchKernelGGL(k_trmv_t_sum, dim3((n * nc + 255) / 256), dim3(256), 0, s, n, nc, nrb, part, base,
+                       sgn, y);
+  }
+  return hipGetLastError();
+}
+
+// Y (n x nc, in place) <- (L L^T)^-1 Y with W = L^-1 formed; scratch from the stream pool
+static hipError_t cho_solve_inv(hipStream_t s, int n, int nc, const double *L, const double *W, double *Y) {
+  const int nrb = (n + TRMV_T_RB - 1) / TRMV_T_RB;
+  DevBuf v, a1, t, part;
+  hipError_t e;
+  if ((e = v.alloc(s, sizeof(double) * n * nc)) || (e = a1.alloc(s, sizeof(double) * n * nc)) ||
+      (e = t.alloc(s, sizeof(double) * n * nc)) || (e = part.alloc(s, sizeof(double) * (size_t)nrb * n * nc)))
+    return e;
+  double *pv = v.as<double>(), *pa = a1.as<double>(), *pt = t.as<double>(), *pp = part.as<double>();
+  if ((e = launch_trmv(s, 0, n, nc, W, n, Y, nullptr, 1.0, pv, pp)) ||       // v = W y
+      (e = launch_trmv(s, 1, n, nc, W, n, pv, nullptr, 1.0, pa, pp)) ||      // alpha1 = W^T v
+      (e = launch_trmv(s, 1, n, nc, L, n, pa, nullptr, 1.0, pt, pp)) ||      // t = L^T alpha1
+      (e = launch_trmv(s, 0, n, nc, L, n, pt, Y, -1.0, pv, pp)) ||           // r = y - L t
+      (e = launch_trmv(s, 0, n, nc, W, n, pv, nullptr, 1.0, pt, pp)) ||      // w = W r
+      (e = launch_trmv(s, 1, n, nc, W, n, pt, pa, 1.0, Y, pp)))              // alpha = alpha1 + W^T w
+    return e;
+  return hipSuccess;
+}
+
 static bool potrs_cols_ok(int n) {
   static const int env = [] {
     const char *e = getenv("GPMPC_POTRS_COLS");
@@ -358,9 +465,9 @@ extern "C" int gpmpc_gp_fit_exact(gpmpc_ctx *ctx, int kind, const double *X, int
   if (rc) { delete gp; return rc; }
   DevBuf Kn, dinfo;
   auto fail = [&](int code) { delete gp; return code; };
-  if (Kn.alloc(sizeof(double) * (size_t)n * n) != hipSuccess ||
+  if (Kn.alloc(s, sizeof(double) * (size_t)n * n) != hipSuccess ||
       gp->L.alloc(sizeof(double) * (size_t)n * n) != hipSuccess ||
-      dinfo.alloc(sizeof(int)) != hipSuccess) {
+      dinfo.alloc(s, sizeof(int)) != hipSuccess) {
     gpmpc_set_error("gp_fit_exact: out of device memory");
     return fail(-1);
   }
@@ -389,6 +496,7 @@ extern "C" int gpmpc_gp_fit_exact(gpmpc_ctx *ctx, int kind, const double *X, int
       return fail(-1);
     }
     if (info == 0) break;
+    if (info < 0) return fail(gpmpc_potrf_info_error(info, "gp_fit_exact"));
     jit = (steps == 0) ? 1e-6 : jit * 10;
     if (!(jit < 1.0)) {
       gpmpc_set_error("Kernel matrix is not positive definite even with jitter");
@@ -400,8 +508,8 @@ extern "C" int gpmpc_gp_fit_exact(gpmpc_ctx *ctx, int kind, const double *X, int
   gp->jitter_steps = steps;
   // normalised targets, alpha = L^-T L^-1 y for all outputs (exact_gp.py:141-150, 179)
   DevBuf dYraw, dY, dyn, dlml;
-  if (dYraw.alloc(sizeof(double) * n * n_out) || dY.alloc(sizeof(double) * n * n_out) ||
-      dyn.alloc(sizeof(double) * n * n_out) || dlml.alloc(sizeof(double) * n_out) ||
+  if (dYraw.alloc(s, sizeof(double) * n * n_out) || dY.alloc(s, sizeof(double) * n * n_out) ||
+      dyn.alloc(s, sizeof(double) * n * n_out) || dlml.alloc(s, sizeof(double) * n_out) ||
       g.ymean.alloc(sizeof(double) * n_out) || g.ystd.alloc(sizeof(double) * n_out) ||
       g.alphaT.alloc(sizeof(double) * n_out * n) ||
       g.W.alloc(sizeof(double) * (size_t)(n + n_out) * n))  // [W; alpha^T]
@@ -411,27 +519,49 @@ extern "C" int gpmpc_gp_fit_exact(gpmpc_ctx *ctx, int kind, const double *X, int
   hipLaunchKernelGGL(k_normalise, dim3(n_out), dim3(256), 0, s, n, n_out, dYraw.as<double>(),
                      dyn.as<double>(), g.ymean.as<double>(), g.ystd.as<double>());
   hipMemcpyAsync(dY.p, dyn.p, sizeof(double) * n * n_out, hipMemcpyDeviceToDevice, s);
-  if (potrs_cols_ok(n)) {
-    hipLaunchKernelGGL(k_potrs_cols, dim3(n_out), dim3(256), sizeof(double) * n, s, n,
-                       gp->L.as<double>(), (int64_t)n, dY.as<double>(), n_out);
-  } else {
-    launch_trsm_lower_ex(s, n, n_out, gp->L.as<double>(), n, dY.as<double>(), n_out, 0, 0, nullptr);
-    launch_trsm_lower_ex(s, n, n_out, gp->L.as<double>(), n, dY.as<double>(), n_out, 1, 0, nullptr);
-  }
-  // log marginal likelihood per output + alpha^T for the posterior GEMM (exact_gp.py:186-204)
-  hipLaunchKernelGGL(k_lml_exact, dim3(n_out), dim3(256), 0, s, n, n_out, gp->L.as<double>(),
-                     dyn.as<double>(), dY.as<double>(), g.alphaT.as<double>(), dlml.as<double>());
-  // W = L^-1 (identity right-hand side, lower-triangular result)
+  // W = L^-1 (identity right-hand side, lower-triangular result): the doubling inverse,
+  // or the blocked TRSM (GPMPC_TRI_INV=0, n <= 128)
   hipLaunchKernelGGL(k_eye, dim3((n + 255) / 256, n), dim3(256), 0, s, n, g.W.as<double>());
   static const int tri_inv_env = [] {
     const char *e = getenv("GPMPC_TRI_INV");
     return e ? atoi(e) : 1;
   }();
-  DevBuf tinv;
-  if (tri_inv_env && n > 128 && tinv.alloc(sizeof(double) * (size_t)n * n) == hipSuccess)
-    launch_tri_inverse(s, n, gp->L.as<double>(), n, g.W.as<double>(), n, tinv.as<double>());
-  else
-    launch_trsm_lower_ex(s, n, n, gp->L.as<double>(), n, g.W.as<double>(), n, 0, 1, nullptr);
+  const bool inv = tri_inv_env && n > 128;
+  {
+    DevBuf tinv;
+    hipError_t e = inv ? tinv.alloc(s, sizeof(double) * (size_t)n * n) : hipSuccess;
+    if (e == hipSuccess)
+      e = inv ? launch_tri_inverse(s, n, gp->L.as<double>(), n, g.W.as<double>(), n, tinv.as<double>())
+              : launch_trsm_lower_ex(s, n, n, gp->L.as<double>(), n, g.W.as<double>(), n, 0, 1, nullptr);
+    if (e != hipSuccess) {
+      gpmpc_set_error("gp_fit_exact: W = L^-1 failed: %s", hipGetErrorString(e));
+      return fail(-1);
+    }
+  }
+  // alpha = L^-T L^-1 y for all outputs: through W with one refinement step
+  // (GPMPC_ALPHA_INV=0: the per-column substitution kernel, or the blocked TRSMs)
+  static const int alpha_inv_env = [] {
+    const char *e = getenv("GPMPC_ALPHA_INV");
+    return e ? atoi(e) : 1;
+  }();
+  hipError_t ea = hipSuccess;
+  if (alpha_inv_env) {
+    ea = cho_solve_inv(s, n, n_out, gp->L.as<double>(), g.W.as<double>(), dY.as<double>());
+  } else if (potrs_cols_ok(n)) {
+    hipLaunchKernelGGL(k_potrs_cols, dim3(n_out), dim3(256), sizeof(double) * n, s, n,
+                       gp->L.as<double>(), (int64_t)n, dY.as<double>(), n_out);
+  } else {
+    ea = launch_trsm_lower_ex(s, n, n_out, gp->L.as<double>(), n, dY.as<double>(), n_out, 0, 0, nullptr);
+    if (ea == hipSuccess)
+      ea = launch_trsm_lower_ex(s, n, n_out, gp->L.as<double>(), n, dY.as<double>(), n_out, 1, 0, nullptr);
+  }
+  if (ea != hipSuccess) {
+    gpmpc_set_error("gp_fit_exact: alpha solve failed: %s", hipGetErrorString(ea));
+    return fail(-1);
+  }
+  // log marginal likelihood per output + alpha^T for the posterior GEMM (exact_gp.py:186-204)
+  hipLaunchKernelGGL(k_lml_exact, dim3(n_out), dim3(256), 0, s, n, n_out, gp->L.as<double>(),
+                     dyn.as<double>(), dY.as<double>(), g.alphaT.as<double>(), dlml.as<double>());
   // alpha^T below W: the variance GEMM produces the posterior mean in the same pass
   hipMemcpyAsync(g.W.as<double>() + (size_t)n * n, g.alphaT.p, sizeof(double) * n_out * n,
                  hipMemcpyDeviceToDevice, s);
@@ -460,8 +590,8 @@ static int core_posterior(gpmpc_ctx *ctx, const GpCore &g, const double *Ks, int
   hipStream_t s = ctx->stream;
   const int nrt = gemm_row_tiles(g.n + g.n_out, p, g.n);
   DevBuf part, meanT;
-  GPMPC_HIP(part.alloc(sizeof(double) * (size_t)nrt * p));
-  GPMPC_HIP(meanT.alloc(sizeof(double) * (size_t)g.n_out * p));
+  GPMPC_HIP(part.alloc(s, sizeof(double) * (size_t)nrt * p));
+  GPMPC_HIP(meanT.alloc(s, sizeof(double) * (size_t)g.n_out * p));
   // one pass over K*: sum_i (W K*^T)_ij^2 per query j and alpha^T K*^T
   GPMPC_HIP(launch_gemm_sumsq_mean(s, g.n, g.n_out, p, g.W.as<double>(), Ks, part.as<double>(), p,
                                    meanT.as<double>(), p));
@@ -481,12 +611,12 @@ extern "C" int gpmpc_gp_predict(gpmpc_ctx *ctx, gpmpc_gp *gp, const double *Xq, 
   hipStream_t s = ctx->stream;
   const GpCore &g = gp->core;
   DevBuf dq, Ks, dmean, dvar;
-  GPMPC_HIP(dq.alloc(sizeof(double) * p * g.d));
+  GPMPC_HIP(dq.alloc(s, sizeof(double) * p * g.d));
   GPMPC_HIP(hipMemcpyAsync(dq.p, Xq, sizeof(double) * p * g.d, hipMemcpyHostToDevice, s));
   int rc = core_cross(ctx, g, dq.as<double>(), p, Ks);
   if (rc) return rc;
-  GPMPC_HIP(dmean.alloc(sizeof(double) * p * g.n_out));
-  GPMPC_HIP(dvar.alloc(sizeof(double) * p * g.n_out));
+  GPMPC_HIP(dmean.alloc(s, sizeof(double) * p * g.n_out));
+  GPMPC_HIP(dvar.alloc(s, sizeof(double) * p * g.n_out));
   rc = core_posterior(ctx, g, Ks.as<double>(), p, dmean.as<double>(), dvar.as<double>());
   if (rc) return rc;
   GPMPC_HIP(hipMemcpyAsync(mean, dmean.p, sizeof(double) * p * g.n_out, hipMemcpyDeviceToHost, s));
@@ -503,22 +633,22 @@ extern "C" int gpmpc_gp_predict_cov(gpmpc_ctx *ctx, gpmpc_gp *gp, const double *
   hipStream_t s = ctx->stream;
   const GpCore &g = gp->core;
   DevBuf dq, Ks, qs, qn, V, C, dmean, dvar;
-  GPMPC_HIP(dq.alloc(sizeof(double) * p * g.d));
+  GPMPC_HIP(dq.alloc(s, sizeof(double) * p * g.d));
   GPMPC_HIP(hipMemcpyAsync(dq.p, Xq, sizeof(double) * p * g.d, hipMemcpyHostToDevice, s));
   int rc = core_cross(ctx, g, dq.as<double>(), p, Ks, &qs, &qn);
   if (rc) return rc;
   // V^T = K* W^T  (p x n):  (V^T)_{jm} = sum_i K*_{ji} W_{mi}
-  GPMPC_HIP(V.alloc(sizeof(double) * (size_t)p * g.n));
+  GPMPC_HIP(V.alloc(s, sizeof(double) * (size_t)p * g.n));
   GPMPC_HIP(launch_gemm_nt(s, EPI_STORE, p, g.n, g.n, Ks.as<double>(), g.n, g.W.as<double>(), g.n,
                            V.as<double>(), g.n, 1.0, 0.0, 0, 0, 1, 0, 0, 0));
   // C = K** - V^T V   (exact_gp.py:250-252), in normalised units
-  GPMPC_HIP(C.alloc(sizeof(double) * (size_t)p * p));
+  GPMPC_HIP(C.alloc(s, sizeof(double) * (size_t)p * p));
   GPMPC_HIP(launch_gram(s, g.kind, qs.as<double>(), qn.as<double>(), p, qs.as<double>(),
                         qn.as<double>(), p, g.d, g.sigma2, g.iso_scale, C.as<double>(), p, 0));
   GPMPC_HIP(launch_gemm_nt(s, EPI_STORE, p, p, g.n, V.as<double>(), g.n, V.as<double>(), g.n,
                            C.as<double>(), p, -1.0, 1.0, 0, 0, 1, 0, 0, 0));
-  GPMPC_HIP(dmean.alloc(sizeof(double) * p * g.n_out));
-  GPMPC_HIP(dvar.alloc(sizeof(double) * p * g.n_out));
+  GPMPC_HIP(dmean.alloc(s, sizeof(double) * p * g.n_out));
+  GPMPC_HIP(dvar.alloc(s, sizeof(double) * p * g.n_out));
   rc = core_posterior(ctx, g, Ks.as<double>(), p, dmean.as<double>(), dvar.as<double>());
   if (rc) return rc;
   GPMPC_HIP(hipMemcpyAsync(mean, dmean.p, sizeof(double) * p * g.n_out, hipMemcpyDeviceToHost, s));
@@ -534,7 +664,7 @@ extern "C" int gpmpc_gp_get_state(gpmpc_ctx *ctx, gpmpc_gp *gp, double *L, doubl
   const int n = gp->core.n, no = gp->core.n_out;
   if (L) {
     DevBuf t;
-    GPMPC_HIP(t.alloc(sizeof(double) * (size_t)n * n));
+    GPMPC_HIP(t.alloc(s, sizeof(double) * (size_t)n * n));
     GPMPC_HIP(launch_copy_lower(s, n, gp->L.as<double>(), n, t.as<double>(), n));
     GPMPC_HIP(hipMemcpyAsync(L, t.p, sizeof(double) * (size_t)n * n, hipMemcpyDeviceToHost, s));
     GPMPC_HIP(hipStreamSynchronize(s));
@@ -651,11 +781,11 @@ static int vfe_tail(gpmpc_ctx *ctx, gpmpc_fitc *gp, DevBuf &Luu, DevBuf &Kuf, De
   const int m = gp->m;
   auto fail = [&](int code) { delete gp; return code; };
   DevBuf Kuu, q, dYraw, dyn, yl, sig, cvec, alpha, dlml;
-  if (Kuu.alloc(sizeof(double) * (size_t)m * m) || q.alloc(sizeof(double) * n) ||
-      dYraw.alloc(sizeof(double) * n * n_out) || dyn.alloc(sizeof(double) * n * n_out) ||
-      yl.alloc(sizeof(double) * n * n_out) || sig.alloc(sizeof(double) * n) ||
-      cvec.alloc(sizeof(double) * m * n_out) || alpha.alloc(sizeof(double) * m * n_out) ||
-      dlml.alloc(sizeof(double) * n_out) || g.ymean.alloc(sizeof(double) * n_out) ||
+  if (Kuu.alloc(s, sizeof(double) * (size_t)m * m) || q.alloc(s, sizeof(double) * n) ||
+      dYraw.alloc(s, sizeof(double) * n * n_out) || dyn.alloc(s, sizeof(double) * n * n_out) ||
+      yl.alloc(s, sizeof(double) * n * n_out) || sig.alloc(s, sizeof(double) * n) ||
+      cvec.alloc(s, sizeof(double) * m * n_out) || alpha.alloc(s, sizeof(double) * m * n_out) ||
+      dlml.alloc(s, sizeof(double) * n_out) || g.ymean.alloc(sizeof(double) * n_out) ||
       g.ystd.alloc(sizeof(double) * n_out) || g.alphaT.alloc(sizeof(double) * n_out * m)) {
     gpmpc_set_error("vfe_fit: out of device memory");
     return fail(-1);
@@ -686,10 +816,7 @@ static int vfe_tail(gpmpc_ctx *ctx, gpmpc_fitc *gp, DevBuf &Luu, DevBuf &Kuf, De
   launch_potrf_batched(s, m, 1, B.as<double>(), m, 0, dinfo.as<int>());
   hipMemcpyAsync(&info, dinfo.p, sizeof(int), hipMemcpyDeviceToHost, s);
   GPMPC_HIP(hipStreamSynchronize(s));
-  if (info) {
-    gpmpc_set_error("Matrix is not positive definite (B, column %d)", info);
-    return fail(info);
-  }
+  if (info) return fail(gpmpc_potrf_info_error(info, "B"));
   // W2 = L_B^-1 L_uu^-1: the predict's w = L_B^-1 v as the reference writes it for both
   // methods (sparse_gp.py:292-296)
   hipMemcpyAsync(gp->W2.p, g.W.p, sizeof(double) * (size_t)m * m, hipMemcpyDeviceToDevice, s);
@@ -746,10 +873,10 @@ static int sparse_fit(gpmpc_ctx *ctx, const double *Z, int m, const double *X, i
   if (rc) { delete gp; return rc; }
   auto fail = [&](int code) { delete gp; return code; };
   DevBuf dX, Kuf, Luu, B, dinfo, lam, Xs, Xn, part;
-  if (dX.alloc(sizeof(double) * n * d) || Kuf.alloc(sizeof(double) * (size_t)m * n) ||
-      Luu.alloc(sizeof(double) * (size_t)m * m) || B.alloc(sizeof(double) * (size_t)m * m) ||
-      dinfo.alloc(sizeof(int)) || lam.alloc(sizeof(double) * n) ||
-      Xs.alloc(sizeof(double) * n * d) || Xn.alloc(sizeof(double) * n) ||
+  if (dX.alloc(s, sizeof(double) * n * d) || Kuf.alloc(s, sizeof(double) * (size_t)m * n) ||
+      Luu.alloc(s, sizeof(double) * (size_t)m * m) || B.alloc(s, sizeof(double) * (size_t)m * m) ||
+      dinfo.alloc(s, sizeof(int)) || lam.alloc(s, sizeof(double) * n) ||
+      Xs.alloc(s, sizeof(double) * n * d) || Xn.alloc(s, sizeof(double) * n) ||
       g.W.alloc(sizeof(double) * (size_t)(m + n_out) * m) ||  // [L_uu^-1; alpha^T]
       gp->W2.alloc(sizeof(double) * (size_t)m * m)) {
     gpmpc_set_error("fitc_fit: out of device memory");
@@ -766,30 +893,32 @@ static int sparse_fit(gpmpc_ctx *ctx, const double *Z, int m, const double *X, i
   launch_potrf_batched(s, m, 1, Luu.as<double>(), m, 0, dinfo.as<int>());
   hipMemcpyAsync(&info, dinfo.p, sizeof(int), hipMemcpyDeviceToHost, s);
   GPMPC_HIP(hipStreamSynchronize(s));
-  if (info) {
-    gpmpc_set_error("Matrix is not positive definite (K_uu, column %d)", info);
-    return fail(info);
-  }
+  if (info) return fail(gpmpc_potrf_info_error(info, "K_uu"));
   // A = L_uu^-1 K_uf  (m x n); VFE forms B and c from K_uf itself first
   launch_gram(s, GPMPC_SE_ARD, g.Xs.as<double>(), g.Xn.as<double>(), m, Xs.as<double>(),
               Xn.as<double>(), n, d, sigma2, 0.0, Kuf.as<double>(), n, 0);
   hipLaunchKernelGGL(k_eye, dim3((m + 255) / 256, m), dim3(256), 0, s, m, g.W.as<double>());
   {
     DevBuf tinv;  // W = L_uu^-1 by the doubling inverse (exact fit's W, §10)
-    if (m > 128 && tinv.alloc(sizeof(double) * (size_t)m * m) == hipSuccess)
-      launch_tri_inverse(s, m, Luu.as<double>(), m, g.W.as<double>(), m, tinv.as<double>());
-    else
-      launch_trsm_lower_ex(s, m, m, Luu.as<double>(), m, g.W.as<double>(), m, 0, 1, nullptr);
+    const bool inv = m > 128;
+    hipError_t e = inv ? tinv.alloc(s, sizeof(double) * (size_t)m * m) : hipSuccess;
+    if (e == hipSuccess)
+      e = inv ? launch_tri_inverse(s, m, Luu.as<double>(), m, g.W.as<double>(), m, tinv.as<double>())
+              : launch_trsm_lower_ex(s, m, m, Luu.as<double>(), m, g.W.as<double>(), m, 0, 1, nullptr);
+    if (e != hipSuccess) {
+      gpmpc_set_error("sparse fit: W = L_uu^-1 failed: %s", hipGetErrorString(e));
+      return fail(-1);
+    }
   }
   if (vfe) return vfe_tail(ctx, gp, Luu, Kuf, B, dinfo, Y, n, n_out, sigma2, noise, jitter, out,
                            y_mean, y_std, lml);
   launch_trsm_lower_ex(s, m, n, Luu.as<double>(), m, Kuf.as<double>(), n, 0, 0, nullptr);
   // normalised targets; c = A (y / Lambda) before A is rescaled  (sparse_gp.py:160-166, 204)
   DevBuf isq, dYraw, dyn, yl, cvec, alpha, dlml;
-  if (isq.alloc(sizeof(double) * n) || dYraw.alloc(sizeof(double) * n * n_out) ||
-      dyn.alloc(sizeof(double) * n * n_out) || yl.alloc(sizeof(double) * n * n_out) ||
-      cvec.alloc(sizeof(double) * m * n_out) || alpha.alloc(sizeof(double) * m * n_out) ||
-      dlml.alloc(sizeof(double) * n_out) || g.ymean.alloc(sizeof(double) * n_out) ||
+  if (isq.alloc(s, sizeof(double) * n) || dYraw.alloc(s, sizeof(double) * n * n_out) ||
+      dyn.alloc(s, sizeof(double) * n * n_out) || yl.alloc(s, sizeof(double) * n * n_out) ||
+      cvec.alloc(s, sizeof(double) * m * n_out) || alpha.alloc(s, sizeof(double) * m * n_out) ||
+      dlml.alloc(s, sizeof(double) * n_out) || g.ymean.alloc(sizeof(double) * n_out) ||
       g.ystd.alloc(sizeof(double) * n_out) || g.alphaT.alloc(sizeof(double) * n_out * m))
     return fail(-1);
   g.n_out = n_out;
@@ -813,10 +942,7 @@ static int sparse_fit(gpmpc_ctx *ctx, const double *Z, int m, const double *X, i
   launch_potrf_batched(s, m, 1, B.as<double>(), m, 0, dinfo.as<int>());
   hipMemcpyAsync(&info, dinfo.p, sizeof(int), hipMemcpyDeviceToHost, s);
   GPMPC_HIP(hipStreamSynchronize(s));
-  if (info) {
-    gpmpc_set_error("Matrix is not positive definite (B, column %d)", info);
-    return fail(info);
-  }
+  if (info) return fail(gpmpc_potrf_info_error(info, "B"));
   // W2 = L_B^-1 L_uu^-1 (a lower right-hand side): the predict gets |w|^2 from one
   // triangular pass over K*u instead of storing v = L_uu^-1 K*u^T and solving again
   hipMemcpyAsync(gp->W2.p, g.W.p, sizeof(double) * (size_t)m * m, hipMemcpyDeviceToDevice, s);
@@ -882,21 +1008,21 @@ extern "C" int gpmpc_fitc_predict(gpmpc_ctx *ctx, gpmpc_fitc *gp, const double *
   const GpCore &g = gp->core;
   const int m = gp->m;
   DevBuf dq, Ks, pv, pw, meanT, dmean, dvar;
-  GPMPC_HIP(dq.alloc(sizeof(double) * p * g.d));
+  GPMPC_HIP(dq.alloc(s, sizeof(double) * p * g.d));
   GPMPC_HIP(hipMemcpyAsync(dq.p, Xq, sizeof(double) * p * g.d, hipMemcpyHostToDevice, s));
   int rc = core_cross(ctx, g, dq.as<double>(), p, Ks);  // K*u (p x m)
   if (rc) return rc;
   const int nrv = gemm_row_tiles(m + g.n_out, p, m), nrw = gemm_row_tiles(m, p, m);
-  GPMPC_HIP(pv.alloc(sizeof(double) * (size_t)nrv * p));
-  GPMPC_HIP(pw.alloc(sizeof(double) * (size_t)nrw * p));
-  GPMPC_HIP(meanT.alloc(sizeof(double) * (size_t)g.n_out * p));
+  GPMPC_HIP(pv.alloc(s, sizeof(double) * (size_t)nrv * p));
+  GPMPC_HIP(pw.alloc(s, sizeof(double) * (size_t)nrw * p));
+  GPMPC_HIP(meanT.alloc(s, sizeof(double) * (size_t)g.n_out * p));
   // |v|^2 = |L_uu^-1 k*|^2 and the mean alpha^T k* in one pass; |w|^2 = |W2 k*|^2
   GPMPC_HIP(launch_gemm_sumsq_mean(s, m, g.n_out, p, g.W.as<double>(), Ks.as<double>(),
                                    pv.as<double>(), p, meanT.as<double>(), p));
   GPMPC_HIP(launch_gemm_nt(s, EPI_SUMSQ, m, p, m, gp->W2.as<double>(), m, Ks.as<double>(), m,
                            pw.as<double>(), p, 1.0, 0.0, 1, 0, 1, 0, 0, 0));
-  GPMPC_HIP(dmean.alloc(sizeof(double) * p * g.n_out));
-  GPMPC_HIP(dvar.alloc(sizeof(double) * p * g.n_out));
+  GPMPC_HIP(dmean.alloc(s, sizeof(double) * p * g.n_out));
+  GPMPC_HIP(dvar.alloc(s, sizeof(double) * p * g.n_out));
   hipLaunchKernelGGL(k_fitc_finish, dim3((p + 255) / 256), dim3(256), 0, s, p, g.n_out, nrv, nrw,
                      pv.as<double>(), pw.as<double>(), (int64_t)p, meanT.as<double>(), (int64_t)p,
                      g.ymean.as<double>(), g.ystd.as<double>(), g.sigma2, dmean.as<double>(),
@@ -999,14 +1125,14 @@ extern "C" int gpmpc_gp_lml_batched(gpmpc_ctx *ctx, int kind, const double *X, i
   const int iso = (kind == GPMPC_SE_ISO);
   const size_t nn = (size_t)n * n;
   DevBuf dX, dY, dyn, dm, dsd, dls, Xs, Xn, dinfo, dlml;
-  GPMPC_HIP(dX.alloc(sizeof(double) * n * d));
-  GPMPC_HIP(dY.alloc(sizeof(double) * n));
-  GPMPC_HIP(dyn.alloc(sizeof(double) * n));
-  GPMPC_HIP(dm.alloc(sizeof(double)));
-  GPMPC_HIP(dsd.alloc(sizeof(double)));
-  GPMPC_HIP(dls.alloc(sizeof(double) * B * d));
-  GPMPC_HIP(Xs.alloc(sizeof(double) * (size_t)B * n * d));
-  GPMPC_HIP(Xn.alloc(sizeof(double) * (size_t)B * n));
+  GPMPC_HIP(dX.alloc(s, sizeof(double) * n * d));
+  GPMPC_HIP(dY.alloc(s, sizeof(double) * n));
+  GPMPC_HIP(dyn.alloc(s, sizeof(double) * n));
+  GPMPC_HIP(dm.alloc(s, sizeof(double)));
+  GPMPC_HIP(dsd.alloc(s, sizeof(double)));
+  GPMPC_HIP(dls.alloc(s, sizeof(double) * B * d));
+  GPMPC_HIP(Xs.alloc(s, sizeof(double) * (size_t)B * n * d));
+  GPMPC_HIP(Xn.alloc(s, sizeof(double) * (size_t)B * n));
   // the B Gram / factor matrices live in persistent scratch (slot 3): one
   // optimiser gradient per call, so a per-call hipMalloc of B n^2 doubles
   // (112 MB at n = 1000) would cost more than the factorisations
@@ -1015,8 +1141,8 @@ extern "C" int gpmpc_gp_lml_batched(gpmpc_ctx *ctx, int kind, const double *X, i
     gpmpc_set_error("gp_lml_batched: out of device memory for %d x %d^2 doubles", B, n);
     return -1;
   }
-  GPMPC_HIP(dinfo.alloc(sizeof(int) * B));
-  GPMPC_HIP(dlml.alloc(sizeof(double) * B));
+  GPMPC_HIP(dinfo.alloc(s, sizeof(int) * B));
+  GPMPC_HIP(dlml.alloc(s, sizeof(double) * B));
   GPMPC_HIP(hipMemcpyAsync(dX.p, X, sizeof(double) * n * d, hipMemcpyHostToDevice, s));
   GPMPC_HIP(hipMemcpyAsync(dY.p, y, sizeof(double) * n, hipMemcpyHostToDevice, s));
   GPMPC_HIP(hipMemcpyAsync(dls.p, ls, sizeof(double) * B * d, hipMemcpyHostToDevice, s));
@@ -1046,6 +1172,7 @@ extern "C" int gpmpc_gp_lml_batched(gpmpc_ctx *ctx, int kind, const double *X, i
   // jitter ladder (exact_gp.py:163-175) for the sets whose first factorisation failed
   for (int b = 0; b < B; ++b) {
     jitter_steps[b] = 0;
+    if (info[b] < 0) return gpmpc_potrf_info_error(info[b], "gp_lml_batched");
     if (!info[b]) continue;
     double jit = 1e-6;
     int steps = 1, ok = 0;
@@ -1056,6 +1183,7 @@ extern "C" int gpmpc_gp_lml_batched(gpmpc_ctx *ctx, int kind, const double *X, i
       int ib = 0;
       GPMPC_HIP(hipMemcpyAsync(&ib, dinfo.as<int>() + b, sizeof(int), hipMemcpyDeviceToHost, s));
       GPMPC_HIP(hipStreamSynchronize(s));
+      if (ib < 0) return gpmpc_potrf_info_error(ib, "gp_lml_batched");
       if (!ib) { ok = 1; break; }
       jit *= 10;
       ++steps;
@@ -1134,6 +1262,7 @@ extern "C" int gpmpc_gp_append(gpmpc_ctx *ctx, gpmpc_gp *gp, const double *Xnew,
   int info = 0;
   GPMPC_HIP(hipMemcpyAsync(&info, dinfo.p, sizeof(int), hipMemcpyDeviceToHost, s));
   GPMPC_HIP(hipStreamSynchronize(s));
+  if (info < 0) return gpmpc_potrf_info_error(info, "gp_append");
   if (info) {
     gpmpc_set_error("gp_append: Schur complement not positive definite (pivot %d); refit", info);
     return GPMPC_ERR_NOT_PD;

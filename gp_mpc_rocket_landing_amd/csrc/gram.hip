@@ -201,11 +201,11 @@ extern "C" int gpmpc_gram(gpmpc_ctx *ctx, int kind, const double *X1, int n1, co
   const int iso = (kind == GPMPC_SE_ISO);
   const double iso_scale = iso ? 1.0 / (2.0 * ls[0] * ls[0]) : 0.0;
   DevBuf dX1, dX2, dls, da, db, dna, dnb, dK;
-  GPMPC_HIP(dX1.alloc(sizeof(double) * n1 * d));
-  GPMPC_HIP(dls.alloc(sizeof(double) * d));
-  GPMPC_HIP(da.alloc(sizeof(double) * n1 * d));
-  GPMPC_HIP(dna.alloc(sizeof(double) * n1));
-  GPMPC_HIP(dK.alloc(sizeof(double) * (size_t)n1 * n2));
+  GPMPC_HIP(dX1.alloc(s, sizeof(double) * n1 * d));
+  GPMPC_HIP(dls.alloc(s, sizeof(double) * d));
+  GPMPC_HIP(da.alloc(s, sizeof(double) * n1 * d));
+  GPMPC_HIP(dna.alloc(s, sizeof(double) * n1));
+  GPMPC_HIP(dK.alloc(s, sizeof(double) * (size_t)n1 * n2));
   GPMPC_HIP(hipMemcpyAsync(dX1.p, X1, sizeof(double) * n1 * d, hipMemcpyHostToDevice, s));
   // SE_ISO reads one lengthscale (ls[0]); the host array may hold just that one
   GPMPC_HIP(hipMemcpyAsync(dls.p, ls, sizeof(double) * (iso ? 1 : d), hipMemcpyHostToDevice, s));
@@ -213,9 +213,9 @@ extern "C" int gpmpc_gram(gpmpc_ctx *ctx, int kind, const double *X1, int n1, co
                               dna.as<double>()));
   const double *pb = da.as<double>(), *pnb = dna.as<double>();
   if (X2) {
-    GPMPC_HIP(dX2.alloc(sizeof(double) * n2 * d));
-    GPMPC_HIP(db.alloc(sizeof(double) * n2 * d));
-    GPMPC_HIP(dnb.alloc(sizeof(double) * n2));
+    GPMPC_HIP(dX2.alloc(s, sizeof(double) * n2 * d));
+    GPMPC_HIP(db.alloc(s, sizeof(double) * n2 * d));
+    GPMPC_HIP(dnb.alloc(s, sizeof(double) * n2));
     GPMPC_HIP(hipMemcpyAsync(dX2.p, X2, sizeof(double) * n2 * d, hipMemcpyHostToDevice, s));
     GPMPC_HIP(launch_scale_rows(s, dX2.as<double>(), n2, d, dls.as<double>(), iso,
                                 db.as<double>(), dnb.as<double>()));
@@ -277,12 +277,12 @@ extern "C" int gpmpc_gram_grad(gpmpc_ctx *ctx, int kind, const double *X1, int n
   const int ng = iso ? 1 : d;
   const size_t nn = (size_t)n1 * n2;
   DevBuf dX1, dX2, dls, da, db, dna, dnb, dK, dG;
-  GPMPC_HIP(dX1.alloc(sizeof(double) * n1 * d));
-  GPMPC_HIP(dls.alloc(sizeof(double) * d));
-  GPMPC_HIP(da.alloc(sizeof(double) * n1 * d));
-  GPMPC_HIP(dna.alloc(sizeof(double) * n1));
-  GPMPC_HIP(dK.alloc(sizeof(double) * nn));
-  GPMPC_HIP(dG.alloc(sizeof(double) * nn * ng));
+  GPMPC_HIP(dX1.alloc(s, sizeof(double) * n1 * d));
+  GPMPC_HIP(dls.alloc(s, sizeof(double) * d));
+  GPMPC_HIP(da.alloc(s, sizeof(double) * n1 * d));
+  GPMPC_HIP(dna.alloc(s, sizeof(double) * n1));
+  GPMPC_HIP(dK.alloc(s, sizeof(double) * nn));
+  GPMPC_HIP(dG.alloc(s, sizeof(double) * nn * ng));
   GPMPC_HIP(hipMemcpyAsync(dX1.p, X1, sizeof(double) * n1 * d, hipMemcpyHostToDevice, s));
   // SE_ISO reads one lengthscale (ls[0]); the host array may hold just that one
   GPMPC_HIP(hipMemcpyAsync(dls.p, ls, sizeof(double) * (iso ? 1 : d), hipMemcpyHostToDevice, s));
@@ -290,9 +290,9 @@ extern "C" int gpmpc_gram_grad(gpmpc_ctx *ctx, int kind, const double *X1, int n
                               dna.as<double>()));
   const double *pX2 = dX1.as<double>(), *pb = da.as<double>(), *pnb = dna.as<double>();
   if (X2) {
-    GPMPC_HIP(dX2.alloc(sizeof(double) * n2 * d));
-    GPMPC_HIP(db.alloc(sizeof(double) * n2 * d));
-    GPMPC_HIP(dnb.alloc(sizeof(double) * n2));
+    GPMPC_HIP(dX2.alloc(s, sizeof(double) * n2 * d));
+    GPMPC_HIP(db.alloc(s, sizeof(double) * n2 * d));
+    GPMPC_HIP(dnb.alloc(s, sizeof(double) * n2));
     GPMPC_HIP(hipMemcpyAsync(dX2.p, X2, sizeof(double) * n2 * d, hipMemcpyHostToDevice, s));
     GPMPC_HIP(launch_scale_rows(s, dX2.as<double>(), n2, d, dls.as<double>(), iso,
                                 db.as<double>(), dnb.as<double>()));

@@ -36,15 +36,49 @@ void *gpmpc_scratch(hipStream_t s, int slot, size_t bytes);
     }                                                            \
   } while (0)
 
-// RAII device buffer (host-side bookkeeping only)
+// Per-stream caching pool for the temporaries of host-boundary calls (fits, predicts,
+// solves): a released block goes back to its stream's free list instead of hipFree
+// (an implicit device-wide synchronisation, ~41 us a call: ~15 per exact fit, DESIGN
+// §11).  A block is handed out again only on the stream it was last used on, so that
+// stream's order keeps its earlier readers ahead of the next writer.  Blocks are sized
+// in classes (<= 12.5% rounding), cached up to a per-stream cap, and released with the
+// context (gpmpc_ctx_destroy).
+void *gpmpc_pool_get(hipStream_t s, size_t bytes, size_t *cls);
+void gpmpc_pool_put(hipStream_t s, void *p, size_t cls);
+
+// RAII device buffer (host-side bookkeeping only).  alloc(bytes): its own hipMalloc
+// (handle-owned state that outlives the call); alloc(stream, bytes): a pooled
+// temporary of that stream.
 struct DevBuf {
   void *p = nullptr;
   size_t bytes = 0;
-  ~DevBuf() { if (p) (void)hipFree(p); }
+  hipStream_t pool = nullptr;  // non-null: pooled on this stream
+  size_t cls = 0;
+  DevBuf() = default;
+  DevBuf(const DevBuf &) = delete;
+  DevBuf &operator=(const DevBuf &) = delete;
+  ~DevBuf() { release(); }
+  void release() {
+    if (p) {
+      if (pool) gpmpc_pool_put(pool, p, cls);
+      else (void)hipFree(p);
+    }
+    p = nullptr;
+    pool = nullptr;
+  }
   hipError_t alloc(size_t b) {
-    if (p) { (void)hipFree(p); p = nullptr; }
+    release();
     bytes = b;
     return b ? hipMalloc(&p, b) : hipSuccess;
+  }
+  hipError_t alloc(hipStream_t s, size_t b) {
+    release();
+    bytes = b;
+    if (!b) return hipSuccess;
+    p = gpmpc_pool_get(s, b, &cls);
+    if (!p) return hipErrorOutOfMemory;
+    pool = s;
+    return hipSuccess;
   }
   template <class T> T *as() const { return static_cast<T *>(p); }
 };
@@ -82,6 +116,11 @@ hipError_t launch_scale_rows(hipStream_t s, const double *X, int n, int d, const
 // blocked Cholesky of batch matrices; info (device int[batch]), 1-based pivot
 hipError_t launch_potrf_batched(hipStream_t s, int n, int batch, double *A, int64_t lda,
                                 int64_t stride, int *info);
+// info < 0 from the blocked Cholesky: the 128-column diagonal kernel's bounded wait
+// for an LDS step flag expired (a broken invariant, not a non-PD matrix); the factor of
+// that matrix is unreliable and is never reported as success or as a pivot column
+#define GPMPC_POTRF_SWEEP_TIMEOUT (-1)
+int gpmpc_potrf_info_error(int info, const char *what);  // sets the message, returns the code
 // X <- L^-1 X (L lower n x n, X n x nrhs row-major ld ldx), batch via strides
 hipError_t launch_trsm_lower(hipStream_t s, int n, int nrhs, const double *L, int64_t ldl,
                              double *X, int64_t ldx, int transpose_L);

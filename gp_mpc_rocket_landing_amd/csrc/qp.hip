@@ -259,18 +259,18 @@ extern "C" int gpmpc_qp_solve_batched(gpmpc_ctx *ctx, int batch, int n, int m, i
   }
   DevBuf dA, dP, dq, dl, du, dx0, drho, dy0, dxo, dyo, dit, dst, dob;
   const size_t B = batch;
-  GPMPC_HIP(dA.alloc(sizeof(double) * B * nnz));
-  GPMPC_HIP(dP.alloc(sizeof(double) * B * n));
-  GPMPC_HIP(dq.alloc(sizeof(double) * B * n));
-  GPMPC_HIP(dl.alloc(sizeof(double) * B * m));
-  GPMPC_HIP(du.alloc(sizeof(double) * B * m));
-  GPMPC_HIP(drho.alloc(sizeof(double) * B));
-  GPMPC_HIP(dy0.alloc(sizeof(double) * B * m));
-  GPMPC_HIP(dxo.alloc(sizeof(double) * B * n));
-  GPMPC_HIP(dyo.alloc(sizeof(double) * B * m));
-  GPMPC_HIP(dit.alloc(sizeof(int) * B));
-  GPMPC_HIP(dst.alloc(sizeof(int) * B));
-  GPMPC_HIP(dob.alloc(sizeof(double) * B));
+  GPMPC_HIP(dA.alloc(s, sizeof(double) * B * nnz));
+  GPMPC_HIP(dP.alloc(s, sizeof(double) * B * n));
+  GPMPC_HIP(dq.alloc(s, sizeof(double) * B * n));
+  GPMPC_HIP(dl.alloc(s, sizeof(double) * B * m));
+  GPMPC_HIP(du.alloc(s, sizeof(double) * B * m));
+  GPMPC_HIP(drho.alloc(s, sizeof(double) * B));
+  GPMPC_HIP(dy0.alloc(s, sizeof(double) * B * m));
+  GPMPC_HIP(dxo.alloc(s, sizeof(double) * B * n));
+  GPMPC_HIP(dyo.alloc(s, sizeof(double) * B * m));
+  GPMPC_HIP(dit.alloc(s, sizeof(int) * B));
+  GPMPC_HIP(dst.alloc(s, sizeof(int) * B));
+  GPMPC_HIP(dob.alloc(s, sizeof(double) * B));
   GPMPC_HIP(hipMemcpyAsync(dA.p, Aval, sizeof(double) * B * nnz, hipMemcpyHostToDevice, s));
   GPMPC_HIP(hipMemcpyAsync(dP.p, Pdiag, sizeof(double) * B * n, hipMemcpyHostToDevice, s));
   GPMPC_HIP(hipMemcpyAsync(dq.p, q, sizeof(double) * B * n, hipMemcpyHostToDevice, s));
@@ -279,7 +279,7 @@ extern "C" int gpmpc_qp_solve_batched(gpmpc_ctx *ctx, int batch, int n, int m, i
   GPMPC_HIP(hipMemcpyAsync(drho.p, rho, sizeof(double) * B, hipMemcpyHostToDevice, s));
   GPMPC_HIP(hipMemcpyAsync(dy0.p, y_scaled, sizeof(double) * B * m, hipMemcpyHostToDevice, s));
   if (x_ws) {
-    GPMPC_HIP(dx0.alloc(sizeof(double) * B * n));
+    GPMPC_HIP(dx0.alloc(s, sizeof(double) * B * n));
     GPMPC_HIP(hipMemcpyAsync(dx0.p, x_ws, sizeof(double) * B * n, hipMemcpyHostToDevice, s));
   }
   GPMPC_HIP(launch_qp_batched(s, pat.dev, to_dev(*st), batch, dA.as<double>(), dP.as<double>(),

@@ -82,9 +82,9 @@ extern "C" int gpmpc_cov_propagate(gpmpc_ctx *ctx, int batch, int N, int nx, con
   hipStream_t s = ctx->stream;
   const size_t mat = (size_t)nx * nx;
   DevBuf dA, dq, dS, dout;
-  GPMPC_HIP(dA.alloc(sizeof(double) * (size_t)batch * N * mat + 8));
-  GPMPC_HIP(dq.alloc(sizeof(double) * (size_t)batch * N * nx + 8));
-  GPMPC_HIP(dout.alloc(sizeof(double) * (size_t)batch * (N + 1) * mat));
+  GPMPC_HIP(dA.alloc(s, sizeof(double) * (size_t)batch * N * mat + 8));
+  GPMPC_HIP(dq.alloc(s, sizeof(double) * (size_t)batch * N * nx + 8));
+  GPMPC_HIP(dout.alloc(s, sizeof(double) * (size_t)batch * (N + 1) * mat));
   if (N > 0) {
     GPMPC_HIP(hipMemcpyAsync(dA.p, A, sizeof(double) * (size_t)batch * N * mat,
                              hipMemcpyHostToDevice, s));
@@ -92,7 +92,7 @@ extern "C" int gpmpc_cov_propagate(gpmpc_ctx *ctx, int batch, int N, int nx, con
                              hipMemcpyHostToDevice, s));
   }
   if (S0) {
-    GPMPC_HIP(dS.alloc(sizeof(double) * (size_t)batch * mat));
+    GPMPC_HIP(dS.alloc(s, sizeof(double) * (size_t)batch * mat));
     GPMPC_HIP(hipMemcpyAsync(dS.p, S0, sizeof(double) * (size_t)batch * mat,
                              hipMemcpyHostToDevice, s));
   }

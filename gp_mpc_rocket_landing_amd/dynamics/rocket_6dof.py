@@ -332,12 +332,11 @@ class Rocket6DoFDynamics:
         return u * (np.clip(t, self.config.T_min, self.config.T_max) / t)
 
     def matches_device_model(self) -> bool:
-        """True when the parameters are the Rocket6DoFConfig defaults that
-        csrc/fleet6.hip compiles in (J, r_T, g_I, alpha)."""
-        d = Rocket6DoFConfig()
-        p = self._params
-        return (np.array_equal(p.J_B, d.J_B) and np.array_equal(p.r_T_B, d.r_T_B)
-                and np.array_equal(p.g_I, d.g_I) and p.alpha == 1.0 / (d.I_sp * d.g0))
+        """True when csrc/fleet6.hip's model can run this rocket: its J, r_T, g_I,
+        alpha and g0 are runtime parameters (gpmpc_rollout6_config, ABI 3), the
+        inertia tensor must be diagonal."""
+        J = np.asarray(self._params.J_B, float)
+        return J.shape == (3, 3) and not np.any(J - np.diag(np.diag(J)))
 
     def __repr__(self) -> str:
         return (f"Rocket6DoFDynamics(m_wet={self.config.m_wet}, m_dry={self.config.m_dry}, "

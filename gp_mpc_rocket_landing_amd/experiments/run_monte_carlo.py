@@ -66,7 +66,7 @@ def main(argv=None):
     import torch.distributed as dist
     from .. import _lib
     from ..fleet import REC_OUTCOME, Fleet, fit_gp, initial_conditions
-    from ..sharding import RCCLRecordGather, gather_records, shard_range
+    from ..sharding import gather_shard_records, shard_range
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -102,17 +102,14 @@ def main(argv=None):
         t = torch.tensor([el], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t[0])
-        if os.environ.get("GPMPC_GATHER", "rccl") == "torch":
-            allrec = gather_records(rec, args.landings, device="cuda")
-        else:  # the C-ABI's ncclGather of the device records (gpmpc_gather_results)
-            g = RCCLRecordGather(ctx)
-            allrec = g.gather(fl.records_dev, args.landings)
-            g.close()
-    else:
-        allrec = rec
+    # the one collective: the C-ABI's ncclGather of the device records (GPMPC_GATHER=torch:
+    # torch.distributed.gather); a set-up failure on any rank is agreed and every rank
+    # falls back together, and `gather` in the summary says what ran
+    allrec, ginfo = gather_shard_records(ctx, fl.records_dev if count else None, rec, args.landings,
+                                         device="cuda")
     if rank == 0:
         s = summarise(allrec)
-        s.update(n_gpus=world, wall_s=round(el, 3), control_steps_per_s=round(s["control_steps"] / el, 1))
+        s.update(n_gpus=world, gather=ginfo, wall_s=round(el, 3), control_steps_per_s=round(s["control_steps"] / el, 1))
         if args.six_dof:
             s.update(config="configs[4] 6-DoF rollouts", rollouts_per_s=round(s["n_landings"] / el, 1))
         print(json.dumps(s), flush=True)

@@ -113,14 +113,35 @@ class GPMPC(_SQPBase):
         self._last_var = np.asarray(var)
         return np.asarray(mean)
 
-    def _initial(self, x0, x_target):
+    def _initial(self, x0, x_target, U_ref=None):
         N = self.config.N
         if self._X_warm is not None:
             return self._X_warm.copy(), self._U_warm.copy()
         a = (np.arange(N + 1) / N)[:, None]
         X = (1 - a) * x0 + a * x_target
+        if U_ref is not None:   # gp_mpc.py:268-269: U_ref as the first guess
+            return X, np.array(U_ref, float)[:N].copy()
         U = np.zeros((N, self.n_u)); U[:, 0] = x0[0] * 1.0
         return X, U
+
+    def _references(self, x_target, X_ref, U_ref):
+        """(X_ref (N+1, n_x), U_ref (N, 3) or None) of gp_mpc.py:442-453: x_target on
+        every stage by default; a reference of N rows takes x_target as its
+        terminal row (:452)."""
+        N = self.config.N
+        if X_ref is None:
+            Xr = np.tile(x_target, (N + 1, 1))
+        else:
+            Xr = np.asarray(X_ref, float).reshape(-1, self.n_x)
+            if Xr.shape[0] < N:
+                raise ValueError(f"X_ref needs at least N = {N} rows, got {Xr.shape[0]}")
+            Xr = np.vstack([Xr[:N], Xr[N:N + 1] if Xr.shape[0] > N else x_target[None]])
+        if U_ref is None:
+            return Xr, None
+        Ur = np.asarray(U_ref, float).reshape(-1, self.n_u)
+        if Ur.shape[0] < N:
+            raise ValueError(f"U_ref needs at least N = {N} rows, got {Ur.shape[0]}")
+        return Xr, Ur[:N]
 
     def _get_tightened_params(self, unc: PropagatedUncertainty, k: int) -> ConstraintParams:
         """gp_mpc.py:177-215; the 7-state model has no attitude / rate rows (0 std)."""
@@ -147,15 +168,18 @@ class GPMPC(_SQPBase):
             x0=x0, U=U[: self.config.N], Sigma_0=np.eye(self.n_x) * 1e-6)
         self.last_tightened_params = self._get_tightened_params(self.last_uncertainty, 0)
 
-    def solve(self, x0, x_target, X_ref=None, U_ref=None) -> MPCSolution:  # noqa: ARG002
+    def solve(self, x0, x_target, X_ref=None, U_ref=None) -> MPCSolution:
+        """X_ref / U_ref: the QP cost's reference trajectory and controls
+        (gp_mpc.py:442-453); U_ref also seeds the first guess (:268-269)."""
         if not self._is_setup:
             self.setup()
         x0 = np.asarray(x0, float); x_target = np.asarray(x_target, float)
-        X, U = self._initial(x0, x_target)
+        Xr, Ur = self._references(x_target, X_ref, U_ref)
+        X, U = self._initial(x0, x_target, Ur)
         self._propagate(x0, U)
         if self.config.max_sqp_iter <= 1:
             t0 = time.perf_counter()
-            P, q = self._qp.cost(np.tile(x_target, (self.config.N + 1, 1)))
+            P, q = self._qp.cost(Xr, Ur)
             Aval, l, u = self._qp.constraints(X, U, x0, gp_dv=self._gp_mean(X, U), sign=-1.0)
             r = self._ws.solve(Aval, P, q, l, u, solution_to_vector(X, U))
             st = int(r["status"][0])
@@ -166,13 +190,13 @@ class GPMPC(_SQPBase):
                 self._X_warm = np.vstack([X[1:], X[-1:]])
                 self._U_warm = np.vstack([U[1:], U[-1:]])
             return MPCSolution(success=ok, X_opt=X, U_opt=U,
-                               cost=trajectory_cost(X, U, x_target) if ok else np.inf,
+                               cost=trajectory_cost(X, U, Xr, Ur) if ok else np.inf,
                                solve_time=time.perf_counter() - t0, iterations=int(r["iter"][0]),
                                status=_lib.QP_STATUS_TEXT.get(st, str(st)))
         X[0] = x0   # X_pred[0] = x0 (gp_mpc.py:263)
-        X, U, conv, it, st, dt = self._sqp(x0, x_target, X, U, self.config.max_sqp_iter, -1.0)
+        X, U, conv, it, st, dt = self._sqp(x0, x_target, X, U, self.config.max_sqp_iter, -1.0, Xr, Ur)
         self._X_warm, self._U_warm = X.copy(), U.copy()
-        return MPCSolution(success=conv, X_opt=X, U_opt=U, cost=trajectory_cost(X, U, x_target),
+        return MPCSolution(success=conv, X_opt=X, U_opt=U, cost=trajectory_cost(X, U, Xr, Ur),
                            solve_time=dt, iterations=it, status="Converged" if conv else "Max iterations")
 
     def get_uncertainty_at_horizon(self, k: Optional[int] = None):
@@ -208,24 +232,28 @@ class GPMPC6DoF(GPMPC):
 
     The GP must be a fitted StructuredRocketGP (FITC or exact); its means are
     what ``gp.predict`` returns (FITC: K*u alpha as written).
-    Cost weights must be diagonal (CostWeights builds them so); X_ref must be
-    x_target on every stage and U_ref zero in the cost (the reference's
-    defaults, :442-445).  The device model is the Rocket6DoFConfig default
-    rocket and N = 30 (BASELINE configs[4]); ``GPMPCConfig()`` without an N
-    gets N = 30 here.
+    Cost weights must be diagonal (CostWeights builds them so).  ``X_ref`` /
+    ``U_ref`` enter the QP cost as the reference writes it (:442-453: x_k -
+    X_ref[k], u_k - U_ref[k], terminal X_ref[N] or x_target when X_ref has N
+    rows); U_ref also seeds the first guess when there is no warm start
+    (:268-269).  The horizon is ``config.N`` -- ``GPMPCConfig()`` is the
+    reference's N = 20 (gp_mpc.py:110, nominal_mpc.py:47); the device
+    controller is compiled for N = 20 and N = 30 (BASELINE configs[4]).  The
+    rocket is ``dynamics.params`` (J_B, r_T_B, g_I, I_sp, g0 of
+    Rocket6DoFConfig); the device model takes a diagonal J_B.
     """
     n_x, n_u = 14, 3
 
     def __init__(self, dynamics, gp_model, config: Optional[GPMPCConfig] = None,
                  constraint_params=None, cost_weights=None, ctx=None):
-        if config is None:
-            config = GPMPCConfig(N=30)
-        if config.N != 30:
-            raise NotImplementedError("the 6-DoF device controller is compiled for N = 30 (BASELINE configs[4])")
-        matches = getattr(dynamics, "matches_device_model", None)
-        if matches is None or not matches():
-            raise NotImplementedError("the 6-DoF device controller runs the Rocket6DoFConfig default rocket "
-                                      "(dynamics.Rocket6DoFDynamics)")
+        config = config or GPMPCConfig()
+        if int(config.N) not in _r6.HORIZONS:
+            raise NotImplementedError(f"the 6-DoF device controller is compiled for N in {_r6.HORIZONS} "
+                                      f"(GPMPCConfig's N = 20, BASELINE configs[4]'s N = 30), not {config.N}")
+        params = getattr(dynamics, "params", None)
+        if params is None:
+            raise TypeError("dynamics must expose the rocket's params (Rocket6DoFDynamics)")
+        self._rocket_kw = _r6.rocket_config(params)
         self.dynamics = dynamics
         self.config = config
         self.gp = gp_model
@@ -251,7 +279,8 @@ class GPMPC6DoF(GPMPC):
         for M in (Q, R, P):
             if np.any(M - np.diag(np.diag(M))):
                 raise NotImplementedError("the device QP takes diagonal cost weights (CostWeights' own)")
-        return dict(q_diag=np.diag(Q), p_diag=np.diag(P), r_diag=np.diag(R), t_min=float(cp.T_min),
+        return dict(horizon=int(self.config.N), **self._rocket_kw,
+                    q_diag=np.diag(Q), p_diag=np.diag(P), r_diag=np.diag(R), t_min=float(cp.T_min),
                     t_max=float(cp.T_max), tan_gamma_gs=float(np.tan(cp.gamma_gs_rad)),
                     dt=float(self.config.dt), use_gp_mean=int(bool(self.config.use_gp_mean)),
                     fitc_mean_as_written=1,   # gp.predict's mean (sparse_gp.py:280-283, D1)
@@ -279,32 +308,48 @@ class GPMPC6DoF(GPMPC):
         """gp_mpc.py:494-497 (+ the ADMM's persistent duals / rho)."""
         self._X_warm = self._U_warm = None
 
+    def _references(self, x_target, X_ref, U_ref):
+        """The QP cost's (X_ref (N+1, 14), U_ref (N, 3)) of gp_mpc.py:442-453: X_ref
+        defaults to x_target on every stage, a reference of N rows takes x_target as
+        its terminal row (:452), U_ref defaults to zero."""
+        N = self.config.N
+        if X_ref is None:
+            Xr = np.tile(x_target, (N + 1, 1))
+        else:
+            Xr = np.asarray(X_ref, float).reshape(-1, 14)
+            if Xr.shape[0] < N:
+                raise ValueError(f"X_ref needs at least N = {N} rows, got {Xr.shape[0]}")
+            Xr = np.vstack([Xr[:N], Xr[N:N + 1] if Xr.shape[0] > N else x_target[None]])
+        Ur = np.zeros((N, 3)) if U_ref is None else np.asarray(U_ref, float).reshape(-1, 3)[:N]
+        if Ur.shape[0] < N:
+            raise ValueError(f"U_ref needs at least N = {N} rows, got {Ur.shape[0]}")
+        return Xr, Ur
+
     def solve(self, x0, x_target, X_ref=None, U_ref=None) -> MPCSolution:
         if not self._is_setup:
             self.setup()
         t0 = time.perf_counter()
         N = self.config.N
         x0 = np.asarray(x0, float).reshape(14); x_target = np.asarray(x_target, float).reshape(14)
-        if X_ref is not None and not np.array_equal(np.asarray(X_ref, float)[:N + 1],
-                                                    np.tile(x_target, (N + 1, 1))):
-            raise NotImplementedError("the device QP tracks x_target on every stage (X_ref=None)")
+        Xr, Ur = self._references(x_target, X_ref, U_ref)
         ro = self._rollout()
         if self._U_warm is not None:
             cold = 0
         elif U_ref is not None:  # gp_mpc.py:268-269: U_ref as the first guess
-            ro.set_state(U=np.asarray(U_ref, float)[:N].reshape(1, N, 3))
+            ro.set_state(U=Ur.reshape(1, N, 3))
             cold = 2
         else:
             cold = 1
         max_sqp = max(1, int(self.config.max_sqp_iter))
-        r = ro.solve(x0[None], x_target[None], cold, max_sqp_iter=max_sqp, sqp_tol=float(self.config.sqp_tol))
+        r = ro.solve(x0[None], x_target[None], cold, max_sqp_iter=max_sqp, sqp_tol=float(self.config.sqp_tol),
+                     X_ref=None if X_ref is None else Xr[None], U_ref=None if U_ref is None else Ur[None])
         X, U = r["X"][0], r["U"][0]
         st, passes = int(r["qp_status"][0]), int(r["passes"][0])
         has = st in (1, 2, -2)
         self.last_status, self.last_iterations, self.last_passes = st, int(r["qp_iters"][0]), passes
         self._X_warm, self._U_warm = X.copy(), U.copy()
         self._propagate(x0, U)
-        cost = self._cost(X, U, x_target) if has else np.inf
+        cost = self._cost(X, U, Xr, Ur) if has else np.inf
         if max_sqp <= 1:
             return MPCSolution(success=has, X_opt=X, U_opt=U, cost=cost, solve_time=time.perf_counter() - t0,
                                iterations=self.last_iterations, status=_lib.QP_STATUS_TEXT.get(st, str(st)))
@@ -312,11 +357,12 @@ class GPMPC6DoF(GPMPC):
         return MPCSolution(success=conv, X_opt=X, U_opt=U, cost=cost, solve_time=time.perf_counter() - t0,
                            iterations=passes, status="Converged" if conv else "Max iterations")
 
-    def _cost(self, X, U, x_target):
-        """gp_mpc.py:447-458 at the returned plan (X_ref = x_target, U_ref = 0)."""
+    def _cost(self, X, U, Xr, Ur):
+        """gp_mpc.py:447-458 at the returned plan against (X_ref, U_ref)."""
         cw = self.cost_weights
-        e = X - x_target
-        return float(np.einsum("ki,ij,kj->", e[:-1], cw.Q, e[:-1]) + np.einsum("ki,ij,kj->", U, cw.R, U)
+        e = X - Xr
+        du = U - Ur
+        return float(np.einsum("ki,ij,kj->", e[:-1], cw.Q, e[:-1]) + np.einsum("ki,ij,kj->", du, cw.R, du)
                      + e[-1] @ cw.P @ e[-1])
 
     def _get_tightened_params(self, unc: PropagatedUncertainty, k: int) -> ConstraintParams:

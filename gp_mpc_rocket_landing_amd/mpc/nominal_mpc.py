@@ -57,10 +57,13 @@ class MPCSolution:
         return self.U_opt[0]
 
 
-def trajectory_cost(X, U, x_ref) -> float:
-    """nominal_mpc.py:619-631: sum (x-x_t)'Q(x-x_t) + u'Ru + 10 (x_N-x_t)'Q(x_N-x_t)."""
+def trajectory_cost(X, U, x_ref, u_ref=None) -> float:
+    """nominal_mpc.py:619-631: sum (x-x_t)'Q(x-x_t) + u'Ru + 10 (x_N-x_t)'Q(x_N-x_t);
+    x_ref may be a trajectory (N+1, 7) and u_ref (N, 3) a control reference
+    (gp_mpc.py:442-453)."""
     e = np.asarray(X) - np.asarray(x_ref)
-    return float(np.sum(e[:-1] ** 2 * Q_DIAG) + np.sum(np.asarray(U) ** 2 * R_DIAG)
+    du = np.asarray(U) - (0.0 if u_ref is None else np.asarray(u_ref))
+    return float(np.sum(e[:-1] ** 2 * Q_DIAG) + np.sum(du ** 2 * R_DIAG)
                  + QF_SCALE * np.sum(e[-1] ** 2 * Q_DIAG))
 
 
@@ -92,9 +95,9 @@ class _SQPBase:
     def _gp_mean(self, X, U):
         return None
 
-    def _sqp(self, x0, x_target, X, U, max_iter, sign):
+    def _sqp(self, x0, x_target, X, U, max_iter, sign, x_ref=None, u_ref=None):
         t0 = time.perf_counter()
-        P, q = self._qp.cost(np.tile(x_target, (self.config.N + 1, 1)))
+        P, q = self._qp.cost(np.tile(x_target, (self.config.N + 1, 1)) if x_ref is None else x_ref, u_ref)
         converged, it, status = False, 0, -10
         for it in range(1, max_iter + 1):
             dv = self._gp_mean(X, U)

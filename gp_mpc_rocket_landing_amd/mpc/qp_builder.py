@@ -115,12 +115,17 @@ class RTIQPBuilder:
         self._lb, self._ub = lb, ub
 
     # ------------------------------------------------------------------
-    def cost(self, x_ref):
-        """(P diagonal, q) for the reference trajectory x_ref (N+1, 7)."""
+    def cost(self, x_ref, u_ref=None):
+        """(P diagonal, q) for the reference trajectory x_ref (N+1, 7) and, when
+        given, the control reference u_ref (N, 3): sum |x_k - x_ref[k]|_Q^2 +
+        |u_k - u_ref[k]|_R^2 (gp_mpc.py:442-453; osqp_rti.py's cost has u_ref = 0)."""
         N = self.N
         x_ref = np.asarray(x_ref, float)
         q = np.zeros(self.n)
-        q[:N * (N_X + N_U)].reshape(N, N_X + N_U)[:, :N_X] = -Q_DIAG * x_ref[:N]
+        qq = q[:N * (N_X + N_U)].reshape(N, N_X + N_U)
+        qq[:, :N_X] = -Q_DIAG * x_ref[:N]
+        if u_ref is not None:
+            qq[:, N_X:] = -R_DIAG * np.asarray(u_ref, float)[:N]
         q[N * (N_X + N_U):] = -QF_SCALE * Q_DIAG * x_ref[N]
         return self.P_diag, q
 

@@ -19,6 +19,25 @@ from .data import synthetic_6dof_training_data
 from .gp.features import CombinedFeatureExtractor
 
 NX6 = 14
+HORIZONS = (20, 30)   # the compiled horizons of csrc/fleet6_n.h (GPMPCConfig's N, BASELINE configs[4])
+
+
+def qp_rows(N: int) -> int:
+    """Rows of the 6-DoF QP at horizon N: x0 + dynamics 14 (N+1), one bound row per
+    variable (17 N + 14), N thrust rows and 4 (N-1) glide-slope rows."""
+    return 14 * (N + 1) + (17 * N + 14) + N + 4 * (N - 1)
+
+
+def rocket_config(params) -> dict:
+    """Rollout6Config rocket fields from a Rocket6DoFParams-like object
+    (rocket_6dof.py:36-84: J_B, r_T_B, g_I, I_sp, g0).  The device model takes a
+    diagonal J_B and raises otherwise."""
+    J = np.asarray(params.J_B, float)
+    if J.shape != (3, 3) or np.any(J - np.diag(np.diag(J))):
+        raise NotImplementedError("the 6-DoF device model takes a diagonal inertia tensor J_B")
+    return dict(rocket_j=np.diag(J).copy(), rocket_r_t=np.asarray(params.r_T_B, float).reshape(3),
+                rocket_g_i=np.asarray(params.g_I, float).reshape(3),
+                rocket_alpha=1.0 / (float(params.I_sp) * float(params.g0)), rocket_g0=float(params.g0))
 
 
 def fit_structured_gp(n_train=4000, n_inducing=2000, seed=0, use_sparse=True):
@@ -86,7 +105,11 @@ class Rollouts6:
         self.ctx = ctx
         self.gp_v, self.gp_w = gp_v, gp_w  # keep alive: the kernels read their device state
         self.cfg = _lib.rollout6_default_config(**config)
+        if int(self.cfg.horizon) not in HORIZONS:
+            raise ValueError(f"horizon {int(self.cfg.horizon)}: the device controller is compiled for N in {HORIZONS}")
         self.batch = int(batch)
+        self.N = int(self.cfg.horizon)
+        self.M = qp_rows(self.N)
         h = ctypes.c_void_p()
         exact = isinstance(gp_v, _lib.ExactGPHandle)
         if exact != isinstance(gp_w, _lib.ExactGPHandle):
@@ -120,32 +143,38 @@ class Rollouts6:
         """Records, states and each rollout's controller state: warm-start U,
         last plan X, forward-simulated X_pred and its GP means, scaled duals, rho."""
         rec, x = self.read()
-        B, N = self.batch, int(self.cfg.horizon)
+        B, N = self.batch, self.N
         U = np.empty((B, N, 3)); X = np.empty((B, N + 1, NX6)); Xp = np.empty((B, N + 1, NX6))
-        gm = np.empty((B, N, 6)); y = np.empty((B, 1104)); rho = np.empty(B)
+        gm = np.empty((B, N, 6)); y = np.empty((B, self.M)); rho = np.empty(B)
         _lib._chk(_lib._L.gpmpc_rollout6_get_state(self.h, _lib._d(U), _lib._d(X), _lib._d(Xp), _lib._d(gm),
                                                    _lib._d(y), _lib._d(rho)), "rollout6_get_state")
         return dict(rec=rec, x=x, U=U, X=X, X_pred=Xp, gm=gm, y=y, rho=rho)
 
     def set_state(self, U=None, y=None, rho=None):
         """gpmpc_rollout6_set_state (None leaves a part unchanged)."""
-        B, N = self.batch, int(self.cfg.horizon)
+        B, N = self.batch, self.N
         a = [None if v is None else _lib.f64(np.reshape(v, shape))
-             for v, shape in ((U, (B, N, 3)), (y, (B, 1104)), (rho, (B,)))]
+             for v, shape in ((U, (B, N, 3)), (y, (B, self.M)), (rho, (B,)))]
         _lib._chk(_lib._L.gpmpc_rollout6_set_state(self.h, *[None if v is None else _lib._d(v) for v in a]),
                   "rollout6_set_state")
 
-    def solve(self, x0, x_target, cold, max_sqp_iter=10, sqp_tol=1e-4):
-        """GPMPC.solve (gp_mpc.py:229-369) for every rollout (gpmpc_rollout6_solve).
+    def solve(self, x0, x_target, cold, max_sqp_iter=10, sqp_tol=1e-4, X_ref=None, U_ref=None):
+        """GPMPC.solve (gp_mpc.py:229-369) for every rollout (gpmpc_rollout6_solve_ref).
+        X_ref (B, N+1, 14) / U_ref (B, N, 3): the QP cost's reference trajectory
+        (gp_mpc.py:442-453; None = x_target on every stage / zero).
         Returns dict(X (B, N+1, 14), U (B, N, 3), passes, converged, qp_status,
         qp_iters) of int arrays (B,)."""
-        B, N = self.batch, int(self.cfg.horizon)
+        B, N = self.batch, self.N
         x0 = _lib.f64(np.reshape(x0, (B, NX6))); xt = _lib.f64(np.reshape(x_target, (B, NX6)))
+        xr = None if X_ref is None else _lib.f64(np.reshape(X_ref, (B, N + 1, NX6)))
+        ur = None if U_ref is None else _lib.f64(np.reshape(U_ref, (B, N, 3)))
         X = np.empty((B, N + 1, NX6)); U = np.empty((B, N, 3))
         ps, cv, qs, qi = (np.zeros(B, np.int32) for _ in range(4))
-        _lib._chk(_lib._L.gpmpc_rollout6_solve(self.h, _lib._d(x0), _lib._d(xt), int(cold),
-                                               int(max_sqp_iter), float(sqp_tol), _lib._d(X), _lib._d(U),
-                                               _lib._i(ps), _lib._i(cv), _lib._i(qs), _lib._i(qi)),
+        _lib._chk(_lib._L.gpmpc_rollout6_solve_ref(self.h, _lib._d(x0), _lib._d(xt),
+                                                   None if xr is None else _lib._d(xr),
+                                                   None if ur is None else _lib._d(ur), int(cold),
+                                                   int(max_sqp_iter), float(sqp_tol), _lib._d(X), _lib._d(U),
+                                                   _lib._i(ps), _lib._i(cv), _lib._i(qs), _lib._i(qi)),
                   "rollout6_solve")
         return dict(X=X, U=U, passes=ps, converged=cv.astype(bool), qp_status=qs, qp_iters=qi)
 

@@ -11,6 +11,8 @@ gather and trimmed on rank 0.
 """
 from __future__ import annotations
 
+import os
+
 import numpy as np
 
 
@@ -43,6 +45,38 @@ def gather_records(records: np.ndarray, total: int, device=None):
     return np.concatenate(out, axis=0)
 
 
+def _world():
+    """(world, rank, dist-or-None) of the default torch.distributed group; a
+    process without one is a world of one."""
+    try:
+        import torch.distributed as dist
+        if dist.is_available() and dist.is_initialized():
+            return dist.get_world_size(), dist.get_rank(), dist
+    except ImportError:
+        pass
+    return 1, 0, None
+
+
+def _count_ready(flag: bool) -> int:
+    """How many ranks of the default group set ``flag`` (one all_reduce of a
+    scalar; 0/1 without a group).  Every rank calls it at the same point, so
+    every rank learns the same count and takes the same branch after it."""
+    world, _, dist = _world()
+    if dist is None:
+        return int(bool(flag))
+    import torch
+    dev = "cuda" if dist.get_backend() == "nccl" else "cpu"
+    t = torch.tensor([1 if flag else 0], dtype=torch.int64, device=dev)
+    dist.all_reduce(t)
+    return int(t.item())
+
+
+class GatherSetupError(RuntimeError):
+    """The RCCL gather could not be set up on every rank; every rank raises it
+    at the same point (the readiness counts are agreed), so no rank is left
+    inside a collective its peers never enter."""
+
+
 class RCCLRecordGather:
     """The gather as the C-ABI's RCCL collective (gpmpc_comm_* /
     gpmpc_gather_results): one ncclGather over xGMI straight from
@@ -50,32 +84,58 @@ class RCCLRecordGather:
 
     The communicator spans the ranks of the default torch.distributed group
     (one process per GPU); rank 0's ncclUniqueId reaches the others through
-    that group.  Without a process group it is a world of one."""
+    that group.  Without a process group it is a world of one.
 
-    def __init__(self, ctx):
+    Set-up is agreed before and after ncclCommInitRank: a rank whose local
+    preparation failed (no context, RCCL not loadable, no unique id on rank 0)
+    still takes part in the id broadcast and the readiness count, so every rank
+    raises GatherSetupError together instead of some blocking in the
+    communicator's bootstrap.  ``nranks`` is what RCCL's communicator reports
+    (gpmpc_comm_count), not what was asked for."""
+
+    def __init__(self, ctx, _fail_local=False):
         import ctypes
 
         from . import _lib
-        self._lib, self.ctx = _lib, ctx
-        world, rank = 1, 0
-        try:
-            import torch.distributed as dist
-            if dist.is_available() and dist.is_initialized():
-                world, rank = dist.get_world_size(), dist.get_rank()
-        except ImportError:
-            dist = None
+        self._lib, self.ctx, self.h = _lib, ctx, None
+        world, rank, dist = _world()
         self.world, self.rank = world, rank
-        uid = ctypes.create_string_buffer(128)
-        if rank == 0:
-            _lib._chk(_lib._L.gpmpc_comm_unique_id(uid), "comm_unique_id")
+        err = None
+        if ctx is None or getattr(ctx, "h", None) is None:
+            err = "no device context on this rank"
+        elif _fail_local:
+            err = "local set-up failure (injected)"
+        uid = ctypes.create_string_buffer(_lib.COMM_ID_BYTES)
         raw = uid.raw
+        if rank == 0 and err is None:
+            try:
+                _lib._chk(_lib._L.gpmpc_comm_unique_id(uid), "comm_unique_id")
+                raw = uid.raw
+            except Exception as e:  # noqa: BLE001  (reported to every rank below)
+                err = str(e)
         if world > 1:
-            box = [raw]
-            dist.broadcast_object_list(box, src=0)
-            raw = box[0]
+            box = [(raw, err if rank == 0 else None)]
+            dist.broadcast_object_list(box, src=0)   # every rank, even after a failure
+            raw, root_err = box[0]
+            if root_err and err is None:
+                err = f"rank 0: {root_err}"
+        ready = _count_ready(err is None)
+        if ready < world:
+            raise GatherSetupError(f"RCCL gather not set up: {world - ready} of {world} ranks not ready"
+                                   + (f" (this rank: {err})" if err else ""))
         h = _lib._vp()
-        _lib._chk(_lib._L.gpmpc_comm_init(ctx.h, raw, world, rank, ctypes.byref(h)), "comm_init")
-        self.h = h
+        rc = _lib._L.gpmpc_comm_init(ctx.h, raw, world, rank, ctypes.byref(h))
+        init_err = None if rc == 0 else _lib._L.gpmpc_last_error().decode(errors="replace")
+        ready = _count_ready(init_err is None)
+        if init_err is None:
+            self.h = h
+        if ready < world:
+            self.close()
+            raise GatherSetupError(f"ncclCommInitRank failed on {world - ready} of {world} ranks"
+                                   + (f" (this rank: {init_err})" if init_err else ""))
+        n = ctypes.c_int(0)
+        _lib._chk(_lib._L.gpmpc_comm_count(self.h, ctypes.byref(n)), "comm_count")
+        self.nranks = int(n.value)
 
     def gather(self, d_records, total: int, root: int = 0):
         """d_records: this rank's device record pointer (shard_range(total, rank, world)
@@ -97,3 +157,48 @@ class RCCLRecordGather:
             self.close()
         except Exception:
             pass
+
+
+def gather_shard_records(ctx, d_records, host_records, total: int, path: str | None = None,
+                         device=None, _fail_local=False):
+    """The one collective of the path, with a record of what ran.
+
+    path "rccl" (default, or GPMPC_GATHER): the C-ABI's ncclGather of the device
+    record arrays.  If its set-up fails on any rank, every rank knows it (the
+    readiness counts are agreed) and all fall back together to
+    torch.distributed.gather of the host records; if the gather itself fails on
+    any rank, likewise.  path "torch": torch.distributed.gather directly.
+
+    Returns (records on rank 0 / None elsewhere, info) with info =
+    {"path": "rccl" | "torch", "nranks": ranks the collective spanned (RCCL's
+    communicator count, or the process group's size), "records": rows gathered
+    on rank 0 (0 elsewhere), "requested": path, "fallback": reason or None}."""
+    path = path or os.environ.get("GPMPC_GATHER", "rccl")
+    world, rank, dist = _world()
+    info = {"path": None, "nranks": None, "records": 0, "requested": path, "fallback": None}
+    if path == "rccl":
+        g = None
+        try:
+            g = RCCLRecordGather(ctx, _fail_local=_fail_local)
+        except GatherSetupError as e:
+            info["fallback"] = str(e)
+        if g is not None:
+            out, err = None, None
+            try:
+                out = g.gather(d_records, total)
+            except Exception as e:  # noqa: BLE001  (agreed below)
+                err = str(e)
+            nr = g.nranks
+            g.close()
+            if _count_ready(err is None) == world:
+                info.update(path="rccl", nranks=nr, records=0 if out is None else int(out.shape[0]))
+                return out, info
+            info["fallback"] = "ncclGather failed" + (f" (this rank: {err})" if err else " on a peer")
+    elif path != "torch":
+        raise ValueError(f"unknown gather path {path!r} (rccl or torch)")
+    if dist is None:
+        out = np.ascontiguousarray(host_records)
+    else:
+        out = gather_records(host_records, total, device=device)
+    info.update(path="torch", nranks=world, records=0 if out is None else int(out.shape[0]))
+    return out, info

@@ -27,8 +27,10 @@ extern "C" {
 #endif
 
 /* 2: gpmpc_fleet_config gained sqp_iters / sqp_tol (round 2) and
- * gpmpc_rollout6_config the GPMPC problem data (round 3) */
-#define GPMPC_ABI_VERSION 2
+ * gpmpc_rollout6_config the GPMPC problem data (round 3);
+ * 3: gpmpc_rollout6_config gained the rocket parameters and horizon 20 or 30,
+ * gpmpc_rollout6_solve_ref (X_ref / U_ref), gpmpc_comm_count (round 4) */
+#define GPMPC_ABI_VERSION 3
 
 typedef struct gpmpc_ctx gpmpc_ctx;
 typedef struct gpmpc_gp gpmpc_gp;
@@ -75,10 +77,14 @@ int gpmpc_gram_grad(gpmpc_ctx *ctx, int kind, const double *X1, int n1, const do
 
 /* ---- Cholesky factor / solve -------------------------------------------
  * Replaces np.linalg.cholesky (exact_gp.py:164,170; sparse_gp.py:187,205).
- * In place on the lower triangle; info = 1-based first non-positive pivot. */
+ * In place on the lower triangle; info = 1-based first non-positive pivot
+ * (returned as well).  info = -1: the factor kernel's bounded internal wait
+ * expired (a broken invariant, factor unreliable); the call then returns -1
+ * with gpmpc_last_error naming it. */
 int gpmpc_potrf(gpmpc_ctx *ctx, int n, double *A, int lda, int *info);
 /* batch x (n x n) SPD matrices, device-resident, stride elements apart;
- * dinfo: device int[batch]. */
+ * dinfo: device int[batch], with gpmpc_potrf's meaning per matrix (the caller
+ * reads it; -1 marks an unreliable factor). */
 int gpmpc_potrf_batched_dev(gpmpc_ctx *ctx, int n, int batch, double *dA, int lda, int64_t stride,
                             int *dinfo);
 /* C = alpha A A^T + beta C on the lower triangle (dsyrk 'L','N') for batch
@@ -217,7 +223,9 @@ typedef struct {
                             :506-508).  The warm start is the unshifted plan (gp_mpc.py
                             :358-359). */
   double sqp_tol;        /* 1e-4 (gp_mpc.py:343) */
-  gpmpc_qp_settings sqp_qp;  /* QP settings of the SQP passes (sqp_iters > 1); default = qp.
+  gpmpc_qp_settings sqp_qp;  /* QP settings of the SQP passes (sqp_iters > 1).  sqp_qp.max_iter
+                                = 0 (the default) means "the same as qp", resolved when the fleet
+                                launches, so a caller that edits only qp changes the passes too.
                                 The reference solves this subproblem with IPOPT (gp_mpc.py:462-470) */
 } gpmpc_fleet_config;
 void gpmpc_fleet_default_config(gpmpc_fleet_config *c);
@@ -278,10 +286,11 @@ int gpmpc_cov_propagate_dev(gpmpc_ctx *ctx, int batch, int N, int nx, const doub
  * (DESIGN.md section 9), the OSQP-0.6 ADMM on the block-tridiagonal reduced
  * KKT matrix, the truth plant step (RK4 + the dispersion.py:349-360 drag) and
  * the plan kept unshifted as the next warm start.  State 14 = [m, r_I, v_I,
- * q_BI (w, x, y, z), omega_B]; horizon fixed at 30. */
+ * q_BI (w, x, y, z), omega_B]; horizon 20 (GPMPCConfig's N, gp_mpc.py:110 /
+ * nominal_mpc.py:47) or 30 (BASELINE configs[4]), each a compiled instance. */
 typedef struct gpmpc_rollout6 gpmpc_rollout6;
 typedef struct {
-  int horizon;           /* must be 30 */
+  int horizon;           /* 20 or 30 (the compiled instances); default 30 */
   double dt;
   int max_steps;
   gpmpc_qp_settings qp;  /* osqp_rti.py:54-60 defaults */
@@ -298,6 +307,15 @@ typedef struct {
   int use_gp_mean;       /* GPMPCConfig.use_gp_mean: 0 drops the GP from the simulation and c_k */
   int upright_target;    /* rollouts: 0 = monte_carlo.py:497-500 as written (x copied, v = 0,
                             altitude - 2); 1 = also q = (1, 0, 0, 0), omega = 0 */
+  /* the rocket (ABI 3): Rocket6DoFConfig (rocket_6dof.py:36-84) as the dynamics of
+   * nominal_mpc.py:163-203 use it.  Defaults J_B = diag(0.02, 1, 1) 0.168 (the device
+   * model takes a diagonal J_B), r_T_B = (-0.25, 0, 0), g_I = (-1, 0, 0), I_sp 30, g0 1:
+   * alpha = 1 / (I_sp g0); g0 also sets the hover guess [0, 0, m g0] (gp_mpc.py:271-275) */
+  double rocket_j[3];    /* diagonal of J_B */
+  double rocket_r_t[3];  /* thrust application point r_T_B */
+  double rocket_g_i[3];  /* gravity g_I */
+  double rocket_alpha;   /* 1 / (I_sp g0) */
+  double rocket_g0;
 } gpmpc_rollout6_config;
 void gpmpc_rollout6_default_config(gpmpc_rollout6_config *c);
 /* gp_v: FITC on the 13 translational features, gp_w: on the 12 rotational
@@ -324,11 +342,19 @@ int gpmpc_rollout6_create_exact(gpmpc_ctx *ctx, gpmpc_gp *gp_v, gpmpc_gp *gp_w,
  * the previous call's plan U, unshifted (:266-267, :358-359).  The batch's Monte-Carlo records are not
  * touched except rec[11] (ADMM iterations of this call), rec[12] (solves with
  * status solved), rec[14] (last QP status), rec[15] (rho).
- * Outputs (any may be NULL): X (batch x 31 x 14), U (batch x 30 x 3), passes,
+ * Outputs (any may be NULL): X (batch x (N+1) x 14), U (batch x N x 3), passes,
  * converged (0 / 1), qp_status of the last pass, qp_iters summed over passes. */
 int gpmpc_rollout6_solve(gpmpc_rollout6 *r, const double *x0, const double *x_target, int cold,
                          int max_sqp_iter, double sqp_tol, double *X, double *U, int *passes,
                          int *converged, int *qp_status, int *qp_iters);
+/* the same with the QP cost's reference trajectory (gp_mpc.py:442-453): X_ref
+ * (batch x (N+1) x 14; NULL = x_target on every stage) and U_ref (batch x N x 3;
+ * NULL = 0) in sum_k |x_k - X_ref[k]|_Q^2 + |u_k - U_ref[k]|_R^2 + |x_N - X_ref[N]|_P^2.
+ * (U_ref's other use, the first guess of :268-269, is cold = 2 after
+ * gpmpc_rollout6_set_state.) */
+int gpmpc_rollout6_solve_ref(gpmpc_rollout6 *r, const double *x0, const double *x_target, const double *X_ref,
+                             const double *U_ref, int cold, int max_sqp_iter, double sqp_tol, double *X,
+                             double *U, int *passes, int *converged, int *qp_status, int *qp_iters);
 /* (re)start rollouts [first, first+count) at x0 (count x 14) */
 int gpmpc_rollout6_reset(gpmpc_rollout6 *r, int first, int count, const double *x0);
 /* nsteps control steps of every running rollout (async on the ctx stream) */
@@ -340,14 +366,14 @@ int gpmpc_rollout6_step_phases(gpmpc_rollout6 *r, int mask);
 /* records (batch x GPMPC_REC_LEN, the fleet layout; state slots hold [m, r, v])
  * and the full states (batch x 14, may be NULL) */
 int gpmpc_rollout6_read(gpmpc_rollout6 *r, double *records, double *x);
-/* controller state, any pointer may be NULL: warm-start controls U (batch x 30
- * x 3), last QP plan X (batch x 31 x 14), forward-simulated X_pred (batch x 31
- * x 14), its GP means (batch x 30 x 6: d_v, d_omega), the ADMM's persistent
- * scaled duals (batch x 1104) and rho (batch) */
+/* controller state, any pointer may be NULL: warm-start controls U (batch x N
+ * x 3), last QP plan X (batch x (N+1) x 14), forward-simulated X_pred (batch x
+ * (N+1) x 14), its GP means (batch x N x 6: d_v, d_omega), the ADMM's persistent
+ * scaled duals (batch x M, M = 36 N + 24: 1104 at N = 30, 744 at N = 20) and rho (batch) */
 int gpmpc_rollout6_get_state(gpmpc_rollout6 *r, double *U, double *X_plan, double *X_pred,
                              double *gp_mean, double *y_scaled, double *rho);
-/* set controller state (any pointer may be NULL): U (batch x 30 x 3), scaled
- * duals (batch x 1104), rho (batch) -- e.g. to carry a warm start across a GP
+/* set controller state (any pointer may be NULL): U (batch x N x 3), scaled
+ * duals (batch x M), rho (batch) -- e.g. to carry a warm start across a GP
  * refit, or to start GPMPC.solve from caller-given controls */
 int gpmpc_rollout6_set_state(gpmpc_rollout6 *r, const double *U, const double *y_scaled, const double *rho);
 int gpmpc_rollout6_destroy(gpmpc_rollout6 *r);
@@ -369,6 +395,8 @@ typedef struct gpmpc_comm gpmpc_comm;
 int gpmpc_comm_unique_id(unsigned char *id /* GPMPC_COMM_ID_BYTES */);
 int gpmpc_comm_init(gpmpc_ctx *ctx, const unsigned char *id, int nranks, int rank, gpmpc_comm **out);
 int gpmpc_comm_destroy(gpmpc_comm *c);
+/* ranks the RCCL communicator spans (ncclCommCount) */
+int gpmpc_comm_count(gpmpc_comm *c, int *nranks);
 /* d_records: this rank's counts[rank] x GPMPC_REC_LEN records (device, e.g.
  * gpmpc_fleet_records_dev); counts: every rank's shard size (host, nranks).
  * On the root, out (host) receives sum(counts) x GPMPC_REC_LEN doubles in

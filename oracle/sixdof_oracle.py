@@ -43,6 +43,15 @@ J_DIAG = np.array([0.02, 1.0, 1.0]) * 0.168
 R_T = np.array([-0.25, 0.0, 0.0])
 G_I = np.array([-1.0, 0.0, 0.0])
 G0 = 1.0
+# Rocket6DoFConfig defaults as one parameter set; every dynamics function takes an
+# optional ``rk`` of this shape (rocket_6dof.py:36-84; diagonal J_B)
+DEFAULT_ROCKET = dict(J=J_DIAG, r_T=R_T, g_I=G_I, alpha=ALPHA, g0=G0)
+
+
+def rocket_params(J=None, r_T=None, g_I=None, I_sp=30.0, g0=1.0):
+    """A parameter set for a Rocket6DoFConfig (diagonal J_B given as its diagonal)."""
+    return dict(J=np.asarray(J_DIAG if J is None else J, float), r_T=np.asarray(R_T if r_T is None else r_T, float),
+                g_I=np.asarray(G_I if g_I is None else g_I, float), alpha=1.0 / (I_sp * g0), g0=float(g0))
 T_MIN, T_MAX = 0.5, 5.0                 # ConstraintParams (constraints.py:35-50)
 TAN_GS = np.tan(np.deg2rad(30.0))       # gamma_gs 30 deg
 TRUST_X, TRUST_U = np.sqrt(10.0), np.sqrt(5.0)   # gp_mpc.py:432-435
@@ -59,42 +68,44 @@ def dcm_ib(q):
                      [2 * (x * z - w * y), 2 * (y * z + w * x), 1 - 2 * (x * x + y * y)]])
 
 
-def f(x, u):
+def f(x, u, rk=None):
     """nominal_mpc.py:163-203."""
+    rk = rk or DEFAULT_ROCKET
     m, v, q, w = x[0], x[4:7], x[7:11], x[11:14]
     tm = np.sqrt(u @ u)
     out = np.empty(NX)
-    out[0] = -ALPHA * tm
+    out[0] = -rk["alpha"] * tm
     out[1:4] = v
-    out[4:7] = dcm_ib(q) @ u / m + G_I
+    out[4:7] = dcm_ib(q) @ u / m + rk["g_I"]
     qv = q[1:4]
     out[7] = 0.5 * -(w @ qv)
     out[8:11] = 0.5 * (q[0] * w + np.cross(w, qv))
-    torque = np.cross(R_T, u)
-    jw = J_DIAG * w
-    out[11:14] = (torque - np.cross(w, jw)) / J_DIAG
+    torque = np.cross(rk["r_T"], u)
+    jw = rk["J"] * w
+    out[11:14] = (torque - np.cross(w, jw)) / rk["J"]
     return out
 
 
-def step(x, u, dt):
+def step(x, u, dt, rk=None):
     """RK4 (discretization.py:229-252) + quaternion normalisation (rocket_6dof.py:371-387)."""
-    k1 = f(x, u)
-    k2 = f(x + dt * k1 / 2, u)
-    k3 = f(x + dt * k2 / 2, u)
-    k4 = f(x + dt * k3, u)
+    k1 = f(x, u, rk)
+    k2 = f(x + dt * k1 / 2, u, rk)
+    k3 = f(x + dt * k2 / 2, u, rk)
+    k4 = f(x + dt * k3, u, rk)
     xn = x + (dt / 6) * (k1 + 2 * k2 + 2 * k3 + k4)
     xn[7:11] = xn[7:11] / np.sqrt(xn[7:11] @ xn[7:11])
     return xn
 
 
-def jacobians(x, u):
+def jacobians(x, u, rk=None):
     """Analytic A_c = df/dx (14 x 14), B_c = df/du (14 x 3) of f."""
+    rk = rk or DEFAULT_ROCKET
     m, q, w = x[0], x[7:11], x[11:14]
     qw, qx, qy, qz = q
     u0, u1, u2 = u
     A = np.zeros((NX, NX)); B = np.zeros((NX, NU))
     tm = np.sqrt(u @ u)
-    B[0] = -ALPHA * u / tm
+    B[0] = -rk["alpha"] * u / tm
     A[1:4, 4:7] = np.eye(3)
     C = dcm_ib(q)
     A[4:7, 0] = -(C @ u) / (m * m)
@@ -111,18 +122,18 @@ def jacobians(x, u):
     A[7:11, 7:11] = 0.5 * np.array([[0, -wx, -wy, -wz], [wx, 0, -wz, wy], [wy, wz, 0, -wx], [wz, -wy, wx, 0]])
     A[7, 11:14] = -0.5 * q[1:4]
     A[8:11, 11:14] = 0.5 * np.array([[qw, qz, -qy], [-qz, qw, qx], [qy, -qx, qw]])
-    j1, j2, j3 = J_DIAG
+    j1, j2, j3 = rk["J"]
     A[11, 11:14] = -(j3 - j2) / j1 * np.array([0, wz, wy])
     A[12, 11:14] = -(j1 - j3) / j2 * np.array([wz, 0, wx])
     A[13, 11:14] = -(j2 - j1) / j3 * np.array([wy, wx, 0])
-    rx, ry, rz = R_T
-    B[11:14] = np.array([[0, -rz, ry], [rz, 0, -rx], [-ry, rx, 0]]) / J_DIAG[:, None]
+    rx, ry, rz = rk["r_T"]
+    B[11:14] = np.array([[0, -rz, ry], [rz, 0, -rx], [-ry, rx, 0]]) / rk["J"][:, None]
     return A, B
 
 
-def linearize(x, u, dt):
+def linearize(x, u, dt, rk=None):
     """rocket_6dof.py:451-457."""
-    A, B = jacobians(x, u)
+    A, B = jacobians(x, u, rk)
     return np.eye(NX) + A * dt, B * dt
 
 
@@ -135,11 +146,11 @@ def drag(x):
     return np.zeros(3)
 
 
-def truth_step(x, u, dt):
+def truth_step(x, u, dt, rk=None):
     """The rollout plant: nominal step + the residual the config-5 GP is trained on
     (data.synthetic_6dof_training_data): the drag dispersion on v and a rate
     damping -0.05 w on w-dot, both at the pre-step state."""
-    xn = step(x, u, dt)
+    xn = step(x, u, dt, rk)
     xn[4:7] += drag(x) * dt
     xn[11:14] += -0.05 * x[11:14] * dt
     return xn
@@ -202,13 +213,17 @@ def default_problem():
                 tan_gs=TAN_GS, trust_x2=10.0, trust_u2=5.0)
 
 
-def build_qp(Xn, Un, gm, x_ref, dt, x0=None, prob=None):
+def build_qp(Xn, Un, gm, x_ref, dt, x0=None, prob=None, rk=None, u_ref=None):
     """QP of gp_mpc.py:394-460 around (Xn, Un) with c_k = GP mean dt (gp_mpc.py:309-314)
-    in deviation variables z = [dx_0, du_0, ..., dx_N], X_ref = x_ref, U_ref = 0.
-    x0 rows: dx_0 = x0 - X_nom[0] (gp_mpc.py:402; 0 when X_nom[0] = x0).
-    Returns Pdiag, q, A (CSR), l, u."""
+    in deviation variables z = [dx_0, du_0, ..., dx_N]; the cost's X_ref is x_ref
+    (one state for every stage, or (N+1, 14)), its U_ref u_ref (N, 3; None = 0)
+    (gp_mpc.py:442-453).  x0 rows: dx_0 = x0 - X_nom[0] (gp_mpc.py:402; 0 when
+    X_nom[0] = x0).  Returns Pdiag, q, A (CSR), l, u."""
     pr = prob or default_problem()
     N = Un.shape[0]
+    x_ref = np.asarray(x_ref, float)
+    Xr = np.broadcast_to(x_ref, (N + 1, NX)) if x_ref.ndim == 1 else x_ref
+    Ur = np.zeros((N, NU)) if u_ref is None else np.asarray(u_ref, float)
     n, m, rp, ci = qp_pattern(N)
     val = np.zeros(rp[-1]); l = np.zeros(m); u = np.zeros(m)
     Pd = np.zeros(n); q = np.zeros(n)
@@ -217,17 +232,17 @@ def build_qp(Xn, Un, gm, x_ref, dt, x0=None, prob=None):
         o = k * (NX + NU)
         w = pr["P"] if k == N else pr["Q"]
         Pd[o:o + NX] = w
-        q[o:o + NX] = w * (Xn[k] - x_ref)
+        q[o:o + NX] = w * (Xn[k] - Xr[k])
         if k < N:
             Pd[o + NX:o + NX + NU] = pr["R"]
-            q[o + NX:o + NX + NU] = pr["R"] * Un[k]
+            q[o + NX:o + NX + NU] = pr["R"] * (Un[k] - Ur[k])
     r = 0
     for i in range(NX):
         val[rp[r]] = 1.0
         l[r] = u[r] = 0.0 if x0 is None else x0[i] - Xn[0, i]
         r += 1
     for k in range(N):
-        Ad, Bd = linearize(Xn[k], Un[k], dt)
+        Ad, Bd = linearize(Xn[k], Un[k], dt, rk)
         c = np.zeros(NX)
         c[4:7] = gm[k, :3] * dt
         c[11:14] = gm[k, 3:] * dt
@@ -279,14 +294,14 @@ def incremental_target(x, upright=False):
     return t
 
 
-def hover_guess(x, N):
+def hover_guess(x, N, g0=G0):
     """gp_mpc.py:271-275: [0, 0, m g0] (thrust on the body z axis, as written) at
     every stage.  As written the loop reads X_pred[k, 0] before the forward
     simulation has filled it, so stages k >= 1 get zero thrust; zero thrust has
     no linearisation of the thrust-magnitude rows (u / |u|), so the evident
     intent m0 g0 is used at every stage."""
     U = np.zeros((N, NU))
-    U[:, 2] = x[0] * G0
+    U[:, 2] = x[0] * g0
     return U
 
 
@@ -300,7 +315,7 @@ def new_rollout(x0, N=30):
                 rho=admm_ref.default_settings().rho, rec=rec, X=None)
 
 
-def rollout_step(gpv, gpw, S, dt=0.1, max_steps=300, qp_settings=None, corrected=True, upright=False):
+def rollout_step(gpv, gpw, S, dt=0.1, max_steps=300, qp_settings=None, corrected=True, upright=False, rk=None):
     """One control step of the 6-DoF rollout (monte_carlo.py:455-537 termination
     rules on the first seven states; one GPMPC.solve pass as the module header)."""
     from . import admm_ref, mc_oracle
@@ -322,10 +337,10 @@ def rollout_step(gpv, gpw, S, dt=0.1, max_steps=300, qp_settings=None, corrected
     for k in range(N):
         dv, dw = gp_mean(gpv, gpw, X[k], U[k], corrected)
         gm[k, :3], gm[k, 3:] = dv, dw
-        X[k + 1] = step(X[k], U[k], dt)
+        X[k + 1] = step(X[k], U[k], dt, rk)
         X[k + 1, 4:7] += dv * dt
         X[k + 1, 11:14] += dw * dt
-    Pd, q, A, l, u = build_qp(X, U, gm, incremental_target(x, upright), dt)
+    Pd, q, A, l, u = build_qp(X, U, gm, incremental_target(x, upright), dt, rk=rk)
     qp = admm_ref.RefQP(len(out["y"]), settings=qp_settings)
     qp.y = out["y"]; qp.rho = np.array([out["rho"]])
     try:
@@ -339,7 +354,7 @@ def rollout_step(gpv, gpw, S, dt=0.1, max_steps=300, qp_settings=None, corrected
     z = r["x"]
     Xo = X + np.array([z[k * (NX + NU):k * (NX + NU) + NX] for k in range(N + 1)])
     Uo = U + np.array([z[k * (NX + NU) + NX:(k + 1) * (NX + NU)] for k in range(N)])
-    xn = truth_step(x, Uo[0], dt)
+    xn = truth_step(x, Uo[0], dt, rk)
     out.update(x=xn, U=Uo, X=Xo, X_pred=X, y=qp.y, rho=float(qp.rho[0]), gm=gm)
     rec[1] += 1; rec[2] = m0 - xn[0]; rec[3] = rec[1] * dt; rec[4:11] = xn[:7]
     rec[11] += r["iter"]; rec[12] += r["status"] == 1; rec[14] = r["status"]; rec[15] = qp.rho[0]
@@ -363,7 +378,7 @@ def initial_condition(seed):
 
 
 def gpmpc_solve(gpv, gpw, S, x0, x_target, max_sqp_iter=10, sqp_tol=1e-4, dt=0.1, qp_settings=None,
-                corrected=True, use_gp=True, prob=None):
+                corrected=True, use_gp=True, prob=None, rk=None, X_ref=None, U_ref=None):
     """GPMPC.solve (gp_mpc.py:229-369) on the 14-state rocket with the QP made
     linear as in build_qp and solved by the OSQP-0.6 restatement:
 
@@ -380,6 +395,9 @@ def gpmpc_solve(gpv, gpw, S, x0, x_target, max_sqp_iter=10, sqp_tol=1e-4, dt=0.1
       a failed pass leaves them as they were (the device writes them back only
       with a solution).
 
+    * the QP cost tracks X_ref ((N+1, 14), default x_target on every stage) and
+      U_ref ((N, 3), default 0) (:442-453); ``rk``: the rocket (rocket_params).
+
     S: dict(U (N, 3), y (m,), rho).  Returns dict(X, U, y, rho, passes,
     converged, qp_status, qp_iters, n_solved, X_pred (of the first pass), gm)."""
     from . import admm_ref
@@ -392,10 +410,11 @@ def gpmpc_solve(gpv, gpw, S, x0, x_target, max_sqp_iter=10, sqp_tol=1e-4, dt=0.1
         if use_gp:
             dv, dw = gp_mean(gpv, gpw, X[k], U[k], corrected)
             gm[k, :3], gm[k, 3:] = dv, dw
-        X[k + 1] = step(X[k], U[k], dt)
+        X[k + 1] = step(X[k], U[k], dt, rk)
         X[k + 1, 4:7] += gm[k, :3] * dt
         X[k + 1, 11:14] += gm[k, 3:] * dt
     X_first = X.copy()
+    x_ref = x_target if X_ref is None else np.asarray(X_ref, float)
     n, m, _, _ = qp_pattern(N)
     qp = admm_ref.RefQP(m, settings=qp_settings)
     qp.y = np.array(S["y"], float); qp.rho = np.array([float(S["rho"])])
@@ -407,7 +426,7 @@ def gpmpc_solve(gpv, gpw, S, x0, x_target, max_sqp_iter=10, sqp_tol=1e-4, dt=0.1
                 for k in range(N):
                     dv, dw = gp_mean(gpv, gpw, X[k], U[k], corrected)
                     gm[k, :3], gm[k, 3:] = dv, dw
-        Pd, q, A, l, u = build_qp(X, U, gm, x_target, dt, x0=x0, prob=prob)
+        Pd, q, A, l, u = build_qp(X, U, gm, x_ref, dt, x0=x0, prob=prob, rk=rk, u_ref=U_ref)
         y_keep, rho_keep = qp.y.copy(), qp.rho.copy()
         try:
             r = qp.solve(Pd, q, A, l, u, np.zeros(Pd.size))
@@ -432,10 +451,11 @@ def gpmpc_solve(gpv, gpw, S, x0, x_target, max_sqp_iter=10, sqp_tol=1e-4, dt=0.1
                 qp_iters=qit, n_solved=nsolved, X_pred=X_first, gm=gm)
 
 
-def solution_cost(X, U, x_target, prob=None):
-    """The QP subproblem's objective at the returned plan (gp_mpc.py:447-458,
-    X_ref = x_target, U_ref = 0)."""
+def solution_cost(X, U, x_target, prob=None, U_ref=None):
+    """The QP subproblem's objective at the returned plan (gp_mpc.py:447-458;
+    x_target: one state or the (N+1, 14) X_ref; U_ref None = 0)."""
     pr = prob or default_problem()
     e = np.asarray(X) - np.asarray(x_target)
-    return float(np.sum(e[:-1] ** 2 * pr["Q"]) + np.sum(np.asarray(U) ** 2 * pr["R"])
+    du = np.asarray(U) - (0.0 if U_ref is None else np.asarray(U_ref))
+    return float(np.sum(e[:-1] ** 2 * pr["Q"]) + np.sum(du ** 2 * pr["R"])
                  + np.sum(e[-1] ** 2 * pr["P"]))

@@ -22,7 +22,7 @@ def test_library_exports_every_declared_symbol():
 
 def test_abi_version_and_error_string():
     from gp_mpc_rocket_landing_amd import _lib
-    assert _lib.abi_version() == 2
+    assert _lib.abi_version() == 3
     assert isinstance(_lib._L.gpmpc_last_error(), bytes)
 
 
@@ -60,3 +60,15 @@ def test_qp_caps_match_the_header():
     src = open(os.path.join(REPO, "gp_mpc_rocket_landing_amd", "csrc", "qp.h")).read()
     caps = {k: int(v) for k, v in re.findall(r"#define (QP_NMAX|QP_MMAX|QP_NNZMAX) (\d+)", src)}
     assert caps == {"QP_NMAX": _lib.QP_NMAX, "QP_MMAX": _lib.QP_MMAX, "QP_NNZMAX": _lib.QP_NNZMAX}
+
+
+def test_sqp_settings_default_to_qp_at_launch():
+    """the SQP passes' settings default to "the same as qp" by a
+    max_iter = 0 sentinel resolved at launch (csrc/fleet.hip fleet_args), so a
+    C caller that edits only cfg.qp after gpmpc_fleet_default_config changes
+    the passes as well; explicit sqp_qp settings start from the final qp."""
+    from gp_mpc_rocket_landing_amd import _lib
+    c = _lib.fleet_default_config()
+    assert c.sqp_qp.max_iter == 0
+    c = _lib.fleet_default_config(max_iter=80, sqp_qp=dict(eps_abs=1e-7))
+    assert c.sqp_qp.max_iter == 80 and c.sqp_qp.eps_abs == 1e-7 and c.qp.eps_abs == 1e-4

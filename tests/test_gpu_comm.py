@@ -22,7 +22,7 @@ def test_rccl_gather_fleet_records_world1(gpu_ctx):
         rec, _ = fl.read()
         out = g.gather(fl.records_dev, 37)
         np.testing.assert_array_equal(out, rec)
-        assert (g.world, g.rank) == (1, 0)
+        assert (g.world, g.rank, g.nranks) == (1, 0, 1)
     finally:
         g.close()
         fl.close()
@@ -42,3 +42,22 @@ def test_rccl_gather_rollout6_records_world1(gpu_ctx):
     finally:
         g.close()
         ro.close()
+
+
+def test_gather_shard_records_world1_reports_rccl(gpu_ctx):
+    """The bench's gather helper on the GPU: the RCCL path runs
+    (no fallback), its info names it, the ranks RCCL's communicator spans
+    (ncclCommCount) and the rows gathered; the records equal the fleet's."""
+    from gp_mpc_rocket_landing_amd.fleet import Fleet, fit_gp, initial_conditions
+    from gp_mpc_rocket_landing_amd.sharding import gather_shard_records
+    gp = fit_gp(gpu_ctx, n_train=200)
+    fl = Fleet(gpu_ctx, gp, 21)
+    try:
+        fl.reset(initial_conditions(21))
+        fl.step(3)
+        rec, _ = fl.read()
+        out, info = gather_shard_records(gpu_ctx, fl.records_dev, rec, 21)
+        np.testing.assert_array_equal(out, rec)
+        assert info == {"path": "rccl", "nranks": 1, "records": 21, "requested": "rccl", "fallback": None}
+    finally:
+        fl.close()

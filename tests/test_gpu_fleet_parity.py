@@ -267,15 +267,22 @@ def test_fleet_flights_match_oracle(gpu_ctx):
 
 
 def test_fleet_mc1024_matches_oracle_monte_carlo(gpu_ctx):
-    """BASELINE configs[3] at full size: the device Monte-Carlo of 1024
-    landings against the oracle's (tests/golden/mc_oracle_1024.npz).  Every
-    landing's outcome and step count is exact (838 SUCCESS / 184
-    CONSTRAINT_VIOLATION / 2 FUEL_EXHAUSTED, 111 614 control steps).  ADMM
-    iteration totals are exact for all but a handful of landings: over
-    111 614 solves a termination check can sit on its threshold to the last
-    bit, where the device's and the C restatement's summation orders decide
-    differently, and that solve runs one more check interval (25 iterations);
-    measured 3 landings.  The bound asserted is 8."""
+    """BASELINE configs[3] at full size, free-running: the device Monte-Carlo
+    of 1024 landings against the oracle's (tests/golden/mc_oracle_1024.npz).
+    Every landing's outcome and step count is exact (838 SUCCESS / 184
+    CONSTRAINT_VIOLATION / 2 FUEL_EXHAUSTED, 111 614 control steps).
+
+    ADMM iteration TOTALS over a free-running flight are not a property of the
+    algorithm but of its exact arithmetic: the oracle against ITSELF with the
+    GP weights alpha scaled by (1 + 2^-52) changes the totals of 2 landings
+    (by 25 and 50 iterations) and the solved counts of 3, and the same oracle
+    with its C ADMM compiled with FMA contraction changes the solved counts of
+    6 (fuel up to 6e-4 relative) -- a ~1e-10 per-step difference that the
+    closed loop carries for ~110 steps until a termination check sits on its
+    threshold (scripts/mc_sensitivity.py, profiles/r4_mc_sensitivity.json).
+    Identical inputs give identical counts at every step of every landing
+    (test_fleet_mc1024_every_step_matches_oracle); here the totals of a few
+    landings may differ by whole check intervals (25 iterations)."""
     from gp_mpc_rocket_landing_amd.fleet import Fleet, fit_gp, initial_conditions
     from conftest import golden
     R = golden("mc_oracle_1024.npz")["records"]
@@ -296,6 +303,92 @@ def test_fleet_mc1024_matches_oracle_monte_carlo(gpu_ctx):
     differ = np.nonzero(rec[:, 11] != R[:, 11])[0]
     assert len(differ) <= 8, differ
     assert np.all(np.mod(rec[differ, 11] - R[differ, 11], 25) == 0)
+
+
+_ORACLE_ST = None
+
+
+def _oracle_state():
+    global _ORACLE_ST
+    if _ORACLE_ST is None:
+        from gp_mpc_rocket_landing_amd.data import synthetic_training_data
+        from oracle import gp_oracle
+        X, U, D = synthetic_training_data(1000, seed=0)
+        _ORACLE_ST = gp_oracle.exact_fit(gp_oracle.features_3dof(X, U), D)
+    return _ORACLE_ST
+
+
+def _check_steps(task):
+    """Pool worker: the oracle's control step (mc_oracle.landing_step) from each
+    landing's device state S against the device's next state T.  Returns
+    (integer mismatches [(landing, fields)], worst relative error per field)."""
+    import os
+    os.environ.setdefault("OPENBLAS_NUM_THREADS", "1")
+    from oracle import mc_oracle
+    idx, S, T = task
+    st = _oracle_state()
+    bad, worst = [], {"x": 0.0, "Xw": 0.0, "Uw": 0.0, "rho": 0.0, "y": 0.0}
+    for j, b in enumerate(idx):
+        s = {k: (v[j] if k != "rho" else float(v[j])) for k, v in S.items()}
+        t = {k: (v[j] if k != "rho" else float(v[j])) for k, v in T.items()}
+        want, info = mc_oracle.landing_step(st, s)
+        f = [0, 1, 11, 12, 13, 14]
+        if not np.array_equal(t["rec"][f], want["rec"][f]):
+            bad.append((int(b), t["rec"][f].tolist(), want["rec"][f].tolist()))
+            continue
+        if info is None:
+            continue
+        for key in ("x", "Xw", "Uw"):
+            worst[key] = max(worst[key], float(np.max(np.abs(t[key] - want[key]) / np.maximum(np.abs(want[key]), 1.0))))
+        worst["rho"] = max(worst["rho"], abs(t["rho"] - want["rho"]) / abs(want["rho"]))
+        ys = max(float(np.abs(want["y"]).max()), 1e-300)
+        worst["y"] = max(worst["y"], float(np.max(np.abs(t["y"] - want["y"]) / np.maximum(np.abs(want["y"]), ys))))
+    return bad, worst
+
+
+def test_fleet_mc1024_every_step_matches_oracle(gpu_ctx):
+    """VERDICT r3 #1, "iteration counts bit-exact" at full size: every control
+    step of all 1024 landings of BASELINE configs[3], flown to termination
+    (~112 000 steps), against the oracle's step (mc_oracle.landing_step =
+    monte_carlo.py:455-537 under the solve protocol: GP posterior, RTI QP, the
+    C OSQP-0.6 restatement, plant) from the device's own previous state (x, the
+    shifted plan, OSQP's persistent scaled y and rho, the record).  Outcome,
+    step count, ADMM iterations, solved count, status exact at EVERY step;
+    state, plan, rho and duals within 1e-6 (unit floor; duals floored at
+    max |y|).  The oracle runs in a pool of CPU processes beside the fleet."""
+    import multiprocessing as mp
+    import os
+    from gp_mpc_rocket_landing_amd.fleet import Fleet, fit_gp, initial_conditions
+    B = 1024
+    gp = fit_gp(gpu_ctx, n_train=1000)
+    fl = Fleet(gpu_ctx, gp, B, max_steps=300)
+    workers = max(1, min(16, len(os.sched_getaffinity(0))))
+    pending, nsteps = [], 0
+    with mp.get_context("spawn").Pool(workers) as pool:
+        try:
+            fl.reset(initial_conditions(B))
+            S = fl.state()
+            for k in range(302):
+                run = np.nonzero(S["rec"][:, 0] == 0)[0]
+                if run.size == 0:
+                    break
+                fl.step(1)
+                T = fl.state()
+                nsteps += run.size
+                for c in np.array_split(run, max(1, min(4 * workers, run.size // 8))):
+                    pending.append(pool.apply_async(_check_steps, ((c, {kk: v[c] for kk, v in S.items()},
+                                                                    {kk: v[c] for kk, v in T.items()}),)))
+                S = T
+            assert np.all(S["rec"][:, 0] != 0), "every landing terminates within max_steps"
+        finally:
+            fl.close()
+        res = [p.get(timeout=600) for p in pending]
+    bad = [b for r, _ in res for b in r]
+    worst = {k: max(w[k] for _, w in res) for k in res[0][1]}
+    assert not bad, (len(bad), bad[:5])
+    assert nsteps > 100000, nsteps
+    for key, tol in (("x", 1e-6), ("Xw", 1e-6), ("Uw", 1e-6), ("rho", 1e-6), ("y", 1e-6)):
+        assert worst[key] <= tol, (key, worst)
 
 
 def test_fleet_shards_reproduce_the_whole_fleet(gpu_ctx):

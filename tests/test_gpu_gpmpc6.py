@@ -1,6 +1,7 @@
-"""The reference's own 14-state GPMPC.solve on the device (VERDICT r2 #1):
-``GPMPC(Rocket6DoFDynamics(), StructuredRocketGP, GPMPCConfig(N=30))`` runs
-csrc/fleet6.hip at a batch of one (gpmpc_rollout6_solve) and is checked per
+"""The reference's own 14-state GPMPC.solve on the device (VERDICT r2 #1, r3 #2):
+``GPMPC(Rocket6DoFDynamics(), StructuredRocketGP, GPMPCConfig())`` (N = 20, or
+N = 30 for BASELINE configs[4]) runs csrc/fleet6.hip at a batch of one
+(gpmpc_rollout6_solve_ref) and is checked per
 control step against oracle/sixdof_oracle.gpmpc_solve (gp_mpc.py:229-369
 restated, the QP made linear as the rollouts, the C OSQP-0.6 restatement),
 from the device's own previous controller state (warm-start U, scaled duals,
@@ -30,26 +31,44 @@ def _target(x):
     return t
 
 
-def _fly(gp, steps, max_sqp_iter, seed_index=0, tol=1e-6, device_alpha=False):
-    from gp_mpc_rocket_landing_amd.dynamics import Rocket6DoFDynamics
+def _fly(gp, steps, max_sqp_iter, seed_index=0, tol=1e-6, device_alpha=False, N=30, rocket_cfg=None,
+         config=None, refs=False):
+    """``rocket_cfg``: a Rocket6DoFConfig for the plant and the oracle; ``config``:
+    the GPMPCConfig as given (default GPMPCConfig(N, max_sqp_iter)); ``refs``: a
+    reference trajectory X_ref (a straight line from x to the target over the
+    horizon) and controls U_ref (hover thrust) in every solve (gp_mpc.py:442-453,
+    U_ref also the first guess, :268-269)."""
+    from gp_mpc_rocket_landing_amd.dynamics import Rocket6DoFConfig, Rocket6DoFDynamics
     from gp_mpc_rocket_landing_amd.mpc import GPMPC, GPMPCConfig
-    from gp_mpc_rocket_landing_amd.rollouts6 import initial_conditions_6dof
+    from gp_mpc_rocket_landing_amd.rollouts6 import initial_conditions_6dof, qp_rows
     from oracle import sixdof_oracle as so
     ov, ow = oracle_gps(gp)
     if device_alpha:  # the oracle loop on the device fit's coefficients (fit pinned elsewhere)
         ov = dict(ov, alpha=gp.gp_v.device_handle.alpha())
         ow = dict(ow, alpha=gp.gp_omega.device_handle.alpha())
-    dyn = Rocket6DoFDynamics()
-    mpc = GPMPC(dyn, gp, GPMPCConfig(N=30, max_sqp_iter=max_sqp_iter, use_gp_uncertainty=False))
+    rc = rocket_cfg or Rocket6DoFConfig()
+    dyn = Rocket6DoFDynamics(rc)
+    rk = so.rocket_params(np.diag(rc.J_B), rc.r_T_B, rc.g_I, rc.I_sp, rc.g0)
+    cfg = config or GPMPCConfig(N=N, max_sqp_iter=max_sqp_iter, use_gp_uncertainty=False)
+    N, max_sqp_iter = cfg.N, cfg.max_sqp_iter
+    mpc = GPMPC(dyn, gp, cfg)
     assert type(mpc).__name__ == "GPMPC6DoF" and isinstance(mpc, GPMPC)
     x = initial_conditions_6dof(seed_index + 1)[seed_index]
-    S = dict(U=so.hover_guess(x, 30), y=np.zeros(1104), rho=0.1)
+    S = dict(U=so.hover_guess(x, N, rc.g0), y=np.zeros(qp_rows(N)), rho=0.1)
     seen = []
     try:
         for k in range(steps):
             xt = _target(x)
-            sol = mpc.solve(x, xt)
-            want = so.gpmpc_solve(ov, ow, S, x, xt, max_sqp_iter=max_sqp_iter, sqp_tol=1e-4, corrected=False)
+            Xr = Ur = None
+            if refs:
+                a = (np.arange(N + 1) / N)[:, None]
+                Xr = (1 - a) * x + a * xt
+                Ur = np.tile([0.0, 0.0, 0.9 * x[0] * rc.g0], (N, 1))
+                if k == 0:
+                    S["U"] = Ur.copy()   # U_ref as the first guess
+            sol = mpc.solve(x, xt, X_ref=Xr, U_ref=Ur)
+            want = so.gpmpc_solve(ov, ow, S, x, xt, max_sqp_iter=max_sqp_iter, sqp_tol=cfg.sqp_tol,
+                                  corrected=False, rk=rk, X_ref=Xr, U_ref=Ur)
             tag = (k, max_sqp_iter)
             assert mpc.last_status == want["qp_status"], (tag, mpc.last_status, want["qp_status"])
             assert mpc.last_iterations == want["qp_iters"], (tag, mpc.last_iterations, want["qp_iters"])
@@ -62,17 +81,55 @@ def _fly(gp, steps, max_sqp_iter, seed_index=0, tol=1e-6, device_alpha=False):
                 ok, worst = close(got, want[key], 1.0, rtol=tol)
                 assert ok, (tag, key, worst)
             if np.isfinite(sol.cost):
-                ok, worst = close(sol.cost, so.solution_cost(want["X"], want["U"], xt), 1.0, rtol=tol)
+                ok, worst = close(sol.cost, so.solution_cost(want["X"], want["U"], xt if Xr is None else Xr,
+                                                             U_ref=Ur), 1.0, rtol=tol)
                 assert ok, (tag, "cost", worst)
             seen.append((want["qp_status"], want["qp_iters"], want["passes"], want["converged"]))
             st = mpc._ro.state()   # the device's controller state for the next step's oracle
             S = dict(U=st["U"][0], y=st["y"][0], rho=float(st["rho"][0]))
             if not sol.success and max_sqp_iter <= 1:
                 break
-            x = so.truth_step(x, sol.u0, 0.1)
+            x = so.truth_step(x, sol.u0, 0.1, rk)
     finally:
         mpc.close()
     return seen
+
+
+def test_gpmpc6_reference_defaults_n20():
+    """``GPMPC(Rocket6DoFDynamics(), gp, GPMPCConfig())`` -- the
+    reference docstring's call (gp_mpc.py:85), N = 20 (gp_mpc.py:110), the
+    default uncertainty propagation on -- runs on the device and matches the
+    oracle over 10 control steps: status, iterations, passes exact, plans 1e-6."""
+    from gp_mpc_rocket_landing_amd.mpc import GPMPCConfig
+    seen = _fly(_surface(), 10, 1, config=GPMPCConfig())
+    assert len(seen) >= 10, seen
+
+
+def test_gpmpc6_reference_loop_n20():
+    """The reference's 10-pass loop at N = 20 (GPMPCConfig(max_sqp_iter=10))."""
+    from gp_mpc_rocket_landing_amd.mpc import GPMPCConfig
+    seen = _fly(_surface(), 6, 10, config=GPMPCConfig(max_sqp_iter=10, use_gp_uncertainty=False))
+    assert len(seen) == 6, seen
+
+
+def test_gpmpc6_nondefault_rocket():
+    """A Rocket6DoFConfig other than the default (diagonal J_B, r_T_B, g_I,
+    I_sp, g0) at N = 20 and N = 30: the device dynamics, Jacobians and hover
+    guess take the caller's rocket; 8 steps each vs the oracle with it."""
+    from gp_mpc_rocket_landing_amd.dynamics import Rocket6DoFConfig
+    rc = Rocket6DoFConfig(J_B=np.diag([0.03, 1.1, 0.9]) * 0.168, r_T_B=np.array([-0.3, 0.0, 0.02]),
+                          g_I=np.array([-1.0, 0.01, 0.0]), I_sp=25.0, g0=1.05)
+    for N in (20, 30):
+        seen = _fly(_surface(), 8, 1, N=N, rocket_cfg=rc)
+        assert len(seen) >= 8, (N, seen)
+
+
+def test_gpmpc6_reference_trajectory():
+    """X_ref / U_ref in the QP cost (gp_mpc.py:442-453) and U_ref as the first
+    guess (:268-269), RTI and the 10-pass loop, N = 20."""
+    for passes in (1, 10):
+        seen = _fly(_surface(), 8, passes, N=20, refs=True)
+        assert len(seen) >= 8, (passes, seen)
 
 
 def test_gpmpc6_rti_step_matches_oracle():

@@ -66,7 +66,11 @@ def test_rocket6dof_api():
     A_d, B_d, c = d.linearize_discrete(x, np.array([2.0, 0.1, 0.0]), 0.1)
     np.testing.assert_allclose(A_d @ x + B_d @ np.array([2.0, 0.1, 0.0]) + c,
                                d.step(x, np.array([2.0, 0.1, 0.0]), 0.1), atol=1e-14)
-    assert not create_rocket_6dof(I_sp=25.0).matches_device_model()
+    # the device model's rocket parameters are runtime values (ABI 3); only a
+    # non-diagonal inertia tensor is outside it
+    assert create_rocket_6dof(I_sp=25.0).matches_device_model()
+    J = np.diag([0.02, 1.0, 1.0]) * 0.168; J[0, 1] = J[1, 0] = 0.01
+    assert not create_rocket_6dof(J_B=J).matches_device_model()
 
 
 def test_gpmpc_dispatches_on_the_state_dimension():
@@ -75,13 +79,21 @@ def test_gpmpc_dispatches_on_the_state_dimension():
     from gp_mpc_rocket_landing_amd.mpc import CostWeights, GPMPC, GPMPCConfig
     from gp_mpc_rocket_landing_amd.mpc.gp_mpc import GPMPC6DoF
     gp = StructuredRocketGP()
-    m = GPMPC(Rocket6DoFDynamics(), gp)          # GPMPCConfig() -> N = 30 on this path
-    assert isinstance(m, GPMPC6DoF) and isinstance(m, GPMPC) and m.config.N == 30
-    assert m._cfg_kw["fitc_mean_as_written"] == 1
+    m = GPMPC(Rocket6DoFDynamics(), gp)          # GPMPCConfig(): the reference's N = 20
+    assert isinstance(m, GPMPC6DoF) and isinstance(m, GPMPC) and m.config.N == 20
+    assert m._cfg_kw["fitc_mean_as_written"] == 1 and m._cfg_kw["horizon"] == 20
+    assert GPMPC(Rocket6DoFDynamics(), gp, GPMPCConfig(N=30))._cfg_kw["horizon"] == 30
+    with pytest.raises(NotImplementedError):    # compiled horizons only
+        GPMPC(Rocket6DoFDynamics(), gp, GPMPCConfig(N=25))
+    # a non-default rocket reaches the device config (rocket_6dof.py:36-84 fields)
+    k = GPMPC(Rocket6DoFDynamics(Rocket6DoFConfig(I_sp=20.0, g0=2.0, r_T_B=np.array([-0.3, 0.01, 0.0]))),
+              gp)._cfg_kw
+    assert k["rocket_alpha"] == 1.0 / 40.0 and k["rocket_g0"] == 2.0
+    np.testing.assert_array_equal(k["rocket_r_t"], [-0.3, 0.01, 0.0])
+    np.testing.assert_array_equal(k["rocket_j"], np.array([0.02, 1.0, 1.0]) * 0.168)
+    J = np.diag([0.02, 1.0, 1.0]) * 0.168; J[0, 2] = J[2, 0] = 0.01
     with pytest.raises(NotImplementedError):
-        GPMPC(Rocket6DoFDynamics(), gp, GPMPCConfig(N=20))
-    with pytest.raises(NotImplementedError):
-        GPMPC(Rocket6DoFDynamics(Rocket6DoFConfig(I_sp=20.0)), gp)
+        GPMPC(Rocket6DoFDynamics(Rocket6DoFConfig(J_B=J)), gp)
     Q = CostWeights().Q.copy(); Q[1, 2] = Q[2, 1] = 0.5
     with pytest.raises(NotImplementedError):
         GPMPC(Rocket6DoFDynamics(), gp, cost_weights=CostWeights(Q=Q))
@@ -101,6 +113,10 @@ def test_rollout6_default_config_is_the_reference_problem():
     assert c.tan_gamma_gs == np.tan(cp.gamma_gs_rad)
     assert (c.trust_x2, c.trust_u2, c.use_gp_mean, c.upright_target) == (10.0, 5.0, 1, 0)
     assert c.horizon == 30 and c.qp.max_iter == 50 and c.qp.eps_abs == 1e-4
+    # Rocket6DoFConfig defaults (rocket_6dof.py:36-84)
+    np.testing.assert_array_equal(np.array(c.rocket_j), np.array([0.02, 1.0, 1.0]) * 0.168)
+    assert list(c.rocket_r_t) == [-0.25, 0.0, 0.0] and list(c.rocket_g_i) == [-1.0, 0.0, 0.0]
+    assert c.rocket_alpha == 1.0 / 30.0 and c.rocket_g0 == 1.0
     c2 = _lib.rollout6_default_config(q_diag=np.arange(14.0), max_iter=7)
     assert list(c2.q_diag) == list(range(14)) and c2.qp.max_iter == 7
     with pytest.raises(ValueError):

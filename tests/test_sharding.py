@@ -108,3 +108,59 @@ def test_gather_real_landing_records_world2_gloo():
         p.join(timeout=120)
         assert p.exitcode == 0
     np.testing.assert_array_equal(out, golden("mc_oracle_1024.npz")["records"][:total])
+
+
+def _agreed_gather_worker(rank, world, total, port, q):
+    """gather_shard_records on a gloo group with no device context on any rank:
+    the RCCL set-up fails everywhere, every rank learns that from the agreed
+    readiness count, and all fall back to torch.distributed.gather together."""
+    import torch.distributed as dist
+    from gp_mpc_rocket_landing_amd.sharding import gather_shard_records
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    first, count = shard_range(total, rank, world)
+    out, info = gather_shard_records(None, None, _records_for(first, count), total)
+    q.put((rank, out, info))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_gather_shard_records_agreed_fallback_world2_gloo():
+    """The bench's / run_monte_carlo's gather: a failed RCCL set-up
+    never leaves one rank in a collective the others skipped -- both ranks
+    return, rank 0 holds the ragged records in global order, and the info
+    records the path that ran, the ranks it spanned and the fallback reason."""
+    total = 11
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_agreed_gather_worker, args=(r, 2, total, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict((r, (o, i)) for r, o, i in (q.get(timeout=120) for _ in range(2)))
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    out0, info0 = res[0]
+    out1, info1 = res[1]
+    np.testing.assert_array_equal(out0, _records_for(0, total))
+    assert out1 is None
+    for info in (info0, info1):
+        assert info["path"] == "torch" and info["nranks"] == 2 and info["requested"] == "rccl"
+        assert "2 of 2 ranks not ready" in info["fallback"], info
+    assert info0["records"] == total and info1["records"] == 0
+
+
+def test_gather_shard_records_world1_without_group():
+    """No process group, no context: a world of one falls back to the host
+    records themselves and says so."""
+    from gp_mpc_rocket_landing_amd.sharding import gather_shard_records
+    rec = _records_for(0, 5)
+    out, info = gather_shard_records(None, None, rec, 5)
+    np.testing.assert_array_equal(out, rec)
+    assert info["path"] == "torch" and info["nranks"] == 1 and info["records"] == 5
+    out, info = gather_shard_records(None, None, rec, 5, path="torch")
+    assert info["fallback"] is None and info["path"] == "torch"
+    import pytest
+    with pytest.raises(ValueError):
+        gather_shard_records(None, None, rec, 5, path="mpi")
