@@ -270,11 +270,24 @@ __global__ __launch_bounds__(256, 2) void k_gemm128(int M, int N, int K, const d
                                                     int tri_grid) {
   // grid z = batch x ksplit: split s of a matrix covers K range [s*kc, (s+1)*kc)
   // and accumulates alpha*acc into C with fp64 atomics (beta must be 1 then)
-  const int bz = blockIdx.z / ksplit, sp = blockIdx.z % ksplit;
+  int bz = blockIdx.z / ksplit, sp = blockIdx.z % ksplit;
+  int ry = blockIdx.y;
+  if (tri_grid == 3) {
+    // XCD-batched row blocks (launch_gemm_nt_rowblock, batch a multiple of 8):
+    // workgroup L runs on XCD L % 8; its m-th workgroup there takes matrix
+    // 8 (m / (ny ks)) + L % 8, so all row tiles and K splits of a matrix share
+    // one XCD and its B panel (the potrf's row block / inverse) is read from
+    // that XCD's L2 instead of once per row tile across all eight
+    const int ny = gridDim.y, L = blockIdx.x + blockIdx.y * gridDim.x + blockIdx.z * gridDim.x * gridDim.y;
+    const int m = L >> 3, per = ny * ksplit, rem = m % per;
+    bz = (L & 7) + 8 * (m / per);
+    sp = rem / ny;
+    ry = rem % ny;
+  }
   A += bz * sA_;
   B += bz * sB_;
   C += bz * sC_;
-  int by = tri_a ? (int)gridDim.y - 1 - (int)blockIdx.y : (int)blockIdx.y, bx = blockIdx.x;
+  int by = tri_a ? (int)gridDim.y - 1 - ry : ry, bx = tri_grid == 3 ? 0 : (int)blockIdx.x;
   if (tri_grid == 1) tri_tile(blockIdx.x, by, bx);  // 1-D grid over the lower-triangular tiles
   if (tri_grid == 2) {
     // column-grouped: workgroup L runs on XCD L % 8; its m-th workgroup there
@@ -832,8 +845,14 @@ hipError_t launch_gemm_nt_rowblock(hipStream_t s, int M, int N, int K, const dou
   // split K (partial products added atomically): only with beta = 1 and C apart from A, B
   if (ksplit < 1 || beta != 1.0) ksplit = 1;
   dim3 g(1, (M + BT - 1) / BT, batch * ksplit);
+  // a batch of >= 8 matrices (a multiple of 8): each matrix's row tiles on one XCD
+  static const int xb_env = [] {
+    const char *e = getenv("GPMPC_ROWBLOCK_XCD");
+    return e ? atoi(e) : 1;
+  }();
+  const int tg = (xb_env && batch >= 8 && batch % 8 == 0) ? 3 : 0;
   hipLaunchKernelGGL(k_gemm128<EPI_STORE>, g, dim3(256), 0, s, M, N, K, A, lda, B, ldb, C, ldc,
-                     alpha, beta, 0, lower_c, sA, sB, sC, M, nullptr, (int64_t)0, ksplit, 0);
+                     alpha, beta, 0, lower_c, sA, sB, sC, M, nullptr, (int64_t)0, ksplit, tg);
   return hipGetLastError();
 }
 

@@ -364,7 +364,18 @@ def test_fleet_mc1024_every_step_matches_oracle(gpu_ctx):
     fl = Fleet(gpu_ctx, gp, B, max_steps=300)
     workers = max(1, min(16, len(os.sched_getaffinity(0))))
     pending, nsteps = [], 0
-    with mp.get_context("spawn").Pool(workers) as pool:
+    # one BLAS thread per worker process (the box sets 16 for every process)
+    saved = {k: os.environ.get(k) for k in ("OMP_NUM_THREADS", "OPENBLAS_NUM_THREADS", "MKL_NUM_THREADS")}
+    os.environ.update(OMP_NUM_THREADS="1", OPENBLAS_NUM_THREADS="1", MKL_NUM_THREADS="1")
+    try:
+        pool = mp.get_context("spawn").Pool(workers)
+    finally:
+        for k, v in saved.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+    with pool:
         try:
             fl.reset(initial_conditions(B))
             S = fl.state()
@@ -379,10 +390,17 @@ def test_fleet_mc1024_every_step_matches_oracle(gpu_ctx):
                     pending.append(pool.apply_async(_check_steps, ((c, {kk: v[c] for kk, v in S.items()},
                                                                     {kk: v[c] for kk, v in T.items()}),)))
                 S = T
+                if k % 10 == 0:
+                    print(f"mc1024 step-locked: device step {k}, {run.size} running, {nsteps} steps queued",
+                          flush=True)
             assert np.all(S["rec"][:, 0] != 0), "every landing terminates within max_steps"
         finally:
             fl.close()
-        res = [p.get(timeout=600) for p in pending]
+        res = []
+        for i, p in enumerate(pending):
+            res.append(p.get(timeout=600))
+            if i % 500 == 0:
+                print(f"mc1024 step-locked: {i} of {len(pending)} oracle chunks checked", flush=True)
     bad = [b for r, _ in res for b in r]
     worst = {k: max(w[k] for _, w in res) for k in res[0][1]}
     assert not bad, (len(bad), bad[:5])
