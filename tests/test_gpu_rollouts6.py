@@ -37,7 +37,7 @@ def _one(S, b):
     return {k: (v[b] if k != "rho" else float(v[b])) for k, v in S.items()}
 
 
-def _run(gpu_ctx, n_train, n_inducing, nb, steps, tol=1e-6, as_written=False, horizon=30, rocket=None):
+def _run(gpu_ctx, n_train, n_inducing, nb, steps, tol=1e-6, as_written=False, horizon=30, rocket=None, qp=None):
     from gp_mpc_rocket_landing_amd.rollouts6 import Rollouts6, fit_structured_fitc, initial_conditions_6dof
     from oracle import sixdof_oracle as so
     gv, gw = fit_structured_fitc(gpu_ctx, n_train=n_train, n_inducing=n_inducing)
@@ -50,6 +50,11 @@ def _run(gpu_ctx, n_train, n_inducing, nb, steps, tol=1e-6, as_written=False, ho
         rk = so.rocket_params(J, rT, gI, isp, g0)
         kw = dict(rocket_j=rk["J"], rocket_r_t=rk["r_T"], rocket_g_i=rk["g_I"], rocket_alpha=rk["alpha"],
                   rocket_g0=rk["g0"])
+    qs = None
+    if qp:   # the same ADMM settings on both sides
+        from oracle import admm_ref
+        kw.update(qp)
+        qs = admm_ref.default_settings(**qp)
     ro = Rollouts6(gpu_ctx, gv, gw, nb, fitc_mean_as_written=int(as_written), horizon=horizon, **kw)
     seen = 0
     try:
@@ -62,7 +67,7 @@ def _run(gpu_ctx, n_train, n_inducing, nb, steps, tol=1e-6, as_written=False, ho
             T = ro.state()
             for b in np.nonzero(S["rec"][:, 0] == 0)[0]:
                 st = dict(x=S["x"][b], U=S["U"][b], y=S["y"][b], rho=float(S["rho"][b]), rec=S["rec"][b], X=None)
-                want, info = so.rollout_step(ov, ow, st, corrected=not as_written, rk=rk)
+                want, info = so.rollout_step(ov, ow, st, corrected=not as_written, rk=rk, qp_settings=qs)
                 got = _one(T, b)
                 tag = (k, int(b))
                 np.testing.assert_array_equal(got["rec"][[0, 1, 11, 12, 13, 14]],
@@ -148,3 +153,13 @@ def test_rollouts6_horizon20_default_rocket(gpu_ctx):
     """N = 20 with the default rocket: 4 rollouts x 25 steps vs the oracle."""
     seen, S = _run(gpu_ctx, 300, 50, 4, 25, horizon=20)
     assert seen >= 25, seen
+
+
+def test_rollouts6_solved_setting(gpu_ctx):
+    """the configs[4] controller at the ADMM setting where >= 90% of
+    its QPs return "solved" (bench.SOLVED_QP6: max_iter 4000, eps 1e-4), 4 rollouts
+    x 8 steps vs the oracle with the same settings: iterations / status exact,
+    plans and duals 1e-6."""
+    import bench
+    seen, S = _run(gpu_ctx, 300, 50, 4, 8, qp=dict(bench.SOLVED_QP6))
+    assert seen >= 8, seen
