@@ -1193,11 +1193,31 @@ static hipError_t launch_potrf_batched128(hipStream_t s, int n, int batch, doubl
     const char *v = getenv("GPMPC_POTRF_KSPLIT");
     return v ? atoi(v) : 0;
   }();
+  // Left-looking block columns, fused: the diagonal block's update alone, the diagonal
+  // kernel, then ONE pass over the rows below (update + panel solve, k_gemm128_updsolve)
+  // instead of an update launch over all rows and a panel-solve launch; for batches that
+  // are a multiple of 8 whose rows below fill >= 512 workgroups (GPMPC_POTRF_FUSE=0: off)
+  static const int fuse_env = [] {
+    const char *v = getenv("GPMPC_POTRF_FUSE");
+    return v ? atoi(v) : 1;
+  }();
+  const bool fuse_ok = fuse_env && OBk > DB && !tblk && !lat && batch % 8 == 0;
   for (int K0 = 0; K0 < n; K0 += OBk) {
     const int pw = min(OBk, n - K0);
     for (int c = K0; c < K0 + pw; c += DB) {
       const int w = min(DB, n - c);
-      if (c > K0) {
+      const int below = n - c - w;
+      const bool fuse = fuse_ok && below > 0 && (below + DB - 1) / DB * batch >= 512;
+      if (c > K0 && fuse) {
+        // the diagonal block's rows only (one tile per matrix), K split to fill the device
+        const int K = c - K0;
+        int ks = 1;
+        if (ksplit_env != 1)
+          while (ks < K / DB && batch * ks < 512) ++ks;
+        e = launch_gemm_nt_rowblock(s, w, w, K, at(c, K0), lda, at(c, K0), lda, at(c, c), lda, -1.0, 1.0, batch,
+                                    stride, stride, stride, 1, ks);
+        if (e != hipSuccess) return e;
+      } else if (c > K0) {
         // the block column's update by all earlier columns of the outer panel; K split
         // (atomic partial sums) when its row tiles give fewer than ~2 workgroups per CU,
         // >= 128 of K per split (GPMPC_POTRF_KSPLIT=1: never)
@@ -1215,7 +1235,13 @@ static hipError_t launch_potrf_batched128(hipStream_t s, int n, int batch, doubl
       else
         hipLaunchKernelGGL(k_potrf_diag128<false>, dim3(batch), dim3(256), DIAG128_LDS, s, n, c,
                            A, lda, stride, info, c + DB < n ? Linv : nullptr, sweep | (tblk ? 2 : 0));
-      if (c + DB < n && (e = psolve(c)) != hipSuccess) return e;
+      if (fuse) {
+        e = launch_gemm_updsolve(s, below, c - K0, at(c + w, K0), lda, at(c, K0), at(c + w, c), Linv, batch,
+                                 stride, stride, (int64_t)DB * DB);
+        if (e != hipSuccess) return e;
+      } else if (c + DB < n && (e = psolve(c)) != hipSuccess) {
+        return e;
+      }
     }
     const int t0 = K0 + pw;
     if (t0 < n) {
@@ -1485,7 +1511,22 @@ hipError_t launch_tri_inverse(hipStream_t s, int n, const double *L, int64_t ldl
   hipLaunchKernelGGL(k_trsm_panel, dim3((std::min(n, TB) + 63) / 64, nd), dim3(256), 0, s, n,
                      std::min(n, TB), L, ldl, Linv, W, ldw, 0, 1);
   for (int b = TB; b < n; b *= 2) {
-    for (int s0 = 0; s0 + b < n; s0 += 2 * b) {
+    // the pairs of a level whose C block is full (mc = b) are one batched launch per
+    // GEMM (their operands sit (2b)(ld + 1) apart on the diagonal); a ragged last pair
+    // goes alone
+    const int full = (n / (2 * b)) > 0 ? ((n - b) / (2 * b) + 1) : 0;   // pairs with s0 + b < n
+    int nf = 0;
+    while (nf < full && (nf * 2 * b) + 2 * b <= n) ++nf;
+    if (nf > 0) {
+      const int64_t dL = (int64_t)2 * b * (ldl + 1), dW = (int64_t)2 * b * (ldw + 1), dT = (int64_t)b * b;
+      hipError_t e = launch_gemm_nn_batched(s, b, b, b, L + (int64_t)b * ldl, ldl, dL, W, ldw, dW, tmp, b, dT,
+                                            1.0, 0.0, nf);
+      if (e != hipSuccess) return e;
+      e = launch_gemm_nn_batched(s, b, b, b, W + (int64_t)b * ldw + b, ldw, dW, tmp, b, dT, W + (int64_t)b * ldw,
+                                 ldw, dW, -1.0, 0.0, nf);
+      if (e != hipSuccess) return e;
+    }
+    for (int s0 = nf * 2 * b; s0 + b < n; s0 += 2 * b) {
       const int c0 = s0 + b, mc = std::min(n, s0 + 2 * b) - c0;
       hipError_t e = launch_gemm_nn(s, mc, b, b, L + (int64_t)c0 * ldl + s0, ldl,
                                     W + (int64_t)s0 * ldw + s0, ldw, tmp, b, 1.0, 0.0);

@@ -20,6 +20,12 @@ hipError_t launch_gemm_nt_rowblock(hipStream_t s, int M, int N, int K, const dou
                                    int64_t ldc, double alpha, double beta, int batch, int64_t sA,
                                    int64_t sB, int64_t sC, int lower_c = 0, int ksplit = 1);
 
+// the potrf's fused left-looking step for the rows below a diagonal block (gemm.hip):
+// C (M x 128) <- (C - A B^T) Linv^T, A (M x K) and B (128 x K) with leading dimension lda,
+// Linv (128 x 128, lower, ld 128); batch a multiple of 8
+hipError_t launch_gemm_updsolve(hipStream_t s, int M, int K, const double *A, int64_t lda, const double *B,
+                                double *C, const double *Linv, int batch, int64_t sA, int64_t sC, int64_t sL);
+
 // latency form for K <= 128 (see gemm.hip): mode 0 = rows in place (N <= 128,
 // C may alias A; tri_b: B lower-triangular), mode 1 = lower C += A A^T (M == N)
 hipError_t launch_gemm_lat(hipStream_t s, int mode, int M, int N, int K, const double *A,
@@ -31,6 +37,10 @@ hipError_t launch_gemm_lat(hipStream_t s, int mode, int M, int N, int K, const d
 hipError_t launch_gemm_nn(hipStream_t s, int M, int N, int K, const double *A, int64_t lda,
                           const double *B, int64_t ldb, double *C, int64_t ldc, double alpha,
                           double beta);
+
+hipError_t launch_gemm_nn_batched(hipStream_t s, int M, int N, int K, const double *A, int64_t lda, int64_t sA,
+                                  const double *B, int64_t ldb, int64_t sB, double *C, int64_t ldc, int64_t sC,
+                                  double alpha, double beta, int batch);
 
 // C = alpha A^T B + beta C with A (K x M) and B (K x N) row-major ("TN")
 hipError_t launch_gemm_tn(hipStream_t s, int M, int N, int K, const double *A, int64_t lda,

@@ -374,6 +374,74 @@ __global__ __launch_bounds__(256, 2) void k_gemm128(int M, int N, int K, const d
 }
 
 
+// The potrf's left-looking block-column step for the rows below the diagonal block,
+// fused (one workgroup per 128-row tile r of matrix b, XCD-batched like the row-block GEMM):
+//   Y = C - A_r B^T              C = the tile's 128 panel columns, A_r = its rows' K = c left
+//                                columns, B = the diagonal block rows' left columns (K = c)
+//   X = Y Linv^T                 Linv = L_cc^-1 (128 x 128, lower) from the diagonal kernel
+// Y goes to C in place and is read back by the second product through agent-scope loads
+// (the vector L1 is not refreshed by this workgroup's own stores); X overwrites it.  The
+// separate update launch, the panel-solve launch and one read + write of the panel
+// between them become one pass; the second product skips the upper triangle of Linv.
+// K = 0 (the first block column) is the plain in-place panel solve.
+__global__ __launch_bounds__(256, 2) void k_gemm128_updsolve(int M, int K, const double *__restrict__ A,
+                                                            int64_t lda, const double *__restrict__ B,
+                                                            double *__restrict__ C, const double *__restrict__ Linv,
+                                                            int64_t sA_, int64_t sC_, int64_t sL_) {
+  const int ny = gridDim.y, L = blockIdx.y + blockIdx.z * ny;
+  const int m = L >> 3;
+  const int bz = (L & 7) + 8 * (m / ny), ry = m % ny;  // matrix b's row tiles on XCD b % 8
+  A += bz * sA_;
+  B += bz * sA_;
+  C += bz * sC_;
+  Linv += bz * sL_;
+  const int r0 = ry * BT;
+  __shared__ double sA[2][BT][GP];
+  __shared__ double sB[2][BT][GP];
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int qj = (wave & 1) * 64;
+  d4_t acc[4][4];
+  if (K > 0) {
+    mma128_tile<true>(A, lda, B, lda, M, BT, r0, 0, 0, K, sA, sB, acc, -1, false);
+#pragma unroll
+    for (int x = 0; x < 4; ++x)
+#pragma unroll
+      for (int y = 0; y < 4; ++y)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = r0 + mma128_row(wave, x, true) + mf_row(lane, r);
+          const int col = qj + y * 16 + mf_col(lane);
+          if (row < M) {
+            double *p = C + (int64_t)row * lda + col;
+            *p = -acc[x][y][r] + *p;   // alpha = -1, beta = 1: the row-block GEMM's epilogue
+          }
+        }
+    // every Y store complete at L2 before any wave reads the tile back
+    __builtin_amdgcn_s_waitcnt(0);
+    __syncthreads();
+  }
+  mma128_tile<true, true>(C, lda, Linv, BT, M, BT, r0, 0, 0, BT, sA, sB, acc, -1, false, true);
+#pragma unroll
+  for (int x = 0; x < 4; ++x)
+#pragma unroll
+    for (int y = 0; y < 4; ++y)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = r0 + mma128_row(wave, x, true) + mf_row(lane, r);
+        const int col = qj + y * 16 + mf_col(lane);
+        if (row < M) C[(int64_t)row * lda + col] = acc[x][y][r];
+      }
+}
+
+hipError_t launch_gemm_updsolve(hipStream_t s, int M, int K, const double *A, int64_t lda, const double *B,
+                                double *C, const double *Linv, int batch, int64_t sA, int64_t sC, int64_t sL) {
+  if (M <= 0) return hipSuccess;
+  if (batch % 8) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_gemm128_updsolve, dim3(1, (M + BT - 1) / BT, batch), dim3(256), 0, s, M, K, A, lda, B, C,
+                     Linv, sA, sC, sL);
+  return hipGetLastError();
+}
+
 // Posterior pass with K* generated in the operand load (no K* in HBM):
 //   part[t][j] = sum over the W rows of row tile t of ((W K*^T)_ij)^2,
 //   meanT = alpha^T K*^T   (rows msum.. of A = [W; alpha^T])
@@ -818,6 +886,17 @@ hipError_t launch_gemm_nn(hipStream_t s, int M, int N, int K, const double *A, i
   hipLaunchKernelGGL((k_gemm_nt<EPI_STORE, 1, 0>), g, dim3(256), 0, s, M, N, K, A, lda, B, ldb, C,
                      ldc, alpha, beta, 0, 0, (int64_t)0, (int64_t)0, (int64_t)0, M, nullptr,
                      (int64_t)0, 0, 0);
+  return hipGetLastError();
+}
+
+// the same for batch products sA / sB / sC elements apart
+hipError_t launch_gemm_nn_batched(hipStream_t s, int M, int N, int K, const double *A, int64_t lda, int64_t sA,
+                                  const double *B, int64_t ldb, int64_t sB, double *C, int64_t ldc, int64_t sC,
+                                  double alpha, double beta, int batch) {
+  if (M <= 0 || N <= 0 || batch <= 0) return hipSuccess;
+  dim3 g((N + GT - 1) / GT, (M + GT - 1) / GT, batch);
+  hipLaunchKernelGGL((k_gemm_nt<EPI_STORE, 1, 0>), g, dim3(256), 0, s, M, N, K, A, lda, B, ldb, C,
+                     ldc, alpha, beta, 0, 0, sA, sB, sC, M, nullptr, (int64_t)0, 0, 0);
   return hipGetLastError();
 }
 

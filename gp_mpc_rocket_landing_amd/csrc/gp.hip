@@ -201,9 +201,9 @@ static int core_setup(gpmpc_ctx *ctx, GpCore &g, int kind, const double *X, int 
   g.iso_scale = iso ? 1.0 / (2.0 * ls[0] * ls[0]) : 0.0;
   DevBuf dX;
   GPMPC_HIP(dX.alloc(s, sizeof(double) * n * d));
-  GPMPC_HIP(g.ls.alloc(sizeof(double) * d));
-  GPMPC_HIP(g.Xs.alloc(sizeof(double) * n * d));
-  GPMPC_HIP(g.Xn.alloc(sizeof(double) * n));
+  GPMPC_HIP(g.ls.alloc(s, sizeof(double) * d));
+  GPMPC_HIP(g.Xs.alloc(s, sizeof(double) * n * d));
+  GPMPC_HIP(g.Xn.alloc(s, sizeof(double) * n));
   GPMPC_HIP(hipMemcpyAsync(dX.p, X, sizeof(double) * n * d, hipMemcpyHostToDevice, s));
   // SE_ISO reads one lengthscale (ls[0]); the host array may hold just that one
   GPMPC_HIP(hipMemcpyAsync(g.ls.p, ls, sizeof(double) * (iso ? 1 : d), hipMemcpyHostToDevice, s));
@@ -466,7 +466,7 @@ extern "C" int gpmpc_gp_fit_exact(gpmpc_ctx *ctx, int kind, const double *X, int
   DevBuf Kn, dinfo;
   auto fail = [&](int code) { delete gp; return code; };
   if (Kn.alloc(s, sizeof(double) * (size_t)n * n) != hipSuccess ||
-      gp->L.alloc(sizeof(double) * (size_t)n * n) != hipSuccess ||
+      gp->L.alloc(s, sizeof(double) * (size_t)n * n) != hipSuccess ||
       dinfo.alloc(s, sizeof(int)) != hipSuccess) {
     gpmpc_set_error("gp_fit_exact: out of device memory");
     return fail(-1);
@@ -510,9 +510,9 @@ extern "C" int gpmpc_gp_fit_exact(gpmpc_ctx *ctx, int kind, const double *X, int
   DevBuf dYraw, dY, dyn, dlml;
   if (dYraw.alloc(s, sizeof(double) * n * n_out) || dY.alloc(s, sizeof(double) * n * n_out) ||
       dyn.alloc(s, sizeof(double) * n * n_out) || dlml.alloc(s, sizeof(double) * n_out) ||
-      g.ymean.alloc(sizeof(double) * n_out) || g.ystd.alloc(sizeof(double) * n_out) ||
-      g.alphaT.alloc(sizeof(double) * n_out * n) ||
-      g.W.alloc(sizeof(double) * (size_t)(n + n_out) * n))  // [W; alpha^T]
+      g.ymean.alloc(s, sizeof(double) * n_out) || g.ystd.alloc(s, sizeof(double) * n_out) ||
+      g.alphaT.alloc(s, sizeof(double) * n_out * n) ||
+      g.W.alloc(s, sizeof(double) * (size_t)(n + n_out) * n))  // [W; alpha^T]
     return fail(-1);
   g.n_out = n_out;
   hipMemcpyAsync(dYraw.p, Y, sizeof(double) * n * n_out, hipMemcpyHostToDevice, s);
@@ -785,8 +785,8 @@ static int vfe_tail(gpmpc_ctx *ctx, gpmpc_fitc *gp, DevBuf &Luu, DevBuf &Kuf, De
       dYraw.alloc(s, sizeof(double) * n * n_out) || dyn.alloc(s, sizeof(double) * n * n_out) ||
       yl.alloc(s, sizeof(double) * n * n_out) || sig.alloc(s, sizeof(double) * n) ||
       cvec.alloc(s, sizeof(double) * m * n_out) || alpha.alloc(s, sizeof(double) * m * n_out) ||
-      dlml.alloc(s, sizeof(double) * n_out) || g.ymean.alloc(sizeof(double) * n_out) ||
-      g.ystd.alloc(sizeof(double) * n_out) || g.alphaT.alloc(sizeof(double) * n_out * m)) {
+      dlml.alloc(s, sizeof(double) * n_out) || g.ymean.alloc(s, sizeof(double) * n_out) ||
+      g.ystd.alloc(s, sizeof(double) * n_out) || g.alphaT.alloc(s, sizeof(double) * n_out * m)) {
     gpmpc_set_error("vfe_fit: out of device memory");
     return fail(-1);
   }
@@ -877,8 +877,8 @@ static int sparse_fit(gpmpc_ctx *ctx, const double *Z, int m, const double *X, i
       Luu.alloc(s, sizeof(double) * (size_t)m * m) || B.alloc(s, sizeof(double) * (size_t)m * m) ||
       dinfo.alloc(s, sizeof(int)) || lam.alloc(s, sizeof(double) * n) ||
       Xs.alloc(s, sizeof(double) * n * d) || Xn.alloc(s, sizeof(double) * n) ||
-      g.W.alloc(sizeof(double) * (size_t)(m + n_out) * m) ||  // [L_uu^-1; alpha^T]
-      gp->W2.alloc(sizeof(double) * (size_t)m * m)) {
+      g.W.alloc(s, sizeof(double) * (size_t)(m + n_out) * m) ||  // [L_uu^-1; alpha^T]
+      gp->W2.alloc(s, sizeof(double) * (size_t)m * m)) {
     gpmpc_set_error("fitc_fit: out of device memory");
     return fail(-1);
   }
@@ -918,8 +918,8 @@ static int sparse_fit(gpmpc_ctx *ctx, const double *Z, int m, const double *X, i
   if (isq.alloc(s, sizeof(double) * n) || dYraw.alloc(s, sizeof(double) * n * n_out) ||
       dyn.alloc(s, sizeof(double) * n * n_out) || yl.alloc(s, sizeof(double) * n * n_out) ||
       cvec.alloc(s, sizeof(double) * m * n_out) || alpha.alloc(s, sizeof(double) * m * n_out) ||
-      dlml.alloc(s, sizeof(double) * n_out) || g.ymean.alloc(sizeof(double) * n_out) ||
-      g.ystd.alloc(sizeof(double) * n_out) || g.alphaT.alloc(sizeof(double) * n_out * m))
+      dlml.alloc(s, sizeof(double) * n_out) || g.ymean.alloc(s, sizeof(double) * n_out) ||
+      g.ystd.alloc(s, sizeof(double) * n_out) || g.alphaT.alloc(s, sizeof(double) * n_out * m))
     return fail(-1);
   g.n_out = n_out;
   // Lambda = max(sigma2 - colsum(A^2) + noise, 1e-10)   (sparse_gp.py:193-199)
@@ -1275,11 +1275,11 @@ extern "C" int gpmpc_gp_append(gpmpc_ctx *ctx, gpmpc_gp *gp, const double *Xnew,
   DevBuf L2, W2, Xs2, Xn2, alphaT;  // kept by the handle
   ScratchPtr yraw{cv.take((size_t)m * no)}, yn{cv.take((size_t)m * no)}, t{cv.take((size_t)m * no)},
       alpha{cv.take((size_t)m * no)}, dlml{cv.take(no)}, ym{cv.take(no)}, ys{cv.take(no)};
-  GPMPC_HIP(L2.alloc(sizeof(double) * (size_t)m * m));
-  GPMPC_HIP(W2.alloc(sizeof(double) * (size_t)(m + no) * m));
-  GPMPC_HIP(Xs2.alloc(sizeof(double) * (size_t)m * d));
-  GPMPC_HIP(Xn2.alloc(sizeof(double) * m));
-  GPMPC_HIP(alphaT.alloc(sizeof(double) * (size_t)no * m));
+  GPMPC_HIP(L2.alloc(s, sizeof(double) * (size_t)m * m));
+  GPMPC_HIP(W2.alloc(s, sizeof(double) * (size_t)(m + no) * m));
+  GPMPC_HIP(Xs2.alloc(s, sizeof(double) * (size_t)m * d));
+  GPMPC_HIP(Xn2.alloc(s, sizeof(double) * m));
+  GPMPC_HIP(alphaT.alloc(s, sizeof(double) * (size_t)no * m));
   GPMPC_HIP(hipMemsetAsync(L2.p, 0, sizeof(double) * (size_t)m * m, s));
   GPMPC_HIP(hipMemsetAsync(W2.p, 0, sizeof(double) * (size_t)(m + no) * m, s));
   const size_t rowb = sizeof(double) * n;
@@ -1326,11 +1326,11 @@ extern "C" int gpmpc_gp_append(gpmpc_ctx *ctx, gpmpc_gp *gp, const double *Xnew,
   GPMPC_HIP(hipStreamSynchronize(s));
   g.h_ymean = hm;
   g.h_ystd = hs;
-  std::swap(gp->L.p, L2.p); std::swap(gp->L.bytes, L2.bytes);
-  std::swap(g.W.p, W2.p); std::swap(g.W.bytes, W2.bytes);
-  std::swap(g.alphaT.p, alphaT.p); std::swap(g.alphaT.bytes, alphaT.bytes);
-  std::swap(g.Xs.p, Xs2.p); std::swap(g.Xs.bytes, Xs2.bytes);
-  std::swap(g.Xn.p, Xn2.p); std::swap(g.Xn.bytes, Xn2.bytes);
+  gp->L.swap(L2);
+  g.W.swap(W2);
+  g.alphaT.swap(alphaT);
+  g.Xs.swap(Xs2);
+  g.Xn.swap(Xn2);
   g.n = m;
   for (int c = 0; c < no; ++c) {
     if (lml) lml[c] = hl[c];

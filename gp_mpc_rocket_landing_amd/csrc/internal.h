@@ -4,6 +4,7 @@
 #include <cstdint>
 #include <cstdio>
 #include <string>
+#include <utility>
 #include "../../include/gpmpc.h"
 
 struct gpmpc_ctx {
@@ -79,6 +80,9 @@ struct DevBuf {
     if (!p) return hipErrorOutOfMemory;
     pool = s;
     return hipSuccess;
+  }
+  void swap(DevBuf &o) {
+    std::swap(p, o.p); std::swap(bytes, o.bytes); std::swap(pool, o.pool); std::swap(cls, o.cls);
   }
   template <class T> T *as() const { return static_cast<T *>(p); }
 };

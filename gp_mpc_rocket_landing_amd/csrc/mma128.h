@@ -28,12 +28,17 @@ __device__ __forceinline__ int mma128_row(int wave, int x, bool il) {
   return il ? 16 * ((wave >> 1) + 2 * x) : (wave >> 1) * 64 + 16 * x;
 }
 
-template <bool IL = false>
+// L2A: the A operand is read with agent-scope loads (global_load sc1: round the vector L1),
+// for an A this workgroup has just written (the fused potrf update + panel solve).
+// tri_b: B is lower triangular over the tile's columns (B[c0 + j][k] = 0 for k > c0 + j,
+// the potrf's L_cc^-1), so a wave's 16-column MFMA block y dies once k is past its last row.
+template <bool IL = false, bool L2A = false>
 __device__ __forceinline__ void mma128_tile(const double *__restrict__ A, int64_t lda,
                                             const double *__restrict__ B, int64_t ldb, int M, int N,
                                             int r0, int c0, int k_lo, int k_hi,
                                             double (*sA)[BT][GP], double (*sB)[BT][GP],
-                                            d4_t (&acc)[4][4], int tri_rows = -1, bool lower_out = false) {
+                                            d4_t (&acc)[4][4], int tri_rows = -1, bool lower_out = false,
+                                            bool tri_b = false) {
   // the wave index through readfirstlane: the compiler then knows every per-wave
   // quantity (and the triangular skips below) is uniform
   const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
@@ -50,7 +55,14 @@ __device__ __forceinline__ void mma128_tile(const double *__restrict__ A, int64_
   double va[8], vb[8];
   auto gload = [&](int k0) {
     const int k = k0 + lk;
-    if (vec && k + 7 < k_hi) {
+    if (L2A) {
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        va[q] = (ra && k + q < k_hi) ? __hip_atomic_load(pa + k + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                     : 0.0;
+        vb[q] = (rb && k + q < k_hi) ? pb[k + q] : 0.0;
+      }
+    } else if (vec && k + 7 < k_hi) {
 #pragma unroll
       for (int q = 0; q < 8; q += 2) {
         const double2 av = ra ? *(const double2 *)(pa + k + q) : make_double2(0.0, 0.0);
@@ -108,7 +120,15 @@ __device__ __forceinline__ void mma128_tile(const double *__restrict__ A, int64_
     cur ^= 1;                                                                            \
   }
 #define MMA_PHASE(XF, XL, KEND) MMA_PHASE_M(((0xFFFF << (4 * (XF))) & (0xFFFF >> (4 * (4 - (XL))))), KEND)
-  if (lower_out && r0 == c0) {
+  if (tri_b) {
+    // column blocks y of this wave (B rows C_y = c0 + qj + 16 y) die one by one: live
+    // blocks of a step are y >= YF (mask bits 4 x + y)
+    const int C0 = c0 + qj;
+    MMA_PHASE_M(0xFFFF, min(k_hi, C0 + 16))
+    MMA_PHASE_M(0xEEEE, min(k_hi, C0 + 32))
+    MMA_PHASE_M(0xCCCC, min(k_hi, C0 + 48))
+    MMA_PHASE_M(0x8888, min(k_hi, C0 + 64))
+  } else if (lower_out && r0 == c0) {
     // a diagonal tile of a lower-triangular output: the blocks wholly above the
     // diagonal are never stored, so they are not computed (the live pattern of
     // wave (w/2, w%2) for its row mapping; one wave of the contiguous mapping has none)
