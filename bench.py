@@ -57,9 +57,11 @@ def pmc_traffic(kernel):
     import glob
     for path in sorted(glob.glob(os.path.join(REPO, "profiles", "*_pmc_traffic.json")), reverse=True):
         try:
-            k = json.load(open(path))["kernels"].get(kernel)
+            ks = json.load(open(path))["kernels"]
         except Exception:  # noqa: BLE001
             continue
+        # the horizon-templated kernels carry their namespace (r6n30::k_r6_control<false>)
+        k = ks.get(kernel) or next((v for n, v in ks.items() if n.endswith("::" + kernel)), None)
         if k:
             return float(k["traffic_bytes"]), os.path.basename(path)
     return None, None
