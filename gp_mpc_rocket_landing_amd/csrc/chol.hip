@@ -1202,13 +1202,28 @@ static hipError_t launch_potrf_batched128(hipStream_t s, int n, int batch, doubl
     return v ? atoi(v) : 1;
   }();
   const bool fuse_ok = fuse_env && OBk > DB && !tblk && !lat && batch % 8 == 0;
+  // look-ahead (GPMPC_POTRF_LA=1): a fused step's first row tile also applies the next
+  // fused step's diagonal-block update (k_gemm128_updsolve<true>), so that launch goes.
+  // Off: the first row tiles become the launch's stragglers (batch 1024: 11.6 -> 15.0 ms)
+  static const int la_env = [] {
+    const char *v = getenv("GPMPC_POTRF_LA");
+    return v ? atoi(v) : 0;
+  }();
+  auto fuses = [&](int c) {
+    const int below = n - c - min(DB, n - c);
+    return fuse_ok && below > 0 && (below + DB - 1) / DB * batch >= 512;
+  };
   for (int K0 = 0; K0 < n; K0 += OBk) {
     const int pw = min(OBk, n - K0);
+    bool la_prev = false;  // this step's diagonal update was applied by the previous step
     for (int c = K0; c < K0 + pw; c += DB) {
       const int w = min(DB, n - c);
       const int below = n - c - w;
-      const bool fuse = fuse_ok && below > 0 && (below + DB - 1) / DB * batch >= 512;
-      if (c > K0 && fuse) {
+      const bool fuse = fuses(c);
+      const bool la = la_env && fuse && w == DB && c + DB < K0 + pw && fuses(c + DB);
+      if (c > K0 && fuse && la_prev) {
+        // the diagonal block's update came with the previous step's first row tile
+      } else if (c > K0 && fuse) {
         // the diagonal block's rows only (one tile per matrix), K split to fill the device
         const int K = c - K0;
         int ks = 1;
@@ -1237,11 +1252,12 @@ static hipError_t launch_potrf_batched128(hipStream_t s, int n, int batch, doubl
                            A, lda, stride, info, c + DB < n ? Linv : nullptr, sweep | (tblk ? 2 : 0));
       if (fuse) {
         e = launch_gemm_updsolve(s, below, c - K0, at(c + w, K0), lda, at(c, K0), at(c + w, c), Linv, batch,
-                                 stride, stride, (int64_t)DB * DB);
+                                 stride, stride, (int64_t)DB * DB, la ? min(DB, below) : 0);
         if (e != hipSuccess) return e;
       } else if (c + DB < n && (e = psolve(c)) != hipSuccess) {
         return e;
       }
+      la_prev = la;
     }
     const int t0 = K0 + pw;
     if (t0 < n) {

@@ -22,9 +22,11 @@ hipError_t launch_gemm_nt_rowblock(hipStream_t s, int M, int N, int K, const dou
 
 // the potrf's fused left-looking step for the rows below a diagonal block (gemm.hip):
 // C (M x 128) <- (C - A B^T) Linv^T, A (M x K) and B (128 x K) with leading dimension lda,
-// Linv (128 x 128, lower, ld 128); batch a multiple of 8
+// Linv (128 x 128, lower, ld 128); batch a multiple of 8.  wn > 0 (<= 128, <= M): also
+// D -= A[0:wn, 0:K+128] A[0:wn, 0:K+128]^T (lower) for the next diagonal block D = C + 128
 hipError_t launch_gemm_updsolve(hipStream_t s, int M, int K, const double *A, int64_t lda, const double *B,
-                                double *C, const double *Linv, int batch, int64_t sA, int64_t sC, int64_t sL);
+                                double *C, const double *Linv, int batch, int64_t sA, int64_t sC, int64_t sL,
+                                int wn = 0);
 
 // latency form for K <= 128 (see gemm.hip): mode 0 = rows in place (N <= 128,
 // C may alias A; tri_b: B lower-triangular), mode 1 = lower C += A A^T (M == N)

@@ -377,17 +377,23 @@ __global__ __launch_bounds__(256, 2) void k_gemm128(int M, int N, int K, const d
 // The potrf's left-looking block-column step for the rows below the diagonal block,
 // fused (one workgroup per 128-row tile r of matrix b, XCD-batched like the row-block GEMM):
 //   Y = C - A_r B^T              C = the tile's 128 panel columns, A_r = its rows' K = c left
-//                                columns, B = the diagonal block rows' left columns (K = c)
+//                                columns, B = the diagonal block rows' left columns (K = c);
+//                                the accumulators start from C and A is staged negated
 //   X = Y Linv^T                 Linv = L_cc^-1 (128 x 128, lower) from the diagonal kernel
 // Y goes to C in place and is read back by the second product through agent-scope loads
 // (the vector L1 is not refreshed by this workgroup's own stores); X overwrites it.  The
-// separate update launch, the panel-solve launch and one read + write of the panel
-// between them become one pass; the second product skips the upper triangle of Linv.
+// second product's column halves take interleaved 16-column blocks, so the blocks that
+// die past Linv's triangle are shared evenly by the two wave columns.
+// LA (look-ahead, tile 0 only, wn = the next block's width): tile 0's rows are the next
+// diagonal block's, and with X stored they are final over all K + 128 left columns, so the
+// same workgroup applies the next step's diagonal update D -= L L^T (lower, K + 128)
+// instead of a separate launch: the diagonal kernel of the next step reads D.
 // K = 0 (the first block column) is the plain in-place panel solve.
+template <bool LA>
 __global__ __launch_bounds__(256, 2) void k_gemm128_updsolve(int M, int K, const double *__restrict__ A,
                                                             int64_t lda, const double *__restrict__ B,
                                                             double *__restrict__ C, const double *__restrict__ Linv,
-                                                            int64_t sA_, int64_t sC_, int64_t sL_) {
+                                                            int64_t sA_, int64_t sC_, int64_t sL_, int wn) {
   const int ny = gridDim.y, L = blockIdx.y + blockIdx.z * ny;
   const int m = L >> 3;
   const int bz = (L & 7) + 8 * (m / ny), ry = m % ny;  // matrix b's row tiles on XCD b % 8
@@ -399,10 +405,10 @@ __global__ __launch_bounds__(256, 2) void k_gemm128_updsolve(int M, int K, const
   __shared__ double sA[2][BT][GP];
   __shared__ double sB[2][BT][GP];
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  const int qj = (wave & 1) * 64;
   d4_t acc[4][4];
   if (K > 0) {
-    mma128_tile<true>(A, lda, B, lda, M, BT, r0, 0, 0, K, sA, sB, acc, -1, false);
+    mma128_tile<true, false, false, false, true>(A, lda, B, lda, M, BT, r0, 0, 0, K, sA, sB, acc, -1, false,
+                                                 false, C, lda);
 #pragma unroll
     for (int x = 0; x < 4; ++x)
 #pragma unroll
@@ -410,17 +416,14 @@ __global__ __launch_bounds__(256, 2) void k_gemm128_updsolve(int M, int K, const
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int row = r0 + mma128_row(wave, x, true) + mf_row(lane, r);
-          const int col = qj + y * 16 + mf_col(lane);
-          if (row < M) {
-            double *p = C + (int64_t)row * lda + col;
-            *p = -acc[x][y][r] + *p;   // alpha = -1, beta = 1: the row-block GEMM's epilogue
-          }
+          const int col = mma128_col(wave, y, false) + mf_col(lane);
+          if (row < M) C[(int64_t)row * lda + col] = acc[x][y][r];
         }
     // every Y store complete at L2 before any wave reads the tile back
     __builtin_amdgcn_s_waitcnt(0);
     __syncthreads();
   }
-  mma128_tile<true, true>(C, lda, Linv, BT, M, BT, r0, 0, 0, BT, sA, sB, acc, -1, false, true);
+  mma128_tile<true, true, false, true>(C, lda, Linv, BT, M, BT, r0, 0, 0, BT, sA, sB, acc, -1, false, true);
 #pragma unroll
   for (int x = 0; x < 4; ++x)
 #pragma unroll
@@ -428,17 +431,41 @@ __global__ __launch_bounds__(256, 2) void k_gemm128_updsolve(int M, int K, const
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int row = r0 + mma128_row(wave, x, true) + mf_row(lane, r);
-        const int col = qj + y * 16 + mf_col(lane);
+        const int col = mma128_col(wave, y, true) + mf_col(lane);
         if (row < M) C[(int64_t)row * lda + col] = acc[x][y][r];
       }
+  if (LA && ry == 0) {
+    __builtin_amdgcn_s_waitcnt(0);
+    __syncthreads();
+    // D = C + 128 columns: rows / columns 0 .. wn-1 of the next diagonal block
+    mma128_tile<true, true, true>(A, lda, A, lda, wn, wn, 0, 0, 0, K + BT, sA, sB, acc, -1, true);
+    double *D = C + BT;
+#pragma unroll
+    for (int x = 0; x < 4; ++x)
+#pragma unroll
+      for (int y = 0; y < 4; ++y)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = mma128_row(wave, x, true) + mf_row(lane, r);
+          const int col = mma128_col(wave, y, false) + mf_col(lane);
+          if (row < wn && col <= row) {
+            double *p = D + (int64_t)row * lda + col;
+            *p = -acc[x][y][r] + *p;
+          }
+        }
+  }
 }
 
 hipError_t launch_gemm_updsolve(hipStream_t s, int M, int K, const double *A, int64_t lda, const double *B,
-                                double *C, const double *Linv, int batch, int64_t sA, int64_t sC, int64_t sL) {
+                                double *C, const double *Linv, int batch, int64_t sA, int64_t sC, int64_t sL,
+                                int wn) {
   if (M <= 0) return hipSuccess;
-  if (batch % 8) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(k_gemm128_updsolve, dim3(1, (M + BT - 1) / BT, batch), dim3(256), 0, s, M, K, A, lda, B, C,
-                     Linv, sA, sC, sL);
+  if (batch % 8 || wn > BT || wn > M) return hipErrorInvalidValue;
+  const dim3 g(1, (M + BT - 1) / BT, batch);
+  if (wn > 0)
+    hipLaunchKernelGGL(k_gemm128_updsolve<true>, g, dim3(256), 0, s, M, K, A, lda, B, C, Linv, sA, sC, sL, wn);
+  else
+    hipLaunchKernelGGL(k_gemm128_updsolve<false>, g, dim3(256), 0, s, M, K, A, lda, B, C, Linv, sA, sC, sL, 0);
   return hipGetLastError();
 }
 

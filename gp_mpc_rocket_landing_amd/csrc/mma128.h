@@ -28,25 +28,45 @@ __device__ __forceinline__ int mma128_row(int wave, int x, bool il) {
   return il ? 16 * ((wave >> 1) + 2 * x) : (wave >> 1) * 64 + 16 * x;
 }
 
-// L2A: the A operand is read with agent-scope loads (global_load sc1: round the vector L1),
-// for an A this workgroup has just written (the fused potrf update + panel solve).
+// ILC: the same interleave for the two column halves (columns 16 (w%2 + 2y),
+// mma128_col), so a triangular B's dying column blocks are shared evenly (tri_b only)
+__device__ __forceinline__ int mma128_col(int wave, int y, bool ilc) {
+  return ilc ? 16 * ((wave & 1) + 2 * y) : (wave & 1) * 64 + 16 * y;
+}
+
+// L2A / L2B: the A / B operand is read with agent-scope loads (global_load sc1: round the
+// vector L1), for an operand this workgroup has just written (the fused potrf steps).
 // tri_b: B is lower triangular over the tile's columns (B[c0 + j][k] = 0 for k > c0 + j,
 // the potrf's L_cc^-1), so a wave's 16-column MFMA block y dies once k is past its last row.
-template <bool IL = false, bool L2A = false>
+// Ci: the accumulators start from the tile of Ci (rows r0.., columns c0.., ldci) instead of
+// zero; with NEGA (A staged negated) the tile computes Ci - A B^T.
+template <bool IL = false, bool L2A = false, bool L2B = false, bool ILC = false, bool NEGA = false>
 __device__ __forceinline__ void mma128_tile(const double *__restrict__ A, int64_t lda,
                                             const double *__restrict__ B, int64_t ldb, int M, int N,
                                             int r0, int c0, int k_lo, int k_hi,
                                             double (*sA)[BT][GP], double (*sB)[BT][GP],
                                             d4_t (&acc)[4][4], int tri_rows = -1, bool lower_out = false,
-                                            bool tri_b = false) {
+                                            bool tri_b = false, const double *Ci = nullptr, int64_t ldci = 0) {
   // the wave index through readfirstlane: the compiler then knows every per-wave
   // quantity (and the triangular skips below) is uniform
   const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
-  const int qi = (wave >> 1) * 64, qj = (wave & 1) * 64;
+  if (Ci) {
 #pragma unroll
-  for (int x = 0; x < 4; ++x)
+    for (int x = 0; x < 4; ++x)
 #pragma unroll
-    for (int y = 0; y < 4; ++y) acc[x][y] = (d4_t){0.0, 0.0, 0.0, 0.0};
+      for (int y = 0; y < 4; ++y)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = r0 + mma128_row(wave, x, IL) + mf_row(lane, r);
+          const int col = c0 + mma128_col(wave, y, ILC) + mf_col(lane);
+          acc[x][y][r] = (row < M && col < N) ? Ci[(int64_t)row * ldci + col] : 0.0;
+        }
+  } else {
+#pragma unroll
+    for (int x = 0; x < 4; ++x)
+#pragma unroll
+      for (int y = 0; y < 4; ++y) acc[x][y] = (d4_t){0.0, 0.0, 0.0, 0.0};
+  }
   const int lr = tid >> 1, lk = (tid & 1) * 8;
   const bool ra = r0 + lr < M, rb = c0 + lr < N;
   const double *pa = A + (int64_t)(ra ? r0 + lr : 0) * lda;
@@ -55,12 +75,12 @@ __device__ __forceinline__ void mma128_tile(const double *__restrict__ A, int64_
   double va[8], vb[8];
   auto gload = [&](int k0) {
     const int k = k0 + lk;
-    if (L2A) {
+    if (L2A || L2B) {
 #pragma unroll
       for (int q = 0; q < 8; ++q) {
-        va[q] = (ra && k + q < k_hi) ? __hip_atomic_load(pa + k + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                                     : 0.0;
-        vb[q] = (rb && k + q < k_hi) ? pb[k + q] : 0.0;
+        const bool ka = ra && k + q < k_hi, kb = rb && k + q < k_hi;
+        va[q] = !ka ? 0.0 : L2A ? __hip_atomic_load(pa + k + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : pa[k + q];
+        vb[q] = !kb ? 0.0 : L2B ? __hip_atomic_load(pb + k + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : pb[k + q];
       }
     } else if (vec && k + 7 < k_hi) {
 #pragma unroll
@@ -81,7 +101,7 @@ __device__ __forceinline__ void mma128_tile(const double *__restrict__ A, int64_
   auto lstore = [&](int buf) {
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
-      sA[buf][lr][lk + q] = va[q];
+      sA[buf][lr][lk + q] = NEGA ? -va[q] : va[q];
       sB[buf][lr][lk + q] = vb[q];
     }
   };
@@ -110,7 +130,7 @@ __device__ __forceinline__ void mma128_tile(const double *__restrict__ A, int64_
       double a[4], b[4];                                                                 \
       _Pragma("unroll") for (int x = 0; x < 4; ++x)                                      \
         if (((MASK) >> (4 * x)) & 15) a[x] = sA[cur][mma128_row(wave, x, IL) + (lane & 15)][kc]; \
-      _Pragma("unroll") for (int y = 0; y < 4; ++y) b[y] = sB[cur][qj + 16 * y + (lane & 15)][kc];   \
+      _Pragma("unroll") for (int y = 0; y < 4; ++y) b[y] = sB[cur][mma128_col(wave, y, ILC) + (lane & 15)][kc]; \
       _Pragma("unroll") for (int x = 0; x < 4; ++x)                                      \
         _Pragma("unroll") for (int y = 0; y < 4; ++y)                                    \
           if (((MASK) >> (4 * x + y)) & 1) acc[x][y] = mfma_f64(a[x], b[y], acc[x][y]);  \
@@ -121,13 +141,12 @@ __device__ __forceinline__ void mma128_tile(const double *__restrict__ A, int64_
   }
 #define MMA_PHASE(XF, XL, KEND) MMA_PHASE_M(((0xFFFF << (4 * (XF))) & (0xFFFF >> (4 * (4 - (XL))))), KEND)
   if (tri_b) {
-    // column blocks y of this wave (B rows C_y = c0 + qj + 16 y) die one by one: live
+    // column blocks y of this wave (B rows c0 + mma128_col(y)) die one by one: live
     // blocks of a step are y >= YF (mask bits 4 x + y)
-    const int C0 = c0 + qj;
-    MMA_PHASE_M(0xFFFF, min(k_hi, C0 + 16))
-    MMA_PHASE_M(0xEEEE, min(k_hi, C0 + 32))
-    MMA_PHASE_M(0xCCCC, min(k_hi, C0 + 48))
-    MMA_PHASE_M(0x8888, min(k_hi, C0 + 64))
+    MMA_PHASE_M(0xFFFF, min(k_hi, c0 + mma128_col(wave, 0, ILC) + 16))
+    MMA_PHASE_M(0xEEEE, min(k_hi, c0 + mma128_col(wave, 1, ILC) + 16))
+    MMA_PHASE_M(0xCCCC, min(k_hi, c0 + mma128_col(wave, 2, ILC) + 16))
+    MMA_PHASE_M(0x8888, min(k_hi, c0 + mma128_col(wave, 3, ILC) + 16))
   } else if (lower_out && r0 == c0) {
     // a diagonal tile of a lower-triangular output: the blocks wholly above the
     // diagonal are never stored, so they are not computed (the live pattern of

@@ -12,3 +12,6 @@ for la in 1 0; do
     > gpurun_out/probe7/potrf_la$la.log 2>&1
 done
 cat gpurun_out/probe7/potrf_la*.log
+timeout -k 10 120 python3 -u scripts/gemm_loop_probe.py > gpurun_out/probe7/gemm_loop.log 2>&1
+bash scripts/pmc_mfma.sh gemmloop python3 scripts/gemm_loop_probe.py > /dev/null 2>&1
+cat gpurun_out/probe7/gemm_loop.log; head -4 gpurun_out/pmc_mfma_gemmloop/summary.txt
