@@ -1209,6 +1209,12 @@ static hipError_t launch_potrf_batched128(hipStream_t s, int n, int batch, doubl
     const char *v = getenv("GPMPC_POTRF_LA");
     return v ? atoi(v) : 0;
   }();
+  // the diagonal block's update by the balanced lower-triangle kernel (k_syrk128_diag,
+  // 9 MFMA blocks per wave) instead of the 128-tile kernel's quadrants (GPMPC_SYRK_DIAG=0)
+  static const int syrk_diag_env = [] {
+    const char *v = getenv("GPMPC_SYRK_DIAG");
+    return v ? atoi(v) : 1;
+  }();
   auto fuses = [&](int c) {
     const int below = n - c - min(DB, n - c);
     return fuse_ok && below > 0 && (below + DB - 1) / DB * batch >= 512;
@@ -1229,8 +1235,9 @@ static hipError_t launch_potrf_batched128(hipStream_t s, int n, int batch, doubl
         int ks = 1;
         if (ksplit_env != 1)
           while (ks < K / DB && batch * ks < 512) ++ks;
-        e = launch_gemm_nt_rowblock(s, w, w, K, at(c, K0), lda, at(c, K0), lda, at(c, c), lda, -1.0, 1.0, batch,
-                                    stride, stride, stride, 1, ks);
+        e = syrk_diag_env ? launch_syrk128_diag(s, w, K, at(c, K0), lda, at(c, c), batch, stride, ks)
+                          : launch_gemm_nt_rowblock(s, w, w, K, at(c, K0), lda, at(c, K0), lda, at(c, c), lda, -1.0,
+                                                    1.0, batch, stride, stride, stride, 1, ks);
         if (e != hipSuccess) return e;
       } else if (c > K0) {
         // the block column's update by all earlier columns of the outer panel; K split
@@ -1240,8 +1247,11 @@ static hipError_t launch_potrf_batched128(hipStream_t s, int n, int batch, doubl
         int ks = 1;
         if (ksplit_env != 1)
           while (ks < K / DB && tiles * ks < 512) ++ks;
-        e = launch_gemm_nt_rowblock(s, n - c, w, K, at(c, K0), lda, at(c, K0), lda, at(c, c), lda,
-                                    -1.0, 1.0, batch, stride, stride, stride, 1, ks);
+        // the last block column of a left-looking panel has no rows below: its diagonal block alone
+        e = (syrk_diag_env && OBk > DB && n - c == w)
+                ? launch_syrk128_diag(s, w, K, at(c, K0), lda, at(c, c), batch, stride, ks)
+                : launch_gemm_nt_rowblock(s, n - c, w, K, at(c, K0), lda, at(c, K0), lda, at(c, c), lda,
+                                          -1.0, 1.0, batch, stride, stride, stride, 1, ks);
         if (e != hipSuccess) return e;
       }
       if (st)

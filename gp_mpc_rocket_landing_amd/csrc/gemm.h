@@ -20,6 +20,11 @@ hipError_t launch_gemm_nt_rowblock(hipStream_t s, int M, int N, int K, const dou
                                    int64_t ldc, double alpha, double beta, int batch, int64_t sA,
                                    int64_t sB, int64_t sC, int lower_c = 0, int ksplit = 1);
 
+// the potrf's diagonal-block update C -= A A^T (lower w x w, w <= 128; A: the block's rows'
+// K left columns, ld lda; C ld lda; batch matrices stride apart; K split in ks, atomics)
+hipError_t launch_syrk128_diag(hipStream_t s, int w, int K, const double *A, int64_t lda, double *C, int batch,
+                               int64_t stride, int ks);
+
 // the potrf's fused left-looking step for the rows below a diagonal block (gemm.hip):
 // C (M x 128) <- (C - A B^T) Linv^T, A (M x K) and B (128 x K) with leading dimension lda,
 // Linv (128 x 128, lower, ld 128); batch a multiple of 8.  wn > 0 (<= 128, <= M): also

@@ -374,6 +374,112 @@ __global__ __launch_bounds__(256, 2) void k_gemm128(int M, int N, int K, const d
 }
 
 
+// The potrf's diagonal-block update C -= A A^T (C the w x w lower diagonal block, A its rows'
+// K left columns; one workgroup per matrix and K split).  Of the 8 x 8 16-wide MFMA blocks
+// of a 128 x 128 lower triangle 36 are live; the 128-tile kernel's quadrant waves own 12,
+// 14, 4 and 6 of them, so every K step waits for the 14.  Here wave w owns column blocks w
+// and 7 - w down to the last row block: 9 blocks each (8 - w + w + 1), fed by the A
+// fragments of row blocks w..7 and B = A's fragments of the two column blocks.  A and B
+// are the same rows, so one LDS tile is staged.  ks > 1: split s covers K range
+// [s kc, (s + 1) kc) and adds its partial product with fp64 atomics.
+template <int W>
+__device__ __forceinline__ void syrk_diag_wave(const double *__restrict__ A, int64_t lda, int w, int k_lo,
+                                               int k_hi, double (*sA)[BT][GP], double *__restrict__ C,
+                                               int64_t ldc, bool atomic) {
+  constexpr int C1 = W, C2 = 7 - W, N1 = 8 - C1, N2 = 8 - C2;  // column blocks and their live rows
+  const int tid = threadIdx.x, lane = tid & 63;
+  d4_t a1[N1], a2[N2];
+#pragma unroll
+  for (int i = 0; i < N1; ++i) a1[i] = (d4_t){0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+  for (int i = 0; i < N2; ++i) a2[i] = (d4_t){0.0, 0.0, 0.0, 0.0};
+  const int lr = tid >> 1, lk = (tid & 1) * 8;
+  const bool ra = lr < w;
+  const double *pa = A + (int64_t)(ra ? lr : 0) * lda;
+  const bool vec = (lda & 1) == 0 && (((uintptr_t)A) & 15) == 0;
+  double va[8];
+  auto gload = [&](int k0) {
+    const int k = k0 + lk;
+    if (vec && k + 7 < k_hi) {
+#pragma unroll
+      for (int q = 0; q < 8; q += 2) {
+        const double2 v = ra ? *(const double2 *)(pa + k + q) : make_double2(0.0, 0.0);
+        va[q] = v.x; va[q + 1] = v.y;
+      }
+    } else {
+#pragma unroll
+      for (int q = 0; q < 8; ++q) va[q] = (ra && k + q < k_hi) ? pa[k + q] : 0.0;
+    }
+  };
+  auto lstore = [&](int buf) {
+#pragma unroll
+    for (int q = 0; q < 8; ++q) sA[buf][lr][lk + q] = va[q];
+  };
+  gload(k_lo);
+  lstore(0);
+  __syncthreads();
+  int cur = 0;
+  for (int k0 = k_lo; k0 < k_hi; k0 += GK) {
+    const bool more = k0 + GK < k_hi;
+    if (more) gload(k0 + GK);
+#pragma unroll
+    for (int kk = 0; kk < GK; kk += 4) {
+      const int kc = kk + (lane >> 4);
+      double fa[8];
+#pragma unroll
+      for (int r = C1; r < 8; ++r) fa[r] = sA[cur][16 * r + (lane & 15)][kc];
+      const double b1 = fa[C1], b2 = fa[C2];  // B = A: the column blocks' own fragments
+#pragma unroll
+      for (int r = C1; r < 8; ++r) a1[r - C1] = mfma_f64(fa[r], b1, a1[r - C1]);
+#pragma unroll
+      for (int r = C2; r < 8; ++r) a2[r - C2] = mfma_f64(fa[r], b2, a2[r - C2]);
+    }
+    if (more) lstore(cur ^ 1);
+    __syncthreads();
+    cur ^= 1;
+  }
+  auto store = [&](const d4_t &acc, int rb, int cb) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int row = 16 * rb + mf_row(lane, i), col = 16 * cb + mf_col(lane);
+      if (row < w && col <= row) {
+        double *p = C + (int64_t)row * ldc + col;
+        if (atomic) atomicAdd(p, -acc[i]);
+        else *p = -acc[i] + *p;
+      }
+    }
+  };
+#pragma unroll
+  for (int r = C1; r < 8; ++r) store(a1[r - C1], r, C1);
+#pragma unroll
+  for (int r = C2; r < 8; ++r) store(a2[r - C2], r, C2);
+}
+
+__global__ __launch_bounds__(256, 2) void k_syrk128_diag(int w, int K, const double *__restrict__ A, int64_t lda,
+                                                        double *__restrict__ C, int64_t stride, int ks) {
+  const int b = blockIdx.x / ks, sp = blockIdx.x % ks;
+  const int kc = ((K + ks - 1) / ks + GK - 1) / GK * GK, k_lo = sp * kc, k_hi = min(K, k_lo + kc);
+  if (k_lo >= k_hi) return;
+  __shared__ double sA[2][BT][GP];
+  A += b * stride;
+  C += b * stride;
+  switch (__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)) {
+    case 0: syrk_diag_wave<0>(A, lda, w, k_lo, k_hi, sA, C, lda, ks > 1); break;
+    case 1: syrk_diag_wave<1>(A, lda, w, k_lo, k_hi, sA, C, lda, ks > 1); break;
+    case 2: syrk_diag_wave<2>(A, lda, w, k_lo, k_hi, sA, C, lda, ks > 1); break;
+    default: syrk_diag_wave<3>(A, lda, w, k_lo, k_hi, sA, C, lda, ks > 1); break;
+  }
+}
+
+hipError_t launch_syrk128_diag(hipStream_t s, int w, int K, const double *A, int64_t lda, double *C, int batch,
+                               int64_t stride, int ks) {
+  if (w <= 0 || K <= 0 || batch <= 0) return hipSuccess;
+  if (w > BT) return hipErrorInvalidValue;
+  if (ks < 1) ks = 1;
+  hipLaunchKernelGGL(k_syrk128_diag, dim3(batch * ks), dim3(256), 0, s, w, K, A, lda, C, stride, ks);
+  return hipGetLastError();
+}
+
 // The potrf's left-looking block-column step for the rows below the diagonal block,
 // fused (one workgroup per 128-row tile r of matrix b, XCD-batched like the row-block GEMM):
 //   Y = C - A_r B^T              C = the tile's 128 panel columns, A_r = its rows' K = c left
