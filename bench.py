@@ -619,6 +619,10 @@ def rollouts6_bench(ctx, torch=None, batches=(64, 512), max_steps=300):
     # return "solved" (scripts/r6_qp_sweep.py: max_iter 50 / 100 / 200 / 400 / 1000 / 4000
     # at eps 1e-4 gave 12 / 53 / 75 / 83 / 89 / 96% solved), beside the osqp_rti setting
     out["solved_setting"] = rollouts6_timed(ctx, gv, gw, batches, max_steps, **SOLVED_QP6)
+    # the reference's FITC mean as written (K*u alpha, sparse_gp.py:280-283; DESIGN D1): the
+    # outcomes and QP statuses of the same rollouts with it, untimed
+    out["fitc_mean_as_written"] = rollouts6_qp_status(ctx, gv, gw, batches[0], max_steps=max_steps,
+                                                      fitc_mean_as_written=1)
     if len(ph):
         pm = ph.mean(axis=0)
         it_f, fac_f = r6_admm_flops()

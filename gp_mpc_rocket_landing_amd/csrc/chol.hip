@@ -1215,9 +1215,14 @@ static hipError_t launch_potrf_batched128(hipStream_t s, int n, int batch, doubl
     const char *v = getenv("GPMPC_SYRK_DIAG");
     return v ? atoi(v) : 1;
   }();
+  // a block column fuses when its rows below fill >= GPMPC_POTRF_FUSE_MIN workgroups (512)
+  static const int fuse_min = [] {
+    const char *v = getenv("GPMPC_POTRF_FUSE_MIN");
+    return v ? atoi(v) : 512;
+  }();
   auto fuses = [&](int c) {
     const int below = n - c - min(DB, n - c);
-    return fuse_ok && below > 0 && (below + DB - 1) / DB * batch >= 512;
+    return fuse_ok && below > 0 && (below + DB - 1) / DB * batch >= fuse_min;
   };
   for (int K0 = 0; K0 < n; K0 += OBk) {
     const int pw = min(OBk, n - K0);

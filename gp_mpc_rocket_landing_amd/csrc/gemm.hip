@@ -495,7 +495,7 @@ hipError_t launch_syrk128_diag(hipStream_t s, int w, int K, const double *A, int
 // same workgroup applies the next step's diagonal update D -= L L^T (lower, K + 128)
 // instead of a separate launch: the diagonal kernel of the next step reads D.
 // K = 0 (the first block column) is the plain in-place panel solve.
-template <bool LA>
+template <bool LA, bool K0 = false>
 __global__ __launch_bounds__(256, 2) void k_gemm128_updsolve(int M, int K, const double *__restrict__ A,
                                                             int64_t lda, const double *__restrict__ B,
                                                             double *__restrict__ C, const double *__restrict__ Linv,
@@ -512,7 +512,7 @@ __global__ __launch_bounds__(256, 2) void k_gemm128_updsolve(int M, int K, const
   __shared__ double sB[2][BT][GP];
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   d4_t acc[4][4];
-  if (K > 0) {
+  if (!K0 && K > 0) {
     mma128_tile<true, false, false, false, true>(A, lda, B, lda, M, BT, r0, 0, 0, K, sA, sB, acc, -1, false,
                                                  false, C, lda);
 #pragma unroll
@@ -529,7 +529,8 @@ __global__ __launch_bounds__(256, 2) void k_gemm128_updsolve(int M, int K, const
     __builtin_amdgcn_s_waitcnt(0);
     __syncthreads();
   }
-  mma128_tile<true, true, false, true>(C, lda, Linv, BT, M, BT, r0, 0, 0, BT, sA, sB, acc, -1, false, true);
+  // K0 (the first block column: no update, nothing written yet): plain 16-byte loads
+  mma128_tile<true, !K0, false, true>(C, lda, Linv, BT, M, BT, r0, 0, 0, BT, sA, sB, acc, -1, false, true);
 #pragma unroll
   for (int x = 0; x < 4; ++x)
 #pragma unroll
@@ -568,7 +569,10 @@ hipError_t launch_gemm_updsolve(hipStream_t s, int M, int K, const double *A, in
   if (M <= 0) return hipSuccess;
   if (batch % 8 || wn > BT || wn > M) return hipErrorInvalidValue;
   const dim3 g(1, (M + BT - 1) / BT, batch);
-  if (wn > 0)
+  if (K == 0 && wn == 0)
+    hipLaunchKernelGGL((k_gemm128_updsolve<false, true>), g, dim3(256), 0, s, M, K, A, lda, B, C, Linv, sA, sC, sL,
+                       0);
+  else if (wn > 0)
     hipLaunchKernelGGL(k_gemm128_updsolve<true>, g, dim3(256), 0, s, M, K, A, lda, B, C, Linv, sA, sC, sL, wn);
   else
     hipLaunchKernelGGL(k_gemm128_updsolve<false>, g, dim3(256), 0, s, M, K, A, lda, B, C, Linv, sA, sC, sL, 0);

@@ -12,6 +12,10 @@
 #define GP 18  // LDS pitch (doubles) of a 16-wide K slice
 #endif
 #define BT 128
+// MMA_PRIO: the wave's issue priority raised over each 4-k step's MFMAs (A/B builds)
+#ifndef MMA_PRIO
+#define MMA_PRIO 0
+#endif
 // acc = A[r0.., k_lo:k_hi] B[c0.., k_lo:k_hi]^T for one 128 x 128 tile (wave w
 // owns quadrant (w/2, w%2)); k_lo must be a multiple of GK.  Ends on a barrier,
 // so the LDS can be reused by the caller straight away.
@@ -73,9 +77,30 @@ __device__ __forceinline__ void mma128_tile(const double *__restrict__ A, int64_
   const double *pb = B + (int64_t)(rb ? c0 + lr : 0) * ldb;
   const bool vec = ((lda | ldb) & 1) == 0 && ((((uintptr_t)A) | ((uintptr_t)B)) & 15) == 0;
   double va[8], vb[8];
+  // agent-scope 16-byte loads: raw buffer loads with the sc1 policy bit (aux 16 on gfx950),
+  // whose completion the compiler tracks like any load; byte offsets must fit 31 bits
+  const bool buf = (L2A || L2B) && vec && (int64_t)(max(r0, c0) + BT) * max(lda, ldb) * 8 < 0x7fffffff;
+  // the operand's element (row, k) through an agent-scope 16-byte raw buffer load (sc1: aux 16
+  // on gfx950), whose completion the compiler tracks like any load's
+  auto ld_agent = [](const double *base, int64_t ld, int row, int k, double &x, double &y) {
+    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void *)base, (short)0, 0x7fffffff, 0x00020000);
+    const double2 v = __builtin_bit_cast(
+        double2, __builtin_amdgcn_raw_buffer_load_b128(r, (int)(row * ld + k) * 8, 0, 16));
+    x = v.x; y = v.y;
+  };
   auto gload = [&](int k0) {
     const int k = k0 + lk;
-    if (L2A || L2B) {
+    if ((L2A || L2B) && buf && k + 7 < k_hi) {
+#pragma unroll
+      for (int q = 0; q < 8; q += 2) {
+        if (!ra) { va[q] = 0.0; va[q + 1] = 0.0; }
+        else if (L2A) ld_agent(A, lda, r0 + lr, k + q, va[q], va[q + 1]);
+        else { const double2 v = *(const double2 *)(pa + k + q); va[q] = v.x; va[q + 1] = v.y; }
+        if (!rb) { vb[q] = 0.0; vb[q + 1] = 0.0; }
+        else if (L2B) ld_agent(B, ldb, c0 + lr, k + q, vb[q], vb[q + 1]);
+        else { const double2 v = *(const double2 *)(pb + k + q); vb[q] = v.x; vb[q + 1] = v.y; }
+      }
+    } else if (L2A || L2B) {
 #pragma unroll
       for (int q = 0; q < 8; ++q) {
         const bool ka = ra && k + q < k_hi, kb = rb && k + q < k_hi;
@@ -131,9 +156,11 @@ __device__ __forceinline__ void mma128_tile(const double *__restrict__ A, int64_
       _Pragma("unroll") for (int x = 0; x < 4; ++x)                                      \
         if (((MASK) >> (4 * x)) & 15) a[x] = sA[cur][mma128_row(wave, x, IL) + (lane & 15)][kc]; \
       _Pragma("unroll") for (int y = 0; y < 4; ++y) b[y] = sB[cur][mma128_col(wave, y, ILC) + (lane & 15)][kc]; \
+      if (MMA_PRIO) __builtin_amdgcn_s_setprio(1);                                       \
       _Pragma("unroll") for (int x = 0; x < 4; ++x)                                      \
         _Pragma("unroll") for (int y = 0; y < 4; ++y)                                    \
           if (((MASK) >> (4 * x + y)) & 1) acc[x][y] = mfma_f64(a[x], b[y], acc[x][y]);  \
+      if (MMA_PRIO) __builtin_amdgcn_s_setprio(0);                                       \
     }                                                                                    \
     if (more) lstore(cur ^ 1);                                                           \
     __syncthreads();                                                                     \

@@ -57,7 +57,11 @@ def test_blocked_trsm_paths(gpu_ctx, n, nrhs):
 @pytest.mark.parametrize("n,batch", [(100, 3), (128, 2), (129, 3), (256, 2), (300, 4), (1000, 3),
                                      (300, 20), (300, 70), (257, 260),
                                      # batches that are multiples of 8: the XCD-batched row-block grid
-                                     (300, 16), (257, 64), (300, 256)])
+                                     (300, 16), (257, 64), (300, 256),
+                                     # left-looking, fused: the solve-only first column, K > 0
+                                     # update + solve, balanced diagonal SYRK with K split, an
+                                     # unfused column, a ragged 8-wide last block
+                                     (520, 256)])
 def test_potrf_batched_dev(gpu_ctx, n, batch):
     """Batched device potrf vs np.linalg.cholesky per matrix (exact_gp.py:164) over
     the batch regimes of launch_potrf_batched128: <= 16 (column-sweep diagonal

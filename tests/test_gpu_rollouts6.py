@@ -105,13 +105,16 @@ def test_rollouts6_match_oracle_fitc_mean_as_written(gpu_ctx):
 
 def test_rollouts6_match_oracle_config5_gp(gpu_ctx):
     """The config-5 GP size (M = 2000 kmeans2 inducing points, N = 4000 training
-    rows, two GPs): 4 rollouts x 4 control steps.  K_uu of 2000 inducing points
-    at unit length scales is badly conditioned (jitter 1e-6), so the device fit (W = L_uu^-1,
-    beta = W^T alpha) and the numpy fit (triangular solves) agree on the GP
-    means to ~2e-9 absolute, and the plans to ~1e-8 (measured): inside the
-    1e-6 spec."""
-    seen, S = _run(gpu_ctx, 4000, 2000, 4, 4)
-    assert seen >= 8, seen
+    rows, two GPs), each side with its own fit: 16 rollouts x 12 control steps.
+    K_uu of 2000 inducing points at unit length scales is badly conditioned
+    (jitter 1e-6), so the device fit (W = L_uu^-1, beta = W^T alpha) and the numpy
+    fit (triangular solves) agree on the GP means to ~2e-9 absolute, and the plans
+    to ~1e-8 (measured): inside the 1e-6 spec.  The as-written mean K*u alpha is
+    not compared at this size: alpha itself is what the conditioning spoils, and
+    two independent fits give plans 2.7 apart at the first step (measured); the
+    small-GP test above covers that arithmetic."""
+    seen, S = _run(gpu_ctx, 4000, 2000, 16, 12)
+    assert seen >= 100, seen
 
 
 def test_rollouts6_shards_reproduce_the_whole_batch(gpu_ctx):
