@@ -1177,18 +1177,20 @@ static hipError_t launch_potrf_batched128(hipStream_t s, int n, int batch, doubl
   // left-looking (a step's columns take the update of the panel's earlier
   // steps, K = c - K0); across panels, one lower SYRK with K = OB, so the
   // O(n^3) work runs as K = OB products (fewer C read-modify-writes, longer K).
-  // Default: 128 (right-looking, K = 128 SYRKs) up to batch 255, 1024 (left-looking:
+  // Default: 128 (right-looking, K = 128 SYRKs) below batch 128, 1024 (left-looking:
   // each 128-column block takes the update of all earlier columns, K = c, with no
-  // trailing SYRK) from batch 256 on -- measured at n = 1000: 64: 1.34 vs 1.60 ms,
-  // 256: 3.62 vs 3.58 ms, 1024: 13.6 vs 13.2 ms (the long-K updates run at 50-70% of
-  // peak, the K = 128 / 256 ones at 30-38%).  256-512: no better than either.
+  // trailing SYRK) from 256 on and from 128 for multiples of 8 (the fused steps) --
+  // measured at n = 1000 (round 3, unfused): 64: 1.34 vs 1.60 ms, 256: 3.62 vs 3.58 ms,
+  // 1024: 13.6 vs 13.2 ms.  256-512: no better than either.
   static const int ob_env = [] {
     const char *v = getenv("GPMPC_POTRF_OB");
     if (!v) return 0;
     const int m = atoi(v) / DB;
     return DB * (m < 1 ? 1 : m > 8 ? 8 : m);
   }();
-  const int OBk = ob_env ? ob_env : (batch >= 256 ? 8 * DB : DB);
+  // left-looking from batch 128 when the fused steps apply (a multiple of 8): measured at
+  // n = 1000, 128: 2.13 -> 1.95 ms, 192: 2.89 -> 2.54 ms; 64 stays right-looking (1.25 vs 1.36)
+  const int OBk = ob_env ? ob_env : ((batch >= 256 || (batch >= 128 && batch % 8 == 0)) ? 8 * DB : DB);
   static const int ksplit_env = [] {
     const char *v = getenv("GPMPC_POTRF_KSPLIT");
     return v ? atoi(v) : 0;
@@ -1216,10 +1218,11 @@ static hipError_t launch_potrf_batched128(hipStream_t s, int n, int batch, doubl
     return v ? atoi(v) : 1;
   }();
   // a block column fuses when its rows below fill >= GPMPC_POTRF_FUSE_MIN workgroups (512)
-  static const int fuse_min = [] {
+  static const int fuse_min_env = [] {
     const char *v = getenv("GPMPC_POTRF_FUSE_MIN");
-    return v ? atoi(v) : 512;
+    return v ? atoi(v) : 0;
   }();
+  const int fuse_min = fuse_min_env ? fuse_min_env : (batch < 256 ? 1 : 512);
   auto fuses = [&](int c) {
     const int below = n - c - min(DB, n - c);
     return fuse_ok && below > 0 && (below + DB - 1) / DB * batch >= fuse_min;

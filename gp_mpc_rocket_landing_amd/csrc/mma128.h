@@ -12,10 +12,6 @@
 #define GP 18  // LDS pitch (doubles) of a 16-wide K slice
 #endif
 #define BT 128
-// MMA_PRIO: the wave's issue priority raised over each 4-k step's MFMAs (A/B builds)
-#ifndef MMA_PRIO
-#define MMA_PRIO 0
-#endif
 // acc = A[r0.., k_lo:k_hi] B[c0.., k_lo:k_hi]^T for one 128 x 128 tile (wave w
 // owns quadrant (w/2, w%2)); k_lo must be a multiple of GK.  Ends on a barrier,
 // so the LDS can be reused by the caller straight away.
@@ -156,11 +152,9 @@ __device__ __forceinline__ void mma128_tile(const double *__restrict__ A, int64_
       _Pragma("unroll") for (int x = 0; x < 4; ++x)                                      \
         if (((MASK) >> (4 * x)) & 15) a[x] = sA[cur][mma128_row(wave, x, IL) + (lane & 15)][kc]; \
       _Pragma("unroll") for (int y = 0; y < 4; ++y) b[y] = sB[cur][mma128_col(wave, y, ILC) + (lane & 15)][kc]; \
-      if (MMA_PRIO) __builtin_amdgcn_s_setprio(1);                                       \
       _Pragma("unroll") for (int x = 0; x < 4; ++x)                                      \
         _Pragma("unroll") for (int y = 0; y < 4; ++y)                                    \
           if (((MASK) >> (4 * x + y)) & 1) acc[x][y] = mfma_f64(a[x], b[y], acc[x][y]);  \
-      if (MMA_PRIO) __builtin_amdgcn_s_setprio(0);                                       \
     }                                                                                    \
     if (more) lstore(cur ^ 1);                                                           \
     __syncthreads();                                                                     \

@@ -61,13 +61,16 @@ def test_blocked_trsm_paths(gpu_ctx, n, nrhs):
                                      # left-looking, fused: the solve-only first column, K > 0
                                      # update + solve, balanced diagonal SYRK with K split, an
                                      # unfused column, a ragged 8-wide last block
-                                     (520, 256)])
+                                     (520, 256),
+                                     # left-looking from batch 128 (multiples of 8), fused from one workgroup
+                                     (300, 136)])
 def test_potrf_batched_dev(gpu_ctx, n, batch):
     """Batched device potrf vs np.linalg.cholesky per matrix (exact_gp.py:164) over
     the batch regimes of launch_potrf_batched128: <= 16 (column-sweep diagonal
     kernel, TRSM-form panel solve, latency-form SYRK), 17-64 (TRSM panel solve,
     tiled SYRK), 65-255 (assembled 128 x 128 inverse, in-place panel GEMM) and
-    >= 256 (left-looking block columns, no trailing SYRK).  The strict upper
+    >= 256, or >= 128 for multiples of 8 (left-looking block columns, no trailing
+    SYRK; fused update + panel solve, balanced diagonal SYRK).  The strict upper
     triangle is left untouched; a matrix with a bad pivot reports its 1-based
     column without disturbing the others."""
     import torch
