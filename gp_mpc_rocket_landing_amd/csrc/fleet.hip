@@ -434,7 +434,7 @@ __global__ __launch_bounds__(256) void k_fleet_control(FleetArgs a) {
 // STAMPS: the diagnostic phase-cycle instance (gpmpc_fleet_set_stamps); the
 // production instance has no stamp code or state at all.
 template <bool STAMPS>
-__global__ __launch_bounds__(FQ_T) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_fleet_control2(FleetArgs a) {
+__global__ __launch_bounds__(FQ_T) __attribute__((amdgpu_waves_per_eu(FQ_NW, FQ_NW))) void k_fleet_control2(FleetArgs a) {
   __shared__ FleetSmem s;
   __shared__ double sx[NX], st_tgt[NX];
   __shared__ int s_out;
@@ -447,7 +447,7 @@ __global__ __launch_bounds__(FQ_T) __attribute__((amdgpu_waves_per_eu(2, 2))) vo
   QPStamps T;
   T.out = (STAMPS && b == 0) ? a.stamps : nullptr;
   T.start();
-  if (a.trace && (tid & 63) == 0) {
+  if (a.trace && (tid & 63) == 0 && tid < 128) {
     // [0] start, [1] end (realtime), [2] wave 0 HW_ID | XCC_ID << 32, [3] wave 1 the same
     unsigned long long *tr = a.trace + (int64_t)b * 4;
     if (tid == 0) tr[0] = __builtin_amdgcn_s_memrealtime();
@@ -462,8 +462,8 @@ __global__ __launch_bounds__(FQ_T) __attribute__((amdgpu_waves_per_eu(2, 2))) vo
   // SIMD slow both (the slowest landings, which set the kernel time, are the
   // ones sharing), so each workgroup claims a SIMD of its CU for its chain:
   // wave 0's if no earlier workgroup of this launch took it, else wave 1's.
-  __shared__ int s_simd1, s_cw;
-  if (a.claims && tid == 64) s_simd1 = (__builtin_amdgcn_s_getreg(4 | (31 << 11)) >> 4) & 3;
+  __shared__ int s_simd[FQ_NW], s_cw;
+  if (a.claims && (tid & 63) == 0) s_simd[tid >> 6] = (__builtin_amdgcn_s_getreg(4 | (31 << 11)) >> 4) & 3;
   if (tid < NX) sx[tid] = x[tid];
   __syncthreads();
   if (tid == 0) {
@@ -471,16 +471,17 @@ __global__ __launch_bounds__(FQ_T) __attribute__((amdgpu_waves_per_eu(2, 2))) vo
     if (a.claims) {
       const unsigned hw = __builtin_amdgcn_s_getreg(4 | (31 << 11));
       const unsigned xcc = __builtin_amdgcn_s_getreg(20 | (31 << 11)) & 15;
-      const int s0 = (hw >> 4) & 3, s1 = s_simd1;
       const unsigned key = (xcc << 8) | (((hw >> 13) & 7) << 5) | (((hw >> 12) & 1) << 4) | ((hw >> 8) & 15);
       unsigned *cl = a.claims + key;
       unsigned old = __hip_atomic_load(cl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       for (int tries = 0; tries < 16; ++tries) {  // bounded: contention is at most 4 workgroups
         const unsigned mask = (old >> 8) == a.epoch ? (old & 15u) : 0u;
-        const int pick = !(mask & (1u << s0)) ? s0 : (!(mask & (1u << s1)) ? s1 : s0);
-        const unsigned nv = (a.epoch << 8) | mask | (1u << pick);
+        int w = 0;  // the first wave whose SIMD no earlier workgroup claimed (else wave 0)
+        while (w < FQ_NW && (mask & (1u << s_simd[w]))) ++w;
+        if (w == FQ_NW) w = 0;
+        const unsigned nv = (a.epoch << 8) | mask | (1u << s_simd[w]);
         const unsigned prev = atomicCAS(cl, old, nv);
-        if (prev == old) { cw0 = pick == s0 ? 0 : 1; break; }
+        if (prev == old) { cw0 = w; break; }
         old = prev;
       }
     }
@@ -520,7 +521,7 @@ __global__ __launch_bounds__(FQ_T) __attribute__((amdgpu_waves_per_eu(2, 2))) vo
   const int MD = NX * (N + 1);
   // ---- QP data (osqp_rti.py:203-372 with the GPMPC sign): variables + bound rows
 #pragma unroll
-  for (int h = 0; h < 2; ++h) {
+  for (int h = 0; h < FQ_H; ++h) {
     if (!R.vok[h]) continue;
     const int j = R.vj[h];
     double p, qq, lo, hi, xw;
@@ -612,7 +613,7 @@ __global__ __launch_bounds__(FQ_T) __attribute__((amdgpu_waves_per_eu(2, 2))) vo
   if (tid == 0) s.rho_s = a.rho[b];
   __syncthreads();
 #pragma unroll
-  for (int h = 0; h < 2; ++h)
+  for (int h = 0; h < FQ_H; ++h)
     if (R.rok[h]) {
       R.ur(h) = s.zt[R.rr[h]];  // l = u
       R.yr(h) = a.ysc[(int64_t)b * m + R.rr[h]];
@@ -624,7 +625,7 @@ __global__ __launch_bounds__(FQ_T) __attribute__((amdgpu_waves_per_eu(2, 2))) vo
   const bool has = !res.factor_fail && (res.status == 1 || res.status == 2 || res.status == -2);
   if (has) {
 #pragma unroll
-    for (int h = 0; h < 2; ++h)
+    for (int h = 0; h < FQ_H; ++h)
       if (R.vok[h]) s.rhs[R.vj[h]] = R.D[h] * R.x[h];  // unscaled solution
   }
   __syncthreads();
@@ -642,7 +643,7 @@ __global__ __launch_bounds__(FQ_T) __attribute__((amdgpu_waves_per_eu(2, 2))) vo
     // X_pred <- X_new (no shift), stop below sqp_tol
     double dm[1] = {0.0};
 #pragma unroll
-    for (int h = 0; h < 2; ++h)
+    for (int h = 0; h < FQ_H; ++h)
       if (R.vok[h]) {
         const int j = R.vj[h], i = (j >= Nv) ? j - Nv : j % (NX + NU), k = j / (NX + NU);
         const double old = (j >= Nv) ? Xw[N * NX + i] : (i < NX ? Xw[k * NX + i] : Uw[k * NU + i - NX]);
@@ -658,7 +659,7 @@ __global__ __launch_bounds__(FQ_T) __attribute__((amdgpu_waves_per_eu(2, 2))) vo
       Uw[e] = s.rhs[k * (NX + NU) + NX + i];
     }
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
+    for (int h = 0; h < FQ_H; ++h) {
       if (R.rok[h]) a.ysc[(int64_t)b * m + R.rr[h]] = R.yr(h);
       if (R.vok[h]) a.ysc[(int64_t)b * m + MD + R.vj[h]] = R.yb[h];
     }
@@ -708,7 +709,7 @@ __global__ __launch_bounds__(FQ_T) __attribute__((amdgpu_waves_per_eu(2, 2))) vo
       Uw[e] = s.rhs[ks * (NX + NU) + NX + i];
     }
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
+    for (int h = 0; h < FQ_H; ++h) {
       if (R.rok[h]) a.ysc[(int64_t)b * m + R.rr[h]] = R.yr(h);
       if (R.vok[h]) a.ysc[(int64_t)b * m + MD + R.vj[h]] = R.yb[h];
     }

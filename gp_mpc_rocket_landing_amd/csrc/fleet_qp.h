@@ -27,7 +27,11 @@
 #pragma once
 #include "qp_device.h"
 
-#define FQ_T 128
+#ifndef FQ_T
+#define FQ_T 128      // threads per landing: 128 (two items per thread) or 256 (one)
+#endif
+#define FQ_H (FQ_T >= 256 ? 1 : 2)  // item slots per thread
+#define FQ_NW (FQ_T / 64)           // waves per landing
 #define FQ_MD 147     // dynamics rows: NX (N+1) at N = 20
 #define FQ_NNZD 527   // their nonzeros: NX + 26 N
 #define FQ_NMAX 224   // x~: n = 207 padded to whole blocks (210) + the solve's look-ahead reads
@@ -57,7 +61,7 @@ struct FleetSmem {
   double band_store[FQ_FAC];
   double gzero[64];      // zero "-G rows" of the non-coupled lanes (they read gzero[0..63])
   double zslot, sink;
-  double red[2][16];
+  double red[FQ_NW][16];
   double c, rho_s;
   int flag;
   __device__ double *band() { return band_store; }
@@ -76,7 +80,12 @@ __device__ __forceinline__ void fq_max(double (&v)[K], double (*red)[16]) {
     for (int k = 0; k < K; ++k) red[wv][k] = v[k];
   __syncthreads();
 #pragma unroll
-  for (int k = 0; k < K; ++k) v[k] = fmax(red[0][k], red[1][k]);
+  for (int k = 0; k < K; ++k) {
+    double m = red[0][k];
+#pragma unroll
+    for (int w = 1; w < FQ_NW; ++w) m = fmax(m, red[w][k]);
+    v[k] = m;
+  }
   __syncthreads();
 }
 
@@ -93,7 +102,12 @@ __device__ __forceinline__ void fq_sum(double (&v)[K], double (*red)[16]) {
     for (int k = 0; k < K; ++k) red[wv][k] = v[k];
   __syncthreads();
 #pragma unroll
-  for (int k = 0; k < K; ++k) v[k] = red[0][k] + red[1][k];
+  for (int k = 0; k < K; ++k) {
+    double t = red[0][k];
+#pragma unroll
+    for (int w = 1; w < FQ_NW; ++w) t += red[w][k];
+    v[k] = t;
+  }
   __syncthreads();
 }
 
@@ -109,8 +123,13 @@ __device__ __forceinline__ void fq_sum_max(double &a, double &b, double (*red)[1
   __syncthreads();
   if (lane == 0) { red[wv][0] = a; red[wv][1] = b; }
   __syncthreads();
-  a = red[0][0] + red[1][0];
-  b = fmax(red[0][1], red[1][1]);
+  a = red[0][0];
+  b = red[0][1];
+#pragma unroll
+  for (int w = 1; w < FQ_NW; ++w) {
+    a += red[w][0];
+    b = fmax(b, red[w][1]);
+  }
   __syncthreads();
 }
 
@@ -153,7 +172,7 @@ static_assert((FQ_RMAX + 1) / 2 + 1 <= FQ_CMAX, "row slot 1 pattern must fit var
 __device__ __forceinline__ void fq_init_pattern(const QPPattern &pt, FleetRegs &R, int n) {
   const int t = threadIdx.x;
 #pragma unroll
-  for (int h = 0; h < 2; ++h) {
+  for (int h = 0; h < FQ_H; ++h) {
     const int j = t + h * FQ_T;
     R.vj[h] = j;
     R.vok[h] = j < n;
@@ -228,7 +247,7 @@ __device__ __forceinline__ double fq_row_dot(const FleetSmem &s, FleetRegs &R, i
 __device__ __forceinline__ void fq_scale(const QPPattern &pt, FleetSmem &s, FleetRegs &R, int iters) {
   const int n = pt.n, tid = threadIdx.x;
 #pragma unroll
-  for (int h = 0; h < 2; ++h) {
+  for (int h = 0; h < FQ_H; ++h) {
     R.D[h] = 1.0;
     if (R.vok[h]) s.E[FQ_MD + R.vj[h]] = 1.0;
     if (R.rok[h]) s.E[R.rr[h]] = 1.0;
@@ -239,7 +258,7 @@ __device__ __forceinline__ void fq_scale(const QPPattern &pt, FleetSmem &s, Flee
     // column factors -> rhs (scratch), row factors -> zt (dynamics) / register (bound)
     double eb[2];
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
+    for (int h = 0; h < FQ_H; ++h) {
       if (R.vok[h]) {
         double v = fabs(R.P[h]);  // padded entries read the zero A[FQ_NNZD]: fmax(v, 0) = v
         _Pragma("unroll") for (int e = 0; e < FQ_CMAX; ++e) v = fmax(v, fabs(s.A[R.ca(h, e)]));
@@ -259,7 +278,7 @@ __device__ __forceinline__ void fq_scale(const QPPattern &pt, FleetSmem &s, Flee
     }
     __syncthreads();
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
+    for (int h = 0; h < FQ_H; ++h) {
       if (R.rok[h]) {
         const double e = s.zt[R.rr[h]];
         _Pragma("unroll") for (int k = 0; k < FQ_RMAX; ++k) if (k < R.rn(h)) {
@@ -276,7 +295,7 @@ __device__ __forceinline__ void fq_scale(const QPPattern &pt, FleetSmem &s, Flee
     }
     double v[1] = {0.0};
 #pragma unroll
-    for (int h = 0; h < 2; ++h)
+    for (int h = 0; h < FQ_H; ++h)
       if (R.vok[h]) {
         const double d = s.rhs[R.vj[h]];
         R.P[h] = d * R.P[h] * d;
@@ -286,7 +305,7 @@ __device__ __forceinline__ void fq_scale(const QPPattern &pt, FleetSmem &s, Flee
       }
     double mx[1] = {0.0};
 #pragma unroll
-    for (int h = 0; h < 2; ++h)
+    for (int h = 0; h < FQ_H; ++h)
       if (R.vok[h]) mx[0] = fmax(mx[0], fabs(R.q[h]));
     fq_sum_max(v[0], mx[0], s.red);  // (its barriers also order the A / rhs updates above)
     double ct = v[0] / n;
@@ -294,13 +313,13 @@ __device__ __forceinline__ void fq_scale(const QPPattern &pt, FleetSmem &s, Flee
     ct = qp_limit(fmax(ct, nq));
     ct = 1.0 / ct;
 #pragma unroll
-    for (int h = 0; h < 2; ++h)
+    for (int h = 0; h < FQ_H; ++h)
       if (R.vok[h]) { R.P[h] *= ct; R.q[h] *= ct; }
     if (tid == 0) s.c *= ct;
     __syncthreads();
   }
 #pragma unroll
-  for (int h = 0; h < 2; ++h) {
+  for (int h = 0; h < FQ_H; ++h) {
     if (R.vok[h]) {
       const double e = s.E[FQ_MD + R.vj[h]];
       R.lb[h] = e * R.lb[h]; R.ub[h] = e * R.ub[h];
@@ -360,7 +379,7 @@ __device__ __forceinline__ int fq_factor(const QPPattern &pt, FleetSmem &s, Flee
   // dynamics rows of column j (the owner's column pattern; pads add re * 0 * 0)
   // and last its bound row -- with no pattern reads
 #pragma unroll
-  for (int h = 0; h < 2; ++h) {
+  for (int h = 0; h < FQ_H; ++h) {
     if (!R.vok[h]) continue;
     const int j = R.vj[h], e = (j / SZ) * BS + (j % SZ) * (SZ + 1);
     double a[FQ_CMAX];
@@ -394,14 +413,14 @@ __device__ __forceinline__ int fq_factor(const QPPattern &pt, FleetSmem &s, Flee
 // re: 0 |Ax - z|  1 max(|z|,|Ax|)  2 |q + Px + A'y|  3 max(|q|,|A'y|,|Px|)   (scaled)
 __device__ __forceinline__ void fq_update_info(FleetSmem &s, FleetRegs &R, double (&o)[8], double (&re)[4]) {
 #pragma unroll
-  for (int h = 0; h < 2; ++h) {
+  for (int h = 0; h < FQ_H; ++h) {
     if (R.vok[h]) s.rhs[R.vj[h]] = R.x[h];
     if (R.rok[h]) s.zt[R.rr[h]] = R.yr(h);
   }
   __syncthreads();
   double v[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
 #pragma unroll
-  for (int h = 0; h < 2; ++h) {
+  for (int h = 0; h < FQ_H; ++h) {
     if (R.rok[h]) {  // dynamics row: (A x)_r
       double ax = 0.0;
       _Pragma("unroll") for (int e = 0; e < FQ_RMAX; ++e) ax += s.A[R.rb(h) + e] * s.rhs[R.rc(h, e)];
@@ -452,7 +471,7 @@ __device__ __forceinline__ bool fq_primal_infeasible(FleetSmem &s, FleetRegs &R,
     return d;
   };
 #pragma unroll
-  for (int h = 0; h < 2; ++h) {
+  for (int h = 0; h < FQ_H; ++h) {
     if (R.rok[h]) {
       R.dyr(h) = proj(R.dyr(h), R.ur(h), R.ur(h));
       v[0] = fmax(v[0], fabs(s.E[R.rr[h]] * R.dyr(h)));
@@ -467,19 +486,19 @@ __device__ __forceinline__ bool fq_primal_infeasible(FleetSmem &s, FleetRegs &R,
   if (!(nrm > QP_DIV_TOL)) return false;
   double sm[1] = {0.0};
 #pragma unroll
-  for (int h = 0; h < 2; ++h) {
+  for (int h = 0; h < FQ_H; ++h) {
     if (R.rok[h]) sm[0] += R.ur(h) * fmax(R.dyr(h), 0.0) + R.ur(h) * fmin(R.dyr(h), 0.0);
     if (R.vok[h]) sm[0] += R.ub[h] * fmax(R.dyb[h], 0.0) + R.lb[h] * fmin(R.dyb[h], 0.0);
   }
   fq_sum<1>(sm, s.red);
   if (!(sm[0] < -eps * nrm)) return false;
 #pragma unroll
-  for (int h = 0; h < 2; ++h)
+  for (int h = 0; h < FQ_H; ++h)
     if (R.rok[h]) s.zt[R.rr[h]] = R.dyr(h);
   __syncthreads();
   double mx[1] = {0.0};
 #pragma unroll
-  for (int h = 0; h < 2; ++h)
+  for (int h = 0; h < FQ_H; ++h)
     if (R.vok[h]) {
       double acc = 0.0;
       _Pragma("unroll") for (int e = 0; e < FQ_CMAX; ++e) acc += s.A[R.ca(h, e)] * s.zt[R.cr(h, e)];
@@ -493,14 +512,14 @@ __device__ __forceinline__ bool fq_primal_infeasible(FleetSmem &s, FleetRegs &R,
 __device__ __forceinline__ bool fq_dual_infeasible(FleetSmem &s, FleetRegs &R, double eps) {
   double v[1] = {0.0};
 #pragma unroll
-  for (int h = 0; h < 2; ++h)
+  for (int h = 0; h < FQ_H; ++h)
     if (R.vok[h]) v[0] = fmax(v[0], fabs(R.D[h] * R.dx[h]));
   fq_max<1>(v, s.red);
   const double nrm = v[0];
   if (!(nrm > QP_DIV_TOL)) return false;
   double a[1] = {0.0}, pm[1] = {0.0};
 #pragma unroll
-  for (int h = 0; h < 2; ++h)
+  for (int h = 0; h < FQ_H; ++h)
     if (R.vok[h]) {
       a[0] += R.q[h] * R.dx[h];
       pm[0] = fmax(pm[0], fabs(R.P[h] * R.dx[h] / R.D[h]));
@@ -510,7 +529,7 @@ __device__ __forceinline__ bool fq_dual_infeasible(FleetSmem &s, FleetRegs &R, d
   if (!(a[0] < s.c * eps * nrm)) return false;
   if (!(pm[0] < s.c * eps * nrm)) return false;
 #pragma unroll
-  for (int h = 0; h < 2; ++h)
+  for (int h = 0; h < FQ_H; ++h)
     if (R.vok[h]) s.rhs[R.vj[h]] = R.dx[h];
   __syncthreads();
   double bad[1] = {0.0};
@@ -520,7 +539,7 @@ __device__ __forceinline__ bool fq_dual_infeasible(FleetSmem &s, FleetRegs &R, d
       bad[0] = 1.0;
   };
 #pragma unroll
-  for (int h = 0; h < 2; ++h) {
+  for (int h = 0; h < FQ_H; ++h) {
     if (R.rok[h]) {
       double adx = 0.0;
       _Pragma("unroll") for (int e = 0; e < FQ_RMAX; ++e) adx += s.A[R.rb(h) + e] * s.rhs[R.rc(h, e)];
@@ -562,7 +581,7 @@ __device__ __forceinline__ double fq_rho_estimate(const FleetSmem &s, const doub
 __device__ __forceinline__ void fq_rebuild_zt(FleetSmem &s, FleetRegs &R) {
   const double rs = s.rho_s;
 #pragma unroll
-  for (int h = 0; h < 2; ++h) {
+  for (int h = 0; h < FQ_H; ++h) {
     if (R.rok[h]) s.zt[R.rr[h]] = QP_RHO_EQ * rs * R.zr(h) - R.yr(h);
   }
   __syncthreads();
@@ -578,7 +597,7 @@ __device__ __forceinline__ QPResult fq_solve(const QPPattern &pt, FleetSmem &s, 
   QPResult res{-10, 0, 0.0, 0};
   QPStamps &T = *ts;  // the caller's (no pointer select: a null `out` folds the stamps away)
 #pragma unroll
-  for (int h = 0; h < 2; ++h) {
+  for (int h = 0; h < FQ_H; ++h) {
     R.lb[h] = fmax(R.lb[h], -QP_OSQP_INFTY); R.ub[h] = fmin(R.ub[h], QP_OSQP_INFTY);
     if (R.rok[h]) R.ur(h) = fmin(fmax(R.ur(h), -QP_OSQP_INFTY), QP_OSQP_INFTY);
   }
@@ -589,7 +608,7 @@ __device__ __forceinline__ QPResult fq_solve(const QPPattern &pt, FleetSmem &s, 
   if (st.scaling) fq_scale(pt, s, R, st.scaling);
   else {
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
+    for (int h = 0; h < FQ_H; ++h) {
       R.D[h] = 1.0;
       if (R.vok[h]) s.E[FQ_MD + R.vj[h]] = 1.0;
       if (R.rok[h]) s.E[R.rr[h]] = 1.0;
@@ -606,11 +625,11 @@ __device__ __forceinline__ QPResult fq_solve(const QPPattern &pt, FleetSmem &s, 
   if (f) { res.factor_fail = f; return res; }
   if (st.warm_start) {
 #pragma unroll
-    for (int h = 0; h < 2; ++h)
+    for (int h = 0; h < FQ_H; ++h)
       if (R.vok[h]) { R.x[h] = R.x[h] / R.D[h]; s.rhs[R.vj[h]] = R.x[h]; }
     __syncthreads();
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {  // z = A x
+    for (int h = 0; h < FQ_H; ++h) {  // z = A x
       if (R.rok[h]) {
         double acc = 0.0;
         _Pragma("unroll") for (int e = 0; e < FQ_RMAX; ++e) acc += s.A[R.rb(h) + e] * s.rhs[R.rc(h, e)];
@@ -620,7 +639,7 @@ __device__ __forceinline__ QPResult fq_solve(const QPPattern &pt, FleetSmem &s, 
     }
   } else {
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
+    for (int h = 0; h < FQ_H; ++h) {
       R.x[h] = 0.0; R.zr(h) = 0.0; R.yr(h) = 0.0; R.zb[h] = 0.0; R.yb[h] = 0.0;
     }
   }
@@ -633,7 +652,7 @@ __device__ __forceinline__ QPResult fq_solve(const QPPattern &pt, FleetSmem &s, 
   for (it = 1; it <= st.max_iter; ++it) {
     // rhs = sigma x - q + A'(rho z - y)
 #pragma unroll
-    for (int h = 0; h < 2; ++h)
+    for (int h = 0; h < FQ_H; ++h)
       if (R.vok[h]) {
         double acc = fq_col_dot(s, R, h);
         acc += R.Ab[h] * (fq_rho(R.lb[h], R.ub[h], s.rho_s) * R.zb[h] - R.yb[h]);
@@ -668,7 +687,7 @@ __device__ __forceinline__ QPResult fq_solve(const QPPattern &pt, FleetSmem &s, 
     T.mark(4);
     const double rs = s.rho_s;
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
+    for (int h = 0; h < FQ_H; ++h) {
       if (R.vok[h]) {
         const double xt = s.rhs[R.vj[h]];
         const double xo = R.x[h];
@@ -738,7 +757,7 @@ __device__ __forceinline__ QPResult fq_solve(const QPPattern &pt, FleetSmem &s, 
   }
   double ob[1] = {0.0};
 #pragma unroll
-  for (int h = 0; h < 2; ++h)
+  for (int h = 0; h < FQ_H; ++h)
     if (R.vok[h]) ob[0] += 0.5 * R.x[h] * (R.P[h] * R.x[h]) + R.q[h] * R.x[h];
   fq_sum<1>(ob, s.red);
   res.obj = ob[0] / s.c;

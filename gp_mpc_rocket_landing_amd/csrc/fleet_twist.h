@@ -307,7 +307,7 @@ __device__ __forceinline__ void ft_solve(S &s, double *b, int cw) {
     // diagonal: u_k / x_10 / w_k, eight blocks a round (one per DPP row of
     // either wave); rows past the last block read the last block and do not store
     const int q = (int)(threadIdx.x >> 4);
-    constexpr int RB = 8, NR = (FT_NB + RB - 1) / RB;
+    constexpr int RB = FQ_T / 16, NR = (FT_NB + RB - 1) / RB;
 #pragma unroll 1
     for (int t = 0; t < NR; ++t) {
       const int kk = RB * t + q, k = kk < FT_NB ? kk : FT_NB - 1;
