@@ -62,7 +62,7 @@ def test_blocked_trsm_paths(gpu_ctx, n, nrhs):
                                      # update + solve, balanced diagonal SYRK with K split, an
                                      # unfused column, a ragged 8-wide last block
                                      (520, 256),
-                                     # left-looking from batch 128 (multiples of 8), fused from one workgroup
+                                     # left-looking from batch 128 (multiples of 8): unfused steps (too few workgroups)
                                      (300, 136)])
 def test_potrf_batched_dev(gpu_ctx, n, batch):
     """Batched device potrf vs np.linalg.cholesky per matrix (exact_gp.py:164) over
