@@ -551,7 +551,7 @@ __global__ __launch_bounds__(FQ_T) __attribute__((amdgpu_waves_per_eu(FQ_NW, FQ_
     }
     R.P[h] = p; R.q[h] = qq; R.x[h] = xw;
     R.Ab[h] = 1.0; R.lb[h] = lo; R.ub[h] = hi;
-    R.yb[h] = a.ysc[(int64_t)b * m + MD + j];
+    R.yb_(h) = a.ysc[(int64_t)b * m + MD + j];
   }
   // dynamics rows: A values (one thread per stage) and c_k, staged in zt for the row owners
   for (int r = tid; r < NX; r += FQ_T) {
@@ -661,7 +661,7 @@ __global__ __launch_bounds__(FQ_T) __attribute__((amdgpu_waves_per_eu(FQ_NW, FQ_
 #pragma unroll
     for (int h = 0; h < FQ_H; ++h) {
       if (R.rok[h]) a.ysc[(int64_t)b * m + R.rr[h]] = R.yr(h);
-      if (R.vok[h]) a.ysc[(int64_t)b * m + MD + R.vj[h]] = R.yb[h];
+      if (R.vok[h]) a.ysc[(int64_t)b * m + MD + R.vj[h]] = R.yb_(h);
     }
     if (tid == 0) {
       const bool conv = dm[0] < a.sqp_tol;
@@ -711,7 +711,7 @@ __global__ __launch_bounds__(FQ_T) __attribute__((amdgpu_waves_per_eu(FQ_NW, FQ_
 #pragma unroll
     for (int h = 0; h < FQ_H; ++h) {
       if (R.rok[h]) a.ysc[(int64_t)b * m + R.rr[h]] = R.yr(h);
-      if (R.vok[h]) a.ysc[(int64_t)b * m + MD + R.vj[h]] = R.yb[h];
+      if (R.vok[h]) a.ysc[(int64_t)b * m + MD + R.vj[h]] = R.yb_(h);
     }
   }
   if (tid == 0) {

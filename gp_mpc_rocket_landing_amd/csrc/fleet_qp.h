@@ -145,7 +145,13 @@ struct FleetRegs {
   int vj[2], rr[2];
   // variable j and bound row MD + j
   double x[2], dx[2], P[2], q[2], D[2];
-  double Ab[2], lb[2], ub[2], yb[2], zb[2], dyb[2];  // (rho z - y of the bound row: recomputed)
+  double Ab[2], lb[2], ub[2];
+  // the bound row's y, z, delta y as scalars per slot, not arrays: an array whose slot-1
+  // element also serves the aliased dynamics row (yr / zr / dyr below) was kept in scratch
+  double yb0, yb1, zb0, zb1, dyb0, dyb1;  // (rho z - y of the bound row: recomputed)
+  __device__ __forceinline__ double &yb_(int h) { return h ? yb1 : yb0; }
+  __device__ __forceinline__ double &zb_(int h) { return h ? zb1 : zb0; }
+  __device__ __forceinline__ double &dyb_(int h) { return h ? dyb1 : dyb0; }
   // dynamics row 0 (l = u = ur).  No thread owns both a second variable and a
   // second dynamics row (t < 79: 2 variables + 1 row; t >= 109: 1 + 2), so row
   // slot 1 lives in variable slot 1's registers: ur <- P, yr <- yb, zr <- zb,
@@ -156,9 +162,9 @@ struct FleetRegs {
   int cn[2], cp[2][FQ_CMAX];
   int rbn0, rcp0[(FQ_RMAX + 1) / 2];
   __device__ __forceinline__ double &ur(int h) { return h ? P[1] : ur0; }
-  __device__ __forceinline__ double &yr(int h) { return h ? yb[1] : yr0; }
-  __device__ __forceinline__ double &zr(int h) { return h ? zb[1] : zr0; }
-  __device__ __forceinline__ double &dyr(int h) { return h ? dyb[1] : dyr0; }
+  __device__ __forceinline__ double &yr(int h) { return h ? yb1 : yr0; }
+  __device__ __forceinline__ double &zr(int h) { return h ? zb1 : zr0; }
+  __device__ __forceinline__ double &dyr(int h) { return h ? dyb1 : dyr0; }
   __device__ __forceinline__ int &rbn(int h) { return h ? cp[1][3] : rbn0; }
   __device__ __forceinline__ int &rcp(int h, int e) { return h ? cp[1][e] : rcp0[e]; }
   __device__ __forceinline__ int ca(int h, int e) const { return cp[h][e] & 0xffff; }
@@ -434,7 +440,7 @@ __device__ __forceinline__ void fq_update_info(FleetSmem &s, FleetRegs &R, doubl
     if (R.vok[h]) {
       {  // bound row
         const double ax = 0.0 + R.Ab[h] * R.x[h];
-        const double e = s.E[FQ_MD + R.vj[h]], z = R.zb[h];
+        const double e = s.E[FQ_MD + R.vj[h]], z = R.zb_(h);
         v[0] = fmax(v[0], fabs((ax - z) / e));
         v[1] = fmax(v[1], fabs(z / e));
         v[2] = fmax(v[2], fabs(ax / e));
@@ -443,7 +449,7 @@ __device__ __forceinline__ void fq_update_info(FleetSmem &s, FleetRegs &R, doubl
       }
       double aty = 0.0;  // (A' y)_j in CSC order, the bound row last
       _Pragma("unroll") for (int e = 0; e < FQ_CMAX; ++e) aty += s.A[R.ca(h, e)] * s.zt[R.cr(h, e)];
-      aty += R.Ab[h] * R.yb[h];
+      aty += R.Ab[h] * R.yb_(h);
       const double px = R.P[h] * R.x[h], d = R.D[h], q = R.q[h];
       v[3] = fmax(v[3], fabs((q + px + aty) / d));
       v[4] = fmax(v[4], fabs(q / d));
@@ -477,8 +483,8 @@ __device__ __forceinline__ bool fq_primal_infeasible(FleetSmem &s, FleetRegs &R,
       v[0] = fmax(v[0], fabs(s.E[R.rr[h]] * R.dyr(h)));
     }
     if (R.vok[h]) {
-      R.dyb[h] = proj(R.dyb[h], R.lb[h], R.ub[h]);
-      v[0] = fmax(v[0], fabs(s.E[FQ_MD + R.vj[h]] * R.dyb[h]));
+      R.dyb_(h) = proj(R.dyb_(h), R.lb[h], R.ub[h]);
+      v[0] = fmax(v[0], fabs(s.E[FQ_MD + R.vj[h]] * R.dyb_(h)));
     }
   }
   fq_max<1>(v, s.red);
@@ -488,7 +494,7 @@ __device__ __forceinline__ bool fq_primal_infeasible(FleetSmem &s, FleetRegs &R,
 #pragma unroll
   for (int h = 0; h < FQ_H; ++h) {
     if (R.rok[h]) sm[0] += R.ur(h) * fmax(R.dyr(h), 0.0) + R.ur(h) * fmin(R.dyr(h), 0.0);
-    if (R.vok[h]) sm[0] += R.ub[h] * fmax(R.dyb[h], 0.0) + R.lb[h] * fmin(R.dyb[h], 0.0);
+    if (R.vok[h]) sm[0] += R.ub[h] * fmax(R.dyb_(h), 0.0) + R.lb[h] * fmin(R.dyb_(h), 0.0);
   }
   fq_sum<1>(sm, s.red);
   if (!(sm[0] < -eps * nrm)) return false;
@@ -502,7 +508,7 @@ __device__ __forceinline__ bool fq_primal_infeasible(FleetSmem &s, FleetRegs &R,
     if (R.vok[h]) {
       double acc = 0.0;
       _Pragma("unroll") for (int e = 0; e < FQ_CMAX; ++e) acc += s.A[R.ca(h, e)] * s.zt[R.cr(h, e)];
-      acc += R.Ab[h] * R.dyb[h];
+      acc += R.Ab[h] * R.dyb_(h);
       mx[0] = fmax(mx[0], fabs(acc / R.D[h]));
     }
   fq_max<1>(mx, s.red);
@@ -635,12 +641,12 @@ __device__ __forceinline__ QPResult fq_solve(const QPPattern &pt, FleetSmem &s, 
         _Pragma("unroll") for (int e = 0; e < FQ_RMAX; ++e) acc += s.A[R.rb(h) + e] * s.rhs[R.rc(h, e)];
         R.zr(h) = acc;
       }
-      if (R.vok[h]) R.zb[h] = 0.0 + R.Ab[h] * R.x[h];
+      if (R.vok[h]) R.zb_(h) = 0.0 + R.Ab[h] * R.x[h];
     }
   } else {
 #pragma unroll
     for (int h = 0; h < FQ_H; ++h) {
-      R.x[h] = 0.0; R.zr(h) = 0.0; R.yr(h) = 0.0; R.zb[h] = 0.0; R.yb[h] = 0.0;
+      R.x[h] = 0.0; R.zr(h) = 0.0; R.yr(h) = 0.0; R.zb_(h) = 0.0; R.yb_(h) = 0.0;
     }
   }
   __syncthreads();
@@ -655,7 +661,7 @@ __device__ __forceinline__ QPResult fq_solve(const QPPattern &pt, FleetSmem &s, 
     for (int h = 0; h < FQ_H; ++h)
       if (R.vok[h]) {
         double acc = fq_col_dot(s, R, h);
-        acc += R.Ab[h] * (fq_rho(R.lb[h], R.ub[h], s.rho_s) * R.zb[h] - R.yb[h]);
+        acc += R.Ab[h] * (fq_rho(R.lb[h], R.ub[h], s.rho_s) * R.zb_(h) - R.yb_(h));
         s.rhs[R.vj[h]] = sig * R.x[h] - R.q[h] + acc;
       }
     T.mark(11);
@@ -696,13 +702,13 @@ __device__ __forceinline__ QPResult fq_solve(const QPPattern &pt, FleetSmem &s, 
         R.x[h] = xn;
         // bound row: z~ = A_b x~_j
         const double ztl = 0.0 + R.Ab[h] * xt;
-        const double rho = fq_rho(R.lb[h], R.ub[h], rs), zo = R.zb[h], yo = R.yb[h];
+        const double rho = fq_rho(R.lb[h], R.ub[h], rs), zo = R.zb_(h), yo = R.yb_(h);
         const double zr = al * ztl + (1.0 - al) * zo;
         double zn = zr + yo / rho;
         zn = fmin(fmax(zn, R.lb[h]), R.ub[h]);
         const double d = rho * (zr - zn);
         const double yn = yo + d;
-        R.dyb[h] = d; R.yb[h] = yn; R.zb[h] = zn;
+        R.dyb_(h) = d; R.yb_(h) = yn; R.zb_(h) = zn;
       }
       if (R.rok[h]) {
         const double ztl = fq_row_dot(s, R, h);
