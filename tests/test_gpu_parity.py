@@ -304,9 +304,12 @@ def test_fleet_runs_and_is_deterministic(gpu_ctx):
     assert np.all(r1["records"][:, 1] > 0)
 
 
-@pytest.mark.parametrize("n,k,batch", [(100, 40, 3), (512, 512, 2), (300, 4096, 1)])
+@pytest.mark.parametrize("n,k,batch", [(100, 40, 3), (512, 512, 2), (300, 4096, 1),
+                                       # stream-K (ragged last tiles), one matrix and batched
+                                       (1000, 1024, 1), (1000, 1024, 2)])
 def test_syrk_batched_paths(gpu_ctx, n, k, batch):
-    """C = I - A A^T (lower) through the 64-tile, 128-tile and split-K (fp64 atomics) GEMM paths."""
+    """C = I - A A^T (lower) through the 64-tile, 128-tile, split-K (fp64 atomics) and
+    stream-K GEMM paths."""
     import torch
     L = _lib()
     g = torch.Generator(device="cuda").manual_seed(n + k)
