@@ -100,6 +100,40 @@ def test_potrf_batched_dev(gpu_ctx, n, batch):
     assert torch.equal(A[:-1, up], up_before[:-1])
 
 
+_SWITCH_CHILD = r"""
+import os, sys, numpy as np, torch
+sys.path.insert(0, os.getcwd())
+from gp_mpc_rocket_landing_amd import _lib as L
+ctx = L.Context(0)
+n, batch = 520, 256
+rs = np.random.RandomState(11)
+As = np.stack([(lambda G: G @ G.T / n + np.eye(n))(rs.normal(size=(n, n))) for _ in range(batch)])
+A = torch.tensor(As, dtype=torch.float64, device="cuda")
+info = torch.zeros(batch, dtype=torch.int32, device="cuda")
+L._chk(L._L.gpmpc_potrf_batched_dev(ctx.h, n, batch, A.data_ptr(), n, n * n, info.data_ptr()), "potrf")
+ctx.sync()
+assert int(info.abs().sum()) == 0
+Ah = A.cpu().numpy()
+for b in range(0, batch, 37):
+    np.testing.assert_allclose(np.tril(Ah[b]), np.linalg.cholesky(As[b]), rtol=1e-10, atol=1e-12)
+print("switch child ok")
+"""
+
+
+@pytest.mark.parametrize("env", [{"GPMPC_POTRF_LA": "1"}, {"GPMPC_SYRK_DIAG": "0"}, {"GPMPC_POTRF_FUSE": "0"}])
+def test_potrf_switch_paths(gpu_ctx, env):
+    """The left-looking potrf's switchable paths (read once per process, so each in a
+    child process): the look-ahead diagonal update inside the fused step, the 128-tile
+    diagonal-block update, and the unfused update + panel solve, at n = 520 x 256."""
+    import os
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, "-c", _SWITCH_CHILD], cwd=repo, env=dict(os.environ, **env),
+                       capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0 and "switch child ok" in r.stdout, (env, r.stdout[-1000:], r.stderr[-3000:])
+
+
 @pytest.mark.parametrize("n", [100, 129, 256, 300, 1000])
 def test_potrf_batched_persistent(gpu_ctx, n):
     """The one-workgroup-per-matrix potrf (k_potrf_persist: left-looking 128-column
