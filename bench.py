@@ -107,16 +107,44 @@ def _cpu_landing_loop(seconds, n_train=1000, horizon=20, seed=42, threads=1):
     return steps, el
 
 
+def cpu_quota():
+    """The CPU share this job is granted: the cgroup quota (v2 ``cpu.max``, v1
+    ``cfs_quota_us / cfs_period_us``) when one is set, else the thread budget the
+    box exports (``OMP_NUM_THREADS`` / ``MAX_JOBS``), else None.  Returns
+    (cores or None, source)."""
+    import math
+    try:
+        q, p = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            return max(1, math.floor(int(q) / int(p))), f"cgroup cpu.max {q}/{p}"
+    except Exception:  # noqa: BLE001
+        pass
+    try:
+        q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+        p = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+        if q > 0:
+            return max(1, math.floor(q / p)), f"cgroup v1 cfs {q}/{p}"
+    except Exception:  # noqa: BLE001
+        pass
+    for var in ("OMP_NUM_THREADS", "MAX_JOBS"):
+        v = os.environ.get(var, "")
+        if v.isdigit() and int(v) > 0:
+            return int(v), f"{var}={v} (no cgroup CPU quota visible)"
+    return None, "none (no cgroup quota, no thread budget in the environment)"
+
+
 def cpu_baseline(seconds, n_train=1000, horizon=20, workers=None):
-    """SURVEY 8d CPU baseline, throughput mode: one process per host core (at
-    most the box's 16-core share), one landing each, BLAS on one thread, for
-    ``seconds``; value = all processes' control steps / the longest elapsed.
-    Runs before the GPU is initialised (spawned workers, fresh interpreters)."""
+    """SURVEY 8d CPU baseline, throughput mode: one process per core of the job's
+    CPU share (cpu_quota(); the affinity mask when no share is stated), one
+    landing each, BLAS on one thread, for ``seconds``; value = all processes'
+    control steps / the longest elapsed.  Runs before the GPU is initialised
+    (spawned workers, fresh interpreters)."""
     import concurrent.futures as cf
     import multiprocessing as mp
     import platform
     aff = len(os.sched_getaffinity(0))
-    workers = workers or max(1, min(16, aff))
+    quota, quota_src = cpu_quota()
+    workers = workers or max(1, min(aff, quota) if quota else aff)
     with cf.ProcessPoolExecutor(workers, mp_context=mp.get_context("spawn")) as ex:
         res = list(ex.map(_cpu_landing_loop, [seconds] * workers, [n_train] * workers,
                           [horizon] * workers, [42 + 1000 * i for i in range(workers)]))
@@ -136,16 +164,16 @@ def cpu_baseline(seconds, n_train=1000, horizon=20, workers=None):
     # SURVEY 8d mode (i): one landing with BLAS on all the workers' cores
     st1, el1 = _cpu_landing_loop(min(5.0, seconds), n_train, horizon, 42, workers)
     return dict(value=steps / el, unit="control steps/s", cores=workers, kind="port",
-                per_core=round(per_core, 3),
-                # the box grants this job a 16-core share of its CPUs, so a whole
-                # socket cannot be run here; landings are independent single-
-                # threaded processes, so per-core x cores is its upper bound
+                per_core=round(per_core, 3), affinity_cpus=aff, cpu_quota=quota,
+                cpu_quota_source=quota_src,
+                # landings are independent single-threaded processes, so per-core x
+                # cores bounds a whole 64-core socket the job's share cannot run
                 socket_64c_extrapolated=round(per_core * 64, 1),
                 single_landing_all_cores=round(st1 / el1, 3),
                 sample=f"{workers} processes x 1 landing closed loop, {steps} control steps in "
                        f"{el:.1f} s (numpy/scipy GP N={n_train}, P={horizon}; numpy QP assembly; "
                        f"C OSQP-0.6 ADMM restatement; {blas} on 1 thread per process; "
-                       f"{aff} CPUs in affinity; {cpu})")
+                       f"{aff} CPUs in affinity, CPU share {quota} from {quota_src}; {cpu})")
 
 
 def cholesky_bench(ctx, torch, n=1000, batch=64, reps=3):

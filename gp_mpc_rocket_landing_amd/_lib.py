@@ -137,6 +137,7 @@ _sig("gpmpc_cov_propagate_dev", _c, _vp, _c, _c, _c, _vp, _vp, _vp, ctypes.c_dou
 _sig("gpmpc_fleet_read", _c, _vp, _dp, _dp)
 _sig("gpmpc_gram_grad", _c, _vp, _c, _dp, _c, _dp, _c, _c, _dp, ctypes.c_double, _dp, _dp)
 _sig("gpmpc_fleet_get_state", _c, _vp, _dp, _dp, _dp, _dp)
+_sig("gpmpc_fleet_get_posterior", _c, _vp, _dp, _dp)
 _sig("gpmpc_fleet_records_dev", _vp, _vp)
 _sig("gpmpc_fleet_destroy", _c, _vp)
 _sig("gpmpc_rollout6_default_config", None, ctypes.POINTER(Rollout6Config))
@@ -152,6 +153,8 @@ _sig("gpmpc_comm_init", _c, _vp, ctypes.c_char_p, _c, _c, ctypes.POINTER(_vp))
 _sig("gpmpc_comm_destroy", _c, _vp)
 _sig("gpmpc_comm_count", _c, _vp, _ip)
 _sig("gpmpc_gather_results", _c, _vp, _vp, _vp, _ip, _c, _dp)
+_sig("gpmpc_gather_prepare", _c, _vp, _vp, _vp, _ip, _c)
+_sig("gpmpc_gather_collective", _c, _vp, _vp, _ip, _c, _dp)
 _sig("gpmpc_rollout6_reset", _c, _vp, _c, _c, _dp)
 _sig("gpmpc_rollout6_step", _c, _vp, _c)
 _sig("gpmpc_rollout6_step_phases", _c, _vp, _c)
@@ -167,14 +170,14 @@ EXPORTED = ["gpmpc_abi_version", "gpmpc_last_error", "gpmpc_ctx_create", "gpmpc_
             "gpmpc_fitc_fit", "gpmpc_fitc_predict", "gpmpc_fitc_destroy",
             "gpmpc_qp_default_settings", "gpmpc_qp_solve_batched", "gpmpc_fleet_default_config",
             "gpmpc_fleet_create", "gpmpc_fleet_reset", "gpmpc_fleet_step", "gpmpc_fleet_read",
-            "gpmpc_fleet_step_phases", "gpmpc_fleet_get_state", "gpmpc_fleet_set_stamps", "gpmpc_fleet_set_trace",
+            "gpmpc_fleet_step_phases", "gpmpc_fleet_get_state", "gpmpc_fleet_get_posterior", "gpmpc_fleet_set_stamps", "gpmpc_fleet_set_trace",
             "gpmpc_syrk_batched_dev", "gpmpc_cov_propagate", "gpmpc_cov_propagate_dev",
             "gpmpc_fleet_records_dev", "gpmpc_fleet_destroy", "gpmpc_rollout6_default_config",
             "gpmpc_rollout6_create", "gpmpc_rollout6_reset", "gpmpc_rollout6_step", "gpmpc_rollout6_read",
             "gpmpc_rollout6_get_state", "gpmpc_rollout6_destroy", "gpmpc_rollout6_create_exact",
             "gpmpc_rollout6_solve", "gpmpc_rollout6_solve_ref", "gpmpc_rollout6_set_state", "gpmpc_fitc_get_state",
             "gpmpc_rollout6_records_dev", "gpmpc_comm_unique_id", "gpmpc_comm_init", "gpmpc_comm_destroy",
-            "gpmpc_comm_count", "gpmpc_gather_results", "gpmpc_rollout6_step_phases", "gpmpc_vfe_fit"]
+            "gpmpc_comm_count", "gpmpc_gather_results", "gpmpc_gather_prepare", "gpmpc_gather_collective", "gpmpc_rollout6_step_phases", "gpmpc_vfe_fit"]
 
 
 class HIPError(RuntimeError):

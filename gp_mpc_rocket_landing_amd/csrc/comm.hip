@@ -69,6 +69,7 @@ struct gpmpc_comm {
   ncclComm_t comm = nullptr;
   int nranks = 0, rank = 0, device = 0;
   DevBuf send, recv;  // padded blocks (grown on demand)
+  bool prepared = false;  // gpmpc_gather_prepare succeeded since the last collective
 };
 
 extern "C" int gpmpc_comm_unique_id(unsigned char *id) {
@@ -122,29 +123,68 @@ __global__ void k_pad_records(int count, int cmax, const double *__restrict__ sr
   dst[i] = i < count * GPMPC_REC_LEN ? src[i] : __builtin_nan("");
 }
 
-extern "C" int gpmpc_gather_results(gpmpc_ctx *ctx, gpmpc_comm *c, const double *d_records, const int *counts,
-                                    int root, double *out) {
-  GPMPC_CHECK_ARG(ctx && c && counts && root >= 0 && root < c->nranks);
-  GPMPC_CHECK_ARG(c->device == ctx->device);
+// The gather in two steps, so that ranks can agree between them: every
+// failure a rank can meet on its own (argument checks, the send / receive buffers'
+// allocation, the pad kernel) happens in gpmpc_gather_prepare, which ends with the
+// stream drained; gpmpc_gather_collective then only issues the ncclGather and the
+// root's compaction.  A caller agrees on every rank's prepare status (one all-reduce)
+// before any rank enters the collective.
+struct GatherPlan {
   int cmax = 0, total = 0;
+};
+
+static int gather_plan(gpmpc_comm *c, const int *counts, int root, GatherPlan &p) {
+  GPMPC_CHECK_ARG(counts && root >= 0 && root < c->nranks);
+  p = GatherPlan{};
   for (int r = 0; r < c->nranks; ++r) {
     GPMPC_CHECK_ARG(counts[r] >= 0);
-    cmax = counts[r] > cmax ? counts[r] : cmax;
-    total += counts[r];
+    p.cmax = counts[r] > p.cmax ? counts[r] : p.cmax;
+    p.total += counts[r];
   }
+  return 0;
+}
+
+extern "C" int gpmpc_gather_prepare(gpmpc_ctx *ctx, gpmpc_comm *c, const double *d_records, const int *counts,
+                                    int root) {
+  GPMPC_CHECK_ARG(ctx && c);
+  GPMPC_CHECK_ARG(c->device == ctx->device);
+  GatherPlan p;
+  if (int rc = gather_plan(c, counts, root, p)) return rc;
   const int count = counts[c->rank];
   GPMPC_CHECK_ARG(count == 0 || d_records);
-  GPMPC_CHECK_ARG(c->rank != root || out || total == 0);
-  if (cmax == 0) return 0;
+  c->prepared = false;
+  if (p.cmax == 0) {
+    c->prepared = true;
+    return 0;
+  }
   GPMPC_HIP(hipSetDevice(ctx->device));
   hipStream_t s = ctx->stream;
-  const size_t blk = (size_t)cmax * GPMPC_REC_LEN;
+  const size_t blk = (size_t)p.cmax * GPMPC_REC_LEN;
   if (c->send.bytes < blk * sizeof(double)) GPMPC_HIP(c->send.alloc(blk * sizeof(double)));
   if (c->rank == root && c->recv.bytes < blk * c->nranks * sizeof(double))
     GPMPC_HIP(c->recv.alloc(blk * c->nranks * sizeof(double)));
-  hipLaunchKernelGGL(k_pad_records, dim3((unsigned)((blk + 255) / 256)), dim3(256), 0, s, count, cmax, d_records,
+  hipLaunchKernelGGL(k_pad_records, dim3((unsigned)((blk + 255) / 256)), dim3(256), 0, s, count, p.cmax, d_records,
                      c->send.as<double>());
   GPMPC_HIP(hipGetLastError());
+  GPMPC_HIP(hipStreamSynchronize(s));
+  c->prepared = true;
+  return 0;
+}
+
+extern "C" int gpmpc_gather_collective(gpmpc_ctx *ctx, gpmpc_comm *c, const int *counts, int root, double *out) {
+  GPMPC_CHECK_ARG(ctx && c);
+  GatherPlan p;
+  if (int rc = gather_plan(c, counts, root, p)) return rc;
+  GPMPC_CHECK_ARG(c->rank != root || out || p.total == 0);
+  if (!c->prepared) {
+    gpmpc_set_error("gather: gpmpc_gather_prepare did not succeed on this rank");
+    return -2;
+  }
+  c->prepared = false;
+  if (p.cmax == 0) return 0;
+  GPMPC_HIP(hipSetDevice(ctx->device));
+  hipStream_t s = ctx->stream;
+  const size_t blk = (size_t)p.cmax * GPMPC_REC_LEN;
   GPMPC_RCCL(rccl().gather(c->send.p, c->rank == root ? c->recv.p : c->send.p, blk, ncclFloat64, root, c->comm, s));
   if (c->rank == root) {
     // compact: rank r's rows [0, counts[r]) in rank order
@@ -158,4 +198,11 @@ extern "C" int gpmpc_gather_results(gpmpc_ctx *ctx, gpmpc_comm *c, const double 
   }
   GPMPC_HIP(hipStreamSynchronize(s));
   return 0;
+}
+
+// both steps in one call, for a caller that does not need the agreement in between
+extern "C" int gpmpc_gather_results(gpmpc_ctx *ctx, gpmpc_comm *c, const double *d_records, const int *counts,
+                                    int root, double *out) {
+  if (int rc = gpmpc_gather_prepare(ctx, c, d_records, counts, root)) return rc;
+  return gpmpc_gather_collective(ctx, c, counts, root, out);
 }

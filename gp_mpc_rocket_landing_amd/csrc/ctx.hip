@@ -2,6 +2,7 @@
 #include "internal.h"
 #include <cstdarg>
 #include <mutex>
+#include <cstdlib>
 
 static thread_local char g_err[1024] = "";
 
@@ -39,14 +40,27 @@ void *gpmpc_scratch(hipStream_t s, int slot, size_t bytes) {
 }
 
 // ---- per-stream caching pool (internal.h) ------------------------------------
+// Each stream's pool carries a generation: a context's destruction ends its pool,
+// and a later context whose stream handle happens to have the same value starts a
+// new generation, so a block allocated under the old one (a handle that outlived
+// its context) is freed on return instead of joining a stranger's free list.
 #include <vector>
 struct StreamPool {
   std::map<size_t, std::vector<void *>> free;  // size class -> cached blocks
   size_t cached = 0;
+  uint64_t gen = 0;
 };
 static std::mutex g_pool_mu;
 static std::map<hipStream_t, StreamPool> g_pool;
-static const size_t kPoolCapBytes = (size_t)8 << 30;  // per stream
+static uint64_t g_pool_gen = 0;
+
+static size_t pool_cap() {  // per stream; GPMPC_POOL_CAP_MB overrides the 8 GB default
+  static const size_t cap = [] {
+    const char *e = getenv("GPMPC_POOL_CAP_MB");
+    return e ? (size_t)strtoull(e, nullptr, 10) << 20 : (size_t)8 << 30;
+  }();
+  return cap;
+}
 
 static size_t pool_class(size_t b) {
   if (b <= 256) return 256;
@@ -56,12 +70,37 @@ static size_t pool_class(size_t b) {
   return (b + g - 1) / g * g;
 }
 
-void *gpmpc_pool_get(hipStream_t s, size_t bytes, size_t *cls) {
+static StreamPool &pool_of(hipStream_t s) {  // g_pool_mu held
+  auto it = g_pool.find(s);
+  if (it == g_pool.end()) {
+    it = g_pool.emplace(s, StreamPool{}).first;
+    it->second.gen = ++g_pool_gen;
+  }
+  return it->second;
+}
+
+// drop every cached block of stream s (after s has drained: its kernels may still read them)
+static void pool_trim(hipStream_t s) {
+  std::vector<void *> blocks;
+  {
+    std::lock_guard<std::mutex> lk(g_pool_mu);
+    auto it = g_pool.find(s);
+    if (it == g_pool.end()) return;
+    for (auto &kv : it->second.free)
+      for (void *p : kv.second) blocks.push_back(p);
+    it->second.free.clear();
+    it->second.cached = 0;
+  }
+  for (void *p : blocks) (void)hipFree(p);
+}
+
+void *gpmpc_pool_get(hipStream_t s, size_t bytes, size_t *cls, uint64_t *gen) {
   const size_t c = pool_class(bytes);
   *cls = c;
   {
     std::lock_guard<std::mutex> lk(g_pool_mu);
-    StreamPool &sp = g_pool[s];
+    StreamPool &sp = pool_of(s);
+    *gen = sp.gen;
     auto it = sp.free.find(c);
     if (it != sp.free.end() && !it->second.empty()) {
       void *p = it->second.back();
@@ -71,25 +110,35 @@ void *gpmpc_pool_get(hipStream_t s, size_t bytes, size_t *cls) {
     }
   }
   void *p = nullptr;
-  if (hipMalloc(&p, c) != hipSuccess) return nullptr;
+  if (hipMalloc(&p, c) == hipSuccess) return p;
+  // out of memory: the stream's cached blocks are the first thing to give back
+  // (ADVICE r4), then one retry
+  (void)hipGetLastError();
+  (void)hipStreamSynchronize(s);
+  pool_trim(s);
+  p = nullptr;
+  if (hipMalloc(&p, c) != hipSuccess) {
+    (void)hipGetLastError();
+    return nullptr;
+  }
   return p;
 }
 
-void gpmpc_pool_put(hipStream_t s, void *p, size_t cls) {
+void gpmpc_pool_put(hipStream_t s, void *p, size_t cls, uint64_t gen) {
   if (!p) return;
   bool live = false;
   {
     std::lock_guard<std::mutex> lk(g_pool_mu);
     auto it = g_pool.find(s);
-    live = it != g_pool.end();
-    if (live && it->second.cached + cls <= kPoolCapBytes) {
+    live = it != g_pool.end() && it->second.gen == gen;
+    if (live && it->second.cached + cls <= pool_cap()) {
       it->second.free[cls].push_back(p);
       it->second.cached += cls;
       return;
     }
   }
-  // over the cap: let the stream's earlier readers finish first; a stream whose pool is
-  // gone was synchronised and destroyed with its context
+  // over the cap: let the stream's earlier readers finish first; a block whose pool
+  // generation is gone belongs to a destroyed context (hipFree synchronises the device)
   if (live) (void)hipStreamSynchronize(s);
   (void)hipFree(p);
 }

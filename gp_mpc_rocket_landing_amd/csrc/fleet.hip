@@ -795,6 +795,27 @@ extern "C" int gpmpc_fleet_create(gpmpc_ctx *ctx, gpmpc_gp *gp, const gpmpc_flee
                     "FastRTI3DoF runs on the host mirror");
     return -2;
   }
+  {
+    // sqp_qp.max_iter = 0 means "use qp".  sqp_qp left at the defaults (a caller that
+    // edits only qp) or equal to qp is that; any other field edited alongside max_iter 0
+    // would be silently ignored, so such a config is refused
+    auto same = [](const gpmpc_qp_settings &a, const gpmpc_qp_settings &b) {
+      return a.rho == b.rho && a.sigma == b.sigma && a.alpha == b.alpha && a.eps_abs == b.eps_abs &&
+             a.eps_rel == b.eps_rel && a.eps_prim_inf == b.eps_prim_inf && a.eps_dual_inf == b.eps_dual_inf &&
+             a.check_termination == b.check_termination && a.adaptive_rho == b.adaptive_rho &&
+             a.adaptive_rho_interval == b.adaptive_rho_interval &&
+             a.adaptive_rho_tolerance == b.adaptive_rho_tolerance && a.scaling == b.scaling &&
+             a.warm_start == b.warm_start;
+    };
+    gpmpc_qp_settings def;
+    gpmpc_qp_default_settings(&def);
+    if (cfg->sqp_iters > 1 && cfg->sqp_qp.max_iter == 0 && !same(cfg->sqp_qp, cfg->qp) &&
+        !same(cfg->sqp_qp, def)) {
+      gpmpc_set_error("fleet: sqp_qp was edited but sqp_qp.max_iter is 0 (= use qp); set "
+                      "sqp_qp.max_iter to use the SQP passes' own settings");
+      return -2;
+    }
+  }
   const int N = cfg->horizon;
   const int n = (N + 1) * NX + N * NU, m = NX * (N + 1) + n;
   GPMPC_CHECK_ARG(N >= 1 && n <= QP_NMAX && m <= QP_MMAX && NX + N * DYN_NNZ + n <= QP_NNZMAX);
@@ -1129,6 +1150,49 @@ extern "C" int gpmpc_fleet_get_state(gpmpc_fleet *f, double *Xw, double *Uw, dou
     GPMPC_HIP(hipMemcpyAsync(y_scaled, f->ysc.p, sizeof(double) * B * f->m, hipMemcpyDeviceToHost, s));
   if (rho) GPMPC_HIP(hipMemcpyAsync(rho, f->rho.p, sizeof(double) * B, hipMemcpyDeviceToHost, s));
   GPMPC_HIP(hipStreamSynchronize(s));
+  return 0;
+}
+
+// The GP posterior of the last control step at every landing's N horizon points, per
+// landing (B x N x 3 each, row-major): the mean and variance the step's QP assembly
+// consumed (the variance is computed beside it, exact_gp.py:256-266, and not read by
+// the QP).  The device rows follow the dispatch slots of that step; they are put back
+// in landing order here.  Valid for the landings that were running at the start of that
+// step; landings past the step's running prefix read NaN, and a landing that terminated
+// at the step's top keeps the values of its last running step.
+extern "C" int gpmpc_fleet_get_posterior(gpmpc_fleet *f, double *mean, double *var) {
+  GPMPC_CHECK_ARG(f && (mean || var));
+  if (!f->cfg.use_gp) {
+    gpmpc_set_error("fleet: use_gp = 0, the fleet runs no GP posterior");
+    return -2;
+  }
+  hipStream_t s = f->ctx->stream;
+  GPMPC_HIP(hipSetDevice(f->ctx->device));
+  const size_t B = (size_t)f->B, N = (size_t)f->N, P = B * N;
+  std::vector<double> dm(P * 3), dv(P * 3), rec(B * GPMPC_REC_LEN);
+  std::vector<int> ord(B);
+  GPMPC_HIP(hipMemcpyAsync(dm.data(), f->mean.p, sizeof(double) * P * 3, hipMemcpyDeviceToHost, s));
+  GPMPC_HIP(hipMemcpyAsync(dv.data(), f->var.p, sizeof(double) * P * 3, hipMemcpyDeviceToHost, s));
+  GPMPC_HIP(hipMemcpyAsync(ord.data(), f->order.p, sizeof(int) * B, hipMemcpyDeviceToHost, s));
+  GPMPC_HIP(hipStreamSynchronize(s));
+  const bool by_slot = f->use_order;  // gp_by_slot of fleet_args (use_gp holds here)
+  const size_t nslots = by_slot ? (size_t)f->post_P / N : B;
+  std::vector<char> ran(B, 0);
+  for (size_t sl = 0; sl < nslots && sl < B; ++sl) {
+    const int b = by_slot ? ord[sl] : (int)sl;
+    if (b < 0 || (size_t)b >= B) continue;
+    ran[b] = 1;
+    for (size_t e = 0; e < N * 3; ++e) {
+      if (mean) mean[(size_t)b * N * 3 + e] = dm[sl * N * 3 + e];
+      if (var) var[(size_t)b * N * 3 + e] = dv[sl * N * 3 + e];
+    }
+  }
+  for (size_t b = 0; b < B; ++b)
+    if (!ran[b])
+      for (size_t e = 0; e < N * 3; ++e) {
+        if (mean) mean[b * N * 3 + e] = NAN;
+        if (var) var[b * N * 3 + e] = NAN;
+      }
   return 0;
 }
 

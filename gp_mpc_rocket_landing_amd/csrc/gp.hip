@@ -680,7 +680,10 @@ extern "C" int gpmpc_gp_get_state(gpmpc_ctx *ctx, gpmpc_gp *gp, double *L, doubl
   return 0;
 }
 
+// A handle's buffers come from its fitting context's stream pool, but fleets and
+// rollouts read them from their own streams: drain the device before they go back.
 extern "C" int gpmpc_gp_destroy(gpmpc_gp *gp) {
+  if (gp) (void)hipDeviceSynchronize();
   delete gp;
   return 0;
 }
@@ -1035,6 +1038,7 @@ extern "C" int gpmpc_fitc_predict(gpmpc_ctx *ctx, gpmpc_fitc *gp, const double *
 }
 
 extern "C" int gpmpc_fitc_destroy(gpmpc_fitc *gp) {
+  if (gp) (void)hipDeviceSynchronize();  // as gpmpc_gp_destroy
   delete gp;
   return 0;
 }
@@ -1332,6 +1336,9 @@ extern "C" int gpmpc_gp_append(gpmpc_ctx *ctx, gpmpc_gp *gp, const double *Xnew,
   g.Xs.swap(Xs2);
   g.Xn.swap(Xn2);
   g.n = m;
+  // the replaced buffers go back to the pool when this returns; another context's
+  // stream may still be reading them (as gpmpc_gp_destroy)
+  (void)hipDeviceSynchronize();
   for (int c = 0; c < no; ++c) {
     if (lml) lml[c] = hl[c];
     if (y_mean) y_mean[c] = g.h_ymean[c];

@@ -42,10 +42,12 @@ void *gpmpc_scratch(hipStream_t s, int slot, size_t bytes);
 // (an implicit device-wide synchronisation, ~41 us a call: ~15 per exact fit, DESIGN
 // §11).  A block is handed out again only on the stream it was last used on, so that
 // stream's order keeps its earlier readers ahead of the next writer.  Blocks are sized
-// in classes (<= 12.5% rounding), cached up to a per-stream cap, and released with the
-// context (gpmpc_ctx_destroy).
-void *gpmpc_pool_get(hipStream_t s, size_t bytes, size_t *cls);
-void gpmpc_pool_put(hipStream_t s, void *p, size_t cls);
+// in classes (<= 12.5% rounding), cached up to a per-stream cap (GPMPC_POOL_CAP_MB, 8 GB),
+// and released with the context (gpmpc_ctx_destroy); a failed hipMalloc first gives the
+// stream's cached blocks back and retries.  gen: the pool generation the block came from
+// (a block returned after its context's destruction is freed, not cached).
+void *gpmpc_pool_get(hipStream_t s, size_t bytes, size_t *cls, uint64_t *gen);
+void gpmpc_pool_put(hipStream_t s, void *p, size_t cls, uint64_t gen);
 
 // RAII device buffer (host-side bookkeeping only).  alloc(bytes): its own hipMalloc
 // (handle-owned state that outlives the call); alloc(stream, bytes): a pooled
@@ -55,13 +57,14 @@ struct DevBuf {
   size_t bytes = 0;
   hipStream_t pool = nullptr;  // non-null: pooled on this stream
   size_t cls = 0;
+  uint64_t gen = 0;            // the pool generation it came from
   DevBuf() = default;
   DevBuf(const DevBuf &) = delete;
   DevBuf &operator=(const DevBuf &) = delete;
   ~DevBuf() { release(); }
   void release() {
     if (p) {
-      if (pool) gpmpc_pool_put(pool, p, cls);
+      if (pool) gpmpc_pool_put(pool, p, cls, gen);
       else (void)hipFree(p);
     }
     p = nullptr;
@@ -76,13 +79,14 @@ struct DevBuf {
     release();
     bytes = b;
     if (!b) return hipSuccess;
-    p = gpmpc_pool_get(s, b, &cls);
+    p = gpmpc_pool_get(s, b, &cls, &gen);
     if (!p) return hipErrorOutOfMemory;
     pool = s;
     return hipSuccess;
   }
   void swap(DevBuf &o) {
     std::swap(p, o.p); std::swap(bytes, o.bytes); std::swap(pool, o.pool); std::swap(cls, o.cls);
+    std::swap(gen, o.gen);
   }
   template <class T> T *as() const { return static_cast<T *>(p); }
 };

@@ -68,6 +68,16 @@ class Fleet:
                                                 _lib._d(rho)), "fleet_get_state")
         return dict(rec=rec, x=x, Xw=Xw, Uw=Uw, y=y, rho=rho)
 
+    def posterior(self):
+        """The last control step's GP posterior at every landing's N horizon points
+        (ExactGP.predict, exact_gp.py:256-266): mean and variance, (batch, N, 3) each,
+        in landing order."""
+        B, N = self.batch, int(self.cfg.horizon)
+        mean = np.empty((B, N, 3)); var = np.empty((B, N, 3))
+        _lib._chk(_lib._L.gpmpc_fleet_get_posterior(self.h, _lib._d(mean), _lib._d(var)),
+                  "fleet_get_posterior")
+        return mean, var
+
     @property
     def records_dev(self):
         return _lib._L.gpmpc_fleet_records_dev(self.h)

@@ -137,15 +137,31 @@ class RCCLRecordGather:
         _lib._chk(_lib._L.gpmpc_comm_count(self.h, ctypes.byref(n)), "comm_count")
         self.nranks = int(n.value)
 
-    def gather(self, d_records, total: int, root: int = 0):
-        """d_records: this rank's device record pointer (shard_range(total, rank, world)
-        rows).  Returns the (total, REC_LEN) records on the root, None elsewhere."""
+    def _counts(self, total):
+        return np.array([shard_range(total, r, self.world)[1] for r in range(self.world)], np.int32)
+
+    def prepare(self, d_records, total: int, root: int = 0):
+        """The local half (gpmpc_gather_prepare): argument checks, buffers, the
+        device padding of this rank's block.  Raises on this rank's failure."""
         lib = self._lib
-        counts = np.array([shard_range(total, r, self.world)[1] for r in range(self.world)], np.int32)
+        self._root = int(root)
+        lib._chk(lib._L.gpmpc_gather_prepare(self.ctx.h, self.h, d_records, lib._i(self._counts(total)),
+                                             int(root)), "gather_prepare")
+
+    def collective(self, total: int, root: int = 0):
+        """The ncclGather itself (gpmpc_gather_collective), after every rank's prepare
+        succeeded.  Returns the (total, REC_LEN) records on the root, None elsewhere."""
+        lib = self._lib
         out = np.empty((int(total), lib.REC_LEN)) if self.rank == root else None
-        lib._chk(lib._L.gpmpc_gather_results(self.ctx.h, self.h, d_records, lib._i(counts), int(root),
-                                             lib._d(out) if out is not None else None), "gather_results")
+        lib._chk(lib._L.gpmpc_gather_collective(self.ctx.h, self.h, lib._i(self._counts(total)), int(root),
+                                                lib._d(out) if out is not None else None), "gather_collective")
         return out
+
+    def gather(self, d_records, total: int, root: int = 0):
+        """prepare + collective without an agreement in between (a world of one,
+        or a caller that has agreed by other means)."""
+        self.prepare(d_records, total, root)
+        return self.collective(total, root)
 
     def close(self):
         if getattr(self, "h", None):
@@ -159,41 +175,60 @@ class RCCLRecordGather:
             pass
 
 
+class GatherCollectiveError(RuntimeError):
+    """The ncclGather failed after every rank had prepared its block.  Peers may
+    be inside the collective or past it, so there is no agreed way back: the
+    caller must treat this as fatal (exit non-zero)."""
+
+
 def gather_shard_records(ctx, d_records, host_records, total: int, path: str | None = None,
-                         device=None, _fail_local=False):
+                         device=None, _fail_local=False, _gather=None):
     """The one collective of the path, with a record of what ran.
 
     path "rccl" (default, or GPMPC_GATHER): the C-ABI's ncclGather of the device
-    record arrays.  If its set-up fails on any rank, every rank knows it (the
-    readiness counts are agreed) and all fall back together to
-    torch.distributed.gather of the host records; if the gather itself fails on
-    any rank, likewise.  path "torch": torch.distributed.gather directly.
+    record arrays, in three agreed stages.  (1) Set-up (communicator): if it
+    fails on any rank every rank knows it (RCCLRecordGather's readiness counts).
+    (2) prepare (gpmpc_gather_prepare: buffers, padding -- everything a rank can
+    fail alone): one readiness count after it on every rank.  If either stage
+    failed anywhere, all ranks fall back together to torch.distributed.gather of
+    the host records, and only then destroy the communicator.  (3) The collective
+    itself: a failure there is fatal (GatherCollectiveError), because a peer may
+    already be inside it or past it.  path "torch": torch.distributed.gather
+    directly.
 
     Returns (records on rank 0 / None elsewhere, info) with info =
     {"path": "rccl" | "torch", "nranks": ranks the collective spanned (RCCL's
     communicator count, or the process group's size), "records": rows gathered
-    on rank 0 (0 elsewhere), "requested": path, "fallback": reason or None}."""
+    on rank 0 (0 elsewhere), "requested": path, "fallback": reason or None}.
+    ``_gather``: a factory standing in for RCCLRecordGather (tests)."""
     path = path or os.environ.get("GPMPC_GATHER", "rccl")
     world, rank, dist = _world()
     info = {"path": None, "nranks": None, "records": 0, "requested": path, "fallback": None}
     if path == "rccl":
         g = None
         try:
-            g = RCCLRecordGather(ctx, _fail_local=_fail_local)
+            g = (_gather or RCCLRecordGather)(ctx, _fail_local=_fail_local)
         except GatherSetupError as e:
             info["fallback"] = str(e)
         if g is not None:
-            out, err = None, None
+            err = None
             try:
-                out = g.gather(d_records, total)
+                g.prepare(d_records, total)
             except Exception as e:  # noqa: BLE001  (agreed below)
                 err = str(e)
-            nr = g.nranks
-            g.close()
-            if _count_ready(err is None) == world:
+            ready = _count_ready(err is None)
+            if ready == world:
+                try:
+                    out = g.collective(total)
+                except Exception as e:  # noqa: BLE001
+                    raise GatherCollectiveError(f"ncclGather failed on rank {rank}: {e}") from e
+                nr = g.nranks
+                g.close()
                 info.update(path="rccl", nranks=nr, records=0 if out is None else int(out.shape[0]))
                 return out, info
-            info["fallback"] = "ncclGather failed" + (f" (this rank: {err})" if err else " on a peer")
+            g.close()   # every rank skips the collective: the communicator is idle everywhere
+            info["fallback"] = (f"gather prepare failed on {world - ready} of {world} ranks"
+                                + (f" (this rank: {err})" if err else ""))
     elif path != "torch":
         raise ValueError(f"unknown gather path {path!r} (rccl or torch)")
     if dist is None:

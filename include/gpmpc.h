@@ -29,7 +29,10 @@ extern "C" {
 /* 2: gpmpc_fleet_config gained sqp_iters / sqp_tol (round 2) and
  * gpmpc_rollout6_config the GPMPC problem data (round 3);
  * 3: gpmpc_rollout6_config gained the rocket parameters and horizon 20 or 30,
- * gpmpc_rollout6_solve_ref (X_ref / U_ref), gpmpc_comm_count (round 4) */
+ * gpmpc_rollout6_solve_ref (X_ref / U_ref), gpmpc_comm_count (round 4); round 4 also
+ * gave gpmpc_fleet_config.sqp_qp the max_iter = 0 "same as qp" meaning.  Round 5 adds
+ * entry points only (gpmpc_fleet_get_posterior, gpmpc_gather_prepare / _collective) and
+ * refuses a fleet config whose sqp_qp was edited with max_iter left 0. */
 #define GPMPC_ABI_VERSION 3
 
 typedef struct gpmpc_ctx gpmpc_ctx;
@@ -226,6 +229,10 @@ typedef struct {
   gpmpc_qp_settings sqp_qp;  /* QP settings of the SQP passes (sqp_iters > 1).  sqp_qp.max_iter
                                 = 0 (the default) means "the same as qp", resolved when the fleet
                                 launches, so a caller that edits only qp changes the passes too.
+                                With sqp_iters > 1 and max_iter 0, an sqp_qp that equals neither
+                                the defaults nor qp (a field edited alongside max_iter 0, which
+                                would be ignored) makes gpmpc_fleet_create fail (-2): set
+                                sqp_qp.max_iter to give the passes their own settings.
                                 The reference solves this subproblem with IPOPT (gp_mpc.py:462-470) */
 } gpmpc_fleet_config;
 void gpmpc_fleet_default_config(gpmpc_fleet_config *c);
@@ -252,6 +259,12 @@ int gpmpc_fleet_read(gpmpc_fleet *f, double *records, double *x /* batch x 7, ma
  * (batch x N x 3), the ADMM's persistent scaled duals (batch x m) and rho
  * (batch) -- what OSQP keeps between solves (osqp_rti.py:517-527) */
 int gpmpc_fleet_get_state(gpmpc_fleet *f, double *Xw, double *Uw, double *y_scaled, double *rho);
+/* the last control step's GP posterior at every landing's N horizon points
+ * (ExactGP.predict, exact_gp.py:256-266, over the step's linearisation
+ * trajectory): mean and variance, batch x N x 3 each, in landing order (either
+ * may be NULL).  Valid for the landings running at the start of that step;
+ * landings past its running prefix read NaN.  -2 when use_gp = 0. */
+int gpmpc_fleet_get_posterior(gpmpc_fleet *f, double *mean, double *var);
 /* diagnostic: accumulate s_memtime cycles of landing 0's control kernel per
  * phase into dev_u64x16 (16 x uint64 device buffer; NULL disables):
  * 0 assembly, 1 scaling, 2 factor, 3 A' rhs, 4 KKT solve (band path, or the
@@ -400,9 +413,19 @@ int gpmpc_comm_count(gpmpc_comm *c, int *nranks);
 /* d_records: this rank's counts[rank] x GPMPC_REC_LEN records (device, e.g.
  * gpmpc_fleet_records_dev); counts: every rank's shard size (host, nranks).
  * On the root, out (host) receives sum(counts) x GPMPC_REC_LEN doubles in
- * rank order; elsewhere out may be NULL.  Collective: every rank calls it. */
+ * rank order; elsewhere out may be NULL.  Collective: every rank calls it.
+ * = gpmpc_gather_prepare + gpmpc_gather_collective. */
 int gpmpc_gather_results(gpmpc_ctx *ctx, gpmpc_comm *c, const double *d_records, const int *counts, int root,
                          double *out);
+/* The same gather in two steps, so that the ranks can agree in between: prepare is
+ * local (argument checks, send/receive buffers, the device padding of the ragged
+ * block; the stream is drained before it returns), so every failure a rank can
+ * meet alone is reported by it; collective issues only the ncclGather and the
+ * root's compaction, and fails with -2 unless prepare succeeded since the last
+ * collective.  Agree on every rank's prepare status before any rank calls
+ * collective (sharding.gather_shard_records does, with one all-reduce). */
+int gpmpc_gather_prepare(gpmpc_ctx *ctx, gpmpc_comm *c, const double *d_records, const int *counts, int root);
+int gpmpc_gather_collective(gpmpc_ctx *ctx, gpmpc_comm *c, const int *counts, int root, double *out);
 int gpmpc_fleet_destroy(gpmpc_fleet *f);
 
 #ifdef __cplusplus

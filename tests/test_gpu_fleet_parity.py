@@ -501,3 +501,43 @@ def test_fleet_sqp_mode_matches_oracle(gpu_ctx):
             assert moved >= nb // 2, moved   # converged at 1e-4 and stepped
         else:
             assert moved > nb, moved   # the converged branch (plant step) ran
+
+
+def test_fleet_posterior_full_size_matches_oracle(gpu_ctx):
+    """The headline kernel's own output: the GP posterior the
+    fleet computes each control step for all 1024 landings x 20 horizon points
+    (P = 20 480 queries against the n = 1000 GP, BASELINE configs[3]) -- the mean
+    the QP assembly consumes and the variance the MFMA sum-of-squares pass forms
+    beside it -- read back through the C-ABI (gpmpc_fleet_get_posterior) and
+    compared with ExactGP.predict (exact_gp.py:256-266, gp_oracle.exact_predict)
+    at every query, over two control steps (the second one with the dispatch order
+    of the first step's iteration counts, so the slot -> landing map is not the
+    identity).  Tolerance spec SURVEY 8c: |a - b| <= 1e-6 max(|b|, s), s = y_std
+    for means, sigma2 y_std^2 for variances."""
+    from gp_mpc_rocket_landing_amd.data import synthetic_training_data
+    from gp_mpc_rocket_landing_amd.fleet import Fleet, fit_gp, initial_conditions
+    from oracle import gp_oracle
+
+    nb, n = 1024, 1000
+    X, U, D = synthetic_training_data(n, seed=0)
+    st = gp_oracle.exact_fit(gp_oracle.features_3dof(X, U), D)
+    gp = fit_gp(gpu_ctx, n_train=n)
+    fl = Fleet(gpu_ctx, gp, nb, horizon=N)
+    try:
+        fl.reset(initial_conditions(nb))
+        for step in range(2):
+            S = fl.state()
+            assert np.all(S["rec"][:, 0] == 0)
+            fl.step(1)
+            mean, var = fl.posterior()
+            Zq = gp_oracle.features_3dof(S["Xw"][:, :N].reshape(-1, 7), S["Uw"].reshape(-1, 3))
+            m_ref, v_ref = gp_oracle.exact_predict(st, Zq)
+            for c in range(3):
+                ok, worst = close(mean.reshape(-1, 3)[:, c], m_ref[:, c], st["y_std"][c])
+                assert ok, (step, "mean", c, worst)
+                ok, worst = close(var.reshape(-1, 3)[:, c], v_ref[:, c], st["sigma2"] * st["y_std"][c] ** 2)
+                assert ok, (step, "var", c, worst)
+            # the variance is not a constant: the posterior really varies over the queries
+            assert np.ptp(v_ref[:, 0]) > 0.0
+    finally:
+        fl.close()

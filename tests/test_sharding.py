@@ -164,3 +164,71 @@ def test_gather_shard_records_world1_without_group():
     import pytest
     with pytest.raises(ValueError):
         gather_shard_records(None, None, rec, 5, path="mpi")
+
+
+class _FakeGather:
+    """Stands in for RCCLRecordGather on a gloo group (no GPU): set-up succeeds,
+    prepare fails on the ranks listed in FAIL_PREPARE, and a collective entered
+    by any rank is recorded (it must never be entered when a prepare failed)."""
+    FAIL_PREPARE = (1,)
+
+    def __init__(self, ctx, _fail_local=False):
+        from gp_mpc_rocket_landing_amd.sharding import _world
+        self.world, self.rank, _ = _world()
+        self.nranks = self.world
+        self.closed = False
+        self.entered = False
+
+    def prepare(self, d_records, total):
+        if self.rank in self.FAIL_PREPARE:
+            raise RuntimeError("gather_prepare failed (-1): hipMalloc out of memory (injected)")
+
+    def collective(self, total):
+        self.entered = True
+        raise AssertionError("collective entered although a peer's prepare failed")
+
+    def close(self):
+        self.closed = True
+
+
+def _prepare_failure_worker(rank, world, total, port, q):
+    import torch.distributed as dist
+    from gp_mpc_rocket_landing_amd.sharding import gather_shard_records
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    first, count = shard_range(total, rank, world)
+    made = []
+
+    def factory(ctx, _fail_local=False):
+        made.append(_FakeGather(ctx))
+        return made[-1]
+    out, info = gather_shard_records(None, None, _records_for(first, count), total, _gather=factory)
+    q.put((rank, out, info, made[0].entered, made[0].closed))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_gather_prepare_failure_on_one_rank_is_agreed_world2_gloo():
+    """a failure in the local half of the gather (buffers, padding --
+    gpmpc_gather_prepare) on ONE rank is agreed before anyone enters the
+    collective: no rank calls it, both fall back to torch.distributed.gather
+    together, and the communicator is closed only after the agreement."""
+    total = 9
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_prepare_failure_worker, args=(r, 2, total, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict((r, rest) for r, *rest in (q.get(timeout=120) for _ in range(2)))
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    (out0, info0, ent0, cl0), (out1, info1, ent1, cl1) = res[0], res[1]
+    np.testing.assert_array_equal(out0, _records_for(0, total))
+    assert out1 is None
+    assert not ent0 and not ent1 and cl0 and cl1
+    for info in (info0, info1):
+        assert info["path"] == "torch" and info["nranks"] == 2
+        assert info["fallback"].startswith("gather prepare failed on 1 of 2 ranks"), info
+    assert "injected" in info1["fallback"] and "injected" not in info0["fallback"]
