@@ -750,8 +750,8 @@ def main():
     t0 = time.perf_counter()
     for k in range(K):
         e = ev[k]
-        e[0].record(stream); fl.phases(1)   # features + K* gram
-        e[1].record(stream); fl.phases(4)   # variance + mean GEMM (MFMA, one pass over K*)
+        e[0].record(stream); fl.phases(1)   # query features (+ the K* gram on the GPMPC_POST_CS=0 path)
+        e[1].record(stream); fl.phases(4)   # posterior: variance + mean in one MFMA pass
         e[2].record(stream); fl.phases(8)   # posterior finish
         e[3].record(stream); fl.phases(2)   # QP assembly + ADMM + plant
         e[4].record(stream)
@@ -794,6 +794,11 @@ def main():
         it_f, fac_f = admm_flops()
         steps_rank0 = steps_done / K
         admm_flop = (admm_iters / K) * it_f + steps_rank0 * 1.5 * fac_f
+        # default posterior (GPMPC_POST_CS, n <= 1008): the column-stationary kernel forms K*
+        # inside its MFMA pass (post.hip), so phase 1 is only the query features; the
+        # K* exponentials (P n, ~26 flop each) are extra work not counted in var_flops
+        cs = os.environ.get("GPMPC_POST_CS", "1") != "0" and n <= 1008
+        q_bytes = 8.0 * B * ((args.horizon + 1) * 7 + args.horizon * 3) + 8.0 * P * 12
         kern = {
             "gram_Kstar": dict(kernel="k_gram_rows<11, 0>", ms=ph_mean[0] * 1e3, bound="hbm",
                                achieved=gram_bytes / ph_mean[0] / 1e9, peak=HBM_PEAK_GBS, unit="GB/s"),
@@ -807,6 +812,15 @@ def main():
                                   achieved=admm_flop / ph_mean[3] / 1e12, peak=FP64_PEAK_TFLOPS,
                                   unit="TFLOP/s"),
         }
+        if cs:
+            kern.pop("gram_Kstar")
+            kern.pop("var_mean_gemm_mfma")
+            kern = {"query_features": dict(kernel="k_fleet_queries", ms=ph_mean[0] * 1e3, bound="hbm",
+                                           achieved=q_bytes / ph_mean[0] / 1e9, peak=HBM_PEAK_GBS, unit="GB/s"),
+                    "posterior_mfma": dict(kernel="k_post_cs<11>", ms=ph_mean[1] * 1e3, bound="mfma",
+                                           achieved=var_flops / ph_mean[1] / 1e12, peak=FP64_PEAK_TFLOPS,
+                                           unit="TFLOP/s"),
+                    **kern}
         if os.environ.get("GPMPC_FLEET_FUSE_POST", "1") != "0":
             # the posterior finish runs inside the control kernel (each landing
             # finishes its own 20 queries while it assembles its QP)
@@ -828,6 +842,9 @@ def main():
                     per_launch={"qp_admm_plant": "ADMM iterations x block-KKT iteration flops + "
                                                  "factorisations (admm_flops)",
                                 "var_mean_gemm_mfma": "n^2 P + 6 n P flop",
+                                "posterior_mfma": "n^2 P + 6 n P flop (W K*^T, lower-triangular W, "
+                                                  "and alpha^T K*^T; K* formed in the pass, not counted)",
+                                "query_features": "8 B ((N+1) 7 + 3 N) + 96 P bytes",
                                 "gram_Kstar": "8 n P + 8 d (P+n) bytes",
                                 "post_finish": "8 P (row tiles + 9) bytes"}[dom],
                     traffic_source=pmc_traffic(d["kernel"])[1], launches_per_step=1)

@@ -107,6 +107,10 @@ _sig("gpmpc_trsm_lower", _c, _vp, _c, _c, _dp, _c, _dp, _c)
 _sig("gpmpc_potrs", _c, _vp, _c, _c, _dp, _c, _dp, _c)
 _sig("gpmpc_gp_fit_exact", _c, _vp, _c, _dp, _c, _c, _dp, _c, _dp, ctypes.c_double,
      ctypes.c_double, ctypes.POINTER(_vp), _dp, _dp, _dp, _ip)
+_sig("gpmpc_gp_fit_exact_prog", _c, _vp, _ip, _c, _dp, _c, _dp, _c, _c, _dp, _c, ctypes.c_double,
+     ctypes.POINTER(_vp), _dp, _dp, _dp, _ip)
+_sig("gpmpc_sparse_fit_prog", _c, _vp, _c, _ip, _c, _dp, _c, _dp, _c, _dp, _c, _c, _dp, _c, ctypes.c_double,
+     ctypes.c_double, ctypes.POINTER(_vp), _dp, _dp, _dp, _dp)
 _sig("gpmpc_gp_predict", _c, _vp, _vp, _dp, _c, _dp, _dp)
 _sig("gpmpc_gp_predict_cov", _c, _vp, _vp, _dp, _c, _dp, _dp)
 _sig("gpmpc_gp_get_state", _c, _vp, _vp, _dp, _dp)
@@ -165,7 +169,7 @@ _sig("gpmpc_rollout6_destroy", _c, _vp)
 EXPORTED = ["gpmpc_abi_version", "gpmpc_last_error", "gpmpc_ctx_create", "gpmpc_ctx_destroy",
             "gpmpc_ctx_sync", "gpmpc_ctx_stream", "gpmpc_gram", "gpmpc_gram_grad", "gpmpc_potrf",
             "gpmpc_potrf_batched_dev", "gpmpc_trsm_lower", "gpmpc_potrs", "gpmpc_gp_fit_exact",
-            "gpmpc_gp_predict", "gpmpc_gp_predict_cov", "gpmpc_gp_get_state", "gpmpc_gp_destroy",
+            "gpmpc_gp_predict", "gpmpc_gp_predict_cov", "gpmpc_gp_fit_exact_prog", "gpmpc_sparse_fit_prog", "gpmpc_gp_get_state", "gpmpc_gp_destroy",
             "gpmpc_gp_lml_batched", "gpmpc_gp_append",
             "gpmpc_fitc_fit", "gpmpc_fitc_predict", "gpmpc_fitc_destroy",
             "gpmpc_qp_default_settings", "gpmpc_qp_solve_batched", "gpmpc_fleet_default_config",
@@ -326,24 +330,51 @@ def gp_lml_batched(ctx, kind, X, y, ls, sigma2, noise):
     return lml, steps
 
 
+KP_WHITE, KP_SUM, KP_PROD = 4, 10, 11   # gpmpc.h GPMPC_KP_*
+
+
+class KernelProgram:
+    """A composite kernel (SumKernel / ProductKernel / WhiteNoise over the stationary
+    kernels, kernels.py:676-844) as the device's postfix program: ``ops`` (code,
+    parameter offset) pairs and ``par`` (gpmpc.h GPMPC_KP_*).  Passed as ``kind`` to
+    ExactGPHandle / FITCHandle, which then ignore ``ls`` / ``sigma2``."""
+
+    def __init__(self, ops, par):
+        self.ops = np.ascontiguousarray(np.asarray(ops, np.int32).reshape(-1, 2))
+        self.par = f64(np.asarray(par, float).reshape(-1))
+
+    def __eq__(self, other):
+        return (isinstance(other, KernelProgram) and np.array_equal(self.ops, other.ops)
+                and np.array_equal(self.par, other.par))
+
+    def __repr__(self):
+        return f"KernelProgram(ops={self.ops.tolist()}, par={self.par.tolist()})"
+
+
 class ExactGPHandle:
-    """Device-resident exact GP (shared factor across outputs)."""
+    """Device-resident exact GP (shared factor across outputs).  ``kind``: one of the
+    four kernel kinds, or a KernelProgram (a composite kernel)."""
 
     def __init__(self, ctx, kind, X, Y, ls, sigma2, noise):
         X = f64(np.atleast_2d(X)); Y = f64(Y)
         if Y.ndim == 1:
             Y = Y[:, None]
         n, d = X.shape; no = Y.shape[1]
-        ls = f64(np.atleast_1d(ls))
-        if ls.size == 1 and kind != SE_ISO:
-            ls = np.full(d, float(ls[0]))
         self.ctx = ctx; self.n = n; self.d = d; self.n_out = no
         self.y_mean = np.empty(no); self.y_std = np.empty(no); self.lml = np.empty(no)
         js = np.zeros(1, np.int32)
         h = _vp()
-        rc = _L.gpmpc_gp_fit_exact(ctx.h, kind, _d(X), n, d, _d(Y), no, _d(ls), float(sigma2),
-                                   float(noise), ctypes.byref(h), _d(self.y_mean), _d(self.y_std),
-                                   _d(self.lml), _i(js))
+        if isinstance(kind, KernelProgram):
+            rc = _L.gpmpc_gp_fit_exact_prog(ctx.h, _i(kind.ops), kind.ops.shape[0], _d(kind.par), kind.par.size,
+                                            _d(X), n, d, _d(Y), no, float(noise), ctypes.byref(h),
+                                            _d(self.y_mean), _d(self.y_std), _d(self.lml), _i(js))
+        else:
+            ls = f64(np.atleast_1d(ls))
+            if ls.size == 1 and kind != SE_ISO:
+                ls = np.full(d, float(ls[0]))
+            rc = _L.gpmpc_gp_fit_exact(ctx.h, kind, _d(X), n, d, _d(Y), no, _d(ls), float(sigma2),
+                                       float(noise), ctypes.byref(h), _d(self.y_mean), _d(self.y_std),
+                                       _d(self.lml), _i(js))
         if rc == ERR_NOT_PD:
             raise ValueError("Kernel matrix is not positive definite even with jitter")
         _chk(rc, "gp_fit_exact")
@@ -403,13 +434,23 @@ class FITCHandle:
         if Y.ndim == 1:
             Y = Y[:, None]
         m, d = Z.shape; n = X.shape[0]; no = Y.shape[1]
-        ls = f64(np.atleast_1d(ls))
-        if ls.size == 1:
-            ls = np.full(d, float(ls[0]))
         self.ctx = ctx; self.n_out = no; self.m = m
         self.y_mean = np.empty(no); self.y_std = np.empty(no); self.lml = np.empty(no)
         h = _vp()
-        if method == "vfe":
+        prog = ls if isinstance(ls, KernelProgram) else None
+        if prog is None:
+            ls = f64(np.atleast_1d(ls))
+            if ls.size == 1:
+                ls = np.full(d, float(ls[0]))
+        if prog is not None and method in ("fitc", "vfe"):
+            # a composite kernel (``ls`` is its KernelProgram): gpmpc_sparse_fit_prog
+            self.lam = np.empty(n) if method == "fitc" else None
+            rc = _L.gpmpc_sparse_fit_prog(ctx.h, 0 if method == "fitc" else 1, _i(prog.ops), prog.ops.shape[0],
+                                          _d(prog.par), prog.par.size, _d(Z), m, _d(X), n, d, _d(Y), no,
+                                          float(noise), float(jitter), ctypes.byref(h), _d(self.y_mean),
+                                          _d(self.y_std), _d(self.lml),
+                                          _d(self.lam) if self.lam is not None else None)
+        elif method == "vfe":
             self.lam = None
             rc = _L.gpmpc_vfe_fit(ctx.h, _d(Z), m, _d(X), n, d, _d(Y), no, _d(ls), float(sigma2),
                                   float(noise), float(jitter), ctypes.byref(h), _d(self.y_mean),

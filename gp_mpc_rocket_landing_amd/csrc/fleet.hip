@@ -22,6 +22,7 @@
 #include "qp.h"
 #include "fleet_qp.h"
 #include <vector>
+#include <algorithm>
 
 #define NX 7
 #define NU 3
@@ -787,6 +788,10 @@ extern "C" int gpmpc_fleet_create(gpmpc_ctx *ctx, gpmpc_gp *gp, const gpmpc_flee
   GPMPC_CHECK_ARG(ctx && gp && cfg && out && batch > 0);
   const GpView g = gp_view(gp);
   GPMPC_CHECK_ARG(g.d == NFEAT && g.n_out == 3);
+  if (g.kind < GPMPC_SE_ARD || g.kind > GPMPC_MATERN52) {
+    gpmpc_set_error("fleet: the GP must use one of the four stationary kernels (not a composite program)");
+    return -2;
+  }
   // the fleet runs MonteCarloSimulator's solve protocol (monte_carlo.py:495-512)
   // with the GPMPC adapter; FastRTI3DoF's step protocol (unshifted linearisation,
   // D2 sign, fallback to the shifted plan) is the host mirror mpc/osqp_rti.py
@@ -832,7 +837,8 @@ extern "C" int gpmpc_fleet_create(gpmpc_ctx *ctx, gpmpc_gp *gp, const gpmpc_flee
     return -1;
   }
   const size_t B = batch, P = (size_t)batch * N;
-  const int nrt = gemm_row_tiles(g.n + 3, (int)P, g.n);  // W rows + the 3 alpha^T rows
+  // W rows + the 3 alpha^T rows; at least the column-stationary posterior's two halves
+  const int nrt = std::max(gemm_row_tiles(g.n + 3, (int)P, g.n), POST_CS_PARTS);
   if (f->x.alloc(sizeof(double) * B * NX) || f->Xw.alloc(sizeof(double) * B * (N + 1) * NX) ||
       f->Uw.alloc(sizeof(double) * B * N * NU) || f->ysc.alloc(sizeof(double) * B * m) ||
       f->rho.alloc(sizeof(double) * B) || f->rec.alloc(sizeof(double) * B * GPMPC_REC_LEN) ||
@@ -916,22 +922,28 @@ static hipError_t fleet_gp_posterior(gpmpc_fleet *f, int mask) {
     const char *v = getenv("GPMPC_POST_FUSED");
     return v ? atoi(v) : 0;
   }();
-  const bool fused = fused_env && g.d >= 11 && g.d <= 13;
-  const int nrt = fused ? (g.n + 3 + 127) / 128 : gemm_row_tiles(g.n + 3, (int)P, g.n);
+  // default: the column-stationary posterior (post.hip), K* formed once per workgroup
+  // inside the MFMA pass, never in HBM; two partial rows
+  const bool cs = g.Wf && post_cs_env();
+  const bool fused = !cs && fused_env && g.d >= 11 && g.d <= 13;
+  const int nrt = cs ? POST_CS_PARTS : fused ? (g.n + 3 + 127) / 128 : gemm_row_tiles(g.n + 3, (int)P, g.n);
   hipError_t e = hipSuccess;
   if (mask & 1) {
     hipLaunchKernelGGL(k_fleet_queries, dim3((P + 255) / 256), dim3(256), 0, s, nb, f->N,
                        f->Xw.as<double>(), f->Uw.as<double>(), g.ls, g.kind == GPMPC_SE_ISO,
                        f->use_order ? f->order.as<int>() : nullptr, f->Q.as<double>(),
                        f->Qn.as<double>());
-    if (!fused) {
+    if (!fused && !cs) {
       e = launch_gram(s, g.kind, f->Q.as<double>(), f->Qn.as<double>(), P, g.Xs, g.Xn, g.n, g.d,
                       g.sigma2, g.iso_scale, f->Ks.as<double>(), g.n, 0);
       if (e != hipSuccess) return e;
     }
   }
   if (mask & 4) {
-    if (fused)
+    if (cs)
+      e = launch_post_cs(s, g.n, 3, P, g.Wf, g.Xp, f->Q.as<double>(), f->Qn.as<double>(), g.d, g.kind, g.sigma2,
+                         g.iso_scale, f->part.as<double>(), P, f->meanT.as<double>(), P);
+    else if (fused)
       e = launch_gemm_post_fused(s, g.n, 3, P, g.W, f->Q.as<double>(), f->Qn.as<double>(), g.Xs,
                                  g.Xn, g.d, g.kind, g.sigma2, g.iso_scale, f->part.as<double>(), P,
                                  f->meanT.as<double>(), P);

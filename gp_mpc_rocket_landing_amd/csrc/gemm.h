@@ -79,6 +79,23 @@ hipError_t launch_gemm_post_fused(hipStream_t s, int n, int n_out, int P, const 
                                   double iso_scale, double *part, int64_t ldp, double *meanT,
                                   int64_t ldm);
 
+// the column-stationary posterior (post.hip): exact GPs with n <= 1008 (63 row blocks of
+// 16 + the alpha block), n_out <= 16, d in 11..13.  launch_post_pack forms its operands
+// (Wf: post_cs_frag_doubles(n) doubles; Xp: n x post_cs_row_pitch(d)) from [W; alpha^T]
+// (ld ldw), Xs, Xn; launch_post_cs forms K* from the scaled queries Qs (P x d) / Qn on the
+// fly and writes part (2 rows, ld ldp: the two row halves' sums of squares) and meanT.
+bool post_cs_ok(int n, int n_out, int d);
+int post_cs_blocks(int n);
+size_t post_cs_frag_doubles(int n);
+int post_cs_row_pitch(int d);
+hipError_t launch_post_pack(hipStream_t s, int n, int n_out, const double *Wext, int64_t ldw,
+                            const double *Xs, const double *Xn, int d, double *Wf, double *Xp);
+hipError_t launch_post_cs(hipStream_t s, int n, int n_out, int P, const double *Wf, const double *Xp,
+                          const double *Qs, const double *Qn, int d, int kind, double sigma2, double iso_scale,
+                          double *part, int64_t ldp, double *meanT, int64_t ldm);
+#define POST_CS_PARTS 2
+bool post_cs_env();  // GPMPC_POST_CS (default 1)
+
 // rows of the SUMSQ partial buffer for an M x N x K product (tile height of
 // the kernel launch_gemm_* picks: 128 when M, N and K >= 256, else 64)
 inline int gemm_row_tiles(int M, int N = 0, int K = 0) {

@@ -24,6 +24,21 @@ struct GpCore {
   DevBuf alphaT;       // n_out x n
   DevBuf ymean, ystd;  // n_out
   std::vector<double> h_ymean, h_ystd;
+  // the column-stationary posterior's operands (post.hip, exact GPs with n <= 1008):
+  // [W; alpha^T] in packed MFMA-fragment order and the scaled rows padded with their norms
+  DevBuf Wf, Xp;
+  // composite kernel (kind == GPMPC_KPROG): the postfix program (gpmpc.h GPMPC_KP_*);
+  // Xs then holds the raw rows, Xn zeros, and sigma2 the program's diagonal constant
+  DevBuf ops, par;
+  int nops = 0;
+};
+
+// a composite kernel program as the entry points receive it (host arrays)
+struct KProgArg {
+  const int *ops;
+  int nops;
+  const double *par;
+  int npar;
 };
 
 struct gpmpc_gp {
@@ -191,12 +206,32 @@ __global__ __launch_bounds__(256) void k_lml_fitc(int m, int n, int n_out, const
 }
 
 static int core_setup(gpmpc_ctx *ctx, GpCore &g, int kind, const double *X, int n, int d,
-                      const double *ls, double sigma2) {
+                      const double *ls, double sigma2, const KProgArg *prog = nullptr) {
   hipStream_t s = ctx->stream;
-  g.kind = kind;
+  g.kind = prog ? GPMPC_KPROG : kind;
   g.n = n;
   g.d = d;
   g.sigma2 = sigma2;
+  if (prog) {
+    double diag = 0.0;
+    if (kprog_check(prog->ops, prog->nops, prog->npar, d, prog->par, &diag)) {
+      gpmpc_set_error("composite kernel program is malformed (codes, offsets, stack, parameters)");
+      return -2;
+    }
+    g.sigma2 = diag;  // k(x, x) of the program: the posterior's and FITC's prior variance
+    g.iso_scale = 0.0;
+    g.nops = prog->nops;
+    GPMPC_HIP(g.ops.alloc(s, sizeof(int) * 2 * prog->nops));
+    GPMPC_HIP(g.par.alloc(s, sizeof(double) * prog->npar));
+    GPMPC_HIP(g.Xs.alloc(s, sizeof(double) * n * d));
+    GPMPC_HIP(g.Xn.alloc(s, sizeof(double) * n));
+    GPMPC_HIP(hipMemcpyAsync(g.ops.p, prog->ops, sizeof(int) * 2 * prog->nops, hipMemcpyHostToDevice, s));
+    GPMPC_HIP(hipMemcpyAsync(g.par.p, prog->par, sizeof(double) * prog->npar, hipMemcpyHostToDevice, s));
+    GPMPC_HIP(hipMemcpyAsync(g.Xs.p, X, sizeof(double) * n * d, hipMemcpyHostToDevice, s));
+    GPMPC_HIP(hipMemsetAsync(g.Xn.p, 0, sizeof(double) * n, s));
+    GPMPC_HIP(hipStreamSynchronize(s));
+    return 0;
+  }
   const int iso = (kind == GPMPC_SE_ISO);
   g.iso_scale = iso ? 1.0 / (2.0 * ls[0] * ls[0]) : 0.0;
   DevBuf dX;
@@ -213,6 +248,50 @@ static int core_setup(gpmpc_ctx *ctx, GpCore &g, int kind, const double *X, int 
   return 0;
 }
 
+// the core's form of device rows (p x d, raw in) for its Grams: scaled by the lengthscales
+// with squared norms, or raw (norms zero) for a composite program
+static hipError_t core_rows(hipStream_t s, const GpCore &g, const double *Xraw, int p, double *A, double *NA) {
+  if (g.kind == GPMPC_KPROG) {
+    hipError_t e = hipMemcpyAsync(A, Xraw, sizeof(double) * p * g.d, hipMemcpyDeviceToDevice, s);
+    return e == hipSuccess ? hipMemsetAsync(NA, 0, sizeof(double) * p, s) : e;
+  }
+  return launch_scale_rows(s, Xraw, p, g.d, g.ls.as<double>(), g.kind == GPMPC_SE_ISO, A, NA);
+}
+
+// K (n1 x n2, ldk) between core-form rows; same = 1: one row set (B ignored for a program,
+// whose WhiteNoise leaves then sit on the diagonal -- kernel(X) vs kernel(X1, X2))
+static hipError_t core_gram(hipStream_t s, const GpCore &g, const double *A, const double *NA, int n1,
+                            const double *B, const double *NB, int n2, int same, double *K, int64_t ldk) {
+  if (g.kind == GPMPC_KPROG)
+    return launch_gram_prog(s, g.ops.as<int>(), g.nops, g.par.as<double>(), A, n1, B, n2, g.d, same, K, ldk);
+  return launch_gram(s, g.kind, A, NA, n1, B, NB, n2, g.d, g.sigma2, g.iso_scale, K, ldk, 0);
+}
+
+// GPMPC_POST_CS=0: the posterior through K* in HBM (gram + 128-tile SUMSQ GEMM) instead
+bool post_cs_env() {
+  static const int v = [] {
+    const char *e = getenv("GPMPC_POST_CS");
+    return e ? atoi(e) : 1;
+  }();
+  return v != 0;
+}
+
+// Wf / Xp for the column-stationary posterior (post.hip) from the current [W; alpha^T],
+// Xs, Xn; released when the GP is outside the kernel's range
+static hipError_t core_pack(hipStream_t s, GpCore &g) {
+  if (g.kind == GPMPC_KPROG || !post_cs_ok(g.n, g.n_out, g.d)) {
+    g.Wf.release();
+    g.Xp.release();
+    return hipSuccess;
+  }
+  hipError_t e = g.Wf.alloc(s, sizeof(double) * post_cs_frag_doubles(g.n));
+  if (e == hipSuccess) e = g.Xp.alloc(s, sizeof(double) * (size_t)g.n * post_cs_row_pitch(g.d));
+  if (e == hipSuccess)
+    e = launch_post_pack(s, g.n, g.n_out, g.W.as<double>(), g.n, g.Xs.as<double>(), g.Xn.as<double>(), g.d,
+                         g.Wf.as<double>(), g.Xp.as<double>());
+  return e;
+}
+
 // K* = k(Xq, X_core) (p x n) on device from host queries; returns scaled queries too
 static int core_cross(gpmpc_ctx *ctx, const GpCore &g, const double *dXq_raw, int p, DevBuf &Ks,
                       DevBuf *qs = nullptr, DevBuf *qn = nullptr) {
@@ -222,12 +301,10 @@ static int core_cross(gpmpc_ctx *ctx, const GpCore &g, const double *dXq_raw, in
   DevBuf &NA = qn ? *qn : na;
   GPMPC_HIP(A.alloc(s, sizeof(double) * p * g.d));
   GPMPC_HIP(NA.alloc(s, sizeof(double) * p));
-  GPMPC_HIP(launch_scale_rows(s, dXq_raw, p, g.d, g.ls.as<double>(), g.kind == GPMPC_SE_ISO,
-                              A.as<double>(), NA.as<double>()));
+  GPMPC_HIP(core_rows(s, g, dXq_raw, p, A.as<double>(), NA.as<double>()));
   GPMPC_HIP(Ks.alloc(s, sizeof(double) * (size_t)p * g.n));
-  GPMPC_HIP(launch_gram(s, g.kind, A.as<double>(), NA.as<double>(), p, g.Xs.as<double>(),
-                        g.Xn.as<double>(), g.n, g.d, g.sigma2, g.iso_scale, Ks.as<double>(), g.n,
-                        0));
+  GPMPC_HIP(core_gram(s, g, A.as<double>(), NA.as<double>(), p, g.Xs.as<double>(), g.Xn.as<double>(), g.n, 0,
+                      Ks.as<double>(), g.n));
   return 0;
 }
 
@@ -450,18 +527,17 @@ static bool potrs_cols_ok(int n) {
   return env && attr && n <= POTRS_COLS_MAXN;
 }
 
-extern "C" int gpmpc_gp_fit_exact(gpmpc_ctx *ctx, int kind, const double *X, int n, int d,
-                                  const double *Y, int n_out, const double *ls, double sigma2,
-                                  double noise, gpmpc_gp **out, double *y_mean, double *y_std,
-                                  double *lml, int *jitter_steps) {
-  GPMPC_CHECK_ARG(ctx && X && Y && ls && out && n >= 1 && d >= 1 && d <= 32);
-  GPMPC_CHECK_ARG(n_out >= 1 && n_out <= 16 && kind >= 0 && kind <= 3);
+static int exact_fit(gpmpc_ctx *ctx, int kind, const double *X, int n, int d, const double *Y, int n_out,
+                     const double *ls, double sigma2, double noise, const KProgArg *prog, gpmpc_gp **out,
+                     double *y_mean, double *y_std, double *lml, int *jitter_steps) {
+  GPMPC_CHECK_ARG(ctx && X && Y && (ls || prog) && out && n >= 1 && d >= 1 && d <= 32);
+  GPMPC_CHECK_ARG(n_out >= 1 && n_out <= 16 && (prog || (kind >= 0 && kind <= 3)));
   GPMPC_HIP(hipSetDevice(ctx->device));
   hipStream_t s = ctx->stream;
   auto *gp = new gpmpc_gp();
   GpCore &g = gp->core;
   gp->noise = noise;
-  int rc = core_setup(ctx, g, kind, X, n, d, ls, sigma2);
+  int rc = core_setup(ctx, g, kind, X, n, d, ls, sigma2, prog);
   if (rc) { delete gp; return rc; }
   DevBuf Kn, dinfo;
   auto fail = [&](int code) { delete gp; return code; };
@@ -472,9 +548,8 @@ extern "C" int gpmpc_gp_fit_exact(gpmpc_ctx *ctx, int kind, const double *X, int
     return fail(-1);
   }
   // K + noise I   (exact_gp.py:156-160)
-  if (launch_gram(s, kind, g.Xs.as<double>(), g.Xn.as<double>(), n, g.Xs.as<double>(),
-                  g.Xn.as<double>(), n, d, sigma2, g.iso_scale, Kn.as<double>(), n, 0) !=
-          hipSuccess ||
+  if (core_gram(s, g, g.Xs.as<double>(), g.Xn.as<double>(), n, g.Xs.as<double>(), g.Xn.as<double>(), n, 1,
+                Kn.as<double>(), n) != hipSuccess ||
       launch_add_diag(s, n, Kn.as<double>(), n, noise, 1, 0) != hipSuccess) {
     gpmpc_set_error("gp_fit_exact: gram launch failed");
     return fail(-1);
@@ -565,6 +640,10 @@ extern "C" int gpmpc_gp_fit_exact(gpmpc_ctx *ctx, int kind, const double *X, int
   // alpha^T below W: the variance GEMM produces the posterior mean in the same pass
   hipMemcpyAsync(g.W.as<double>() + (size_t)n * n, g.alphaT.p, sizeof(double) * n_out * n,
                  hipMemcpyDeviceToDevice, s);
+  if (core_pack(s, g) != hipSuccess) {
+    gpmpc_set_error("gp_fit_exact: posterior operand pack failed");
+    return fail(-1);
+  }
   g.h_ymean.resize(n_out);
   g.h_ystd.resize(n_out);
   hipMemcpyAsync(g.h_ymean.data(), g.ymean.p, sizeof(double) * n_out, hipMemcpyDeviceToHost, s);
@@ -582,6 +661,25 @@ extern "C" int gpmpc_gp_fit_exact(gpmpc_ctx *ctx, int kind, const double *X, int
   }
   *out = gp;
   return 0;
+}
+
+extern "C" int gpmpc_gp_fit_exact(gpmpc_ctx *ctx, int kind, const double *X, int n, int d,
+                                  const double *Y, int n_out, const double *ls, double sigma2,
+                                  double noise, gpmpc_gp **out, double *y_mean, double *y_std,
+                                  double *lml, int *jitter_steps) {
+  GPMPC_CHECK_ARG(ls);
+  return exact_fit(ctx, kind, X, n, d, Y, n_out, ls, sigma2, noise, nullptr, out, y_mean, y_std, lml,
+                   jitter_steps);
+}
+
+extern "C" int gpmpc_gp_fit_exact_prog(gpmpc_ctx *ctx, const int *ops, int nops, const double *par, int npar,
+                                       const double *X, int n, int d, const double *Y, int n_out, double noise,
+                                       gpmpc_gp **out, double *y_mean, double *y_std, double *lml,
+                                       int *jitter_steps) {
+  GPMPC_CHECK_ARG(ops && par && nops >= 1 && npar >= 1);
+  const KProgArg prog{ops, nops, par, npar};
+  return exact_fit(ctx, GPMPC_KPROG, X, n, d, Y, n_out, nullptr, 0.0, noise, &prog, out, y_mean, y_std, lml,
+                   jitter_steps);
 }
 
 // device-side posterior for p queries given K* (p x n): mean/var (p x n_out) device
@@ -613,12 +711,29 @@ extern "C" int gpmpc_gp_predict(gpmpc_ctx *ctx, gpmpc_gp *gp, const double *Xq, 
   DevBuf dq, Ks, dmean, dvar;
   GPMPC_HIP(dq.alloc(s, sizeof(double) * p * g.d));
   GPMPC_HIP(hipMemcpyAsync(dq.p, Xq, sizeof(double) * p * g.d, hipMemcpyHostToDevice, s));
-  int rc = core_cross(ctx, g, dq.as<double>(), p, Ks);
-  if (rc) return rc;
   GPMPC_HIP(dmean.alloc(s, sizeof(double) * p * g.n_out));
   GPMPC_HIP(dvar.alloc(s, sizeof(double) * p * g.n_out));
-  rc = core_posterior(ctx, g, Ks.as<double>(), p, dmean.as<double>(), dvar.as<double>());
-  if (rc) return rc;
+  if (g.Wf.p && post_cs_env()) {
+    // K* formed inside the column-stationary posterior (post.hip): no K* in HBM
+    DevBuf qs, qn, part, meanT;
+    GPMPC_HIP(qs.alloc(s, sizeof(double) * p * g.d));
+    GPMPC_HIP(qn.alloc(s, sizeof(double) * p));
+    GPMPC_HIP(part.alloc(s, sizeof(double) * POST_CS_PARTS * p));
+    GPMPC_HIP(meanT.alloc(s, sizeof(double) * g.n_out * p));
+    GPMPC_HIP(launch_scale_rows(s, dq.as<double>(), p, g.d, g.ls.as<double>(), g.kind == GPMPC_SE_ISO,
+                                qs.as<double>(), qn.as<double>()));
+    GPMPC_HIP(launch_post_cs(s, g.n, g.n_out, p, g.Wf.as<double>(), g.Xp.as<double>(), qs.as<double>(),
+                             qn.as<double>(), g.d, g.kind, g.sigma2, g.iso_scale, part.as<double>(), p,
+                             meanT.as<double>(), p));
+    GPMPC_HIP(launch_post_finish(s, p, g.n_out, POST_CS_PARTS, part.as<double>(), p, meanT.as<double>(), p,
+                                 g.ymean.as<double>(), g.ystd.as<double>(), g.sigma2, dmean.as<double>(),
+                                 dvar.as<double>()));
+  } else {
+    int rc = core_cross(ctx, g, dq.as<double>(), p, Ks);
+    if (rc) return rc;
+    rc = core_posterior(ctx, g, Ks.as<double>(), p, dmean.as<double>(), dvar.as<double>());
+    if (rc) return rc;
+  }
   GPMPC_HIP(hipMemcpyAsync(mean, dmean.p, sizeof(double) * p * g.n_out, hipMemcpyDeviceToHost, s));
   GPMPC_HIP(hipMemcpyAsync(var, dvar.p, sizeof(double) * p * g.n_out, hipMemcpyDeviceToHost, s));
   GPMPC_HIP(hipStreamSynchronize(s));
@@ -643,8 +758,8 @@ extern "C" int gpmpc_gp_predict_cov(gpmpc_ctx *ctx, gpmpc_gp *gp, const double *
                            V.as<double>(), g.n, 1.0, 0.0, 0, 0, 1, 0, 0, 0));
   // C = K** - V^T V   (exact_gp.py:250-252), in normalised units
   GPMPC_HIP(C.alloc(s, sizeof(double) * (size_t)p * p));
-  GPMPC_HIP(launch_gram(s, g.kind, qs.as<double>(), qn.as<double>(), p, qs.as<double>(),
-                        qn.as<double>(), p, g.d, g.sigma2, g.iso_scale, C.as<double>(), p, 0));
+  GPMPC_HIP(core_gram(s, g, qs.as<double>(), qn.as<double>(), p, qs.as<double>(), qn.as<double>(), p, 1,
+                      C.as<double>(), p));
   GPMPC_HIP(launch_gemm_nt(s, EPI_STORE, p, p, g.n, V.as<double>(), g.n, V.as<double>(), g.n,
                            C.as<double>(), p, -1.0, 1.0, 0, 0, 1, 0, 0, 0));
   GPMPC_HIP(dmean.alloc(s, sizeof(double) * p * g.n_out));
@@ -706,14 +821,14 @@ GpView gp_view(const gpmpc_gp *gp) {
   const GpCore &g = gp->core;
   return GpView{g.kind, g.n, g.d, g.n_out, g.sigma2, g.iso_scale, g.ls.as<double>(),
                 g.Xs.as<double>(), g.Xn.as<double>(), g.W.as<double>(), g.alphaT.as<double>(),
-                g.ymean.as<double>(), g.ystd.as<double>()};
+                g.ymean.as<double>(), g.ystd.as<double>(), g.Wf.as<double>(), g.Xp.as<double>()};
 }
 
 GpView fitc_view(const gpmpc_fitc *gp) {
   const GpCore &g = gp->core;
   return GpView{g.kind, g.n, g.d, g.n_out, g.sigma2, g.iso_scale, g.ls.as<double>(),
                 g.Xs.as<double>(), g.Xn.as<double>(), g.W.as<double>(), g.alphaT.as<double>(),
-                g.ymean.as<double>(), g.ystd.as<double>()};
+                g.ymean.as<double>(), g.ystd.as<double>(), nullptr, nullptr};
 }
 
 // ---------------------------------------------------------------------------
@@ -796,8 +911,8 @@ static int vfe_tail(gpmpc_ctx *ctx, gpmpc_fitc *gp, DevBuf &Luu, DevBuf &Kuf, De
   g.n_out = n_out;
   // K_uu into B (kept for alpha^T K_uu alpha), then B += K_uf K_fu / s2n (SYRK on
   // MFMA, lower triangle), then + jitter I in the reference's order
-  launch_gram(s, GPMPC_SE_ARD, g.Xs.as<double>(), g.Xn.as<double>(), m, g.Xs.as<double>(),
-              g.Xn.as<double>(), m, g.d, sigma2, 0.0, B.as<double>(), m, 0);
+  core_gram(s, g, g.Xs.as<double>(), g.Xn.as<double>(), m, g.Xs.as<double>(), g.Xn.as<double>(), m, 1,
+            B.as<double>(), m);
   hipMemcpyAsync(Kuu.p, B.p, sizeof(double) * (size_t)m * m, hipMemcpyDeviceToDevice, s);
   launch_gemm_nt(s, EPI_STORE, m, m, n, Kuf.as<double>(), n, Kuf.as<double>(), n, B.as<double>(), m,
                  1.0 / noise, 1.0, 0, 1, 1, 0, 0, 0);
@@ -863,8 +978,8 @@ static int vfe_tail(gpmpc_ctx *ctx, gpmpc_fitc *gp, DevBuf &Luu, DevBuf &Kuf, De
 static int sparse_fit(gpmpc_ctx *ctx, const double *Z, int m, const double *X, int n, int d,
                       const double *Y, int n_out, const double *ls, double sigma2, double noise,
                       double jitter, gpmpc_fitc **out, double *y_mean, double *y_std, double *lml,
-                      double *lambda_diag, int vfe) {
-  GPMPC_CHECK_ARG(ctx && Z && X && Y && ls && out && m >= 1 && n >= 1 && d >= 1 && d <= 32);
+                      double *lambda_diag, int vfe, const KProgArg *prog = nullptr) {
+  GPMPC_CHECK_ARG(ctx && Z && X && Y && (ls || prog) && out && m >= 1 && n >= 1 && d >= 1 && d <= 32);
   GPMPC_CHECK_ARG(n_out >= 1 && n_out <= 16);
   GPMPC_CHECK_ARG(!vfe || noise > 0.0);
   GPMPC_HIP(hipSetDevice(ctx->device));
@@ -872,8 +987,9 @@ static int sparse_fit(gpmpc_ctx *ctx, const double *Z, int m, const double *X, i
   auto *gp = new gpmpc_fitc();
   GpCore &g = gp->core;
   gp->m = m;
-  int rc = core_setup(ctx, g, GPMPC_SE_ARD, Z, m, d, ls, sigma2);
+  int rc = core_setup(ctx, g, GPMPC_SE_ARD, Z, m, d, ls, sigma2, prog);
   if (rc) { delete gp; return rc; }
+  sigma2 = g.sigma2;  // a program's diagonal: kernel.diagonal(X) in Lambda and the VFE trace
   auto fail = [&](int code) { delete gp; return code; };
   DevBuf dX, Kuf, Luu, B, dinfo, lam, Xs, Xn, part;
   if (dX.alloc(s, sizeof(double) * n * d) || Kuf.alloc(s, sizeof(double) * (size_t)m * n) ||
@@ -886,11 +1002,10 @@ static int sparse_fit(gpmpc_ctx *ctx, const double *Z, int m, const double *X, i
     return fail(-1);
   }
   hipMemcpyAsync(dX.p, X, sizeof(double) * n * d, hipMemcpyHostToDevice, s);
-  launch_scale_rows(s, dX.as<double>(), n, d, g.ls.as<double>(), 0, Xs.as<double>(),
-                    Xn.as<double>());
+  core_rows(s, g, dX.as<double>(), n, Xs.as<double>(), Xn.as<double>());
   // K_uu + jitter I -> L_uu   (sparse_gp.py:181-187; no jitter ladder in the reference)
-  launch_gram(s, GPMPC_SE_ARD, g.Xs.as<double>(), g.Xn.as<double>(), m, g.Xs.as<double>(),
-              g.Xn.as<double>(), m, d, sigma2, 0.0, Luu.as<double>(), m, 0);
+  core_gram(s, g, g.Xs.as<double>(), g.Xn.as<double>(), m, g.Xs.as<double>(), g.Xn.as<double>(), m, 1,
+            Luu.as<double>(), m);
   launch_add_diag(s, m, Luu.as<double>(), m, jitter, 1, 0);
   int info = 0;
   launch_potrf_batched(s, m, 1, Luu.as<double>(), m, 0, dinfo.as<int>());
@@ -898,8 +1013,8 @@ static int sparse_fit(gpmpc_ctx *ctx, const double *Z, int m, const double *X, i
   GPMPC_HIP(hipStreamSynchronize(s));
   if (info) return fail(gpmpc_potrf_info_error(info, "K_uu"));
   // A = L_uu^-1 K_uf  (m x n); VFE forms B and c from K_uf itself first
-  launch_gram(s, GPMPC_SE_ARD, g.Xs.as<double>(), g.Xn.as<double>(), m, Xs.as<double>(),
-              Xn.as<double>(), n, d, sigma2, 0.0, Kuf.as<double>(), n, 0);
+  core_gram(s, g, g.Xs.as<double>(), g.Xn.as<double>(), m, Xs.as<double>(), Xn.as<double>(), n, 0,
+            Kuf.as<double>(), n);
   hipLaunchKernelGGL(k_eye, dim3((m + 255) / 256, m), dim3(256), 0, s, m, g.W.as<double>());
   {
     DevBuf tinv;  // W = L_uu^-1 by the doubling inverse (exact fit's W, §10)
@@ -1000,6 +1115,16 @@ extern "C" int gpmpc_vfe_fit(gpmpc_ctx *ctx, const double *Z, int m, const doubl
                              double *y_std, double *lml) {
   return sparse_fit(ctx, Z, m, X, n, d, Y, n_out, ls, sigma2, noise, jitter, out, y_mean, y_std,
                     lml, nullptr, 1);
+}
+
+extern "C" int gpmpc_sparse_fit_prog(gpmpc_ctx *ctx, int method, const int *ops, int nops, const double *par,
+                                     int npar, const double *Z, int m, const double *X, int n, int d,
+                                     const double *Y, int n_out, double noise, double jitter, gpmpc_fitc **out,
+                                     double *y_mean, double *y_std, double *lml, double *lambda_diag) {
+  GPMPC_CHECK_ARG(ops && par && nops >= 1 && npar >= 1 && (method == 0 || method == 1));
+  const KProgArg prog{ops, nops, par, npar};
+  return sparse_fit(ctx, Z, m, X, n, d, Y, n_out, nullptr, 0.0, noise, jitter, out, y_mean, y_std, lml,
+                    method == 0 ? lambda_diag : nullptr, method, &prog);
 }
 
 extern "C" int gpmpc_fitc_predict(gpmpc_ctx *ctx, gpmpc_fitc *gp, const double *Xq, int p,
@@ -1235,6 +1360,10 @@ extern "C" int gpmpc_gp_append(gpmpc_ctx *ctx, gpmpc_gp *gp, const double *Xnew,
     gpmpc_set_error("gp_append: the GP was fitted with jitter; refit the concatenated data");
     return GPMPC_ERR_NOT_PD;
   }
+  if (g.kind == GPMPC_KPROG) {
+    gpmpc_set_error("gp_append: composite-kernel GP; refit the concatenated data");
+    return GPMPC_ERR_NOT_PD;
+  }
   const int n = g.n, m = n + k, d = g.d, no = g.n_out;
   // temporaries carved from persistent scratch (slot 4): a per-call hipMalloc /
   // hipFree of each cost more than the O(n^2 k) arithmetic
@@ -1336,6 +1465,12 @@ extern "C" int gpmpc_gp_append(gpmpc_ctx *ctx, gpmpc_gp *gp, const double *Xnew,
   g.Xs.swap(Xs2);
   g.Xn.swap(Xn2);
   g.n = m;
+  if (core_pack(s, g) != hipSuccess) {  // the handle is committed: predicts take the K* path
+    (void)hipGetLastError();
+    g.Wf.release();
+    g.Xp.release();
+  }
+  GPMPC_HIP(hipStreamSynchronize(s));
   // the replaced buffers go back to the pool when this returns; another context's
   // stream may still be reading them (as gpmpc_gp_destroy)
   (void)hipDeviceSynchronize();

@@ -309,3 +309,88 @@ extern "C" int gpmpc_gram_grad(gpmpc_ctx *ctx, int kind, const double *X1, int n
   GPMPC_HIP(hipStreamSynchronize(s));
   return 0;
 }
+
+// ---------------------------------------------------------------------------
+// Composite kernels (kernels.py:676-844: SumKernel, ProductKernel, WhiteNoise over the
+// stationary kernels) as a postfix program of (code, parameter offset) pairs:
+//   GPMPC_SE_ARD / _MATERN32 / _MATERN52: par[off] = sigma2, par[off + 1 ..] = the d
+//     lengthscales (expansion-form distance of the scaled rows, clamped at 0, as k_gram)
+//   GPMPC_SE_ISO: par[off] = sigma2, par[off + 1] = l (distance of the raw rows)
+//   GPMPC_KP_WHITE: par[off] = sigma2 on the diagonal of a Gram of one row set (X2 None
+//     in the reference), zero between two sets
+//   GPMPC_KP_SUM / GPMPC_KP_PROD: the two values on top of the stack
+// Rows are raw.  One thread per entry: the composite Grams are fit/predict-time work.
+__device__ double kprog_leaf(int code, const double *__restrict__ p, const double *__restrict__ a,
+                             const double *__restrict__ b, int d, bool diag_entry) {
+  if (code == GPMPC_KP_WHITE) return diag_entry ? p[0] : 0.0;
+  double na = 0.0, nb = 0.0, dot = 0.0;
+  if (code == GPMPC_SE_ISO) {
+    for (int i = 0; i < d; ++i) {
+      na = fma(a[i], a[i], na);
+      nb = fma(b[i], b[i], nb);
+      dot = fma(a[i], b[i], dot);
+    }
+    const double l = p[1];
+    return kernel_epilogue(GPMPC_SE_ISO, (na + nb) - 2.0 * dot, p[0], 1.0 / (2.0 * l * l));
+  }
+  for (int i = 0; i < d; ++i) {
+    const double x = a[i] / p[1 + i], y = b[i] / p[1 + i];
+    na = fma(x, x, na);
+    nb = fma(y, y, nb);
+    dot = fma(x, y, dot);
+  }
+  return kernel_epilogue(code, (na + nb) - 2.0 * dot, p[0], 0.0);
+}
+
+__global__ void k_gram_prog(const int *__restrict__ ops, int nops, const double *__restrict__ par,
+                            const double *__restrict__ X1, int n1, const double *__restrict__ X2, int n2, int d,
+                            int same, double *__restrict__ K, int64_t ldk) {
+  const int col = blockIdx.x * blockDim.x + threadIdx.x, row = blockIdx.y;
+  if (col >= n2 || row >= n1) return;
+  const double *a = X1 + (int64_t)row * d, *b = X2 + (int64_t)col * d;
+  double st[GPMPC_KP_MAXSTACK];
+  int sp = 0;
+  for (int o = 0; o < nops; ++o) {
+    const int code = ops[2 * o], off = ops[2 * o + 1];
+    if (code == GPMPC_KP_SUM) { st[sp - 2] = st[sp - 2] + st[sp - 1]; --sp; }
+    else if (code == GPMPC_KP_PROD) { st[sp - 2] = st[sp - 2] * st[sp - 1]; --sp; }
+    else st[sp++] = kprog_leaf(code, par + off, a, b, d, same && row == col);
+  }
+  K[(int64_t)row * ldk + col] = st[0];
+}
+
+hipError_t launch_gram_prog(hipStream_t s, const int *ops, int nops, const double *par, const double *X1, int n1,
+                            const double *X2, int n2, int d, int same, double *K, int64_t ldk) {
+  if (n1 <= 0 || n2 <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_gram_prog, dim3((n2 + 127) / 128, n1), dim3(128), 0, s, ops, nops, par, X1, n1,
+                     same ? X1 : X2, n2, d, same, K, ldk);
+  return hipGetLastError();
+}
+
+// Host checks of a program (stack depth, operand counts, offsets in range, d lengthscales
+// > 0); its diagonal k(x, x): every leaf's is its sigma2 (stationary kernels, white noise),
+// so the diagonal of a composite is one constant (kernels.py diagonal methods)
+int kprog_check(const int *ops, int nops, int npar, int d, const double *par, double *diag) {
+  if (!ops || !par || nops < 1 || nops > GPMPC_KP_MAXOPS) return -2;
+  double st[GPMPC_KP_MAXSTACK];
+  int sp = 0;
+  for (int o = 0; o < nops; ++o) {
+    const int code = ops[2 * o], off = ops[2 * o + 1];
+    if (code == GPMPC_KP_SUM || code == GPMPC_KP_PROD) {
+      if (sp < 2) return -2;
+      st[sp - 2] = code == GPMPC_KP_SUM ? st[sp - 2] + st[sp - 1] : st[sp - 2] * st[sp - 1];
+      --sp;
+      continue;
+    }
+    const int np = code == GPMPC_KP_WHITE ? 1 : code == GPMPC_SE_ISO ? 2
+                 : (code == GPMPC_SE_ARD || code == GPMPC_MATERN32 || code == GPMPC_MATERN52) ? 1 + d : -1;
+    if (np < 0 || off < 0 || off + np > npar || sp >= GPMPC_KP_MAXSTACK) return -2;
+    if (!(par[off] >= 0.0)) return -2;
+    for (int i = 1; i < np; ++i)
+      if (!(par[off + i] > 0.0)) return -2;
+    st[sp++] = par[off];
+  }
+  if (sp != 1) return -2;
+  if (diag) *diag = st[0];
+  return 0;
+}

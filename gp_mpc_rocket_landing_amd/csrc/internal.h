@@ -118,6 +118,12 @@ __device__ __forceinline__ double kernel_epilogue(int kind, double d2, double si
 hipError_t launch_gram(hipStream_t s, int kind, const double *a, const double *na, int n1,
                        const double *b, const double *nb, int n2, int d, double sigma2,
                        double iso_scale, double *K, int64_t ldk, int transpose_out);
+#define GPMPC_KPROG 16  // GpCore kind of a composite-kernel program
+// composite kernel programs (gram.hip; codes GPMPC_KP_* in gpmpc.h): Gram of raw rows,
+// same = 1: one row set (X2 ignored; WhiteNoise on the diagonal)
+hipError_t launch_gram_prog(hipStream_t s, const int *ops, int nops, const double *par, const double *X1, int n1,
+                            const double *X2, int n2, int d, int same, double *K, int64_t ldk);
+int kprog_check(const int *ops, int nops, int npar, int d, const double *par, double *diag);
 // rows / lengthscales -> scaled rows + squared norms
 hipError_t launch_scale_rows(hipStream_t s, const double *X, int n, int d, const double *ls,
                              int iso, double *out, double *norms);
@@ -144,6 +150,7 @@ struct GpView {
   int kind, n, d, n_out;
   double sigma2, iso_scale;
   const double *ls, *Xs, *Xn, *W, *alphaT, *ymean, *ystd;
+  const double *Wf, *Xp;  // column-stationary posterior operands (post.hip), or null
 };
 GpView gp_view(const gpmpc_gp *gp);
 // the same view of a FITC GP: n = inducing points, Xs / Xn their scaled rows, alphaT

@@ -17,8 +17,11 @@ f(x + h e_i) of each gradient as ONE batched device call
 (gpmpc_gp_lml_batched: all Grams, one batched Cholesky, batched triangular
 solves).
 
-Not on this path: mean_function / normalize_y=False (NotImplementedError),
-composite kernels in a fitted GP.
+Any Kernel can be fitted, as in the reference (exact_gp.py:157): the four
+stationary kernels take the fast device Gram, composites (SumKernel,
+ProductKernel, WhiteNoise) their device program (Kernel.device_program,
+gpmpc_gp_fit_exact_prog).  Not on this path: mean_function /
+normalize_y=False (NotImplementedError).
 """
 from __future__ import annotations
 
@@ -45,10 +48,11 @@ class GPPrediction:
 
 
 def _spec(kernel: Kernel):
+    """(kind, lengthscales, sigma2) of a stationary kernel, or (KernelProgram, None,
+    None) for any other (composite) kernel: ExactGPHandle / FITCHandle take either."""
     spec = kernel._device_spec()
     if spec is None:
-        raise NotImplementedError(f"{type(kernel).__name__} has no device Gram; "
-                                  "fit with SE-ARD, SE, Matern32 or Matern52")
+        return kernel.device_program(), None, None
     return spec
 
 
@@ -208,10 +212,22 @@ class ExactGP:
     def _lml_batch(self, P, X, y):
         """Log marginal likelihoods at the rows of P = [kernel params (log
         space, kernels.py:320-371 order), log noise] -- the objective of
-        exact_gp.py:375-386 for every row, one device call."""
+        exact_gp.py:375-386 for every row, one device call (a composite
+        kernel: one device fit of its program per row)."""
         P = np.atleast_2d(P)
         nk = self.kernel.n_params
         k2 = copy.deepcopy(self.kernel)
+        if k2._device_spec() is None:
+            lml, steps = np.empty(len(P)), np.empty(len(P), np.int32)
+            for i, p in enumerate(P):
+                k2.set_params(p[:nk])
+                try:
+                    h = _lib.ExactGPHandle(_lib.default_context(), k2.device_program(), X, y[:, None], None,
+                                           None, float(np.exp(p[nk])))
+                    lml[i], steps[i] = h.lml[0], h.jitter_steps
+                except ValueError:   # exact_gp.py:383-386: a failed fit is +inf for the optimiser
+                    lml[i], steps[i] = -np.inf, -1
+            return lml, steps
         kind = None
         ls, s2 = [], []
         for p in P:
@@ -288,8 +304,10 @@ class ExactGP:
 
 
 def _same_kernel(a: Kernel, b: Kernel) -> bool:
-    sa, sb = a._device_spec(), b._device_spec()
-    return (sa is not None and sb is not None and sa[0] == sb[0] and sa[2] == sb[2]
+    sa, sb = _spec(a), _spec(b)
+    if isinstance(sa[0], _lib.KernelProgram) or isinstance(sb[0], _lib.KernelProgram):
+        return sa[0] == sb[0]
+    return (sa[0] == sb[0] and sa[2] == sb[2]
             and np.array_equal(np.asarray(sa[1]), np.asarray(sb[1])))
 
 

@@ -5,6 +5,10 @@ through gpmpc_gram (csrc/gram.hip: expansion-form scaled distance, clamped at
 0, kernels.py:205-236).  Hyperparameters are exposed in log space exactly as
 get_params/set_params/n_params/param_names define them (kernels.py:320-371).
 Sum/product kernels combine device Grams elementwise; WhiteNoise is diagonal.
+Every kernel also describes itself as a device program (``device_program``:
+the postfix form csrc/gram.hip evaluates), so a GP fitted with a composite
+kernel forms its Grams on the device too (gpmpc_gp_fit_exact_prog,
+gpmpc_sparse_fit_prog).
 ``gradients`` (kernels.py:279-318 and the per-kernel variants) returns the
 same dictionaries as the reference: SE-ARD / isotropic SE gradient matrices
 come from the device (gpmpc_gram_grad), the Matern kernels give only the
@@ -51,6 +55,16 @@ class Kernel(ABC):
     def _device_spec(self):
         return None
 
+    # the kernel as postfix program pairs (code, parameter offset) appended to ops / par
+    def _device_prog(self, ops: list, par: list) -> None:
+        raise NotImplementedError(f"{type(self).__name__} has no device program")
+
+    def device_program(self) -> "_lib.KernelProgram":
+        """This kernel as the device's postfix Gram program (gpmpc.h GPMPC_KP_*)."""
+        ops, par = [], []
+        self._device_prog(ops, par)
+        return _lib.KernelProgram(ops, par)
+
     def __add__(self, other):
         return SumKernel(self, other)
 
@@ -96,6 +110,10 @@ class _StationaryARD(Kernel):
 
     def _device_spec(self):
         return self.KIND, self._lengthscales, self._signal_variance
+
+    def _device_prog(self, ops, par):
+        ops.append((self.KIND, len(par)))
+        par.extend([self._signal_variance, *self._lengthscales])
 
     def __call__(self, X1, X2=None) -> np.ndarray:
         return _lib.gram(_ctx(), self.KIND, X1, X2, self._lengthscales, self._signal_variance)
@@ -188,6 +206,10 @@ class SquaredExponential(Kernel):
     def _device_spec(self):
         return _lib.SE_ISO, np.array([self._lengthscale]), self._signal_variance
 
+    def _device_prog(self, ops, par):
+        ops.append((_lib.SE_ISO, len(par)))
+        par.extend([self._signal_variance, self._lengthscale])
+
     def __call__(self, X1, X2=None) -> np.ndarray:
         return _lib.gram(_ctx(), _lib.SE_ISO, X1, X2, np.array([self._lengthscale]), self._signal_variance)
 
@@ -218,8 +240,15 @@ class SquaredExponential(Kernel):
 class SumKernel(Kernel):
     """kernels.py:676-726."""
 
+    OP = _lib.KP_SUM
+
     def __init__(self, k1: Kernel, k2: Kernel):
         self.k1, self.k2 = k1, k2
+
+    def _device_prog(self, ops, par):
+        self.k1._device_prog(ops, par)
+        self.k2._device_prog(ops, par)
+        ops.append((self.OP, 0))
 
     def __call__(self, X1, X2=None):
         return self.k1(X1, X2) + self.k2(X1, X2)
@@ -252,6 +281,7 @@ class SumKernel(Kernel):
 
 class ProductKernel(SumKernel):
     """kernels.py:729-782."""
+    OP = _lib.KP_PROD
 
     def __call__(self, X1, X2=None):
         return self.k1(X1, X2) * self.k2(X1, X2)
@@ -272,6 +302,10 @@ class WhiteNoise(Kernel):
 
     def __init__(self, noise_variance: float = 1e-6):
         self._noise_variance = float(noise_variance)
+
+    def _device_prog(self, ops, par):
+        ops.append((_lib.KP_WHITE, len(par)))
+        par.append(self._noise_variance)
 
     @property
     def noise_variance(self) -> float:

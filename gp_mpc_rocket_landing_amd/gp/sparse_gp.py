@@ -79,8 +79,7 @@ class SparseGP:
         y = np.atleast_1d(y).flatten()
         if self._Z is None:
             self._Z = self._initialize_inducing_points(X)
-        _, ls, s2 = _spec(self.kernel)
-        h = _lib.FITCHandle(_lib.default_context(), self._Z, X, y[:, None], ls, s2,
+        h = _lib.FITCHandle(_lib.default_context(), self._Z, X, y[:, None], *_sparse_kernel(self.kernel),
                             self._noise_variance, self.jitter, method=self.method)
         self._attach(X, y, h, 0)
         return self
@@ -126,6 +125,15 @@ class SparseGP:
         return f"SparseGP(n_train={self.n_train}, n_inducing={self.n_inducing}, method={self.method})"
 
 
+def _sparse_kernel(kernel):
+    """(ls, sigma2) of FITCHandle: the SE-ARD fast path, or any other kernel as its
+    device program (sparse_gp.py:182-183 takes any Kernel) with sigma2 unused."""
+    kind, ls, s2 = _spec(kernel)
+    if kind == _lib.SE_ARD:
+        return ls, s2
+    return kernel.device_program(), None
+
+
 class _SharedFITC:
     def __init__(self, h):
         self.h = h
@@ -163,8 +171,7 @@ class MultiOutputSparseGP:
             for gp in self.gps:
                 gp._Z = Z.copy()
             g0 = self.gps[0]
-            _, ls, s2 = _spec(g0.kernel)
-            h = _SharedFITC(_lib.FITCHandle(_lib.default_context(), Z, X, Y, ls, s2,
+            h = _SharedFITC(_lib.FITCHandle(_lib.default_context(), Z, X, Y, *_sparse_kernel(g0.kernel),
                                             g0.noise_variance, g0.jitter))
             for i, gp in enumerate(self.gps):
                 gp._attach(X, Y[:, i], h, i)

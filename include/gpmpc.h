@@ -43,6 +43,17 @@ typedef struct gpmpc_fleet gpmpc_fleet;
 /* kernel kinds: kernels.py:130 (SE-ARD), :392 (isotropic SE), :482 (Matern32), :579 (Matern52) */
 enum { GPMPC_SE_ARD = 0, GPMPC_SE_ISO = 1, GPMPC_MATERN32 = 2, GPMPC_MATERN52 = 3 };
 
+/* Composite kernels (kernels.py:676-844: SumKernel, ProductKernel, WhiteNoise) as a
+ * postfix program: nops pairs (code, offset into par).  Leaves: the four kinds above
+ * (par[off] = sigma2, then the d lengthscales; SE_ISO: sigma2, l) and GPMPC_KP_WHITE
+ * (par[off] = its noise variance: on the diagonal of a Gram of one row set, zero
+ * between two sets, kernels.py:805-815).  GPMPC_KP_SUM / _PROD combine the two values
+ * on top of the stack.  E.g. SumKernel(SE_ARD(d), WhiteNoise(s)): ops = {0,0, 4,d+1, 10,0},
+ * par = {sigma2, l_0..l_{d-1}, s}.  At most GPMPC_KP_MAXOPS pairs, stack depth 8. */
+enum { GPMPC_KP_WHITE = 4, GPMPC_KP_SUM = 10, GPMPC_KP_PROD = 11 };
+#define GPMPC_KP_MAXOPS 64
+#define GPMPC_KP_MAXSTACK 8
+
 /* OSQP-style status values (OSQP 0.6 constants.h), reported by the ADMM. */
 enum {
   GPMPC_QP_SOLVED = 1, GPMPC_QP_SOLVED_INACCURATE = 2, GPMPC_QP_MAX_ITER_REACHED = -2,
@@ -113,6 +124,15 @@ int gpmpc_potrs(gpmpc_ctx *ctx, int n, int nrhs, const double *L, int ldl, doubl
 int gpmpc_gp_fit_exact(gpmpc_ctx *ctx, int kind, const double *X, int n, int d, const double *Y,
                        int n_out, const double *ls, double sigma2, double noise, gpmpc_gp **out,
                        double *y_mean, double *y_std, double *lml, int *jitter_steps);
+/* gpmpc_gp_fit_exact with any kernel (ExactGP(kernel=...) fits whatever Kernel it is
+ * given, exact_gp.py:157): the Gram from a composite-kernel program over the raw rows
+ * (GPMPC_KP_*); predict / predict_cov then form K* and K** from the same program, and
+ * the prior variance k(x, x) is the program's diagonal (a constant: the sum / product
+ * of its leaves' sigma2).  -2 for a malformed program.  gpmpc_gp_append refits such a
+ * GP (returns GPMPC_ERR_NOT_PD). */
+int gpmpc_gp_fit_exact_prog(gpmpc_ctx *ctx, const int *ops, int nops, const double *par, int npar,
+                            const double *X, int n, int d, const double *Y, int n_out, double noise,
+                            gpmpc_gp **out, double *y_mean, double *y_std, double *lml, int *jitter_steps);
 /* ExactGP.predict (exact_gp.py:213-268) for all outputs: mean/var (p x n_out). */
 int gpmpc_gp_predict(gpmpc_ctx *ctx, gpmpc_gp *gp, const double *Xq, int p, double *mean,
                      double *var);
@@ -165,6 +185,13 @@ int gpmpc_fitc_fit(gpmpc_ctx *ctx, const double *Z, int m, const double *X, int 
 int gpmpc_vfe_fit(gpmpc_ctx *ctx, const double *Z, int m, const double *X, int n, int d,
                   const double *Y, int n_out, const double *ls, double sigma2, double noise,
                   double jitter, gpmpc_fitc **out, double *y_mean, double *y_std, double *lml);
+/* SparseGP(kernel=any).fit (sparse_gp.py:182-183: K_uu = kernel(Z), K_uf = kernel(Z, X),
+ * the diagonal kernel.diagonal(X)) with a composite-kernel program (above); method 0 =
+ * FITC (lambda_diag optional), 1 = VFE. */
+int gpmpc_sparse_fit_prog(gpmpc_ctx *ctx, int method, const int *ops, int nops, const double *par, int npar,
+                          const double *Z, int m, const double *X, int n, int d, const double *Y, int n_out,
+                          double noise, double jitter, gpmpc_fitc **out, double *y_mean, double *y_std,
+                          double *lml, double *lambda_diag);
 /* SparseGP.predict (sparse_gp.py:255-305), mean as written. */
 int gpmpc_fitc_predict(gpmpc_ctx *ctx, gpmpc_fitc *gp, const double *Xq, int p, double *mean,
                        double *var);

@@ -28,8 +28,21 @@ def scaled_sqdist(X1, X2, ls):
     return np.maximum(d, 0.0)
 
 
+def composite_diag(spec):
+    """k(x, x) of a composite spec (kernels.py diagonal methods, :694-695, :747-748,
+    :817-819): every leaf's diagonal is its sigma2, so the composite's is a constant."""
+    if spec[0] == "sum":
+        return composite_diag(spec[1]) + composite_diag(spec[2])
+    if spec[0] == "prod":
+        return composite_diag(spec[1]) * composite_diag(spec[2])
+    return float(spec[1])
+
+
 def gram(kind, X1, X2, sigma2, ls):
-    """K(X1, X2) for kind in {se_ard, se_iso, matern32, matern52}.
+    """K(X1, X2) for kind in {se_ard, se_iso, matern32, matern52}, or a composite
+    spec (kernels.py:676-844): ("sum", a, b), ("prod", a, b), ("white", s2) or a
+    leaf (kind, sigma2, ls); sigma2 / ls are then ignored.  WhiteNoise is s2 I on a
+    Gram of one set (X2 None) and zero across sets (kernels.py:805-815).
 
     se_ard   kernels.py:238-262   sigma2*exp(-0.5 r^2)
     se_iso   kernels.py:417-432   sigma2*exp(-r^2/(2 l^2)), distance on raw inputs
@@ -38,6 +51,14 @@ def gram(kind, X1, X2, sigma2, ls):
     """
     X1 = np.atleast_2d(X1)
     X2 = None if X2 is None else np.atleast_2d(X2)
+    if isinstance(kind, tuple):
+        if kind[0] == "sum":
+            return gram(kind[1], X1, X2, None, None) + gram(kind[2], X1, X2, None, None)
+        if kind[0] == "prod":
+            return gram(kind[1], X1, X2, None, None) * gram(kind[2], X1, X2, None, None)
+        if kind[0] == "white":
+            return kind[1] * np.eye(X1.shape[0]) if X2 is None else np.zeros((X1.shape[0], X2.shape[0]))
+        return gram(kind[0], X1, X2, kind[1], kind[2])
     if kind == "se_ard":
         return sigma2 * np.exp(-0.5 * scaled_sqdist(X1, X2, np.asarray(ls, float)))
     if kind == "se_iso":
@@ -186,6 +207,8 @@ def exact_fit(Z, Y, kind="se_ard", sigma2=1.0, ls=None, noise=1e-4):
     n = Z.shape[0]
     if ls is None:
         ls = np.ones(Z.shape[1])
+    if isinstance(kind, tuple):   # composite: the prior variance is its diagonal constant
+        sigma2 = composite_diag(kind)
     K = gram(kind, Z, None, sigma2, ls)
     L, jit = chol_with_jitter(K + noise * np.eye(n))
     out = dict(L=L, jitter_steps=jit, Z=Z, kind=kind, sigma2=sigma2, ls=np.asarray(ls, float),
@@ -225,23 +248,26 @@ def exact_predict_cov(st, Zq, out=0):
 # --------------------------------------------------------------------------
 # sparse FITC GP (src/gp/sparse_gp.py)
 # --------------------------------------------------------------------------
-def fitc_fit(Zi, X, Y, sigma2=1.0, ls=None, noise=1e-4, jitter=1e-6):
+def fitc_fit(Zi, X, Y, sigma2=1.0, ls=None, noise=1e-4, jitter=1e-6, kind="se_ard"):
     """SparseGP.fit, FITC branch (sparse_gp.py:150-219), for every column of Y with a
-    shared inducing set Zi (MultiOutputSparseGP.fit sparse_gp.py:430-456)."""
+    shared inducing set Zi (MultiOutputSparseGP.fit sparse_gp.py:430-456).  kind: a
+    kernel kind or a composite spec (gram); k_ff_diag = its diagonal constant."""
     X = np.atleast_2d(X); Y = np.asarray(Y, float)
     if Y.ndim == 1:
         Y = Y[:, None]
     if ls is None:
         ls = np.ones(X.shape[1])
+    if isinstance(kind, tuple):
+        sigma2 = composite_diag(kind)
     M = Zi.shape[0]; N = X.shape[0]
-    Kuu = gram("se_ard", Zi, None, sigma2, ls)
-    Kuf = gram("se_ard", Zi, X, sigma2, ls)
+    Kuu = gram(kind, Zi, None, sigma2, ls)
+    Kuf = gram(kind, Zi, X, sigma2, ls)
     Luu = np.linalg.cholesky(Kuu + jitter * np.eye(M))
     A = solve_triangular(Luu, Kuf, lower=True)
     lam = np.maximum(np.full(N, sigma2) - np.sum(A ** 2, axis=0) + noise, 1e-10)
     As = A * (1.0 / np.sqrt(lam))
     LB = np.linalg.cholesky(np.eye(M) + As @ As.T)
-    st = dict(Zi=Zi, Luu=Luu, LB=LB, lam=lam, sigma2=sigma2, ls=np.asarray(ls, float),
+    st = dict(Zi=Zi, Luu=Luu, LB=LB, lam=lam, sigma2=sigma2, ls=np.asarray(ls, float), kind=kind,
               alpha=[], y_mean=[], y_std=[], lml=[])
     for c in range(Y.shape[1]):
         yn, m, s = normalise(Y[:, c])
@@ -258,7 +284,7 @@ def fitc_fit(Zi, X, Y, sigma2=1.0, ls=None, noise=1e-4, jitter=1e-6):
     return st
 
 
-def vfe_fit(Zi, X, Y, sigma2=1.0, ls=None, noise=1e-4, jitter=1e-6):
+def vfe_fit(Zi, X, Y, sigma2=1.0, ls=None, noise=1e-4, jitter=1e-6, kind="se_ard"):
     """SparseGP.fit, VFE branch (sparse_gp.py:221-249 after the shared :181-188), every
     column of Y over one inducing set.  Returns the fitc_fit state layout, so
     fitc_predict evaluates it (the reference's predict has one body for both)."""
@@ -267,15 +293,17 @@ def vfe_fit(Zi, X, Y, sigma2=1.0, ls=None, noise=1e-4, jitter=1e-6):
         Y = Y[:, None]
     if ls is None:
         ls = np.ones(X.shape[1])
+    if isinstance(kind, tuple):
+        sigma2 = composite_diag(kind)
     M = Zi.shape[0]; N = X.shape[0]
-    Kuu = gram("se_ard", Zi, None, sigma2, ls)
-    Kuf = gram("se_ard", Zi, X, sigma2, ls)
+    Kuu = gram(kind, Zi, None, sigma2, ls)
+    Kuf = gram(kind, Zi, X, sigma2, ls)
     Luu = np.linalg.cholesky(Kuu + jitter * np.eye(M))
     A = solve_triangular(Luu, Kuf, lower=True)
     B = Kuu + (1.0 / noise) * Kuf @ Kuf.T + jitter * np.eye(M)
     LB = np.linalg.cholesky(B)
     trace_term = (N * sigma2 - np.sum(A ** 2)) / noise
-    st = dict(Zi=Zi, Luu=Luu, LB=LB, lam=None, sigma2=sigma2, ls=np.asarray(ls, float),
+    st = dict(Zi=Zi, Luu=Luu, LB=LB, lam=None, sigma2=sigma2, ls=np.asarray(ls, float), kind=kind,
               alpha=[], y_mean=[], y_std=[], lml=[])
     for c in range(Y.shape[1]):
         yn, m, s = normalise(Y[:, c])
@@ -294,7 +322,7 @@ def vfe_fit(Zi, X, Y, sigma2=1.0, ls=None, noise=1e-4, jitter=1e-6):
 def fitc_predict(st, Xq):
     """SparseGP.predict (sparse_gp.py:255-305); the mean is K*u @ alpha as written (D1)."""
     Xq = np.atleast_2d(Xq)
-    Ksu = gram("se_ard", Xq, st["Zi"], st["sigma2"], st["ls"])
+    Ksu = gram(st.get("kind", "se_ard"), Xq, st["Zi"], st["sigma2"], st["ls"])
     mean = (Ksu @ st["alpha"]) * st["y_std"] + st["y_mean"]
     v = solve_triangular(st["Luu"], Ksu.T, lower=True)
     w = solve_triangular(st["LB"], v, lower=True)

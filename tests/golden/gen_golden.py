@@ -1,4 +1,4 @@
-"""Generate the golden fixtures F1-F11 from the reference itself.
+"""Generate the golden fixtures F1-F13 (plus F9-F13 of later rounds) from the reference itself.
 
 Container-only: it imports /root/reference/src/{gp,mpc,experiments} through a
 namespace shim that bypasses src/__init__.py (which needs the absent simdyn /
@@ -424,7 +424,65 @@ def f12():
     save("f12_vfe_3dof.npz", **out)
 
 
+# ---------------------------------------------------------------- F13
+def f13():
+    """Composite kernels in fitted GPs (kernels.py:676-844 through exact_gp.py:157,
+    237-266 and sparse_gp.py:182-183, 193-199, 277-301): the reference's own ExactGP
+    with SumKernel(SE-ARD, WhiteNoise), ProductKernel(SE-ARD, Matern52) and
+    SumKernel(ProductKernel(SE iso, Matern32), WhiteNoise), and its FITC and VFE
+    SparseGP with SumKernel(Matern52, WhiteNoise) -- fit (alpha, LML, diag L) and
+    predict (mean, variance; return_cov for the first) on the 3-DoF features."""
+    X, U, D = synthetic_training_data(300, seed=21)
+    fe = features.Simple3DoFFeatureExtractor()
+    Z = fe.extract_batch(X, U)
+    d = Z.shape[1]
+    rs = np.random.RandomState(13)
+    sd = Z.std(0)
+    sd[sd < 1e-6] = 1.0
+    ls1 = 2.0 * sd * (0.8 + 0.4 * rs.rand(d))
+    ls2 = 3.0 * sd * (0.8 + 0.4 * rs.rand(d))
+    Xq, Uq = query_points(X, U, 17, seed=14)
+    Zq = fe.extract_batch(Xq, Uq)
+    out = dict(Z=Z, Y=D, Zq=Zq, ls1=ls1, ls2=ls2)
+
+    def k_sum_white():
+        return kernels.SumKernel(kernels.SquaredExponentialARD(d, 1.3, ls1.copy()), kernels.WhiteNoise(2e-3))
+
+    def k_prod():
+        return kernels.ProductKernel(kernels.SquaredExponentialARD(d, 1.1, ls1.copy()),
+                                     kernels.Matern52(d, 0.9, ls2.copy()))
+
+    def k_nested():
+        return kernels.SumKernel(kernels.ProductKernel(kernels.SquaredExponential(1.2, 2.5),
+                                                       kernels.Matern32(d, 0.8, ls2.copy())),
+                                 kernels.WhiteNoise(5e-3))
+
+    for name, make in (("sumwhite", k_sum_white), ("prod", k_prod), ("nested", k_nested)):
+        for c in range(2):
+            g = exact_gp.ExactGP(make(), noise_variance=1e-3)
+            g.fit(Z, D[:, c])
+            pr = g.predict(Zq)
+            out[f"{name}_mean{c}"] = pr.mean; out[f"{name}_var{c}"] = pr.variance
+            out[f"{name}_alpha{c}"] = g._alpha; out[f"{name}_lml{c}"] = np.array(g.log_marginal_likelihood)
+            out[f"{name}_diagL{c}"] = np.diag(g._L).copy()
+            if name == "sumwhite" and c == 0:
+                m, cov = g.predict(Zq, return_cov=True)
+                out["sumwhite_covmean0"] = m; out["sumwhite_cov0"] = cov
+    Zi = Z[rs.choice(Z.shape[0], 40, replace=False)].copy()
+    out["Zi"] = Zi
+    for method in ("fitc", "vfe"):
+        for c in range(2):
+            k = kernels.SumKernel(kernels.Matern52(d, 1.4, ls2.copy()), kernels.WhiteNoise(1e-3))
+            g = sparse_gp.SparseGP(k, n_inducing=40, noise_variance=2e-2, method=method, inducing_points=Zi.copy())
+            g.fit(Z, D[:, c])
+            pr = g.predict(Zq)
+            out[f"{method}_mean{c}"] = pr.mean; out[f"{method}_var{c}"] = pr.variance
+            out[f"{method}_alpha{c}"] = g._alpha; out[f"{method}_lml{c}"] = np.array(g.log_marginal_likelihood)
+    save("f13_composite_kernels.npz", **out)
+
+
 if __name__ == "__main__":
-    which = sys.argv[1:] or ["f1", "f2", "f3", "f4", "f5", "f6", "f6b", "f7_f8", "f9", "f10", "f11", "f12"]
+    which = sys.argv[1:] or ["f1", "f2", "f3", "f4", "f5", "f6", "f6b", "f7_f8", "f9", "f10", "f11", "f12",
+                             "f13"]
     for w in which:
         globals()[w]()

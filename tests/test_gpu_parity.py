@@ -380,3 +380,33 @@ def test_fitc_config5_scale(gpu_ctx):
     ok, e = close(var, rv, (st["y_std"] ** 2)[None, :]); assert ok, e
     np.testing.assert_allclose(h.lml, st["lml"], rtol=1e-8)
     np.testing.assert_allclose(h.lam, st["lam"], rtol=1e-10, atol=1e-14)
+
+
+@pytest.mark.parametrize("n,d,kind,n_out,P", [
+    (1, 11, "se_ard", 1, 5), (17, 11, "se_ard", 3, 33), (100, 12, "matern32", 2, 31),
+    (257, 13, "matern52", 3, 64), (500, 11, "se_iso", 3, 1), (1000, 11, "se_ard", 3, 700),
+    (1008, 13, "se_ard", 16, 97), (1009, 11, "se_ard", 3, 40)])
+def test_posterior_column_stationary_matches_oracle(gpu_ctx, n, d, kind, n_out, P):
+    """ExactGP.predict (exact_gp.py:237-266) through gpmpc_gp_predict, which for
+    n <= 1008 runs the column-stationary posterior (post.hip: K* formed in the MFMA
+    pass, W in packed fragments, two row halves) and above it the K*-in-HBM path
+    (n = 1009): every shape edge of the kernel -- one block, a partial last block,
+    the alpha block on a wave with fewer W blocks, 63 + 1 blocks exactly (n = 1008)
+    with 16 output rows, a partial last query group, d = 11 / 12 / 13, every
+    kernel kind -- against the numpy oracle at the SURVEY 8c tolerance."""
+    from gp_mpc_rocket_landing_amd import _lib
+    from oracle import gp_oracle
+    rs = np.random.RandomState(n + P)
+    Z = rs.randn(n, d) * 0.8
+    Y = rs.randn(n, n_out) * np.arange(1, n_out + 1) + 0.5
+    ls = rs.uniform(0.8, 1.6, d) if kind != "se_iso" else np.array([1.3])
+    s2, noise = 1.4, 1e-3
+    Zq = np.vstack([Z[rs.randint(0, n, P // 2)] + 0.05 * rs.randn(P // 2, d), rs.randn(P - P // 2, d)])
+    code = {"se_ard": _lib.SE_ARD, "se_iso": _lib.SE_ISO, "matern32": _lib.MATERN32, "matern52": _lib.MATERN52}
+    gp = _lib.ExactGPHandle(gpu_ctx, code[kind], Z, Y, ls, s2, noise)
+    m, v = gp.predict(Zq)
+    st = gp_oracle.exact_fit(Z, Y, kind=kind, sigma2=s2, ls=ls, noise=noise)
+    mo, vo = gp_oracle.exact_predict(st, Zq)
+    for c in range(n_out):
+        ok, w = close(m[:, c], mo[:, c], st["y_std"][c]); assert ok, ("mean", c, w)
+        ok, w = close(v[:, c], vo[:, c], s2 * st["y_std"][c] ** 2); assert ok, ("var", c, w)

@@ -372,3 +372,57 @@ def test_rti_with_callers_plant_vs_oracle(gpu_ctx, cls_name):
         if r["status"] in (1, 2):
             assert close(sol.u0, qp.from_vector(r["x"], N)[1][0], 1.0)[0], step
         x = plant.step(x, sol.u0, dt)
+
+
+def test_composite_kernels_through_the_surfaces_vs_f13(gpu_ctx):
+    """a22: ExactGP and SparseGP (FITC, VFE) fitted with
+    SumKernel / ProductKernel / WhiteNoise (kernels.py:676-844), as the reference's
+    exact_gp.py:157 / sparse_gp.py:182-183 take any Kernel: the device forms every
+    Gram from the kernel's postfix program (gpmpc_gp_fit_exact_prog,
+    gpmpc_sparse_fit_prog).  Against F13, produced by the reference's own GPs:
+    mean, variance, LML (and the full covariance) at the SURVEY 8c tolerance; the
+    composite hyperparameter objective (one device fit per row) against the oracle."""
+    from gp_mpc_rocket_landing_amd.gp import kernels as K
+    from gp_mpc_rocket_landing_amd.gp.exact_gp import ExactGP
+    from gp_mpc_rocket_landing_amd.gp.sparse_gp import SparseGP
+    from oracle import gp_oracle
+    g = golden("f13_composite_kernels.npz")
+    Z, Y, Zq, ls1, ls2 = g["Z"], g["Y"], g["Zq"], g["ls1"], g["ls2"]
+    d = Z.shape[1]
+    kern = {"sumwhite": lambda: K.SumKernel(K.SquaredExponentialARD(d, 1.3, ls1.copy()), K.WhiteNoise(2e-3)),
+            "prod": lambda: K.ProductKernel(K.SquaredExponentialARD(d, 1.1, ls1.copy()), K.Matern52(d, 0.9, ls2.copy())),
+            "nested": lambda: K.SumKernel(K.ProductKernel(K.SquaredExponential(1.2, 2.5), K.Matern32(d, 0.8, ls2.copy())),
+                                          K.WhiteNoise(5e-3))}
+    for name, make in kern.items():
+        for c in range(2):
+            gp = ExactGP(make(), noise_variance=1e-3).fit(Z, Y[:, c])
+            pr = gp.predict(Zq)
+            ys = gp._y_std
+            kd = float(make().diagonal(Zq[:1])[0])  # the prior variance: the kernel's diagonal
+            ok, w = close(pr.mean, g[f"{name}_mean{c}"], ys); assert ok, (name, c, "mean", w)
+            ok, w = close(pr.variance, g[f"{name}_var{c}"], kd * ys ** 2); assert ok, (name, c, "var", w)
+            assert abs(gp.log_marginal_likelihood - g[f"{name}_lml{c}"]) <= 1e-6 * abs(g[f"{name}_lml{c}"])
+            if name == "sumwhite" and c == 0:
+                m, cov = gp.predict(Zq, return_cov=True)
+                ok, w = close(cov, g["sumwhite_cov0"], kd * ys ** 2); assert ok, ("cov", w)
+                ok, w = close(m, g["sumwhite_covmean0"], ys); assert ok, ("covmean", w)
+    for method in ("fitc", "vfe"):
+        for c in range(2):
+            k = K.SumKernel(K.Matern52(d, 1.4, ls2.copy()), K.WhiteNoise(1e-3))
+            gp = SparseGP(k, n_inducing=40, noise_variance=2e-2, method=method,
+                          inducing_points=g["Zi"].copy()).fit(Z, Y[:, c])
+            pr = gp.predict(Zq)
+            ys = gp._y_std
+            ok, w = close(pr.mean, g[f"{method}_mean{c}"], ys); assert ok, (method, c, "mean", w)
+            ok, w = close(pr.variance, g[f"{method}_var{c}"], (1.4 + 1e-3) * ys ** 2); assert ok, (method, c, "var", w)
+            assert abs(gp.log_marginal_likelihood - g[f"{method}_lml{c}"]) <= 1e-6 * abs(g[f"{method}_lml{c}"])
+    # the composite hyperparameter objective: LML at three parameter rows vs the oracle
+    gp = ExactGP(kern["sumwhite"](), noise_variance=1e-3).fit(Z, Y[:, 0])
+    p0 = np.concatenate([gp.kernel.get_params(), [np.log(1e-3)]])
+    P = np.stack([p0, p0 + 0.1, p0 - 0.05])
+    lml, _ = gp._lml_batch(P, Z, Y[:, 0])
+    for i, p in enumerate(P):
+        nk = gp.kernel.n_params
+        spec = ("sum", ("se_ard", np.exp(p[0]), np.exp(p[1:nk - 1])), ("white", np.exp(p[nk - 1])))
+        want = gp_oracle.exact_fit(Z, Y[:, :1], kind=spec, noise=np.exp(p[nk]))["lml"][0]
+        assert abs(lml[i] - want) <= 1e-6 * abs(want), (i, lml[i], want)

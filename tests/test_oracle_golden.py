@@ -239,3 +239,48 @@ def test_f11_kernel_gradients():
     g = gp_oracle.gram_gradients("se_ard", X1, None, s2, ls)
     for j, gj in enumerate(g):
         np.testing.assert_allclose(gj, f[f"se_ard_x11_{j}"], rtol=1e-12, atol=1e-14)
+
+
+def f13_specs(g):
+    """The F13 kernels as gp_oracle composite specs (gen_golden.f13)."""
+    ls1, ls2 = g["ls1"], g["ls2"]
+    return {"sumwhite": (("sum", ("se_ard", 1.3, ls1), ("white", 2e-3)), 1e-3),
+            "prod": (("prod", ("se_ard", 1.1, ls1), ("matern52", 0.9, ls2)), 1e-3),
+            "nested": (("sum", ("prod", ("se_iso", 1.2, np.array([2.5])), ("matern32", 0.8, ls2)),
+                        ("white", 5e-3)), 1e-3)}
+
+
+F13_SPARSE = lambda g: ("sum", ("matern52", 1.4, g["ls2"]), ("white", 1e-3))  # noqa: E731
+
+
+def test_f13_composite_kernels():
+    """F13: the reference's ExactGP / SparseGP (FITC, VFE) fitted with composite
+    kernels (kernels.py:676-844) -- the oracle's composite specs reproduce alpha,
+    LML, diag L, predictions and the full covariance."""
+    g = golden("f13_composite_kernels.npz")
+    Z, Y, Zq = g["Z"], g["Y"], g["Zq"]
+    for name, (spec, noise) in f13_specs(g).items():
+        st = gp_oracle.exact_fit(Z, Y[:, :2], kind=spec, noise=noise)
+        m, v = gp_oracle.exact_predict(st, Zq)
+        for c in range(2):
+            ys = st["y_std"][c]
+            ok, w = close(st["alpha"][:, c], g[f"{name}_alpha{c}"], np.abs(g[f"{name}_alpha{c}"]).max(), 1e-8)
+            assert ok, (name, "alpha", w)
+            assert abs(st["lml"][c] - g[f"{name}_lml{c}"]) <= 1e-8 * abs(g[f"{name}_lml{c}"])
+            ok, w = close(np.diag(st["L"]), g[f"{name}_diagL{c}"], 1.0, 1e-10); assert ok, (name, "L", w)
+            ok, w = close(m[:, c], g[f"{name}_mean{c}"], ys, 1e-8); assert ok, (name, "mean", w)
+            ok, w = close(v[:, c], g[f"{name}_var{c}"], st["sigma2"] * ys ** 2, 1e-8); assert ok, (name, "var", w)
+    st = gp_oracle.exact_fit(Z, Y[:, :1], kind=f13_specs(g)["sumwhite"][0], noise=1e-3)
+    mc, cov = gp_oracle.exact_predict_cov(st, Zq)
+    ok, w = close(cov, g["sumwhite_cov0"], 1.0, 1e-8); assert ok, ("cov", w)
+    ok, w = close(mc, g["sumwhite_covmean0"], st["y_std"][0], 1e-8); assert ok, ("covmean", w)
+    for method, fit in (("fitc", gp_oracle.fitc_fit), ("vfe", gp_oracle.vfe_fit)):
+        st = fit(g["Zi"], Z, Y[:, :2], noise=2e-2, kind=F13_SPARSE(g))
+        m, v = gp_oracle.fitc_predict(st, Zq)
+        for c in range(2):
+            ys = st["y_std"][c]
+            ok, w = close(st["alpha"][:, c], g[f"{method}_alpha{c}"], np.abs(g[f"{method}_alpha{c}"]).max(), 1e-8)
+            assert ok, (method, "alpha", w)
+            assert abs(st["lml"][c] - g[f"{method}_lml{c}"]) <= 1e-8 * abs(g[f"{method}_lml{c}"]), method
+            ok, w = close(m[:, c], g[f"{method}_mean{c}"], ys, 1e-8); assert ok, (method, "mean", w)
+            ok, w = close(v[:, c], g[f"{method}_var{c}"], st["sigma2"] * ys ** 2, 1e-8); assert ok, (method, "var", w)
