@@ -36,33 +36,8 @@
 // 256 VGPRs is the same register file without them.  The 14 x 17 dynamics
 // block of each equality row lives in its owner's registers, a column copy in
 // the variable owner's; only the factor and the cross-thread vectors are LDS.
-#include "internal.h"
-#include "gemm.h"
-#include "qp.h"
+#include "fleet6.h"
 #include <vector>
-
-#define R6_NX 14
-#define R6_NU 3
-#define R6_SZ 17
-// the horizon N is a compile-time constant of the kernels (fully unrolled chains,
-// LDS layout): fleet6_n.h is compiled once per supported horizon, in namespaces
-// r6n20 (GPMPCConfig's N = 20, gp_mpc.py:110 / nominal_mpc.py:47) and r6n30
-// (BASELINE configs[4]); the C-ABI dispatches on the config's horizon
-#define R6_T 512                              // two items (variables / rows) per thread
-#define R6_TRI 153                            // packed lower 17 x 17
-#define R6_PT 512                             // predict threads (7 kernel-row waves + the RK4 wave)
-#define R6_FOR_H _Pragma("unroll") for (int h = 0; h < 2; ++h)
-
-// ConstraintParams (constraints.py:35-50), CostWeights (cost_functions.py:39-98),
-// gp_mpc.py trust regions (:432-435)
-#define R6_T_MIN 0.5
-#define R6_T_MAX 5.0
-
-// the rocket (Rocket6DoFConfig, rocket_6dof.py:36-84): diagonal J_B, thrust point
-// r_T_B, gravity g_I, alpha = 1 / (I_sp g0), g0 -- kernel arguments (uniform values)
-struct R6Rocket {
-  double J[3], rT[3], gI[3], alpha, g0;
-};
 
 struct R6Impl;  // the kernels of one horizon (fleet6_n.h), below
 struct gpmpc_rollout6 {
@@ -77,19 +52,6 @@ struct gpmpc_rollout6 {
   DevBuf prm;           // problem data (R6_PRM doubles, r6_prm layout)
   DevBuf xt, ut, done, passes, qit, qst, xin;  // GPMPC.solve mode: X_ref (B x (N+1) x 14), U_ref (B x N x 3)
 };
-
-// problem data in device memory (read per thread with a dynamic index, so not a
-// by-value kernel argument): Q (14), P (14), R (3), T_min, T_max, tan gamma_gs,
-// trust x / u radii
-#define R6_PQ 0
-#define R6_PP 14
-#define R6_PR 28
-#define R6_PTMIN 31
-#define R6_PTMAX 32
-#define R6_PTAN 33
-#define R6_PTRX 34
-#define R6_PTRU 35
-#define R6_PRM 36
 
 extern "C" void gpmpc_rollout6_default_config(gpmpc_rollout6_config *c) {
   c->horizon = 30;     // BASELINE configs[4]: N = 30
@@ -117,282 +79,23 @@ extern "C" void gpmpc_rollout6_default_config(gpmpc_rollout6_config *c) {
   c->rocket_g0 = 1.0;
 }
 
-// beta^T = alpha^T L_uu^-1 (3 x M): the FITC posterior mean is K*u beta.
-// W = L_uu^-1 (lower, row-major, ld M) is the fit's first M rows of core.W; the
-// product is one FP64-MFMA NN GEMM (a thread-per-column loop took 614 us at M = 2000)
-
-// ---------------------------------------------------------------------------
-// dynamics (nominal_mpc.py:163-203)
-__device__ __forceinline__ void r6_dcm(const double *q, double C[3][3]) {
-  const double w = q[0], x = q[1], y = q[2], z = q[3];
-  C[0][0] = 1 - 2 * (y * y + z * z); C[0][1] = 2 * (x * y - w * z); C[0][2] = 2 * (x * z + w * y);
-  C[1][0] = 2 * (x * y + w * z); C[1][1] = 1 - 2 * (x * x + z * z); C[1][2] = 2 * (y * z - w * x);
-  C[2][0] = 2 * (x * z - w * y); C[2][1] = 2 * (y * z + w * x); C[2][2] = 1 - 2 * (x * x + y * y);
-}
-
-__device__ void r6_f(const R6Rocket &rk, const double *x, const double *u, double *o) {
-  const double m = x[0];
-  const double tm = sqrt(u[0] * u[0] + u[1] * u[1] + u[2] * u[2]);
-  double C[3][3];
-  r6_dcm(x + 7, C);
-  o[0] = -rk.alpha * tm;
-  o[1] = x[4]; o[2] = x[5]; o[3] = x[6];
-  for (int i = 0; i < 3; ++i) o[4 + i] = (C[i][0] * u[0] + C[i][1] * u[1] + C[i][2] * u[2]) / m + rk.gI[i];
-  const double qw = x[7], qx = x[8], qy = x[9], qz = x[10], wx = x[11], wy = x[12], wz = x[13];
-  o[7] = 0.5 * -((wx * qx + wy * qy) + wz * qz);
-  o[8] = 0.5 * (qw * wx + (wy * qz - wz * qy));
-  o[9] = 0.5 * (qw * wy + (wz * qx - wx * qz));
-  o[10] = 0.5 * (qw * wz + (wx * qy - wy * qx));
-  // r_T x u; w x J w
-  const double *rT = rk.rT, *J = rk.J;
-  const double tq[3] = {rT[1] * u[2] - rT[2] * u[1], rT[2] * u[0] - rT[0] * u[2], rT[0] * u[1] - rT[1] * u[0]};
-  const double jw[3] = {J[0] * wx, J[1] * wy, J[2] * wz};
-  const double cx[3] = {wy * jw[2] - wz * jw[1], wz * jw[0] - wx * jw[2], wx * jw[1] - wy * jw[0]};
-  for (int i = 0; i < 3; ++i) o[11 + i] = (tq[i] - cx[i]) / J[i];
-}
-
-// RK4 (discretization.py:229-252) + quaternion normalisation (rocket_6dof.py:371-387)
-__device__ void r6_step(const R6Rocket &rk, const double *x, const double *u, double dt, double *xn) {
-  double k1[R6_NX], k2[R6_NX], k3[R6_NX], k4[R6_NX], t[R6_NX];
-  r6_f(rk, x, u, k1);
-  for (int i = 0; i < R6_NX; ++i) t[i] = x[i] + dt * k1[i] / 2;
-  r6_f(rk, t, u, k2);
-  for (int i = 0; i < R6_NX; ++i) t[i] = x[i] + dt * k2[i] / 2;
-  r6_f(rk, t, u, k3);
-  for (int i = 0; i < R6_NX; ++i) t[i] = x[i] + dt * k3[i];
-  r6_f(rk, t, u, k4);
-  for (int i = 0; i < R6_NX; ++i) xn[i] = x[i] + (dt / 6) * (k1[i] + 2 * k2[i] + 2 * k3[i] + k4[i]);
-  const double nq = sqrt(xn[7] * xn[7] + xn[8] * xn[8] + xn[9] * xn[9] + xn[10] * xn[10]);
-  for (int i = 7; i < 11; ++i) xn[i] = xn[i] / nq;
-}
-
-// -[A_d | B_d] (A_d = I + A_c dt, B_d = B_c dt) into a zeroed 14 x 17 row-major block
-__device__ void r6_neg_lin(const R6Rocket &rk, const double *x, const double *u, double dt, double *blk) {
-  auto set = [&](int i, int j, double v) { blk[i * R6_SZ + j] = v; };
-  const double m = x[0], qw = x[7], qx = x[8], qy = x[9], qz = x[10], wx = x[11], wy = x[12], wz = x[13];
-  const double u0 = u[0], u1 = u[1], u2 = u[2];
-  const double tm = sqrt(u0 * u0 + u1 * u1 + u2 * u2);
-  double C[3][3];
-  r6_dcm(x + 7, C);
-  for (int i = 0; i < R6_NX; ++i) set(i, i, -(1.0 + 0.0 * dt));
-  set(0, 14, -(-rk.alpha * u0 / tm * dt)); set(0, 15, -(-rk.alpha * u1 / tm * dt));
-  set(0, 16, -(-rk.alpha * u2 / tm * dt));
-  for (int i = 0; i < 3; ++i) set(1 + i, 4 + i, -(1.0 * dt));
-  for (int i = 0; i < 3; ++i) {
-    const double cu = C[i][0] * u0 + C[i][1] * u1 + C[i][2] * u2;
-    set(4 + i, 0, -(-cu / (m * m) * dt));
-    for (int j = 0; j < 3; ++j) set(4 + i, 14 + j, -(C[i][j] / m * dt));
-  }
-  const double dCu[3][4] = {
-      {-2 * qz * u1 + 2 * qy * u2, 2 * qy * u1 + 2 * qz * u2, -4 * qy * u0 + 2 * qx * u1 + 2 * qw * u2,
-       -4 * qz * u0 - 2 * qw * u1 + 2 * qx * u2},
-      {2 * qz * u0 - 2 * qx * u2, 2 * qy * u0 - 4 * qx * u1 - 2 * qw * u2, 2 * qx * u0 + 2 * qz * u2,
-       2 * qw * u0 - 4 * qz * u1 + 2 * qy * u2},
-      {-2 * qy * u0 + 2 * qx * u1, 2 * qz * u0 + 2 * qw * u1 - 4 * qx * u2,
-       -2 * qw * u0 + 2 * qz * u1 - 4 * qy * u2, 2 * qx * u0 + 2 * qy * u1}};
-  for (int i = 0; i < 3; ++i)
-    for (int j = 0; j < 4; ++j) set(4 + i, 7 + j, -(dCu[i][j] / m * dt));
-  const double Om[4][4] = {{0, -wx, -wy, -wz}, {wx, 0, -wz, wy}, {wy, wz, 0, -wx}, {wz, -wy, wx, 0}};
-  for (int i = 0; i < 4; ++i)
-    for (int j = 0; j < 4; ++j) set(7 + i, 7 + j, -((i == j ? 1.0 : 0.0) + 0.5 * Om[i][j] * dt));
-  const double Qw[4][3] = {{-qx, -qy, -qz}, {qw, qz, -qy}, {-qz, qw, qx}, {qy, -qx, qw}};
-  for (int i = 0; i < 4; ++i)
-    for (int j = 0; j < 3; ++j) set(7 + i, 11 + j, -(0.5 * Qw[i][j] * dt));
-  const double j1 = rk.J[0], j2 = rk.J[1], j3 = rk.J[2];
-  const double Aw[3][3] = {{0, wz, wy}, {wz, 0, wx}, {wy, wx, 0}};
-  const double cw[3] = {-(j3 - j2) / j1, -(j1 - j3) / j2, -(j2 - j1) / j3};
-  for (int i = 0; i < 3; ++i)
-    for (int j = 0; j < 3; ++j) set(11 + i, 11 + j, -((i == j ? 1.0 : 0.0) + cw[i] * Aw[i][j] * dt));
-  // B_c omega rows: J^-1 [r_T]x
-  const double rx = rk.rT[0], ry = rk.rT[1], rz = rk.rT[2];
-  const double Rx[3][3] = {{0, -rz, ry}, {rz, 0, -rx}, {-ry, rx, 0}};
-  for (int i = 0; i < 3; ++i)
-    for (int j = 0; j < 3; ++j) set(11 + i, 14 + j, -(Rx[i][j] / rk.J[i] * dt));
-}
-
-// ---------------------------------------------------------------------------
-// StructuredRocketGP features (features.py:196-263, :304-356), scaled by the GP's
-// lengthscales (the k_scale_rows arithmetic).  The formulas are split over six
-// wave-uniform roles, one lane each, so the transcendental chains of a point run
-// side by side instead of one after another on one lane:
-//   0: v 0-2, 7-11 (velocity, thrust, altitude)    1: v 3, w 0-6, 10 (speeds, rates, thrust)
-//   2: v 4, 12, w 11 (density: exp)                3: v 5 (angle of attack: atan2)
-//   4: v 6 (sideslip: asin)                        5: w 7-9 (body-frame velocity)
-// Each role evaluates its features with the same expressions as the whole set
-// would, so the scaled features are the same bits.
-#define R6_FEAT_ROLES 6
-__device__ __forceinline__ double r6_speed(const double *x) {
-  const double vx = x[4], vy = x[5], vz = x[6];
-  return sqrt((vx * vx + vy * vy) + vz * vz);
-}
-__device__ __forceinline__ void r6_body_velocity(const double *x, double *vb) {
-  const double vx = x[4], vy = x[5], vz = x[6];
-  // body-from-inertial DCM (features.py:265-270)
-  const double w = x[7], qx = x[8], qy = x[9], qz = x[10];
-  const double Cb[3][3] = {{1 - 2 * (qy * qy + qz * qz), 2 * (qx * qy + w * qz), 2 * (qx * qz - w * qy)},
-                           {2 * (qx * qy - w * qz), 1 - 2 * (qx * qx + qz * qz), 2 * (qy * qz + w * qx)},
-                           {2 * (qx * qz + w * qy), 2 * (qy * qz - w * qx), 1 - 2 * (qx * qx + qy * qy)}};
-  for (int i = 0; i < 3; ++i) vb[i] = (Cb[i][0] * vx + Cb[i][1] * vy) + Cb[i][2] * vz;
-}
-
-__device__ void r6_features_role(int role, const double *x, const double *u, const double *lsv,
-                                 const double *lsw, double *zv, double *zw) {
-  const double qn = 0.5 * 1.225 * 100.0;
-  switch (role) {
-    case 0: {
-      const double tm = sqrt((u[0] * u[0] + u[1] * u[1]) + u[2] * u[2]);
-      zv[0] = (x[4] / 10.0) / lsv[0]; zv[1] = (x[5] / 10.0) / lsv[1]; zv[2] = (x[6] / 10.0) / lsv[2];
-      zv[7] = (u[0] / 10.0) / lsv[7]; zv[8] = (u[1] / 10.0) / lsv[8]; zv[9] = (u[2] / 10.0) / lsv[9];
-      zv[10] = (tm / 10.0) / lsv[10]; zv[11] = (x[1] / 100.0) / lsv[11];
-      break;
-    }
-    case 1: {
-      const double speed = r6_speed(x);
-      const double wxx = x[11], wyy = x[12], wzz = x[13];
-      const double wm = sqrt((wxx * wxx + wyy * wyy) + wzz * wzz);
-      zv[3] = (speed / 10.0) / lsv[3];
-      zw[0] = wxx / lsw[0]; zw[1] = wyy / lsw[1]; zw[2] = wzz / lsw[2]; zw[3] = wm / lsw[3];
-      zw[4] = (u[0] / 10.0) / lsw[4]; zw[5] = (u[1] / 10.0) / lsw[5]; zw[6] = (u[2] / 10.0) / lsw[6];
-      zw[10] = (speed / 10.0) / lsw[10];
-      break;
-    }
-    case 2: {
-      const double speed = r6_speed(x);
-      const double rho = 1.225 * exp(-x[1] / 8500.0);
-      const double qd = 0.5 * rho * speed * speed;
-      zv[4] = (qd / qn) / lsv[4]; zv[12] = (rho / 1.225) / lsv[12];
-      zw[11] = (qd / qn) / lsw[11];
-      break;
-    }
-    case 3: {
-      const double speed = r6_speed(x);
-      double vb[3];
-      r6_body_velocity(x, vb);
-      zv[5] = (speed > 1e-3 ? atan2(-vb[2], vb[0]) : 0.0) / lsv[5];
-      break;
-    }
-    case 4: {
-      const double speed = r6_speed(x);
-      double vb[3];
-      r6_body_velocity(x, vb);
-      const bool moving = speed > 1e-3;
-      double sb = vb[1] / (moving ? speed : 1.0);
-      sb = fmin(fmax(sb, -1.0), 1.0);
-      zv[6] = (moving ? asin(sb) : 0.0) / lsv[6];
-      break;
-    }
-    default: {
-      double vb[3];
-      r6_body_velocity(x, vb);
-      zw[7] = (vb[0] / 10.0) / lsw[7]; zw[8] = (vb[1] / 10.0) / lsw[8]; zw[9] = (vb[2] / 10.0) / lsw[9];
-      break;
-    }
-  }
-}
-
-__device__ __forceinline__ bool r6_landing_ok(const double *x, double m0) {
-  // LandingConstraints.check_landing (monte_carlo.py:54-104), run_experiments tolerances
-  if (fabs(x[1]) > 1.0) return false;
-  if (fabs(x[2]) > 5.0 || fabs(x[3]) > 5.0) return false;
-  if (fabs(x[4]) > 3.0) return false;
-  if (fabs(x[5]) > 1.0 || fabs(x[6]) > 1.0) return false;
-  if (1.0 - x[0] / m0 > 1.0 - 0.05) return false;
-  return true;
-}
-
-struct R6Args {
-  QPSettingsDev st;
-  double dt;
-  int max_steps;
-  double *x, *U, *Xp, *gm, *Xo, *ysc, *rho, *rec;
-  double *lin;   // per rollout and stage: -[A_d | B_d] (14 x 17), from k_r6_predict
-  int *pending;  // the control kernel solved: k_r6_plant applies U[0]
-  // the two FITC GPs (d_v: 13 features, d_w: 12)
-  GpView gv, gw;
-  int Mv, Mw;
-  const double *cv, *cw;  // mean coefficients (3 x M): beta^T, or alpha^T as written
-  const double *prm;      // problem data (R6_PRM, r6 layout above)
-  int use_gp, upright;
-  // GPMPC.solve mode (gpmpc_rollout6_solve): 0 = Monte-Carlo rollout step; 1 = first
-  // pass (forward simulation of U); 2 = later pass (GP means and Jacobians at the plan)
-  int mode;
-  double sqp_tol;
-  const double *xt;       // GPMPC.solve: per-rollout X_ref (B x (N+1) x 14)
-  const double *ut;       // GPMPC.solve: per-rollout U_ref (B x N x 3)
-  R6Rocket rk;
-  int *done, *passes, *qit, *qst;
-};
-
-// ---------------------------------------------------------------------------
-// 1. termination rules + forward simulation with the GP mean
-// sum over the inducing rows i = t0, t0 + stride, .. of k(z, x_i) coef[c][i] (c < 3),
-// two rows per trip with all their loads issued before either is used
-template <int D>
-__device__ __forceinline__ void r6_kernel_rows(const GpView &v, int M, const double *__restrict__ cf,
-                                               const double *zs, int t0, int stride, double *acc) {
-  double z[D], zn = 0.0;
-#pragma unroll
-  for (int f = 0; f < D; ++f) { z[f] = zs[f]; zn += z[f] * z[f]; }  // |z|^2 in the feature order
-  const double *__restrict__ Xs = v.Xs;
-  const double *__restrict__ Xn = v.Xn;
-  int i = t0;
-  for (; i + stride < M; i += 2 * stride) {
-    const int j = i + stride;
-    double xa[D], xb[D], ca[3], cb[3];
-#pragma unroll
-    for (int f = 0; f < D; ++f) { xa[f] = Xs[(int64_t)i * D + f]; xb[f] = Xs[(int64_t)j * D + f]; }
-    const double na = Xn[i], nb = Xn[j];
-#pragma unroll
-    for (int c = 0; c < 3; ++c) { ca[c] = cf[(int64_t)c * M + i]; cb[c] = cf[(int64_t)c * M + j]; }
-    double da = 0.0, db = 0.0;
-#pragma unroll
-    for (int f = 0; f < D; ++f) { da = fma(z[f], xa[f], da); db = fma(z[f], xb[f], db); }
-    const double ka = kernel_epilogue(GPMPC_SE_ARD, (zn + na) - 2.0 * da, v.sigma2, 0.0);
-    const double kb = kernel_epilogue(GPMPC_SE_ARD, (zn + nb) - 2.0 * db, v.sigma2, 0.0);
-#pragma unroll
-    for (int c = 0; c < 3; ++c) { acc[c] += ka * ca[c]; acc[c] += kb * cb[c]; }
-  }
-  if (i < M) {
-    double dot = 0.0;
-#pragma unroll
-    for (int f = 0; f < D; ++f) dot = fma(z[f], Xs[(int64_t)i * D + f], dot);
-    const double kv = kernel_epilogue(GPMPC_SE_ARD, (zn + Xn[i]) - 2.0 * dot, v.sigma2, 0.0);
-#pragma unroll
-    for (int c = 0; c < 3; ++c) acc[c] += kv * cf[(int64_t)c * M + i];
-  }
-}
-
-
-// the kernels of one horizon, compiled per supported N (fleet6_n.h)
-struct R6Impl {
-  int N, M;
-  size_t smem;
-  hipError_t (*init)();
-  void (*predict)(hipStream_t, int B, const R6Args &, bool stamps);
-  void (*control)(hipStream_t, int B, const R6Args &, bool stamps);
-  void (*plant)(hipStream_t, int B, const R6Args &);
-  void (*reset)(hipStream_t, int first, int count, const double *x0, const R6Args &, double rho0);
-  void (*solve_begin)(hipStream_t, int B, const R6Args &, int cold, double rho0);
-  void (*print_stamps)();
-};
-
-namespace r6n20 {
-#define R6_N 20
-#include "fleet6_n.h"
-#undef R6_N
-}  // namespace r6n20
-namespace r6n30 {
-#define R6_N 30
-#include "fleet6_n.h"
-#undef R6_N
-}  // namespace r6n30
+// the kernels of every horizon (fleet6_h*.hip instantiate fleet6_n.h per N)
+#define R6_DECL(N) namespace r6n##N { const R6Impl *impl(); }
+R6_DECL(2) R6_DECL(3) R6_DECL(4) R6_DECL(5) R6_DECL(6) R6_DECL(7) R6_DECL(8) R6_DECL(9) R6_DECL(10)
+R6_DECL(11) R6_DECL(12) R6_DECL(13) R6_DECL(14) R6_DECL(15) R6_DECL(16) R6_DECL(17) R6_DECL(18) R6_DECL(19)
+R6_DECL(20) R6_DECL(21) R6_DECL(22) R6_DECL(23) R6_DECL(24) R6_DECL(25) R6_DECL(26) R6_DECL(27) R6_DECL(28)
+R6_DECL(29) R6_DECL(30)
+#undef R6_DECL
 
 static const R6Impl *r6_impl(int N) {
-  switch (N) {
-    case 20: return &r6n20::impl;
-    case 30: return &r6n30::impl;
-    default: return nullptr;
-  }
+  using F = const R6Impl *(*)();
+  static const F tab[R6_NMAX + 1] = {
+      nullptr, nullptr, r6n2::impl, r6n3::impl, r6n4::impl, r6n5::impl, r6n6::impl, r6n7::impl,
+      r6n8::impl, r6n9::impl, r6n10::impl, r6n11::impl, r6n12::impl, r6n13::impl, r6n14::impl,
+      r6n15::impl, r6n16::impl, r6n17::impl, r6n18::impl, r6n19::impl, r6n20::impl, r6n21::impl,
+      r6n22::impl, r6n23::impl, r6n24::impl, r6n25::impl, r6n26::impl, r6n27::impl, r6n28::impl,
+      r6n29::impl, r6n30::impl};
+  return N >= R6_NMIN && N <= R6_NMAX ? tab[N]() : nullptr;
 }
 // ---------------------------------------------------------------------------
 static int r6_create(gpmpc_ctx *ctx, const GpView &gv, const GpView &gw, bool exact,

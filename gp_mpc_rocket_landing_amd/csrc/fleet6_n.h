@@ -11,7 +11,7 @@
 #define R6_MG (4 * (R6_N - 1))                // 116 glideslope rows (76)
 #define R6_MGEN (R6_MT + R6_MG)               // 146 general rows (96)
 #define R6_M (R6_MD + R6_NV + R6_MGEN)        // 1104 rows (744)
-static_assert(R6_N % 2 == 0, "the twisted factor meets in the middle block x_N/2");
+static_assert(R6_N >= 2, "the twisted factor needs a top and a bottom end");
 static_assert(R6_NV <= 2 * R6_T && R6_NV + R6_MD <= 2 * R6_T && R6_MGEN <= R6_T, "two items per thread");
 
 // diagnostic phase cycles of the predict kernel's rollout 0 (GPMPC_R6_STAMPS=1)
@@ -328,7 +328,10 @@ __device__ __forceinline__ double r6_gen_dot(const R6Var &V, const double *v) {
 //   middle  Z = D_15 - G_14 C_14^T - H_15 E_15^T
 // -G_k goes to slot k (k < 15) and -H_k to slot k (k = 15..29) of s.G, over the
 // staged dynamics rows of its own stage once their last reader is done.
-#define R6_MID (R6_N / 2)
+// the middle block x_MID; the top end runs MID block steps, the bottom end BOTS = N - MID
+// (one fewer for an odd N: it then idles through the top's last step)
+#define R6_MID ((R6_N + 1) / 2)
+#define R6_BOTS (R6_N - R6_MID)
 
 __device__ __forceinline__ int r6_nat(int k, int e) {
   return k * R6_SZ + e - ((k > R6_MID && e >= R6_NX) ? R6_SZ : 0);
@@ -467,7 +470,10 @@ __device__ __forceinline__ int r6_factor(R6Smem &s, R6Var (&V)[2], R6Row (&R)[2]
   const int half = tid >> 8, lt = tid & 255;
   int bad = 0;
   for (int t = 0; t < R6_MID; ++t) {
-    const int k = half ? R6_N - t : t;    // factor block
+    // an odd N: the bottom end has one block step fewer, and sweeps an identity block
+    // through the top's last step (the sweep's barriers are the workgroup's), storing nothing
+    const bool idle = half && t >= R6_BOTS;
+    const int k = half ? (idle ? R6_N : R6_N - t) : t;  // factor block
     const int kc = half ? k - 1 : k;      // its coupling's slot
     double (*T)[R6_TRI] = s.T[half];
     if (lt < R6_TRI) {
@@ -475,9 +481,9 @@ __device__ __forceinline__ int r6_factor(R6Smem &s, R6Var (&V)[2], R6Row (&R)[2]
       r6_untri(lt, ti, tj);
       double v = s.Sinv[k * R6_TRI + lt];
       if (t > 0 && ti < R6_NX) v -= s.Sch[half][ti * R6_NX + tj];  // tj <= ti
-      T[0][lt] = v;
+      T[0][lt] = idle ? (ti == tj ? 1.0 : 0.0) : v;
     }
-    if (lt < R6_NX * R6_SZ) {  // top C_k[i][c]: x_k+1[i] with (k, c); bottom E_k-1[i][c]: x_k-1[i] with entry c of block k
+    if (!idle && lt < R6_NX * R6_SZ) {  // top C_k[i][c]: x_k+1[i] with (k, c); bottom E_k-1[i][c]: x_k-1[i] with entry c of block k
       const int i = lt / R6_SZ, c = lt - i * R6_SZ;
       double v;
       if (!half) v = r6_m_next(s, k, i, c, re);
@@ -487,18 +493,18 @@ __device__ __forceinline__ int r6_factor(R6Smem &s, R6Var (&V)[2], R6Row (&R)[2]
     }
     __syncthreads();
     const int cb = r6_sweep(T, lt, R6_SZ, k + 1, bad);  // W = -S_k^-1; bad: uniform over the half
-    if (lt < R6_TRI) s.Sinv[k * R6_TRI + lt] = -T[cb][lt];
+    if (!idle && lt < R6_TRI) s.Sinv[k * R6_TRI + lt] = -T[cb][lt];
     mark(10);
     // -G_k = -C_k S_k^-1 = C_k W / -H_k-1 over the staged rows of its slot
     double *Gs = s.G + kc * R6_NX * R6_SZ;
-    if (lt < R6_NX * R6_SZ) {
+    if (!idle && lt < R6_NX * R6_SZ) {
       const int i = lt / R6_SZ, c = lt - i * R6_SZ;
       double acc = 0.0;
       for (int e = 0; e < R6_SZ; ++e) acc += s.Ct[half][i * R6_SZ + e] * T[cb][r6_tri(e, c)];
       Gs[lt] = acc;  // stored negated: the chains accumulate
     }
     __syncthreads();
-    if (lt < R6_NX * R6_NX) {  // the next block's update G_k C_k^T / H_k-1 E_k-1^T (14 x 14)
+    if (!idle && lt < R6_NX * R6_NX) {  // the next block's update G_k C_k^T / H_k-1 E_k-1^T (14 x 14)
       const int i = lt / R6_NX, i2 = lt - i * R6_NX;
       double acc = 0.0;
       for (int e = 0; e < R6_SZ; ++e) acc += Gs[i * R6_SZ + e] * s.Ct[half][i2 * R6_SZ + e];
@@ -618,9 +624,11 @@ __device__ __forceinline__ void r6_solve(R6Smem &s, MK &mark) {
     double g16 = F[go + R6_SZ - 1];
     double y = s.rhs[ib + offo(ms)];
     double b16 = s.rhs[ib + o16], bn = s.rhs[ib + db + offo(m)];
+    // block steps of this end (wave-uniform; a compile-time count for an even N)
+    const int nst = (R6_BOTS == R6_MID) ? R6_MID : (bot ? R6_BOTS : R6_MID);
 #pragma unroll 3
-    for (int t = 0; t < R6_MID; ++t) {
-      const bool last = t == R6_MID - 1;
+    for (int t = 0; t < nst; ++t) {
+      const bool last = t == nst - 1;
       const int gn = go + gs;
       const double init = h ? 0.0 : fma(g16, b16, (bot && last) ? 0.0 : bn);
       b16 = s.rhs[ib + db + o16];
@@ -672,8 +680,10 @@ __device__ __forceinline__ void r6_solve(R6Smem &s, MK &mark) {
     for (int i = 0; i < R6_NX; ++i) g[i] = F[go + i * R6_SZ];
     double x = a < R6_NX ? s.xs[R6_MID * R6_SZ + a] : 0.0;
     double u = s.xs[ib + off];
+    // block steps of this end (wave-uniform; a compile-time count for an even N)
+    const int nst = (R6_BOTS == R6_MID) ? R6_MID : (bot ? R6_BOTS : R6_MID);
 #pragma unroll 3
-    for (int t = 0; t < R6_MID; ++t) {
+    for (int t = 0; t < nst; ++t) {
       const int gn = min(max(go + gs, a), (R6_N - 1) * R6_NX * R6_SZ + a);
       double a0 = u, a1 = 0.0;
       u = s.xs[min(max(ib + db, 0), R6_N * R6_SZ) + off];
@@ -1365,8 +1375,13 @@ static void r6_print_stamps() {  // diagnostic: phase cycles of rollout 0, summe
     fprintf(stderr, "r6 predict stamps N=%d: kernel rows + rk4 %llu means + next features %llu\n", R6_N, hp[1],
             hp[0]);
 }
-static const R6Impl impl = {R6_N, R6_M, sizeof(R6Smem), r6_init, r6_launch_predict, r6_launch_control,
-                            r6_launch_plant, r6_launch_reset, r6_launch_solve_begin, r6_print_stamps};
+// (a host function, not a namespace-scope object: the device pass would emit the object
+// with references to these host launchers)
+const R6Impl *impl() {
+  static const R6Impl i = {R6_N, R6_M, sizeof(R6Smem), r6_init, r6_launch_predict, r6_launch_control,
+                           r6_launch_plant, r6_launch_reset, r6_launch_solve_begin, r6_print_stamps};
+  return &i;
+}
 
 #undef R6_NBLK
 #undef R6_NV
@@ -1376,3 +1391,4 @@ static const R6Impl impl = {R6_N, R6_M, sizeof(R6Smem), r6_init, r6_launch_predi
 #undef R6_MGEN
 #undef R6_M
 #undef R6_MID
+#undef R6_BOTS

@@ -28,8 +28,15 @@
 #include "gemm.h"
 
 namespace {
-constexpr int PQ = 32;   // queries per workgroup
-constexpr int PT = 512;  // threads per workgroup (8 waves)
+constexpr int PQ = 32;              // queries per workgroup
+constexpr int NCW = 8;              // consumer (MFMA) waves
+constexpr int NPW = 4;              // producer (K*) waves
+constexpr int PT = 64 * (NCW + NPW);  // 768 threads: three waves per SIMD
+constexpr int SLAB = 16 * PQ;       // K* values of one 16-wide K step
+#ifndef POST_RING
+#define POST_RING 8
+#endif
+constexpr int RING = POST_RING;     // slabs in flight between producers and consumers
 
 __host__ __device__ inline int64_t post_foff(int j, int NB) {  // first fragment of K step j
   return (int64_t)j * (NB + 1) - (int64_t)j * (j - 1) / 2;
@@ -108,155 +115,192 @@ __global__ __launch_bounds__(PT, 1) void k_post_cs(int n, int NB, int P, int n_o
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int NS = NB;  // K steps of 16 over n (zero padded)
-  __shared__ double sK[2][PT];
-  __shared__ double red[8][PQ];
-  // this wave's blocks in slot order (increasing b): the existing ones are a prefix
-  int bt[4];
-  int T = 0;
-#pragma unroll
-  for (int t = 0; t < 4; ++t) {
-    bt[t] = wave + 8 * post_slot(h, t);
-    if (bt[t] <= NB) T = t + 1;
-  }
-  // producer role: K*[q][16 j + kk] -> sK[buf][tid], read back as the B fragment of
-  // substep sp, lane lp, column block yp (lane lp: column lp % 16, k offset lp / 16)
-  const int sp = tid >> 7, lp = (tid >> 1) & 63, yp = tid & 1;
-  const int kk = 4 * sp + (lp >> 4);
-  const int qg = min(c0 + 16 * yp + (lp & 15), P - 1);
-  double qv[D];
-#pragma unroll
-  for (int i = 0; i < D; ++i) qv[i] = Qs[(int64_t)qg * D + i];
-  const double qn = Qn[qg];
-  double xr[DP];
-  auto load_row = [&](int j) {
-    const int k = min(16 * j + kk, n - 1);
-    const double2 *x = (const double2 *)(Xp + (int64_t)k * DP);
-#pragma unroll
-    for (int i = 0; i < DP / 2; ++i) {
-      const double2 v = x[i];
-      xr[2 * i] = v.x;
-      xr[2 * i + 1] = v.y;
-    }
-  };
-  auto produce = [&](int j, int buf) {  // the k_gram arithmetic (k_gram_rows): same bits
-    double dot = 0.0;
-#pragma unroll
-    for (int i = 0; i < D; ++i) dot = fma(qv[i], xr[i], dot);
-    const double d2 = (qn + xr[D]) - 2.0 * dot;
-    const double v = 16 * j + kk < n ? kernel_epilogue(kind, d2, sigma2, iso_scale) : 0.0;
-    sK[buf][tid] = v;
-  };
-  const double *wl = Wf + lane * 4;
-  // the A fragment of block b at K step j: substeps 2 h2 and 2 h2 + 1 (16 bytes)
-  auto frag2 = [&](int j, int b, int h2, double &f0, double &f1) {
-    const double2 a = *(const double2 *)(wl + (post_foff(j, NB) + (b - j)) * 256 + 2 * h2);
-    f0 = a.x;
-    f1 = a.y;
-  };
-  d4_t acc[4][2];
-#pragma unroll
-  for (int t = 0; t < 4; ++t) acc[t][0] = acc[t][1] = (d4_t){0.0, 0.0, 0.0, 0.0};
-  double fr[4][4];
-  // prologue: K* slab 0, fragments of step 0
-  load_row(0);
-  produce(0, 0);
-#pragma unroll
-  for (int t = 0; t < 4; ++t)
-    if (t < T) {
-      frag2(0, bt[t], 0, fr[t][0], fr[t][1]);
-      frag2(0, bt[t], 1, fr[t][2], fr[t][3]);
-    }
+  __shared__ double sK[RING][SLAB];
+  __shared__ double red[NCW][PQ];
+  // per-wave progress words (one writer each): slabs formed by producer p, slabs released
+  // by consumer w; a wait that expired (a broken invariant: the group's output goes NaN)
+  __shared__ int s_ready[NPW], s_free[NCW], s_fail;
+  if (tid < NPW) s_ready[tid] = 0;
+  if (tid < NCW) s_free[tid] = 0;
+  if (tid == 0) s_fail = 0;
   __syncthreads();
-  int j = 0;
+  auto ld = [](int *f) { return __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); };
+  // bounded wait until every word of f[0 .. cnt) is >= v
+  auto wait_all = [&](int *f, int cnt, int v) {
+    for (int it = 0;; ++it) {
+      bool ok = true;
+      for (int i = 0; i < cnt; ++i) ok = ok && ld(f + i) >= v;
+      if (ok) break;
+      if (it > (1 << 20)) {
+        __hip_atomic_store(&s_fail, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+    asm volatile("" ::: "memory");  // the slab accesses stay behind the flags
+  };
+  // publish this wave's progress after its LDS accesses of the slab have completed
+  auto publish = [&](int *f, int v) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (lane == 0) __hip_atomic_store(f, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  };
+  if (wave >= NCW) {
+    // ---- producer waves: slab j (32 queries x 16 k) into ring slot j % RING.  Thread
+    // (p, l) forms entries 128 p + 2 l + y (y = 0, 1): training row k = 16 j + 4 p + l / 16
+    // against queries 16 y + l % 16 -- the B fragment of substep p, lane l, column block y
+    const int p = wave - NCW;
+    const int kk = 4 * p + (lane >> 4);
+    double qv[2][D], qn[2];
+#pragma unroll
+    for (int y = 0; y < 2; ++y) {
+      const int qg = min(c0 + 16 * y + (lane & 15), P - 1);
+#pragma unroll
+      for (int i = 0; i < D; ++i) qv[y][i] = Qs[(int64_t)qg * D + i];
+      qn[y] = Qn[qg];
+    }
+    double xr[DP];
+    auto load_row = [&](int j) {
+      const int k = min(16 * j + kk, n - 1);
+      const double2 *x = (const double2 *)(Xp + (int64_t)k * DP);
+#pragma unroll
+      for (int i = 0; i < DP / 2; ++i) {
+        const double2 v = x[i];
+        xr[2 * i] = v.x;
+        xr[2 * i + 1] = v.y;
+      }
+    };
+    load_row(0);
+    for (int j = 0; j < NS; ++j) {
+      double v[2];
+#pragma unroll
+      for (int y = 0; y < 2; ++y) {  // the k_gram arithmetic (k_gram_rows): same bits
+        double dot = 0.0;
+#pragma unroll
+        for (int i = 0; i < D; ++i) dot = fma(qv[y][i], xr[i], dot);
+        const double d2 = (qn[y] + xr[D]) - 2.0 * dot;
+        v[y] = 16 * j + kk < n ? kernel_epilogue(kind, d2, sigma2, iso_scale) : 0.0;
+      }
+      if (j + 1 < NS) load_row(j + 1);
+      if (j >= RING) wait_all(s_free, NCW, j - RING + 1);  // every consumer is done with slot j % RING
+      *(double2 *)&sK[j % RING][p * 128 + 2 * lane] = make_double2(v[0], v[1]);
+      publish(&s_ready[p], j + 1);
+    }
+  } else {
+    // ---- consumer (MFMA) waves: this wave's blocks in slot order (increasing b): the
+    // existing ones are a prefix
+    int bt[4];
+    int T = 0;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      bt[t] = wave + 8 * post_slot(h, t);
+      if (bt[t] <= NB) T = t + 1;
+    }
+    const double *wl = Wf + lane * 4;
+    // the A fragment of block b at K step j: substeps 2 h2 and 2 h2 + 1 (16 bytes)
+    auto frag2 = [&](int j, int b, int h2, double &f0, double &f1) {
+      const double2 a = *(const double2 *)(wl + (post_foff(j, NB) + (b - j)) * 256 + 2 * h2);
+      f0 = a.x;
+      f1 = a.y;
+    };
+    d4_t acc[4][2];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) acc[t][0] = acc[t][1] = (d4_t){0.0, 0.0, 0.0, 0.0};
+    double fr[4][4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+      if (t < T) {
+        frag2(0, bt[t], 0, fr[t][0], fr[t][1]);
+        frag2(0, bt[t], 1, fr[t][2], fr[t][3]);
+      }
+    int j = 0;
 // One K step with the live blocks [XF, XL) of this wave (literals: the unrolled loops
-// hold no branch around the MFMAs).  A fragment register pair is reloaded with the next
-// step's values as soon as its two substeps have issued (one set of fragment registers,
-// not two).  The last block XF may die at j + 1: its reload then reads the previous
-// fragment of the packed array (in bounds, unused).
+// hold no branch around the MFMAs): wait for slab j, its four B fragment reads, the
+// MFMAs, slot j released.  A fragment register pair is reloaded with the next step's
+// values as soon as its two substeps have issued (one set of fragment registers).  The
+// last block XF may die at j + 1: its reload then reads the previous fragment of the
+// packed array (in bounds, unused).
 #define POST_PHASE(XF, XL, JEND)                                                     \
   for (const int je_ = (JEND); j < je_; ++j) {                                       \
-    const int cur = j & 1;                                                           \
+    const double *sl = sK[j % RING];                                                 \
     const bool more = j + 1 < NS;                                                    \
-    if (more) load_row(j + 1);                                                       \
+    wait_all(s_ready, NPW, j + 1);                                                   \
+    double2 bv[4];                                                                   \
+    _Pragma("unroll") for (int s = 0; s < 4; ++s)                                    \
+      bv[s] = *(const double2 *)&sl[(s * 64 + lane) * 2];                            \
     _Pragma("unroll") for (int s = 0; s < 4; ++s) {                                  \
-      const double2 bv = *(const double2 *)&sK[cur][(s * 64 + lane) * 2];            \
       _Pragma("unroll") for (int t = XF; t < XL; ++t) {                              \
-        acc[t][0] = mfma_f64(fr[t][s], bv.x, acc[t][0]);                             \
-        acc[t][1] = mfma_f64(fr[t][s], bv.y, acc[t][1]);                             \
+        acc[t][0] = mfma_f64(fr[t][s], bv[s].x, acc[t][0]);                          \
+        acc[t][1] = mfma_f64(fr[t][s], bv[s].y, acc[t][1]);                          \
       }                                                                              \
       if ((s & 1) && more) {                                                         \
         _Pragma("unroll") for (int t = XF; t < XL; ++t)                              \
           frag2(j + 1, bt[t], s >> 1, fr[t][s - 1], fr[t][s]);                       \
       }                                                                              \
     }                                                                                \
-    if (more) produce(j + 1, cur ^ 1);                                               \
-    __syncthreads();                                                                 \
+    publish(&s_free[wave], j + 1);                                                   \
   }
 #define POST_END(t) min(bt[t] + 1, NS)
-  switch (T) {
-    case 4:
-      POST_PHASE(0, 4, POST_END(0))
-      POST_PHASE(1, 4, POST_END(1))
-      POST_PHASE(2, 4, POST_END(2))
-      POST_PHASE(3, 4, POST_END(3))
-      break;
-    case 3:
-      POST_PHASE(0, 3, POST_END(0))
-      POST_PHASE(1, 3, POST_END(1))
-      POST_PHASE(2, 3, POST_END(2))
-      break;
-    case 2:
-      POST_PHASE(0, 2, POST_END(0))
-      POST_PHASE(1, 2, POST_END(1))
-      break;
-    case 1:
-      POST_PHASE(0, 1, POST_END(0))
-      break;
-    default:
-      break;
-  }
+    switch (T) {
+      case 4:
+        POST_PHASE(0, 4, POST_END(0))
+        POST_PHASE(1, 4, POST_END(1))
+        POST_PHASE(2, 4, POST_END(2))
+        POST_PHASE(3, 4, POST_END(3))
+        break;
+      case 3:
+        POST_PHASE(0, 3, POST_END(0))
+        POST_PHASE(1, 3, POST_END(1))
+        POST_PHASE(2, 3, POST_END(2))
+        break;
+      case 2:
+        POST_PHASE(0, 2, POST_END(0))
+        POST_PHASE(1, 2, POST_END(1))
+        break;
+      case 1:
+        POST_PHASE(0, 1, POST_END(0))
+        break;
+      default:
+        break;
+    }
 #undef POST_END
 #undef POST_PHASE
-  for (; j < NS; ++j) {  // this wave's blocks are done: it still forms its share of K*
-    if (j + 1 < NS) {
-      load_row(j + 1);
-      produce(j + 1, (j & 1) ^ 1);
+    if (j < NS) publish(&s_free[wave], NS);  // this wave's blocks are done: it releases the rest at once
+    // epilogue: per query, the sum of squares over this half's W rows; the mean rows
+    double ss[2] = {0.0, 0.0};
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      if (t < T && bt[t] < NB) {
+#pragma unroll
+        for (int y = 0; y < 2; ++y)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) ss[y] = fma(acc[t][y][r], acc[t][y][r], ss[y]);
+      } else if (t < T) {  // the alpha block: row o = lane / 16 + 4 r
+#pragma unroll
+        for (int y = 0; y < 2; ++y)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int o = (lane >> 4) + 4 * r, q = c0 + 16 * y + (lane & 15);
+            if (o < n_out && q < P) meanT[(int64_t)o * ldm + q] = acc[t][y][r];
+          }
+      }
     }
-    __syncthreads();
-  }
-  // epilogue: per query, the sum of squares over this half's W rows; the mean rows
-  double ss[2] = {0.0, 0.0};
 #pragma unroll
-  for (int t = 0; t < 4; ++t) {
-    if (t < T && bt[t] < NB) {
-#pragma unroll
-      for (int y = 0; y < 2; ++y)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) ss[y] = fma(acc[t][y][r], acc[t][y][r], ss[y]);
-    } else if (t < T) {  // the alpha block: row o = lane / 16 + 4 r
-#pragma unroll
-      for (int y = 0; y < 2; ++y)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int o = (lane >> 4) + 4 * r, q = c0 + 16 * y + (lane & 15);
-          if (o < n_out && q < P) meanT[(int64_t)o * ldm + q] = acc[t][y][r];
-        }
+    for (int y = 0; y < 2; ++y) {
+      ss[y] += __shfl_xor(ss[y], 16);
+      ss[y] += __shfl_xor(ss[y], 32);
     }
-  }
-#pragma unroll
-  for (int y = 0; y < 2; ++y) {
-    ss[y] += __shfl_xor(ss[y], 16);
-    ss[y] += __shfl_xor(ss[y], 32);
-  }
-  if (lane < 16) {
-    red[wave][lane] = ss[0];
-    red[wave][16 + lane] = ss[1];
+    if (lane < 16) {
+      red[wave][lane] = ss[0];
+      red[wave][16 + lane] = ss[1];
+    }
   }
   __syncthreads();
   if (tid < PQ) {
     double v = 0.0;
 #pragma unroll
-    for (int w = 0; w < 8; ++w) v += red[w][tid];
+    for (int w = 0; w < NCW; ++w) v += red[w][tid];
+    // an expired wait (never expected) makes the whole group's output NaN, not quietly wrong
+    if (s_fail) v = __builtin_nan("");
     if (c0 + tid < P) part[(int64_t)h * ldp + c0 + tid] = v;
   }
 }

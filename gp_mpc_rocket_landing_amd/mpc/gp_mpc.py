@@ -238,7 +238,7 @@ class GPMPC6DoF(GPMPC):
     rows); U_ref also seeds the first guess when there is no warm start
     (:268-269).  The horizon is ``config.N`` -- ``GPMPCConfig()`` is the
     reference's N = 20 (gp_mpc.py:110, nominal_mpc.py:47); the device
-    controller is compiled for N = 20 and N = 30 (BASELINE configs[4]).  The
+    controller is compiled for every N from 2 to 30 (BASELINE configs[4]: 30).  The
     rocket is ``dynamics.params`` (J_B, r_T_B, g_I, I_sp, g0 of
     Rocket6DoFConfig); the device model takes a diagonal J_B.
     """
@@ -248,8 +248,9 @@ class GPMPC6DoF(GPMPC):
                  constraint_params=None, cost_weights=None, ctx=None):
         config = config or GPMPCConfig()
         if int(config.N) not in _r6.HORIZONS:
-            raise NotImplementedError(f"the 6-DoF device controller is compiled for N in {_r6.HORIZONS} "
-                                      f"(GPMPCConfig's N = 20, BASELINE configs[4]'s N = 30), not {config.N}")
+            raise NotImplementedError(f"the 6-DoF device controller is compiled for N = {_r6.HORIZONS[0]} .. "
+                                      f"{_r6.HORIZONS[-1]} (two QP items per thread of its 512-thread "
+                                      f"workgroup), not {config.N}")
         params = getattr(dynamics, "params", None)
         if params is None:
             raise TypeError("dynamics must expose the rocket's params (Rocket6DoFDynamics)")

@@ -19,7 +19,9 @@ from .data import synthetic_6dof_training_data
 from .gp.features import CombinedFeatureExtractor
 
 NX6 = 14
-HORIZONS = (20, 30)   # the compiled horizons of csrc/fleet6_n.h (GPMPCConfig's N, BASELINE configs[4])
+# the compiled horizons of csrc/fleet6_n.h: every N from 2 to 30 (one instance each,
+# csrc/fleet6_h*.hip; 30 = the two-items-per-thread cap of the 512-thread control kernel)
+HORIZONS = tuple(range(2, 31))
 
 
 def qp_rows(N: int) -> int:
@@ -106,7 +108,8 @@ class Rollouts6:
         self.gp_v, self.gp_w = gp_v, gp_w  # keep alive: the kernels read their device state
         self.cfg = _lib.rollout6_default_config(**config)
         if int(self.cfg.horizon) not in HORIZONS:
-            raise ValueError(f"horizon {int(self.cfg.horizon)}: the device controller is compiled for N in {HORIZONS}")
+            raise ValueError(f"horizon {int(self.cfg.horizon)}: the device controller is compiled for "
+                             f"N = {HORIZONS[0]} .. {HORIZONS[-1]}")
         self.batch = int(batch)
         self.N = int(self.cfg.horizon)
         self.M = qp_rows(self.N)

@@ -127,6 +127,19 @@ def test_gpmpc6_nondefault_rocket():
         assert len(seen) >= 8, (N, seen)
 
 
+def test_gpmpc6_any_horizon():
+    """MPCConfig.N is a free integer in the reference
+    (nominal_mpc.py:47, gp_mpc.py:253, 392); the device controller is compiled for
+    every N from 2 to 30, odd ones included (the twisted factor's bottom end then
+    has one block step fewer).  N = 15 (OSQPRTIConfig's default horizon), the odd
+    extremes 3 and 29, and 2: RTI steps vs the oracle."""
+    for N, steps in ((15, 8), (3, 4), (2, 4), (29, 4)):
+        seen = _fly(_surface(), steps, 1, N=N)
+        assert len(seen) >= steps, (N, seen)
+    seen = _fly(_surface(), 4, 10, N=15)   # the reference's 10-pass loop at N = 15
+    assert len(seen) >= 4, seen
+
+
 def test_gpmpc6_reference_trajectory():
     """X_ref / U_ref in the QP cost (gp_mpc.py:442-453) and U_ref as the first
     guess (:268-269), RTI and the 10-pass loop, N = 20."""

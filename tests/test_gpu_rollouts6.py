@@ -177,6 +177,15 @@ def test_rollouts6_horizon20_default_rocket(gpu_ctx):
     assert seen >= 25, seen
 
 
+@pytest.mark.parametrize("horizon", [15, 7, 2])
+def test_rollouts6_odd_and_short_horizons(gpu_ctx, horizon):
+    """Rollouts at a horizon other than the two round-4 instances: odd N (the
+    bottom end of the twisted factor one block step shorter) and the shortest,
+    N = 2; 4 rollouts x 20 steps, small GP, vs the oracle."""
+    seen, S = _run(gpu_ctx, 300, 50, 4, 20, horizon=horizon)
+    assert seen >= 20, seen
+
+
 def test_rollouts6_solved_setting(gpu_ctx):
     """the configs[4] controller at the ADMM setting where >= 90% of
     its QPs return "solved" (bench.SOLVED_QP6: max_iter 4000, eps 1e-4), 4 rollouts
