@@ -83,8 +83,10 @@ def test_gpmpc_dispatches_on_the_state_dimension():
     assert isinstance(m, GPMPC6DoF) and isinstance(m, GPMPC) and m.config.N == 20
     assert m._cfg_kw["fitc_mean_as_written"] == 1 and m._cfg_kw["horizon"] == 20
     assert GPMPC(Rocket6DoFDynamics(), gp, GPMPCConfig(N=30))._cfg_kw["horizon"] == 30
-    with pytest.raises(NotImplementedError):    # compiled horizons only
-        GPMPC(Rocket6DoFDynamics(), gp, GPMPCConfig(N=25))
+    assert GPMPC(Rocket6DoFDynamics(), gp, GPMPCConfig(N=15))._cfg_kw["horizon"] == 15   # any N in 2..30
+    for bad in (1, 31):
+        with pytest.raises(NotImplementedError):    # outside the compiled horizons
+            GPMPC(Rocket6DoFDynamics(), gp, GPMPCConfig(N=bad))
     # a non-default rocket reaches the device config (rocket_6dof.py:36-84 fields)
     k = GPMPC(Rocket6DoFDynamics(Rocket6DoFConfig(I_sp=20.0, g0=2.0, r_T_B=np.array([-0.3, 0.01, 0.0]))),
               gp)._cfg_kw
