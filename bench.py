@@ -794,10 +794,10 @@ def main():
         it_f, fac_f = admm_flops()
         steps_rank0 = steps_done / K
         admm_flop = (admm_iters / K) * it_f + steps_rank0 * 1.5 * fac_f
-        # default posterior (GPMPC_POST_CS, n <= 1008): the column-stationary kernel forms K*
-        # inside its MFMA pass (post.hip), so phase 1 is only the query features; the
-        # K* exponentials (P n, ~26 flop each) are extra work not counted in var_flops
-        cs = os.environ.get("GPMPC_POST_CS", "1") != "0" and n <= 1008
+        # GPMPC_POST_CS=1 (n <= 1008): the column-stationary kernel forms K* inside its MFMA
+        # pass (post.hip), so phase 1 is only the query features; the K* exponentials
+        # (P n, ~26 flop each) are extra work not counted in var_flops.  Off by default.
+        cs = os.environ.get("GPMPC_POST_CS", "0") != "0" and n <= 1008
         q_bytes = 8.0 * B * ((args.horizon + 1) * 7 + args.horizon * 3) + 8.0 * P * 12
         kern = {
             "gram_Kstar": dict(kernel="k_gram_rows<11, 0>", ms=ph_mean[0] * 1e3, bound="hbm",

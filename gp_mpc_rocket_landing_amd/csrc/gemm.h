@@ -94,7 +94,7 @@ hipError_t launch_post_cs(hipStream_t s, int n, int n_out, int P, const double *
                           const double *Qs, const double *Qn, int d, int kind, double sigma2, double iso_scale,
                           double *part, int64_t ldp, double *meanT, int64_t ldm);
 #define POST_CS_PARTS 2
-bool post_cs_env();  // GPMPC_POST_CS (default 1)
+bool post_cs_env();  // GPMPC_POST_CS (default 0)
 
 // rows of the SUMSQ partial buffer for an M x N x K product (tile height of
 // the kernel launch_gemm_* picks: 128 when M, N and K >= 256, else 64)

@@ -267,19 +267,18 @@ static hipError_t core_gram(hipStream_t s, const GpCore &g, const double *A, con
   return launch_gram(s, g.kind, A, NA, n1, B, NB, n2, g.d, g.sigma2, g.iso_scale, K, ldk, 0);
 }
 
-// GPMPC_POST_CS=0: the posterior through K* in HBM (gram + 128-tile SUMSQ GEMM) instead
+// GPMPC_POST_CS=1: the column-stationary posterior (post.hip) instead of K* in HBM (gram +
+// 128-tile SUMSQ GEMM).  Off by default: measured slower at the bench workload (DESIGN.md
+// section 3).  Read at every fit and predict, so a process can switch it between handles.
 bool post_cs_env() {
-  static const int v = [] {
-    const char *e = getenv("GPMPC_POST_CS");
-    return e ? atoi(e) : 1;
-  }();
-  return v != 0;
+  const char *e = getenv("GPMPC_POST_CS");
+  return e && atoi(e) != 0;
 }
 
 // Wf / Xp for the column-stationary posterior (post.hip) from the current [W; alpha^T],
 // Xs, Xn; released when the GP is outside the kernel's range
 static hipError_t core_pack(hipStream_t s, GpCore &g) {
-  if (g.kind == GPMPC_KPROG || !post_cs_ok(g.n, g.n_out, g.d)) {
+  if (g.kind == GPMPC_KPROG || !post_cs_env() || !post_cs_ok(g.n, g.n_out, g.d)) {
     g.Wf.release();
     g.Xp.release();
     return hipSuccess;

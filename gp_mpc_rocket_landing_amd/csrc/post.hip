@@ -36,6 +36,9 @@ constexpr int SLAB = 16 * PQ;       // K* values of one 16-wide K step
 #ifndef POST_RING
 #define POST_RING 8
 #endif
+#ifndef POST_PF
+#define POST_PF 2  // training rows a producer thread keeps in flight
+#endif
 constexpr int RING = POST_RING;     // slabs in flight between producers and consumers
 
 __host__ __device__ inline int64_t post_foff(int j, int NB) {  // first fragment of K step j
@@ -125,19 +128,23 @@ __global__ __launch_bounds__(PT, 1) void k_post_cs(int n, int NB, int P, int n_o
   if (tid == 0) s_fail = 0;
   __syncthreads();
   auto ld = [](int *f) { return __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); };
-  // bounded wait until every word of f[0 .. cnt) is >= v
+  // bounded wait until every word of f[0 .. cnt) is >= v; returns their minimum, which the
+  // caller keeps so that it reads the flags again only when it has caught up with them
   auto wait_all = [&](int *f, int cnt, int v) {
+    int mn = 0;
     for (int it = 0;; ++it) {
-      bool ok = true;
-      for (int i = 0; i < cnt; ++i) ok = ok && ld(f + i) >= v;
-      if (ok) break;
+      mn = 1 << 30;
+      for (int i = 0; i < cnt; ++i) mn = min(mn, ld(f + i));
+      if (mn >= v) break;
       if (it > (1 << 20)) {
         __hip_atomic_store(&s_fail, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        mn = 1 << 30;
         break;
       }
       __builtin_amdgcn_s_sleep(1);
     }
     asm volatile("" ::: "memory");  // the slab accesses stay behind the flags
+    return mn;
   };
   // publish this wave's progress after its LDS accesses of the slab have completed
   auto publish = [&](int *f, int v) {
@@ -158,32 +165,43 @@ __global__ __launch_bounds__(PT, 1) void k_post_cs(int n, int NB, int P, int n_o
       for (int i = 0; i < D; ++i) qv[y][i] = Qs[(int64_t)qg * D + i];
       qn[y] = Qn[qg];
     }
-    double xr[DP];
-    auto load_row = [&](int j) {
+    // the training rows of the next PF slabs in flight (a register ring, PF-step unrolled)
+    constexpr int PF = POST_PF;
+    double xr[PF][DP];
+    auto load_row = [&](int j, double (&x)[DP]) {
       const int k = min(16 * j + kk, n - 1);
-      const double2 *x = (const double2 *)(Xp + (int64_t)k * DP);
+      const double2 *src = (const double2 *)(Xp + (int64_t)k * DP);
 #pragma unroll
       for (int i = 0; i < DP / 2; ++i) {
-        const double2 v = x[i];
-        xr[2 * i] = v.x;
-        xr[2 * i + 1] = v.y;
+        const double2 v = src[i];
+        x[2 * i] = v.x;
+        x[2 * i + 1] = v.y;
       }
     };
-    load_row(0);
-    for (int j = 0; j < NS; ++j) {
-      double v[2];
 #pragma unroll
-      for (int y = 0; y < 2; ++y) {  // the k_gram arithmetic (k_gram_rows): same bits
-        double dot = 0.0;
+    for (int q = 0; q < PF; ++q) load_row(q, xr[q]);
+    int free_upto = RING;  // slots known free: slabs < free_upto may be written
+    for (int j0 = 0; j0 < NS; j0 += PF) {
 #pragma unroll
-        for (int i = 0; i < D; ++i) dot = fma(qv[y][i], xr[i], dot);
-        const double d2 = (qn[y] + xr[D]) - 2.0 * dot;
-        v[y] = 16 * j + kk < n ? kernel_epilogue(kind, d2, sigma2, iso_scale) : 0.0;
+      for (int q = 0; q < PF; ++q) {
+        const int j = j0 + q;
+        if (j < NS) {
+          double v[2];
+#pragma unroll
+          for (int y = 0; y < 2; ++y) {  // the k_gram arithmetic (k_gram_rows): same bits
+            double dot = 0.0;
+#pragma unroll
+            for (int i = 0; i < D; ++i) dot = fma(qv[y][i], xr[q][i], dot);
+            const double d2 = (qn[y] + xr[q][D]) - 2.0 * dot;
+            v[y] = 16 * j + kk < n ? kernel_epilogue(kind, d2, sigma2, iso_scale) : 0.0;
+          }
+          if (j + PF < NS) load_row(j + PF, xr[q]);
+          if (j >= free_upto)  // every consumer must be done with slot j % RING
+            free_upto = wait_all(s_free, NCW, j - RING + 1) + RING;
+          *(double2 *)&sK[j % RING][p * 128 + 2 * lane] = make_double2(v[0], v[1]);
+          publish(&s_ready[p], j + 1);
+        }
       }
-      if (j + 1 < NS) load_row(j + 1);
-      if (j >= RING) wait_all(s_free, NCW, j - RING + 1);  // every consumer is done with slot j % RING
-      *(double2 *)&sK[j % RING][p * 128 + 2 * lane] = make_double2(v[0], v[1]);
-      publish(&s_ready[p], j + 1);
     }
   } else {
     // ---- consumer (MFMA) waves: this wave's blocks in slot order (increasing b): the
@@ -212,7 +230,7 @@ __global__ __launch_bounds__(PT, 1) void k_post_cs(int n, int NB, int P, int n_o
         frag2(0, bt[t], 0, fr[t][0], fr[t][1]);
         frag2(0, bt[t], 1, fr[t][2], fr[t][3]);
       }
-    int j = 0;
+    int j = 0, ready_upto = 0;  // slabs known formed: slabs < ready_upto may be read
 // One K step with the live blocks [XF, XL) of this wave (literals: the unrolled loops
 // hold no branch around the MFMAs): wait for slab j, its four B fragment reads, the
 // MFMAs, slot j released.  A fragment register pair is reloaded with the next step's
@@ -223,7 +241,7 @@ __global__ __launch_bounds__(PT, 1) void k_post_cs(int n, int NB, int P, int n_o
   for (const int je_ = (JEND); j < je_; ++j) {                                       \
     const double *sl = sK[j % RING];                                                 \
     const bool more = j + 1 < NS;                                                    \
-    wait_all(s_ready, NPW, j + 1);                                                   \
+    if (j >= ready_upto) ready_upto = wait_all(s_ready, NPW, j + 1);                 \
     double2 bv[4];                                                                   \
     _Pragma("unroll") for (int s = 0; s < 4; ++s)                                    \
       bv[s] = *(const double2 *)&sl[(s * 64 + lane) * 2];                            \

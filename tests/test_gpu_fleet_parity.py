@@ -503,7 +503,8 @@ def test_fleet_sqp_mode_matches_oracle(gpu_ctx):
             assert moved > nb, moved   # the converged branch (plant step) ran
 
 
-def test_fleet_posterior_full_size_matches_oracle(gpu_ctx):
+@pytest.mark.parametrize("cs", ["0", "1"])
+def test_fleet_posterior_full_size_matches_oracle(gpu_ctx, monkeypatch, cs):
     """The headline kernel's own output: the GP posterior the
     fleet computes each control step for all 1024 landings x 20 horizon points
     (P = 20 480 queries against the n = 1000 GP, BASELINE configs[3]) -- the mean
@@ -513,11 +514,13 @@ def test_fleet_posterior_full_size_matches_oracle(gpu_ctx):
     at every query, over two control steps (the second one with the dispatch order
     of the first step's iteration counts, so the slot -> landing map is not the
     identity).  Tolerance spec SURVEY 8c: |a - b| <= 1e-6 max(|b|, s), s = y_std
-    for means, sigma2 y_std^2 for variances."""
+    for means, sigma2 y_std^2 for variances.  Both posterior paths: K* in HBM (the
+    default) and GPMPC_POST_CS=1's column-stationary kernel."""
     from gp_mpc_rocket_landing_amd.data import synthetic_training_data
     from gp_mpc_rocket_landing_amd.fleet import Fleet, fit_gp, initial_conditions
     from oracle import gp_oracle
 
+    monkeypatch.setenv("GPMPC_POST_CS", cs)
     nb, n = 1024, 1000
     X, U, D = synthetic_training_data(n, seed=0)
     st = gp_oracle.exact_fit(gp_oracle.features_3dof(X, U), D)

@@ -386,16 +386,19 @@ def test_fitc_config5_scale(gpu_ctx):
     (1, 11, "se_ard", 1, 5), (17, 11, "se_ard", 3, 33), (100, 12, "matern32", 2, 31),
     (257, 13, "matern52", 3, 64), (500, 11, "se_iso", 3, 1), (1000, 11, "se_ard", 3, 700),
     (1008, 13, "se_ard", 16, 97), (1009, 11, "se_ard", 3, 40)])
-def test_posterior_column_stationary_matches_oracle(gpu_ctx, n, d, kind, n_out, P):
-    """ExactGP.predict (exact_gp.py:237-266) through gpmpc_gp_predict, which for
-    n <= 1008 runs the column-stationary posterior (post.hip: K* formed in the MFMA
-    pass, W in packed fragments, two row halves) and above it the K*-in-HBM path
-    (n = 1009): every shape edge of the kernel -- one block, a partial last block,
-    the alpha block on a wave with fewer W blocks, 63 + 1 blocks exactly (n = 1008)
-    with 16 output rows, a partial last query group, d = 11 / 12 / 13, every
-    kernel kind -- against the numpy oracle at the SURVEY 8c tolerance."""
+@pytest.mark.parametrize("cs", ["1", "0"])
+def test_posterior_column_stationary_matches_oracle(gpu_ctx, monkeypatch, cs, n, d, kind, n_out, P):
+    """ExactGP.predict (exact_gp.py:237-266) through gpmpc_gp_predict.  With
+    GPMPC_POST_CS=1 and n <= 1008 it runs the column-stationary posterior (post.hip:
+    K* formed in the MFMA pass, W in packed fragments, two row halves), otherwise
+    the K*-in-HBM path (the default, and n = 1009 always): every shape edge of the
+    kernel -- one block, a partial last block, the alpha block on a wave with fewer
+    W blocks, 63 + 1 blocks exactly (n = 1008) with 16 output rows, a partial last
+    query group, d = 11 / 12 / 13, every kernel kind -- against the numpy oracle at
+    the SURVEY 8c tolerance."""
     from gp_mpc_rocket_landing_amd import _lib
     from oracle import gp_oracle
+    monkeypatch.setenv("GPMPC_POST_CS", cs)   # read by the library at fit and predict
     rs = np.random.RandomState(n + P)
     Z = rs.randn(n, d) * 0.8
     Y = rs.randn(n, n_out) * np.arange(1, n_out + 1) + 0.5
