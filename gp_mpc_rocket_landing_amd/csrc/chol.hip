@@ -1009,8 +1009,8 @@ __global__ __launch_bounds__(256) void k_potrf_persist(int n, double *A, int64_t
       for (int rt = nrt - 1; rt >= 0; --rt) {
         d4_t acc[4][4];
         const int r0 = J + rt * DB;
-        mma128_tile(Mb + (int64_t)r0 * lda, lda, Mb + (int64_t)J * lda, lda, n - r0, pw, 0, 0, 0, J,
-                    sA, sB, acc);
+        mma128_tile<false, false, false, false, false, false>(Mb + (int64_t)r0 * lda, lda, Mb + (int64_t)J * lda,
+                                                              lda, n - r0, pw, 0, 0, 0, J, sA, sB, acc);
 #pragma unroll
         for (int x = 0; x < 4; ++x)
 #pragma unroll
@@ -1057,7 +1057,8 @@ __global__ __launch_bounds__(256) void k_potrf_persist(int n, double *A, int64_t
     for (int rt = 1; rt < nrt; ++rt) {
       d4_t acc[4][4];
       const int r0 = J + rt * DB;
-      mma128_tile(Mb + (int64_t)r0 * lda + J, lda, Li, DB, n - r0, DB, 0, 0, 0, DB, sA, sB, acc);
+      mma128_tile<false, false, false, false, false, false>(Mb + (int64_t)r0 * lda + J, lda, Li, DB, n - r0, DB, 0,
+                                                            0, 0, DB, sA, sB, acc);
 #pragma unroll
       for (int x = 0; x < 4; ++x)
 #pragma unroll

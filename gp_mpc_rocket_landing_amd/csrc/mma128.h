@@ -40,13 +40,198 @@ __device__ __forceinline__ int mma128_col(int wave, int y, bool ilc) {
 // the potrf's L_cc^-1), so a wave's 16-column MFMA block y dies once k is past its last row.
 // Ci: the accumulators start from the tile of Ci (rows r0.., columns c0.., ldci) instead of
 // zero; with NEGA (A staged negated) the tile computes Ci - A B^T.
-template <bool IL = false, bool L2A = false, bool L2B = false, bool ILC = false, bool NEGA = false>
+#ifndef MMA_V2
+#define MMA_V2 1
+#endif
+
+// whether mma128_tile takes the LDS-DMA loop (its callers size their own LDS by it)
+template <bool L2A, bool L2B, bool ILC, bool NEGA, bool DMA>
+constexpr bool mma128_dma() { return MMA_V2 && DMA && !L2A && !L2B && !NEGA && !ILC; }
+
+// A zero 16-byte chunk: the LDS-DMA source of a tile's padding rows.
+static __device__ double g_mma_zero[2] = {0.0, 0.0};
+
+// mma128_tile's loop with LDS-DMA staging (global_load_lds_dwordx4, no staging registers,
+// no ds_write pass) and 16-byte fragment reads.  An operand's K step is 128 rows x 16
+// doubles, 128 B a row, unpadded (one DMA wave-instruction fills 8 whole rows); the row's
+// 16-byte chunk c (k = 2c, 2c + 1) sits in slot c ^ ((r >> 1) & 7), so the 16 rows of a
+// fragment read hit 16 distinct (r & 1, slot) bank groups: conflict-free ds_read_b128.
+// The swizzle is applied on the DMA's per-lane global source address.  Substep q of a
+// K step reads k = 4 (lane >> 4) + q (A and B alike), so one ds_read_b128 serves two
+// substeps and a lane's four k's are two reads.  The step with a partial K slice (k_hi
+// not a multiple of GK) and operands without 16-byte alignment are staged through
+// registers in the same layout, zero filled.  Same tile semantics as mma128_tile; the
+// sums run in another k order (not the same bits as the register-staged loop).
+template <bool IL, bool ILC>
+__device__ __forceinline__ void mma128_tile_v2(const double *__restrict__ A, int64_t lda,
+                                               const double *__restrict__ B, int64_t ldb, int M, int N,
+                                               int r0, int c0, int k_lo, int k_hi, d4_t (&acc)[4][4],
+                                               int tri_rows, bool lower_out, bool tri_b, const double *Ci,
+                                               int64_t ldci) {
+  constexpr int TS = BT * GK;  // doubles of one operand tile
+  // [A buffer 0 | A buffer 1 | B buffer 0 | B buffer 1]
+  __shared__ __attribute__((aligned(16))) double vS[4 * TS];
+  const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+  if (Ci) {
+#pragma unroll
+    for (int x = 0; x < 4; ++x)
+#pragma unroll
+      for (int y = 0; y < 4; ++y)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = r0 + mma128_row(wave, x, IL) + mf_row(lane, r);
+          const int col = c0 + mma128_col(wave, y, ILC) + mf_col(lane);
+          acc[x][y][r] = (row < M && col < N) ? Ci[(int64_t)row * ldci + col] : 0.0;
+        }
+  } else {
+#pragma unroll
+    for (int x = 0; x < 4; ++x)
+#pragma unroll
+      for (int y = 0; y < 4; ++y) acc[x][y] = (d4_t){0.0, 0.0, 0.0, 0.0};
+  }
+  const bool vec = ((lda | ldb) & 1) == 0 && ((((uintptr_t)A) | ((uintptr_t)B)) & 15) == 0;
+  // staging map: instruction j of this wave fills tile row (4 wave + j) * 8 + lane / 8,
+  // slot lane % 8, with the row's chunk (lane % 8) ^ ((row >> 1) & 7)
+  const int rs = (4 * wave) * 8 + (lane >> 3);
+  auto st_row = [&](int j) { return rs + 8 * j; };
+  auto st_chunk = [&](int j) { return (lane & 7) ^ ((st_row(j) >> 1) & 7); };
+  // The DMA is issued from inline asm: the compiler does not see it as an LDS write, so it
+  // adds no wait before the fragment reads of the other buffer (which it cannot tell apart
+  // from the DMA's); every step ends on an explicit vmcnt(0) + barrier instead.
+  auto dma = [](const double *g, const double *l) {
+    const uint32_t lds = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void *)l;
+    int keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\t"
+                 "s_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(g), "s"(__builtin_amdgcn_readfirstlane(lds))
+                 : "memory");
+  };
+  auto stage = [&](int buf, int k0) {
+    double *LA = vS + buf * TS, *LB = vS + (2 + buf) * TS;
+    if (vec && k0 + GK <= k_hi) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int r = st_row(j), c = st_chunk(j);
+        const double *sa = r0 + r < M ? A + (int64_t)(r0 + r) * lda + k0 + 2 * c : g_mma_zero;
+        const double *sb = c0 + r < N ? B + (int64_t)(c0 + r) * ldb + k0 + 2 * c : g_mma_zero;
+        dma(sa, LA + (4 * wave + j) * 128);  // this instruction's 1 KB (wave-uniform)
+        dma(sb, LB + (4 * wave + j) * 128);
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int r = st_row(j), k = k0 + 2 * st_chunk(j);
+        const bool ra = r0 + r < M, rb = c0 + r < N;
+        const double *pa = A + (int64_t)(ra ? r0 + r : 0) * lda;
+        const double *pb = B + (int64_t)(rb ? c0 + r : 0) * ldb;
+        const double a0 = ra && k < k_hi ? pa[k] : 0.0, a1 = ra && k + 1 < k_hi ? pa[k + 1] : 0.0;
+        const double b0 = rb && k < k_hi ? pb[k] : 0.0, b1 = rb && k + 1 < k_hi ? pb[k + 1] : 0.0;
+        *(double2 *)(LA + (4 * wave + j) * 128 + 2 * lane) = make_double2(a0, a1);
+        *(double2 *)(LB + (4 * wave + j) * 128 + 2 * lane) = make_double2(b0, b1);
+      }
+    }
+  };
+  // fragment reads: row R = (16-aligned block row) + lane % 16, so (R >> 1) & 7 = (lane % 16) / 2
+  const int sw = (lane & 15) >> 1;
+  const int foff0 = (lane & 15) * 16 + 2 * ((2 * (lane >> 4)) ^ sw);      // k = 4 (lane >> 4) + {0, 1}
+  const int foff1 = (lane & 15) * 16 + 2 * ((2 * (lane >> 4) + 1) ^ sw);  // k = 4 (lane >> 4) + {2, 3}
+  stage(0, k_lo);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  int cur = 0;
+  const int R0 = r0 + mma128_row(wave, 0, IL), R1 = r0 + mma128_row(wave, 1, IL);
+  const int R2 = r0 + mma128_row(wave, 2, IL), R3 = r0 + mma128_row(wave, 3, IL);
+  int k0 = k_lo;
+#define MMA2_PHASE_M(MASK, KEND)                                                              \
+  for (const int ke_ = (KEND); k0 < ke_; k0 += GK) {                                          \
+    if (k0 + GK < k_hi) stage(cur ^ 1, k0 + GK);                                              \
+    const double *la = vS + cur * TS, *lb = vS + (2 + cur) * TS;                              \
+    double2 fa[2][4], fb[2][4];                                                               \
+    _Pragma("unroll") for (int x = 0; x < 4; ++x) if (((MASK) >> (4 * x)) & 15) {             \
+      fa[0][x] = *(const double2 *)(la + mma128_row(wave, x, IL) * 16 + foff0);               \
+      fa[1][x] = *(const double2 *)(la + mma128_row(wave, x, IL) * 16 + foff1);               \
+    }                                                                                         \
+    _Pragma("unroll") for (int y = 0; y < 4; ++y) {                                           \
+      fb[0][y] = *(const double2 *)(lb + mma128_col(wave, y, ILC) * 16 + foff0);              \
+      fb[1][y] = *(const double2 *)(lb + mma128_col(wave, y, ILC) * 16 + foff1);              \
+    }                                                                                         \
+    _Pragma("unroll") for (int q = 0; q < 4; ++q)                                             \
+      _Pragma("unroll") for (int x = 0; x < 4; ++x)                                           \
+        _Pragma("unroll") for (int y = 0; y < 4; ++y)                                         \
+          if (((MASK) >> (4 * x + y)) & 1) {                                                  \
+            const double av = (q & 1) ? fa[q >> 1][x].y : fa[q >> 1][x].x;                    \
+            const double bv = (q & 1) ? fb[q >> 1][y].y : fb[q >> 1][y].x;                    \
+            acc[x][y] = mfma_f64(av, bv, acc[x][y]);                                          \
+          }                                                                                   \
+    __builtin_amdgcn_sched_barrier(0); /* the DMA wait and the barrier stay behind the MFMAs */ \
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");                                          \
+    __syncthreads();                                                                          \
+    cur ^= 1;                                                                                 \
+  }
+#define MMA2_PHASE(XF, XL, KEND) MMA2_PHASE_M(((0xFFFF << (4 * (XF))) & (0xFFFF >> (4 * (4 - (XL))))), KEND)
+  if (tri_b) {
+    MMA2_PHASE_M(0xFFFF, min(k_hi, c0 + mma128_col(wave, 0, ILC) + 16))
+    MMA2_PHASE_M(0xEEEE, min(k_hi, c0 + mma128_col(wave, 1, ILC) + 16))
+    MMA2_PHASE_M(0xCCCC, min(k_hi, c0 + mma128_col(wave, 2, ILC) + 16))
+    MMA2_PHASE_M(0x8888, min(k_hi, c0 + mma128_col(wave, 3, ILC) + 16))
+  } else if (lower_out && r0 == c0) {
+    const int wi = wave >> 1, wj = wave & 1;
+    if (IL) {
+      if (wj == 0 && wi == 0) { MMA2_PHASE_M(0xFF71, k_hi) }
+      else if (wj == 0) { MMA2_PHASE_M(0xFFF3, k_hi) }
+      else if (wi == 0) { MMA2_PHASE_M(0x7100, k_hi) }
+      else { MMA2_PHASE_M(0xF300, k_hi) }
+    } else {
+      if (wi == wj) { MMA2_PHASE_M(0xF731, k_hi) }
+      else if (wi == 1) { MMA2_PHASE_M(0xFFFF, k_hi) }
+    }
+  } else if (tri_rows >= 0 && R3 + 15 < tri_rows) {
+    MMA2_PHASE(0, 4, min(k_hi, R0 + 16))
+    MMA2_PHASE(1, 4, min(k_hi, R1 + 16))
+    MMA2_PHASE(2, 4, min(k_hi, R2 + 16))
+    MMA2_PHASE(3, 4, min(k_hi, R3 + 16))
+  } else if (tri_rows < 0 || R3 < M) {
+    MMA2_PHASE(0, 4, k_hi)
+  } else if (R2 < M) {
+    MMA2_PHASE(0, 3, k_hi)
+  } else if (R1 < M) {
+    MMA2_PHASE(0, 2, k_hi)
+  } else if (R0 < M) {
+    MMA2_PHASE(0, 1, k_hi)
+  }
+#undef MMA2_PHASE
+#undef MMA2_PHASE_M
+  for (; k0 < k_hi; k0 += GK) {  // dead steps: staging only
+    if (k0 + GK < k_hi) stage(cur ^ 1, k0 + GK);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    cur ^= 1;
+  }
+}
+
+// The staging buffers a kernel declares for mma128_tile with default flags: none when the
+// LDS-DMA loop runs (it has its own), else the register-staged loop's double buffers.
+#if MMA_V2
+#define MMA128_STAGING(SA, SB) double(*SA)[BT][GP] = nullptr, (*SB)[BT][GP] = nullptr
+#else
+#define MMA128_STAGING(SA, SB) __shared__ double SA[2][BT][GP], SB[2][BT][GP]
+#endif
+
+// DMA: the LDS-DMA loop (mma128_tile_v2, on its own LDS buffers: sA / sB unused) where
+// the flags allow it; false keeps the register-staged loop on the caller's sA / sB
+template <bool IL = false, bool L2A = false, bool L2B = false, bool ILC = false, bool NEGA = false,
+          bool DMA = true>
 __device__ __forceinline__ void mma128_tile(const double *__restrict__ A, int64_t lda,
                                             const double *__restrict__ B, int64_t ldb, int M, int N,
                                             int r0, int c0, int k_lo, int k_hi,
                                             double (*sA)[BT][GP], double (*sB)[BT][GP],
                                             d4_t (&acc)[4][4], int tri_rows = -1, bool lower_out = false,
                                             bool tri_b = false, const double *Ci = nullptr, int64_t ldci = 0) {
+  if constexpr (mma128_dma<L2A, L2B, ILC, NEGA, DMA>()) {
+    mma128_tile_v2<IL, ILC>(A, lda, B, ldb, M, N, r0, c0, k_lo, k_hi, acc, tri_rows, lower_out, tri_b, Ci, ldci);
+    return;
+  }
   // the wave index through readfirstlane: the compiler then knows every per-wave
   // quantity (and the triangular skips below) is uniform
   const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
