@@ -309,7 +309,8 @@ __global__ __launch_bounds__(256, 2) void k_gemm128(int M, int N, int K, const d
     B += kbeg;
     K = min(K - kbeg, kc);
   }
-  MMA128_STAGING(sA, sB);
+  __shared__ double sA[2][BT][GP];
+  __shared__ double sB[2][BT][GP];
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int qi = (wave >> 1) * 64, qj = (wave & 1) * 64;
   int kend = K;
@@ -755,7 +756,8 @@ __global__ __launch_bounds__(256, 2) void k_gemm128_sk(int M, int N, int K,
                                                        double alpha, int tri, int tx, int T,
                                                        int64_t sA_, int64_t sB_, int64_t sC_,
                                                        int64_t total) {
-  MMA128_STAGING(sA, sB);
+  __shared__ double sA[2][BT][GP];
+  __shared__ double sB[2][BT][GP];
   const int kiters = (K + GK - 1) / GK;
   int64_t u = (int64_t)blockIdx.x * total / gridDim.x;
   const int64_t u1 = (int64_t)(blockIdx.x + 1) * total / gridDim.x;

@@ -44,9 +44,9 @@ __device__ __forceinline__ int mma128_col(int wave, int y, bool ilc) {
 #define MMA_V2 1
 #endif
 
-// whether mma128_tile takes the LDS-DMA loop (its callers size their own LDS by it)
+// whether mma128_tile takes the LDS-DMA loop
 template <bool L2A, bool L2B, bool ILC, bool NEGA, bool DMA>
-constexpr bool mma128_dma() { return MMA_V2 && DMA && !L2A && !L2B && !NEGA && !ILC; }
+constexpr bool mma128_dma() { return MMA_V2 && DMA && !L2A && !L2B && !ILC; }
 
 // A zero 16-byte chunk: the LDS-DMA source of a tile's padding rows.
 static __device__ double g_mma_zero[2] = {0.0, 0.0};
@@ -60,17 +60,16 @@ static __device__ double g_mma_zero[2] = {0.0, 0.0};
 // K step reads k = 4 (lane >> 4) + q (A and B alike), so one ds_read_b128 serves two
 // substeps and a lane's four k's are two reads.  The step with a partial K slice (k_hi
 // not a multiple of GK) and operands without 16-byte alignment are staged through
-// registers in the same layout, zero filled.  Same tile semantics as mma128_tile; the
+// registers in the same layout, zero filled.  NEGA: the A fragments are negated as they
+// are read (fma(-a, b, c): the bits of staging -A).  Same tile semantics as mma128_tile; the
 // sums run in another k order (not the same bits as the register-staged loop).
-template <bool IL, bool ILC>
+template <bool IL, bool ILC, bool NEGA>
 __device__ __forceinline__ void mma128_tile_v2(const double *__restrict__ A, int64_t lda,
                                                const double *__restrict__ B, int64_t ldb, int M, int N,
-                                               int r0, int c0, int k_lo, int k_hi, d4_t (&acc)[4][4],
-                                               int tri_rows, bool lower_out, bool tri_b, const double *Ci,
-                                               int64_t ldci) {
-  constexpr int TS = BT * GK;  // doubles of one operand tile
-  // [A buffer 0 | A buffer 1 | B buffer 0 | B buffer 1]
-  __shared__ __attribute__((aligned(16))) double vS[4 * TS];
+                                               int r0, int c0, int k_lo, int k_hi, double *sA, double *sB,
+                                               d4_t (&acc)[4][4], int tri_rows, bool lower_out, bool tri_b,
+                                               const double *Ci, int64_t ldci) {
+  constexpr int TS = BT * GK;  // doubles of one operand tile: two per operand fit the caller's sA / sB
   const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
   if (Ci) {
 #pragma unroll
@@ -108,7 +107,7 @@ __device__ __forceinline__ void mma128_tile_v2(const double *__restrict__ A, int
                  : "memory");
   };
   auto stage = [&](int buf, int k0) {
-    double *LA = vS + buf * TS, *LB = vS + (2 + buf) * TS;
+    double *LA = sA + buf * TS, *LB = sB + buf * TS;
     if (vec && k0 + GK <= k_hi) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
@@ -146,11 +145,15 @@ __device__ __forceinline__ void mma128_tile_v2(const double *__restrict__ A, int
 #define MMA2_PHASE_M(MASK, KEND)                                                              \
   for (const int ke_ = (KEND); k0 < ke_; k0 += GK) {                                          \
     if (k0 + GK < k_hi) stage(cur ^ 1, k0 + GK);                                              \
-    const double *la = vS + cur * TS, *lb = vS + (2 + cur) * TS;                              \
+    const double *la = sA + cur * TS, *lb = sB + cur * TS;                                    \
     double2 fa[2][4], fb[2][4];                                                               \
     _Pragma("unroll") for (int x = 0; x < 4; ++x) if (((MASK) >> (4 * x)) & 15) {             \
       fa[0][x] = *(const double2 *)(la + mma128_row(wave, x, IL) * 16 + foff0);               \
       fa[1][x] = *(const double2 *)(la + mma128_row(wave, x, IL) * 16 + foff1);               \
+      if (NEGA) {                                                                             \
+        fa[0][x].x = -fa[0][x].x; fa[0][x].y = -fa[0][x].y;                                   \
+        fa[1][x].x = -fa[1][x].x; fa[1][x].y = -fa[1][x].y;                                   \
+      }                                                                                       \
     }                                                                                         \
     _Pragma("unroll") for (int y = 0; y < 4; ++y) {                                           \
       fb[0][y] = *(const double2 *)(lb + mma128_col(wave, y, ILC) * 16 + foff0);              \
@@ -210,16 +213,8 @@ __device__ __forceinline__ void mma128_tile_v2(const double *__restrict__ A, int
   }
 }
 
-// The staging buffers a kernel declares for mma128_tile with default flags: none when the
-// LDS-DMA loop runs (it has its own), else the register-staged loop's double buffers.
-#if MMA_V2
-#define MMA128_STAGING(SA, SB) double(*SA)[BT][GP] = nullptr, (*SB)[BT][GP] = nullptr
-#else
-#define MMA128_STAGING(SA, SB) __shared__ double SA[2][BT][GP], SB[2][BT][GP]
-#endif
-
-// DMA: the LDS-DMA loop (mma128_tile_v2, on its own LDS buffers: sA / sB unused) where
-// the flags allow it; false keeps the register-staged loop on the caller's sA / sB
+// DMA: the LDS-DMA loop (mma128_tile_v2, in the caller's sA / sB) where the flags allow
+// it; false keeps the register-staged loop
 template <bool IL = false, bool L2A = false, bool L2B = false, bool ILC = false, bool NEGA = false,
           bool DMA = true>
 __device__ __forceinline__ void mma128_tile(const double *__restrict__ A, int64_t lda,
@@ -229,7 +224,8 @@ __device__ __forceinline__ void mma128_tile(const double *__restrict__ A, int64_
                                             d4_t (&acc)[4][4], int tri_rows = -1, bool lower_out = false,
                                             bool tri_b = false, const double *Ci = nullptr, int64_t ldci = 0) {
   if constexpr (mma128_dma<L2A, L2B, ILC, NEGA, DMA>()) {
-    mma128_tile_v2<IL, ILC>(A, lda, B, ldb, M, N, r0, c0, k_lo, k_hi, acc, tri_rows, lower_out, tri_b, Ci, ldci);
+    mma128_tile_v2<IL, ILC, NEGA>(A, lda, B, ldb, M, N, r0, c0, k_lo, k_hi, &sA[0][0][0], &sB[0][0][0], acc,
+                                  tri_rows, lower_out, tri_b, Ci, ldci);
     return;
   }
   // the wave index through readfirstlane: the compiler then knows every per-wave
