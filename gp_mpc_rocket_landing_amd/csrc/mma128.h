@@ -43,10 +43,13 @@ __device__ __forceinline__ int mma128_col(int wave, int y, bool ilc) {
 #ifndef MMA_V2
 #define MMA_V2 1
 #endif
+#ifndef MMA_V2_ALL
+#define MMA_V2_ALL 1  // also the agent-scope (L2A / L2B) and column-interleaved (ILC) tiles
+#endif
 
 // whether mma128_tile takes the LDS-DMA loop
 template <bool L2A, bool L2B, bool ILC, bool NEGA, bool DMA>
-constexpr bool mma128_dma() { return MMA_V2 && DMA && !L2A && !L2B && !ILC; }
+constexpr bool mma128_dma() { return MMA_V2 && DMA && (MMA_V2_ALL || (!L2A && !L2B && !ILC)); }
 
 // A zero 16-byte chunk: the LDS-DMA source of a tile's padding rows.
 static __device__ double g_mma_zero[2] = {0.0, 0.0};
@@ -63,7 +66,7 @@ static __device__ double g_mma_zero[2] = {0.0, 0.0};
 // registers in the same layout, zero filled.  NEGA: the A fragments are negated as they
 // are read (fma(-a, b, c): the bits of staging -A).  Same tile semantics as mma128_tile; the
 // sums run in another k order (not the same bits as the register-staged loop).
-template <bool IL, bool ILC, bool NEGA>
+template <bool IL, bool ILC, bool NEGA, bool L2A, bool L2B>
 __device__ __forceinline__ void mma128_tile_v2(const double *__restrict__ A, int64_t lda,
                                                const double *__restrict__ B, int64_t ldb, int M, int N,
                                                int r0, int c0, int k_lo, int k_hi, double *sA, double *sB,
@@ -97,14 +100,23 @@ __device__ __forceinline__ void mma128_tile_v2(const double *__restrict__ A, int
   // The DMA is issued from inline asm: the compiler does not see it as an LDS write, so it
   // adds no wait before the fragment reads of the other buffer (which it cannot tell apart
   // from the DMA's); every step ends on an explicit vmcnt(0) + barrier instead.
-  auto dma = [](const double *g, const double *l) {
+  // (sc1: the agent-scope form of L2A / L2B, past the vector L1 that this workgroup's own
+  // stores do not refresh)
+  auto dma = [](const double *g, const double *l, bool sc1) {
     const uint32_t lds = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void *)l;
     int keep;
-    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\t"
-                 "s_mov_b32 m0, %0"
-                 : "=&s"(keep)
-                 : "v"(g), "s"(__builtin_amdgcn_readfirstlane(lds))
-                 : "memory");
+    if (sc1)
+      asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off sc1\n\t"
+                   "s_mov_b32 m0, %0"
+                   : "=&s"(keep)
+                   : "v"(g), "s"(__builtin_amdgcn_readfirstlane(lds))
+                   : "memory");
+    else
+      asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\t"
+                   "s_mov_b32 m0, %0"
+                   : "=&s"(keep)
+                   : "v"(g), "s"(__builtin_amdgcn_readfirstlane(lds))
+                   : "memory");
   };
   auto stage = [&](int buf, int k0) {
     double *LA = sA + buf * TS, *LB = sB + buf * TS;
@@ -114,8 +126,8 @@ __device__ __forceinline__ void mma128_tile_v2(const double *__restrict__ A, int
         const int r = st_row(j), c = st_chunk(j);
         const double *sa = r0 + r < M ? A + (int64_t)(r0 + r) * lda + k0 + 2 * c : g_mma_zero;
         const double *sb = c0 + r < N ? B + (int64_t)(c0 + r) * ldb + k0 + 2 * c : g_mma_zero;
-        dma(sa, LA + (4 * wave + j) * 128);  // this instruction's 1 KB (wave-uniform)
-        dma(sb, LB + (4 * wave + j) * 128);
+        dma(sa, LA + (4 * wave + j) * 128, L2A);  // this instruction's 1 KB (wave-uniform)
+        dma(sb, LB + (4 * wave + j) * 128, L2B);
       }
     } else {
 #pragma unroll
@@ -124,8 +136,11 @@ __device__ __forceinline__ void mma128_tile_v2(const double *__restrict__ A, int
         const bool ra = r0 + r < M, rb = c0 + r < N;
         const double *pa = A + (int64_t)(ra ? r0 + r : 0) * lda;
         const double *pb = B + (int64_t)(rb ? c0 + r : 0) * ldb;
-        const double a0 = ra && k < k_hi ? pa[k] : 0.0, a1 = ra && k + 1 < k_hi ? pa[k + 1] : 0.0;
-        const double b0 = rb && k < k_hi ? pb[k] : 0.0, b1 = rb && k + 1 < k_hi ? pb[k + 1] : 0.0;
+        auto ld = [](const double *p, bool agent) {
+          return agent ? __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : *p;
+        };
+        const double a0 = ra && k < k_hi ? ld(pa + k, L2A) : 0.0, a1 = ra && k + 1 < k_hi ? ld(pa + k + 1, L2A) : 0.0;
+        const double b0 = rb && k < k_hi ? ld(pb + k, L2B) : 0.0, b1 = rb && k + 1 < k_hi ? ld(pb + k + 1, L2B) : 0.0;
         *(double2 *)(LA + (4 * wave + j) * 128 + 2 * lane) = make_double2(a0, a1);
         *(double2 *)(LB + (4 * wave + j) * 128 + 2 * lane) = make_double2(b0, b1);
       }
@@ -224,7 +239,7 @@ __device__ __forceinline__ void mma128_tile(const double *__restrict__ A, int64_
                                             d4_t (&acc)[4][4], int tri_rows = -1, bool lower_out = false,
                                             bool tri_b = false, const double *Ci = nullptr, int64_t ldci = 0) {
   if constexpr (mma128_dma<L2A, L2B, ILC, NEGA, DMA>()) {
-    mma128_tile_v2<IL, ILC, NEGA>(A, lda, B, ldb, M, N, r0, c0, k_lo, k_hi, &sA[0][0][0], &sB[0][0][0], acc,
+    mma128_tile_v2<IL, ILC, NEGA, L2A, L2B>(A, lda, B, ldb, M, N, r0, c0, k_lo, k_hi, &sA[0][0][0], &sB[0][0][0], acc,
                                   tri_rows, lower_out, tri_b, Ci, ldci);
     return;
   }
