@@ -152,6 +152,12 @@ __device__ __forceinline__ int ft_factor(S &s, int cw) {
 #ifndef FT_PF2
 #define FT_PF2 0
 #endif
+// FT_DIAG_UNROLL 1: the diagonal phase's three rounds unrolled, their LDS reads in flight
+// together (control kernel 306 -> 293 us at 1024 landings, two runs each, although the
+// unrolled rounds' registers raise the kernel's spills 7 -> 54 VGPRs; same bits)
+#ifndef FT_DIAG_UNROLL
+#define FT_DIAG_UNROLL 1
+#endif
 
 // init + sum_j g[j] bcast_j(src) (two accumulators, as dot_bc_init), reloading
 // g[j] from nx[j * ST] right after its FMA when rl
@@ -308,7 +314,11 @@ __device__ __forceinline__ void ft_solve(S &s, double *b, int cw) {
     // either wave); rows past the last block read the last block and do not store
     const int q = (int)(threadIdx.x >> 4);
     constexpr int RB = FQ_T / 16, NR = (FT_NB + RB - 1) / RB;
+#if FT_DIAG_UNROLL
+#pragma unroll
+#else
 #pragma unroll 1
+#endif
     for (int t = 0; t < NR; ++t) {
       const int kk = RB * t + q, k = kk < FT_NB ? kk : FT_NB - 1;
       const double *Sk = F + k * FT_BS;

@@ -8,7 +8,7 @@
 #include <cstdint>
 typedef double d4_t __attribute__((ext_vector_type(4)));
 #define MF(acc, a, b) asm volatile("v_mfma_f64_16x16x4_f64 %0, %1, %2, %0" : "+v"(acc) : "v"(a), "v"(b))
-template <bool BAR, bool LDS, bool DMA>
+template <bool BAR, bool LDS, bool DMA, int AHEAD = 1>
 __global__ __launch_bounds__(256, 2) void k_loop(int steps, const double *src, double *out) {
   __shared__ __attribute__((aligned(16))) double S[4 * 2048];
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -51,7 +51,8 @@ __global__ __launch_bounds__(256, 2) void k_loop(int steps, const double *src, d
           MF(acc[4 * x + y], a, b);
         }
     __builtin_amdgcn_sched_barrier(0);
-    if (DMA) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (DMA && AHEAD == 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (DMA && AHEAD == 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
     if (BAR) __syncthreads();
     cur ^= 1;
   }
@@ -60,14 +61,14 @@ __global__ __launch_bounds__(256, 2) void k_loop(int steps, const double *src, d
   for (int i = 0; i < 16; ++i) t += acc[i][0] + acc[i][1] + acc[i][2] + acc[i][3];
   out[blockIdx.x * 256 + tid] = t;
 }
-template <bool BAR, bool LDS, bool DMA>
+template <bool BAR, bool LDS, bool DMA, int AHEAD = 1>
 void run(const char *name, const double *src, double *out) {
   const int wgs = 512, steps = 2000;
-  hipLaunchKernelGGL((k_loop<BAR, LDS, DMA>), dim3(wgs), dim3(256), 0, 0, steps, src, out);
+  hipLaunchKernelGGL((k_loop<BAR, LDS, DMA, AHEAD>), dim3(wgs), dim3(256), 0, 0, steps, src, out);
   hipEvent_t e0, e1;
   hipEventCreate(&e0); hipEventCreate(&e1);
   hipEventRecord(e0);
-  hipLaunchKernelGGL((k_loop<BAR, LDS, DMA>), dim3(wgs), dim3(256), 0, 0, steps, src, out);
+  hipLaunchKernelGGL((k_loop<BAR, LDS, DMA, AHEAD>), dim3(wgs), dim3(256), 0, 0, steps, src, out);
   hipEventRecord(e1);
   hipEventSynchronize(e1);
   float ms; hipEventElapsedTime(&ms, e0, e1);
@@ -85,5 +86,7 @@ int main() {
   run<true, true, false>("mfma+lds+bar", src, out);
   run<true, true, true>("mfma+lds+bar+dma", src, out);
   run<true, false, true>("mfma+bar+dma", src, out);
+  run<true, true, true, 2>("...+dma 2 ahead", src, out);
+  run<true, false, true, 2>("bar+dma 2 ahead", src, out);
   return 0;
 }
