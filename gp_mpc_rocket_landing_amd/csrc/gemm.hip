@@ -911,6 +911,71 @@ hipError_t launch_gemm_lat(hipStream_t s, int mode, int M, int N, int K, const d
   return hipGetLastError();
 }
 
+// ---------------------------------------------------------------------------
+// Skinny products (M or N <= 32) with a long K -- the GEMVs of alpha = W^T (W y), the
+// append's B^T = K21 W^T, S -= B^T B: on the 64-tile kernel they were a few workgroups
+// each walking K / 16 dependent steps (70-90 us at K = 1000).  K is cut into S chunks
+// (multiples of GK) whose partial products go to scratch slot 5 as a batch of the
+// 64-tile kernel, then k_splitk_reduce forms C = alpha sum_s P_s + beta C in chunk order
+// (deterministic; the sums run in another order than the one-pass product).
+__global__ __launch_bounds__(256) void k_splitk_reduce(int M, int N, int S, const double *__restrict__ P,
+                                                       double *__restrict__ C, int64_t ldc, double alpha,
+                                                       double beta) {
+  const int64_t MN = (int64_t)M * N;
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < MN; e += (int64_t)gridDim.x * 256) {
+    double acc = 0.0;
+    for (int q = 0; q < S; ++q) acc += P[q * MN + e];
+    const int i = (int)(e / N), j = (int)(e - (int64_t)i * N);
+    double *c = C + (int64_t)i * ldc + j;
+    *c = beta == 0.0 ? alpha * acc : alpha * acc + beta * *c;
+  }
+}
+
+static bool splitk_env() {
+  static const int v = [] {
+    const char *e = getenv("GPMPC_SPLITK");
+    return e ? atoi(e) : 1;
+  }();
+  return v != 0;
+}
+
+// form: 0 NT (A M x K, B N x K), 1 NN (B K x N), 2 TN (A K x M, B K x N).  Returns false
+// (nothing launched) when the product is not skinny enough or scratch is unavailable.
+static bool launch_splitk(hipStream_t s, int form, int M, int N, int K, const double *A, int64_t lda,
+                          const double *B, int64_t ldb, double *C, int64_t ldc, double alpha, double beta,
+                          hipError_t &err) {
+  if (!splitk_env() || !(M <= 32 || N <= 32) || K < 256) return false;
+  const int tiles = ((M + GT - 1) / GT) * ((N + GT - 1) / GT);
+  int S = std::max(1, std::min(512 / tiles, K / 64));
+  if (S < 2) return false;
+  const int kc = ((K + S - 1) / S + GK - 1) / GK * GK;
+  S = (K + kc - 1) / kc;
+  const int64_t MN = (int64_t)M * N;
+  double *P = (double *)gpmpc_scratch(s, 5, sizeof(double) * MN * S);
+  if (!P) return false;
+  // chunk q: A and B advance by kc along K
+  const int64_t sA = form == 2 ? (int64_t)kc * lda : kc, sB = form == 0 ? kc : (int64_t)kc * ldb;
+  const int full = (K % kc == 0) ? S : S - 1;
+  const dim3 g((N + GT - 1) / GT, (M + GT - 1) / GT, full);
+  auto go = [&](dim3 grid, int Kc, const double *a, const double *b, double *c) {
+    if (form == 0)
+      hipLaunchKernelGGL((k_gemm_nt<EPI_STORE, 0, 0>), grid, dim3(256), 0, s, M, N, Kc, a, lda, b, ldb, c,
+                         (int64_t)N, 1.0, 0.0, 0, 0, sA, sB, MN, M, nullptr, (int64_t)0, 0, 0);
+    else if (form == 1)
+      hipLaunchKernelGGL((k_gemm_nt<EPI_STORE, 1, 0>), grid, dim3(256), 0, s, M, N, Kc, a, lda, b, ldb, c,
+                         (int64_t)N, 1.0, 0.0, 0, 0, sA, sB, MN, M, nullptr, (int64_t)0, 0, 0);
+    else
+      hipLaunchKernelGGL((k_gemm_nt<EPI_STORE, 1, 1>), grid, dim3(256), 0, s, M, N, Kc, a, lda, b, ldb, c,
+                         (int64_t)N, 1.0, 0.0, 0, 0, sA, sB, MN, M, nullptr, (int64_t)0, 0, 0);
+  };
+  if (full > 0) go(g, kc, A, B, P);
+  if (full < S) go(dim3(g.x, g.y, 1), K - full * kc, A + full * sA, B + full * sB, P + full * MN);
+  const int rb = (int)std::min<int64_t>((MN + 255) / 256, 1024);
+  hipLaunchKernelGGL(k_splitk_reduce, dim3(rb), dim3(256), 0, s, M, N, S, P, C, ldc, alpha, beta);
+  err = hipGetLastError();
+  return true;
+}
+
 static hipError_t launch_gemm_impl(hipStream_t s, int epi, int M, int N, int K, const double *A,
                                    int64_t lda, const double *B, int64_t ldb, double *C,
                                    int64_t ldc, double alpha, double beta, int tri_a, int lower_c,
@@ -990,6 +1055,10 @@ static hipError_t launch_gemm_impl(hipStream_t s, int epi, int M, int N, int K, 
                          (post_xcd() && batch == 1 && tx % 8 == 0) ? 2 : 0);
     return hipGetLastError();
   }
+  if (epi == EPI_STORE && batch == 1 && !tri_a && !lower_c) {
+    hipError_t e = hipSuccess;
+    if (launch_splitk(s, 0, M, N, K, A, lda, B, ldb, C, ldc, alpha, beta, e)) return e;
+  }
   const int tx = (N + GT - 1) / GT, ty = (M + GT - 1) / GT;
   static const int remap_env = [] {
     const char *e = getenv("GPMPC_GEMM_REMAP");
@@ -1019,6 +1088,8 @@ hipError_t launch_gemm_nn(hipStream_t s, int M, int N, int K, const double *A, i
                           const double *B, int64_t ldb, double *C, int64_t ldc, double alpha,
                           double beta) {
   if (M <= 0 || N <= 0) return hipSuccess;
+  hipError_t e = hipSuccess;
+  if (launch_splitk(s, 1, M, N, K, A, lda, B, ldb, C, ldc, alpha, beta, e)) return e;
   dim3 g((N + GT - 1) / GT, (M + GT - 1) / GT, 1);
   hipLaunchKernelGGL((k_gemm_nt<EPI_STORE, 1, 0>), g, dim3(256), 0, s, M, N, K, A, lda, B, ldb, C,
                      ldc, alpha, beta, 0, 0, (int64_t)0, (int64_t)0, (int64_t)0, M, nullptr,
@@ -1042,6 +1113,8 @@ hipError_t launch_gemm_tn(hipStream_t s, int M, int N, int K, const double *A, i
                           const double *B, int64_t ldb, double *C, int64_t ldc, double alpha,
                           double beta) {
   if (M <= 0 || N <= 0) return hipSuccess;
+  hipError_t e = hipSuccess;
+  if (launch_splitk(s, 2, M, N, K, A, lda, B, ldb, C, ldc, alpha, beta, e)) return e;
   dim3 g((N + GT - 1) / GT, (M + GT - 1) / GT, 1);
   hipLaunchKernelGGL((k_gemm_nt<EPI_STORE, 1, 1>), g, dim3(256), 0, s, M, N, K, A, lda, B, ldb, C,
                      ldc, alpha, beta, 0, 0, (int64_t)0, (int64_t)0, (int64_t)0, M, nullptr,

@@ -1391,14 +1391,8 @@ extern "C" int gpmpc_gp_append(gpmpc_ctx *ctx, gpmpc_gp *gp, const double *Xnew,
   GPMPC_HIP(launch_gemm_nt(s, EPI_STORE, k, k, n, Bt.as<double>(), n, Bt.as<double>(), n,
                            Sm.as<double>(), k, -1.0, 1.0, 0, 0, 1, 0, 0, 0));
   GPMPC_HIP(launch_potrf_batched(s, k, 1, Sm.as<double>(), k, 0, dinfo.as<int>()));
-  int info = 0;
-  GPMPC_HIP(hipMemcpyAsync(&info, dinfo.p, sizeof(int), hipMemcpyDeviceToHost, s));
-  GPMPC_HIP(hipStreamSynchronize(s));
-  if (info < 0) return gpmpc_potrf_info_error(info, "gp_append");
-  if (info) {
-    gpmpc_set_error("gp_append: Schur complement not positive definite (pivot %d); refit", info);
-    return GPMPC_ERR_NOT_PD;
-  }
+  // the pivot check comes with the one read-back below: nothing before the commit
+  // touches the handle, so a failed factor only discards the new buffers
   // Ls^-1 (lower) and the new rows of W: [-(Ls^-1 (B^T W)) | Ls^-1]
   hipLaunchKernelGGL(k_eye, dim3((k + 255) / 256, k), dim3(256), 0, s, k, Li.as<double>());
   GPMPC_HIP(launch_trsm_lower_ex(s, k, k, Sm.as<double>(), k, Li.as<double>(), k, 0, 1, nullptr));
@@ -1447,15 +1441,22 @@ extern "C" int gpmpc_gp_append(gpmpc_ctx *ctx, gpmpc_gp *gp, const double *Xnew,
   GPMPC_HIP(hipMemcpyAsync(W2.as<double>() + (size_t)m * m, alphaT.p, sizeof(double) * (size_t)no * m,
                            hipMemcpyDeviceToDevice, s));
   std::vector<double> hl(no), hm(no), hs(no);
+  int info = 0;
+  GPMPC_HIP(hipMemcpyAsync(&info, dinfo.p, sizeof(int), hipMemcpyDeviceToHost, s));
   GPMPC_HIP(hipMemcpyAsync(hm.data(), ym.p, sizeof(double) * no, hipMemcpyDeviceToHost, s));
   GPMPC_HIP(hipMemcpyAsync(hs.data(), ys.p, sizeof(double) * no, hipMemcpyDeviceToHost, s));
   GPMPC_HIP(hipMemcpyAsync(hl.data(), dlml.p, sizeof(double) * no, hipMemcpyDeviceToHost, s));
   GPMPC_HIP(hipStreamSynchronize(s));
+  if (info < 0) return gpmpc_potrf_info_error(info, "gp_append");
+  if (info) {
+    gpmpc_set_error("gp_append: Schur complement not positive definite (pivot %d); refit", info);
+    return GPMPC_ERR_NOT_PD;
+  }
   // commit: the new normalisation, then swap the grown buffers into the handle
-  // (nothing below can fail half-way: the copies are of buffers already sized)
+  // (nothing below can fail half-way: the copies are of buffers already sized; the
+  // device synchronisation at the end covers them)
   GPMPC_HIP(hipMemcpyAsync(g.ymean.p, ym.p, sizeof(double) * no, hipMemcpyDeviceToDevice, s));
   GPMPC_HIP(hipMemcpyAsync(g.ystd.p, ys.p, sizeof(double) * no, hipMemcpyDeviceToDevice, s));
-  GPMPC_HIP(hipStreamSynchronize(s));
   g.h_ymean = hm;
   g.h_ystd = hs;
   gp->L.swap(L2);
@@ -1469,7 +1470,6 @@ extern "C" int gpmpc_gp_append(gpmpc_ctx *ctx, gpmpc_gp *gp, const double *Xnew,
     g.Wf.release();
     g.Xp.release();
   }
-  GPMPC_HIP(hipStreamSynchronize(s));
   // the replaced buffers go back to the pool when this returns; another context's
   // stream may still be reading them (as gpmpc_gp_destroy)
   (void)hipDeviceSynchronize();
