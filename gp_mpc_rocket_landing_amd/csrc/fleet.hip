@@ -435,7 +435,10 @@ __global__ __launch_bounds__(256) void k_fleet_control(FleetArgs a) {
 // STAMPS: the diagnostic phase-cycle instance (gpmpc_fleet_set_stamps); the
 // production instance has no stamp code or state at all.
 template <bool STAMPS>
-__global__ __launch_bounds__(FQ_T) __attribute__((amdgpu_waves_per_eu(FQ_NW, FQ_NW))) void k_fleet_control2(FleetArgs a) {
+#ifndef FQ_WPE
+#define FQ_WPE FQ_NW  // waves per SIMD the register budget is sized for
+#endif
+__global__ __launch_bounds__(FQ_T) __attribute__((amdgpu_waves_per_eu(FQ_WPE, FQ_WPE))) void k_fleet_control2(FleetArgs a) {
   __shared__ FleetSmem s;
   __shared__ double sx[NX], st_tgt[NX];
   __shared__ int s_out;

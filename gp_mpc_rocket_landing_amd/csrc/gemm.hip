@@ -976,6 +976,66 @@ static bool launch_splitk(hipStream_t s, int form, int M, int N, int K, const do
   return true;
 }
 
+// The SUMSQ form of the same split for few columns (the posterior of one landing's 20
+// queries, a predict of a few points): v = sum_s P_s per element, then per 64-row tile t
+// part[t][j] = sum over its rows r < msum of v(r, j)^2 and the rows msum..M-1 to Cm -- the
+// 64-tile SUMSQ kernel's output layout (gemm_row_tiles rows), so consumers are unchanged.
+// Block t: wave w takes columns w, w + 4, ..., lane = row of the tile; the S partials of an
+// element are independent loads (in flight together), the column's sum of squares a wave
+// reduction.
+__global__ __launch_bounds__(256) void k_splitk_sumsq(int M, int N, int S, const double *__restrict__ P, int msum,
+                                                      double *__restrict__ part, int64_t ldp,
+                                                      double *__restrict__ Cm, int64_t ldm) {
+  const int t = blockIdx.x, lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int r = t * 64 + lane;
+  const int64_t MN = (int64_t)M * N;
+  for (int j = w; j < N; j += 4) {
+    double v = 0.0;
+    if (r < M) {
+      const double *pe = P + (int64_t)r * N + j;
+      double a[8];
+      int q = 0;
+      for (; q + 8 <= S; q += 8) {
+#pragma unroll
+        for (int u = 0; u < 8; ++u) a[u] = pe[(q + u) * MN];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v += a[u];
+      }
+      for (; q < S; ++q) v += pe[q * MN];
+    }
+    double sq = (r < msum) ? v * v : 0.0;
+    if (r >= msum && r < M) Cm[(int64_t)(r - msum) * ldm + j] = v;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) sq += __shfl_xor(sq, o);
+    if (lane == 0) part[(int64_t)t * ldp + j] = sq;
+  }
+}
+
+static bool launch_splitk_sumsq(hipStream_t s, int M, int N, int K, const double *A, int64_t lda, const double *B,
+                                int64_t ldb, double *part, int64_t ldp, int msum, double *Cm, int64_t ldm,
+                                hipError_t &err) {
+  if (!splitk_env() || N > GT || K < 256) return false;
+  const int ty = (M + GT - 1) / GT;
+  int S = std::max(1, std::min(512 / ty, K / 64));
+  if (S < 2) return false;
+  const int kc = ((K + S - 1) / S + GK - 1) / GK * GK;
+  S = (K + kc - 1) / kc;
+  const int64_t MN = (int64_t)M * N;
+  double *P = (double *)gpmpc_scratch(s, 5, sizeof(double) * MN * S);
+  if (!P) return false;
+  const int full = (K % kc == 0) ? S : S - 1;
+  if (full > 0)
+    hipLaunchKernelGGL((k_gemm_nt<EPI_STORE, 0, 0>), dim3(1, ty, full), dim3(256), 0, s, M, N, kc, A, lda, B, ldb,
+                       P, (int64_t)N, 1.0, 0.0, 0, 0, (int64_t)kc, (int64_t)kc, MN, M, nullptr, (int64_t)0, 0, 0);
+  if (full < S)
+    hipLaunchKernelGGL((k_gemm_nt<EPI_STORE, 0, 0>), dim3(1, ty, 1), dim3(256), 0, s, M, N, K - full * kc,
+                       A + (int64_t)full * kc, lda, B + (int64_t)full * kc, ldb, P + full * MN, (int64_t)N, 1.0, 0.0,
+                       0, 0, (int64_t)0, (int64_t)0, (int64_t)0, M, nullptr, (int64_t)0, 0, 0);
+  hipLaunchKernelGGL(k_splitk_sumsq, dim3(ty), dim3(256), 0, s, M, N, S, P, msum, part, ldp, Cm, ldm);
+  err = hipGetLastError();
+  return true;
+}
+
 static hipError_t launch_gemm_impl(hipStream_t s, int epi, int M, int N, int K, const double *A,
                                    int64_t lda, const double *B, int64_t ldb, double *C,
                                    int64_t ldc, double alpha, double beta, int tri_a, int lower_c,
@@ -1058,6 +1118,10 @@ static hipError_t launch_gemm_impl(hipStream_t s, int epi, int M, int N, int K, 
   if (epi == EPI_STORE && batch == 1 && !tri_a && !lower_c) {
     hipError_t e = hipSuccess;
     if (launch_splitk(s, 0, M, N, K, A, lda, B, ldb, C, ldc, alpha, beta, e)) return e;
+  }
+  if (epi == EPI_SUMSQ && batch == 1 && gemm_row_tiles(M, N, K) == (M + GT - 1) / GT) {
+    hipError_t e = hipSuccess;  // (a triangular A's zero chunks are multiplied: the split is latency work)
+    if (launch_splitk_sumsq(s, M, N, K, A, lda, B, ldb, C, ldc, msum, Cm, ldm, e)) return e;
   }
   const int tx = (N + GT - 1) / GT, ty = (M + GT - 1) / GT;
   static const int remap_env = [] {
