@@ -24,11 +24,15 @@
 #include <vector>
 #include <algorithm>
 
+#ifndef FQ_KNS
+#define FQ_KNS fq_narrow
+#endif
 #define NX 7
 #define NU 3
 #define NFEAT 11
 #define DYN_NNZ 26
 
+#ifndef FLEET_WIDE_TU  // (fleet_wide.hip compiles only the control kernel below)
 struct gpmpc_fleet {
   gpmpc_ctx *ctx = nullptr;
   gpmpc_gp *gp = nullptr;
@@ -48,6 +52,7 @@ struct gpmpc_fleet {
   unsigned long long *trace = nullptr;       // diagnostic (gpmpc_fleet_set_trace)
   bool use_order = true;                     // GPMPC_FLEET_ORDER=0 launches in landing order
   bool use_fq = true;                        // fleet-specialised solver (GPMPC_FLEET_SOLVER=0: generic)
+  bool wide = false;                         // its 256-thread build (fleet_wide.hip): fleets of <= 1 landing per CU
   int alt_wave = 0;                          // GPMPC_FLEET_ALTWAVE=1: alternate the chain wave
   DevBuf claims;                             // per-CU chain-SIMD claims (k_fleet_control2)
   DevBuf sqp_done;                           // SQP mode: landing converged this control step
@@ -110,6 +115,7 @@ static void mpc_pattern(int N, std::vector<int> &rp, std::vector<int> &ci) {
   (void)m;
 }
 
+#endif  // FLEET_WIDE_TU
 __device__ __forceinline__ void features3(const double *x, const double *u, double *z) {
   // Simple3DoFFeatureExtractor.extract (features.py:403-444)
   const double vx = x[4], vy = x[5], vz = x[6], alt = x[1];
@@ -125,6 +131,7 @@ __device__ __forceinline__ void features3(const double *x, const double *u, doub
 
 // GPMPC.solve's loop: X_pred[0] = x0 (gp_mpc.py:263) -- before the first pass of
 // a control step the unshifted plan's first point becomes the current state
+#ifndef FLEET_WIDE_TU
 __global__ void k_fleet_x0_to_plan(int B, int N, const double *__restrict__ x, const double *__restrict__ rec,
                                    double *__restrict__ Xw) {
   const int g = blockIdx.x * blockDim.x + threadIdx.x;
@@ -154,6 +161,7 @@ __global__ void k_fleet_queries(int B, int N, const double *__restrict__ Xw,
   Qn[g] = s;
 }
 
+#endif  // FLEET_WIDE_TU
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ void plant_euler(const double *x, const double *u, double dt,
                                             double *o) {
@@ -217,6 +225,10 @@ struct FleetArgs {
   int *sqp_done;               // landing converged in an earlier pass of this control step
 };
 
+// the 256-thread build of k_fleet_control2 (fleet_wide.hip)
+hipError_t launch_fleet_control_wide(hipStream_t s, int nb, const FleetArgs &a, bool stamps);
+
+#ifndef FLEET_WIDE_TU
 __global__ __launch_bounds__(256) void k_fleet_control(FleetArgs a) {
   __shared__ QPSmemStd s;
   __shared__ double sx[NX], st_tgt[NX];
@@ -434,6 +446,10 @@ __global__ __launch_bounds__(256) void k_fleet_control(FleetArgs a) {
 // straight into the owners' registers; results and the plant step as above.
 // STAMPS: the diagnostic phase-cycle instance (gpmpc_fleet_set_stamps); the
 // production instance has no stamp code or state at all.
+#endif  // FLEET_WIDE_TU
+// the control kernel lives in a namespace of its build: fleet.hip (128 threads, four
+// landings per CU) and fleet_wide.hip (256 threads, one wave per SIMD) each have one
+namespace FQ_KNS {
 template <bool STAMPS>
 #ifndef FQ_WPE
 #define FQ_WPE FQ_NW  // waves per SIMD the register budget is sized for
@@ -748,6 +764,17 @@ __global__ __launch_bounds__(FQ_T) __attribute__((amdgpu_waves_per_eu(FQ_WPE, FQ
   if (a.trace && tid == 0) a.trace[(int64_t)b * 4 + 1] = __builtin_amdgcn_s_memrealtime();
 }
 
+}  // namespace FQ_KNS
+
+#ifdef FLEET_WIDE_TU
+hipError_t launch_fleet_control_wide(hipStream_t s, int nb, const FleetArgs &a, bool stamps) {
+  if (stamps)
+    hipLaunchKernelGGL(FQ_KNS::k_fleet_control2<true>, dim3(nb), dim3(FQ_T), 0, s, a);
+  else
+    hipLaunchKernelGGL(FQ_KNS::k_fleet_control2<false>, dim3(nb), dim3(FQ_T), 0, s, a);
+  return hipGetLastError();
+}
+#else
 __global__ void k_fleet_reset(int first, int count, int N, int target_mode,
                               const double *__restrict__ x0, double *x, double *Xw, double *Uw,
                               double *ysc, int m, double *rho, double rho0, double *rec,
@@ -880,6 +907,15 @@ extern "C" int gpmpc_fleet_create(gpmpc_ctx *ctx, gpmpc_gp *gp, const gpmpc_flee
   // the specialised solver assumes the N = 20 stage layout of its LDS caps
   f->use_fq = (!se || atoi(se) != 0) && N == 20 && f->pat.mode == 1 && f->pat.nblk == FQ_NBLK &&
               m - n == FQ_MD && f->pat.nnz - n == FQ_NNZD;
+  // small fleets (at most one landing per CU) take the 256-thread, one-wave-per-SIMD build of
+  // the control kernel: twice the threads for the parallel ADMM phases and no register
+  // spills (single landing 216 -> 192 us per step); decided by the fleet size, not by the
+  // running count, so a fleet's landings always see the same arithmetic (GPMPC_FLEET_WIDE
+  // = 0 / 1 forces it)
+  int cus = 0;
+  (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device);
+  const char *we = getenv("GPMPC_FLEET_WIDE");
+  f->wide = f->use_fq && (we ? atoi(we) != 0 : (int)B <= cus);
   if (cfg->sqp_iters > 1 && !f->use_fq) {  // the SQP pass is implemented in k_fleet_control2
     delete f;
     gpmpc_set_error("fleet: sqp_iters > 1 needs the fleet solver (N = 20, GPMPC_FLEET_SOLVER != 0)");
@@ -1105,12 +1141,14 @@ extern "C" int gpmpc_fleet_step_phases(gpmpc_fleet *f, int phase_mask) {
   if (phase_mask & 2) {
     const int nb = f->use_order ? f->n_active : f->B;
     if (nb > 0) {
-      if (f->use_fq) {
+      if (f->use_fq && f->wide) {
+        GPMPC_HIP(launch_fleet_control_wide(f->ctx->stream, nb, fleet_args(f), f->stamps != nullptr));
+      } else if (f->use_fq) {
         if (f->stamps)
-          hipLaunchKernelGGL(k_fleet_control2<true>, dim3(nb), dim3(FQ_T), 0, f->ctx->stream,
+          hipLaunchKernelGGL(FQ_KNS::k_fleet_control2<true>, dim3(nb), dim3(FQ_T), 0, f->ctx->stream,
                              fleet_args(f));
         else
-          hipLaunchKernelGGL(k_fleet_control2<false>, dim3(nb), dim3(FQ_T), 0, f->ctx->stream,
+          hipLaunchKernelGGL(FQ_KNS::k_fleet_control2<false>, dim3(nb), dim3(FQ_T), 0, f->ctx->stream,
                              fleet_args(f));
       } else {
         hipLaunchKernelGGL(k_fleet_control, dim3(nb), dim3(256), 0, f->ctx->stream, fleet_args(f));
@@ -1218,3 +1256,5 @@ extern "C" int gpmpc_fleet_destroy(gpmpc_fleet *f) {
   delete f;
   return 0;
 }
+
+#endif  // FLEET_WIDE_TU
