@@ -154,7 +154,9 @@ __device__ __forceinline__ int ft_factor(S &s, int cw) {
 #endif
 // FT_DIAG_UNROLL 1: the diagonal phase's three rounds unrolled, their LDS reads in flight
 // together (control kernel 306 -> 293 us at 1024 landings, two runs each, although the
-// unrolled rounds' registers raise the kernel's spills 7 -> 54 VGPRs; same bits)
+// unrolled rounds' registers raise the kernel's spills 7 -> 54 VGPRs, its scratch traffic
+// 19.9 -> 47 MB per launch, L2-resident; a two-deep software pipeline of the rounds spills
+// 52 as well; same bits)
 #ifndef FT_DIAG_UNROLL
 #define FT_DIAG_UNROLL 1
 #endif
