@@ -161,6 +161,52 @@ __global__ void k_fleet_queries(int B, int N, const double *__restrict__ Xw,
   Qn[g] = s;
 }
 
+// The queries and K* in one launch for a fleet of at most 64 query rows (one to three
+// landings: the single-landing step): every workgroup forms all the rows' features in LDS
+// (k_fleet_queries' arithmetic) and its 64 training columns of K* as k_gram does (same
+// fma order, same kernel_epilogue: the same bits as the two-launch path).
+__global__ __launch_bounds__(256) void k_fleet_queries_gram(int B, int N, const double *__restrict__ Xw,
+                                                            const double *__restrict__ Uw,
+                                                            const double *__restrict__ ls, int iso,
+                                                            const int *__restrict__ order, int kind,
+                                                            const double *__restrict__ Xs,
+                                                            const double *__restrict__ Xn, int n, double sigma2,
+                                                            double iso_scale, double *__restrict__ Ks) {
+  __shared__ double sq[64][NFEAT + 1];
+  __shared__ double sqn[64];
+  const int P = B * N, tid = threadIdx.x;
+  if (tid < P) {
+    const int sl = tid / N, k = tid - sl * N;
+    const int b = order ? order[sl] : sl;
+    double z[NFEAT];
+    features3(Xw + ((int64_t)b * (N + 1) + k) * NX, Uw + ((int64_t)b * N + k) * NU, z);
+    double sn = 0.0;
+#pragma unroll
+    for (int f = 0; f < NFEAT; ++f) {
+      const double v = iso ? z[f] : z[f] / ls[f];
+      sq[tid][f] = v;
+      sn += v * v;
+    }
+    sqn[tid] = sn;
+  }
+  __syncthreads();
+  const int col = blockIdx.x * 64 + (tid & 63), rg = tid >> 6;
+  if (col >= n) return;
+  double bj[NFEAT];
+#pragma unroll
+  for (int k = 0; k < NFEAT; ++k) bj[k] = Xs[(int64_t)col * NFEAT + k];
+  const double nbj = Xn[col];
+  for (int rr = 0; rr < 16; ++rr) {
+    const int row = rg * 16 + rr;
+    if (row >= P) break;
+    double dot = 0.0;
+#pragma unroll
+    for (int k = 0; k < NFEAT; ++k) dot = fma(sq[row][k], bj[k], dot);
+    const double d2 = (sqn[row] + nbj) - 2.0 * dot;
+    Ks[(int64_t)row * n + col] = kernel_epilogue(kind, d2, sigma2, iso_scale);
+  }
+}
+
 #endif  // FLEET_WIDE_TU
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ void plant_euler(const double *x, const double *u, double dt,
@@ -961,13 +1007,18 @@ static hipError_t fleet_gp_posterior(gpmpc_fleet *f, int mask) {
     const char *v = getenv("GPMPC_POST_FUSED");
     return v ? atoi(v) : 0;
   }();
-  // default: the column-stationary posterior (post.hip), K* formed once per workgroup
-  // inside the MFMA pass, never in HBM; two partial rows
+  // GPMPC_POST_CS=1: the column-stationary posterior (post.hip), K* formed once per
+  // workgroup inside the MFMA pass, never in HBM; two partial rows
   const bool cs = g.Wf && post_cs_env();
   const bool fused = !cs && fused_env && g.d >= 11 && g.d <= 13;
   const int nrt = cs ? POST_CS_PARTS : fused ? (g.n + 3 + 127) / 128 : gemm_row_tiles(g.n + 3, (int)P, g.n);
   hipError_t e = hipSuccess;
-  if (mask & 1) {
+  if ((mask & 1) && !fused && !cs && P <= 64 && g.d == NFEAT) {
+    hipLaunchKernelGGL(k_fleet_queries_gram, dim3((g.n + 63) / 64), dim3(256), 0, s, nb, f->N, f->Xw.as<double>(),
+                       f->Uw.as<double>(), g.ls, g.kind == GPMPC_SE_ISO, f->use_order ? f->order.as<int>() : nullptr,
+                       g.kind, g.Xs, g.Xn, g.n, g.sigma2, g.iso_scale, f->Ks.as<double>());
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+  } else if (mask & 1) {
     hipLaunchKernelGGL(k_fleet_queries, dim3((P + 255) / 256), dim3(256), 0, s, nb, f->N,
                        f->Xw.as<double>(), f->Uw.as<double>(), g.ls, g.kind == GPMPC_SE_ISO,
                        f->use_order ? f->order.as<int>() : nullptr, f->Q.as<double>(),
@@ -1132,7 +1183,8 @@ extern "C" int gpmpc_fleet_step_phases(gpmpc_fleet *f, int phase_mask) {
                        f->cfg.horizon, f->x.as<double>(), f->rec.as<double>(), f->Xw.as<double>());
   // the dispatch order of this step, before the GP phase when there is one:
   // the posterior rows then follow the same slots as the control workgroups
-  const bool order_now = f->use_order && f->sqp_it == 0 &&
+  // (one landing: the identity order set at creation is the only one)
+  const bool order_now = f->use_order && f->sqp_it == 0 && f->B > 1 &&
                          ((f->cfg.use_gp && (phase_mask & 1)) || (!f->cfg.use_gp && (phase_mask & 2)));
   if (order_now)
     hipLaunchKernelGGL(k_fleet_order, dim3(1), dim3(1024), 0, f->ctx->stream, f->B,

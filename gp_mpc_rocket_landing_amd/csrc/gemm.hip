@@ -43,8 +43,11 @@ __global__ __launch_bounds__(256) void k_gemm_nt(int M, int N, int K, const doub
                                                  double alpha, double beta, int tri_a,
                                                  int lower_c, int64_t sA_, int64_t sB_,
                                                  int64_t sC_, int msum, double *__restrict__ Cm,
-                                                 int64_t ldm, int remap_ty, int xcd_batch) {
+                                                 int64_t ldm, int remap_ty, int xcd_batch, int klast) {
   int bz = blockIdx.z;
+  // klast > 0: the batch is the K chunks of a split product (launch_splitk): the last
+  // chunk is klast long instead of K
+  if (klast > 0 && !xcd_batch && (int)blockIdx.z == (int)gridDim.z - 1) K = klast;
   int bx = blockIdx.x, by = blockIdx.y;
   if (xcd_batch) {
     // lower-triangular batch, one matrix per XCD at a time: workgroup i runs
@@ -955,21 +958,17 @@ static bool launch_splitk(hipStream_t s, int form, int M, int N, int K, const do
   if (!P) return false;
   // chunk q: A and B advance by kc along K
   const int64_t sA = form == 2 ? (int64_t)kc * lda : kc, sB = form == 0 ? kc : (int64_t)kc * ldb;
-  const int full = (K % kc == 0) ? S : S - 1;
-  const dim3 g((N + GT - 1) / GT, (M + GT - 1) / GT, full);
-  auto go = [&](dim3 grid, int Kc, const double *a, const double *b, double *c) {
-    if (form == 0)
-      hipLaunchKernelGGL((k_gemm_nt<EPI_STORE, 0, 0>), grid, dim3(256), 0, s, M, N, Kc, a, lda, b, ldb, c,
-                         (int64_t)N, 1.0, 0.0, 0, 0, sA, sB, MN, M, nullptr, (int64_t)0, 0, 0);
-    else if (form == 1)
-      hipLaunchKernelGGL((k_gemm_nt<EPI_STORE, 1, 0>), grid, dim3(256), 0, s, M, N, Kc, a, lda, b, ldb, c,
-                         (int64_t)N, 1.0, 0.0, 0, 0, sA, sB, MN, M, nullptr, (int64_t)0, 0, 0);
-    else
-      hipLaunchKernelGGL((k_gemm_nt<EPI_STORE, 1, 1>), grid, dim3(256), 0, s, M, N, Kc, a, lda, b, ldb, c,
-                         (int64_t)N, 1.0, 0.0, 0, 0, sA, sB, MN, M, nullptr, (int64_t)0, 0, 0);
-  };
-  if (full > 0) go(g, kc, A, B, P);
-  if (full < S) go(dim3(g.x, g.y, 1), K - full * kc, A + full * sA, B + full * sB, P + full * MN);
+  const int klast = K - (S - 1) * kc;  // the last chunk's length (one launch for all chunks)
+  const dim3 g((N + GT - 1) / GT, (M + GT - 1) / GT, S);
+  if (form == 0)
+    hipLaunchKernelGGL((k_gemm_nt<EPI_STORE, 0, 0>), g, dim3(256), 0, s, M, N, kc, A, lda, B, ldb, P, (int64_t)N,
+                       1.0, 0.0, 0, 0, sA, sB, MN, M, nullptr, (int64_t)0, 0, 0, klast);
+  else if (form == 1)
+    hipLaunchKernelGGL((k_gemm_nt<EPI_STORE, 1, 0>), g, dim3(256), 0, s, M, N, kc, A, lda, B, ldb, P, (int64_t)N,
+                       1.0, 0.0, 0, 0, sA, sB, MN, M, nullptr, (int64_t)0, 0, 0, klast);
+  else
+    hipLaunchKernelGGL((k_gemm_nt<EPI_STORE, 1, 1>), g, dim3(256), 0, s, M, N, kc, A, lda, B, ldb, P, (int64_t)N,
+                       1.0, 0.0, 0, 0, sA, sB, MN, M, nullptr, (int64_t)0, 0, 0, klast);
   const int rb = (int)std::min<int64_t>((MN + 255) / 256, 1024);
   hipLaunchKernelGGL(k_splitk_reduce, dim3(rb), dim3(256), 0, s, M, N, S, P, C, ldc, alpha, beta);
   err = hipGetLastError();
@@ -980,7 +979,7 @@ static bool launch_splitk(hipStream_t s, int form, int M, int N, int K, const do
 // queries, a predict of a few points): v = sum_s P_s per element, then per 64-row tile t
 // part[t][j] = sum over its rows r < msum of v(r, j)^2 and the rows msum..M-1 to Cm -- the
 // 64-tile SUMSQ kernel's output layout (gemm_row_tiles rows), so consumers are unchanged.
-// Block t: wave w takes columns w, w + 4, ..., lane = row of the tile; the S partials of an
+// Block (t, c): wave w takes column 4 c + w, lane = row of the tile; the S partials of an
 // element are independent loads (in flight together), the column's sum of squares a wave
 // reduction.
 __global__ __launch_bounds__(256) void k_splitk_sumsq(int M, int N, int S, const double *__restrict__ P, int msum,
@@ -989,7 +988,7 @@ __global__ __launch_bounds__(256) void k_splitk_sumsq(int M, int N, int S, const
   const int t = blockIdx.x, lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int r = t * 64 + lane;
   const int64_t MN = (int64_t)M * N;
-  for (int j = w; j < N; j += 4) {
+  for (int j = 4 * (int)blockIdx.y + w; j < N; j += 4 * (int)gridDim.y) {
     double v = 0.0;
     if (r < M) {
       const double *pe = P + (int64_t)r * N + j;
@@ -1023,15 +1022,10 @@ static bool launch_splitk_sumsq(hipStream_t s, int M, int N, int K, const double
   const int64_t MN = (int64_t)M * N;
   double *P = (double *)gpmpc_scratch(s, 5, sizeof(double) * MN * S);
   if (!P) return false;
-  const int full = (K % kc == 0) ? S : S - 1;
-  if (full > 0)
-    hipLaunchKernelGGL((k_gemm_nt<EPI_STORE, 0, 0>), dim3(1, ty, full), dim3(256), 0, s, M, N, kc, A, lda, B, ldb,
-                       P, (int64_t)N, 1.0, 0.0, 0, 0, (int64_t)kc, (int64_t)kc, MN, M, nullptr, (int64_t)0, 0, 0);
-  if (full < S)
-    hipLaunchKernelGGL((k_gemm_nt<EPI_STORE, 0, 0>), dim3(1, ty, 1), dim3(256), 0, s, M, N, K - full * kc,
-                       A + (int64_t)full * kc, lda, B + (int64_t)full * kc, ldb, P + full * MN, (int64_t)N, 1.0, 0.0,
-                       0, 0, (int64_t)0, (int64_t)0, (int64_t)0, M, nullptr, (int64_t)0, 0, 0);
-  hipLaunchKernelGGL(k_splitk_sumsq, dim3(ty), dim3(256), 0, s, M, N, S, P, msum, part, ldp, Cm, ldm);
+  hipLaunchKernelGGL((k_gemm_nt<EPI_STORE, 0, 0>), dim3(1, ty, S), dim3(256), 0, s, M, N, kc, A, lda, B, ldb, P,
+                     (int64_t)N, 1.0, 0.0, 0, 0, (int64_t)kc, (int64_t)kc, MN, M, nullptr, (int64_t)0, 0, 0,
+                     K - (S - 1) * kc);
+  hipLaunchKernelGGL(k_splitk_sumsq, dim3(ty, (N + 3) / 4), dim3(256), 0, s, M, N, S, P, msum, part, ldp, Cm, ldm);
   err = hipGetLastError();
   return true;
 }
@@ -1140,10 +1134,10 @@ static hipError_t launch_gemm_impl(hipStream_t s, int epi, int M, int N, int K, 
   const int rt = tg ? -1 : remap ? ty : 0;
   if (epi == EPI_STORE)
     hipLaunchKernelGGL(k_gemm_nt<EPI_STORE>, g, dim3(256), 0, s, M, N, K, A, lda, B, ldb, C, ldc,
-                       alpha, beta, tri_a, lower_c, sA, sB, sC, M, nullptr, (int64_t)0, rt, xb);
+                       alpha, beta, tri_a, lower_c, sA, sB, sC, M, nullptr, (int64_t)0, rt, xb, 0);
   else
     hipLaunchKernelGGL(k_gemm_nt<EPI_SUMSQ>, g, dim3(256), 0, s, M, N, K, A, lda, B, ldb, C, ldc,
-                       alpha, beta, tri_a, 0, sA, sB, sC, msum, Cm, ldm, rt, 0);
+                       alpha, beta, tri_a, 0, sA, sB, sC, msum, Cm, ldm, rt, 0, 0);
   return hipGetLastError();
 }
 
@@ -1157,7 +1151,7 @@ hipError_t launch_gemm_nn(hipStream_t s, int M, int N, int K, const double *A, i
   dim3 g((N + GT - 1) / GT, (M + GT - 1) / GT, 1);
   hipLaunchKernelGGL((k_gemm_nt<EPI_STORE, 1, 0>), g, dim3(256), 0, s, M, N, K, A, lda, B, ldb, C,
                      ldc, alpha, beta, 0, 0, (int64_t)0, (int64_t)0, (int64_t)0, M, nullptr,
-                     (int64_t)0, 0, 0);
+                     (int64_t)0, 0, 0, 0);
   return hipGetLastError();
 }
 
@@ -1168,7 +1162,7 @@ hipError_t launch_gemm_nn_batched(hipStream_t s, int M, int N, int K, const doub
   if (M <= 0 || N <= 0 || batch <= 0) return hipSuccess;
   dim3 g((N + GT - 1) / GT, (M + GT - 1) / GT, batch);
   hipLaunchKernelGGL((k_gemm_nt<EPI_STORE, 1, 0>), g, dim3(256), 0, s, M, N, K, A, lda, B, ldb, C,
-                     ldc, alpha, beta, 0, 0, sA, sB, sC, M, nullptr, (int64_t)0, 0, 0);
+                     ldc, alpha, beta, 0, 0, sA, sB, sC, M, nullptr, (int64_t)0, 0, 0, 0);
   return hipGetLastError();
 }
 
@@ -1182,7 +1176,7 @@ hipError_t launch_gemm_tn(hipStream_t s, int M, int N, int K, const double *A, i
   dim3 g((N + GT - 1) / GT, (M + GT - 1) / GT, 1);
   hipLaunchKernelGGL((k_gemm_nt<EPI_STORE, 1, 1>), g, dim3(256), 0, s, M, N, K, A, lda, B, ldb, C,
                      ldc, alpha, beta, 0, 0, (int64_t)0, (int64_t)0, (int64_t)0, M, nullptr,
-                     (int64_t)0, 0, 0);
+                     (int64_t)0, 0, 0, 0);
   return hipGetLastError();
 }
 

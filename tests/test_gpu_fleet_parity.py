@@ -45,7 +45,7 @@ def _oracle_landing(st, x0, steps):
     return out
 
 
-def test_fleet_closed_loop_matches_oracle(gpu_ctx):
+def _closed_loop(gpu_ctx, nb, steps):
     from gp_mpc_rocket_landing_amd.data import synthetic_training_data
     from gp_mpc_rocket_landing_amd.fleet import (REC_ADMM_ITERS, REC_LAST_STATUS, REC_OUTCOME,
                                                  Fleet, fit_gp, initial_conditions)
@@ -53,21 +53,21 @@ def test_fleet_closed_loop_matches_oracle(gpu_ctx):
 
     X, U, D = synthetic_training_data(1000, seed=0)
     st = gp_oracle.exact_fit(gp_oracle.features_3dof(X, U), D)
-    x0 = initial_conditions(B)
-    ref = [_oracle_landing(st, x0[b], STEPS) for b in range(B)]
+    x0 = initial_conditions(nb)
+    ref = [_oracle_landing(st, x0[b], steps) for b in range(nb)]
 
     gp = fit_gp(gpu_ctx, n_train=1000)
-    fl = Fleet(gpu_ctx, gp, B, horizon=N)
+    fl = Fleet(gpu_ctx, gp, nb, horizon=N)
     try:
         fl.reset(x0)
-        prev_iters = np.zeros(B)
-        for k in range(STEPS):
+        prev_iters = np.zeros(nb)
+        for k in range(steps):
             fl.step(1)
             rec, xs = fl.read()
             assert np.all(rec[:, REC_OUTCOME] == 0), "no landing terminates this early"
             iters = rec[:, REC_ADMM_ITERS] - prev_iters
             prev_iters = rec[:, REC_ADMM_ITERS].copy()
-            for b in range(B):
+            for b in range(nb):
                 xr, itr, str_ = ref[b][k]
                 assert int(iters[b]) == itr, (k, b, int(iters[b]), itr)
                 assert int(rec[b, REC_LAST_STATUS]) == str_, (k, b)
@@ -76,6 +76,27 @@ def test_fleet_closed_loop_matches_oracle(gpu_ctx):
                 assert ok, (k, b, worst)
     finally:
         fl.close()
+
+
+@pytest.mark.parametrize("wide", ["1", "0"])
+def test_fleet_closed_loop_matches_oracle(gpu_ctx, monkeypatch, wide):
+    """16 landings x 40 closed-loop steps against the CPU restatement: ADMM
+    iterations and statuses exact, states within 1e-6.  Both builds of the control
+    kernel: a fleet this small takes the 256-thread, one-wave-per-SIMD build
+    (fleet_wide.hip, GPMPC_FLEET_WIDE=1, the default below one landing per CU), and
+    GPMPC_FLEET_WIDE=0 forces the 128-thread, four-landings-per-CU build the
+    1024-landing fleet runs."""
+    monkeypatch.setenv("GPMPC_FLEET_WIDE", wide)
+    _closed_loop(gpu_ctx, B, STEPS)
+
+
+@pytest.mark.parametrize("nb", [1, 3])
+def test_fleet_few_landings_match_oracle(gpu_ctx, nb):
+    """The few-query step (at most 64 query rows: the single landing of BASELINE
+    configs[2]): features and K* in one launch (k_fleet_queries_gram), the posterior
+    GEMM split over K (launch_splitk_sumsq), no dispatch-order launch for one
+    landing, the wide control kernel -- against the CPU restatement over 40 steps."""
+    _closed_loop(gpu_ctx, nb, STEPS)
 
 
 def test_fleet_specialised_solver_matches_generic(gpu_ctx):
