@@ -52,7 +52,7 @@ template <bool L2A, bool L2B, bool ILC, bool NEGA, bool DMA>
 constexpr bool mma128_dma() { return MMA_V2 && DMA && (MMA_V2_ALL || (!L2A && !L2B && !ILC)); }
 
 // A zero 16-byte chunk: the LDS-DMA source of a tile's padding rows.
-static __device__ double g_mma_zero[2] = {0.0, 0.0};
+static __device__ __attribute__((aligned(16))) double g_mma_zero[2] = {0.0, 0.0};
 
 // mma128_tile's loop with LDS-DMA staging (global_load_lds_dwordx4, no staging registers,
 // no ds_write pass) and 16-byte fragment reads.  An operand's K step is 128 rows x 16
