@@ -86,7 +86,12 @@ __global__ __launch_bounds__(256) void k_gram(int kind, const double *__restrict
 // Row-major K (no transpose), compile-time kernel kind and width: 64 columns x
 // 128 rows per workgroup (each thread one column, 32 rows, 8 independent
 // exponentials in flight), same arithmetic as k_gram (identical bits).
+#ifndef GRAM_ROWS
 #define GRAM_ROWS 128
+#endif
+#ifndef GRAM_UNROLL
+#define GRAM_UNROLL 8
+#endif
 template <int D, int KIND>
 __global__ __launch_bounds__(256) void k_gram_rows(const double *__restrict__ a,
                                                    const double *__restrict__ na, int n1,
@@ -104,7 +109,8 @@ __global__ __launch_bounds__(256) void k_gram_rows(const double *__restrict__ a,
   }
   if (tid < GRAM_ROWS) sna[tid] = (r0 + tid < n1) ? na[r0 + tid] : 0.0;
   const int col = c0 + (tid & 63);
-  const int rb = (tid >> 6) * 32;
+  constexpr int RPT = GRAM_ROWS / 4;  // rows per thread
+  const int rb = (tid >> 6) * RPT;
   double bj[D];
   double nbj = 0.0;
   const bool cv = col < n2;
@@ -113,8 +119,8 @@ __global__ __launch_bounds__(256) void k_gram_rows(const double *__restrict__ a,
   if (cv) nbj = nb[col];
   __syncthreads();
   if (!cv) return;
-#pragma unroll 8
-  for (int rr = 0; rr < 32; ++rr) {
+#pragma unroll GRAM_UNROLL
+  for (int rr = 0; rr < RPT; ++rr) {
     const int r = rb + rr, row = r0 + r;
     double dot = 0.0;
 #pragma unroll
