@@ -19,6 +19,12 @@
 #define R6_TRI 153                            // packed lower 17 x 17
 #define R6_PT 512                             // predict threads (7 kernel-row waves + the RK4 wave)
 #define R6_FOR_H _Pragma("unroll") for (int h = 0; h < 2; ++h)
+// 1: the control kernel's item indices and thread index are made opaque once per ADMM
+// iteration (fleet6_n.h r6_launder / r6_tid), so the addresses derived from them are
+// not hoisted out of the loop into spilled registers (N = 30: scratch 360 -> 112 B/lane)
+#ifndef R6_LAUNDER
+#define R6_LAUNDER 1
+#endif
 
 // ConstraintParams (constraints.py:35-50), CostWeights (cost_functions.py:39-98),
 // gp_mpc.py trust regions (:432-435)

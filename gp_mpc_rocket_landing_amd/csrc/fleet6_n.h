@@ -162,6 +162,16 @@ struct R6Smem {
   int flag, bad[2];
 };
 
+// threadIdx.x behind an opaque copy (R6_LAUNDER): the phases of the ADMM loop derive
+// their addresses from it afresh on every iteration instead of from hoisted registers
+__device__ __forceinline__ int r6_tid() {
+  int t = threadIdx.x;
+#if R6_LAUNDER
+  asm volatile("" : "+v"(t));
+#endif
+  return t;
+}
+
 __device__ __forceinline__ int r6_tri(int a, int b) { return a >= b ? a * (a + 1) / 2 + b : b * (b + 1) / 2 + a; }
 
 template <int K>
@@ -251,13 +261,19 @@ __device__ __forceinline__ bool r6_gen_slot(int k, int i, int e, int &g, int &sl
 struct R6Var {  // variable j and its bound row MD + j; general row j (< 146)
   bool ok;
   int j, k, i;
-  double x, dx, P, q, D, Ab, lb, ub, yb, zb, dyb, ztb;
+  double x, P, q, D, Ab, lb, ub, yb, zb;
   // colA[0..13]: -A_d[:, i] / -B_d[:, i-14] of the dynamics rows of block k
   // (scaled).  An equality-row thread (no variable) keeps its row here instead.
   double colA[R6_SZ + 1];
   bool gok;
   int gn;
-  double gA[3], gl, gu, gy, gz, gdy;
+  double gA[3], gl, gu, gy, gz;
+};
+// an item's changes of one ADMM iteration (dx, the bound row's / equality row's dy,
+// the general row's dy): read by that iteration's termination checks only, so they
+// live in the iteration's scope instead of the items' persistent registers
+struct R6Dy {
+  double dx, dyb, gdy;
 };
 // equality row r (x0 row r < 14, else dynamics row (k, i)).  Rows and variables
 // live on different threads, so the row's registers alias the variable slots.
@@ -265,8 +281,8 @@ struct R6Row {
   bool ok;
   int r, k, i;
   double (&A)[R6_SZ + 1];
-  double &ur, &yr, &zr, &dyr;
-  __device__ explicit R6Row(R6Var &V) : A(V.colA), ur(V.lb), yr(V.yb), zr(V.zb), dyr(V.dyb) {}
+  double &ur, &yr, &zr;
+  __device__ explicit R6Row(R6Var &V) : A(V.colA), ur(V.lb), yr(V.yb), zr(V.zb) {}
 };
 
 __device__ __forceinline__ int r6_eqid_row(int k, int i) { return k == 0 ? i : R6_NX + R6_NX * (k - 1) + i; }
@@ -431,7 +447,7 @@ __device__ __forceinline__ int r6_sweep(double (*T)[R6_TRI], int lt, int nb, int
 // assemble M and factor it: returns 0 or a failing block + 1
 template <class MK>
 __device__ __forceinline__ int r6_factor(R6Smem &s, R6Var (&V)[2], R6Row (&R)[2], double sigma, MK &mark) {
-  const int tid = threadIdx.x;
+  const int tid = r6_tid();
   const double rs = s.rho_s, re = QP_RHO_EQ * rs;
   // stage: dynamics rows' block values, per-variable P + sigma and bound terms
   R6_FOR_H {
@@ -598,7 +614,7 @@ __device__ __forceinline__ double ror8_odd(double v) {
 // (u_k-1) sit 17 below its x_k in the natural order (offsets rr - 17).
 template <class MK>
 __device__ __forceinline__ void r6_solve(R6Smem &s, MK &mark) {
-  const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
+  const int tid = r6_tid(), wv = tid >> 6, lane = tid & 63;
   if (wv < 2) {
     // Two DPP rows per end: row h = 0 takes terms 0-7 and row 1 terms 8-15 of the
     // 16 on the chain, row 1 holding the vector rotated by 8 lanes so that its
@@ -760,14 +776,16 @@ __device__ __forceinline__ double r6_proj(double d, double l, double u) {
   return d;
 }
 
-__device__ __forceinline__ bool r6_primal_infeasible(R6Smem &s, R6Var (&V)[2], R6Row (&R)[2], double eps) {
+__device__ __forceinline__ bool r6_primal_infeasible(R6Smem &s, R6Var (&V)[2], R6Row (&R)[2], R6Dy (&Dl)[2],
+                                                     double eps) {
   double v[1] = {0.0};
   R6_FOR_H {
     R6Var &W = V[h];
     R6Row &Q = R[h];
-    if (Q.ok) { Q.dyr = r6_proj(Q.dyr, Q.ur, Q.ur); v[0] = fmax(v[0], fabs(s.E[Q.r] * Q.dyr)); }
-    if (W.ok) { W.dyb = r6_proj(W.dyb, W.lb, W.ub); v[0] = fmax(v[0], fabs(s.E[R6_MD + W.j] * W.dyb)); }
-    if (W.gok) { W.gdy = r6_proj(W.gdy, W.gl, W.gu); v[0] = fmax(v[0], fabs(s.E[R6_MD + R6_NV + W.j] * W.gdy)); }
+    R6Dy &d = Dl[h];
+    if (Q.ok) { d.dyb = r6_proj(d.dyb, Q.ur, Q.ur); v[0] = fmax(v[0], fabs(s.E[Q.r] * d.dyb)); }
+    if (W.ok) { d.dyb = r6_proj(d.dyb, W.lb, W.ub); v[0] = fmax(v[0], fabs(s.E[R6_MD + W.j] * d.dyb)); }
+    if (W.gok) { d.gdy = r6_proj(d.gdy, W.gl, W.gu); v[0] = fmax(v[0], fabs(s.E[R6_MD + R6_NV + W.j] * d.gdy)); }
   }
   r6_max<1>(v, s.red);
   const double nrm = v[0];
@@ -776,43 +794,45 @@ __device__ __forceinline__ bool r6_primal_infeasible(R6Smem &s, R6Var (&V)[2], R
   R6_FOR_H {
     R6Var &W = V[h];
     R6Row &Q = R[h];
-    if (Q.ok) sm[0] += Q.ur * fmax(Q.dyr, 0.0) + Q.ur * fmin(Q.dyr, 0.0);
-    if (W.ok) sm[0] += W.ub * fmax(W.dyb, 0.0) + W.lb * fmin(W.dyb, 0.0);
-    if (W.gok) sm[0] += W.gu * fmax(W.gdy, 0.0) + W.gl * fmin(W.gdy, 0.0);
+    const R6Dy &d = Dl[h];
+    if (Q.ok) sm[0] += Q.ur * fmax(d.dyb, 0.0) + Q.ur * fmin(d.dyb, 0.0);
+    if (W.ok) sm[0] += W.ub * fmax(d.dyb, 0.0) + W.lb * fmin(d.dyb, 0.0);
+    if (W.gok) sm[0] += W.gu * fmax(d.gdy, 0.0) + W.gl * fmin(d.gdy, 0.0);
   }
   r6_sum<1>(sm, s.red);
   if (!(sm[0] < -eps * nrm)) return false;
   R6_FOR_H {
-    if (R[h].ok) s.w[R[h].r] = R[h].dyr;
-    if (V[h].gok) s.w[R6_MD + V[h].j] = V[h].gdy;
+    if (R[h].ok) s.w[R[h].r] = Dl[h].dyb;
+    if (V[h].gok) s.w[R6_MD + V[h].j] = Dl[h].gdy;
   }
   __syncthreads();
   double mx[1] = {0.0};
   R6_FOR_H {
-    if (V[h].ok) mx[0] = fmax(mx[0], fabs(r6_col_dot(s, V[h], s.w, V[h].dyb, s.w + R6_MD) / V[h].D));
+    if (V[h].ok) mx[0] = fmax(mx[0], fabs(r6_col_dot(s, V[h], s.w, Dl[h].dyb, s.w + R6_MD) / V[h].D));
   }
   r6_max<1>(mx, s.red);
   return mx[0] < eps * nrm;
 }
 
-__device__ __forceinline__ bool r6_dual_infeasible(R6Smem &s, R6Var (&V)[2], R6Row (&R)[2], double eps) {
+__device__ __forceinline__ bool r6_dual_infeasible(R6Smem &s, R6Var (&V)[2], R6Row (&R)[2], const R6Dy (&Dl)[2],
+                                                   double eps) {
   double v[1] = {0.0};
   R6_FOR_H {
-    if (V[h].ok) v[0] = fmax(v[0], fabs(V[h].D * V[h].dx));
+    if (V[h].ok) v[0] = fmax(v[0], fabs(V[h].D * Dl[h].dx));
   }
   r6_max<1>(v, s.red);
   const double nrm = v[0];
   if (!(nrm > QP_DIV_TOL)) return false;
   double a[1] = {0.0}, pm[1] = {0.0};
   R6_FOR_H {
-    if (V[h].ok) { a[0] += V[h].q * V[h].dx; pm[0] = fmax(pm[0], fabs(V[h].P * V[h].dx / V[h].D)); }
+    if (V[h].ok) { a[0] += V[h].q * Dl[h].dx; pm[0] = fmax(pm[0], fabs(V[h].P * Dl[h].dx / V[h].D)); }
   }
   r6_sum<1>(a, s.red);
   r6_max<1>(pm, s.red);
   if (!(a[0] < s.c * eps * nrm)) return false;
   if (!(pm[0] < s.c * eps * nrm)) return false;
   R6_FOR_H {
-    if (V[h].ok) s.rhs[V[h].j] = V[h].dx;
+    if (V[h].ok) s.rhs[V[h].j] = Dl[h].dx;
   }
   __syncthreads();
   double bad[1] = {0.0};
@@ -824,14 +844,14 @@ __device__ __forceinline__ bool r6_dual_infeasible(R6Smem &s, R6Var (&V)[2], R6R
   R6_FOR_H {
     R6Var &W = V[h];
     if (R[h].ok) test(r6_row_dot(R[h], s.rhs) / s.E[R[h].r], R[h].ur, R[h].ur);
-    if (W.ok) test((0.0 + W.Ab * W.dx) / s.E[R6_MD + W.j], W.lb, W.ub);
+    if (W.ok) test((0.0 + W.Ab * Dl[h].dx) / s.E[R6_MD + W.j], W.lb, W.ub);
     if (W.gok) test(r6_gen_dot(W, s.rhs) / s.E[R6_MD + R6_NV + W.j], W.gl, W.gu);
   }
   r6_max<1>(bad, s.red);
   return bad[0] == 0.0;
 }
 
-__device__ __forceinline__ bool r6_check(R6Smem &s, R6Var (&V)[2], R6Row (&R)[2], const QPSettingsDev &st,
+__device__ __forceinline__ bool r6_check(R6Smem &s, R6Var (&V)[2], R6Row (&R)[2], R6Dy (&Dl)[2], const QPSettingsDev &st,
                                          const double (&o)[8], bool approx, int &status) {
   const double pri = o[0], dua = o[3] / s.c;
   double ea = st.eps_abs, er = st.eps_rel, epi = st.eps_prim_inf, edi = st.eps_dual_inf;
@@ -839,9 +859,9 @@ __device__ __forceinline__ bool r6_check(R6Smem &s, R6Var (&V)[2], R6Row (&R)[2]
   if (approx) { ea *= 10; er *= 10; epi *= 10; edi *= 10; }
   bool prim_ok = false, prim_inf = false, dual_ok = false, dual_inf = false;
   if (pri < ea + er * fmax(o[1], o[2])) prim_ok = true;
-  else prim_inf = r6_primal_infeasible(s, V, R, epi);
+  else prim_inf = r6_primal_infeasible(s, V, R, Dl, epi);
   if (dua < ea + er * fmax(fmax(o[4], o[5]), o[6]) / s.c) dual_ok = true;
-  else dual_inf = r6_dual_infeasible(s, V, R, edi);
+  else dual_inf = r6_dual_infeasible(s, V, R, Dl, edi);
   if (prim_ok && dual_ok) { status = approx ? 2 : 1; return true; }
   if (prim_inf) { status = approx ? 3 : -3; return true; }
   if (dual_inf) { status = approx ? 4 : -4; return true; }
@@ -852,10 +872,21 @@ __device__ __forceinline__ void r6_rebuild_w(R6Smem &s, R6Var (&V)[2], R6Row (&R
   const double rs = s.rho_s;
   R6_FOR_H {
     if (R[h].ok) s.w[R[h].r] = QP_RHO_EQ * rs * R[h].zr - R[h].yr;
-    if (V[h].ok) V[h].ztb = r6_rho(V[h].lb, V[h].ub, rs) * V[h].zb - V[h].yb;
     if (V[h].gok) s.w[R6_MD + V[h].j] = r6_rho(V[h].gl, V[h].gu, rs) * V[h].gz - V[h].gy;
   }
   __syncthreads();
+}
+
+// The items' indices, opaque to the compiler once per ADMM iteration: every address
+// and row-structure decision derived from them is recomputed inside the loop instead
+// of hoisted out of it as a live register (hoisted, they were most of the spills)
+__device__ __forceinline__ void r6_launder(R6Var (&V)[2], R6Row (&R)[2]) {
+#if R6_LAUNDER
+  R6_FOR_H {
+    asm volatile("" : "+v"(V[h].j), "+v"(V[h].k), "+v"(V[h].i));
+    asm volatile("" : "+v"(R[h].r), "+v"(R[h].k), "+v"(R[h].i));
+  }
+#endif
 }
 
 // diagnostic phase cycles of workgroup 0 (GPMPC_R6_STAMPS=1 launches the <true> instance)
@@ -1107,24 +1138,32 @@ __global__ __launch_bounds__(R6_T) void k_r6_control(R6Args a) {
     }
     r6_rebuild_w(s, V, R);
     const double sig = st.sigma, al = st.alpha;
-    bool can_check = false;
-    int it;
     double o[8], re_[4];
-    for (it = 1; it <= st.max_iter; ++it) {
-      R6_FOR_H {
-        if (V[h].ok) s.rhs[V[h].j] = sig * V[h].x - V[h].q + r6_col_dot(s, V[h], s.w, V[h].ztb, s.w + R6_MD);
+    for (int it = 1; it <= st.max_iter; ++it) {
+      r6_launder(V, R);
+      {
+        const double rs = s.rho_s;
+        R6_FOR_H {
+          // the bound row's rho z - y (formed here rather than kept per item)
+          const double ztb = r6_rho(V[h].lb, V[h].ub, rs) * V[h].zb - V[h].yb;
+          if (V[h].ok) s.rhs[V[h].j] = sig * V[h].x - V[h].q + r6_col_dot(s, V[h], s.w, ztb, s.w + R6_MD);
+        }
       }
       __syncthreads();
       mark(3);
       r6_solve(s, mark);
+#if R6_LAUNDER > 1
+      r6_launder(V, R);
+#endif
       const double rs = s.rho_s;
+      R6Dy Dl[2];
       R6_FOR_H {
         R6Var &W = V[h];
         R6Row &Q = R[h];
         if (W.ok) {
           const double xt = s.xs[W.j], xo = W.x;
           const double xn = al * xt + (1.0 - al) * xo;
-          W.dx = xn - xo;
+          Dl[h].dx = xn - xo;
           W.x = xn;
           const double ztl = 0.0 + W.Ab * xt;
           const double rho = r6_rho(W.lb, W.ub, rs), zo = W.zb, yo = W.yb;
@@ -1132,8 +1171,7 @@ __global__ __launch_bounds__(R6_T) void k_r6_control(R6Args a) {
           double zn = zr + yo / rho;
           zn = fmin(fmax(zn, W.lb), W.ub);
           const double d = rho * (zr - zn);
-          W.dyb = d; W.yb = yo + d; W.zb = zn;
-          W.ztb = rho * zn - W.yb;
+          Dl[h].dyb = d; W.yb = yo + d; W.zb = zn;
         }
         if (W.gok) {
           const double ztl = r6_gen_dot(W, s.xs);
@@ -1142,7 +1180,7 @@ __global__ __launch_bounds__(R6_T) void k_r6_control(R6Args a) {
           double zn = zr + yo / rho;
           zn = fmin(fmax(zn, W.gl), W.gu);
           const double d = rho * (zr - zn);
-          W.gdy = d; W.gy = yo + d; W.gz = zn;
+          Dl[h].gdy = d; W.gy = yo + d; W.gz = zn;
         }
         if (Q.ok) {
           const double ztl = r6_row_dot(Q, s.xs);
@@ -1151,7 +1189,7 @@ __global__ __launch_bounds__(R6_T) void k_r6_control(R6Args a) {
           double zn = zr + yo / rho;
           zn = fmin(fmax(zn, Q.ur), Q.ur);
           const double d = rho * (zr - zn);
-          Q.dyr = d; Q.yr = yo + d; Q.zr = zn;
+          Dl[h].dyb = d; Q.yr = yo + d; Q.zr = zn;
         }
       }
       __syncthreads();  // every read of s.w / s.xs of this iteration is done
@@ -1161,13 +1199,14 @@ __global__ __launch_bounds__(R6_T) void k_r6_control(R6Args a) {
       }
       __syncthreads();
       mark(7);
-      can_check = st.check_termination && (it % st.check_termination == 0);
+      const bool can_check = st.check_termination && (it % st.check_termination == 0);
       const bool adapt = st.adaptive_rho && st.adaptive_rho_interval && (it % st.adaptive_rho_interval == 0);
-      if (can_check || adapt) {
+      const bool last = it == st.max_iter;
+      if (can_check || adapt || last) {
         res.iter = it;
         r6_update_info(s, V, R, o, re_);
       }
-      if (can_check && r6_check(s, V, R, st, o, false, res.status)) break;
+      if (can_check && r6_check(s, V, R, Dl, st, o, false, res.status)) break;
       if (adapt) {
         const double pr = re_[0] / (re_[1] + 1e-10);
         const double du = re_[2] / (re_[3] + 1e-10);
@@ -1185,15 +1224,14 @@ __global__ __launch_bounds__(R6_T) void k_r6_control(R6Args a) {
       }
       if (can_check || adapt) r6_rebuild_w(s, V, R);
       mark(8);
-    }
-    if (!res.factor_fail) {
-      if (!can_check) {
-        res.iter = it - 1;
-        r6_update_info(s, V, R, o, re_);
-        r6_check(s, V, R, st, o, false, res.status);
-      }
-      if (res.status == -10) {
-        if (!r6_check(s, V, R, st, o, true, res.status)) res.status = -2;
+      if (last) {
+        // max_iter reached (inside the iteration, where its dx / dy live): the final
+        // check unless one just ran, then the approximate one (qp_device.h)
+#pragma unroll 1
+        for (int ap = can_check ? 1 : 0; ap < 2; ++ap) {
+          if (r6_check(s, V, R, Dl, st, o, ap == 1, res.status)) break;
+          if (ap == 1) res.status = -2;
+        }
       }
     }
   }
