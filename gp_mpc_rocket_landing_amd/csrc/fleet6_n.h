@@ -1227,7 +1227,6 @@ __global__ __launch_bounds__(R6_T) void k_r6_control(R6Args a) {
       if (last) {
         // max_iter reached (inside the iteration, where its dx / dy live): the final
         // check unless one just ran, then the approximate one (qp_device.h)
-#pragma unroll 1
         for (int ap = can_check ? 1 : 0; ap < 2; ++ap) {
           if (r6_check(s, V, R, Dl, st, o, ap == 1, res.status)) break;
           if (ap == 1) res.status = -2;

@@ -52,6 +52,23 @@ __device__ __forceinline__ void lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)\
 #ifndef FQ_FUSED_DIAG
 #define FQ_FUSED_DIAG false  // block solve: G chain first, then the diagonal blocks 4 at a time
 #endif
+// FQ_LAUNDER 1: the diagonal phase's thread index (2: and the items' indices, once per
+// ADMM iteration) made opaque, so that the addresses derived from them are formed inside
+// the loop rather than hoisted out of it into spilled registers.  Measured
+// (profiles/r5_fleet_launder_ab.log, 3 runs each at 1024 landings): spills 54 -> 3,
+// traffic 47 -> 17 MB per launch, but the kernel 291 -> 303 us (the 17 packed-row
+// addresses of a diagonal round recomputed on the phase's path); off.  The 6-DoF
+// kernel, where the hoisted values were the loop's live state, keeps it (fleet6.h).
+#ifndef FQ_LAUNDER
+#define FQ_LAUNDER 0
+#endif
+__device__ __forceinline__ int fq_tid() {
+  int t = threadIdx.x;
+#if FQ_LAUNDER
+  asm volatile("" : "+v"(t));
+#endif
+  return t;
+}
 // FQ_TWIST: the two-ended factor / solve of fleet_twist.h (10-block chains instead of 20)
 #ifndef FQ_TWIST
 #define FQ_TWIST 1
@@ -684,6 +701,10 @@ __device__ __forceinline__ QPResult fq_solve(const QPPattern &pt, FleetSmem &s, 
   int it;
   double o[8], re[4];
   for (it = 1; it <= st.max_iter; ++it) {
+#if FQ_LAUNDER > 1
+#pragma unroll
+    for (int h = 0; h < FQ_H; ++h) asm volatile("" : "+v"(R.vj[h]), "+v"(R.rr[h]));
+#endif
     // rhs = sigma x - q + A'(rho z - y)
 #if FQ_RHS_PAIR && FQ_T < 256
     {

@@ -181,11 +181,14 @@ __device__ __forceinline__ double ft_dot_reload(double init, double src, double 
 // on the chain wave only; PH 2 on both waves of the workgroup (caller barriers).
 template <int PH, class S>
 __device__ __forceinline__ void ft_solve(S &s, double *b, int cw) {
-  const int lane = threadIdx.x & 63, rr = lane & 15;
+  // the diagonal phase's thread index is opaque (its unrolled rounds otherwise keep
+  // hoisted addresses live across the loop); the chains keep threadIdx.x, whose wave
+  // index the compiler knows to be uniform
+  const int tid = PH == 2 ? fq_tid() : (int)threadIdx.x, lane = tid & 63, rr = lane & 15;
   const int rs = rr < FT_SZ ? rr : FT_SZ - 1;
   const double *F = s.band();
   if constexpr (PH == 1 || PH == 4) {
-    if ((int)(threadIdx.x >> 6) != cw || lane >= 32 || rr >= FT_SZ) return;
+    if ((tid >> 6) != cw || lane >= 32 || rr >= FT_SZ) return;
     const bool top = lane < 16;
     // Block offsets are element indices advanced step by step behind an empty asm:
     // the two rows walk in opposite directions, so a step's address is not an
@@ -314,7 +317,7 @@ __device__ __forceinline__ void ft_solve(S &s, double *b, int cw) {
   } else {
     // diagonal: u_k / x_10 / w_k, eight blocks a round (one per DPP row of
     // either wave); rows past the last block read the last block and do not store
-    const int q = (int)(threadIdx.x >> 4);
+    const int q = tid >> 4;
     constexpr int RB = FQ_T / 16, NR = (FT_NB + RB - 1) / RB;
 #if FT_DIAG_UNROLL
 #pragma unroll
