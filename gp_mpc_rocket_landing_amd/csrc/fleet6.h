@@ -25,6 +25,15 @@
 #ifndef R6_LAUNDER
 #define R6_LAUNDER 1
 #endif
+// block steps per chain-loop trip and diagonal-product operands in flight per chunk
+#ifndef R6_CHAIN_UNROLL
+#define R6_CHAIN_UNROLL 3
+#endif
+#ifndef R6_DIAG_CHUNK
+#define R6_DIAG_CHUNK 6
+#endif
+#define R6_STR_(x) #x
+#define R6_STR(x) R6_STR_(x)
 
 // ConstraintParams (constraints.py:35-50), CostWeights (cost_functions.py:39-98),
 // gp_mpc.py trust regions (:432-435)

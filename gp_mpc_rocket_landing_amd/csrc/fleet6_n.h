@@ -560,17 +560,17 @@ __device__ __forceinline__ void r6_diag_row(R6Smem &s, int k, int a) {
     // once spilled the items' registers)
     double acc0 = 0.0, acc1 = 0.0;
 #pragma unroll
-    for (int c0 = 0; c0 < R6_SZ; c0 += 6) {
-      double sv[6], yv[6];
+    for (int c0 = 0; c0 < R6_SZ; c0 += R6_DIAG_CHUNK) {
+      double sv[R6_DIAG_CHUNK], yv[R6_DIAG_CHUNK];
 #pragma unroll
-      for (int q = 0; q < 6; ++q) {
+      for (int q = 0; q < R6_DIAG_CHUNK; ++q) {
         const int bb = c0 + q < R6_SZ ? c0 + q : R6_SZ - 1;
         sv[q] = S[r6_tri(a, bb)];
         yv[q] = y[bb >= R6_NX ? bb - lo : bb];
         if (bb < R6_NX && mid) yv[q] += s.zmid[bb];
       }
 #pragma unroll
-      for (int q = 0; q < 6; ++q) {
+      for (int q = 0; q < R6_DIAG_CHUNK; ++q) {
         const int bb = c0 + q;
         if (bb >= R6_SZ) continue;
         if (bb & 1) acc1 = bb < nb ? fma(sv[q], yv[q], acc1) : acc1;
@@ -642,7 +642,7 @@ __device__ __forceinline__ void r6_solve(R6Smem &s, MK &mark) {
     double b16 = s.rhs[ib + o16], bn = s.rhs[ib + db + offo(m)];
     // block steps of this end (wave-uniform; a compile-time count for an even N)
     const int nst = (R6_BOTS == R6_MID) ? R6_MID : (bot ? R6_BOTS : R6_MID);
-#pragma unroll 3
+_Pragma(R6_STR(unroll R6_CHAIN_UNROLL))
     for (int t = 0; t < nst; ++t) {
       const bool last = t == nst - 1;
       const int gn = go + gs;
@@ -698,7 +698,7 @@ __device__ __forceinline__ void r6_solve(R6Smem &s, MK &mark) {
     double u = s.xs[ib + off];
     // block steps of this end (wave-uniform; a compile-time count for an even N)
     const int nst = (R6_BOTS == R6_MID) ? R6_MID : (bot ? R6_BOTS : R6_MID);
-#pragma unroll 3
+_Pragma(R6_STR(unroll R6_CHAIN_UNROLL))
     for (int t = 0; t < nst; ++t) {
       const int gn = min(max(go + gs, a), (R6_N - 1) * R6_NX * R6_SZ + a);
       double a0 = u, a1 = 0.0;
