@@ -25,9 +25,11 @@
 #ifndef R6_LAUNDER
 #define R6_LAUNDER 1
 #endif
-// block steps per chain-loop trip and diagonal-product operands in flight per chunk
+// block steps per chain-loop trip (the whole chain since the spills went: 64 rollouts
+// 0.881-0.888 -> 0.869-0.870 ms per step against 3, profiles/r5_r6_unroll_ab.log) and
+// diagonal-product operands in flight per chunk (6, 9, 17 measured level)
 #ifndef R6_CHAIN_UNROLL
-#define R6_CHAIN_UNROLL 3
+#define R6_CHAIN_UNROLL 15
 #endif
 #ifndef R6_DIAG_CHUNK
 #define R6_DIAG_CHUNK 6
