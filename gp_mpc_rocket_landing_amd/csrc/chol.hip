@@ -276,6 +276,149 @@ __device__ __forceinline__ void inv_assemble(double (*S)[DP], double *Li, bool z
   }
 }
 
+// LDS layouts of the 128 x 128 block for the column sweep.  Full: 128 rows at pitch DP
+// (130 KB: one workgroup per CU).  Packed lower (PK): 16-row block ib stores columns
+// 0 .. 16 ib + 15 (its rows' lower part and the full 16 x 16 diagonal tile) at pitch
+// 16 ib + 18 (18 or 2 mod 32, so the 16-row MFMA operand gathers stay conflict-free):
+// 74 KB, two workgroups per CU.  No upper triangle: the factor's owner stores no zeros
+// above the diagonal, the 32 x 32 inverses keep their Y = L21 T11 in registers
+// (tinv32_pk) and the inverse is assembled in place of L (inv_assemble_pk).
+struct LdsFull {
+  static constexpr bool PK = false;
+  double *p;
+  __device__ __forceinline__ double &operator()(int r, int c) const { return p[r * DP + c]; }
+  __device__ __forceinline__ double (*rows() const)[DP] { return reinterpret_cast<double (*)[DP]>(p); }
+};
+struct LdsPk {
+  static constexpr bool PK = true;
+  double *p;
+  __device__ __forceinline__ double &operator()(int r, int c) const {
+    const int ib = r >> 4;
+    return p[128 * ib * (ib + 1) + 32 * ib + (r & 15) * (16 * ib + 18) + c];
+  }
+};
+#define DPK_ELEMS (128 * 8 * 9 + 32 * 8)  // 9472 doubles
+#define DIAG128_LDS_PK (sizeof(double) * (DPK_ELEMS + DB + 4))
+// does row r of the packed layout store column c
+__device__ __forceinline__ bool pk_has(int r, int c) { return c < 16 * (r >> 4) + 16; }
+
+// tinv32 on the packed layout: T11 / T22 by column substitution as tinv32, then
+// T21 = -T22 (L21 T11) with Y = L21 T11 kept in the MFMA accumulators: the second
+// product's k index is permuted so that lane l's k slot at step s is row
+// (l >> 4) + 4 s of Y, which is exactly its own accumulator entry s.
+__device__ __forceinline__ void tinv32_pk(LdsPk S, int c0, const double *dinv) {
+  const int lane = threadIdx.x & 63, li = lane & 15, lk = lane >> 4;
+  const int base = lane & 16, c = lane & 15;
+  double x[16];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    double sum = (r == c) ? 1.0 : 0.0;
+#pragma unroll
+    for (int k = 0; k < r; ++k) sum = fma(-S(c0 + base + r, c0 + base + k), x[k], sum);
+    x[r] = (r >= c) ? sum * dinv[base + r] : 0.0;
+  }
+  wave_lds_sync();
+  if (lane < NB) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r)
+      if (r >= c) S(c0 + base + r, c0 + base + c) = x[r];
+  }
+  wave_lds_sync();
+  d4_t y = d4_t{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+  for (int kk = 0; kk < 16; kk += 4) {
+    const int m = kk + lk;
+    y = mfma_f64(S(c0 + 16 + li, c0 + m), (m >= li) ? S(c0 + m, c0 + li) : 0.0, y);
+  }
+  d4_t t21 = d4_t{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+  for (int s4 = 0; s4 < 4; ++s4) {
+    const int m = lk + 4 * s4;  // = mf_row(lane, s4): y[s4] is Y[m][li]
+    t21 = mfma_f64((m <= li) ? S(c0 + 16 + li, c0 + 16 + m) : 0.0, y[s4], t21);
+  }
+  wave_lds_sync();
+#pragma unroll
+  for (int r = 0; r < 4; ++r) S(c0 + 16 + mf_row(lane, r), c0 + li) = -t21[r];
+}
+
+// inv_assemble on the packed layout, in place of L: block row i = 1..3 (32 rows), job
+// (j, cb) (j < i, 16-column half cb) forms both 16-row tiles of
+//   Y_j = sum_{k=j}^{i-1} L_ik X_kj       (X_jj = T_j; X_kj, k > j, already in place of L_kj)
+// in its accumulators; after a barrier (every read of row i's L blocks done)
+//   X_ij = -T_i Y_j                        (Y_j's 32 rows from the two accumulators, k permuted)
+// goes in place of L_ij and to Li.
+__device__ __forceinline__ void inv_assemble_pk(LdsPk S, double *Li, bool zero_upper) {
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int li = lane & 15, lk = lane >> 4;
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    const int e = tid + 256 * q, blk = e >> 10, rr = (e >> 5) & 31, cc = e & 31;
+    const int i = blk * NB + rr, j = blk * NB + cc;
+    Li[i * DB + j] = (cc > rr) ? 0.0 : S(i, j);
+  }
+  if (zero_upper) {
+#pragma unroll 2
+    for (int q = 0; q < 24; ++q) {
+      const int e = tid + 256 * q, ub = e >> 10, rr = (e >> 5) & 31, cc = e & 31;
+      const int bi = ub < 3 ? 0 : ub < 5 ? 1 : 2, bj = ub < 3 ? ub + 1 : ub < 5 ? ub - 1 : 3;
+      Li[(bi * NB + rr) * DB + bj * NB + cc] = 0.0;
+    }
+  }
+  for (int i = 1; i < DB / NB; ++i) {
+    const int njob = 2 * i;
+    d4_t y[2][2];  // [job round][row tile]
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      y[q][0] = y[q][1] = d4_t{0.0, 0.0, 0.0, 0.0};
+      const int jt = wave + 4 * q;
+      if (jt < njob) {
+        const int j = jt >> 1, cb = (jt & 1) * 16, cc = cb + li;
+        for (int k = j; k < i; ++k) {
+#pragma unroll
+          for (int mm = 0; mm < NB; mm += 4) {
+            const int m = mm + lk;
+            double bv;  // X_kj[m][cc]
+            if (k == j) bv = (cc <= m) ? S(j * NB + m, j * NB + cc) : 0.0;
+            else bv = S(k * NB + m, j * NB + cc);
+            y[q][0] = mfma_f64(S(i * NB + li, k * NB + m), bv, y[q][0]);
+            y[q][1] = mfma_f64(S(i * NB + 16 + li, k * NB + m), bv, y[q][1]);
+          }
+        }
+      }
+    }
+    lds_barrier();
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int jt = wave + 4 * q;
+      if (jt < njob) {
+        const int j = jt >> 1, cb = (jt & 1) * 16;
+#pragma unroll
+        for (int ro = 0; ro < 2; ++ro) {  // output row tile
+          d4_t x = d4_t{0.0, 0.0, 0.0, 0.0};
+          const int rr = ro * 16 + li;    // A row: T_i[rr][m]
+#pragma unroll
+          for (int rb = 0; rb < 2; ++rb) {
+            if (rb > ro) continue;  // T_i lower: rows 0-15 see only m < 16
+#pragma unroll
+            for (int s4 = 0; s4 < 4; ++s4) {
+              const int m = rb * 16 + lk + 4 * s4;  // y[q][rb][s4] = Y_j[m][cb + li]
+              const double av = (m <= rr) ? S(i * NB + rr, i * NB + m) : 0.0;
+              x = mfma_f64(av, y[q][rb][s4], x);
+            }
+          }
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int row = i * NB + ro * 16 + mf_row(lane, r);
+            S(row, j * NB + cb + li) = -x[r];
+            Li[row * DB + j * NB + cb + li] = -x[r];
+          }
+        }
+      }
+    }
+    lds_barrier();
+  }
+}
+
 // The factor + inverse of a 128 x 128 diagonal block already in LDS (S: lower
 // triangle, identity padding beyond pw, zero upper triangle; sfail = 0), for
 // k_potrf_diag128 and the per-matrix k_potrf_persist.  Writes L (rows < pw) at
@@ -488,8 +631,8 @@ __device__ __forceinline__ int diag128_core(double (*S)[DP], double *col, int &s
 // raises them all (SW_BIG), so no wave waits forever.  Afterwards each wave
 // inverts its own diagonal block (tinv32) and inv_assemble forms Linv.
 #define SW_BIG (1 << 20)
-template <bool ST>
-__device__ __forceinline__ int diag128_sweep(double (*S)[DP], double *dinv, int &sfail, int *fl,
+template <bool ST, class LS>
+__device__ __forceinline__ int diag128_sweep(LS S, double *dinv, int &sfail, int *fl,
                                              double *M, int64_t lda, int pw, int K0, int *infob,
                                              double *Li, bool stamp, bool zero_upper, bool tblk) {
   const int tid = threadIdx.x, lane = tid & 63;
@@ -556,7 +699,7 @@ __device__ __forceinline__ int diag128_sweep(double (*S)[DP], double *dinv, int 
         // the step's four columns of this lane's row (two 16-byte reads; rows above
         // the step read as zero)
         {
-          const double2 *rp = reinterpret_cast<const double2 *>(&S[r][cb0 + j]);
+          const double2 *rp = reinterpret_cast<const double2 *>(&S(r, cb0 + j));
           const double2 x01 = rp[0], x23 = rp[1];
           const bool on = lv && lane >= j;
           p[0] = on ? x01.x : 0.0;
@@ -624,8 +767,8 @@ __device__ __forceinline__ int diag128_sweep(double (*S)[DP], double *dinv, int 
           dp[0] = make_double2(id0, id1);
           dp[1] = make_double2(id2, id3);
         }
-        if (lv) {
-          double2 *rp = reinterpret_cast<double2 *>(&S[r][cb0 + j]);
+        if (lv && (!LS::PK || lane >= j)) {  // (packed: no upper-triangle storage)
+          double2 *rp = reinterpret_cast<double2 *>(&S(r, cb0 + j));
           rp[0] = make_double2(p[0], p[1]);
           rp[1] = make_double2(p[2], p[3]);
         }
@@ -635,8 +778,8 @@ __device__ __forceinline__ int diag128_sweep(double (*S)[DP], double *dinv, int 
         const int j4 = j + 4;
         if (j4 < NB) {
           const bool lo = j4 < 16;
-          const double v16 = S[cb0 + 16 + li][cb0 + j + lk];
-          const double v0 = lo ? S[cb0 + li][cb0 + j + lk] : 0.0;
+          const double v16 = S(cb0 + 16 + li, cb0 + j + lk);
+          const double v0 = lo ? S(cb0 + li, cb0 + j + lk) : 0.0;
           const double a16 = (16 + li >= j4) ? v16 : 0.0, a0 = (li >= j4) ? v0 : 0.0;
           const d4_t t11 = mfma_f64(a16, a16, z4);
           const d4_t t10 = lo ? mfma_f64(a16, a0, z4) : z4;
@@ -644,18 +787,18 @@ __device__ __forceinline__ int diag128_sweep(double (*S)[DP], double *dinv, int 
           double o11[4], o10[4], o00[4];
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
-            o11[q] = S[cb0 + 16 + mf_row(lane, q)][cb0 + 16 + li];
+            o11[q] = S(cb0 + 16 + mf_row(lane, q), cb0 + 16 + li);
             if (lo) {
-              o10[q] = S[cb0 + 16 + mf_row(lane, q)][cb0 + li];
-              o00[q] = S[cb0 + mf_row(lane, q)][cb0 + li];
+              o10[q] = S(cb0 + 16 + mf_row(lane, q), cb0 + li);
+              o00[q] = S(cb0 + mf_row(lane, q), cb0 + li);
             }
           }
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
-            S[cb0 + 16 + mf_row(lane, q)][cb0 + 16 + li] = o11[q] - t11[q];
+            S(cb0 + 16 + mf_row(lane, q), cb0 + 16 + li) = o11[q] - t11[q];
             if (lo) {
-              S[cb0 + 16 + mf_row(lane, q)][cb0 + li] = o10[q] - t10[q];
-              S[cb0 + mf_row(lane, q)][cb0 + li] = o00[q] - t00[q];
+              S(cb0 + 16 + mf_row(lane, q), cb0 + li) = o10[q] - t10[q];
+              S(cb0 + mf_row(lane, q), cb0 + li) = o00[q] - t00[q];
             }
           }
           asm volatile("" ::: "memory");
@@ -685,7 +828,7 @@ __device__ __forceinline__ int diag128_sweep(double (*S)[DP], double *dinv, int 
 #pragma unroll 4
         for (int k = 0; k < NB * NB / 64; ++k) {
           const int e = lane + 64 * k, rr = e >> 5, cc = e & 31;
-          if (cc <= rr && rr < pw) M[(int64_t)rr * lda + cc] = S[rr][cc];
+          if (cc <= rr && rr < pw) M[(int64_t)rr * lda + cc] = S(rr, cc);
         }
       }
       if (wave + 1 < nblk) {
@@ -695,7 +838,7 @@ __device__ __forceinline__ int diag128_sweep(double (*S)[DP], double *dinv, int 
           wait_ge(0, (wave + 1) * 8 + j / 4 + 1);
           if (ld_flag(&sfail)) break;
           const int cc = n0 + j + ch;
-          const double2 v = *reinterpret_cast<const double2 *>(&S[rr][cc]);
+          const double2 v = *reinterpret_cast<const double2 *>(&S(rr, cc));
           if (rr < pw) {
             if (cc <= rr) M[(int64_t)rr * lda + cc] = v.x;
             if (cc + 1 <= rr) M[(int64_t)rr * lda + cc + 1] = v.y;
@@ -717,9 +860,9 @@ __device__ __forceinline__ int diag128_sweep(double (*S)[DP], double *dinv, int 
         const int c = cb0 + j;
         double p[4];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) p[q] = lv ? S[r][c + q] : 0.0;
-        const double l10 = S[c + 1][c], l20 = S[c + 2][c], l30 = S[c + 3][c];
-        const double l21 = S[c + 2][c + 1], l31 = S[c + 3][c + 1], l32 = S[c + 3][c + 2];
+        for (int q = 0; q < 4; ++q) p[q] = lv ? S(r, c + q) : 0.0;
+        const double l10 = S(c + 1, c), l20 = S(c + 2, c), l30 = S(c + 3, c);
+        const double l21 = S(c + 2, c + 1), l31 = S(c + 3, c + 1), l32 = S(c + 3, c + 2);
         p[0] *= dinv[c];
         p[1] = fma(-p[0], l10, p[1]);
         p[2] = fma(-p[0], l20, p[2]);
@@ -733,12 +876,12 @@ __device__ __forceinline__ int diag128_sweep(double (*S)[DP], double *dinv, int 
         if (lv) {
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
-            S[r][c + q] = p[q];
+            S(r, c + q) = p[q];
             if (r < pw) M[(int64_t)r * lda + c + q] = p[q];
           }
         }
         asm volatile("" ::: "memory");
-        const double a0 = S[w0 + li][c + lk], a1 = S[w0 + 16 + li][c + lk];
+        const double a0 = S(w0 + li, c + lk), a1 = S(w0 + 16 + li, c + lk);
         d00 = mfma_f64(a0, a0, d00);
         d10 = mfma_f64(a1, a0, d10);
         d11 = mfma_f64(a1, a1, d11);
@@ -746,28 +889,28 @@ __device__ __forceinline__ int diag128_sweep(double (*S)[DP], double *dinv, int 
         if (j4 < NB) {
           // own rows (two 16-row tiles) x the block's columns >= j4
           const bool lo = j4 < 16;
-          const double b1 = (16 + li >= j4) ? S[cb0 + 16 + li][c + lk] : 0.0;
-          const double b0 = (lo && li >= j4) ? S[cb0 + li][c + lk] : 0.0;
+          const double b1 = (16 + li >= j4) ? S(cb0 + 16 + li, c + lk) : 0.0;
+          const double b0 = (lo && li >= j4) ? S(cb0 + li, c + lk) : 0.0;
           const d4_t t01 = mfma_f64(a0, b1, z4), t11 = mfma_f64(a1, b1, z4);
           const d4_t t00 = lo ? mfma_f64(a0, b0, z4) : z4;
           const d4_t t10 = lo ? mfma_f64(a1, b0, z4) : z4;
           double o01[4], o11[4], o00[4], o10[4];
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
-            o01[q] = S[w0 + mf_row(lane, q)][cb0 + 16 + li];
-            o11[q] = S[w0 + 16 + mf_row(lane, q)][cb0 + 16 + li];
+            o01[q] = S(w0 + mf_row(lane, q), cb0 + 16 + li);
+            o11[q] = S(w0 + 16 + mf_row(lane, q), cb0 + 16 + li);
             if (lo) {
-              o00[q] = S[w0 + mf_row(lane, q)][cb0 + li];
-              o10[q] = S[w0 + 16 + mf_row(lane, q)][cb0 + li];
+              o00[q] = S(w0 + mf_row(lane, q), cb0 + li);
+              o10[q] = S(w0 + 16 + mf_row(lane, q), cb0 + li);
             }
           }
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
-            S[w0 + mf_row(lane, q)][cb0 + 16 + li] = o01[q] - t01[q];
-            S[w0 + 16 + mf_row(lane, q)][cb0 + 16 + li] = o11[q] - t11[q];
+            S(w0 + mf_row(lane, q), cb0 + 16 + li) = o01[q] - t01[q];
+            S(w0 + 16 + mf_row(lane, q), cb0 + 16 + li) = o11[q] - t11[q];
             if (lo) {
-              S[w0 + mf_row(lane, q)][cb0 + li] = o00[q] - t00[q];
-              S[w0 + 16 + mf_row(lane, q)][cb0 + li] = o10[q] - t10[q];
+              S(w0 + mf_row(lane, q), cb0 + li) = o00[q] - t00[q];
+              S(w0 + 16 + mf_row(lane, q), cb0 + li) = o10[q] - t10[q];
             }
           }
           asm volatile("" ::: "memory");
@@ -780,9 +923,9 @@ __device__ __forceinline__ int diag128_sweep(double (*S)[DP], double *dinv, int 
       // v's: behind its flag)
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        S[w0 + mf_row(lane, q)][w0 + li] -= d00[q];
-        S[w0 + 16 + mf_row(lane, q)][w0 + li] -= d10[q];
-        S[w0 + 16 + mf_row(lane, q)][w0 + 16 + li] -= d11[q];
+        S(w0 + mf_row(lane, q), w0 + li) -= d00[q];
+        S(w0 + 16 + mf_row(lane, q), w0 + li) -= d10[q];
+        S(w0 + 16 + mf_row(lane, q), w0 + 16 + li) -= d11[q];
       }
       asm volatile("" ::: "memory");
       for (int v = jb + 1; v < wave; ++v) {
@@ -796,8 +939,8 @@ __device__ __forceinline__ int diag128_sweep(double (*S)[DP], double *dinv, int 
 #pragma unroll
         for (int kk = 0; kk < NB; kk += 4) {
           const int k = cb0 + kk + lk;
-          const double a0 = S[w0 + li][k], a1 = S[w0 + 16 + li][k];
-          const double b0 = S[v0 + li][k], b1 = S[v0 + 16 + li][k];
+          const double a0 = S(w0 + li, k), a1 = S(w0 + 16 + li, k);
+          const double b0 = S(v0 + li, k), b1 = S(v0 + 16 + li, k);
           t00 = mfma_f64(a0, b0, t00);
           t10 = mfma_f64(a1, b0, t10);
           t11 = mfma_f64(a1, b1, t11);
@@ -805,10 +948,10 @@ __device__ __forceinline__ int diag128_sweep(double (*S)[DP], double *dinv, int 
         }
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-          S[w0 + mf_row(lane, q)][v0 + li] -= t00[q];
-          S[w0 + 16 + mf_row(lane, q)][v0 + li] -= t10[q];
-          S[w0 + 16 + mf_row(lane, q)][v0 + 16 + li] -= t11[q];
-          S[w0 + mf_row(lane, q)][v0 + 16 + li] -= t01[q];
+          S(w0 + mf_row(lane, q), v0 + li) -= t00[q];
+          S(w0 + 16 + mf_row(lane, q), v0 + li) -= t10[q];
+          S(w0 + 16 + mf_row(lane, q), v0 + 16 + li) -= t11[q];
+          S(w0 + mf_row(lane, q), v0 + 16 + li) -= t01[q];
         }
         asm volatile("" ::: "memory");
       }
@@ -820,7 +963,8 @@ __device__ __forceinline__ int diag128_sweep(double (*S)[DP], double *dinv, int 
   mark(7);
   if (sfail) return 1;
   if (pw < DB || !Li) return 0;  // the last panel has no rows below: no inverse needed
-  tinv32(S, w0, dinv + w0);
+  if constexpr (LS::PK) tinv32_pk(S, w0, dinv + w0);
+  else tinv32(S.rows(), w0, dinv + w0);
   if (tblk) {
     // the TRSM-form panel solve (k_potrf_psolve_lat) takes the four inverted
     // diagonal blocks (lower part; it masks the rest) instead of the full inverse
@@ -828,14 +972,15 @@ __device__ __forceinline__ int diag128_sweep(double (*S)[DP], double *dinv, int 
 #pragma unroll
     for (int q = 0; q < NB * NB / 64; ++q) {
       const int e = lane + 64 * q;
-      Li[wave * NB * NB + e] = S[w0 + (e >> 5)][w0 + (e & 31)];
+      Li[wave * NB * NB + e] = S(w0 + (e >> 5), w0 + (e & 31));
     }
     mark(1);
     return 0;
   }
   lds_barrier();
   mark(1);
-  inv_assemble(S, Li, zero_upper);
+  if constexpr (LS::PK) inv_assemble_pk(S, Li, zero_upper);
+  else inv_assemble(S.rows(), Li, zero_upper);
   mark(5);
   return 0;
 }
@@ -926,7 +1071,7 @@ __global__ __launch_bounds__(256) void k_potrf_psolve_lat(int M, const double *L
   }
 }
 
-template <bool ST>
+template <bool ST, bool PK = false>
 __global__ __launch_bounds__(256) void k_potrf_diag128(int n, int K0, double *A, int64_t lda,
                                                        int64_t stride, int *info, double *Linv,
                                                        int sweep) {
@@ -934,16 +1079,16 @@ __global__ __launch_bounds__(256) void k_potrf_diag128(int n, int K0, double *A,
   if (info[b]) return;
   // one dynamic region (no static LDS in front of it): S, then col, then the fail flag
   extern __shared__ double S_[];
-  double(*S)[DP] = reinterpret_cast<double(*)[DP]>(S_);
-  double *col = S_ + DB * DP;
-  int &sfail = *reinterpret_cast<int *>(S_ + DB * DP + DB);
-  int *sflags = reinterpret_cast<int *>(S_ + DB * DP + DB) + 1;
+  constexpr int SN = PK ? DPK_ELEMS : DB * DP;
+  double *col = S_ + SN;
+  int &sfail = *reinterpret_cast<int *>(S_ + SN + DB);
+  int *sflags = reinterpret_cast<int *>(S_ + SN + DB) + 1;
   double *M = A + (int64_t)b * stride + (int64_t)K0 * lda + K0;
   const int pw = min(DB, n - K0);
   const int tid = threadIdx.x;
-  // lower triangle in, identity padding beyond pw, zero upper triangle; 32 loads
-  // in flight per lane before the LDS stores (a load-store loop waits out the
-  // HBM latency once per element)
+  // lower triangle in, identity padding beyond pw, zero upper triangle (packed: the
+  // diagonal tiles' upper parts only); 32 loads in flight per lane before the LDS
+  // stores (a load-store loop waits out the HBM latency once per element)
 #pragma unroll 1
   for (int q0 = 0; q0 < DB * DB / 256; q0 += 32) {
     double v[32];
@@ -954,18 +1099,25 @@ __global__ __launch_bounds__(256) void k_potrf_diag128(int n, int K0, double *A,
     }
 #pragma unroll
     for (int q = 0; q < 32; ++q) {
-      const int e = tid + 256 * (q0 + q);
-      S[e >> 7][e & 127] = v[q];
+      const int e = tid + 256 * (q0 + q), i = e >> 7, j = e & 127;
+      if (!PK) S_[i * DP + j] = v[q];
+      else if (pk_has(i, j)) LdsPk{S_}(i, j) = v[q];
     }
   }
   if (tid == 0) sfail = 0;
   lds_barrier();
   double *Li = Linv ? Linv + (int64_t)b * DB * DB : nullptr;
-  if (sweep)
-    diag128_sweep<ST>(S, col, sfail, sflags, M, lda, pw, K0, info + b, Li, b == 0, K0 == 0,
+  if constexpr (PK) {
+    diag128_sweep<ST>(LdsPk{S_}, col, sfail, sflags, M, lda, pw, K0, info + b, Li, b == 0, K0 == 0,
                       (sweep & 2) != 0);
-  else
-    diag128_core<ST>(S, col, sfail, M, lda, pw, K0, info + b, Li, b == 0, K0 == 0);
+  } else {
+    double(*S)[DP] = reinterpret_cast<double(*)[DP]>(S_);
+    if (sweep)
+      diag128_sweep<ST>(LdsFull{S_}, col, sfail, sflags, M, lda, pw, K0, info + b, Li, b == 0, K0 == 0,
+                        (sweep & 2) != 0);
+    else
+      diag128_core<ST>(S, col, sfail, M, lda, pw, K0, info + b, Li, b == 0, K0 == 0);
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -1132,7 +1284,13 @@ static hipError_t launch_potrf_batched128(hipStream_t s, int n, int batch, doubl
                                (int)DIAG128_LDS) == hipSuccess &&
            hipFuncSetAttribute((const void *)k_potrf_diag128<true>,
                                hipFuncAttributeMaxDynamicSharedMemorySize,
-                               (int)DIAG128_LDS) == hipSuccess;
+                               (int)DIAG128_LDS) == hipSuccess &&
+           hipFuncSetAttribute((const void *)k_potrf_diag128<false, true>,
+                               hipFuncAttributeMaxDynamicSharedMemorySize,
+                               (int)DIAG128_LDS_PK) == hipSuccess &&
+           hipFuncSetAttribute((const void *)k_potrf_diag128<true, true>,
+                               hipFuncAttributeMaxDynamicSharedMemorySize,
+                               (int)DIAG128_LDS_PK) == hipSuccess;
   }();
   if (!attr) return hipErrorInvalidConfiguration;
   hipError_t e = hipMemsetAsync(info, 0, sizeof(int) * batch, s);
@@ -1160,6 +1318,14 @@ static hipError_t launch_potrf_batched128(hipStream_t s, int n, int batch, doubl
   }();
   // (measured: batch 32 0.99 -> 0.86 ms, 64 1.35 -> 1.28 ms, 256 3.64 -> 3.75 ms)
   const bool tblk = sweep && (trsm_env >= 0 ? trsm_env > 0 : batch <= 64);
+  // the diagonal kernel on the packed lower layout (74 KB of LDS: two workgroups per CU)
+  // where there are more matrices than CUs (GPMPC_DIAG_PK = 0 / 1: off / whenever the
+  // sweep runs)
+  static const int pk_env = [] {
+    const char *v = getenv("GPMPC_DIAG_PK");
+    return v ? atoi(v) : -1;
+  }();
+  const bool pk = sweep && (pk_env >= 0 ? pk_env > 0 : batch > 256);
   // panel solve A[c+128:n, c:c+128] <- A[c+128:n, c:c+128] Linv^T (in place)
   auto psolve = [&](int c) {
     const int r = c + DB;
@@ -1264,7 +1430,13 @@ static hipError_t launch_potrf_batched128(hipStream_t s, int n, int batch, doubl
                                           -1.0, 1.0, batch, stride, stride, stride, 1, ks);
         if (e != hipSuccess) return e;
       }
-      if (st)
+      if (pk && st)
+        hipLaunchKernelGGL((k_potrf_diag128<true, true>), dim3(batch), dim3(256), DIAG128_LDS_PK, s, n, c, A,
+                           lda, stride, info, c + DB < n ? Linv : nullptr, sweep | (tblk ? 2 : 0));
+      else if (pk)
+        hipLaunchKernelGGL((k_potrf_diag128<false, true>), dim3(batch), dim3(256), DIAG128_LDS_PK, s, n, c, A,
+                           lda, stride, info, c + DB < n ? Linv : nullptr, sweep | (tblk ? 2 : 0));
+      else if (st)
         hipLaunchKernelGGL(k_potrf_diag128<true>, dim3(batch), dim3(256), DIAG128_LDS, s, n, c, A,
                            lda, stride, info, c + DB < n ? Linv : nullptr, sweep | (tblk ? 2 : 0));
       else

@@ -63,7 +63,10 @@ def test_blocked_trsm_paths(gpu_ctx, n, nrhs):
                                      # unfused column, a ragged 8-wide last block
                                      (520, 256),
                                      # left-looking from batch 128 (multiples of 8): unfused steps (too few workgroups)
-                                     (300, 136)])
+                                     (300, 136),
+                                     # more matrices than CUs: the diagonal kernel on the packed
+                                     # lower LDS layout (two workgroups per CU)
+                                     (300, 520)])
 def test_potrf_batched_dev(gpu_ctx, n, batch):
     """Batched device potrf vs np.linalg.cholesky per matrix (exact_gp.py:164) over
     the batch regimes of launch_potrf_batched128: <= 16 (column-sweep diagonal
@@ -120,11 +123,13 @@ print("switch child ok")
 """
 
 
-@pytest.mark.parametrize("env", [{"GPMPC_POTRF_LA": "1"}, {"GPMPC_SYRK_DIAG": "0"}, {"GPMPC_POTRF_FUSE": "0"}])
+@pytest.mark.parametrize("env", [{"GPMPC_POTRF_LA": "1"}, {"GPMPC_SYRK_DIAG": "0"}, {"GPMPC_POTRF_FUSE": "0"},
+                                 {"GPMPC_DIAG_PK": "1"}, {"GPMPC_DIAG_PK": "1", "GPMPC_POTRF_FUSE": "0"}])
 def test_potrf_switch_paths(gpu_ctx, env):
     """The left-looking potrf's switchable paths (read once per process, so each in a
     child process): the look-ahead diagonal update inside the fused step, the 128-tile
-    diagonal-block update, and the unfused update + panel solve, at n = 520 x 256."""
+    diagonal-block update, the unfused update + panel solve, and the packed-layout
+    diagonal kernel (default above 256 matrices) forced on, at n = 520 x 256."""
     import os
     import subprocess
     import sys
