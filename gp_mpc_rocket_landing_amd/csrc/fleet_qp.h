@@ -52,7 +52,7 @@ __device__ __forceinline__ void lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)\
 #ifndef FQ_FUSED_DIAG
 #define FQ_FUSED_DIAG false  // block solve: G chain first, then the diagonal blocks 4 at a time
 #endif
-// FQ_LAUNDER 1: the diagonal phase's thread index (2: and the items' indices, once per
+// FQ_LAUNDER bit 0: the diagonal phase's thread index, bit 1: the items' indices (once per
 // ADMM iteration) made opaque, so that the addresses derived from them are formed inside
 // the loop rather than hoisted out of it into spilled registers.  Measured
 // (profiles/r5_fleet_launder_ab.log, 3 runs each at 1024 landings): spills 54 -> 3,
@@ -64,7 +64,7 @@ __device__ __forceinline__ void lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)\
 #endif
 __device__ __forceinline__ int fq_tid() {
   int t = threadIdx.x;
-#if FQ_LAUNDER
+#if FQ_LAUNDER & 1
   asm volatile("" : "+v"(t));
 #endif
   return t;
@@ -701,7 +701,7 @@ __device__ __forceinline__ QPResult fq_solve(const QPPattern &pt, FleetSmem &s, 
   int it;
   double o[8], re[4];
   for (it = 1; it <= st.max_iter; ++it) {
-#if FQ_LAUNDER > 1
+#if FQ_LAUNDER & 2
 #pragma unroll
     for (int h = 0; h < FQ_H; ++h) asm volatile("" : "+v"(R.vj[h]), "+v"(R.rr[h]));
 #endif
