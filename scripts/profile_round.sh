@@ -19,7 +19,7 @@ cd /tmp && export TMPDIR=/tmp
 for p in $PASSES; do
   case $p in
     trace) timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run -- \
-             python3 "$ROOT/bench.py" --steps 10 --warmup 3 --no-cpu --no-chol > "$OUT/bench_trace.log" 2>&1 ;;
+             python3 "$ROOT/bench.py" --no-cpu --no-chol > "$OUT/bench_trace.log" 2>&1 ;;
     fulltrace) timeout -k 10 560 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/fulltrace" -o run -- \
              python3 "$ROOT/bench.py" --steps 10 --warmup 3 --no-cpu > "$OUT/bench_fulltrace.log" 2>&1 ;;
     fetch) timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/fetch" -o run -- \
