@@ -266,27 +266,31 @@ struct R6Args {
   const double *ut;       // GPMPC.solve: per-rollout U_ref (B x N x 3)
   R6Rocket rk;
   int *done, *passes, *qit, *qst;
+  int mcv, mcw;  // inducing rows of each GP the predict kernel keeps in LDS (r6_pcache_rows)
 };
+// rows of each GP the predict kernel caches in LDS, feature-major: 720 x (13 + 12) doubles =
+// 141 KB beside its ~4 KB of static LDS (GPMPC_R6_PCACHE rows; 0 = none)
+#define R6_PCACHE_ROWS 720
 
 // ---------------------------------------------------------------------------
 // 1. termination rules + forward simulation with the GP mean
-// sum over the inducing rows i = t0, t0 + stride, .. of k(z, x_i) coef[c][i] (c < 3),
-// two rows per trip with all their loads issued before either is used
+// The kernel rows K*u . coefficients of one GP for this thread's inducing rows t0, t0 +
+// stride, ...: rows below Mc come from the feature-major LDS copy sx (sx[f Mc + i], loaded
+// once per launch), the rest from the row-major global Xs.  Same rows, same order, same
+// fma sequence either way (identical bits); the LDS rows spare the texture path the
+// lane-strided 8-byte loads that bound the phase.
 template <int D>
 __device__ __forceinline__ void r6_kernel_rows(const GpView &v, int M, const double *__restrict__ cf,
-                                               const double *zs, int t0, int stride, double *acc) {
+                                               const double *zs, int t0, int stride, double *acc,
+                                               const double *sx = nullptr, int Mc = 0) {
   double z[D], zn = 0.0;
 #pragma unroll
   for (int f = 0; f < D; ++f) { z[f] = zs[f]; zn += z[f] * z[f]; }  // |z|^2 in the feature order
   const double *__restrict__ Xs = v.Xs;
   const double *__restrict__ Xn = v.Xn;
-  int i = t0;
-  for (; i + stride < M; i += 2 * stride) {
-    const int j = i + stride;
-    double xa[D], xb[D], ca[3], cb[3];
-#pragma unroll
-    for (int f = 0; f < D; ++f) { xa[f] = Xs[(int64_t)i * D + f]; xb[f] = Xs[(int64_t)j * D + f]; }
+  auto row2 = [&](int i, int j, const double (&xa)[D], const double (&xb)[D]) {
     const double na = Xn[i], nb = Xn[j];
+    double ca[3], cb[3];
 #pragma unroll
     for (int c = 0; c < 3; ++c) { ca[c] = cf[(int64_t)c * M + i]; cb[c] = cf[(int64_t)c * M + j]; }
     double da = 0.0, db = 0.0;
@@ -296,17 +300,53 @@ __device__ __forceinline__ void r6_kernel_rows(const GpView &v, int M, const dou
     const double kb = kernel_epilogue(GPMPC_SE_ARD, (zn + nb) - 2.0 * db, v.sigma2, 0.0);
 #pragma unroll
     for (int c = 0; c < 3; ++c) { acc[c] += ka * ca[c]; acc[c] += kb * cb[c]; }
-  }
-  if (i < M) {
+  };
+  auto row1 = [&](int i, const double (&x)[D]) {
     double dot = 0.0;
 #pragma unroll
-    for (int f = 0; f < D; ++f) dot = fma(z[f], Xs[(int64_t)i * D + f], dot);
+    for (int f = 0; f < D; ++f) dot = fma(z[f], x[f], dot);
     const double kv = kernel_epilogue(GPMPC_SE_ARD, (zn + Xn[i]) - 2.0 * dot, v.sigma2, 0.0);
 #pragma unroll
     for (int c = 0; c < 3; ++c) acc[c] += kv * cf[(int64_t)c * M + i];
+  };
+  int i = t0;
+  if (Mc > 0) {  // the LDS rows (feature-major: a wave's 64 rows are 64 consecutive doubles)
+    for (; i + stride < Mc; i += 2 * stride) {
+      double xa[D], xb[D];
+#pragma unroll
+      for (int f = 0; f < D; ++f) { xa[f] = sx[f * Mc + i]; xb[f] = sx[f * Mc + i + stride]; }
+      row2(i, i + stride, xa, xb);
+    }
+    if (i < Mc) {
+      double xa[D];
+#pragma unroll
+      for (int f = 0; f < D; ++f) xa[f] = sx[f * Mc + i];
+      if (i + stride < M) {  // pair it with the first global row (keeps two rows in flight)
+        double xb[D];
+#pragma unroll
+        for (int f = 0; f < D; ++f) xb[f] = Xs[(int64_t)(i + stride) * D + f];
+        row2(i, i + stride, xa, xb);
+        i += 2 * stride;
+      } else {
+        row1(i, xa);
+        i += stride;
+      }
+    }
+  }
+  for (; i + stride < M; i += 2 * stride) {
+    const int j = i + stride;
+    double xa[D], xb[D];
+#pragma unroll
+    for (int f = 0; f < D; ++f) { xa[f] = Xs[(int64_t)i * D + f]; xb[f] = Xs[(int64_t)j * D + f]; }
+    row2(i, j, xa, xb);
+  }
+  if (i < M) {
+    double x[D];
+#pragma unroll
+    for (int f = 0; f < D; ++f) x[f] = Xs[(int64_t)i * D + f];
+    row1(i, x);
   }
 }
-
 
 // the kernels of one horizon, compiled per supported N (fleet6_n.h)
 struct R6Impl {

@@ -78,6 +78,19 @@ __global__ __launch_bounds__(R6_PT) void k_r6_predict(R6Args a) {
   const bool feat_lane = lane == 0 && wave < R6_FEAT_ROLES;
   // features of point 0
   if (a.use_gp && feat_lane) r6_features_role(wave, X[0], Ub, a.gv.ls, a.gw.ls, zq[0], zq[1]);
+  // the first mcv / mcw inducing rows of either GP, feature-major in LDS
+  extern __shared__ double r6_sx[];
+  double *sxv = r6_sx, *sxw = r6_sx + a.mcv * 13;
+  if (a.use_gp) {
+    for (int e = tid; e < a.mcv * 13; e += R6_PT) {
+      const int i = e / 13, f = e - i * 13;
+      sxv[f * a.mcv + i] = a.gv.Xs[e];
+    }
+    for (int e = tid; e < a.mcw * 12; e += R6_PT) {
+      const int i = e / 12, f = e - i * 12;
+      sxw[f * a.mcw + i] = a.gw.Xs[e];
+    }
+  }
   __syncthreads();
   mark(-1);
   for (int k = 0; k < R6_N; ++k) {
@@ -86,8 +99,8 @@ __global__ __launch_bounds__(R6_PT) void k_r6_predict(R6Args a) {
     double acc[6] = {0, 0, 0, 0, 0, 0};
     if (tid < NRT) {
       if (a.use_gp) {
-        r6_kernel_rows<13>(a.gv, a.Mv, a.cv, zq[0], tid, NRT, acc);
-        r6_kernel_rows<12>(a.gw, a.Mw, a.cw, zq[1], tid, NRT, acc + 3);
+        r6_kernel_rows<13>(a.gv, a.Mv, a.cv, zq[0], tid, NRT, acc, sxv, a.mcv);
+        r6_kernel_rows<12>(a.gw, a.Mw, a.cw, zq[1], tid, NRT, acc + 3, sxw, a.mcw);
       }
 #pragma unroll
       for (int c = 0; c < 6; ++c)
@@ -1378,9 +1391,25 @@ static hipError_t r6_init() {
   }();
   return e;
 }
-static void r6_launch_predict(hipStream_t s, int B, const R6Args &a, bool st) {
-  if (st) hipLaunchKernelGGL(k_r6_predict<true>, dim3(B), dim3(R6_PT), 0, s, a);
-  else hipLaunchKernelGGL(k_r6_predict<false>, dim3(B), dim3(R6_PT), 0, s, a);
+static void r6_launch_predict(hipStream_t s, int B, const R6Args &a0, bool st) {
+  static const int cap = [] {
+    const char *v = getenv("GPMPC_R6_PCACHE");
+    return v ? atoi(v) : R6_PCACHE_ROWS;
+  }();
+  static const bool attr = [] {
+    const int mx = (int)(sizeof(double) * 2 * 13 * R6_PCACHE_ROWS);
+    return hipFuncSetAttribute((const void *)k_r6_predict<false>, hipFuncAttributeMaxDynamicSharedMemorySize, mx) ==
+               hipSuccess &&
+           hipFuncSetAttribute((const void *)k_r6_predict<true>, hipFuncAttributeMaxDynamicSharedMemorySize, mx) ==
+               hipSuccess;
+  }();
+  R6Args a = a0;
+  const int c = (attr && a.use_gp) ? min(cap, R6_PCACHE_ROWS) : 0;
+  a.mcv = min(a.Mv, c);
+  a.mcw = min(a.Mw, c);
+  const size_t lds = sizeof(double) * (size_t)(a.mcv * 13 + a.mcw * 12);
+  if (st) hipLaunchKernelGGL(k_r6_predict<true>, dim3(B), dim3(R6_PT), lds, s, a);
+  else hipLaunchKernelGGL(k_r6_predict<false>, dim3(B), dim3(R6_PT), lds, s, a);
 }
 static void r6_launch_control(hipStream_t s, int B, const R6Args &a, bool st) {
   if (st) hipLaunchKernelGGL(k_r6_control<true>, dim3(B), dim3(R6_T), sizeof(R6Smem), s, a);
