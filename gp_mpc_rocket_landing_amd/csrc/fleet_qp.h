@@ -59,6 +59,13 @@ __device__ __forceinline__ void lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)\
 // traffic 47 -> 17 MB per launch, but the kernel 291 -> 303 us (the 17 packed-row
 // addresses of a diagonal round recomputed on the phase's path); off.  The 6-DoF
 // kernel, where the hoisted values were the loop's live state, keeps it (fleet6.h).
+// FQ_AREG 1: each item's column of scaled dynamics values in registers for the solve
+// (the right-hand side's column dots then read only rho z - y from LDS).  Measured
+// (profiles/r5_fleet_areg_ab.log, 3 runs each): 291 -> 322 us (306 with the diagonal
+// phase rolled): the registers are worth more than the LDS reads; off.
+#ifndef FQ_AREG
+#define FQ_AREG 0
+#endif
 #ifndef FQ_LAUNDER
 #define FQ_LAUNDER 0
 #endif
@@ -182,6 +189,9 @@ struct FleetRegs {
   // patterns: column j's dynamics entries, (CSR value index) | (row << 16);
   // row r: first value index | count << 16, column indices two per int
   int cn[2], cp[2][FQ_CMAX];
+#if FQ_AREG
+  double av[2][FQ_CMAX];  // the column's scaled dynamics values (FQ_AREG: read once per solve)
+#endif
   int rbn0, rcp0[(FQ_RMAX + 1) / 2];
   __device__ __forceinline__ double &ur(int h) { return h ? P[1] : ur0; }
   __device__ __forceinline__ double &yr(int h) { return h ? yb1 : yr0; }
@@ -244,7 +254,11 @@ __device__ __forceinline__ double fq_col_dot(const FleetSmem &s, const FleetRegs
   double a[FQ_CMAX], z[FQ_CMAX];
 #pragma unroll
   for (int e = 0; e < FQ_CMAX; ++e) {
+#if FQ_AREG
+    a[e] = R.av[h][e];
+#else
     a[e] = s.A[R.ca(h, e)];
+#endif
     z[e] = s.zt[R.cr(h, e)];
   }
   asm volatile("" : "+v"(a[0]), "+v"(a[1]), "+v"(a[2]), "+v"(a[3]), "+v"(a[4]), "+v"(a[5]),
@@ -670,6 +684,12 @@ __device__ __forceinline__ QPResult fq_solve(const QPPattern &pt, FleetSmem &s, 
   for (int j = n + tid; j < FQ_NMAX; j += FQ_T) s.rhs[j] = 0.0;
   if (tid == 0) s.rho_s = fmin(fmax(s.rho_s, QP_RHO_MIN), QP_RHO_MAX);
   __syncthreads();
+#if FQ_AREG
+#pragma unroll
+  for (int h = 0; h < FQ_H; ++h)
+#pragma unroll
+    for (int e = 0; e < FQ_CMAX; ++e) R.av[h][e] = s.A[R.ca(h, e)];
+#endif
   T.mark(1);
   int f = fq_factor(pt, s, R, st.sigma, cw);
   T.mark(2);
