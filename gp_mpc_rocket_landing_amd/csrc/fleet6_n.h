@@ -1397,7 +1397,7 @@ static void r6_launch_predict(hipStream_t s, int B, const R6Args &a0, bool st) {
     return v ? atoi(v) : R6_PCACHE_ROWS;
   }();
   static const bool attr = [] {
-    const int mx = (int)(sizeof(double) * 2 * 13 * R6_PCACHE_ROWS);
+    const int mx = (int)(sizeof(double) * (13 + 12) * R6_PCACHE_ROWS);  // the largest dynamic size used
     return hipFuncSetAttribute((const void *)k_r6_predict<false>, hipFuncAttributeMaxDynamicSharedMemorySize, mx) ==
                hipSuccess &&
            hipFuncSetAttribute((const void *)k_r6_predict<true>, hipFuncAttributeMaxDynamicSharedMemorySize, mx) ==
