@@ -1404,7 +1404,7 @@ static void r6_launch_predict(hipStream_t s, int B, const R6Args &a0, bool st) {
                hipSuccess;
   }();
   R6Args a = a0;
-  const int c = (attr && a.use_gp) ? min(cap, R6_PCACHE_ROWS) : 0;
+  const int c = (attr && a.use_gp) ? max(0, min(cap, R6_PCACHE_ROWS)) : 0;
   a.mcv = min(a.Mv, c);
   a.mcw = min(a.Mw, c);
   const size_t lds = sizeof(double) * (size_t)(a.mcv * 13 + a.mcw * 12);
