@@ -117,6 +117,10 @@ static int r6_create(gpmpc_ctx *ctx, const GpView &gv, const GpView &gw, bool ex
       gpmpc_set_error("rollout6: cost weights must be non-negative");
       return -2;
     }
+  if (cfg->qp.max_iter < 1) {  // OSQP's validate_settings: "max_iter must be positive"
+    gpmpc_set_error("rollout6: qp.max_iter must be positive");
+    return -2;
+  }
   if (!(cfg->t_max > 0.0) || !(cfg->trust_x2 > 0.0) || !(cfg->trust_u2 > 0.0)) {
     gpmpc_set_error("rollout6: t_max and the trust radii must be positive");
     return -2;

@@ -1239,7 +1239,8 @@ __global__ __launch_bounds__(R6_T) void k_r6_control(R6Args a) {
       mark(8);
       if (last) {
         // max_iter reached (inside the iteration, where its dx / dy live): the final
-        // check unless one just ran, then the approximate one (qp_device.h)
+        // check unless one just ran, then the approximate one (qp_device.h).  max_iter
+        // >= 1 always: r6_create refuses less, as OSQP's settings check does
         for (int ap = can_check ? 1 : 0; ap < 2; ++ap) {
           if (r6_check(s, V, R, Dl, st, o, ap == 1, res.status)) break;
           if (ap == 1) res.status = -2;

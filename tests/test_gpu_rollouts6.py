@@ -194,3 +194,14 @@ def test_rollouts6_solved_setting(gpu_ctx):
     import bench
     seen, S = _run(gpu_ctx, 300, 50, 4, 8, qp=dict(bench.SOLVED_QP6))
     assert seen >= 8, seen
+
+
+def test_rollouts6_rejects_nonpositive_max_iter(gpu_ctx):
+    """OSQP's settings check refuses max_iter <= 0 ("max_iter must be positive"); the
+    device controller, which runs its final termination checks inside the last ADMM
+    iteration, refuses it at creation the same way."""
+    from gp_mpc_rocket_landing_amd import _lib
+    from gp_mpc_rocket_landing_amd.rollouts6 import Rollouts6, fit_structured_fitc
+    gv, gw = fit_structured_fitc(gpu_ctx, n_train=120, n_inducing=20)
+    with pytest.raises(_lib.HIPError, match="max_iter must be positive"):
+        Rollouts6(gpu_ctx, gv, gw, 2, max_iter=0)
