@@ -15,6 +15,7 @@
 #include <rccl/rccl.h>
 #include <dlfcn.h>
 #include <cmath>
+#include <algorithm>
 #include <cstring>
 #include <vector>
 
@@ -70,6 +71,10 @@ struct gpmpc_comm {
   int nranks = 0, rank = 0, device = 0;
   DevBuf send, recv;  // padded blocks (grown on demand)
   bool prepared = false;  // gpmpc_gather_prepare succeeded since the last collective
+  // what that prepare was for: the collective must be called with the same counts and
+  // root, since the send / receive buffers were sized and padded for them
+  int prep_root = -1;
+  std::vector<int> prep_counts;
 };
 
 extern "C" int gpmpc_comm_unique_id(unsigned char *id) {
@@ -154,6 +159,8 @@ extern "C" int gpmpc_gather_prepare(gpmpc_ctx *ctx, gpmpc_comm *c, const double 
   GPMPC_CHECK_ARG(count == 0 || d_records);
   c->prepared = false;
   if (p.cmax == 0) {
+    c->prep_root = root;
+    c->prep_counts.assign(counts, counts + c->nranks);
     c->prepared = true;
     return 0;
   }
@@ -167,6 +174,8 @@ extern "C" int gpmpc_gather_prepare(gpmpc_ctx *ctx, gpmpc_comm *c, const double 
                      c->send.as<double>());
   GPMPC_HIP(hipGetLastError());
   GPMPC_HIP(hipStreamSynchronize(s));
+  c->prep_root = root;
+  c->prep_counts.assign(counts, counts + c->nranks);
   c->prepared = true;
   return 0;
 }
@@ -179,6 +188,10 @@ extern "C" int gpmpc_gather_collective(gpmpc_ctx *ctx, gpmpc_comm *c, const int 
   if (!c->prepared) {
     gpmpc_set_error("gather: gpmpc_gather_prepare did not succeed on this rank");
     return -2;
+  }
+  if (root != c->prep_root || !std::equal(c->prep_counts.begin(), c->prep_counts.end(), counts)) {
+    gpmpc_set_error("gather: counts / root differ from those gpmpc_gather_prepare was called with");
+    return -2;  // (the prepared block stays valid for a call with the right arguments)
   }
   c->prepared = false;
   if (p.cmax == 0) return 0;

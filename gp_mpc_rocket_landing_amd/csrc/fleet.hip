@@ -62,6 +62,13 @@ struct gpmpc_fleet {
   bool fuse_post = true;                     // GPMPC_FLEET_FUSE_POST=0: separate k_post_finish
   int64_t post_P = 0;                        // query rows / partial row tiles of the last
   int post_nrt = 0;                          //   posterior GEMM (fused finish reads them)
+  // Every size-dependent path choice is made once, at creation, for plan_B landings (the
+  // fleet's own size, or the whole Monte-Carlo fleet this one is a shard of): the kernels
+  // differ in summation order, so choosing them from the running count or the shard size
+  // would make a landing's bits depend on how many others fly beside it
+  int plan_B = 0;
+  int post_kind = 0;                         // posterior GEMM kernel (gemm_sumsq_kind at plan_B N)
+  bool post_few = false;                     // queries + K* in one launch (<= 64 planned query rows)
 };
 
 extern "C" int gpmpc_fleet_set_stamps(gpmpc_fleet *f, void *dev_u64x16) {
@@ -508,8 +515,32 @@ __global__ __launch_bounds__(FQ_T) __attribute__((amdgpu_waves_per_eu(FQ_WPE, FQ
   const int N = a.N, n = a.pt.n, m = a.pt.m;
   const double dt = a.dt;
   double *rec = a.rec + (int64_t)b * GPMPC_REC_LEN;
-  if (rec[0] != 0.0) return;  // terminated landing
-  if (a.sqp && !a.sqp_first && a.sqp_done[b]) return;  // converged in an earlier SQP pass
+  // The posterior finish of this slot's queries (k_post_finish's arithmetic) for a landing
+  // that returns before its QP assembly: every launched slot is finished, so a slot never
+  // keeps the values another landing left in it at an earlier step; the
+  // posterior is the one at this landing's linearisation trajectory, as on the unfused path
+  auto finish_only = [&]() {
+    if (!(a.part && a.use_gp)) return;
+    for (int k = tid; k < N; k += FQ_T) {
+      const int64_t q = (int64_t)(a.gp_by_slot ? (int)blockIdx.x : b) * N + k;
+      double ss = 0.0;
+      for (int t = 0; t < a.nrt; ++t) ss += a.part[(int64_t)t * a.pld + q];
+      double lat = a.sigma2 - ss;
+      lat = lat > 1e-10 ? lat : 1e-10;
+      for (int c = 0; c < 3; ++c) {
+        a.mean_out[q * 3 + c] = a.meanT[(int64_t)c * a.pld + q] * a.ystd[c] + a.ymean[c];
+        a.var_out[q * 3 + c] = lat * a.ystd[c] * a.ystd[c];
+      }
+    }
+  };
+  if (rec[0] != 0.0) {  // terminated landing
+    finish_only();
+    return;
+  }
+  if (a.sqp && !a.sqp_first && a.sqp_done[b]) {  // converged in an earlier SQP pass
+    finish_only();
+    return;
+  }
   QPStamps T;
   T.out = (STAMPS && b == 0) ? a.stamps : nullptr;
   T.start();
@@ -579,6 +610,7 @@ __global__ __launch_bounds__(FQ_T) __attribute__((amdgpu_waves_per_eu(FQ_WPE, FQ
       rec[2] = rec[13] - sx[0];
       for (int i = 0; i < NX; ++i) rec[4 + i] = sx[i];
     }
+    finish_only();
     return;
   }
   FleetRegs R;
@@ -859,9 +891,9 @@ __global__ void k_fleet_reset(int first, int count, int N, int target_mode,
 }
 
 // ---------------------------------------------------------------------------
-extern "C" int gpmpc_fleet_create(gpmpc_ctx *ctx, gpmpc_gp *gp, const gpmpc_fleet_config *cfg,
-                                  int batch, gpmpc_fleet **out) {
-  GPMPC_CHECK_ARG(ctx && gp && cfg && out && batch > 0);
+extern "C" int gpmpc_fleet_create_shard(gpmpc_ctx *ctx, gpmpc_gp *gp, const gpmpc_fleet_config *cfg,
+                                        int batch, int fleet_batch, gpmpc_fleet **out) {
+  GPMPC_CHECK_ARG(ctx && gp && cfg && out && batch > 0 && fleet_batch >= batch);
   const GpView g = gp_view(gp);
   GPMPC_CHECK_ARG(g.d == NFEAT && g.n_out == 3);
   if (g.kind < GPMPC_SE_ARD || g.kind > GPMPC_MATERN52) {
@@ -913,8 +945,12 @@ extern "C" int gpmpc_fleet_create(gpmpc_ctx *ctx, gpmpc_gp *gp, const gpmpc_flee
     return -1;
   }
   const size_t B = batch, P = (size_t)batch * N;
-  // W rows + the 3 alpha^T rows; at least the column-stationary posterior's two halves
-  const int nrt = std::max(gemm_row_tiles(g.n + 3, (int)P, g.n), POST_CS_PARTS);
+  f->plan_B = fleet_batch;
+  f->post_kind = gemm_sumsq_kind(g.n + 3, (int)std::min<int64_t>((int64_t)fleet_batch * N, 1 << 30), g.n);
+  f->post_few = (int64_t)fleet_batch * N <= 64 && g.d == NFEAT;
+  // partial rows of any posterior path: W rows + the 3 alpha^T rows in 64-row tiles (the
+  // most rows any kernel writes), at least the column-stationary posterior's two halves
+  const int nrt = std::max(gemm_sumsq_rows(GEMM_SUMSQ_64, g.n + 3), POST_CS_PARTS);
   if (f->x.alloc(sizeof(double) * B * NX) || f->Xw.alloc(sizeof(double) * B * (N + 1) * NX) ||
       f->Uw.alloc(sizeof(double) * B * N * NU) || f->ysc.alloc(sizeof(double) * B * m) ||
       f->rho.alloc(sizeof(double) * B) || f->rec.alloc(sizeof(double) * B * GPMPC_REC_LEN) ||
@@ -961,7 +997,7 @@ extern "C" int gpmpc_fleet_create(gpmpc_ctx *ctx, gpmpc_gp *gp, const gpmpc_flee
   int cus = 0;
   (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device);
   const char *we = getenv("GPMPC_FLEET_WIDE");
-  f->wide = f->use_fq && (we ? atoi(we) != 0 : (int)B <= cus);
+  f->wide = f->use_fq && (we ? atoi(we) != 0 : fleet_batch <= cus);
   if (cfg->sqp_iters > 1 && !f->use_fq) {  // the SQP pass is implemented in k_fleet_control2
     delete f;
     gpmpc_set_error("fleet: sqp_iters > 1 needs the fleet solver (N = 20, GPMPC_FLEET_SOLVER != 0)");
@@ -970,6 +1006,11 @@ extern "C" int gpmpc_fleet_create(gpmpc_ctx *ctx, gpmpc_gp *gp, const gpmpc_flee
   GPMPC_HIP(hipStreamSynchronize(ctx->stream));
   *out = f;
   return 0;
+}
+
+extern "C" int gpmpc_fleet_create(gpmpc_ctx *ctx, gpmpc_gp *gp, const gpmpc_fleet_config *cfg, int batch,
+                                  gpmpc_fleet **out) {
+  return gpmpc_fleet_create_shard(ctx, gp, cfg, batch, batch, out);
 }
 
 extern "C" int gpmpc_fleet_reset(gpmpc_fleet *f, int first, int count, const double *x0) {
@@ -1011,9 +1052,9 @@ static hipError_t fleet_gp_posterior(gpmpc_fleet *f, int mask) {
   // workgroup inside the MFMA pass, never in HBM; two partial rows
   const bool cs = g.Wf && post_cs_env();
   const bool fused = !cs && fused_env && g.d >= 11 && g.d <= 13;
-  const int nrt = cs ? POST_CS_PARTS : fused ? (g.n + 3 + 127) / 128 : gemm_row_tiles(g.n + 3, (int)P, g.n);
+  const int nrt = cs ? POST_CS_PARTS : fused ? (g.n + 3 + 127) / 128 : gemm_sumsq_rows(f->post_kind, g.n + 3);
   hipError_t e = hipSuccess;
-  if ((mask & 1) && !fused && !cs && P <= 64 && g.d == NFEAT) {
+  if ((mask & 1) && !fused && !cs && f->post_few) {
     hipLaunchKernelGGL(k_fleet_queries_gram, dim3((g.n + 63) / 64), dim3(256), 0, s, nb, f->N, f->Xw.as<double>(),
                        f->Uw.as<double>(), g.ls, g.kind == GPMPC_SE_ISO, f->use_order ? f->order.as<int>() : nullptr,
                        g.kind, g.Xs, g.Xn, g.n, g.sigma2, g.iso_scale, f->Ks.as<double>());
@@ -1039,7 +1080,7 @@ static hipError_t fleet_gp_posterior(gpmpc_fleet *f, int mask) {
                                  f->meanT.as<double>(), P);
     else
       e = launch_gemm_sumsq_mean(s, g.n, 3, P, g.W, f->Ks.as<double>(), f->part.as<double>(), P,
-                                 f->meanT.as<double>(), P);
+                                 f->meanT.as<double>(), P, f->post_kind);
     if (e != hipSuccess) return e;
   }
   if (mask & 4) {
@@ -1262,9 +1303,9 @@ extern "C" int gpmpc_fleet_get_state(gpmpc_fleet *f, double *Xw, double *Uw, dou
 // landing (B x N x 3 each, row-major): the mean and variance the step's QP assembly
 // consumed (the variance is computed beside it, exact_gp.py:256-266, and not read by
 // the QP).  The device rows follow the dispatch slots of that step; they are put back
-// in landing order here.  Valid for the landings that were running at the start of that
-// step; landings past the step's running prefix read NaN, and a landing that terminated
-// at the step's top keeps the values of its last running step.
+// in landing order here.  Every slot of the step's launched prefix is finished (the
+// control kernel finishes the slots of landings that return before their QP too), so a
+// landing in it reads the posterior at its own trajectory; landings past it read NaN.
 extern "C" int gpmpc_fleet_get_posterior(gpmpc_fleet *f, double *mean, double *var) {
   GPMPC_CHECK_ARG(f && (mean || var));
   if (!f->cfg.use_gp) {

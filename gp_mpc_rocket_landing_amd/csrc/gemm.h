@@ -64,10 +64,15 @@ hipError_t launch_trsm_lower_ex(hipStream_t s, int n, int nrhs, const double *L,
 
 // posterior in one pass: Wext = [W (n x n, lower); alpha^T (n_out x n)]:
 // part[t][j] = sum over W rows of tile t of (W K*^T)^2, meanT = alpha^T K*^T
-// (n_out x P).  part has gemm_row_tiles(n + n_out) rows.
+// (n_out x P).  part has gemm_row_tiles(n + n_out) rows -- gemm_sumsq_rows(kind) with a
+// forced kind.  The kernels sum in different k orders (not the same bits), so a caller
+// whose P shrinks over time passes the kind of its planned size (gemm_sumsq_kind).
+enum { GEMM_SUMSQ_64 = 0, GEMM_SUMSQ_128 = 1, GEMM_SUMSQ_SPLITK = 2 };
+int gemm_sumsq_kind(int M, int N, int K);
+inline int gemm_sumsq_rows(int kind, int M) { return kind == GEMM_SUMSQ_128 ? (M + 127) / 128 : (M + 63) / 64; }
 hipError_t launch_gemm_sumsq_mean(hipStream_t s, int n, int n_out, int P, const double *Wext,
                                   const double *Ks, double *part, int64_t ldp, double *meanT,
-                                  int64_t ldm);
+                                  int64_t ldm, int kind = -1);
 
 // the same pass with K* formed in the operand load from the scaled query rows
 // Qs (P x d) / norms Qn and training rows Xs (n x d) / norms Xn (d = 11..13;

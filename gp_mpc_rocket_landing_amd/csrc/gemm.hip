@@ -1030,16 +1030,42 @@ static bool launch_splitk_sumsq(hipStream_t s, int M, int N, int K, const double
   return true;
 }
 
+static int gemm_big_env() {
+  static const int v = [] {
+    const char *e = getenv("GPMPC_GEMM128");
+    return e ? atoi(e) : 1;
+  }();
+  return v;
+}
+
+static int gemm_kmin_env() {
+  static const int v = [] {
+    const char *e = getenv("GPMPC_GEMM128_KMIN");
+    return e ? atoi(e) : 2 * BT;
+  }();
+  return v;
+}
+
+// The kernel launch_gemm_sumsq_mean picks for an (M x K) [W; alpha^T] against N query
+// rows (batch 1, triangular A): the rules of launch_gemm_impl below.  A caller whose column
+// count shrinks over time (the fleet's running prefix) fixes this at its planned size and
+// passes it back, so every column sees the same kernel, hence the same bits.
+int gemm_sumsq_kind(int M, int N, int K) {
+  if (gemm_big_env() && M >= 2 * BT && N >= 2 * BT && K >= gemm_kmin_env()) return GEMM_SUMSQ_128;
+  if (splitk_env() && N <= GT && K >= 256 && std::max(1, std::min(512 / ((M + GT - 1) / GT), K / 64)) >= 2)
+    return GEMM_SUMSQ_SPLITK;
+  return GEMM_SUMSQ_64;
+}
+
 static hipError_t launch_gemm_impl(hipStream_t s, int epi, int M, int N, int K, const double *A,
                                    int64_t lda, const double *B, int64_t ldb, double *C,
                                    int64_t ldc, double alpha, double beta, int tri_a, int lower_c,
                                    int batch, int64_t sA, int64_t sB, int64_t sC, int msum,
-                                   double *Cm, int64_t ldm) {
+                                   double *Cm, int64_t ldm, int kind = -1) {
   if (M <= 0 || N <= 0) return hipSuccess;
-  static const int big_env = [] {
-    const char *e = getenv("GPMPC_GEMM128");
-    return e ? atoi(e) : 1;
-  }();
+  const int big_env = gemm_big_env();
+  // kind >= 0 (EPI_SUMSQ, batch 1): that kernel, whatever the size (gemm_sumsq_kind)
+  if (epi != EPI_SUMSQ || batch != 1) kind = -1;
   const bool tg = lower_c && M == N && !tri_a;
   // a lower-triangular batch takes 128-tiles only when they fill >= 2 rounds
   // of 512 resident workgroups or K is long enough to split; otherwise they
@@ -1070,11 +1096,9 @@ static hipError_t launch_gemm_impl(hipStream_t s, int epi, int M, int N, int K, 
                        alpha, (int)tg, tx, T, sA, sB, sC, total);
     return hipGetLastError();
   }
-  static const int kmin_env = [] {
-    const char *e = getenv("GPMPC_GEMM128_KMIN");
-    return e ? atoi(e) : 2 * BT;
-  }();
-  if (big_env && tri_ok && M >= 2 * BT && N >= 2 * BT && K >= kmin_env) {
+  const int kmin_env = gemm_kmin_env();
+  const bool use128 = kind >= 0 ? kind == GEMM_SUMSQ_128 : big_env && tri_ok && M >= 2 * BT && N >= 2 * BT && K >= kmin_env;
+  if (use128) {
     const int tx = (N + BT - 1) / BT, ty = (M + BT - 1) / BT;
     // split K when the tiles cannot give each CU ~4 workgroups to interleave (STORE
     // with beta = 1: partial products are added atomically); >= 512 of K per split
@@ -1113,7 +1137,8 @@ static hipError_t launch_gemm_impl(hipStream_t s, int epi, int M, int N, int K, 
     hipError_t e = hipSuccess;
     if (launch_splitk(s, 0, M, N, K, A, lda, B, ldb, C, ldc, alpha, beta, e)) return e;
   }
-  if (epi == EPI_SUMSQ && batch == 1 && gemm_row_tiles(M, N, K) == (M + GT - 1) / GT) {
+  if (epi == EPI_SUMSQ && batch == 1 &&
+      (kind >= 0 ? kind == GEMM_SUMSQ_SPLITK : gemm_row_tiles(M, N, K) == (M + GT - 1) / GT)) {
     hipError_t e = hipSuccess;  // (a triangular A's zero chunks are multiplied: the split is latency work)
     if (launch_splitk_sumsq(s, M, N, K, A, lda, B, ldb, C, ldc, msum, Cm, ldm, e)) return e;
   }
@@ -1213,7 +1238,7 @@ hipError_t launch_gemm_nt(hipStream_t s, int epi, int M, int N, int K, const dou
 
 hipError_t launch_gemm_sumsq_mean(hipStream_t s, int n, int n_out, int P, const double *Wext,
                                   const double *Ks, double *part, int64_t ldp, double *meanT,
-                                  int64_t ldm) {
+                                  int64_t ldm, int kind) {
   return launch_gemm_impl(s, EPI_SUMSQ, n + n_out, P, n, Wext, n, Ks, n, part, ldp, 1.0, 0.0, 1, 0,
-                          1, 0, 0, 0, n, meanT, ldm);
+                          1, 0, 0, 0, n, meanT, ldm, kind);
 }

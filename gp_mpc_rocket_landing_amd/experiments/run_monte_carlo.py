@@ -83,7 +83,9 @@ def main(argv=None):
         x0 = initial_conditions_6dof(count, args.seed0, first) if count else None
     else:
         gp = fit_gp(ctx, n_train=args.train)          # every rank fits the same GP deterministically
-        fl = Fleet(ctx, gp, max(count, 1), max_steps=args.max_steps)
+        # a shard of the whole fleet: kernel choices made for args.landings, so every
+        # landing's record is bit-identical to the unsharded run's
+        fl = Fleet(ctx, gp, max(count, 1), fleet_batch=max(args.landings, 1), max_steps=args.max_steps)
         x0 = initial_conditions(count, args.seed0, first) if count else None
     t0 = time.perf_counter()
     rec = np.zeros((0, _lib.REC_LEN))

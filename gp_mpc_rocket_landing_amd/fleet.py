@@ -32,14 +32,20 @@ def fit_gp(ctx, n_train=1000, seed=0, noise=1e-4):
 
 
 class Fleet:
-    def __init__(self, ctx, gp, batch, **config):
+    """``fleet_batch``: the size of the whole Monte-Carlo fleet when this one is a
+    shard of it (gpmpc_fleet_create_shard): every size-dependent kernel choice is made
+    for that size, so the shard's landings come out bit-identical to the same landings
+    in the whole fleet.  Default: the fleet is whole."""
+
+    def __init__(self, ctx, gp, batch, fleet_batch=None, **config):
         self.ctx = ctx
         self.gp = gp  # keep the GP alive: the fleet reads its device factor
         self.cfg = _lib.fleet_default_config(**config)
         self.batch = int(batch)
+        self.fleet_batch = int(fleet_batch) if fleet_batch is not None else self.batch
         h = ctypes.c_void_p()
-        _lib._chk(_lib._L.gpmpc_fleet_create(ctx.h, gp.h, ctypes.byref(self.cfg), self.batch,
-                                             ctypes.byref(h)), "fleet_create")
+        _lib._chk(_lib._L.gpmpc_fleet_create_shard(ctx.h, gp.h, ctypes.byref(self.cfg), self.batch,
+                                                   self.fleet_batch, ctypes.byref(h)), "fleet_create")
         self.h = h
 
     def reset(self, x0, first=0):

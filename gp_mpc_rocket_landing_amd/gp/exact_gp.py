@@ -227,6 +227,14 @@ class ExactGP:
                     lml[i], steps[i] = h.lml[0], h.jitter_steps
                 except ValueError:   # exact_gp.py:383-386: a failed fit is +inf for the optimiser
                     lml[i], steps[i] = -np.inf, -1
+                except _lib.HIPError as e:
+                    # parameters the device refuses as a kernel program (a lengthscale that
+                    # underflowed to 0 from exp(p), a negative variance): the reference's
+                    # fit fails on them too (a non-finite Gram), which its objective turns
+                    # into +inf; any other device error propagates
+                    if e.rc != -2:
+                        raise
+                    lml[i], steps[i] = -np.inf, -1
             return lml, steps
         kind = None
         ls, s2 = [], []

@@ -32,7 +32,8 @@ extern "C" {
  * gpmpc_rollout6_solve_ref (X_ref / U_ref), gpmpc_comm_count (round 4); round 4 also
  * gave gpmpc_fleet_config.sqp_qp the max_iter = 0 "same as qp" meaning.  Round 5 adds
  * entry points only (gpmpc_fleet_get_posterior, gpmpc_gather_prepare / _collective) and
- * refuses a fleet config whose sqp_qp was edited with max_iter left 0. */
+ * refuses a fleet config whose sqp_qp was edited with max_iter left 0.  Round 6 adds
+ * entry points only (gpmpc_fleet_create_shard). */
 #define GPMPC_ABI_VERSION 3
 
 typedef struct gpmpc_ctx gpmpc_ctx;
@@ -265,6 +266,14 @@ typedef struct {
 void gpmpc_fleet_default_config(gpmpc_fleet_config *c);
 int gpmpc_fleet_create(gpmpc_ctx *ctx, gpmpc_gp *gp, const gpmpc_fleet_config *cfg, int batch,
                        gpmpc_fleet **out);
+/* A shard of batch landings of a Monte-Carlo fleet of fleet_batch landings (>= batch;
+ * gpmpc_fleet_create = fleet_batch equal to batch).  Every size-dependent path choice
+ * (the posterior GEMM's kernel, the few-query posterior launch, the control kernel's
+ * build) is made once, here, for fleet_batch landings -- never from the running count --
+ * so each landing's results are bit-identical whatever the shard size and however many
+ * landings still fly beside it. */
+int gpmpc_fleet_create_shard(gpmpc_ctx *ctx, gpmpc_gp *gp, const gpmpc_fleet_config *cfg, int batch,
+                             int fleet_batch, gpmpc_fleet **out);
 /* (re)initialise landings [first, first+count) from x0 (count x 7) */
 int gpmpc_fleet_reset(gpmpc_fleet *f, int first, int count, const double *x0);
 /* advance every active landing by nsteps control steps (async on the ctx stream) */
@@ -289,8 +298,10 @@ int gpmpc_fleet_get_state(gpmpc_fleet *f, double *Xw, double *Uw, double *y_scal
 /* the last control step's GP posterior at every landing's N horizon points
  * (ExactGP.predict, exact_gp.py:256-266, over the step's linearisation
  * trajectory): mean and variance, batch x N x 3 each, in landing order (either
- * may be NULL).  Valid for the landings running at the start of that step;
- * landings past its running prefix read NaN.  -2 when use_gp = 0. */
+ * may be NULL).  The step covers the running prefix of its dispatch order (every
+ * landing running at its start, plus terminated ones the host had not yet read):
+ * those read the posterior at their own trajectory, landings past it read NaN.
+ * -2 when use_gp = 0. */
 int gpmpc_fleet_get_posterior(gpmpc_fleet *f, double *mean, double *var);
 /* diagnostic: accumulate s_memtime cycles of landing 0's control kernel per
  * phase into dev_u64x16 (16 x uint64 device buffer; NULL disables):
@@ -449,7 +460,8 @@ int gpmpc_gather_results(gpmpc_ctx *ctx, gpmpc_comm *c, const double *d_records,
  * block; the stream is drained before it returns), so every failure a rank can
  * meet alone is reported by it; collective issues only the ncclGather and the
  * root's compaction, and fails with -2 unless prepare succeeded since the last
- * collective.  Agree on every rank's prepare status before any rank calls
+ * collective with the same counts and root (the buffers were sized and padded for
+ * them; a call with other arguments leaves the prepared block for the right one).  Agree on every rank's prepare status before any rank calls
  * collective (sharding.gather_shard_records does, with one all-reduce). */
 int gpmpc_gather_prepare(gpmpc_ctx *ctx, gpmpc_comm *c, const double *d_records, const int *counts, int root);
 int gpmpc_gather_collective(gpmpc_ctx *ctx, gpmpc_comm *c, const int *counts, int root, double *out);

@@ -61,3 +61,27 @@ def test_gather_shard_records_world1_reports_rccl(gpu_ctx):
         assert info == {"path": "rccl", "nranks": 1, "records": 21, "requested": "rccl", "fallback": None}
     finally:
         fl.close()
+
+
+def test_gather_collective_refuses_counts_other_than_prepared(gpu_ctx):
+    """gpmpc_gather_collective with counts or a root other than those its prepare
+    sized and padded the buffers for returns -2 instead of gathering a block of
+    another size; the prepared block stays valid for the right call."""
+    from gp_mpc_rocket_landing_amd import _lib
+    from gp_mpc_rocket_landing_amd.fleet import Fleet, fit_gp, initial_conditions
+    from gp_mpc_rocket_landing_amd.sharding import RCCLRecordGather
+    gp = fit_gp(gpu_ctx, n_train=200)
+    fl = Fleet(gpu_ctx, gp, 9)
+    g = RCCLRecordGather(gpu_ctx)
+    try:
+        fl.reset(initial_conditions(9))
+        fl.step(2)
+        rec, _ = fl.read()
+        g.prepare(fl.records_dev, 9)
+        out = np.empty((40, _lib.REC_LEN))
+        rc = _lib._L.gpmpc_gather_collective(gpu_ctx.h, g.h, _lib._i(np.array([40], np.int32)), 0, _lib._d(out))
+        assert rc == -2 and "differ" in _lib._L.gpmpc_last_error().decode()
+        np.testing.assert_array_equal(g.collective(9), rec)
+    finally:
+        g.close()
+        fl.close()

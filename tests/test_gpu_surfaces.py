@@ -426,3 +426,9 @@ def test_composite_kernels_through_the_surfaces_vs_f13(gpu_ctx):
         spec = ("sum", ("se_ard", np.exp(p[0]), np.exp(p[1:nk - 1])), ("white", np.exp(p[nk - 1])))
         want = gp_oracle.exact_fit(Z, Y[:, :1], kind=spec, noise=np.exp(p[nk]))["lml"][0]
         assert abs(lml[i] - want) <= 1e-6 * abs(want), (i, lml[i], want)
+    # a row whose lengthscale underflows to 0 (exp(-800)): the device refuses the program
+    # (rc -2), which the objective records as a failed fit (-inf LML, +inf for the
+    # optimiser, exact_gp.py:383-387) beside the valid rows instead of aborting
+    bad = p0.copy(); bad[1] = -800.0
+    lml2, steps2 = gp._lml_batch(np.stack([p0, bad]), Z, Y[:, 0])
+    assert lml2[0] == lml[0] and lml2[1] == -np.inf and steps2[1] == -1
