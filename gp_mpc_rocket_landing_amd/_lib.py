@@ -76,7 +76,7 @@ class Rollout6Config(ctypes.Structure):
                 ("trust_u2", ctypes.c_double), ("use_gp_mean", ctypes.c_int), ("upright_target", ctypes.c_int),
                 ("rocket_j", ctypes.c_double * 3), ("rocket_r_t", ctypes.c_double * 3),
                 ("rocket_g_i", ctypes.c_double * 3), ("rocket_alpha", ctypes.c_double),
-                ("rocket_g0", ctypes.c_double)]
+                ("rocket_g0", ctypes.c_double), ("rocket_J", ctypes.c_double * 9)]
 
 
 class FleetConfig(ctypes.Structure):
@@ -95,6 +95,10 @@ def _sig(name, res, *args):
 
 _c = ctypes.c_int
 _sig("gpmpc_abi_version", _c)
+ABI_VERSION = 4   # include/gpmpc.h GPMPC_ABI_VERSION this binding's structures follow
+if _L.gpmpc_abi_version() != ABI_VERSION:
+    raise ImportError(f"{LIB_PATH} has C-ABI {_L.gpmpc_abi_version()}, this binding needs {ABI_VERSION}: "
+                      "rebuild it (__graft_entry__.build())")
 _sig("gpmpc_last_error", ctypes.c_char_p)
 _sig("gpmpc_ctx_create", _c, _c, ctypes.POINTER(_vp))
 _sig("gpmpc_ctx_destroy", _c, _vp)

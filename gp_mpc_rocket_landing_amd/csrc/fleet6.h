@@ -42,11 +42,20 @@
 #define R6_T_MIN 0.5
 #define R6_T_MAX 5.0
 
-// the rocket (Rocket6DoFConfig, rocket_6dof.py:36-84): diagonal J_B, thrust point
-// r_T_B, gravity g_I, alpha = 1 / (I_sp g0), g0 -- kernel arguments (uniform values)
+// the rocket (Rocket6DoFConfig, rocket_6dof.py:36-84): J_B, thrust point r_T_B, gravity
+// g_I, alpha = 1 / (I_sp g0), g0 -- kernel arguments (uniform values).  A diagonal J_B
+// runs as its diagonal J (divisions, the arithmetic of round 5); any other (full = 1)
+// as the row-major tensor Jf and its inverse Ji: w' = Ji (r_T x u - w x Jf w), the
+// ca.solve(J, .) of nominal_mpc.py:196-199 with the inverse formed once on the host
 struct R6Rocket {
   double J[3], rT[3], gI[3], alpha, g0;
+  double Jf[9], Ji[9];
+  int full;
 };
+
+__device__ __forceinline__ void r6_mat3(const double *M, const double *v, double *o) {
+  for (int i = 0; i < 3; ++i) o[i] = (M[3 * i] * v[0] + M[3 * i + 1] * v[1]) + M[3 * i + 2] * v[2];
+}
 
 
 // problem data in device memory (read per thread with a dynamic index, so not a
@@ -91,6 +100,15 @@ static __device__ void r6_f(const R6Rocket &rk, const double *x, const double *u
   // r_T x u; w x J w
   const double *rT = rk.rT, *J = rk.J;
   const double tq[3] = {rT[1] * u[2] - rT[2] * u[1], rT[2] * u[0] - rT[0] * u[2], rT[0] * u[1] - rT[1] * u[0]};
+  if (rk.full) {
+    const double w[3] = {wx, wy, wz};
+    double jw[3];
+    r6_mat3(rk.Jf, w, jw);
+    const double r[3] = {tq[0] - (wy * jw[2] - wz * jw[1]), tq[1] - (wz * jw[0] - wx * jw[2]),
+                         tq[2] - (wx * jw[1] - wy * jw[0])};
+    r6_mat3(rk.Ji, r, o + 11);
+    return;
+  }
   const double jw[3] = {J[0] * wx, J[1] * wy, J[2] * wz};
   const double cx[3] = {wy * jw[2] - wz * jw[1], wz * jw[0] - wx * jw[2], wx * jw[1] - wy * jw[0]};
   for (int i = 0; i < 3; ++i) o[11 + i] = (tq[i] - cx[i]) / J[i];
@@ -143,14 +161,34 @@ static __device__ void r6_neg_lin(const R6Rocket &rk, const double *x, const dou
   const double Qw[4][3] = {{-qx, -qy, -qz}, {qw, qz, -qy}, {-qz, qw, qx}, {qy, -qx, qw}};
   for (int i = 0; i < 4; ++i)
     for (int j = 0; j < 3; ++j) set(7 + i, 11 + j, -(0.5 * Qw[i][j] * dt));
+  const double rx = rk.rT[0], ry = rk.rT[1], rz = rk.rT[2];
+  const double Rx[3][3] = {{0, -rz, ry}, {rz, 0, -rx}, {-ry, rx, 0}};
+  if (rk.full) {
+    // d/dw Ji (-w x Jf w) = Ji ([Jf w]x - [w]x Jf);  B_c omega rows: Ji [r_T]x
+    const double w[3] = {wx, wy, wz};
+    double jw[3];
+    r6_mat3(rk.Jf, w, jw);
+    const double Wx[3][3] = {{0, -wz, wy}, {wz, 0, -wx}, {-wy, wx, 0}};
+    const double JWx[3][3] = {{0, -jw[2], jw[1]}, {jw[2], 0, -jw[0]}, {-jw[1], jw[0], 0}};
+    double D[3][3];
+    for (int i = 0; i < 3; ++i)
+      for (int j = 0; j < 3; ++j)
+        D[i][j] = JWx[i][j] - ((Wx[i][0] * rk.Jf[j] + Wx[i][1] * rk.Jf[3 + j]) + Wx[i][2] * rk.Jf[6 + j]);
+    for (int i = 0; i < 3; ++i)
+      for (int j = 0; j < 3; ++j) {
+        const double a = (rk.Ji[3 * i] * D[0][j] + rk.Ji[3 * i + 1] * D[1][j]) + rk.Ji[3 * i + 2] * D[2][j];
+        const double bu = (rk.Ji[3 * i] * Rx[0][j] + rk.Ji[3 * i + 1] * Rx[1][j]) + rk.Ji[3 * i + 2] * Rx[2][j];
+        set(11 + i, 11 + j, -((i == j ? 1.0 : 0.0) + a * dt));
+        set(11 + i, 14 + j, -(bu * dt));
+      }
+    return;
+  }
   const double j1 = rk.J[0], j2 = rk.J[1], j3 = rk.J[2];
   const double Aw[3][3] = {{0, wz, wy}, {wz, 0, wx}, {wy, wx, 0}};
   const double cw[3] = {-(j3 - j2) / j1, -(j1 - j3) / j2, -(j2 - j1) / j3};
   for (int i = 0; i < 3; ++i)
     for (int j = 0; j < 3; ++j) set(11 + i, 11 + j, -((i == j ? 1.0 : 0.0) + cw[i] * Aw[i][j] * dt));
   // B_c omega rows: J^-1 [r_T]x
-  const double rx = rk.rT[0], ry = rk.rT[1], rz = rk.rT[2];
-  const double Rx[3][3] = {{0, -rz, ry}, {rz, 0, -rx}, {-ry, rx, 0}};
   for (int i = 0; i < 3; ++i)
     for (int j = 0; j < 3; ++j) set(11 + i, 14 + j, -(Rx[i][j] / rk.J[i] * dt));
 }

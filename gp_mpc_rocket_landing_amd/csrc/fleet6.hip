@@ -37,6 +37,8 @@
 // block of each equality row lives in its owner's registers, a column copy in
 // the variable owner's; only the factor and the cross-thread vectors are LDS.
 #include "fleet6.h"
+#include <algorithm>
+#include <cmath>
 #include <vector>
 
 struct R6Impl;  // the kernels of one horizon (fleet6_n.h), below
@@ -46,6 +48,8 @@ struct gpmpc_rollout6 {
   bool exact = false;  // the GP pair is exact (mean K* alpha over the training rows)
   gpmpc_rollout6_config cfg{};
   const R6Impl *impl = nullptr;
+  double Jd[3] = {}, Jf[9] = {}, Ji[9] = {};  // the rocket's inertia: diagonal, or full + inverse
+  int jfull = 0;
   int B = 0, N = 0, M = 0;  // batch, horizon, QP rows
   DevBuf x, U, Xp, gm, Xo, ysc, rho, rec, lin, pending;
   DevBuf betav, betaw;  // (L_uu^-T alpha)^T of each GP, 3 x M
@@ -58,7 +62,10 @@ extern "C" void gpmpc_rollout6_default_config(gpmpc_rollout6_config *c) {
   c->dt = 0.1;
   c->max_steps = 300;
   gpmpc_qp_default_settings(&c->qp);   // osqp_rti.py:54-60 settings, as the 3-DoF path
-  c->fitc_mean_as_written = 0;         // FITC posterior mean (SURVEY D1 fixed, flag 1 = as written)
+  // the reference's FITC mean as written, K*u alpha (sparse_gp.py:280-283): compat by
+  // default, as the GPMPC surface (D1 kept, the fix behind a flag); 0 = the
+  // FITC posterior mean K*u L_uu^-T alpha (SURVEY D1 fixed)
+  c->fitc_mean_as_written = 1;
   // CostWeights (cost_functions.py:39-98): Q = diag(w_mass, w_pos x3, w_vel x3, 0, w_att x2, 0,
   // w_omega x3), R = w_thrust I, P = terminal_weight Q
   const double q[R6_NX] = {0.0, 10, 10, 10, 1, 1, 1, 0, 5, 5, 0, 0.1, 0.1, 0.1};
@@ -77,6 +84,7 @@ extern "C" void gpmpc_rollout6_default_config(gpmpc_rollout6_config *c) {
   c->rocket_g_i[0] = -1.0; c->rocket_g_i[1] = 0.0; c->rocket_g_i[2] = 0.0;
   c->rocket_alpha = 1.0 / (30.0 * 1.0);  // I_sp 30, g0 1
   c->rocket_g0 = 1.0;
+  for (int i = 0; i < 9; ++i) c->rocket_J[i] = 0.0;  // unset: diag(rocket_j)
 }
 
 // the kernels of every horizon (fleet6_h*.hip instantiate fleet6_n.h per N)
@@ -125,11 +133,38 @@ static int r6_create(gpmpc_ctx *ctx, const GpView &gv, const GpView &gw, bool ex
     gpmpc_set_error("rollout6: t_max and the trust radii must be positive");
     return -2;
   }
-  for (int i = 0; i < 3; ++i)
-    if (!(cfg->rocket_j[i] > 0.0)) {
-      gpmpc_set_error("rollout6: the rocket's J_B diagonal must be positive");
+  // the inertia tensor: rocket_J (ABI 4, row-major) when it is set, else diag(rocket_j).
+  // A diagonal tensor runs as its diagonal (the divisions of the diagonal model); any
+  // other as J and J^-1, which is formed here once (adjugate / determinant)
+  double Jd[3], Jf[9], Ji[9];
+  bool jset = false, joff = false;
+  for (int i = 0; i < 9; ++i) jset = jset || cfg->rocket_J[i] != 0.0;
+  for (int i = 0; i < 9; ++i) joff = joff || (i % 4 != 0 && cfg->rocket_J[i] != 0.0);
+  for (int i = 0; i < 3; ++i) Jd[i] = jset ? cfg->rocket_J[4 * i] : cfg->rocket_j[i];
+  if (!joff) {
+    for (int i = 0; i < 3; ++i)
+      if (!(Jd[i] > 0.0)) {
+        gpmpc_set_error("rollout6: the rocket's J_B diagonal must be positive");
+        return -2;
+      }
+  } else {
+    for (int i = 0; i < 9; ++i) Jf[i] = cfg->rocket_J[i];
+    const double c00 = Jf[4] * Jf[8] - Jf[5] * Jf[7], c01 = Jf[5] * Jf[6] - Jf[3] * Jf[8],
+                 c02 = Jf[3] * Jf[7] - Jf[4] * Jf[6];
+    const double det = Jf[0] * c00 + Jf[1] * c01 + Jf[2] * c02;
+    bool fin = std::isfinite(det);
+    for (int i = 0; i < 9; ++i) fin = fin && std::isfinite(Jf[i]);
+    double scale = 0.0;
+    for (int i = 0; i < 9; ++i) scale = std::max(scale, std::fabs(Jf[i]));
+    if (!fin || !(std::fabs(det) > 1e-14 * scale * scale * scale)) {
+      gpmpc_set_error("rollout6: the rocket's J_B must be finite and invertible");
       return -2;
     }
+    const double adj[9] = {c00, Jf[2] * Jf[7] - Jf[1] * Jf[8], Jf[1] * Jf[5] - Jf[2] * Jf[4],
+                           c01, Jf[0] * Jf[8] - Jf[2] * Jf[6], Jf[2] * Jf[3] - Jf[0] * Jf[5],
+                           c02, Jf[1] * Jf[6] - Jf[0] * Jf[7], Jf[0] * Jf[4] - Jf[1] * Jf[3]};
+    for (int i = 0; i < 9; ++i) Ji[i] = adj[i] / det;
+  }
   if (!(cfg->rocket_alpha >= 0.0) || !(cfg->rocket_g0 > 0.0)) {
     gpmpc_set_error("rollout6: rocket alpha must be >= 0 and g0 > 0");
     return -2;
@@ -137,6 +172,10 @@ static int r6_create(gpmpc_ctx *ctx, const GpView &gv, const GpView &gw, bool ex
   GPMPC_HIP(hipSetDevice(ctx->device));
   auto *r = new gpmpc_rollout6();
   r->ctx = ctx; r->gv = gv; r->gw = gw; r->exact = exact; r->cfg = *cfg; r->B = batch;
+  r->jfull = joff;
+  for (int i = 0; i < 3; ++i) r->Jd[i] = Jd[i];
+  if (joff)
+    for (int i = 0; i < 9; ++i) { r->Jf[i] = Jf[i]; r->Ji[i] = Ji[i]; }
   r->impl = impl; r->N = impl->N; r->M = impl->M;
   const size_t B = batch, N = r->N;
   if (r->x.alloc(sizeof(double) * B * R6_NX) || r->U.alloc(sizeof(double) * B * N * R6_NU) ||
@@ -222,7 +261,9 @@ static R6Args r6_args(gpmpc_rollout6 *r) {
   a.done = r->done.as<int>(); a.passes = r->passes.as<int>();
   a.qit = r->qit.as<int>(); a.qst = r->qst.as<int>();
   const gpmpc_rollout6_config &c = r->cfg;
-  for (int i = 0; i < 3; ++i) { a.rk.J[i] = c.rocket_j[i]; a.rk.rT[i] = c.rocket_r_t[i]; a.rk.gI[i] = c.rocket_g_i[i]; }
+  for (int i = 0; i < 3; ++i) { a.rk.J[i] = r->Jd[i]; a.rk.rT[i] = c.rocket_r_t[i]; a.rk.gI[i] = c.rocket_g_i[i]; }
+  for (int i = 0; i < 9; ++i) { a.rk.Jf[i] = r->Jf[i]; a.rk.Ji[i] = r->Ji[i]; }
+  a.rk.full = r->jfull;
   a.rk.alpha = c.rocket_alpha;
   a.rk.g0 = c.rocket_g0;
   return a;

@@ -333,10 +333,10 @@ class Rocket6DoFDynamics:
 
     def matches_device_model(self) -> bool:
         """True when csrc/fleet6.hip's model can run this rocket: its J, r_T, g_I,
-        alpha and g0 are runtime parameters (gpmpc_rollout6_config, ABI 3), the
-        inertia tensor must be diagonal."""
+        alpha and g0 are runtime parameters (gpmpc_rollout6_config), the inertia
+        tensor any invertible 3 x 3 matrix (rocket_J, ABI 4)."""
         J = np.asarray(self._params.J_B, float)
-        return J.shape == (3, 3) and not np.any(J - np.diag(np.diag(J)))
+        return J.shape == (3, 3) and bool(np.all(np.isfinite(J))) and abs(np.linalg.det(J)) > 0.0
 
     def __repr__(self) -> str:
         return (f"Rocket6DoFDynamics(m_wet={self.config.m_wet}, m_dry={self.config.m_dry}, "

@@ -240,7 +240,7 @@ class GPMPC6DoF(GPMPC):
     reference's N = 20 (gp_mpc.py:110, nominal_mpc.py:47); the device
     controller is compiled for every N from 2 to 30 (BASELINE configs[4]: 30).  The
     rocket is ``dynamics.params`` (J_B, r_T_B, g_I, I_sp, g0 of
-    Rocket6DoFConfig); the device model takes a diagonal J_B.
+    Rocket6DoFConfig); J_B may be any invertible tensor (ABI 4 rocket_J).
     """
     n_x, n_u = 14, 3
 

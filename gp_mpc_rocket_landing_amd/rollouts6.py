@@ -32,14 +32,19 @@ def qp_rows(N: int) -> int:
 
 def rocket_config(params) -> dict:
     """Rollout6Config rocket fields from a Rocket6DoFParams-like object
-    (rocket_6dof.py:36-84: J_B, r_T_B, g_I, I_sp, g0).  The device model takes a
-    diagonal J_B and raises otherwise."""
+    (rocket_6dof.py:36-84: J_B, r_T_B, g_I, I_sp, g0).  J_B is any invertible 3 x 3
+    tensor (rocket_6dof.py:44, 77-78, 147): a diagonal one goes as its diagonal
+    (rocket_j), any other as the full tensor (rocket_J, ABI 4), which the device
+    inverts once and applies as nominal_mpc.py:196-199's ca.solve(J, .)."""
     J = np.asarray(params.J_B, float)
-    if J.shape != (3, 3) or np.any(J - np.diag(np.diag(J))):
-        raise NotImplementedError("the 6-DoF device model takes a diagonal inertia tensor J_B")
-    return dict(rocket_j=np.diag(J).copy(), rocket_r_t=np.asarray(params.r_T_B, float).reshape(3),
-                rocket_g_i=np.asarray(params.g_I, float).reshape(3),
-                rocket_alpha=1.0 / (float(params.I_sp) * float(params.g0)), rocket_g0=float(params.g0))
+    if J.shape != (3, 3):
+        raise ValueError(f"J_B must be 3 x 3, got {J.shape}")
+    kw = dict(rocket_j=np.diag(J).copy(), rocket_r_t=np.asarray(params.r_T_B, float).reshape(3),
+              rocket_g_i=np.asarray(params.g_I, float).reshape(3),
+              rocket_alpha=1.0 / (float(params.I_sp) * float(params.g0)), rocket_g0=float(params.g0))
+    if np.any(J - np.diag(np.diag(J))):
+        kw["rocket_J"] = J.reshape(9).copy()
+    return kw
 
 
 def fit_structured_gp(n_train=4000, n_inducing=2000, seed=0, use_sparse=True):

@@ -32,9 +32,10 @@ extern "C" {
  * gpmpc_rollout6_solve_ref (X_ref / U_ref), gpmpc_comm_count (round 4); round 4 also
  * gave gpmpc_fleet_config.sqp_qp the max_iter = 0 "same as qp" meaning.  Round 5 adds
  * entry points only (gpmpc_fleet_get_posterior, gpmpc_gather_prepare / _collective) and
- * refuses a fleet config whose sqp_qp was edited with max_iter left 0.  Round 6 adds
- * entry points only (gpmpc_fleet_create_shard). */
-#define GPMPC_ABI_VERSION 3
+ * refuses a fleet config whose sqp_qp was edited with max_iter left 0.
+ * 4 (round 6): gpmpc_rollout6_config gained rocket_J (the full inertia tensor); new
+ * entry point gpmpc_fleet_create_shard. */
+#define GPMPC_ABI_VERSION 4
 
 typedef struct gpmpc_ctx gpmpc_ctx;
 typedef struct gpmpc_gp gpmpc_gp;
@@ -345,8 +346,9 @@ typedef struct {
   double dt;
   int max_steps;
   gpmpc_qp_settings qp;  /* osqp_rti.py:54-60 defaults */
-  int fitc_mean_as_written;  /* 0: the FITC posterior mean K*u L_uu^-T alpha; 1: the
-                                reference's K*u alpha (sparse_gp.py:280-283) */
+  int fitc_mean_as_written;  /* 1 (default since round 6): the reference's K*u alpha
+                                (sparse_gp.py:280-283, SURVEY D1 kept); 0: the FITC
+                                posterior mean K*u L_uu^-T alpha (D1 fixed) */
   /* GPMPC's problem data (ABI 2).  Defaults: CostWeights (cost_functions.py:39-98),
    * ConstraintParams (constraints.py:35-50), gp_mpc.py:432-435. */
   double q_diag[14];     /* stage cost Q (diagonal) */
@@ -359,14 +361,18 @@ typedef struct {
   int upright_target;    /* rollouts: 0 = monte_carlo.py:497-500 as written (x copied, v = 0,
                             altitude - 2); 1 = also q = (1, 0, 0, 0), omega = 0 */
   /* the rocket (ABI 3): Rocket6DoFConfig (rocket_6dof.py:36-84) as the dynamics of
-   * nominal_mpc.py:163-203 use it.  Defaults J_B = diag(0.02, 1, 1) 0.168 (the device
-   * model takes a diagonal J_B), r_T_B = (-0.25, 0, 0), g_I = (-1, 0, 0), I_sp 30, g0 1:
+   * nominal_mpc.py:163-203 use it.  Defaults J_B = diag(0.02, 1, 1) 0.168 (a full
+   * tensor: rocket_J below), r_T_B = (-0.25, 0, 0), g_I = (-1, 0, 0), I_sp 30, g0 1:
    * alpha = 1 / (I_sp g0); g0 also sets the hover guess [0, 0, m g0] (gp_mpc.py:271-275) */
   double rocket_j[3];    /* diagonal of J_B */
   double rocket_r_t[3];  /* thrust application point r_T_B */
   double rocket_g_i[3];  /* gravity g_I */
   double rocket_alpha;   /* 1 / (I_sp g0) */
   double rocket_g0;
+  /* ABI 4: the full inertia tensor J_B (row-major 3 x 3, rocket_6dof.py:44, 77-78, 147:
+   * any invertible matrix; nominal_mpc.py:196-199 solves with it).  All zeros (the
+   * default) = diag(rocket_j).  A diagonal tensor runs exactly as its diagonal would. */
+  double rocket_J[9];
 } gpmpc_rollout6_config;
 void gpmpc_rollout6_default_config(gpmpc_rollout6_config *c);
 /* gp_v: FITC on the 13 translational features, gp_w: on the 12 rotational

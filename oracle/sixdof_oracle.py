@@ -44,14 +44,24 @@ R_T = np.array([-0.25, 0.0, 0.0])
 G_I = np.array([-1.0, 0.0, 0.0])
 G0 = 1.0
 # Rocket6DoFConfig defaults as one parameter set; every dynamics function takes an
-# optional ``rk`` of this shape (rocket_6dof.py:36-84; diagonal J_B)
+# optional ``rk`` of this shape (rocket_6dof.py:36-84)
 DEFAULT_ROCKET = dict(J=J_DIAG, r_T=R_T, g_I=G_I, alpha=ALPHA, g0=G0)
 
 
 def rocket_params(J=None, r_T=None, g_I=None, I_sp=30.0, g0=1.0):
-    """A parameter set for a Rocket6DoFConfig (diagonal J_B given as its diagonal)."""
-    return dict(J=np.asarray(J_DIAG if J is None else J, float), r_T=np.asarray(R_T if r_T is None else r_T, float),
-                g_I=np.asarray(G_I if g_I is None else g_I, float), alpha=1.0 / (I_sp * g0), g0=float(g0))
+    """A parameter set for a Rocket6DoFConfig.  J: the diagonal of a diagonal J_B, or
+    the 3 x 3 tensor (rocket_6dof.py:44, 77-78: any matrix).  A full tensor adds
+    ``Jf`` and its inverse ``Ji``: w' = Ji (r_T x u - w x Jf w), nominal_mpc.py:196-199's
+    ca.solve(J, .) as the host mirror (dynamics/rocket_6dof.py) states it; a diagonal
+    3 x 3 tensor is its diagonal."""
+    J = np.asarray(J_DIAG if J is None else J, float)
+    rk = dict(r_T=np.asarray(R_T if r_T is None else r_T, float),
+              g_I=np.asarray(G_I if g_I is None else g_I, float), alpha=1.0 / (I_sp * g0), g0=float(g0))
+    if J.ndim == 2 and np.any(J - np.diag(np.diag(J))):
+        rk.update(J=np.diag(J).copy(), Jf=J.copy(), Ji=np.linalg.inv(J))
+    else:
+        rk["J"] = np.diag(J).copy() if J.ndim == 2 else J
+    return rk
 T_MIN, T_MAX = 0.5, 5.0                 # ConstraintParams (constraints.py:35-50)
 TAN_GS = np.tan(np.deg2rad(30.0))       # gamma_gs 30 deg
 TRUST_X, TRUST_U = np.sqrt(10.0), np.sqrt(5.0)   # gp_mpc.py:432-435
@@ -81,6 +91,9 @@ def f(x, u, rk=None):
     out[7] = 0.5 * -(w @ qv)
     out[8:11] = 0.5 * (q[0] * w + np.cross(w, qv))
     torque = np.cross(rk["r_T"], u)
+    if "Jf" in rk:   # a full inertia tensor
+        out[11:14] = rk["Ji"] @ (torque - np.cross(w, rk["Jf"] @ w))
+        return out
     jw = rk["J"] * w
     out[11:14] = (torque - np.cross(w, jw)) / rk["J"]
     return out
@@ -122,12 +135,19 @@ def jacobians(x, u, rk=None):
     A[7:11, 7:11] = 0.5 * np.array([[0, -wx, -wy, -wz], [wx, 0, -wz, wy], [wy, wz, 0, -wx], [wz, -wy, wx, 0]])
     A[7, 11:14] = -0.5 * q[1:4]
     A[8:11, 11:14] = 0.5 * np.array([[qw, qz, -qy], [-qz, qw, qx], [qy, -qx, qw]])
+    rx, ry, rz = rk["r_T"]
+    Rx = np.array([[0, -rz, ry], [rz, 0, -rx], [-ry, rx, 0]])
+    if "Jf" in rk:   # d/dw Ji (-w x Jf w) = Ji ([Jf w]x - [w]x Jf); B: Ji [r_T]x
+        def skew(a):
+            return np.array([[0.0, -a[2], a[1]], [a[2], 0.0, -a[0]], [-a[1], a[0], 0.0]])
+        A[11:14, 11:14] = rk["Ji"] @ (skew(rk["Jf"] @ w) - skew(w) @ rk["Jf"])
+        B[11:14] = rk["Ji"] @ Rx
+        return A, B
     j1, j2, j3 = rk["J"]
     A[11, 11:14] = -(j3 - j2) / j1 * np.array([0, wz, wy])
     A[12, 11:14] = -(j1 - j3) / j2 * np.array([wz, 0, wx])
     A[13, 11:14] = -(j2 - j1) / j3 * np.array([wy, wx, 0])
-    rx, ry, rz = rk["r_T"]
-    B[11:14] = np.array([[0, -rz, ry], [rz, 0, -rx], [-ry, rx, 0]]) / rk["J"][:, None]
+    B[11:14] = Rx / rk["J"][:, None]
     return A, B
 
 

@@ -22,7 +22,7 @@ def test_library_exports_every_declared_symbol():
 
 def test_abi_version_and_error_string():
     from gp_mpc_rocket_landing_amd import _lib
-    assert _lib.abi_version() == 3
+    assert _lib.abi_version() == 4 == _lib.ABI_VERSION
     assert isinstance(_lib._L.gpmpc_last_error(), bytes)
 
 
