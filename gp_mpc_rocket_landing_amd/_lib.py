@@ -134,6 +134,7 @@ _sig("gpmpc_qp_solve_batched", _c, _vp, _c, _c, _c, _c, _ip, _ip, _dp, _dp, _dp,
 _sig("gpmpc_fleet_default_config", None, ctypes.POINTER(FleetConfig))
 _sig("gpmpc_fleet_create", _c, _vp, _vp, ctypes.POINTER(FleetConfig), _c, ctypes.POINTER(_vp))
 _sig("gpmpc_fleet_create_shard", _c, _vp, _vp, ctypes.POINTER(FleetConfig), _c, _c, ctypes.POINTER(_vp))
+_sig("gpmpc_fleet_create_fitc", _c, _vp, _vp, ctypes.POINTER(FleetConfig), _c, _c, ctypes.POINTER(_vp))
 _sig("gpmpc_fleet_reset", _c, _vp, _c, _c, _dp)
 _sig("gpmpc_fleet_step", _c, _vp, _c)
 _sig("gpmpc_fleet_step_phases", _c, _vp, _c)
@@ -178,7 +179,7 @@ EXPORTED = ["gpmpc_abi_version", "gpmpc_last_error", "gpmpc_ctx_create", "gpmpc_
             "gpmpc_gp_lml_batched", "gpmpc_gp_append",
             "gpmpc_fitc_fit", "gpmpc_fitc_predict", "gpmpc_fitc_destroy",
             "gpmpc_qp_default_settings", "gpmpc_qp_solve_batched", "gpmpc_fleet_default_config",
-            "gpmpc_fleet_create", "gpmpc_fleet_create_shard", "gpmpc_fleet_reset", "gpmpc_fleet_step", "gpmpc_fleet_read",
+            "gpmpc_fleet_create", "gpmpc_fleet_create_shard", "gpmpc_fleet_create_fitc", "gpmpc_fleet_reset", "gpmpc_fleet_step", "gpmpc_fleet_read",
             "gpmpc_fleet_step_phases", "gpmpc_fleet_get_state", "gpmpc_fleet_get_posterior", "gpmpc_fleet_set_stamps", "gpmpc_fleet_set_trace",
             "gpmpc_syrk_batched_dev", "gpmpc_cov_propagate", "gpmpc_cov_propagate_dev",
             "gpmpc_fleet_records_dev", "gpmpc_fleet_destroy", "gpmpc_rollout6_default_config",

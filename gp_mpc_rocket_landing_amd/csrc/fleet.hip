@@ -69,7 +69,16 @@ struct gpmpc_fleet {
   int plan_B = 0;
   int post_kind = 0;                         // posterior GEMM kernel (gemm_sumsq_kind at plan_B N)
   bool post_few = false;                     // queries + K* in one launch (<= 64 planned query rows)
+  // a sparse GP (FITC or VFE, gpmpc_fleet_create_fitc) instead of the exact one: the
+  // posterior is K*u against the inducing rows, mean K*u alpha as the reference writes it
+  // (sparse_gp.py:280-283), variance sigma2 - |L_uu^-1 k*|^2 + |W2 k*|^2
+  gpmpc_fitc *fitc = nullptr;
+  DevBuf part2;                              // |W2 k*|^2 partials
+  int post_kind2 = 0, post_nrt2 = 0;
 };
+
+// the GP the fleet reads: its exact GP, or the sparse one's inducing-point view
+static GpView fleet_view(const gpmpc_fleet *f) { return f->fitc ? fitc_view(f->fitc) : gp_view(f->gp); }
 
 extern "C" int gpmpc_fleet_set_stamps(gpmpc_fleet *f, void *dev_u64x16) {
   GPMPC_CHECK_ARG(f);
@@ -267,6 +276,8 @@ struct FleetArgs {
   double sigma2;
   int nrt;
   int64_t pld;          // leading dimension of part / meanT (P)
+  const double *part2;  // a sparse GP's second partials |W2 k*|^2 (or null: exact GP)
+  int nrt2;
   unsigned *claims;     // per-CU claimed chain SIMDs, (epoch << 8) | 4-bit mask (or null)
   unsigned epoch;       // this launch's claim generation (never 0)
   int *lastit;          // ADMM iterations of each landing's last solve
@@ -277,6 +288,23 @@ struct FleetArgs {
   double sqp_tol;
   int *sqp_done;               // landing converged in an earlier pass of this control step
 };
+
+// The latent variance of query row q from the SUMSQ partials (k_post_finish / k_fitc_finish
+// arithmetic): exact GP sigma2 - |L^-1 k*|^2 (exact_gp.py:256-266); a sparse GP (FITC / VFE,
+// one predict body, sparse_gp.py:285-301) sigma2 - |L_uu^-1 k*|^2 + |L_B^-1 L_uu^-1 k*|^2
+__device__ __forceinline__ double fleet_latent_var(const FleetArgs &a, int64_t q) {
+  double ss = 0.0;
+  for (int t = 0; t < a.nrt; ++t) ss += a.part[(int64_t)t * a.pld + q];
+  double lat;
+  if (a.part2) {
+    double sw = 0.0;
+    for (int t = 0; t < a.nrt2; ++t) sw += a.part2[(int64_t)t * a.pld + q];
+    lat = a.sigma2 - ss + sw;
+  } else {
+    lat = a.sigma2 - ss;
+  }
+  return lat > 1e-10 ? lat : 1e-10;
+}
 
 // the 256-thread build of k_fleet_control2 (fleet_wide.hip)
 hipError_t launch_fleet_control_wide(hipStream_t s, int nb, const FleetArgs &a, bool stamps);
@@ -523,10 +551,7 @@ __global__ __launch_bounds__(FQ_T) __attribute__((amdgpu_waves_per_eu(FQ_WPE, FQ
     if (!(a.part && a.use_gp)) return;
     for (int k = tid; k < N; k += FQ_T) {
       const int64_t q = (int64_t)(a.gp_by_slot ? (int)blockIdx.x : b) * N + k;
-      double ss = 0.0;
-      for (int t = 0; t < a.nrt; ++t) ss += a.part[(int64_t)t * a.pld + q];
-      double lat = a.sigma2 - ss;
-      lat = lat > 1e-10 ? lat : 1e-10;
+      const double lat = fleet_latent_var(a, q);
       for (int c = 0; c < 3; ++c) {
         a.mean_out[q * 3 + c] = a.meanT[(int64_t)c * a.pld + q] * a.ystd[c] + a.ymean[c];
         a.var_out[q * 3 + c] = lat * a.ystd[c] * a.ystd[c];
@@ -689,11 +714,8 @@ __global__ __launch_bounds__(FQ_T) __attribute__((amdgpu_waves_per_eu(FQ_WPE, FQ
     const int64_t q = (int64_t)(a.gp_by_slot ? (int)blockIdx.x : b) * N + k;  // query row
     double gm[3];
     if (a.part && a.use_gp) {
-      // the posterior finish of this landing's query (k_post_finish, same arithmetic)
-      double ss = 0.0;
-      for (int t = 0; t < a.nrt; ++t) ss += a.part[(int64_t)t * a.pld + q];
-      double lat = a.sigma2 - ss;
-      lat = lat > 1e-10 ? lat : 1e-10;
+      // the posterior finish of this landing's query (k_post_finish / k_fitc_finish arithmetic)
+      const double lat = fleet_latent_var(a, q);
       for (int c = 0; c < 3; ++c) {
         gm[c] = a.meanT[(int64_t)c * a.pld + q] * a.ystd[c] + a.ymean[c];
         a.mean_out[q * 3 + c] = gm[c];
@@ -891,10 +913,10 @@ __global__ void k_fleet_reset(int first, int count, int N, int target_mode,
 }
 
 // ---------------------------------------------------------------------------
-extern "C" int gpmpc_fleet_create_shard(gpmpc_ctx *ctx, gpmpc_gp *gp, const gpmpc_fleet_config *cfg,
-                                        int batch, int fleet_batch, gpmpc_fleet **out) {
-  GPMPC_CHECK_ARG(ctx && gp && cfg && out && batch > 0 && fleet_batch >= batch);
-  const GpView g = gp_view(gp);
+static int fleet_create(gpmpc_ctx *ctx, gpmpc_gp *gp, gpmpc_fitc *fitc, const gpmpc_fleet_config *cfg,
+                        int batch, int fleet_batch, gpmpc_fleet **out) {
+  GPMPC_CHECK_ARG(ctx && (gp || fitc) && cfg && out && batch > 0 && fleet_batch >= batch);
+  const GpView g = fitc ? fitc_view(fitc) : gp_view(gp);
   GPMPC_CHECK_ARG(g.d == NFEAT && g.n_out == 3);
   if (g.kind < GPMPC_SE_ARD || g.kind > GPMPC_MATERN52) {
     gpmpc_set_error("fleet: the GP must use one of the four stationary kernels (not a composite program)");
@@ -934,7 +956,7 @@ extern "C" int gpmpc_fleet_create_shard(gpmpc_ctx *ctx, gpmpc_gp *gp, const gpmp
   GPMPC_CHECK_ARG(N >= 1 && n <= QP_NMAX && m <= QP_MMAX && NX + N * DYN_NNZ + n <= QP_NNZMAX);
   GPMPC_HIP(hipSetDevice(ctx->device));
   auto *f = new gpmpc_fleet();
-  f->ctx = ctx; f->gp = gp; f->cfg = *cfg; f->B = batch; f->N = N; f->n = n; f->m = m;
+  f->ctx = ctx; f->gp = gp; f->fitc = fitc; f->cfg = *cfg; f->B = batch; f->N = N; f->n = n; f->m = m;
   f->gp_n = g.n;
   f->n_active = batch;
   std::vector<int> rp, ci;
@@ -951,6 +973,15 @@ extern "C" int gpmpc_fleet_create_shard(gpmpc_ctx *ctx, gpmpc_gp *gp, const gpmp
   // partial rows of any posterior path: W rows + the 3 alpha^T rows in 64-row tiles (the
   // most rows any kernel writes), at least the column-stationary posterior's two halves
   const int nrt = std::max(gemm_sumsq_rows(GEMM_SUMSQ_64, g.n + 3), POST_CS_PARTS);
+  if (fitc) {
+    f->post_kind2 = gemm_sumsq_kind(g.n, (int)std::min<int64_t>((int64_t)fleet_batch * N, 1 << 30), g.n);
+    f->post_nrt2 = gemm_sumsq_rows(f->post_kind2, g.n);
+    if (f->part2.alloc(sizeof(double) * gemm_sumsq_rows(GEMM_SUMSQ_64, g.n) * P)) {
+      delete f;
+      gpmpc_set_error("fleet: out of device memory");
+      return -1;
+    }
+  }
   if (f->x.alloc(sizeof(double) * B * NX) || f->Xw.alloc(sizeof(double) * B * (N + 1) * NX) ||
       f->Uw.alloc(sizeof(double) * B * N * NU) || f->ysc.alloc(sizeof(double) * B * m) ||
       f->rho.alloc(sizeof(double) * B) || f->rec.alloc(sizeof(double) * B * GPMPC_REC_LEN) ||
@@ -1008,9 +1039,21 @@ extern "C" int gpmpc_fleet_create_shard(gpmpc_ctx *ctx, gpmpc_gp *gp, const gpmp
   return 0;
 }
 
+extern "C" int gpmpc_fleet_create_shard(gpmpc_ctx *ctx, gpmpc_gp *gp, const gpmpc_fleet_config *cfg,
+                                        int batch, int fleet_batch, gpmpc_fleet **out) {
+  GPMPC_CHECK_ARG(gp);
+  return fleet_create(ctx, gp, nullptr, cfg, batch, fleet_batch, out);
+}
+
 extern "C" int gpmpc_fleet_create(gpmpc_ctx *ctx, gpmpc_gp *gp, const gpmpc_fleet_config *cfg, int batch,
                                   gpmpc_fleet **out) {
   return gpmpc_fleet_create_shard(ctx, gp, cfg, batch, batch, out);
+}
+
+extern "C" int gpmpc_fleet_create_fitc(gpmpc_ctx *ctx, gpmpc_fitc *gp, const gpmpc_fleet_config *cfg, int batch,
+                                       int fleet_batch, gpmpc_fleet **out) {
+  GPMPC_CHECK_ARG(gp);
+  return fleet_create(ctx, nullptr, gp, cfg, batch, fleet_batch, out);
 }
 
 extern "C" int gpmpc_fleet_reset(gpmpc_fleet *f, int first, int count, const double *x0) {
@@ -1035,7 +1078,7 @@ extern "C" int gpmpc_fleet_reset(gpmpc_fleet *f, int first, int count, const dou
 //   variance partial sums (SUMSQ epilogue) and the means;  bit 3: finish
 static hipError_t fleet_gp_posterior(gpmpc_fleet *f, int mask) {
   hipStream_t s = f->ctx->stream;
-  const GpView g = gp_view(f->gp);
+  const GpView g = fleet_view(f);
   const int nb = f->use_order ? f->n_active : f->B;  // slots 0 .. nb-1 (running first)
   const int P = nb * f->N;
   if (P == 0) return hipSuccess;
@@ -1050,8 +1093,8 @@ static hipError_t fleet_gp_posterior(gpmpc_fleet *f, int mask) {
   }();
   // GPMPC_POST_CS=1: the column-stationary posterior (post.hip), K* formed once per
   // workgroup inside the MFMA pass, never in HBM; two partial rows
-  const bool cs = g.Wf && post_cs_env();
-  const bool fused = !cs && fused_env && g.d >= 11 && g.d <= 13;
+  const bool cs = !f->fitc && g.Wf && post_cs_env();
+  const bool fused = !f->fitc && !cs && fused_env && g.d >= 11 && g.d <= 13;
   const int nrt = cs ? POST_CS_PARTS : fused ? (g.n + 3 + 127) / 128 : gemm_sumsq_rows(f->post_kind, g.n + 3);
   hipError_t e = hipSuccess;
   if ((mask & 1) && !fused && !cs && f->post_few) {
@@ -1082,6 +1125,11 @@ static hipError_t fleet_gp_posterior(gpmpc_fleet *f, int mask) {
       e = launch_gemm_sumsq_mean(s, g.n, 3, P, g.W, f->Ks.as<double>(), f->part.as<double>(), P,
                                  f->meanT.as<double>(), P, f->post_kind);
     if (e != hipSuccess) return e;
+    if (f->fitc) {  // |w|^2 = |L_B^-1 L_uu^-1 k*|^2 (sparse_gp.py:293-299)
+      e = launch_gemm_sumsq(s, g.n, P, fitc_W2(f->fitc), f->Ks.as<double>(), f->part2.as<double>(), P,
+                            f->post_kind2);
+      if (e != hipSuccess) return e;
+    }
   }
   if (mask & 4) {
     f->post_P = P;
@@ -1089,8 +1137,13 @@ static hipError_t fleet_gp_posterior(gpmpc_fleet *f, int mask) {
   }
   // fused: k_fleet_control2 finishes each landing's own queries as it assembles
   if ((mask & 8) && !(f->use_fq && f->fuse_post)) {
-    e = launch_post_finish(s, P, 3, nrt, f->part.as<double>(), P, f->meanT.as<double>(), P,
-                           g.ymean, g.ystd, g.sigma2, f->mean.as<double>(), f->var.as<double>());
+    if (f->fitc)
+      e = launch_fitc_finish(s, P, 3, nrt, f->post_nrt2, f->part.as<double>(), f->part2.as<double>(), P,
+                             f->meanT.as<double>(), P, g.ymean, g.ystd, g.sigma2, f->mean.as<double>(),
+                             f->var.as<double>());
+    else
+      e = launch_post_finish(s, P, 3, nrt, f->part.as<double>(), P, f->meanT.as<double>(), P,
+                             g.ymean, g.ystd, g.sigma2, f->mean.as<double>(), f->var.as<double>());
   }
   return e;
 }
@@ -1185,8 +1238,14 @@ static FleetArgs fleet_args(gpmpc_fleet *f) {
   a.alt_wave = f->alt_wave;
   a.claims = f->simd_pick ? f->claims.as<unsigned>() : nullptr;
   a.part = nullptr;
+  a.part2 = nullptr;
+  a.nrt2 = 0;
   if (f->use_fq && f->fuse_post && f->cfg.use_gp && f->post_P > 0) {
-    const GpView g = gp_view(f->gp);
+    const GpView g = fleet_view(f);
+    if (f->fitc) {
+      a.part2 = f->part2.as<double>();
+      a.nrt2 = f->post_nrt2;
+    }
     a.part = f->part.as<double>();
     a.meanT = f->meanT.as<double>();
     a.ymean = g.ymean;
@@ -1213,9 +1272,9 @@ static FleetArgs fleet_args(gpmpc_fleet *f) {
 
 extern "C" int gpmpc_fleet_step_phases(gpmpc_fleet *f, int phase_mask) {
   GPMPC_CHECK_ARG(f);
-  if (gp_view(f->gp).n != f->gp_n) {  // gpmpc_gp_append grew the GP under the fleet
+  if (fleet_view(f).n != f->gp_n) {  // gpmpc_gp_append grew the GP under the fleet
     gpmpc_set_error("fleet: the GP has %d training rows, the fleet was built for %d; recreate it",
-                    gp_view(f->gp).n, f->gp_n);
+                    fleet_view(f).n, f->gp_n);
     return -2;
   }
   GPMPC_HIP(hipSetDevice(f->ctx->device));

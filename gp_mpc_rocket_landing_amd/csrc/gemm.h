@@ -73,6 +73,9 @@ inline int gemm_sumsq_rows(int kind, int M) { return kind == GEMM_SUMSQ_128 ? (M
 hipError_t launch_gemm_sumsq_mean(hipStream_t s, int n, int n_out, int P, const double *Wext,
                                   const double *Ks, double *part, int64_t ldp, double *meanT,
                                   int64_t ldm, int kind = -1);
+// part[t][j] = sum over the rows of tile t of (A K*^T)^2, A (n x n lower, ld n), K* (P x n)
+hipError_t launch_gemm_sumsq(hipStream_t s, int n, int P, const double *A, const double *Ks, double *part,
+                             int64_t ldp, int kind = -1);
 
 // the same pass with K* formed in the operand load from the scaled query rows
 // Qs (P x d) / norms Qn and training rows Xs (n x d) / norms Xn (d = 11..13;

@@ -1236,6 +1236,12 @@ hipError_t launch_gemm_nt(hipStream_t s, int epi, int M, int N, int K, const dou
                           batch, sA, sB, sC, M, nullptr, 0);
 }
 
+hipError_t launch_gemm_sumsq(hipStream_t s, int n, int P, const double *A, const double *Ks, double *part,
+                             int64_t ldp, int kind) {
+  return launch_gemm_impl(s, EPI_SUMSQ, n, P, n, A, n, Ks, n, part, ldp, 1.0, 0.0, 1, 0, 1, 0, 0, 0, n, nullptr,
+                          0, kind);
+}
+
 hipError_t launch_gemm_sumsq_mean(hipStream_t s, int n, int n_out, int P, const double *Wext,
                                   const double *Ks, double *part, int64_t ldp, double *meanT,
                                   int64_t ldm, int kind) {

@@ -823,6 +823,17 @@ GpView gp_view(const gpmpc_gp *gp) {
                 g.ymean.as<double>(), g.ystd.as<double>(), g.Wf.as<double>(), g.Xp.as<double>()};
 }
 
+const double *fitc_W2(const gpmpc_fitc *gp) { return gp->W2.as<double>(); }
+
+hipError_t launch_fitc_finish(hipStream_t s, int P, int n_out, int nrv, int nrw, const double *pv,
+                              const double *pw, int64_t ldp, const double *meanT, int64_t ldm,
+                              const double *ymean, const double *ystd, double sigma2, double *mean,
+                              double *var) {
+  hipLaunchKernelGGL(k_fitc_finish, dim3((P + 255) / 256), dim3(256), 0, s, P, n_out, nrv, nrw, pv, pw, ldp,
+                     meanT, ldm, ymean, ystd, sigma2, mean, var);
+  return hipGetLastError();
+}
+
 GpView fitc_view(const gpmpc_fitc *gp) {
   const GpCore &g = gp->core;
   return GpView{g.kind, g.n, g.d, g.n_out, g.sigma2, g.iso_scale, g.ls.as<double>(),

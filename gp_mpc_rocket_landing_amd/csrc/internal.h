@@ -155,6 +155,13 @@ struct GpView {
 GpView gp_view(const gpmpc_gp *gp);
 // the same view of a FITC GP: n = inducing points, Xs / Xn their scaled rows, alphaT
 GpView fitc_view(const gpmpc_fitc *gp);
+// its W2 = L_B^-1 L_uu^-1 (n x n lower): the predict's w = W2 k* (sparse_gp.py:293-296)
+const double *fitc_W2(const gpmpc_fitc *gp);
+// the sparse posterior finish (k_fitc_finish): var = sigma2 - sum pv + sum pw, mean
+hipError_t launch_fitc_finish(hipStream_t s, int P, int n_out, int nrv, int nrw, const double *pv,
+                              const double *pw, int64_t ldp, const double *meanT, int64_t ldm,
+                              const double *ymean, const double *ystd, double sigma2, double *mean,
+                              double *var);
 // posterior finish: var/mean (P x n_out) from SUMSQ partials and K* alpha (gp.hip)
 hipError_t launch_post_finish(hipStream_t s, int P, int n_out, int nrt, const double *part,
                               int64_t ldp, const double *meanT, int64_t ldm, const double *ymean,

@@ -31,11 +31,32 @@ def fit_gp(ctx, n_train=1000, seed=0, noise=1e-4):
     return _lib.ExactGPHandle(ctx, _lib.SE_ARD, Z, D, np.ones(Z.shape[1]), 1.0, noise)
 
 
+def fit_gp_sparse(n_train=1000, n_inducing=50, seed=0):
+    """The reference-default ``Simple3DoFGP()`` (structured_gp.py:423-428: a
+    MultiOutputSparseGP, FITC, 50 inducing points shared by the 3 outputs, kmeans2 on
+    the global RNG, sparse_gp.py:122-148, seeded here by ``np.random.seed(seed)``)
+    fitted through the surface on generator G data.  Returns its device FITCHandle
+    (``.surface`` keeps the surface alive)."""
+    from .gp.structured_gp import Simple3DoFGP
+    X, U, D = synthetic_training_data(n_train, seed=seed)
+    gp = Simple3DoFGP(n_inducing=n_inducing)
+    gp.add_data(X, U, D)
+    np.random.seed(seed)
+    gp.fit()
+    h = gp.gp.device_handle
+    if h is None:
+        raise RuntimeError("the Simple3DoFGP's outputs must share one device GP")
+    h.surface = gp
+    return h
+
+
 class Fleet:
-    """``fleet_batch``: the size of the whole Monte-Carlo fleet when this one is a
-    shard of it (gpmpc_fleet_create_shard): every size-dependent kernel choice is made
-    for that size, so the shard's landings come out bit-identical to the same landings
-    in the whole fleet.  Default: the fleet is whole."""
+    """``gp``: an exact GP (ExactGPHandle) or a sparse one (FITCHandle: FITC or VFE,
+    gpmpc_fleet_create_fitc -- the reference-default ``Simple3DoFGP()`` is FITC with
+    50 inducing points).  ``fleet_batch``: the size of the whole Monte-Carlo fleet when
+    this one is a shard of it (gpmpc_fleet_create_shard): every size-dependent kernel
+    choice is made for that size, so the shard's landings come out bit-identical to
+    the same landings in the whole fleet.  Default: the fleet is whole."""
 
     def __init__(self, ctx, gp, batch, fleet_batch=None, **config):
         self.ctx = ctx
@@ -44,8 +65,10 @@ class Fleet:
         self.batch = int(batch)
         self.fleet_batch = int(fleet_batch) if fleet_batch is not None else self.batch
         h = ctypes.c_void_p()
-        _lib._chk(_lib._L.gpmpc_fleet_create_shard(ctx.h, gp.h, ctypes.byref(self.cfg), self.batch,
-                                                   self.fleet_batch, ctypes.byref(h)), "fleet_create")
+        create = (_lib._L.gpmpc_fleet_create_fitc if isinstance(gp, _lib.FITCHandle)
+                  else _lib._L.gpmpc_fleet_create_shard)
+        _lib._chk(create(ctx.h, gp.h, ctypes.byref(self.cfg), self.batch, self.fleet_batch, ctypes.byref(h)),
+                  "fleet_create")
         self.h = h
 
     def reset(self, x0, first=0):

@@ -34,7 +34,7 @@ extern "C" {
  * entry points only (gpmpc_fleet_get_posterior, gpmpc_gather_prepare / _collective) and
  * refuses a fleet config whose sqp_qp was edited with max_iter left 0.
  * 4 (round 6): gpmpc_rollout6_config gained rocket_J (the full inertia tensor); new
- * entry point gpmpc_fleet_create_shard. */
+ * entry points gpmpc_fleet_create_shard, gpmpc_fleet_create_fitc. */
 #define GPMPC_ABI_VERSION 4
 
 typedef struct gpmpc_ctx gpmpc_ctx;
@@ -275,6 +275,15 @@ int gpmpc_fleet_create(gpmpc_ctx *ctx, gpmpc_gp *gp, const gpmpc_fleet_config *c
  * landings still fly beside it. */
 int gpmpc_fleet_create_shard(gpmpc_ctx *ctx, gpmpc_gp *gp, const gpmpc_fleet_config *cfg, int batch,
                              int fleet_batch, gpmpc_fleet **out);
+/* The same fleet over a sparse GP (gpmpc_fitc_fit / gpmpc_vfe_fit, 11 features, 3
+ * outputs): the reference-default Simple3DoFGP() is MultiOutputSparseGP FITC with 50
+ * inducing points (structured_gp.py:423-428, sparse_gp.py:400-456).  Every step's
+ * posterior is the reference's SparseGP.predict (sparse_gp.py:255-305) at every horizon
+ * point: the mean K*u alpha as written (what GPMPC consumes through
+ * gp.predict), the variance sigma2 - |L_uu^-1 k*|^2 + |L_B^-1 L_uu^-1 k*|^2.  The
+ * sparse GP must outlive the fleet. */
+int gpmpc_fleet_create_fitc(gpmpc_ctx *ctx, gpmpc_fitc *gp, const gpmpc_fleet_config *cfg, int batch,
+                            int fleet_batch, gpmpc_fleet **out);
 /* (re)initialise landings [first, first+count) from x0 (count x 7) */
 int gpmpc_fleet_reset(gpmpc_fleet *f, int first, int count, const double *x0);
 /* advance every active landing by nsteps control steps (async on the ctx stream) */

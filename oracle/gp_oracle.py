@@ -330,6 +330,12 @@ def fitc_predict(st, Xq):
     return mean, lat[:, None] * st["y_std"] ** 2
 
 
+def predict(st, Xq):
+    """The predict of whichever GP ``st`` holds: a sparse fit (fitc_fit: "Luu") through
+    SparseGP.predict (sparse_gp.py:255-305, mean as written), else ExactGP.predict."""
+    return fitc_predict(st, Xq) if "Luu" in st else exact_predict(st, Xq)
+
+
 # --------------------------------------------------------------------------
 # surfaces
 # --------------------------------------------------------------------------

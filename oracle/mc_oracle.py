@@ -140,7 +140,7 @@ def landing_step(st, S, max_steps=300, dt=0.1, cfg=RUN_EXPERIMENTS_CFG, use_gp=T
     tgt = incremental_target(x)
     mean = None
     if use_gp:
-        mean, _var = gp_oracle.exact_predict(st, gp_oracle.features_3dof(Xw[:-1], Uw))
+        mean, _var = gp_oracle.predict(st, gp_oracle.features_3dof(Xw[:-1], Uw))
     P0, q = qp_oracle.cost(N, np.tile(tgt, (N + 1, 1)))
     A, l, u = qp_oracle.constraints(Xw, Uw, x, dt, gp_dv=mean, sign=-1.0, filter_small=False)
     qp = admm_ref.RefQP(len(out["y"]), settings=qp_settings)
@@ -196,7 +196,7 @@ def _sqp_landing_step(st, S, max_steps, dt, cfg, use_gp, residual_model, sqp_ite
     for it in range(sqp_iters):
         mean = None
         if use_gp:
-            mean, _var = gp_oracle.exact_predict(st, gp_oracle.features_3dof(Xw[:-1], Uw))
+            mean, _var = gp_oracle.predict(st, gp_oracle.features_3dof(Xw[:-1], Uw))
         A, l, u = qp_oracle.constraints(Xw, Uw, x, dt, gp_dv=mean, sign=-1.0, filter_small=False)
         try:
             r = qp.solve(P0.diagonal(), q, A, l, u, qp_oracle.to_vector(Xw, Uw))

@@ -624,3 +624,79 @@ def test_fleet_posterior_full_size_matches_oracle(gpu_ctx, monkeypatch, cs):
             assert np.ptp(v_ref[:, 0]) > 0.0
     finally:
         fl.close()
+
+
+def _fitc_fleet_setup(gpu_ctx):
+    """The reference-default Simple3DoFGP() (FITC, 50 kmeans2 inducing points) as the
+    fleet's GP, and the oracle's FITC fit with the surface's own inducing points."""
+    from gp_mpc_rocket_landing_amd.data import synthetic_training_data
+    from gp_mpc_rocket_landing_amd.fleet import fit_gp_sparse
+    from oracle import gp_oracle
+    h = fit_gp_sparse(n_train=1000, n_inducing=50, seed=0)
+    X, U, D = synthetic_training_data(1000, seed=0)
+    Zi = np.array(h.surface.gp.gps[0].inducing_points)
+    st = gp_oracle.fitc_fit(Zi, gp_oracle.features_3dof(X, U), D, noise=1e-4, jitter=1e-6)
+    return h, st
+
+
+def test_fleet_on_the_default_sparse_gp_matches_oracle_every_step(gpu_ctx):
+    """the fleet on the reference-default Simple3DoFGP() -- FITC,
+    M = 50 (structured_gp.py:423-428) -- through gpmpc_fleet_create_fitc.  Every
+    control step of 16 landings flown to termination against mc_oracle.landing_step
+    with the oracle's FITC GP (SparseGP.predict, sparse_gp.py:255-305, mean K*u alpha
+    as written), from the device's own previous state: outcome, steps, ADMM
+    iterations, solved count and status exact; state, plan, rho and duals within the
+    tolerance spec.  Then the fleet's own posterior at 1024 landings x 20 points
+    (P = 20 480 against the 50 inducing rows) read back through the C-ABI against
+    SparseGP.predict: mean and variance within the spec."""
+    from gp_mpc_rocket_landing_amd.fleet import Fleet, initial_conditions
+    from oracle import gp_oracle, mc_oracle
+    h, st = _fitc_fleet_setup(gpu_ctx)
+    nb = 16
+    fl = Fleet(gpu_ctx, h, nb, max_steps=300)
+    seen, steps = set(), 0
+    try:
+        fl.reset(initial_conditions(nb))
+        S = fl.state()
+        for k in range(302):
+            if np.all(S["rec"][:, 0] != 0):
+                break
+            fl.step(1)
+            T = fl.state()
+            for b in np.nonzero(S["rec"][:, 0] == 0)[0]:
+                want, info = mc_oracle.landing_step(st, _landing(S, b))
+                got = _landing(T, b)
+                tag = (k, int(b))
+                np.testing.assert_array_equal(got["rec"][[0, 1, 11, 12, 13, 14]],
+                                              want["rec"][[0, 1, 11, 12, 13, 14]], err_msg=str(tag))
+                if info is None:
+                    seen.add(int(got["rec"][0]))
+                    continue
+                steps += 1
+                for key in ("x", "Xw", "Uw"):
+                    ok, worst = close(got[key], want[key], 1.0)
+                    assert ok, (tag, key, worst)
+                ok, worst = close(got["rho"], want["rho"], 0.0); assert ok, (tag, "rho", worst)
+                ok, worst = close(got["y"], want["y"], np.abs(want["y"]).max()); assert ok, (tag, "y", worst)
+            S = T
+        assert np.all(S["rec"][:, 0] != 0) and steps > 500, (steps, S["rec"][:, 0])
+    finally:
+        fl.close()
+    nb = 1024
+    fl = Fleet(gpu_ctx, h, nb, horizon=N)
+    try:
+        fl.reset(initial_conditions(nb))
+        for step in range(2):
+            S = fl.state()
+            fl.step(1)
+            mean, var = fl.posterior()
+            Zq = gp_oracle.features_3dof(S["Xw"][:, :N].reshape(-1, 7), S["Uw"].reshape(-1, 3))
+            m_ref, v_ref = gp_oracle.fitc_predict(st, Zq)
+            for c in range(3):
+                ok, worst = close(mean.reshape(-1, 3)[:, c], m_ref[:, c], st["y_std"][c])
+                assert ok, (step, "mean", c, worst)
+                ok, worst = close(var.reshape(-1, 3)[:, c], v_ref[:, c], st["sigma2"] * st["y_std"][c] ** 2)
+                assert ok, (step, "var", c, worst)
+            assert np.ptp(v_ref[:, 0]) > 0.0
+    finally:
+        fl.close()
