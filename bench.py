@@ -404,6 +404,82 @@ def single_landing_bench(ctx, gp, steps=100, reps=3):
             "steps_per_s": round(steps / t, 1)}
 
 
+def surface_single_landing_bench(ctx, steps=100, reps=2):
+    """the drop-in surface timed, as an unchanged reference caller
+    drives it -- MonteCarloSimulator.run_single (monte_carlo.py:491-516): per control
+    step the incremental target (:497-500), ``GPMPC(dyn, Simple3DoFGP(use_sparse=False),
+    GPMPCConfig(N=20)).solve(x, target)``, u0 into the plant (+ the drag residual the GP
+    learns).  Each solve is the host mirror's path: one device GP posterior call for
+    the N horizon points, host QP assembly (mpc/qp_builder.py), one device ADMM call;
+    with GPMPCConfig's default use_gp_uncertainty=True also the covariance
+    propagation (one batched GP call + the device covariance kernel).  Beside it the
+    same loop with use_gp_uncertainty=False.  The fleet's B = 1 figure
+    (``single_landing``) is the device-resident form of the same step."""
+    from gp_mpc_rocket_landing_amd.data import drag_accel, synthetic_training_data
+    from gp_mpc_rocket_landing_amd.dynamics import create_normalized_rocket
+    from gp_mpc_rocket_landing_amd.fleet import initial_conditions
+    from gp_mpc_rocket_landing_amd.gp import Simple3DoFGP
+    from gp_mpc_rocket_landing_amd.mpc import GPMPC, GPMPCConfig
+    X, U, D = synthetic_training_data(1000, seed=0)
+    gp = Simple3DoFGP(use_sparse=False)
+    gp.add_data(X, U, D)
+    gp.fit()
+    dyn = create_normalized_rocket()
+    x0 = initial_conditions(1)[0]
+    out = {"workload": "1 landing (seed 42), GPMPC(dyn, Simple3DoFGP(use_sparse=False), GPMPCConfig(N=20))"
+                       ".solve per step, monte_carlo.py:491-516 protocol", "steps": steps}
+    for name, unc in (("us_per_step", True), ("us_per_step_no_uncertainty", False)):
+        ts = []
+        for _ in range(reps):
+            ctl = GPMPC(dyn, gp, GPMPCConfig(N=20, dt=0.1, use_gp_uncertainty=unc))
+            x = x0.copy()
+            done = 0
+            t0 = time.perf_counter()
+            for _ in range(steps):
+                tgt = x.copy(); tgt[4:7] = 0.0; tgt[1] = max(0.5, x[1] - 2.0)
+                sol = ctl.solve(x, tgt)
+                if not sol.success:
+                    break
+                xn = dyn.step(x, sol.u0, 0.1)
+                xn[4:7] += drag_accel(x)[0] * 0.1
+                x = xn
+                done += 1
+                if x[1] < 1.0:   # the protocol's landing check (altitude < 1) ends the flight
+                    break
+            ts.append((time.perf_counter() - t0) / max(done, 1))
+        out[name] = round(min(ts) * 1e6, 1)
+        out["steps_flown" if unc else "steps_flown_no_uncertainty"] = done
+    out["steps_per_s"] = round(1e6 / out["us_per_step"], 1)
+    return out
+
+
+def fleet_fitc_bench(ctx, batch=1024, steps=20, warmup=5):
+    """the fleet on the reference-default Simple3DoFGP() -- FITC,
+    50 kmeans2 inducing points (structured_gp.py:423-428) -- gpmpc_fleet_create_fitc:
+    the BASELINE configs[3] fleet with that GP, timed like the headline (device-resident,
+    one sync at the end)."""
+    from gp_mpc_rocket_landing_amd.fleet import Fleet, fit_gp_sparse, initial_conditions
+    h = fit_gp_sparse(n_train=1000, n_inducing=50, seed=0)
+    fl = Fleet(ctx, h, batch)
+    try:
+        fl.reset(initial_conditions(batch))
+        fl.step(warmup)
+        ctx.sync()
+        rec0, _ = fl.read()
+        t0 = time.perf_counter()
+        fl.step(steps)
+        ctx.sync()
+        el = time.perf_counter() - t0
+        rec1, _ = fl.read()
+    finally:
+        fl.close()
+    done = float(np.sum(rec1[:, 1] - rec0[:, 1]))
+    return {"workload": f"{batch} landings, Simple3DoFGP() default: FITC M=50 (mean as written), N=20, RTI",
+            "steps": steps, "ms_per_step": round(el / steps * 1e3, 4),
+            "control_steps_per_s": round(done / el, 1),
+            "admm_iters_per_solve": round(float(np.sum(rec1[:, 11] - rec0[:, 11])) / max(done, 1.0), 2)}
+
+
 def qp_status_histogram(fl, steps=10):
     """Status of every landing's QP over ``steps`` further control steps of the
     bench fleet (untimed): solved / solved inaccurate / maximum iterations
@@ -884,17 +960,21 @@ def main():
             out["outcomes"] = {str(int(c)): int(np.sum(oc == c)) for c in np.unique(oc)}
         out["qp_status"] = qp_status_histogram(fl)
         if not args.no_chol and world == 1:  # single-GPU legs: the N > 1 runs keep to the metric
-            try:
-                out["single_landing"] = single_landing_bench(ctx, gp)
-                out["gpmpc_loop"] = gpmpc_loop_bench(ctx, gp)
-                out["simple3dof_gp"] = simple3dof_gp_bench(ctx, cpu=not args.no_cpu)
-                out["cholesky"] = cholesky_bench(ctx, torch)
-                out["structured_fitc"] = structured_fitc_bench(ctx)
-                out["rollouts6"] = rollouts6_bench(ctx, torch)
-                out["lml_batched"] = lml_bench(ctx, cpu=not args.no_cpu)
-                out["gp_append"] = append_bench(ctx)
-            except Exception as e:  # noqa: BLE001
-                out["cholesky"] = {"error": str(e)[:200]}
+            legs = [("single_landing", lambda: single_landing_bench(ctx, gp)),
+                    ("surface_single_landing", lambda: surface_single_landing_bench(ctx)),
+                    ("fleet_fitc", lambda: fleet_fitc_bench(ctx)),
+                    ("gpmpc_loop", lambda: gpmpc_loop_bench(ctx, gp)),
+                    ("simple3dof_gp", lambda: simple3dof_gp_bench(ctx, cpu=not args.no_cpu)),
+                    ("cholesky", lambda: cholesky_bench(ctx, torch)),
+                    ("structured_fitc", lambda: structured_fitc_bench(ctx)),
+                    ("rollouts6", lambda: rollouts6_bench(ctx, torch)),
+                    ("lml_batched", lambda: lml_bench(ctx, cpu=not args.no_cpu)),
+                    ("gp_append", lambda: append_bench(ctx))]
+            for name, leg in legs:   # a failing leg is recorded as such; the others still run
+                try:
+                    out[name] = leg()
+                except Exception as e:  # noqa: BLE001
+                    out[name] = {"error": f"{type(e).__name__}: {e}"[:300]}
         if cb is not None:
             cb["value"] = round(cb["value"], 3)
             out["cpu_baseline"] = cb
