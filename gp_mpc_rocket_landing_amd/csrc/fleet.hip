@@ -319,6 +319,7 @@ __global__ __launch_bounds__(256) void k_fleet_control(FleetArgs a) {
   const double dt = a.dt;
   double *rec = a.rec + (int64_t)b * GPMPC_REC_LEN;
   if (rec[0] != 0.0) return;  // terminated landing
+  if (a.sqp && !a.sqp_first && a.sqp_done[b]) return;  // converged in an earlier SQP pass
   QPStamps T;
   T.out = (b == 0) ? a.stamps : nullptr;
   T.start();
@@ -339,11 +340,13 @@ __global__ __launch_bounds__(256) void k_fleet_control(FleetArgs a) {
     const double m0 = rec[13];
     bool div = false;
     for (int i = 0; i < NX; ++i) div = div || !(fabs(sx[i]) <= 1e6);
-    if ((int)rec[1] >= a.max_steps) out = 5;                    // TIMEOUT
+    if (a.sqp && !a.sqp_first) out = 0;                         // later SQP passes: checks done
+    else if ((int)rec[1] >= a.max_steps) out = 5;               // TIMEOUT
     else if (sx[1] < 0.0) out = 2;                              // CRASH
     else if (sx[0] <= 1.0 + 0.01) out = 3;                      // FUEL_EXHAUSTED
     else if (div) out = 6;                                      // DIVERGENCE
     else if (sx[1] < 1.0 && fabs(sx[4]) < 5.0) out = landing_ok(sx, m0) ? 1 : 4;
+    if (a.sqp && a.sqp_first) a.sqp_done[b] = 0;
     s_out = out;
     // target: incremental (monte_carlo.py:497-500) or fixed
     for (int i = 0; i < NX; ++i) st_tgt[i] = a.target_mode ? sx[i] : a.xt[(int64_t)b * NX + i];
@@ -474,6 +477,63 @@ __global__ __launch_bounds__(256) void k_fleet_control(FleetArgs a) {
       for (int i = 0; i < NX; ++i) rec[4 + i] = sx[i];
       rec[2] = rec[13] - sx[0];
     }
+    return;
+  }
+  if (a.sqp) {
+    // GPMPC.solve's loop (gp_mpc.py:336-353), as k_fleet_control2: the change of the
+    // trajectory, X_pred <- X_new (no shift), stop below sqp_tol
+    __shared__ double s_dm[4];
+    double dm = 0.0;
+    for (int j = tid; j < n; j += nt) {
+      const int i = (j >= Nv) ? j - Nv : j % (NX + NU), k = j / (NX + NU);
+      const double old = (j >= Nv) ? Xw[N * NX + i] : (i < NX ? Xw[k * NX + i] : Uw[k * NU + i - NX]);
+      dm = fmax(dm, fabs(s.x[j] - old));
+    }
+    for (int o = 32; o > 0; o >>= 1) dm = fmax(dm, __shfl_xor(dm, o));
+    if ((tid & 63) == 0) s_dm[tid >> 6] = dm;
+    __syncthreads();  // (also orders every read of Xw / Uw before the writes)
+    dm = s_dm[0];
+    for (int w = 1; w < nt / 64; ++w) dm = fmax(dm, s_dm[w]);
+    for (int e = tid; e < (N + 1) * NX; e += nt) {
+      const int k = e / NX, i = e - k * NX;
+      Xw[e] = s.x[(k == N) ? Nv + i : k * (NX + NU) + i];
+    }
+    for (int e = tid; e < N * NU; e += nt) {
+      const int k = e / NU, i = e - k * NU;
+      Uw[e] = s.x[k * (NX + NU) + NX + i];
+    }
+    for (int r = tid; r < m; r += nt) a.ysc[(int64_t)b * m + r] = s.y[r];
+    if (tid == 0) {
+      const bool conv = dm < a.sqp_tol;
+      a.rho[b] = s.rho_s;
+      rec[11] += res.iter;
+      a.lastit[b] = res.iter;
+      rec[12] += (res.status == 1) ? 1.0 : 0.0;
+      rec[14] = res.status;
+      rec[15] = s.rho_s;
+      if (conv) {
+        const double u0[NU] = {s.x[NX], s.x[NX + 1], s.x[NX + 2]};
+        double xn[NX], dr[3];
+        plant_euler(sx, u0, dt, xn);
+        if (a.residual_model) {
+          drag_residual(sx, dr);
+          xn[4] += dr[0] * dt; xn[5] += dr[1] * dt; xn[6] += dr[2] * dt;
+        }
+        for (int i = 0; i < NX; ++i) x[i] = xn[i];
+        rec[1] += 1.0;
+        rec[3] = rec[1] * dt;
+        rec[2] = rec[13] - xn[0];
+        for (int i = 0; i < NX; ++i) rec[4 + i] = xn[i];
+        a.sqp_done[b] = 1;
+      } else if (a.sqp_last) {  // MPCSolution.success False -> DIVERGENCE (monte_carlo.py:506-508)
+        rec[0] = 6;
+        rec[2] = rec[13] - sx[0];
+        for (int i = 0; i < NX; ++i) rec[4 + i] = sx[i];
+      }
+    }
+    T.mark(7);
+    T.flush();
+    if (a.trace && tid == 0) a.trace[(int64_t)b * 4 + 1] = __builtin_amdgcn_s_memrealtime();
     return;
   }
   if (has) {
@@ -1029,11 +1089,6 @@ static int fleet_create(gpmpc_ctx *ctx, gpmpc_gp *gp, gpmpc_fitc *fitc, const gp
   (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device);
   const char *we = getenv("GPMPC_FLEET_WIDE");
   f->wide = f->use_fq && (we ? atoi(we) != 0 : fleet_batch <= cus);
-  if (cfg->sqp_iters > 1 && !f->use_fq) {  // the SQP pass is implemented in k_fleet_control2
-    delete f;
-    gpmpc_set_error("fleet: sqp_iters > 1 needs the fleet solver (N = 20, GPMPC_FLEET_SOLVER != 0)");
-    return -2;
-  }
   GPMPC_HIP(hipStreamSynchronize(ctx->stream));
   *out = f;
   return 0;
