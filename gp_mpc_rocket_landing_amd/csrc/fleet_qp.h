@@ -81,6 +81,18 @@ __device__ __forceinline__ int fq_tid() {
 #define FQ_TWIST 1
 #endif
 #include "fleet_twist.h"
+// FQ_PART: the partitioned solve of fleet_part.h, opt-in for the wide build (-DFQ_PART=1).
+// Measured (profiles/r6_partitioned_kkt.md): its substitution takes 4235 cycles against the
+// twisted solve's 5560, but its factor (segment chains, spikes, the 30 x 30 Shat^-1) 85.9K
+// against 41.7K and the consumers' V x_S terms add ~550 a iteration: 194 us a single-landing
+// step against 177 us.  Kept for the record and the probe (scripts/fp_probe.hip).
+#ifndef FQ_PART
+#define FQ_PART 0
+#endif
+#if FQ_PART
+static_assert(FQ_T >= 256, "the partitioned solve's correction takes one variable per thread");
+#include "fleet_part.h"
+#endif
 
 struct FleetSmem {
   double A[FQ_NNZD + 1];
@@ -93,6 +105,14 @@ struct FleetSmem {
   double red[FQ_NW][16];
   double c, rho_s;
   int flag;
+#if FQ_PART
+  double spk[FP_SPK];          // spikes V = M_II^-1 M_IS (fleet_part.h)
+  double sinv[FP_NS * FP_NS];  // Shat^-1
+  alignas(16) double xs[32];   // x_S (read as 16-byte pairs)
+  double bh[64];               // bhat_S; the Shat inverse's pivot rows
+  double brhs[FQ_NMAX];        // copy of the KKT right-hand side (the spike partial sums read it)
+  double part[80];             // the partial sums L_k^T b_k of segments B and C
+#endif
   __device__ double *band() { return band_store; }
 };
 
@@ -191,6 +211,11 @@ struct FleetRegs {
   int cn[2], cp[2][FQ_CMAX];
 #if FQ_AREG
   double av[2][FQ_CMAX];  // the column's scaled dynamics values (FQ_AREG: read once per solve)
+#endif
+#if FQ_PART
+  double vsp[17];         // the variable's spike row (fleet_part.h), reloaded after each factor
+  double wsp[17];         // dynamics row 0's: sum_e A[r][e] (spike row of column e)
+  int vseg, rseg;         // the segments those spikes belong to
 #endif
   int rbn0, rcp0[(FQ_RMAX + 1) / 2];
   __device__ __forceinline__ double &ur(int h) { return h ? P[1] : ur0; }
@@ -463,13 +488,25 @@ __device__ __forceinline__ int fq_factor(const QPPattern &pt, FleetSmem &s, Flee
   __syncthreads();
   if (T) T->mark(13);
   int f = 0;
-#if FQ_TWIST && !defined(FT_OLD_FACTOR)
+#if FQ_PART
+  f = fp_factor(s, cw);
+#elif FQ_TWIST && !defined(FT_OLD_FACTOR)
   f = ft_factor(s, cw);
 #else
   if ((tid >> 6) == cw) f = blk_factor_dispatch(pt, s);
 #endif
   if ((tid & 63) == 0 && (tid >> 6) == cw) s.flag = f;  // the chain wave's lane 0 reports
   __syncthreads();
+#if FQ_PART
+  fp_load_spikes(s, R.vj[0], R.vsp);
+  R.vseg = fp_seg(R.vj[0] / FT_SZ);
+  {
+    int cols[FQ_RMAX];
+#pragma unroll
+    for (int e = 0; e < FQ_RMAX; ++e) cols[e] = R.rc(0, e);
+    R.rseg = fp_load_rowspikes(s, R.rb(0), R.rok[0] ? R.rn(0) : 0, cols, R.wsp);
+  }
+#endif
   return s.flag;
 }
 
@@ -682,6 +719,7 @@ __device__ __forceinline__ QPResult fq_solve(const QPPattern &pt, FleetSmem &s, 
   }
   // the block solve reads b in whole blocks (plus look-ahead): zero the tail
   for (int j = n + tid; j < FQ_NMAX; j += FQ_T) s.rhs[j] = 0.0;
+
   if (tid == 0) s.rho_s = fmin(fmax(s.rho_s, QP_RHO_MIN), QP_RHO_MAX);
   __syncthreads();
 #if FQ_AREG
@@ -744,13 +782,29 @@ __device__ __forceinline__ QPResult fq_solve(const QPPattern &pt, FleetSmem &s, 
       if (R.vok[h]) {
         double acc = fq_col_dot(s, R, h);
         acc += R.Ab[h] * (fq_rho(R.lb[h], R.ub[h], s.rho_s) * R.zb_(h) - R.yb_(h));
-        s.rhs[R.vj[h]] = sig * R.x[h] - R.q[h] + acc;
+        const double rv = sig * R.x[h] - R.q[h] + acc;
+        s.rhs[R.vj[h]] = rv;
+#if FQ_PART
+        s.brhs[R.vj[h]] = rv;
+#endif
       }
 #endif
     T.mark(11);
     __syncthreads();
     T.mark(3);
-#if FQ_TWIST
+#if FQ_PART
+    // x~ but the separator correction: the segment chains (wave cw) and the separators'
+    // Schur solve beside them (fleet_part.h), LDS-only barriers between; each consumer
+    // below subtracts its V x_S itself (fp_corr)
+    fp_solve<1>(s, s.rhs, cw);
+    T.mark(8);
+    lds_sync();
+    fp_solve<2>(s, s.rhs, cw);
+    T.mark(9);
+    lds_sync();
+    fp_solve<4>(s, s.rhs, cw);
+    T.mark(10);
+#elif FQ_TWIST
     // x~: two-ended forward chains (wave cw), diagonal products (both waves),
     // two-ended backward chains (wave cw), LDS-only barriers between
     ft_solve<1>(s, s.rhs, cw);
@@ -778,7 +832,11 @@ __device__ __forceinline__ QPResult fq_solve(const QPPattern &pt, FleetSmem &s, 
 #pragma unroll
     for (int h = 0; h < FQ_H; ++h) {
       if (R.vok[h]) {
+#if FQ_PART
+        const double xt = s.rhs[R.vj[h]] - fp_corr(s, R.vseg, R.vsp);
+#else
         const double xt = s.rhs[R.vj[h]];
+#endif
         const double xo = R.x[h];
         const double xn = al * xt + (1.0 - al) * xo;
         R.dx[h] = xn - xo;
@@ -794,7 +852,11 @@ __device__ __forceinline__ QPResult fq_solve(const QPPattern &pt, FleetSmem &s, 
         R.dyb_(h) = d; R.yb_(h) = yn; R.zb_(h) = zn;
       }
       if (R.rok[h]) {
+#if FQ_PART
+        const double ztl = fq_row_dot(s, R, h) - fp_corr(s, R.rseg, R.wsp);
+#else
         const double ztl = fq_row_dot(s, R, h);
+#endif
         const double rho = QP_RHO_EQ * rs, zo = R.zr(h), yo = R.yr(h);
         const double zr = al * ztl + (1.0 - al) * zo;
         double zn = zr + yo / rho;

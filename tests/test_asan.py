@@ -29,7 +29,7 @@ CHILD = textwrap.dedent(r'''
     import ctypes, numpy as np
     from gp_mpc_rocket_landing_amd import _lib
     L = _lib._L
-    assert _lib.abi_version() == 3 and _lib.LIB_PATH.endswith("libgpmpc_hip_asan.so")
+    assert _lib.abi_version() == _lib.ABI_VERSION == 4 and _lib.LIB_PATH.endswith("libgpmpc_hip_asan.so")
     assert isinstance(L.gpmpc_last_error(), bytes)
     s = _lib.qp_default_settings(max_iter=7)
     assert s.max_iter == 7 and s.rho == 0.1
@@ -53,6 +53,8 @@ CHILD = textwrap.dedent(r'''
         L.gpmpc_fitc_fit(None, dp, 2, dp, 4, 2, dp, 1, dp, 1.0, 1e-4, 1e-6, ctypes.byref(h), None, None, None, None),
         L.gpmpc_fitc_predict(None, None, dp, 1, dp, dp),
         L.gpmpc_fleet_create(None, None, None, 4, ctypes.byref(h)),
+        L.gpmpc_fleet_create_shard(None, None, None, 4, 8, ctypes.byref(h)),
+        L.gpmpc_fleet_create_fitc(None, None, None, 4, 4, ctypes.byref(h)),
         L.gpmpc_fleet_step(None, 1),
         L.gpmpc_fleet_read(None, dp, dp),
         L.gpmpc_rollout6_create(None, None, None, None, 4, ctypes.byref(h)),
