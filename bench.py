@@ -53,7 +53,7 @@ CONTROL_KERNEL = "k_fleet_control" if os.environ.get("GPMPC_FLEET_SOLVER", "1") 
 
 def pmc_traffic(kernel):
     """Per-launch HBM bytes of ``kernel`` from the committed rocprofv3 --pmc
-    passes (profiles/*_pmc_traffic.json, scripts/pmc_traffic.py), else None."""
+    passes (profiles/*_pmc_traffic.json, scripts/pmc.py traffic), else None."""
     import glob
     for path in sorted(glob.glob(os.path.join(REPO, "profiles", "*_pmc_traffic.json")), reverse=True):
         try:
@@ -722,7 +722,7 @@ def rollouts6_bench(ctx, torch=None, batches=(64, 512), max_steps=300):
     out["qp_status"] = {"rollouts": B, "solves": tot, "status": hist,
                         "status_frac": {k: round(v / tot, 4) for k, v in hist.items()}}
     # the same controller with ADMM settings at which >= 90% of its QPs
-    # return "solved" (scripts/r6_qp_sweep.py: max_iter 50 / 100 / 200 / 400 / 1000 / 4000
+    # return "solved" (scripts/probe.py qp_sweep: max_iter 50 / 100 / 200 / 400 / 1000 / 4000
     # at eps 1e-4 gave 12 / 53 / 75 / 83 / 89 / 96% solved), beside the osqp_rti setting
     out["solved_setting"] = rollouts6_timed(ctx, gv, gw, batches, max_steps, **SOLVED_QP6)
     # the FITC posterior mean (K*u L_uu^-T alpha, SURVEY D1 fixed): the same rollouts timed

@@ -31,7 +31,7 @@
 #define FP_SPK (FT_NB * FT_BS)
 #define FP_NS 30                // separator unknowns: blocks 5, 10, 15
 
-// section timestamps of fp_factor (scripts/fp_probe.hip defines it)
+// section timestamps of fp_factor (scripts/hip/fp_probe.hip defines it)
 #ifndef FP_MARK
 #define FP_MARK(k)
 #endif

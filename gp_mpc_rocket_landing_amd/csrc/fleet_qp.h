@@ -85,7 +85,7 @@ __device__ __forceinline__ int fq_tid() {
 // Measured (profiles/r6_partitioned_kkt.md): its substitution takes 4235 cycles against the
 // twisted solve's 5560, but its factor (segment chains, spikes, the 30 x 30 Shat^-1) 85.9K
 // against 41.7K and the consumers' V x_S terms add ~550 a iteration: 194 us a single-landing
-// step against 177 us.  Kept for the record and the probe (scripts/fp_probe.hip).
+// step against 177 us.  Kept for the record and the probe (scripts/hip/fp_probe.hip).
 #ifndef FQ_PART
 #define FQ_PART 0
 #endif

@@ -4,7 +4,7 @@
 // first 7 rows, the last block padded to identity).  One workgroup of 256 threads, each
 // wave's lane 0 stamps s_memtime around every phase.  Prints per-phase cycles per solve
 // and the solution's error against a host Gaussian elimination.
-//   hipcc -O3 --offload-arch=gfx950 -I gp_mpc_rocket_landing_amd/csrc scripts/fp_probe.hip -o /tmp/fp_probe
+//   hipcc -O3 --offload-arch=gfx950 -I gp_mpc_rocket_landing_amd/csrc scripts/hip/fp_probe.hip -o /tmp/fp_probe
 #define FQ_T 256
 #define FQ_WPE 1
 #define FQ_PART 1

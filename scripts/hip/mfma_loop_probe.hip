@@ -2,7 +2,7 @@
 // (16 accumulators x 4 substeps), 256-thread workgroups, two per CU, with
 //   BAR: one __syncthreads per step;  LDS: the step's 16 ds_read_b128 operand reads;
 //   DMA: 8 global_load_lds_dwordx4 per wave and step, vmcnt(0) before the barrier.
-//   hipcc --offload-arch=gfx950 -O3 scripts/mfma_loop_probe.hip -o scripts/mfma_loop_probe.bin
+//   hipcc --offload-arch=gfx950 -O3 scripts/hip/mfma_loop_probe.hip -o scripts/mfma_loop_probe.bin
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <cstdint>

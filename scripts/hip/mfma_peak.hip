@@ -1,6 +1,6 @@
 // FP64 MFMA issue-rate probe: v_mfma_f64_16x16x4f64 from registers only (no memory in the
 // loop), NACC independent accumulators per wave, W waves per workgroup, G workgroups.
-//   hipcc --offload-arch=gfx950 -O3 scripts/mfma_peak.hip -o /tmp/mfma_peak && /tmp/mfma_peak
+//   hipcc --offload-arch=gfx950 -O3 scripts/hip/mfma_peak.hip -o /tmp/mfma_peak && /tmp/mfma_peak
 #include <hip/hip_runtime.h>
 #include <cstdio>
 typedef double d4_t __attribute__((ext_vector_type(4)));

@@ -1,6 +1,6 @@
 // Accuracy of v_rsq_f64 and of 0 / 1 / 2 Newton steps on it (the Cholesky
 // pivot's 1/sqrt), in ulps of the correctly rounded host value.
-// Build: hipcc -O3 --offload-arch=gfx950 scripts/rsq_probe.hip -o /tmp/rsq_probe
+// Build: hipcc -O3 --offload-arch=gfx950 scripts/hip/rsq_probe.hip -o /tmp/rsq_probe
 #include <hip/hip_runtime.h>
 #include <cmath>
 #include <cstdio>
