@@ -51,14 +51,22 @@ __device__ __forceinline__ int mma128_col(int wave, int y, bool ilc) {
 template <bool L2A, bool L2B, bool ILC, bool NEGA, bool DMA>
 constexpr bool mma128_dma() { return MMA_V2 && DMA && (MMA_V2_ALL || (!L2A && !L2B && !ILC)); }
 
+// The slot swizzle of row r: (r >> 1) & 5.  Over a lane group the even rows split into
+// {0, 2, 12, 14} (k quad q) and {4, 6, 8, 10} (quad q ^ 1), likewise the odd rows; each set
+// takes the swizzles {0, 1, 4, 5} and the other quad's chunk differs by 2, which maps them
+// onto {2, 3, 6, 7}.  ((r >> 1) & 7, the consecutive-16-lane design, put the two quads on
+// the same slots: every read 2-way conflicted, SQ_LDS_BANK_CONFLICT 0.49 of the LDS cycles.)
+__device__ __forceinline__ int mma128_swz(int r) { return (r >> 1) & 5; }
+
 // A zero 16-byte chunk: the LDS-DMA source of a tile's padding rows.
 static __device__ __attribute__((aligned(16))) double g_mma_zero[2] = {0.0, 0.0};
 
 // mma128_tile's loop with LDS-DMA staging (global_load_lds_dwordx4, no staging registers,
 // no ds_write pass) and 16-byte fragment reads.  An operand's K step is 128 rows x 16
 // doubles, 128 B a row, unpadded (one DMA wave-instruction fills 8 whole rows); the row's
-// 16-byte chunk c (k = 2c, 2c + 1) sits in slot c ^ ((r >> 1) & 7), so the 16 rows of a
-// fragment read hit 16 distinct (r & 1, slot) bank groups: conflict-free ds_read_b128.
+// 16-byte chunk c (k = 2c, 2c + 1) sits in slot c ^ mma128_swz(r), so each of ds_read_b128's
+// four lane groups ({0-3,12-15,20-27}, {4-11,16-19,28-31} and the same +32: lanes of two
+// different k quads) hits 16 distinct (r & 1, slot) bank groups: conflict-free.
 // The swizzle is applied on the DMA's per-lane global source address.  Substep q of a
 // K step reads k = 4 (lane >> 4) + q (A and B alike), so one ds_read_b128 serves two
 // substeps and a lane's four k's are two reads.  The step with a partial K slice (k_hi
@@ -93,10 +101,10 @@ __device__ __forceinline__ void mma128_tile_v2(const double *__restrict__ A, int
   }
   const bool vec = ((lda | ldb) & 1) == 0 && ((((uintptr_t)A) | ((uintptr_t)B)) & 15) == 0;
   // staging map: instruction j of this wave fills tile row (4 wave + j) * 8 + lane / 8,
-  // slot lane % 8, with the row's chunk (lane % 8) ^ ((row >> 1) & 7)
+  // slot lane % 8, with the row's chunk (lane % 8) ^ mma128_swz(row)
   const int rs = (4 * wave) * 8 + (lane >> 3);
   auto st_row = [&](int j) { return rs + 8 * j; };
-  auto st_chunk = [&](int j) { return (lane & 7) ^ ((st_row(j) >> 1) & 7); };
+  auto st_chunk = [&](int j) { return (lane & 7) ^ mma128_swz(st_row(j)); };
   // The DMA is issued from inline asm: the compiler does not see it as an LDS write, so it
   // adds no wait before the fragment reads of the other buffer (which it cannot tell apart
   // from the DMA's); every step ends on an explicit vmcnt(0) + barrier instead.
@@ -146,8 +154,8 @@ __device__ __forceinline__ void mma128_tile_v2(const double *__restrict__ A, int
       }
     }
   };
-  // fragment reads: row R = (16-aligned block row) + lane % 16, so (R >> 1) & 7 = (lane % 16) / 2
-  const int sw = (lane & 15) >> 1;
+  // fragment reads: row R = (16-aligned block row) + lane % 16, so mma128_swz(R) = mma128_swz(lane % 16)
+  const int sw = mma128_swz(lane & 15);
   const int foff0 = (lane & 15) * 16 + 2 * ((2 * (lane >> 4)) ^ sw);      // k = 4 (lane >> 4) + {0, 1}
   const int foff1 = (lane & 15) * 16 + 2 * ((2 * (lane >> 4) + 1) ^ sw);  // k = 4 (lane >> 4) + {2, 3}
   stage(0, k_lo);

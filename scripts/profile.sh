@@ -12,6 +12,8 @@
 #   r6mem      two --pmc passes of memory-pipeline counters over the rollouts leg (k_r6_* sums)
 #   mfma       --pmc MFMA busy / clock / waits of the command (default: the main workload)
 #   kstats     --kernel-trace --stats of the command, top kernels
+#   pmc        one --pmc pass of the counters in $PMC over the command (default: the main
+#              workload), per-kernel means of the kernels starting with $PMC_PREFIX (default k_)
 set -euo pipefail
 TAG=$1; PASSES=$2; shift 2
 [ "${1:-}" = "--" ] && shift
@@ -60,6 +62,11 @@ for p in $PASSES; do
     kstats)
       prof 400 kstats --kernel-trace --stats --output-format csv -d "$OUT/kstats" -o run -- "${CMD[@]}"
       python3 scripts/pmc.py top "$(csv kstats kernel_stats)" | tee "$OUT/kstats.txt" ;;
+    pmc)
+      [ ${#CMD[@]} -gt 0 ] || CMD=("${MAIN[@]}")
+      (cd /tmp && TMPDIR=/tmp timeout -s KILL 300 rocprofv3 --pmc $PMC --output-format csv -d "$OUT/pmc" -o run \
+         -- "${CMD[@]}" > "$OUT/pmc.log" 2>&1)
+      python3 scripts/pmc.py sum "$(csv pmc counter_collection)" "${PMC_PREFIX:-k_}" > "$OUT/pmc.txt" ;;
     *) echo "unknown pass $p" >&2; exit 2 ;;
   esac
 done
