@@ -35,8 +35,7 @@ run() {
     *) echo "unknown workload $WL" >&2; exit 2 ;;
   esac
 }
-summary() {
-  python3 - "$WL" "$1" <<'PY'
+SUMMARY=$(cat <<'PY'
 import json, sys
 wl, lab = sys.argv[1], sys.argv[2]
 lines = sys.stdin.read().splitlines()
@@ -58,7 +57,8 @@ else:
     s = [d]
 print(lab, *s)
 PY
-}
+)
+summary() { python3 -c "$SUMMARY" "$WL" "$1"; }
 for r in $(seq 1 "$REPS"); do
   for S in $SETS; do
     if [ "$S" = - ]; then out=$(run 2>/dev/null)
