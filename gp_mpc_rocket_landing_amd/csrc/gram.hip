@@ -92,6 +92,9 @@ __global__ __launch_bounds__(256) void k_gram(int kind, const double *__restrict
 #ifndef GRAM_UNROLL
 #define GRAM_UNROLL 8
 #endif
+#ifndef GRAM_NT
+#define GRAM_NT 1
+#endif
 template <int D, int KIND>
 __global__ __launch_bounds__(256) void k_gram_rows(const double *__restrict__ a,
                                                    const double *__restrict__ na, int n1,
@@ -119,15 +122,33 @@ __global__ __launch_bounds__(256) void k_gram_rows(const double *__restrict__ a,
   if (cv) nbj = nb[col];
   __syncthreads();
   if (!cv) return;
-#pragma unroll GRAM_UNROLL
-  for (int rr = 0; rr < RPT; ++rr) {
-    const int r = rb + rr, row = r0 + r;
+  // K* is streamed: written once here, read once by the posterior GEMM from the Infinity
+  // Cache / HBM (GRAM_NT: non-temporal stores, no L2 write-allocate).  A full row tile
+  // (every tile but the last) stores without the per-row bound test.
+  double *Kc = K + (int64_t)(r0 + rb) * ldk + col;
+  auto put = [&](int rr, double v) {
+#if GRAM_NT
+    __builtin_nontemporal_store(v, Kc + (int64_t)rr * ldk);
+#else
+    Kc[(int64_t)rr * ldk] = v;
+#endif
+  };
+  auto elem = [&](int r) {
     double dot = 0.0;
 #pragma unroll
     for (int k = 0; k < D; ++k) dot = fma(sa[r][k], bj[k], dot);
     const double d2 = (sna[r] + nbj) - 2.0 * dot;
-    const double v = kernel_epilogue(KIND, d2, sigma2, iso_scale);
-    if (row < n1) K[(int64_t)row * ldk + col] = v;
+    return kernel_epilogue(KIND, d2, sigma2, iso_scale);
+  };
+  if (r0 + GRAM_ROWS <= n1) {
+#pragma unroll GRAM_UNROLL
+    for (int rr = 0; rr < RPT; ++rr) put(rr, elem(rb + rr));
+  } else {
+#pragma unroll GRAM_UNROLL
+    for (int rr = 0; rr < RPT; ++rr) {
+      const double v = elem(rb + rr);
+      if (r0 + rb + rr < n1) put(rr, v);
+    }
   }
 }
 
