@@ -1563,9 +1563,13 @@ __device__ __forceinline__ double ld_l2(const double *p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// X (n x nrhs, ld ldx) <- op(L)^-1 X ; op = L (trans=0) or L^T (trans=1)
+// X (n x nrhs, ld ldx) <- op(L)^-1 X ; op = L (trans=0) or L^T (trans=1), n <= TB.
 // rhs_lower: X is known lower-triangular (X[r][c] = 0 for r < c, e.g. identity):
 // the forward walk starts at the panel's first column.
+// The workgroup's 64-column panel of X stays in LDS for the whole walk: each 32-row
+// block is solved from the blocks solved before it (read from LDS, not re-read through
+// the L2 after a store drain) and written to X once at the end.  Same operations in the
+// same order as the block-by-block walk (same bits).
 __global__ __launch_bounds__(256) void k_trsm_panel(int n, int nrhs, const double *L, int64_t ldl,
                                                     const double *Linv, double *X, int64_t ldx,
                                                     int trans, int rhs_lower) {
@@ -1582,21 +1586,23 @@ __global__ __launch_bounds__(256) void k_trsm_panel(int n, int nrhs, const doubl
   const int c0 = blockIdx.x * 64;
   const int nblk = (n + NB - 1) / NB;
   __shared__ double sL[NB][TP];
-  __shared__ double sX[NB][64 + 1];
+  __shared__ double sXp[TB][64 + 1];
   const int tid = threadIdx.x;
   const int rr = tid >> 3;        // 0..31 row within block
   const int cc = (tid & 7) * 8;   // 8 columns
+  for (int e = tid; e < TB * 64; e += 256) {
+    const int i = e >> 6, j = e & 63, c = c0 + j;
+    sXp[i][j] = (i < n && c < nrhs) ? X[(int64_t)i * ldx + c] : 0.0;
+  }
   for (int step = 0; step < nblk; ++step) {
     const int ib = trans ? (nblk - 1 - step) : step;
     if (!trans && rhs_lower && (ib + 1) * NB <= c0) continue;
     const int r0 = ib * NB;
     const int nbi = min(NB, n - r0);
+    __syncthreads();  // the previous block's rows (and the panel load) before they are read
     double acc[8];
 #pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      int c = c0 + cc + q;
-      acc[q] = (rr < nbi && c < nrhs) ? ld_l2(X + (int64_t)(r0 + rr) * ldx + c) : 0.0;
-    }
+    for (int q = 0; q < 8; ++q) acc[q] = sXp[r0 + rr][cc + q];
     // subtract contributions of already-solved blocks
     const int kb_lo = trans ? ib + 1 : ((rhs_lower) ? (c0 / NB) : 0);
     const int kb_hi = trans ? nblk : ib;
@@ -1614,16 +1620,11 @@ __global__ __launch_bounds__(256) void k_trsm_panel(int n, int nrhs, const doubl
         }
         sL[i][j] = v;
       }
-      for (int e = tid; e < NB * 64; e += 256) {
-        int i = e / 64, j = e % 64;
-        int c = c0 + j;
-        sX[i][j] = (i < nbk && c < nrhs) ? ld_l2(X + (int64_t)(k0 + i) * ldx + c) : 0.0;
-      }
       __syncthreads();
       for (int j = 0; j < NB; ++j) {
         const double l = sL[rr][j];
 #pragma unroll
-        for (int q = 0; q < 8; ++q) acc[q] = fma(-l, sX[j][cc + q], acc[q]);
+        for (int q = 0; q < 8; ++q) acc[q] = fma(-l, sXp[k0 + j][cc + q], acc[q]);
       }
     }
     // apply the inverse of the diagonal block: X_ib = inv(op(L_ii)) * acc
@@ -1634,7 +1635,7 @@ __global__ __launch_bounds__(256) void k_trsm_panel(int n, int nrhs, const doubl
       sL[i][j] = trans ? Linv[(int64_t)ib * NB * NB + j * NB + i] : Linv[(int64_t)ib * NB * NB + e];
     }
 #pragma unroll
-    for (int q = 0; q < 8; ++q) sX[rr][cc + q] = acc[q];
+    for (int q = 0; q < 8; ++q) sXp[r0 + rr][cc + q] = acc[q];  // rows past n: zeros times zero columns
     __syncthreads();
     double out[8];
 #pragma unroll
@@ -1642,15 +1643,16 @@ __global__ __launch_bounds__(256) void k_trsm_panel(int n, int nrhs, const doubl
     for (int j = 0; j < NB; ++j) {
       const double l = sL[rr][j];
 #pragma unroll
-      for (int q = 0; q < 8; ++q) out[q] = fma(l, sX[j][cc + q], out[q]);
+      for (int q = 0; q < 8; ++q) out[q] = fma(l, sXp[r0 + j][cc + q], out[q]);
     }
-#pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      int c = c0 + cc + q;
-      if (rr < nbi && c < nrhs) X[(int64_t)(r0 + rr) * ldx + c] = out[q];
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+#pragma unroll
+    for (int q = 0; q < 8; ++q) sXp[r0 + rr][cc + q] = rr < nbi ? out[q] : 0.0;
+  }
+  __syncthreads();
+  for (int e = tid; e < TB * 64; e += 256) {
+    const int i = e >> 6, j = e & 63, c = c0 + j;
+    if (i < n && c < nrhs) X[(int64_t)i * ldx + c] = sXp[i][j];
   }
 }
 
