@@ -305,7 +305,15 @@ struct R6Args {
   R6Rocket rk;
   int *done, *passes, *qit, *qst;
   int mcv, mcw;  // inducing rows of each GP the predict kernel keeps in LDS (r6_pcache_rows)
+  // the split predict (r6_predict_parts): each rollout's kernel rows over `parts`
+  // co-resident workgroups, their per-wave sums exchanged as tagged 8-byte granules
+  // (R6_GRAN per point, two point parities per rollout, zeroed before every launch)
+  int parts, nb;  // workgroups per rollout; the batch (the split's grid covers it in eights)
+  unsigned long long *gran;
+  unsigned *tmo;  // a bounded spin that gave up (nonzero: the results are unreliable)
 };
+// per rollout and point parity: 7 kernel-row waves x 6 sums x 2 granules (hi, lo words)
+#define R6_GRAN 84
 // rows of each GP the predict kernel caches in LDS, feature-major: 720 x (13 + 12) doubles =
 // 141 KB beside its ~4 KB of static LDS (GPMPC_R6_PCACHE rows; 0 = none)
 #define R6_PCACHE_ROWS 720

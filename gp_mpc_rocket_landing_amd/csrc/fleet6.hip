@@ -55,6 +55,8 @@ struct gpmpc_rollout6 {
   DevBuf betav, betaw;  // (L_uu^-T alpha)^T of each GP, 3 x M
   DevBuf prm;           // problem data (R6_PRM doubles, r6_prm layout)
   DevBuf xt, ut, done, passes, qit, qst, xin;  // GPMPC.solve mode: X_ref (B x (N+1) x 14), U_ref (B x N x 3)
+  DevBuf gran;          // the split predict's granules (B x 2 x R6_GRAN) and timeout word, one block
+  int cus = 0;          // compute units of the device (the split predict needs parts x B of them)
 };
 
 extern "C" void gpmpc_rollout6_default_config(gpmpc_rollout6_config *c) {
@@ -177,6 +179,10 @@ static int r6_create(gpmpc_ctx *ctx, const GpView &gv, const GpView &gw, bool ex
   if (joff)
     for (int i = 0; i < 9; ++i) { r->Jf[i] = Jf[i]; r->Ji[i] = Ji[i]; }
   r->impl = impl; r->N = impl->N; r->M = impl->M;
+  {
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device) == hipSuccess) r->cus = cus;
+  }
   const size_t B = batch, N = r->N;
   if (r->x.alloc(sizeof(double) * B * R6_NX) || r->U.alloc(sizeof(double) * B * N * R6_NU) ||
       r->Xp.alloc(sizeof(double) * B * (N + 1) * R6_NX) || r->gm.alloc(sizeof(double) * B * N * 6) ||
@@ -187,7 +193,8 @@ static int r6_create(gpmpc_ctx *ctx, const GpView &gv, const GpView &gw, bool ex
       r->prm.alloc(sizeof(double) * R6_PRM) || r->xt.alloc(sizeof(double) * B * (N + 1) * R6_NX) ||
       r->ut.alloc(sizeof(double) * B * N * R6_NU) ||
       r->xin.alloc(sizeof(double) * B * R6_NX) || r->done.alloc(sizeof(int) * B) ||
-      r->passes.alloc(sizeof(int) * B) || r->qit.alloc(sizeof(int) * B) || r->qst.alloc(sizeof(int) * B)) {
+      r->passes.alloc(sizeof(int) * B) || r->qit.alloc(sizeof(int) * B) || r->qst.alloc(sizeof(int) * B) ||
+      r->gran.alloc(sizeof(unsigned long long) * (B * 2 * R6_GRAN + 2))) {
     delete r;
     gpmpc_set_error("rollout6: out of device memory");
     return -1;
@@ -205,6 +212,7 @@ static int r6_create(gpmpc_ctx *ctx, const GpView &gv, const GpView &gw, bool ex
   hipMemsetAsync(r->ut.p, 0, sizeof(double) * B * N * R6_NU, ctx->stream);
   hipMemsetAsync(r->pending.p, 0, sizeof(int) * B, ctx->stream);
   hipMemsetAsync(r->done.p, 0, sizeof(int) * B, ctx->stream);
+  hipMemsetAsync(r->gran.p, 0, sizeof(unsigned long long) * (B * 2 * R6_GRAN + 2), ctx->stream);
   if (!exact) {  // beta^T = alpha^T L_uu^-1: the FITC posterior mean's coefficients
     if (launch_gemm_nn(ctx->stream, 3, gv.n, gv.n, gv.alphaT, gv.n, gv.W, gv.n, r->betav.as<double>(), gv.n, 1.0,
                        0.0) != hipSuccess ||
@@ -237,6 +245,16 @@ extern "C" int gpmpc_rollout6_create_exact(gpmpc_ctx *ctx, gpmpc_gp *gp_v, gpmpc
   return r6_create(ctx, gp_view(gp_v), gp_view(gp_w), true, cfg, batch, out);
 }
 
+// Workgroups per rollout for the predict kernel: 4 when four per rollout fit the device
+// at once (one per CU: each needs a CU's whole register file), else 1.  The kernel rows
+// of a point are split by whole waves, so every split gives the same bits.
+// GPMPC_R6_SPLIT=0 keeps one workgroup per rollout (read at every step).
+static int r6_predict_parts(int B, int cus) {
+  const char *e = getenv("GPMPC_R6_SPLIT");
+  if (e && atoi(e) == 0) return 1;
+  return (cus > 0 && 4 * ((B + 7) / 8) * 8 <= cus) ? 4 : 1;
+}
+
 static R6Args r6_args(gpmpc_rollout6 *r) {
   R6Args a;
   a.st = to_dev(r->cfg.qp);
@@ -266,6 +284,9 @@ static R6Args r6_args(gpmpc_rollout6 *r) {
   a.rk.full = r->jfull;
   a.rk.alpha = c.rocket_alpha;
   a.rk.g0 = c.rocket_g0;
+  a.parts = r6_predict_parts(r->B, r->cus);
+  a.gran = r->gran.as<unsigned long long>();
+  a.tmo = (unsigned *)(a.gran + (size_t)r->B * 2 * R6_GRAN);
   return a;
 }
 
@@ -311,6 +332,18 @@ extern "C" int gpmpc_rollout6_step(gpmpc_rollout6 *r, int nsteps) {
   return 0;
 }
 
+static int r6_check_timeout(gpmpc_rollout6 *r) {
+  unsigned t = 0;
+  GPMPC_HIP(hipMemcpy(&t, r->gran.as<unsigned long long>() + (size_t)r->B * 2 * R6_GRAN, sizeof(t),
+                      hipMemcpyDeviceToHost));
+  if (t) {
+    gpmpc_set_error("rollout6: the split predict timed out waiting for its co-resident workgroups "
+                    "(set GPMPC_R6_SPLIT=0)");
+    return -1;
+  }
+  return 0;
+}
+
 extern "C" int gpmpc_rollout6_solve_ref(gpmpc_rollout6 *r, const double *x0, const double *x_target,
                                         const double *X_ref, const double *U_ref, int cold, int max_sqp_iter,
                                         double sqp_tol, double *X, double *U, int *passes, int *converged,
@@ -349,7 +382,7 @@ extern "C" int gpmpc_rollout6_solve_ref(gpmpc_rollout6 *r, const double *x0, con
   if (qp_status) GPMPC_HIP(hipMemcpyAsync(qp_status, r->qst.p, sizeof(int) * B, hipMemcpyDeviceToHost, s));
   if (qp_iters) GPMPC_HIP(hipMemcpyAsync(qp_iters, r->qit.p, sizeof(int) * B, hipMemcpyDeviceToHost, s));
   GPMPC_HIP(hipStreamSynchronize(s));
-  return 0;
+  return r6_check_timeout(r);
 }
 
 extern "C" int gpmpc_rollout6_solve(gpmpc_rollout6 *r, const double *x0, const double *x_target, int cold,
@@ -359,6 +392,8 @@ extern "C" int gpmpc_rollout6_solve(gpmpc_rollout6 *r, const double *x0, const d
                                   converged, qp_status, qp_iters);
 }
 
+// the split predict's sticky timeout word: a part that gave up waiting for its siblings
+// (they were not co-resident) leaves results that cannot be trusted
 extern "C" int gpmpc_rollout6_read(gpmpc_rollout6 *r, double *records, double *x) {
   GPMPC_CHECK_ARG(r);
   hipStream_t s = r->ctx->stream;
@@ -367,7 +402,7 @@ extern "C" int gpmpc_rollout6_read(gpmpc_rollout6 *r, double *records, double *x
                              hipMemcpyDeviceToHost, s));
   if (x) GPMPC_HIP(hipMemcpyAsync(x, r->x.p, sizeof(double) * r->B * R6_NX, hipMemcpyDeviceToHost, s));
   GPMPC_HIP(hipStreamSynchronize(s));
-  return 0;
+  return r6_check_timeout(r);
 }
 
 extern "C" int gpmpc_rollout6_get_state(gpmpc_rollout6 *r, double *U, double *X_plan, double *X_pred,

@@ -15,7 +15,7 @@ static_assert(R6_N >= 2, "the twisted factor needs a top and a bottom end");
 static_assert(R6_NV <= 2 * R6_T && R6_NV + R6_MD <= 2 * R6_T && R6_MGEN <= R6_T, "two items per thread");
 
 // diagnostic phase cycles of the predict kernel's rollout 0 (GPMPC_R6_STAMPS=1)
-__device__ unsigned long long g_r6p_stamps[4];
+__device__ unsigned long long g_r6p_stamps[8];
 
 // Per horizon point k (the points are sequential: X[k+1] needs the GP mean at X[k]):
 //   waves 0 .. R6_PT/64 - 2: the 2 x M kernel rows of both GPs (K*u . coefficients);
@@ -23,13 +23,46 @@ __device__ unsigned long long g_r6p_stamps[4];
 //   barrier; lanes 0 of waves 0 .. 5: the means, X[k+1] = RK4 + [.., d_v dt, .., d_w dt],
 //   then the six roles of point k+1's features (r6_features_role);
 //   barrier.
+// Split (a.parts > 1, r6_predict_parts): a rollout's kernel rows run on a.parts co-resident
+// workgroups, by whole waves (part p: waves [2p, min(2p + 2, 7)) of the 7 kernel-row
+// waves), each wave's six sums published as twelve tagged 8-byte granules {tag = point
+// + 1, one 32-bit word} with agent-scope (sc1) stores; one idle wave of every part polls
+// all 84 granules of the point until every tag matches (bounded: a.tmo on give-up) and
+// rebuilds the per-wave sums.  Every part then runs the same serial tail (means, RK4,
+// next features) on the same values, so all parts agree bit for bit with each other and
+// with the unsplit kernel; part 0 alone writes the outputs.  Two point parities per
+// rollout: a part writes point k + 2 only after every part has published point k + 1,
+// hence finished reading point k.
+__device__ __forceinline__ bool r6_spin_fail(unsigned &spins, unsigned *tmo, int lane) {
+  if (++spins < (1u << 20)) {
+    __builtin_amdgcn_s_sleep(2);
+    return false;
+  }
+  if (lane == 0) __hip_atomic_store(tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return true;
+}
+
 template <bool ST>
 __global__ __launch_bounds__(R6_PT) void k_r6_predict(R6Args a) {
-  const int b = blockIdx.x, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   constexpr int NW = R6_PT / 64, NRT = R6_PT - 64;  // waves; kernel-row threads
+  static_assert(NW == 8 && (NW - 1) * 12 == R6_GRAN, "seven kernel-row waves of twelve granules");
+  // the parts of a rollout on one XCD (blocks L and L + 8 share one): block L is part
+  // (L / 8) % parts of rollout (L / 8 / parts) * 8 + L % 8
+  int b = blockIdx.x, part = 0;
+  if (a.parts > 1) {
+    const int m = (int)blockIdx.x >> 3;
+    b = (m / a.parts) * 8 + ((int)blockIdx.x & 7);
+    part = m % a.parts;
+    if (b >= a.nb) return;
+  }
+  const bool out_here = part == 0;               // the part that writes the outputs
+  const int wlo = 2 * part, whi = min(2 * part + 2, NW - 1);
+  const int poller = wlo > 0 ? 0 : NW - 2;       // a kernel-row wave idle in this part
+  const unsigned long long t_start = ST ? __builtin_amdgcn_s_memtime() : 0;
   unsigned long long tl = 0;
   auto mark = [&](int k) {
-    if (ST && b == 0 && tid == 0) {
+    if (ST && b == 0 && out_here && tid == 0) {
       const unsigned long long t = __builtin_amdgcn_s_memtime();
       if (k >= 0) g_r6p_stamps[k] += t - tl;
       tl = t;
@@ -41,6 +74,7 @@ __global__ __launch_bounds__(R6_PT) void k_r6_predict(R6Args a) {
   __shared__ double zq[2][16];
   __shared__ double red[NW][6];
   __shared__ double xrk[R6_NX];
+  __shared__ unsigned gwords[R6_GRAN];
   __shared__ int s_out;
   const double dt = a.dt;
   const bool relin = a.mode == 2;  // a later GPMPC.solve pass: X_pred = the last plan
@@ -65,7 +99,7 @@ __global__ __launch_bounds__(R6_PT) void k_r6_predict(R6Args a) {
     else if (div7) out = 6;
     else if (x[1] < 1.0 && fabs(x[4]) < 5.0) out = r6_landing_ok(x, m0) ? 1 : 4;
     else if (div) out = 6;
-    if (out) {
+    if (out && out_here) {
       rec[0] = out;
       rec[2] = m0 - x[0];
       for (int i = 0; i < 7; ++i) rec[4 + i] = x[i];
@@ -92,26 +126,66 @@ __global__ __launch_bounds__(R6_PT) void k_r6_predict(R6Args a) {
     }
   }
   __syncthreads();
+  if (ST && b == 0 && out_here && tid == 0) g_r6p_stamps[3] += __builtin_amdgcn_s_memtime() - t_start;
   mark(-1);
   for (int k = 0; k < R6_N; ++k) {
     // K*u . coefficients of both GPs: the expansion form of the gram kernel (same
     // bits per kernel value); 3 outputs each
     double acc[6] = {0, 0, 0, 0, 0, 0};
     if (tid < NRT) {
-      if (a.use_gp) {
-        r6_kernel_rows<13>(a.gv, a.Mv, a.cv, zq[0], tid, NRT, acc, sxv, a.mcv);
-        r6_kernel_rows<12>(a.gw, a.Mw, a.cw, zq[1], tid, NRT, acc + 3, sxw, a.mcw);
+      if (a.parts == 1 || (wave >= wlo && wave < whi)) {
+        const unsigned long long tr0 = ST ? __builtin_amdgcn_s_memtime() : 0;
+        if (a.use_gp) {
+          r6_kernel_rows<13>(a.gv, a.Mv, a.cv, zq[0], tid, NRT, acc, sxv, a.mcv);
+          r6_kernel_rows<12>(a.gw, a.Mw, a.cw, zq[1], tid, NRT, acc + 3, sxw, a.mcw);
+        }
+#pragma unroll
+        for (int c = 0; c < 6; ++c)
+#pragma unroll
+          for (int o = 32; o > 0; o >>= 1) acc[c] += __shfl_xor(acc[c], o);
+        if (ST && b == 0 && out_here && tid == 0) g_r6p_stamps[5] += __builtin_amdgcn_s_memtime() - tr0;
+        if (a.parts == 1) {
+          if (lane == 0)
+#pragma unroll
+            for (int c = 0; c < 6; ++c) red[wave][c] = acc[c];
+        } else if (lane < 12) {  // every lane holds the sums: lane 2c + h publishes word h of sum c
+          double v = acc[0];
+#pragma unroll
+          for (int c = 1; c < 6; ++c) v = (lane >> 1) == c ? acc[c] : v;
+          const unsigned wd = (lane & 1) ? (unsigned)__double2hiint(v) : (unsigned)__double2loint(v);
+          unsigned long long *g = a.gran + ((size_t)b * 2 + (k & 1)) * R6_GRAN + wave * 12 + lane;
+          __hip_atomic_store(g, ((unsigned long long)(k + 1) << 32) | wd, __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+        }
+      } else if (wave == poller) {  // every wave's granules of point k, this part's included
+        const unsigned long long *g = a.gran + ((size_t)b * 2 + (k & 1)) * R6_GRAN;
+        const unsigned tag = (unsigned)(k + 1);
+        const bool two = lane + 64 < R6_GRAN;
+        unsigned long long x0, x1;
+        const unsigned long long tp0 = ST ? __builtin_amdgcn_s_memtime() : 0;
+        for (unsigned spins = 0;;) {
+          x0 = __hip_atomic_load(g + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          x1 = two ? __hip_atomic_load(g + lane + 64, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                   : ((unsigned long long)tag << 32);
+          if (__all((unsigned)(x0 >> 32) == tag && (unsigned)(x1 >> 32) == tag)) break;
+          if (r6_spin_fail(spins, a.tmo, lane)) break;
+        }
+        if (ST && b == 0 && out_here && lane == 0) g_r6p_stamps[6] += __builtin_amdgcn_s_memtime() - tp0;
+        gwords[lane] = (unsigned)x0;
+        if (two) gwords[lane + 64] = (unsigned)x1;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        if (lane < (NW - 1) * 6) {
+          const int w = lane / 6, c = lane - 6 * (lane / 6);
+          red[w][c] = __hiloint2double((int)gwords[w * 12 + 2 * c + 1], (int)gwords[w * 12 + 2 * c]);
+        }
       }
-#pragma unroll
-      for (int c = 0; c < 6; ++c)
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) acc[c] += __shfl_xor(acc[c], o);
-      if (lane == 0)
-#pragma unroll
-        for (int c = 0; c < 6; ++c) red[wave][c] = acc[c];
     } else if (!relin && lane == 0) {  // _predict_with_gp's nominal step (gp_mpc.py:156)
       double xn[R6_NX];
+      const unsigned long long t0 = ST ? __builtin_amdgcn_s_memtime() : 0;
       r6_step(a.rk, X[k], Ub + k * R6_NU, dt, xn);
+      if (ST && b == 0 && out_here) g_r6p_stamps[2] += __builtin_amdgcn_s_memtime() - t0;
       for (int i = 0; i < R6_NX; ++i) xrk[i] = xn[i];
     }
     __syncthreads();
@@ -132,7 +206,8 @@ __global__ __launch_bounds__(R6_PT) void k_r6_predict(R6Args a) {
         for (int i = 0; i < 3; ++i) { xn[4 + i] += gmk[i] * dt; xn[11 + i] += gmk[3 + i] * dt; }
       }
       if (wave == 0) {
-        for (int c = 0; c < 6; ++c) a.gm[((int64_t)b * R6_N + k) * 6 + c] = gmk[c];
+        if (out_here)
+          for (int c = 0; c < 6; ++c) a.gm[((int64_t)b * R6_N + k) * 6 + c] = gmk[c];
         if (!relin)
           for (int i = 0; i < R6_NX; ++i) X[k + 1][i] = xn[i];
       }
@@ -142,6 +217,7 @@ __global__ __launch_bounds__(R6_PT) void k_r6_predict(R6Args a) {
     __syncthreads();
     mark(0);
   }
+  if (!out_here) return;
   for (int e = tid; e < (R6_N + 1) * R6_NX; e += R6_PT)
     a.Xp[(int64_t)b * (R6_N + 1) * R6_NX + e] = (&X[0][0])[e];
   // linearisation at the simulated points (gp_mpc.py:303-304): -[A_d | B_d] per stage
@@ -149,6 +225,10 @@ __global__ __launch_bounds__(R6_PT) void k_r6_predict(R6Args a) {
   for (int e = tid; e < R6_N * R6_NX * R6_SZ; e += R6_PT) lin[e] = 0.0;
   __syncthreads();
   if (tid < R6_N) r6_neg_lin(a.rk, X[tid], Ub + tid * R6_NU, dt, lin + tid * R6_NX * R6_SZ);
+  if (ST && b == 0) {
+    __syncthreads();
+    if (tid == 0) g_r6p_stamps[4] += __builtin_amdgcn_s_memtime() - tl;
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -1408,9 +1488,20 @@ static void r6_launch_predict(hipStream_t s, int B, const R6Args &a0, bool st) {
   const int c = (attr && a.use_gp) ? max(0, min(cap, R6_PCACHE_ROWS)) : 0;
   a.mcv = min(a.Mv, c);
   a.mcw = min(a.Mw, c);
+  a.nb = B;
+  if (!a.use_gp) a.parts = 1;  // (no kernel rows to split)
   const size_t lds = sizeof(double) * (size_t)(a.mcv * 13 + a.mcw * 12);
-  if (st) hipLaunchKernelGGL(k_r6_predict<true>, dim3(B), dim3(R6_PT), lds, s, a);
-  else hipLaunchKernelGGL(k_r6_predict<false>, dim3(B), dim3(R6_PT), lds, s, a);
+  if (a.parts > 1) {
+    // every granule zeroed before the launch (the timeout word behind them is sticky: zeroed
+    // at creation, read by gpmpc_rollout6_read / _solve)
+    (void)hipMemsetAsync(a.gran, 0, sizeof(unsigned long long) * (size_t)B * 2 * R6_GRAN, s);
+    if (st) hipLaunchKernelGGL(k_r6_predict<true>, dim3((B + 7) / 8 * 8 * a.parts), dim3(R6_PT), lds, s, a);
+    else hipLaunchKernelGGL(k_r6_predict<false>, dim3((B + 7) / 8 * 8 * a.parts), dim3(R6_PT), lds, s, a);
+  } else if (st) {
+    hipLaunchKernelGGL(k_r6_predict<true>, dim3(B), dim3(R6_PT), lds, s, a);
+  } else {
+    hipLaunchKernelGGL(k_r6_predict<false>, dim3(B), dim3(R6_PT), lds, s, a);
+  }
 }
 static void r6_launch_control(hipStream_t s, int B, const R6Args &a, bool st) {
   if (st) hipLaunchKernelGGL(k_r6_control<true>, dim3(B), dim3(R6_T), sizeof(R6Smem), s, a);
@@ -1437,10 +1528,11 @@ static void r6_print_stamps() {  // diagnostic: phase cycles of rollout 0, summe
       fprintf(stderr, "r6 stamps N=%d %-14s %12llu cycles %5.1f%%\n", R6_N, nm[k], h[k],
               tot ? 100.0 * h[k] / tot : 0.0);
   }
-  unsigned long long hp[4] = {0};
+  unsigned long long hp[8] = {0};
   if (hipMemcpyFromSymbol(hp, HIP_SYMBOL(g_r6p_stamps), sizeof(hp)) == hipSuccess)
-    fprintf(stderr, "r6 predict stamps N=%d: kernel rows + rk4 %llu means + next features %llu\n", R6_N, hp[1],
-            hp[0]);
+    fprintf(stderr, "r6 predict stamps N=%d: start %llu, kernel rows + rk4 %llu means + next features %llu "
+            "(rk4 alone %llu), end (states, Jacobians) %llu; part-0 wave-0 rows %llu, poll %llu\n", R6_N, hp[3], hp[1],
+            hp[0], hp[2], hp[4], hp[5], hp[6]);
 }
 // (a host function, not a namespace-scope object: the device pass would emit the object
 // with references to these host launchers)

@@ -224,3 +224,40 @@ def test_rollouts6_rejects_nonpositive_max_iter(gpu_ctx):
     gv, gw = fit_structured_fitc(gpu_ctx, n_train=120, n_inducing=20)
     with pytest.raises(_lib.HIPError, match="max_iter must be positive"):
         Rollouts6(gpu_ctx, gv, gw, 2, max_iter=0)
+
+
+@pytest.mark.gpu
+def test_rollouts6_split_predict_is_bit_identical(gpu_ctx, monkeypatch):
+    """The predict kernel's split (each rollout's kernel rows over four co-resident
+    workgroups, per-wave sums exchanged as tagged granules; on by default when four
+    workgroups per rollout fit the device) gives the same bits as one workgroup per
+    rollout (GPMPC_R6_SPLIT=0): the rows are split by whole waves and every part sums
+    the same per-wave values in the same order.  M = 1000 inducing rows: past the LDS
+    row cache, so both the LDS and the global row paths run; the Monte-Carlo steps and
+    a GPMPC.solve loop (modes 1 and 2) both checked."""
+    from gp_mpc_rocket_landing_amd.rollouts6 import Rollouts6, fit_structured_fitc, initial_conditions_6dof
+    gv, gw = fit_structured_fitc(gpu_ctx, n_train=2000, n_inducing=1000)
+
+    def fly(split):
+        monkeypatch.setenv("GPMPC_R6_SPLIT", "1" if split else "0")
+        r = Rollouts6(gpu_ctx, gv, gw, 64)
+        try:
+            x0 = initial_conditions_6dof(64)
+            r.reset(x0)
+            r.step(6)
+            rec, x = r.read()
+            st = r.state()
+            tgt = np.zeros_like(x0)
+            tgt[:, 0] = x0[:, 0]
+            sol = r.solve(x0, tgt, cold=1, max_sqp_iter=3)
+            return rec, x, st, sol
+        finally:
+            r.close()
+
+    a, b = fly(True), fly(False)
+    np.testing.assert_array_equal(a[0], b[0])
+    np.testing.assert_array_equal(a[1], b[1])
+    for k in a[2]:
+        np.testing.assert_array_equal(a[2][k], b[2][k], err_msg=k)
+    for k in a[3]:
+        np.testing.assert_array_equal(a[3][k], b[3][k], err_msg=k)
