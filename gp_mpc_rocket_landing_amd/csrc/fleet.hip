@@ -1464,4 +1464,143 @@ extern "C" int gpmpc_fleet_destroy(gpmpc_fleet *f) {
   return 0;
 }
 
+
+// ---------------------------------------------------------------------------
+// UncertaintyPropagator._propagate_linear (uncertainty_prop.py:117-177) for the 3-DoF model
+// on the device, batch trajectories at once (gpmpc_uprop3_linear).  The mean recursion is
+// sequential -- x_k+1 needs the GP mean at x_k -- so one workgroup per trajectory walks the
+// N steps: the query's features (features3, the fleet's), the exact GP mean over the n
+// training rows (256 threads, a fixed-order block reduction), the explicit-Euler step of
+// rocket_3dof.py (x + dt f, f = [-alpha |u|, v, u / m + g], products and sums unfused as
+// numpy forms them) plus dt d_v on the velocity rows, and A_k = I + dt J(x_k, u_k).  The
+// variances of all B N queries then come from the GP's own batched posterior, and one
+// launch propagates every covariance (k_cov_propagate).
+__global__ __launch_bounds__(256) void k_uprop3_means(GpView g, int N, double dt, double alpha, double g0,
+                                                      double g1, double g2, const double *__restrict__ x0,
+                                                      const double *__restrict__ U, double *__restrict__ Q,
+                                                      double *__restrict__ A, double *__restrict__ means) {
+  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  __shared__ double sx[NX], sz[NFEAT], szn, red[4][3], sm[3];
+  if (tid < NX) {
+    sx[tid] = x0[(int64_t)b * NX + tid];
+    means[(int64_t)b * (N + 1) * NX + tid] = sx[tid];
+  }
+  __syncthreads();
+  for (int k = 0; k < N; ++k) {
+    const double *u = U + ((int64_t)b * N + k) * NU;
+    if (tid == 0) {
+      double z[NFEAT];
+      features3(sx, u, z);
+      double sn = 0.0;
+      for (int f = 0; f < NFEAT; ++f) {
+        Q[((int64_t)b * N + k) * NFEAT + f] = z[f];
+        const double v = g.kind == GPMPC_SE_ISO ? z[f] : z[f] / g.ls[f];
+        sz[f] = v;
+        sn += v * v;
+      }
+      szn = sn;
+      // A_k = I + dt J: J[1:4, 4:7] = I, J[4:7, 0] = -u / m^2 (rocket_3dof.py jacobian_x)
+      double *Ak = A + ((int64_t)b * N + k) * NX * NX;
+      for (int e = 0; e < NX * NX; ++e) Ak[e] = (e % (NX + 1) == 0) ? 1.0 : 0.0;
+      for (int i = 0; i < 3; ++i) Ak[(1 + i) * NX + 4 + i] = __dmul_rn(1.0, dt);
+      const double m2 = __dmul_rn(sx[0], sx[0]);
+      for (int i = 0; i < 3; ++i) Ak[(4 + i) * NX] = __dmul_rn(-u[i] / m2, dt);
+    }
+    __syncthreads();
+    double acc[3] = {0.0, 0.0, 0.0};
+    const double zn = szn;
+    for (int j = tid; j < g.n; j += 256) {
+      double dot = 0.0;
+#pragma unroll
+      for (int f = 0; f < NFEAT; ++f) dot = fma(sz[f], g.Xs[(int64_t)j * NFEAT + f], dot);
+      const double kv = kernel_epilogue(g.kind, (zn + g.Xn[j]) - 2.0 * dot, g.sigma2, g.iso_scale);
+#pragma unroll
+      for (int c = 0; c < 3; ++c) acc[c] = fma(kv, g.alphaT[(int64_t)c * g.n + j], acc[c]);
+    }
+#pragma unroll
+    for (int c = 0; c < 3; ++c)
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) acc[c] += __shfl_xor(acc[c], o);
+    if (lane == 0)
+      for (int c = 0; c < 3; ++c) red[wave][c] = acc[c];
+    __syncthreads();
+    if (tid == 0) {
+      double dv[3];
+      for (int c = 0; c < 3; ++c) {
+        const double m = ((red[0][c] + red[1][c]) + red[2][c]) + red[3][c];
+        dv[c] = __dadd_rn(__dmul_rn(m, g.ystd[c]), g.ymean[c]);
+      }
+      // x + dt f(x, u), then + d_v dt on the velocity rows
+      const double um = sqrt(__dadd_rn(__dadd_rn(__dmul_rn(u[0], u[0]), __dmul_rn(u[1], u[1])), __dmul_rn(u[2], u[2])));
+      double f[NX];
+      f[0] = __dmul_rn(-alpha, um);
+      f[1] = sx[4]; f[2] = sx[5]; f[3] = sx[6];
+      f[4] = __dadd_rn(u[0] / sx[0], g0); f[5] = __dadd_rn(u[1] / sx[0], g1); f[6] = __dadd_rn(u[2] / sx[0], g2);
+      double xn[NX];
+      for (int i = 0; i < NX; ++i) xn[i] = __dadd_rn(sx[i], __dmul_rn(dt, f[i]));
+      for (int c = 0; c < 3; ++c) xn[4 + c] = __dadd_rn(xn[4 + c], __dmul_rn(dv[c], dt));
+      for (int i = 0; i < NX; ++i) {
+        sx[i] = xn[i];
+        means[((int64_t)b * (N + 1) + k + 1) * NX + i] = xn[i];
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// q_k = var dt^2 on the velocity rows (uncertainty_prop.py:160-161)
+__global__ void k_uprop3_q(int P, double dt2, const double *__restrict__ var, double *__restrict__ q) {
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= P) return;
+  for (int i = 0; i < NX; ++i) q[(int64_t)j * NX + i] = (i >= 4) ? __dmul_rn(var[(int64_t)j * 3 + i - 4], dt2) : 0.0;
+}
+
+extern "C" int gpmpc_uprop3_linear(gpmpc_ctx *ctx, gpmpc_gp *gp, int batch, int N, double dt, double alpha,
+                                   const double *g3, const double *x0, const double *U, const double *S0,
+                                   double s0_diag, double *means, double *covs) {
+  GPMPC_CHECK_ARG(ctx && gp && g3 && x0 && U && means && covs && batch >= 0 && N >= 0);
+  const GpView g = gp_view(gp);
+  if (g.d != NFEAT || g.n_out != 3 || g.kind == GPMPC_KPROG) {
+    gpmpc_set_error("uprop3_linear: needs the 3-DoF exact GP (11 features, 3 outputs, a leaf kernel)");
+    return -2;
+  }
+  if (batch == 0) return 0;
+  GPMPC_HIP(hipSetDevice(ctx->device));
+  hipStream_t s = ctx->stream;
+  const size_t B = batch, P = B * N;
+  DevBuf dx0, dU, dQ, dA, dmeans, dq, dvar, dmu, dS0, dcov;
+  GPMPC_HIP(dx0.alloc(s, sizeof(double) * B * NX));
+  GPMPC_HIP(dU.alloc(s, sizeof(double) * (P * NU + 1)));
+  GPMPC_HIP(dQ.alloc(s, sizeof(double) * (P * NFEAT + 1)));
+  GPMPC_HIP(dA.alloc(s, sizeof(double) * (P * NX * NX + 1)));
+  GPMPC_HIP(dq.alloc(s, sizeof(double) * (P * NX + 1)));
+  GPMPC_HIP(dmeans.alloc(s, sizeof(double) * B * (N + 1) * NX));
+  GPMPC_HIP(dcov.alloc(s, sizeof(double) * B * (N + 1) * NX * NX));
+  GPMPC_HIP(hipMemcpyAsync(dx0.p, x0, sizeof(double) * B * NX, hipMemcpyHostToDevice, s));
+  if (P) GPMPC_HIP(hipMemcpyAsync(dU.p, U, sizeof(double) * P * NU, hipMemcpyHostToDevice, s));
+  if (S0) {
+    GPMPC_HIP(dS0.alloc(s, sizeof(double) * B * NX * NX));
+    GPMPC_HIP(hipMemcpyAsync(dS0.p, S0, sizeof(double) * B * NX * NX, hipMemcpyHostToDevice, s));
+  }
+  hipLaunchKernelGGL(k_uprop3_means, dim3(batch), dim3(256), 0, s, g, N, dt, alpha, g3[0], g3[1], g3[2],
+                     dx0.as<double>(), dU.as<double>(), dQ.as<double>(), dA.as<double>(), dmeans.as<double>());
+  GPMPC_HIP(hipGetLastError());
+  if (P) {
+    GPMPC_HIP(dmu.alloc(s, sizeof(double) * P * 3));
+    GPMPC_HIP(dvar.alloc(s, sizeof(double) * P * 3));
+    const int rc = gp_posterior_dev(ctx, gp, dQ.as<double>(), (int)P, dmu.as<double>(), dvar.as<double>());
+    if (rc) return rc;
+    hipLaunchKernelGGL(k_uprop3_q, dim3((unsigned)((P + 255) / 256)), dim3(256), 0, s, (int)P, dt * dt,
+                       dvar.as<double>(), dq.as<double>());
+    GPMPC_HIP(hipGetLastError());
+  }
+  const int rc = gpmpc_cov_propagate_dev(ctx, batch, N, NX, dA.as<double>(), dq.as<double>(),
+                                         S0 ? dS0.as<double>() : nullptr, s0_diag, dcov.as<double>());
+  if (rc) return rc;
+  GPMPC_HIP(hipMemcpyAsync(means, dmeans.p, sizeof(double) * B * (N + 1) * NX, hipMemcpyDeviceToHost, s));
+  GPMPC_HIP(hipMemcpyAsync(covs, dcov.p, sizeof(double) * B * (N + 1) * NX * NX, hipMemcpyDeviceToHost, s));
+  GPMPC_HIP(hipStreamSynchronize(s));
+  return 0;
+}
+
 #endif  // FLEET_WIDE_TU

@@ -700,6 +700,15 @@ static int core_posterior(gpmpc_ctx *ctx, const GpCore &g, const double *Ks, int
   return 0;
 }
 
+// the posterior of p device-resident raw query rows (p x d): device mean / var (p x n_out)
+int gp_posterior_dev(gpmpc_ctx *ctx, gpmpc_gp *gp, const double *dq, int p, double *dmean, double *dvar) {
+  const GpCore &g = gp->core;
+  DevBuf Ks;
+  const int rc = core_cross(ctx, g, dq, p, Ks);
+  if (rc) return rc;
+  return core_posterior(ctx, g, Ks.as<double>(), p, dmean, dvar);
+}
+
 extern "C" int gpmpc_gp_predict(gpmpc_ctx *ctx, gpmpc_gp *gp, const double *Xq, int p,
                                 double *mean, double *var) {
   GPMPC_CHECK_ARG(ctx && gp && Xq && mean && var && p >= 0);

@@ -89,6 +89,36 @@ class UncertaintyPropagator:
             return self._propagate_monte_carlo(x0, U, Sigma_0, dt)
         raise ValueError(f"Unknown method: {self.method}")
 
+    # the whole linear propagation in one device call (gpmpc_uprop3_linear) for the 3-DoF
+    # explicit-Euler model over the 3-DoF exact GP: the N sequential GP predictions of the
+    # host loop below become one kernel; the same recursion, rounding aside
+    use_device = True
+
+    def _device_3dof(self, X0, U, Sigma_0, dt):
+        if not self.use_device or self.n_x != 7:
+            return None
+        from ..dynamics.rocket_3dof import Rocket3DoFDynamics
+        from ..gp.exact_gp import MultiOutputExactGP
+        from ..gp.features import Simple3DoFFeatureExtractor
+        gp = self.gp
+        inner = getattr(gp, "gp", None)
+        # (only the exact GP's handle is a gpmpc_gp; a FITC handle is another type)
+        if (type(self.dynamics) is not Rocket3DoFDynamics or not isinstance(inner, MultiOutputExactGP)
+                or type(getattr(gp, "feature_extractor", None)) is not Simple3DoFFeatureExtractor
+                or not getattr(gp, "_is_fitted", False)):
+            return None
+        h = inner.device_handle
+        if h is None:
+            return None
+        p = self.dynamics.params
+        S0 = None
+        if Sigma_0 is not None:
+            S0 = np.broadcast_to(np.asarray(Sigma_0, float), (X0.shape[0], 7, 7))
+        try:
+            return _lib.uprop3_linear(self.ctx, h, X0, U, S0, dt, float(p.alpha), np.asarray(p.g_vec, float))
+        except _lib.HIPError:
+            return None   # (a composite-kernel GP: the host loop)
+
     # ------------------------------------------------------------------ linear
     def _propagate_linear(self, x0, U, Sigma_0, dt) -> PropagatedUncertainty:
         """uncertainty_prop.py:117-177 for one trajectory (a batch of one)."""
@@ -111,6 +141,9 @@ class UncertaintyPropagator:
         nx = self.n_x
         if X0.shape != (B, nx):
             raise ValueError(f"X0 shape {X0.shape}, expected {(B, nx)}")
+        dev = self._device_3dof(X0, U, Sigma_0, dt)
+        if dev is not None:
+            return dev
         rv, rw = self._rows()
         means = np.zeros((B, N + 1, nx)); means[:, 0] = X0
         A = np.zeros((B, N, nx, nx)); q = np.zeros((B, N, nx))

@@ -337,6 +337,18 @@ int gpmpc_cov_propagate(gpmpc_ctx *ctx, int batch, int N, int nx, const double *
                         const double *S0, double s0_diag, double *out);
 int gpmpc_cov_propagate_dev(gpmpc_ctx *ctx, int batch, int N, int nx, const double *dA,
                             const double *dq, const double *dS0, double s0_diag, double *dout);
+/* UncertaintyPropagator._propagate_linear (uncertainty_prop.py:117-177) of the 3-DoF model
+ * on the device, for batch trajectories in one call (what GPMPC.solve runs on every call,
+ * gp_mpc.py:284-290, with N sequential GP predictions on the host): the explicit-Euler
+ * dynamics of rocket_3dof.py (x+ = x + dt f, f = [-alpha |u|, v, u / m + g3]) plus dt times
+ * the exact GP's mean on the velocity rows, A_k = I + dt J(x_k, u_k), q_k = dt^2 times the
+ * GP variance on the velocity rows, Sigma_0 = S0 (batch x 7 x 7) or s0_diag I.  gp: the
+ * 3-DoF exact GP (11 features, 3 outputs, a leaf kernel; else -2).  Host buffers: x0
+ * (batch x 7), U (batch x N x 3) in; means (batch x (N+1) x 7), covs (batch x (N+1) x 7 x 7)
+ * out.  (Round 6, ABI 4: an added entry point.) */
+int gpmpc_uprop3_linear(gpmpc_ctx *ctx, gpmpc_gp *gp, int batch, int N, double dt, double alpha,
+                        const double *g3, const double *x0, const double *U, const double *S0,
+                        double s0_diag, double *means, double *covs);
 
 /* ---- BASELINE configs[4]: batched 6-DoF GP-MPC rollouts --------------------
  * gpmpc_rollout_batched of SURVEY 8b.  One step = for every running rollout:

@@ -130,3 +130,56 @@ def test_simple_gp_predictor_rollout_vs_f9(gpu_ctx):
     assert Dm.shape == (10, 14) and np.all(Dv[:, [0, 1, 2, 3, 7, 8, 9, 10]] == 0)
     np.testing.assert_allclose(np.diff(X, axis=0)[:, 4:7] - (np.array([ToyRocket14().step(X[k], f9["U"][k], 0.1) for k in range(10)]) - X[:-1])[:, 4:7],
                                Dm[:, 4:7] * 0.1, rtol=1e-9, atol=1e-12)
+
+
+@pytest.mark.parametrize("B,N,s0", [(16, 20, False), (3, 20, True), (2, 0, False), (1, 1, True)])
+def test_propagate_batch_3dof_device_vs_host_loop(gpu_ctx, monkeypatch, B, N, s0):
+    """gpmpc_uprop3_linear (the whole 3-DoF linear propagation in one device call) vs
+    the per-step host loop over the same GP handle: the same recursion, equal up to
+    the GP mean's summation order -- alpha . k over 1000 rows cancels, so 1e-15 of the
+    terms reaches the residual at ~1e-12 absolute, carried through N steps."""
+    _ctx_default(gpu_ctx)
+    from gp_mpc_rocket_landing_amd import _lib
+    from gp_mpc_rocket_landing_amd.dynamics import create_normalized_rocket
+    from gp_mpc_rocket_landing_amd.gp import Simple3DoFGP
+    from gp_mpc_rocket_landing_amd.mpc import UncertaintyPropagator
+    f1 = golden("f1_exact_simple3dof.npz")
+    gp = Simple3DoFGP(use_sparse=False)
+    gp.add_data(f1["X"], f1["U"], f1["D"]); gp.fit()
+    dyn = create_normalized_rocket()
+    rs = np.random.RandomState(B * 10 + N)
+    X0 = f1["X"][:B] + 0.01 * rs.randn(B, 7)
+    U = np.repeat(f1["U"][:B, None, :], N, axis=1) * (1 + 0.05 * rs.randn(B, N, 1))
+    S0 = None
+    if s0:
+        L = rs.randn(B, 7, 7) * 1e-3
+        S0 = np.einsum("bij,bkj->bik", L, L)
+    calls = []
+    real = _lib.uprop3_linear
+    monkeypatch.setattr(_lib, "uprop3_linear", lambda *a, **k: calls.append(1) or real(*a, **k))
+    p = UncertaintyPropagator(dyn, gp, ctx=gpu_ctx)
+    md, cd = p.propagate_batch(X0, U, S0, 0.1)
+    assert calls, "the device path was not taken"
+    p.use_device = False
+    mh, ch = p.propagate_batch(X0, U, S0, 0.1)
+    assert len(calls) == 1
+    assert md.shape == (B, N + 1, 7) and cd.shape == (B, N + 1, 7, 7)
+    np.testing.assert_array_equal(md[:, 0], X0)
+    np.testing.assert_allclose(md, mh, rtol=1e-10, atol=1e-10)
+    np.testing.assert_allclose(cd, ch, rtol=1e-7, atol=1e-15)
+
+
+def test_propagate_3dof_sparse_gp_stays_on_host_loop(gpu_ctx, monkeypatch):
+    """A FITC Simple3DoFGP has no exact device handle: the host loop runs."""
+    _ctx_default(gpu_ctx)
+    from gp_mpc_rocket_landing_amd import _lib
+    from gp_mpc_rocket_landing_amd.dynamics import create_normalized_rocket
+    from gp_mpc_rocket_landing_amd.gp import Simple3DoFGP
+    from gp_mpc_rocket_landing_amd.mpc import UncertaintyPropagator
+    f1 = golden("f1_exact_simple3dof.npz")
+    gp = Simple3DoFGP(use_sparse=True)
+    gp.add_data(f1["X"], f1["U"], f1["D"]); gp.fit()
+    monkeypatch.setattr(_lib, "uprop3_linear", lambda *a, **k: pytest.fail("device path on a sparse GP"))
+    m, c = UncertaintyPropagator(create_normalized_rocket(), gp, ctx=gpu_ctx).propagate_batch(
+        f1["X"][:2], np.repeat(f1["U"][:2, None], 5, axis=1), None, 0.1)
+    assert m.shape == (2, 6, 7) and np.all(np.isfinite(c))
