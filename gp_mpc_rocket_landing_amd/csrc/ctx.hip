@@ -39,6 +39,26 @@ void *gpmpc_scratch(hipStream_t s, int slot, size_t bytes) {
   return e.p;
 }
 
+// Pinned host arena of a stream's Stage (internal.h), grown like the scratch slots.
+struct StageHost { char *p = nullptr; size_t bytes = 0; };
+static std::map<hipStream_t, StageHost> g_stage;
+
+char *gpmpc_stage_host(hipStream_t s, size_t bytes) {
+  std::lock_guard<std::mutex> lk(g_scratch_mu);
+  StageHost &e = g_stage[s];
+  if (e.bytes < bytes) {
+    (void)hipStreamSynchronize(s);  // a copy on this stream may still read or fill it
+    if (e.p) (void)hipHostFree(e.p);
+    e.p = nullptr;
+    e.bytes = 0;
+    void *p = nullptr;
+    if (hipHostMalloc(&p, bytes, hipHostMallocDefault) != hipSuccess) return nullptr;
+    e.p = (char *)p;
+    e.bytes = bytes;
+  }
+  return e.p;
+}
+
 // ---- per-stream caching pool (internal.h) ------------------------------------
 // Each stream's pool carries a generation: a context's destruction ends its pool,
 // and a later context whose stream handle happens to have the same value starts a
@@ -154,6 +174,11 @@ static void pool_release(hipStream_t s) {
 
 static void scratch_release(hipStream_t s) {
   std::lock_guard<std::mutex> lk(g_scratch_mu);
+  auto st = g_stage.find(s);
+  if (st != g_stage.end()) {
+    if (st->second.p) (void)hipHostFree(st->second.p);
+    g_stage.erase(st);
+  }
   auto it = g_scratch.find(s);
   if (it == g_scratch.end()) return;
   for (ScratchSlot &e : it->second)
@@ -187,6 +212,7 @@ extern "C" int gpmpc_ctx_destroy(gpmpc_ctx *ctx) {
   (void)hipSetDevice(ctx->device);
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
   if (ctx->stream) scratch_release(ctx->stream);
+  if (ctx->stream) gpmpc_qp_cache_release(ctx->stream);
   if (ctx->stream) pool_release(ctx->stream);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx;

@@ -1568,22 +1568,24 @@ extern "C" int gpmpc_uprop3_linear(gpmpc_ctx *ctx, gpmpc_gp *gp, int batch, int 
   GPMPC_HIP(hipSetDevice(ctx->device));
   hipStream_t s = ctx->stream;
   const size_t B = batch, P = B * N;
-  DevBuf dx0, dU, dQ, dA, dmeans, dq, dvar, dmu, dS0, dcov;
-  GPMPC_HIP(dx0.alloc(s, sizeof(double) * B * NX));
-  GPMPC_HIP(dU.alloc(s, sizeof(double) * (P * NU + 1)));
+  DevBuf dQ, dA, dq, dvar, dmu;
   GPMPC_HIP(dQ.alloc(s, sizeof(double) * (P * NFEAT + 1)));
   GPMPC_HIP(dA.alloc(s, sizeof(double) * (P * NX * NX + 1)));
   GPMPC_HIP(dq.alloc(s, sizeof(double) * (P * NX + 1)));
-  GPMPC_HIP(dmeans.alloc(s, sizeof(double) * B * (N + 1) * NX));
-  GPMPC_HIP(dcov.alloc(s, sizeof(double) * B * (N + 1) * NX * NX));
-  GPMPC_HIP(hipMemcpyAsync(dx0.p, x0, sizeof(double) * B * NX, hipMemcpyHostToDevice, s));
-  if (P) GPMPC_HIP(hipMemcpyAsync(dU.p, U, sizeof(double) * P * NU, hipMemcpyHostToDevice, s));
-  if (S0) {
-    GPMPC_HIP(dS0.alloc(s, sizeof(double) * B * NX * NX));
-    GPMPC_HIP(hipMemcpyAsync(dS0.p, S0, sizeof(double) * B * NX * NX, hipMemcpyHostToDevice, s));
+  // inputs in one pinned upload, means and covariances in one read-back
+  const size_t bytes = Stage::pad(8 * B * NX) + Stage::pad(8 * P * NU) + (S0 ? Stage::pad(8 * B * NX * NX) : 0) +
+                       Stage::pad(8 * B * (N + 1) * NX) + Stage::pad(8 * B * (N + 1) * NX * NX);
+  Stage sg(s, bytes);
+  if (!sg.ok()) {
+    gpmpc_set_error("uprop3_linear: staging buffers: out of memory");
+    return -1;
   }
-  hipLaunchKernelGGL(k_uprop3_means, dim3(batch), dim3(256), 0, s, g, N, dt, alpha, g3[0], g3[1], g3[2],
-                     dx0.as<double>(), dU.as<double>(), dQ.as<double>(), dA.as<double>(), dmeans.as<double>());
+  const double *dx0 = sg.in(x0, B * NX), *dU = sg.in(U, P * NU);
+  const double *dS0 = S0 ? sg.in(S0, B * NX * NX) : nullptr;
+  double *dmeans = sg.out(means, B * (N + 1) * NX), *dcov = sg.out(covs, B * (N + 1) * NX * NX);
+  GPMPC_HIP(sg.upload());
+  hipLaunchKernelGGL(k_uprop3_means, dim3(batch), dim3(256), 0, s, g, N, dt, alpha, g3[0], g3[1], g3[2], dx0, dU,
+                     dQ.as<double>(), dA.as<double>(), dmeans);
   GPMPC_HIP(hipGetLastError());
   if (P) {
     GPMPC_HIP(dmu.alloc(s, sizeof(double) * P * 3));
@@ -1594,12 +1596,9 @@ extern "C" int gpmpc_uprop3_linear(gpmpc_ctx *ctx, gpmpc_gp *gp, int batch, int 
                        dvar.as<double>(), dq.as<double>());
     GPMPC_HIP(hipGetLastError());
   }
-  const int rc = gpmpc_cov_propagate_dev(ctx, batch, N, NX, dA.as<double>(), dq.as<double>(),
-                                         S0 ? dS0.as<double>() : nullptr, s0_diag, dcov.as<double>());
+  const int rc = gpmpc_cov_propagate_dev(ctx, batch, N, NX, dA.as<double>(), dq.as<double>(), dS0, s0_diag, dcov);
   if (rc) return rc;
-  GPMPC_HIP(hipMemcpyAsync(means, dmeans.p, sizeof(double) * B * (N + 1) * NX, hipMemcpyDeviceToHost, s));
-  GPMPC_HIP(hipMemcpyAsync(covs, dcov.p, sizeof(double) * B * (N + 1) * NX * NX, hipMemcpyDeviceToHost, s));
-  GPMPC_HIP(hipStreamSynchronize(s));
+  GPMPC_HIP(sg.download());
   return 0;
 }
 

@@ -716,11 +716,16 @@ extern "C" int gpmpc_gp_predict(gpmpc_ctx *ctx, gpmpc_gp *gp, const double *Xq, 
   GPMPC_HIP(hipSetDevice(ctx->device));
   hipStream_t s = ctx->stream;
   const GpCore &g = gp->core;
-  DevBuf dq, Ks, dmean, dvar;
-  GPMPC_HIP(dq.alloc(s, sizeof(double) * p * g.d));
-  GPMPC_HIP(hipMemcpyAsync(dq.p, Xq, sizeof(double) * p * g.d, hipMemcpyHostToDevice, s));
-  GPMPC_HIP(dmean.alloc(s, sizeof(double) * p * g.n_out));
-  GPMPC_HIP(dvar.alloc(s, sizeof(double) * p * g.n_out));
+  DevBuf Ks;
+  // the queries in one pinned upload, mean and variance in one read-back
+  const size_t P = p, bo = Stage::pad(8 * P * g.n_out);
+  Stage sg(s, Stage::pad(8 * P * g.d) + 2 * bo);
+  if (!sg.ok()) {
+    gpmpc_set_error("gp_predict: staging buffers: out of memory");
+    return -1;
+  }
+  double *dq = sg.in(Xq, P * g.d), *dmean = sg.out(mean, P * g.n_out), *dvar = sg.out(var, P * g.n_out);
+  GPMPC_HIP(sg.upload());
   if (g.Wf.p && post_cs_env()) {
     // K* formed inside the column-stationary posterior (post.hip): no K* in HBM
     DevBuf qs, qn, part, meanT;
@@ -728,23 +733,21 @@ extern "C" int gpmpc_gp_predict(gpmpc_ctx *ctx, gpmpc_gp *gp, const double *Xq, 
     GPMPC_HIP(qn.alloc(s, sizeof(double) * p));
     GPMPC_HIP(part.alloc(s, sizeof(double) * POST_CS_PARTS * p));
     GPMPC_HIP(meanT.alloc(s, sizeof(double) * g.n_out * p));
-    GPMPC_HIP(launch_scale_rows(s, dq.as<double>(), p, g.d, g.ls.as<double>(), g.kind == GPMPC_SE_ISO,
+    GPMPC_HIP(launch_scale_rows(s, dq, p, g.d, g.ls.as<double>(), g.kind == GPMPC_SE_ISO,
                                 qs.as<double>(), qn.as<double>()));
     GPMPC_HIP(launch_post_cs(s, g.n, g.n_out, p, g.Wf.as<double>(), g.Xp.as<double>(), qs.as<double>(),
                              qn.as<double>(), g.d, g.kind, g.sigma2, g.iso_scale, part.as<double>(), p,
                              meanT.as<double>(), p));
     GPMPC_HIP(launch_post_finish(s, p, g.n_out, POST_CS_PARTS, part.as<double>(), p, meanT.as<double>(), p,
-                                 g.ymean.as<double>(), g.ystd.as<double>(), g.sigma2, dmean.as<double>(),
-                                 dvar.as<double>()));
+                                 g.ymean.as<double>(), g.ystd.as<double>(), g.sigma2, dmean,
+                                 dvar));
   } else {
-    int rc = core_cross(ctx, g, dq.as<double>(), p, Ks);
+    int rc = core_cross(ctx, g, dq, p, Ks);
     if (rc) return rc;
-    rc = core_posterior(ctx, g, Ks.as<double>(), p, dmean.as<double>(), dvar.as<double>());
+    rc = core_posterior(ctx, g, Ks.as<double>(), p, dmean, dvar);
     if (rc) return rc;
   }
-  GPMPC_HIP(hipMemcpyAsync(mean, dmean.p, sizeof(double) * p * g.n_out, hipMemcpyDeviceToHost, s));
-  GPMPC_HIP(hipMemcpyAsync(var, dvar.p, sizeof(double) * p * g.n_out, hipMemcpyDeviceToHost, s));
-  GPMPC_HIP(hipStreamSynchronize(s));
+  GPMPC_HIP(sg.download());
   return 0;
 }
 

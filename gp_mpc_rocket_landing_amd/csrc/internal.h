@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 #include <cstdint>
 #include <cstdio>
+#include <cstring>
 #include <string>
 #include <utility>
 #include "../../include/gpmpc.h"
@@ -15,7 +16,7 @@ struct gpmpc_ctx {
 void gpmpc_set_error(const char *fmt, ...);
 // persistent scratch per stream (= per context; slots: 0 trsm block inverses,
 // 1 potrf 32x32 inverses, 2 potrf 128x128 inverses, 3 batched-LML Gram/factor
-// matrices, 4 gp_append temporaries; slots 0..7).  Valid until the next call
+// matrices, 4 gp_append temporaries, 5 split-K partials, 7 the Stage device arena; slots 0..7).  Valid until the next call
 // on the same stream that asks the slot for more bytes.
 #define GPMPC_SCRATCH_SLOTS 8
 void *gpmpc_scratch(hipStream_t s, int slot, size_t bytes);
@@ -89,6 +90,70 @@ struct DevBuf {
     std::swap(gen, o.gen);
   }
   template <class T> T *as() const { return static_cast<T *>(p); }
+};
+
+// Staging for the host-buffer entry points: a call packs its inputs into one pinned
+// arena and uploads them with ONE copy, and places its outputs in one device range
+// read back with ONE copy (a pageable hipMemcpyAsync costs 10-30 us of host time; a
+// single-landing QP solve made 14 of them).  The arenas are per stream (= per
+// context; device side = gpmpc_scratch slot 7), grown after the stream drains, and
+// valid until the next Stage on the stream.  Order of use: in() for pure inputs,
+// inout() for buffers both read and written back, then out(); upload() after the
+// last in/inout, download() after the last kernel (it synchronises the stream).
+char *gpmpc_stage_host(hipStream_t s, size_t bytes);
+void gpmpc_qp_cache_release(hipStream_t s);  // qp.hip: the stream's kept QP pattern
+struct Stage {
+  struct Back { void *dst; size_t off, bytes; };
+  hipStream_t s;
+  char *h = nullptr, *d = nullptr;
+  size_t off = 0, in_end = 0, back_lo = (size_t)-1;
+  Back backs[24];
+  int nback = 0;
+  static size_t pad(size_t b) { return (b + 255) & ~(size_t)255; }
+  // bytes: the sum of pad(size) over every buffer the call stages
+  Stage(hipStream_t st, size_t bytes) : s(st) {
+    h = gpmpc_stage_host(s, bytes);
+    d = (char *)gpmpc_scratch(s, 7, bytes);
+  }
+  bool ok() const { return h && d; }
+  template <class T> T *in(const T *src, size_t n) {
+    const size_t b = sizeof(T) * n;
+    if (b) memcpy(h + off, src, b);
+    T *r = (T *)(d + off);
+    off += pad(b);
+    return r;
+  }
+  template <class T> T *inout(T *src, size_t n) {
+    const size_t o = off;
+    T *r = in(src, n);
+    back(src, o, sizeof(T) * n);
+    return r;
+  }
+  template <class T> T *out(T *dst, size_t n) {
+    const size_t o = off;
+    off += pad(sizeof(T) * n);
+    back(dst, o, sizeof(T) * n);
+    return (T *)(d + o);
+  }
+  void back(void *dst, size_t o, size_t b) {
+    if (o < back_lo) back_lo = o;
+    backs[nback++] = Back{dst, o, b};
+  }
+  hipError_t upload() {
+    in_end = off;
+    return off ? hipMemcpyAsync(d, h, off, hipMemcpyHostToDevice, s) : hipSuccess;
+  }
+  hipError_t download() {
+    if (nback) {
+      hipError_t e = hipMemcpyAsync(h + back_lo, d + back_lo, off - back_lo, hipMemcpyDeviceToHost, s);
+      if (e != hipSuccess) return e;
+    }
+    hipError_t e = hipStreamSynchronize(s);
+    if (e != hipSuccess) return e;
+    for (int i = 0; i < nback; ++i)
+      if (backs[i].bytes) memcpy(backs[i].dst, h + backs[i].off, backs[i].bytes);
+    return hipSuccess;
+  }
 };
 
 // kernel value from r^2 of the length-scaled rows (the k_gram epilogue; shared

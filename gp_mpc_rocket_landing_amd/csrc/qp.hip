@@ -232,6 +232,43 @@ hipError_t launch_qp_batched(hipStream_t s, const QPPattern &pt, const QPSetting
   return hipGetLastError();
 }
 
+// The last pattern of each stream, kept: a caller that re-solves one pattern (the OSQP
+// workspace, QPWorkspace.solve, once per control step) pays its host pre-processing,
+// upload and the upload's synchronisation once instead of per solve.
+#include <map>
+#include <memory>
+#include <mutex>
+struct QPPatCache {
+  std::vector<int> rowptr, colidx;
+  int n = 0;
+  std::unique_ptr<QPPatternHost> pat;
+};
+static std::mutex g_qpcache_mu;
+static std::map<hipStream_t, QPPatCache> g_qpcache;
+
+void gpmpc_qp_cache_release(hipStream_t s) {
+  std::lock_guard<std::mutex> lk(g_qpcache_mu);
+  g_qpcache.erase(s);
+}
+
+static QPPatternHost *qp_pattern(hipStream_t s, int n, int m, const int *rowptr, const int *colidx) {
+  std::lock_guard<std::mutex> lk(g_qpcache_mu);
+  QPPatCache &c = g_qpcache[s];
+  const int nnz = rowptr[m];
+  if (c.pat && c.n == n && (int)c.rowptr.size() == m + 1 && (int)c.colidx.size() == nnz &&
+      !memcmp(c.rowptr.data(), rowptr, sizeof(int) * (m + 1)) &&
+      !memcmp(c.colidx.data(), colidx, sizeof(int) * nnz))
+    return c.pat.get();
+  c.pat.reset();
+  auto pat = std::make_unique<QPPatternHost>();
+  if (pat->build(n, m, rowptr, colidx, s)) return nullptr;
+  c.rowptr.assign(rowptr, rowptr + m + 1);
+  c.colidx.assign(colidx, colidx + nnz);
+  c.n = n;
+  c.pat = std::move(pat);
+  return c.pat.get();
+}
+
 extern "C" int gpmpc_qp_solve_batched(gpmpc_ctx *ctx, int batch, int n, int m, int nnz,
                                       const int *rowptr, const int *colidx, const double *Aval,
                                       const double *Pdiag, const double *q, const double *l,
@@ -246,54 +283,37 @@ extern "C" int gpmpc_qp_solve_batched(gpmpc_ctx *ctx, int batch, int n, int m, i
   if (batch == 0) return 0;
   GPMPC_HIP(hipSetDevice(ctx->device));
   hipStream_t s = ctx->stream;
-  QPPatternHost pat;
-  if (pat.build(n, m, rowptr, colidx, s)) {
+  const QPPatternHost *pat = qp_pattern(s, n, m, rowptr, colidx);
+  if (!pat) {
     gpmpc_set_error("qp: pattern upload failed");
     return -1;
   }
-  if (!pat.fits()) {
+  if (!pat->fits()) {
     gpmpc_set_error("qp: pattern outside the compiled caps (n %d<=256, m %d<=512, half-bandwidth "
-                    "%d<=%d, row nnz %d<=%d, col nnz %d<=%d)", pat.n, pat.m, pat.w, QP_W,
-                    pat.maxrow, QP_RMAX, pat.maxcol, QP_CMAX);
+                    "%d<=%d, row nnz %d<=%d, col nnz %d<=%d)", pat->n, pat->m, pat->w, QP_W,
+                    pat->maxrow, QP_RMAX, pat->maxcol, QP_CMAX);
     return -2;
   }
-  DevBuf dA, dP, dq, dl, du, dx0, drho, dy0, dxo, dyo, dit, dst, dob;
-  const size_t B = batch;
-  GPMPC_HIP(dA.alloc(s, sizeof(double) * B * nnz));
-  GPMPC_HIP(dP.alloc(s, sizeof(double) * B * n));
-  GPMPC_HIP(dq.alloc(s, sizeof(double) * B * n));
-  GPMPC_HIP(dl.alloc(s, sizeof(double) * B * m));
-  GPMPC_HIP(du.alloc(s, sizeof(double) * B * m));
-  GPMPC_HIP(drho.alloc(s, sizeof(double) * B));
-  GPMPC_HIP(dy0.alloc(s, sizeof(double) * B * m));
-  GPMPC_HIP(dxo.alloc(s, sizeof(double) * B * n));
-  GPMPC_HIP(dyo.alloc(s, sizeof(double) * B * m));
-  GPMPC_HIP(dit.alloc(s, sizeof(int) * B));
-  GPMPC_HIP(dst.alloc(s, sizeof(int) * B));
-  GPMPC_HIP(dob.alloc(s, sizeof(double) * B));
-  GPMPC_HIP(hipMemcpyAsync(dA.p, Aval, sizeof(double) * B * nnz, hipMemcpyHostToDevice, s));
-  GPMPC_HIP(hipMemcpyAsync(dP.p, Pdiag, sizeof(double) * B * n, hipMemcpyHostToDevice, s));
-  GPMPC_HIP(hipMemcpyAsync(dq.p, q, sizeof(double) * B * n, hipMemcpyHostToDevice, s));
-  GPMPC_HIP(hipMemcpyAsync(dl.p, l, sizeof(double) * B * m, hipMemcpyHostToDevice, s));
-  GPMPC_HIP(hipMemcpyAsync(du.p, u, sizeof(double) * B * m, hipMemcpyHostToDevice, s));
-  GPMPC_HIP(hipMemcpyAsync(drho.p, rho, sizeof(double) * B, hipMemcpyHostToDevice, s));
-  GPMPC_HIP(hipMemcpyAsync(dy0.p, y_scaled, sizeof(double) * B * m, hipMemcpyHostToDevice, s));
-  if (x_ws) {
-    GPMPC_HIP(dx0.alloc(s, sizeof(double) * B * n));
-    GPMPC_HIP(hipMemcpyAsync(dx0.p, x_ws, sizeof(double) * B * n, hipMemcpyHostToDevice, s));
+  // every input in one pinned upload, every output in one read-back
+  const size_t B = batch, dn = 8 * B * n, dm = 8 * B * m;
+  const size_t bytes = Stage::pad(8 * B * nnz) + 2 * Stage::pad(dn) + 2 * Stage::pad(dm) +
+                       (x_ws ? Stage::pad(dn) : 0) + Stage::pad(8 * B) + Stage::pad(dm) + Stage::pad(dn) +
+                       Stage::pad(dm) + 2 * Stage::pad(4 * B) + Stage::pad(8 * B);
+  Stage sg(s, bytes);
+  if (!sg.ok()) {
+    gpmpc_set_error("qp: staging buffers: out of memory");
+    return -1;
   }
-  GPMPC_HIP(launch_qp_batched(s, pat.dev, to_dev(*st), batch, dA.as<double>(), dP.as<double>(),
-                              dq.as<double>(), dl.as<double>(), du.as<double>(),
-                              x_ws ? dx0.as<double>() : nullptr, drho.as<double>(),
-                              dy0.as<double>(), dxo.as<double>(), dyo.as<double>(), dit.as<int>(),
-                              dst.as<int>(), dob.as<double>()));
-  GPMPC_HIP(hipMemcpyAsync(x, dxo.p, sizeof(double) * B * n, hipMemcpyDeviceToHost, s));
-  GPMPC_HIP(hipMemcpyAsync(y, dyo.p, sizeof(double) * B * m, hipMemcpyDeviceToHost, s));
-  GPMPC_HIP(hipMemcpyAsync(y_scaled, dy0.p, sizeof(double) * B * m, hipMemcpyDeviceToHost, s));
-  GPMPC_HIP(hipMemcpyAsync(rho, drho.p, sizeof(double) * B, hipMemcpyDeviceToHost, s));
-  GPMPC_HIP(hipMemcpyAsync(iters, dit.p, sizeof(int) * B, hipMemcpyDeviceToHost, s));
-  GPMPC_HIP(hipMemcpyAsync(status, dst.p, sizeof(int) * B, hipMemcpyDeviceToHost, s));
-  GPMPC_HIP(hipMemcpyAsync(obj, dob.p, sizeof(double) * B, hipMemcpyDeviceToHost, s));
-  GPMPC_HIP(hipStreamSynchronize(s));
+  const double *dA = sg.in(Aval, B * nnz), *dP = sg.in(Pdiag, B * n), *dq = sg.in(q, B * n);
+  const double *dl = sg.in(l, B * m), *du = sg.in(u, B * m);
+  const double *dx0 = x_ws ? sg.in(x_ws, B * n) : nullptr;
+  double *drho = sg.inout(rho, B), *dy0 = sg.inout(y_scaled, B * m);
+  double *dxo = sg.out(x, B * n), *dyo = sg.out(y, B * m);
+  int *dit = sg.out(iters, B), *dst = sg.out(status, B);
+  double *dob = sg.out(obj, B);
+  GPMPC_HIP(sg.upload());
+  GPMPC_HIP(launch_qp_batched(s, pat->dev, to_dev(*st), batch, dA, dP, dq, dl, du, dx0, drho, dy0, dxo, dyo,
+                              dit, dst, dob));
+  GPMPC_HIP(sg.download());
   return 0;
 }
