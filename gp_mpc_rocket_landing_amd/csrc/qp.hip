@@ -8,6 +8,7 @@
 #include "internal.h"
 #include "qp.h"
 #include <algorithm>
+#include <cstdlib>
 #include <vector>
 
 extern "C" void gpmpc_qp_default_settings(gpmpc_qp_settings *s) {
@@ -186,7 +187,8 @@ __global__ __launch_bounds__(256) void k_qp_batched(QPPattern pt, QPSettingsDev 
                                                     const double *__restrict__ u,
                                                     const double *__restrict__ xws, double *rho,
                                                     double *yst, double *xo, double *yo,
-                                                    int *iters, int *status, double *obj) {
+                                                    int *iters, int *status, double *obj,
+                                                    unsigned long long *stamps) {
   __shared__ QPSmemStd s;
   const int b = blockIdx.x, tid = threadIdx.x, nt = blockDim.x;
   const int n = pt.n, m = pt.m, nnz = pt.nnz;
@@ -203,7 +205,12 @@ __global__ __launch_bounds__(256) void k_qp_batched(QPPattern pt, QPSettingsDev 
   }
   if (tid == 0) s.rho_s = rho[b];
   __syncthreads();
-  QPResult res = qp_solve(pt, s, st);
+  QPStamps T;
+  if (b == 0) T.out = stamps;  // (GPMPC_QP_STAMPS: problem 0's phase cycles)
+  T.start();
+  QPResult res = qp_solve(pt, s, st, &T);
+  T.mark(7);
+  T.flush();
   if (res.factor_fail) {
     if (tid == 0) { status[b] = -100; iters[b] = 0; obj[b] = nan(""); }
     return;
@@ -226,9 +233,9 @@ hipError_t launch_qp_batched(hipStream_t s, const QPPattern &pt, const QPSetting
                              int batch, const double *Aval, const double *Pd, const double *q,
                              const double *l, const double *u, const double *xws, double *rho,
                              double *yst, double *xo, double *yo, int *iters, int *status,
-                             double *obj) {
+                             double *obj, unsigned long long *stamps = nullptr) {
   hipLaunchKernelGGL(k_qp_batched, dim3(batch), dim3(256), 0, s, pt, st, Aval, Pd, q, l, u, xws,
-                     rho, yst, xo, yo, iters, status, obj);
+                     rho, yst, xo, yo, iters, status, obj, stamps);
   return hipGetLastError();
 }
 
@@ -312,8 +319,22 @@ extern "C" int gpmpc_qp_solve_batched(gpmpc_ctx *ctx, int batch, int n, int m, i
   int *dit = sg.out(iters, B), *dst = sg.out(status, B);
   double *dob = sg.out(obj, B);
   GPMPC_HIP(sg.upload());
+  // GPMPC_QP_STAMPS=1: problem 0's phase cycles (s_memtime) to stderr, a diagnostic
+  static const bool stamp = getenv("GPMPC_QP_STAMPS") && atoi(getenv("GPMPC_QP_STAMPS"));
+  DevBuf dts;
+  if (stamp) {
+    GPMPC_HIP(dts.alloc(s, 16 * sizeof(unsigned long long)));
+    GPMPC_HIP(hipMemsetAsync(dts.p, 0, 16 * sizeof(unsigned long long), s));
+  }
   GPMPC_HIP(launch_qp_batched(s, pat->dev, to_dev(*st), batch, dA, dP, dq, dl, du, dx0, drho, dy0, dxo, dyo,
-                              dit, dst, dob));
+                              dit, dst, dob, dts.as<unsigned long long>()));
   GPMPC_HIP(sg.download());
+  if (stamp) {
+    unsigned long long h[16];
+    GPMPC_HIP(hipMemcpy(h, dts.p, sizeof(h), hipMemcpyDeviceToHost));
+    fprintf(stderr, "qp_stamps iter %d:", iters[0]);
+    for (int k = 0; k < 16; ++k) fprintf(stderr, " %llu", h[k]);
+    fprintf(stderr, "\n");
+  }
   return 0;
 }

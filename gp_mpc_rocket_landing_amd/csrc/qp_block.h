@@ -567,6 +567,7 @@ __device__ __forceinline__ void blk_solve(const QPPattern &pt, S &s, double *b, 
 // the compiled (SZ, CM) instantiations; the host only selects mode 1 for these
 #define QP_BLK_SZ 10  // 3-DoF MPC stage [x_k (7), u_k (3)]
 #define QP_BLK_CM 7   // coupled through x_{k+1}
+#define QP_NBLK_MPC20 21  // its block count at N = 20 (207 variables), unrolled by the generic solver
 
 template <class S>
 __device__ __forceinline__ int blk_factor_dispatch(const QPPattern &pt, S &s) {

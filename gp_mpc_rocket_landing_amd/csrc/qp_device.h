@@ -652,7 +652,16 @@ __device__ QPResult qp_solve(const QPPattern &pt, S &s, const QPSettingsDev &st,
     }
     __syncthreads();
     T.mark(3);
-    if (pt.mode == 1) blk_solve_dispatch(pt, s, s.rhs, &T);  // x~
+    if (pt.mode == 1 && pt.nblk == QP_NBLK_MPC20) {
+      // x~ for the 3-DoF MPC at N = 20 (21 blocks): the G chain fully unrolled (wave 0),
+      // the diagonal blocks eight a round on waves 0-1, the unrolled backward chain --
+      // the fused chain's arithmetic in the same order (same bits), ~2.5x shorter
+      blk_solve_dispatch<false, QP_NBLK_MPC20, 1>(pt, s, s.rhs, &T);
+      __syncthreads();
+      if (tid < 128) blk_solve_dispatch<false, QP_NBLK_MPC20, 2>(pt, s, s.rhs, &T);
+      __syncthreads();
+      blk_solve_dispatch<false, QP_NBLK_MPC20, 4>(pt, s, s.rhs, &T);
+    } else if (pt.mode == 1) blk_solve_dispatch(pt, s, s.rhs, &T);  // x~
     else qp_band_solve(pt, s, s.rhs);
     __syncthreads();
     T.mark(4);
