@@ -1475,12 +1475,27 @@ extern "C" int gpmpc_fleet_destroy(gpmpc_fleet *f) {
 // numpy forms them) plus dt d_v on the velocity rows, and A_k = I + dt J(x_k, u_k).  The
 // variances of all B N queries then come from the GP's own batched posterior, and one
 // launch propagates every covariance (k_cov_propagate).
+#define UP3_R 4  // training rows per thread held in registers (n <= 1024); larger n reads them per step
 __global__ __launch_bounds__(256) void k_uprop3_means(GpView g, int N, double dt, double alpha, double g0,
                                                       double g1, double g2, const double *__restrict__ x0,
                                                       const double *__restrict__ U, double *__restrict__ Q,
                                                       double *__restrict__ A, double *__restrict__ means) {
   const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  __shared__ double sx[NX], sz[NFEAT], szn, red[4][3], sm[3];
+  __shared__ double sx[NX], sz[NFEAT], szn, red[4][3];
+  // this thread's training rows j = tid + 256 r (scaled features, |x_j|^2, alpha), loaded once:
+  // the N sequential steps then read no global memory on their critical path
+  const bool reg = g.n <= 256 * UP3_R;
+  double xr[UP3_R][NFEAT], xnr[UP3_R], ar[UP3_R][3];
+#pragma unroll
+  for (int r = 0; r < UP3_R; ++r) {
+    const int j = tid + 256 * r;
+    const bool ok = reg && j < g.n;
+#pragma unroll
+    for (int f = 0; f < NFEAT; ++f) xr[r][f] = ok ? g.Xs[(int64_t)j * NFEAT + f] : 0.0;
+    xnr[r] = ok ? g.Xn[j] : 0.0;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) ar[r][c] = ok ? g.alphaT[(int64_t)c * g.n + j] : 0.0;
+  }
   if (tid < NX) {
     sx[tid] = x0[(int64_t)b * NX + tid];
     means[(int64_t)b * (N + 1) * NX + tid] = sx[tid];
@@ -1499,23 +1514,40 @@ __global__ __launch_bounds__(256) void k_uprop3_means(GpView g, int N, double dt
         sn += v * v;
       }
       szn = sn;
-      // A_k = I + dt J: J[1:4, 4:7] = I, J[4:7, 0] = -u / m^2 (rocket_3dof.py jacobian_x)
-      double *Ak = A + ((int64_t)b * N + k) * NX * NX;
-      for (int e = 0; e < NX * NX; ++e) Ak[e] = (e % (NX + 1) == 0) ? 1.0 : 0.0;
-      for (int i = 0; i < 3; ++i) Ak[(1 + i) * NX + 4 + i] = __dmul_rn(1.0, dt);
-      const double m2 = __dmul_rn(sx[0], sx[0]);
-      for (int i = 0; i < 3; ++i) Ak[(4 + i) * NX] = __dmul_rn(-u[i] / m2, dt);
+    } else if (tid >= 64 && tid < 64 + NX * NX) {
+      // A_k = I + dt J: J[1:4, 4:7] = I, J[4:7, 0] = -u / m^2 (rocket_3dof.py jacobian_x), one entry a thread
+      const int e = tid - 64, r = e / NX, c = e - r * NX;
+      double v = (r == c) ? 1.0 : 0.0;
+      if (r >= 1 && r <= 3 && c == r + 3) v = __dmul_rn(1.0, dt);
+      if (r >= 4 && c == 0) v = __dmul_rn(-u[r - 4] / __dmul_rn(sx[0], sx[0]), dt);
+      A[((int64_t)b * N + k) * NX * NX + e] = v;
     }
     __syncthreads();
     double acc[3] = {0.0, 0.0, 0.0};
     const double zn = szn;
-    for (int j = tid; j < g.n; j += 256) {
-      double dot = 0.0;
+    if (reg) {
+      double zv[NFEAT];
 #pragma unroll
-      for (int f = 0; f < NFEAT; ++f) dot = fma(sz[f], g.Xs[(int64_t)j * NFEAT + f], dot);
-      const double kv = kernel_epilogue(g.kind, (zn + g.Xn[j]) - 2.0 * dot, g.sigma2, g.iso_scale);
+      for (int f = 0; f < NFEAT; ++f) zv[f] = sz[f];
 #pragma unroll
-      for (int c = 0; c < 3; ++c) acc[c] = fma(kv, g.alphaT[(int64_t)c * g.n + j], acc[c]);
+      for (int r = 0; r < UP3_R; ++r) {
+        if (tid + 256 * r >= g.n) break;
+        double dot = 0.0;
+#pragma unroll
+        for (int f = 0; f < NFEAT; ++f) dot = fma(zv[f], xr[r][f], dot);
+        const double kv = kernel_epilogue(g.kind, (zn + xnr[r]) - 2.0 * dot, g.sigma2, g.iso_scale);
+#pragma unroll
+        for (int c = 0; c < 3; ++c) acc[c] = fma(kv, ar[r][c], acc[c]);
+      }
+    } else {
+      for (int j = tid; j < g.n; j += 256) {
+        double dot = 0.0;
+#pragma unroll
+        for (int f = 0; f < NFEAT; ++f) dot = fma(sz[f], g.Xs[(int64_t)j * NFEAT + f], dot);
+        const double kv = kernel_epilogue(g.kind, (zn + g.Xn[j]) - 2.0 * dot, g.sigma2, g.iso_scale);
+#pragma unroll
+        for (int c = 0; c < 3; ++c) acc[c] = fma(kv, g.alphaT[(int64_t)c * g.n + j], acc[c]);
+      }
     }
 #pragma unroll
     for (int c = 0; c < 3; ++c)

@@ -183,3 +183,27 @@ def test_propagate_3dof_sparse_gp_stays_on_host_loop(gpu_ctx, monkeypatch):
     m, c = UncertaintyPropagator(create_normalized_rocket(), gp, ctx=gpu_ctx).propagate_batch(
         f1["X"][:2], np.repeat(f1["U"][:2, None], 5, axis=1), None, 0.1)
     assert m.shape == (2, 6, 7) and np.all(np.isfinite(c))
+
+
+@pytest.mark.parametrize("n", [1000, 1100])
+def test_propagate_batch_3dof_device_training_sizes(gpu_ctx, n):
+    """The device propagation's training rows in registers (n <= 1024) and read per
+    step (n > 1024), vs the host loop."""
+    _ctx_default(gpu_ctx)
+    from gp_mpc_rocket_landing_amd.data import synthetic_training_data
+    from gp_mpc_rocket_landing_amd.dynamics import create_normalized_rocket
+    from gp_mpc_rocket_landing_amd.fleet import initial_conditions
+    from gp_mpc_rocket_landing_amd.gp import Simple3DoFGP
+    from gp_mpc_rocket_landing_amd.mpc import UncertaintyPropagator
+    X, U, D = synthetic_training_data(n, seed=1)
+    gp = Simple3DoFGP(use_sparse=False)
+    gp.add_data(X, U, D); gp.fit()
+    X0 = initial_conditions(3)
+    rs = np.random.RandomState(n)
+    Uh = np.tile((-X0[:, 0:1] * np.array([-1.0, 0, 0]))[:, None, :], (1, 12, 1)) * (1 + 0.1 * rs.randn(3, 12, 1))
+    p = UncertaintyPropagator(create_normalized_rocket(), gp, ctx=gpu_ctx)
+    md, cd = p.propagate_batch(X0, Uh, None, 0.1)
+    p.use_device = False
+    mh, ch = p.propagate_batch(X0, Uh, None, 0.1)
+    np.testing.assert_allclose(md, mh, rtol=1e-10, atol=1e-10)
+    np.testing.assert_allclose(cd, ch, rtol=1e-7, atol=1e-15)
