@@ -21,6 +21,7 @@
 #include "gemm.h"
 #include "qp.h"
 #include "fleet_qp.h"
+#include <mutex>
 #include <vector>
 #include <algorithm>
 
@@ -924,9 +925,84 @@ __global__ __launch_bounds__(FQ_T) __attribute__((amdgpu_waves_per_eu(FQ_WPE, FQ
   if (a.trace && tid == 0) a.trace[(int64_t)b * 4 + 1] = __builtin_amdgcn_s_memrealtime();
 }
 
+
+// gpmpc_qp_solve_batched on this solver (qp.hip picks it): problems whose pattern is the
+// fleet's MPC pattern at N = 20 (fleet_qp.h's fixed row layout: dynamics rows 0..MD-1 as
+// equalities, then the identity bound rows) -- the host surface's QPWorkspace.solve.  The
+// QP data come from global memory instead of the fleet's assembly; rho, the scaled y and
+// the outputs are the generic kernel's (k_qp_batched), one problem per workgroup.
+__global__ __launch_bounds__(FQ_T) __attribute__((amdgpu_waves_per_eu(FQ_WPE, FQ_WPE))) void k_qp_fleet(
+    QPPattern pt, QPSettingsDev st, const double *__restrict__ Aval, const double *__restrict__ Pd,
+    const double *__restrict__ q, const double *__restrict__ l, const double *__restrict__ u,
+    const double *__restrict__ xws, double *rho, double *yst, double *xo, double *yo, int *iters, int *status,
+    double *obj) {
+  __shared__ FleetSmem s;
+  const int b = blockIdx.x, tid = threadIdx.x, n = pt.n, m = pt.m;
+  const double *Ab = Aval + (int64_t)b * pt.nnz;
+  FleetRegs R;
+  fq_init_pattern(pt, R, n);
+  for (int e = tid; e < FQ_NNZD; e += FQ_T) s.A[e] = Ab[e];
+#pragma unroll
+  for (int h = 0; h < FQ_H; ++h) {
+    if (!R.vok[h]) continue;
+    const int j = R.vj[h];
+    R.P[h] = Pd[(int64_t)b * n + j];
+    R.q[h] = q[(int64_t)b * n + j];
+    R.x[h] = xws ? xws[(int64_t)b * n + j] : 0.0;
+    R.Ab[h] = Ab[FQ_NNZD + j];  // bound row MD + j: its one entry
+    R.lb[h] = l[(int64_t)b * m + FQ_MD + j];
+    R.ub[h] = u[(int64_t)b * m + FQ_MD + j];
+    R.yb_(h) = yst[(int64_t)b * m + FQ_MD + j];
+  }
+#pragma unroll
+  for (int h = 0; h < FQ_H; ++h)
+    if (R.rok[h]) {
+      R.ur(h) = l[(int64_t)b * m + R.rr[h]];  // l = u (checked by the host)
+      R.yr(h) = yst[(int64_t)b * m + R.rr[h]];
+    }
+  if (tid == 0) s.rho_s = rho[b];
+  __syncthreads();
+  QPStamps T;
+  const QPResult res = fq_solve(pt, s, R, st, &T, 0);
+  if (res.factor_fail) {
+    if (tid == 0) { status[b] = -100; iters[b] = 0; obj[b] = nan(""); }
+    return;
+  }
+  const bool has = (res.status == 1 || res.status == 2 || res.status == -2);
+  const double c = s.c;
+#pragma unroll
+  for (int h = 0; h < FQ_H; ++h) {
+    if (R.vok[h]) {
+      const int j = R.vj[h];
+      xo[(int64_t)b * n + j] = has ? R.D[h] * R.x[h] : nan("");
+      yo[(int64_t)b * m + FQ_MD + j] = has ? s.E[FQ_MD + j] * R.yb_(h) / c : nan("");
+      yst[(int64_t)b * m + FQ_MD + j] = R.yb_(h);
+    }
+    if (R.rok[h]) {
+      yo[(int64_t)b * m + R.rr[h]] = has ? s.E[R.rr[h]] * R.yr(h) / c : nan("");
+      yst[(int64_t)b * m + R.rr[h]] = R.yr(h);
+    }
+  }
+  if (tid == 0) {
+    rho[b] = s.rho_s;
+    iters[b] = res.iter;
+    status[b] = res.status;
+    obj[b] = has ? res.obj : nan("");
+  }
+}
+
 }  // namespace FQ_KNS
 
+#define QP_FLEET_LAUNCH                                                                                      \
+  (hipStream_t s, int batch, const QPPattern &pt, const QPSettingsDev &st, const double *Aval, const double *Pd, \
+   const double *q, const double *l, const double *u, const double *xws, double *rho, double *yst, double *xo,  \
+   double *yo, int *iters, int *status, double *obj) {                                                         \
+    hipLaunchKernelGGL(FQ_KNS::k_qp_fleet, dim3(batch), dim3(FQ_T), 0, s, pt, st, Aval, Pd, q, l, u, xws, rho,   \
+                       yst, xo, yo, iters, status, obj);                                                        \
+    return hipGetLastError();                                                                                  \
+  }
 #ifdef FLEET_WIDE_TU
+hipError_t launch_qp_fleet_wide QP_FLEET_LAUNCH
 hipError_t launch_fleet_control_wide(hipStream_t s, int nb, const FleetArgs &a, bool stamps) {
   if (stamps)
     hipLaunchKernelGGL(FQ_KNS::k_fleet_control2<true>, dim3(nb), dim3(FQ_T), 0, s, a);
@@ -935,6 +1011,17 @@ hipError_t launch_fleet_control_wide(hipStream_t s, int nb, const FleetArgs &a, 
   return hipGetLastError();
 }
 #else
+hipError_t launch_qp_fleet_narrow QP_FLEET_LAUNCH
+// the fleet solver's pattern: the MPC pattern at N = 20 (fleet_qp.h's compiled sizes)
+static_assert(FQ_MD == QP_FLEET_MD, "qp.h's copy of the dynamics row count");
+bool qp_is_fleet_pattern(int n, int m, const int *rowptr, const int *colidx) {
+  static std::vector<int> rp, ci;
+  static std::once_flag once;
+  std::call_once(once, [] { mpc_pattern(20, rp, ci); });
+  const int nv = (20 + 1) * NX + 20 * NU;
+  if (n != nv || m + 1 != (int)rp.size() || rowptr[m] != (int)ci.size()) return false;
+  return !memcmp(rowptr, rp.data(), sizeof(int) * rp.size()) && !memcmp(colidx, ci.data(), sizeof(int) * ci.size());
+}
 __global__ void k_fleet_reset(int first, int count, int N, int target_mode,
                               const double *__restrict__ x0, double *x, double *Xw, double *Uw,
                               double *ysc, int m, double *rho, double rho0, double *rec,

@@ -29,3 +29,13 @@ struct QPPatternHost {
 };
 
 QPSettingsDev to_dev(const gpmpc_qp_settings &s);
+// the fleet's specialised solver for batched QPs on its pattern (fleet.hip k_qp_fleet): the
+// 128-thread build (four problems per CU) and the 256-thread one (one per CU)
+bool qp_is_fleet_pattern(int n, int m, const int *rowptr, const int *colidx);
+#define QP_FLEET_MD 147  // its dynamics rows (fleet_qp.h FQ_MD)
+#define QP_FLEET_DECL(name)                                                                                    \
+  hipError_t name(hipStream_t s, int batch, const QPPattern &pt, const QPSettingsDev &st, const double *Aval,  \
+                  const double *Pd, const double *q, const double *l, const double *u, const double *xws,      \
+                  double *rho, double *yst, double *xo, double *yo, int *iters, int *status, double *obj);
+QP_FLEET_DECL(launch_qp_fleet_narrow)
+QP_FLEET_DECL(launch_qp_fleet_wide)

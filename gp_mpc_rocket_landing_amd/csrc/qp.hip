@@ -276,6 +276,13 @@ static QPPatternHost *qp_pattern(hipStream_t s, int n, int m, const int *rowptr,
   return c.pat.get();
 }
 
+static int qp_cu_count(int dev) {
+  static int cus[64] = {0};
+  if (dev < 0 || dev >= 64) return 0;
+  if (!cus[dev]) (void)hipDeviceGetAttribute(&cus[dev], hipDeviceAttributeMultiprocessorCount, dev);
+  return cus[dev];
+}
+
 extern "C" int gpmpc_qp_solve_batched(gpmpc_ctx *ctx, int batch, int n, int m, int nnz,
                                       const int *rowptr, const int *colidx, const double *Aval,
                                       const double *Pdiag, const double *q, const double *l,
@@ -301,6 +308,15 @@ extern "C" int gpmpc_qp_solve_batched(gpmpc_ctx *ctx, int batch, int n, int m, i
                     pat->maxrow, QP_RMAX, pat->maxcol, QP_CMAX);
     return -2;
   }
+  // The fleet's solver (fleet_qp.h, registers + twisted KKT solve) for its own pattern -- the
+  // 3-DoF MPC at N = 20 -- when the dynamics rows are equalities, as that solver assumes
+  // (GPMPC_QP_FLEET=0: always the generic kernel).  The same OSQP iteration; the block-wide
+  // sums and the KKT solve round differently from the generic kernel's.
+  const char *fe = getenv("GPMPC_QP_FLEET");  // (read per call: tests switch it)
+  const bool fleet_env = !fe || atoi(fe);
+  bool fleet = fleet_env && qp_is_fleet_pattern(n, m, rowptr, colidx);
+  for (int64_t r = 0; fleet && r < (int64_t)batch * m; ++r)
+    if (r % m < QP_FLEET_MD && l[r] != u[r]) fleet = false;
   // every input in one pinned upload, every output in one read-back
   const size_t B = batch, dn = 8 * B * n, dm = 8 * B * m;
   const size_t bytes = Stage::pad(8 * B * nnz) + 2 * Stage::pad(dn) + 2 * Stage::pad(dm) +
@@ -326,8 +342,13 @@ extern "C" int gpmpc_qp_solve_batched(gpmpc_ctx *ctx, int batch, int n, int m, i
     GPMPC_HIP(dts.alloc(s, 16 * sizeof(unsigned long long)));
     GPMPC_HIP(hipMemsetAsync(dts.p, 0, 16 * sizeof(unsigned long long), s));
   }
-  GPMPC_HIP(launch_qp_batched(s, pat->dev, to_dev(*st), batch, dA, dP, dq, dl, du, dx0, drho, dy0, dxo, dyo,
-                              dit, dst, dob, dts.as<unsigned long long>()));
+  if (fleet) {
+    GPMPC_HIP((batch <= qp_cu_count(ctx->device) ? launch_qp_fleet_wide : launch_qp_fleet_narrow)(
+        s, batch, pat->dev, to_dev(*st), dA, dP, dq, dl, du, dx0, drho, dy0, dxo, dyo, dit, dst, dob));
+  } else {
+    GPMPC_HIP(launch_qp_batched(s, pat->dev, to_dev(*st), batch, dA, dP, dq, dl, du, dx0, drho, dy0, dxo, dyo,
+                                dit, dst, dob, dts.as<unsigned long long>()));
+  }
   GPMPC_HIP(sg.download());
   if (stamp) {
     unsigned long long h[16];

@@ -298,12 +298,15 @@ def _qp_batch(B, seed=0, N=20):
     return probs
 
 
-def test_qp_batched_vs_c_oracle(gpu_ctx):
+@pytest.mark.parametrize("fleet,B", [("1", 24), ("1", 300), ("0", 24)])
+def test_qp_batched_vs_c_oracle(gpu_ctx, monkeypatch, fleet, B):
     """Batched HIP ADMM vs the C restatement: status and iteration counts exact,
-    primal within 1e-6 rel, over three warm-started solves (rho / y carried)."""
+    primal within 1e-6 rel, over three warm-started solves (rho / y carried).  The
+    N = 20 MPC pattern runs on the fleet's solver (fleet=1, the default) or the
+    generic kernel (GPMPC_QP_FLEET=0); 300 problems take its 128-thread build."""
+    monkeypatch.setenv("GPMPC_QP_FLEET", fleet)
     L = _lib()
     from oracle import admm_ref
-    B = 24
     probs = _qp_batch(B)
     A0 = probs[0][2]
     A0.sort_indices()
