@@ -453,6 +453,43 @@ def surface_single_landing_bench(ctx, steps=100, reps=2):
     return out
 
 
+def surface_gpmpc6_bench(ctx, steps=30, reps=2):
+    """The reference's own 14-state surface as an unchanged caller drives it:
+    ``GPMPC(Rocket6DoFDynamics(), StructuredRocketGP(StructuredGPConfig()), GPMPCConfig())``
+    (the reference defaults: FITC, 50 inducing points, 1000 rows; N = 20) ``.solve(x, target)``
+    per step under the Monte-Carlo protocol (monte_carlo.py:495-512: incremental target, u0
+    into the plant).  Each solve is one gpmpc_rollout6_solve call (batch 1); with the default
+    use_gp_uncertainty=True also the host-loop covariance propagation (one batched GP call
+    per horizon step + the device covariance kernel).  Beside it the same loop without."""
+    from gp_mpc_rocket_landing_amd.dynamics import Rocket6DoFDynamics
+    from gp_mpc_rocket_landing_amd.mpc import GPMPC, GPMPCConfig
+    from gp_mpc_rocket_landing_amd.rollouts6 import fit_structured_gp, initial_conditions_6dof
+    gp = fit_structured_gp(1000, 50, seed=0)
+    dyn = Rocket6DoFDynamics()
+    x0 = initial_conditions_6dof(1)[0]
+    out = {"workload": "1 landing, GPMPC(Rocket6DoFDynamics(), StructuredRocketGP() [FITC M=50, 1000 rows], "
+                       "GPMPCConfig()).solve per step, monte_carlo.py:495-512 protocol", "steps": steps}
+    for name, unc in (("us_per_step", True), ("us_per_step_no_uncertainty", False)):
+        ts = []
+        for _ in range(reps):
+            ctl = GPMPC(dyn, gp, GPMPCConfig(use_gp_uncertainty=unc))
+            try:
+                x = x0.copy()
+                done = 0
+                t0 = time.perf_counter()
+                for _ in range(steps):
+                    tgt = x.copy(); tgt[4:7] = 0.0; tgt[1] = max(0.5, x[1] - 2.0)
+                    sol = ctl.solve(x, tgt)
+                    x = dyn.step(x, sol.u0, 0.1)
+                    done += 1
+                ts.append((time.perf_counter() - t0) / max(done, 1))
+            finally:
+                ctl.close()
+        out[name] = round(min(ts) * 1e6, 1)
+    out["steps_per_s"] = round(1e6 / out["us_per_step"], 1)
+    return out
+
+
 def fleet_fitc_bench(ctx, batch=1024, steps=20, warmup=5):
     """the fleet on the reference-default Simple3DoFGP() -- FITC,
     50 kmeans2 inducing points (structured_gp.py:423-428) -- gpmpc_fleet_create_fitc:
@@ -962,6 +999,7 @@ def main():
         if not args.no_chol and world == 1:  # single-GPU legs: the N > 1 runs keep to the metric
             legs = [("single_landing", lambda: single_landing_bench(ctx, gp)),
                     ("surface_single_landing", lambda: surface_single_landing_bench(ctx)),
+                    ("surface_gpmpc6", lambda: surface_gpmpc6_bench(ctx)),
                     ("fleet_fitc", lambda: fleet_fitc_bench(ctx)),
                     ("gpmpc_loop", lambda: gpmpc_loop_bench(ctx, gp)),
                     ("simple3dof_gp", lambda: simple3dof_gp_bench(ctx, cpu=not args.no_cpu)),

@@ -146,6 +146,8 @@ _sig("gpmpc_cov_propagate", _c, _vp, _c, _c, _c, _dp, _dp, _vp, ctypes.c_double,
 _sig("gpmpc_cov_propagate_dev", _c, _vp, _c, _c, _c, _vp, _vp, _vp, ctypes.c_double, _vp)
 _sig("gpmpc_uprop3_linear", _c, _vp, _vp, _c, _c, ctypes.c_double, ctypes.c_double, _dp, _dp, _dp, _vp,
      ctypes.c_double, _dp, _dp)
+_sig("gpmpc_uprop6_linear", _c, _vp, _vp, _vp, _c, _dp, _c, _c, ctypes.c_double, _dp, _dp, _vp,
+     ctypes.c_double, _dp, _dp)
 _sig("gpmpc_fleet_read", _c, _vp, _dp, _dp)
 _sig("gpmpc_gram_grad", _c, _vp, _c, _dp, _c, _dp, _c, _c, _dp, ctypes.c_double, _dp, _dp)
 _sig("gpmpc_fleet_get_state", _c, _vp, _dp, _dp, _dp, _dp)
@@ -183,7 +185,7 @@ EXPORTED = ["gpmpc_abi_version", "gpmpc_last_error", "gpmpc_ctx_create", "gpmpc_
             "gpmpc_qp_default_settings", "gpmpc_qp_solve_batched", "gpmpc_fleet_default_config",
             "gpmpc_fleet_create", "gpmpc_fleet_create_shard", "gpmpc_fleet_create_fitc", "gpmpc_fleet_reset", "gpmpc_fleet_step", "gpmpc_fleet_read",
             "gpmpc_fleet_step_phases", "gpmpc_fleet_get_state", "gpmpc_fleet_get_posterior", "gpmpc_fleet_set_stamps", "gpmpc_fleet_set_trace",
-            "gpmpc_syrk_batched_dev", "gpmpc_cov_propagate", "gpmpc_cov_propagate_dev", "gpmpc_uprop3_linear",
+            "gpmpc_syrk_batched_dev", "gpmpc_cov_propagate", "gpmpc_cov_propagate_dev", "gpmpc_uprop3_linear", "gpmpc_uprop6_linear",
             "gpmpc_fleet_records_dev", "gpmpc_fleet_destroy", "gpmpc_rollout6_default_config",
             "gpmpc_rollout6_create", "gpmpc_rollout6_reset", "gpmpc_rollout6_step", "gpmpc_rollout6_read",
             "gpmpc_rollout6_get_state", "gpmpc_rollout6_destroy", "gpmpc_rollout6_create_exact",
@@ -624,6 +626,28 @@ def uprop3_linear(ctx, gp, X0, U, S0=None, dt=0.1, alpha=1.0 / 30.0, g=(-1.0, 0.
         s0 = S0.ctypes.data_as(_vp)
     _chk(_L.gpmpc_uprop3_linear(ctx.h, gp.h, B, N, float(dt), float(alpha), _d(g3), _d(X0), _d(U), s0,
                                 float(s0_diag), _d(means), _d(covs)), "uprop3_linear")
+    return means, covs
+
+
+def uprop6_linear(ctx, hv, hw, exact, rocket, X0, U, S0=None, dt=0.1, s0_diag=1e-6):
+    """gpmpc_uprop6_linear: the 14-state linear uncertainty propagation of B trajectories on
+    the device.  hv, hw: the StructuredRocketGP's device pair (ExactGPHandle with exact=True,
+    else FITCHandle); rocket: 17 doubles (J_B row-major, r_T_B, g_I, alpha, g0); X0 (B, 14),
+    U (B, N, 3), S0 None or (B, 14, 14) -> means (B, N+1, 14), covariances (B, N+1, 14, 14)."""
+    X0 = f64(np.atleast_2d(X0)); U = f64(U)
+    B, N = U.shape[0], U.shape[1]
+    if X0.shape != (B, 14) or U.shape != (B, N, 3):
+        raise ValueError(f"uprop6_linear: shapes X0 {X0.shape}, U {U.shape}")
+    rk = f64(np.asarray(rocket, float).reshape(17))
+    means = np.empty((B, N + 1, 14)); covs = np.empty((B, N + 1, 14, 14))
+    s0 = None
+    if S0 is not None:
+        S0 = f64(S0)
+        if S0.shape != (B, 14, 14):
+            raise ValueError(f"uprop6_linear: S0 shape {S0.shape}")
+        s0 = S0.ctypes.data_as(_vp)
+    _chk(_L.gpmpc_uprop6_linear(ctx.h, hv.h, hw.h, int(bool(exact)), _d(rk), B, N, float(dt), _d(X0), _d(U), s0,
+                                float(s0_diag), _d(means), _d(covs)), "uprop6_linear")
     return means, covs
 
 

@@ -108,6 +108,44 @@ static const R6Impl *r6_impl(int N) {
   return N >= R6_NMIN && N <= R6_NMAX ? tab[N]() : nullptr;
 }
 // ---------------------------------------------------------------------------
+// the inertia tensor: rocket_J (ABI 4, row-major) when it is set, else diag(rocket_j).
+// A diagonal tensor runs as its diagonal (the divisions of the diagonal model); any
+// other as J and J^-1, which is formed here once (adjugate / determinant).  0, or -2
+// with the error set.
+static int r6_inertia(const double *rocket_J, const double *rocket_j, double Jd[3], double Jf[9], double Ji[9],
+                      bool &joff) {
+  bool jset = false;
+  joff = false;
+  for (int i = 0; i < 9; ++i) jset = jset || rocket_J[i] != 0.0;
+  for (int i = 0; i < 9; ++i) joff = joff || (i % 4 != 0 && rocket_J[i] != 0.0);
+  for (int i = 0; i < 3; ++i) Jd[i] = jset ? rocket_J[4 * i] : rocket_j[i];
+  if (!joff) {
+    for (int i = 0; i < 3; ++i)
+      if (!(Jd[i] > 0.0)) {
+        gpmpc_set_error("rollout6: the rocket's J_B diagonal must be positive");
+        return -2;
+      }
+    return 0;
+  }
+  for (int i = 0; i < 9; ++i) Jf[i] = rocket_J[i];
+  const double c00 = Jf[4] * Jf[8] - Jf[5] * Jf[7], c01 = Jf[5] * Jf[6] - Jf[3] * Jf[8],
+               c02 = Jf[3] * Jf[7] - Jf[4] * Jf[6];
+  const double det = Jf[0] * c00 + Jf[1] * c01 + Jf[2] * c02;
+  bool fin = std::isfinite(det);
+  for (int i = 0; i < 9; ++i) fin = fin && std::isfinite(Jf[i]);
+  double scale = 0.0;
+  for (int i = 0; i < 9; ++i) scale = std::max(scale, std::fabs(Jf[i]));
+  if (!fin || !(std::fabs(det) > 1e-14 * scale * scale * scale)) {
+    gpmpc_set_error("rollout6: the rocket's J_B must be finite and invertible");
+    return -2;
+  }
+  const double adj[9] = {c00, Jf[2] * Jf[7] - Jf[1] * Jf[8], Jf[1] * Jf[5] - Jf[2] * Jf[4],
+                         c01, Jf[0] * Jf[8] - Jf[2] * Jf[6], Jf[2] * Jf[3] - Jf[0] * Jf[5],
+                         c02, Jf[1] * Jf[6] - Jf[0] * Jf[7], Jf[0] * Jf[4] - Jf[1] * Jf[3]};
+  for (int i = 0; i < 9; ++i) Ji[i] = adj[i] / det;
+  return 0;
+}
+
 static int r6_create(gpmpc_ctx *ctx, const GpView &gv, const GpView &gw, bool exact,
                      const gpmpc_rollout6_config *cfg, int batch, gpmpc_rollout6 **out) {
   GPMPC_CHECK_ARG(ctx && cfg && out && batch > 0);
@@ -135,38 +173,9 @@ static int r6_create(gpmpc_ctx *ctx, const GpView &gv, const GpView &gw, bool ex
     gpmpc_set_error("rollout6: t_max and the trust radii must be positive");
     return -2;
   }
-  // the inertia tensor: rocket_J (ABI 4, row-major) when it is set, else diag(rocket_j).
-  // A diagonal tensor runs as its diagonal (the divisions of the diagonal model); any
-  // other as J and J^-1, which is formed here once (adjugate / determinant)
   double Jd[3], Jf[9], Ji[9];
-  bool jset = false, joff = false;
-  for (int i = 0; i < 9; ++i) jset = jset || cfg->rocket_J[i] != 0.0;
-  for (int i = 0; i < 9; ++i) joff = joff || (i % 4 != 0 && cfg->rocket_J[i] != 0.0);
-  for (int i = 0; i < 3; ++i) Jd[i] = jset ? cfg->rocket_J[4 * i] : cfg->rocket_j[i];
-  if (!joff) {
-    for (int i = 0; i < 3; ++i)
-      if (!(Jd[i] > 0.0)) {
-        gpmpc_set_error("rollout6: the rocket's J_B diagonal must be positive");
-        return -2;
-      }
-  } else {
-    for (int i = 0; i < 9; ++i) Jf[i] = cfg->rocket_J[i];
-    const double c00 = Jf[4] * Jf[8] - Jf[5] * Jf[7], c01 = Jf[5] * Jf[6] - Jf[3] * Jf[8],
-                 c02 = Jf[3] * Jf[7] - Jf[4] * Jf[6];
-    const double det = Jf[0] * c00 + Jf[1] * c01 + Jf[2] * c02;
-    bool fin = std::isfinite(det);
-    for (int i = 0; i < 9; ++i) fin = fin && std::isfinite(Jf[i]);
-    double scale = 0.0;
-    for (int i = 0; i < 9; ++i) scale = std::max(scale, std::fabs(Jf[i]));
-    if (!fin || !(std::fabs(det) > 1e-14 * scale * scale * scale)) {
-      gpmpc_set_error("rollout6: the rocket's J_B must be finite and invertible");
-      return -2;
-    }
-    const double adj[9] = {c00, Jf[2] * Jf[7] - Jf[1] * Jf[8], Jf[1] * Jf[5] - Jf[2] * Jf[4],
-                           c01, Jf[0] * Jf[8] - Jf[2] * Jf[6], Jf[2] * Jf[3] - Jf[0] * Jf[5],
-                           c02, Jf[1] * Jf[6] - Jf[0] * Jf[7], Jf[0] * Jf[4] - Jf[1] * Jf[3]};
-    for (int i = 0; i < 9; ++i) Ji[i] = adj[i] / det;
-  }
+  bool joff = false;
+  if (r6_inertia(cfg->rocket_J, cfg->rocket_j, Jd, Jf, Ji, joff)) return -2;
   if (!(cfg->rocket_alpha >= 0.0) || !(cfg->rocket_g0 > 0.0)) {
     gpmpc_set_error("rollout6: rocket alpha must be >= 0 and g0 > 0");
     return -2;
@@ -440,5 +449,189 @@ extern "C" int gpmpc_rollout6_destroy(gpmpc_rollout6 *r) {
   if (r && r->ctx) (void)hipStreamSynchronize(r->ctx->stream);
   if (r && r6_stamps_on() && r->impl) r->impl->print_stamps();
   delete r;
+  return 0;
+}
+
+// ---------------------------------------------------------------------------
+// UncertaintyPropagator._propagate_linear (uncertainty_prop.py:117-177) for the 14-state
+// model over a StructuredRocketGP pair, batch trajectories at once (gpmpc_uprop6_linear).
+// One workgroup per trajectory walks the N steps: the raw features of (x_k, u_k) (six
+// roles on six lanes, r6_features_role with unit length-scales) and -[A_d | B_d] at
+// (x_k, u_k) (r6_neg_lin, one lane of wave 1) side by side; then the features scaled by
+// each GP's length-scales (the k_scale_rows arithmetic), both GPs' means over their rows
+// (all threads, a fixed-order reduction), and on thread 0 the RK4 step with quaternion
+// normalisation (rocket_6dof.py step) plus dt d_v / dt d_w on the velocity / rate rows.
+// The variances of all B N queries then come from each GP's batched posterior, and one
+// launch propagates every covariance (k_cov_propagate).
+__global__ __launch_bounds__(256) void k_uprop6_means(GpView gv, GpView gw, R6Rocket rk, int N, double dt,
+                                                      const double *__restrict__ x0, const double *__restrict__ U,
+                                                      double *__restrict__ Qv, double *__restrict__ Qw,
+                                                      double *__restrict__ A, double *__restrict__ means) {
+  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  __shared__ double sx[R6_NX], su[R6_NU], qv[13], qw[12], zv[13], zw[12], red[4][6];
+  __shared__ double blk[R6_NX * R6_SZ];
+  if (tid < R6_NX) {
+    sx[tid] = x0[(int64_t)b * R6_NX + tid];
+    means[(int64_t)b * (N + 1) * R6_NX + tid] = sx[tid];
+  }
+  __syncthreads();
+  for (int k = 0; k < N; ++k) {
+    const int64_t pk = (int64_t)b * N + k;
+    if (tid < R6_NU) su[tid] = U[pk * R6_NU + tid];
+    __syncthreads();
+    if (tid < R6_FEAT_ROLES) {
+      const double one[13] = {1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1};
+      r6_features_role(tid, sx, su, one, one, qv, qw);
+    } else if (tid == 64) {
+      for (int e = 0; e < R6_NX * R6_SZ; ++e) blk[e] = 0.0;
+      r6_neg_lin(rk, sx, su, dt, blk);
+    }
+    __syncthreads();
+    if (tid < 13) {
+      zv[tid] = gv.kind == GPMPC_SE_ISO ? qv[tid] : qv[tid] / gv.ls[tid];
+      Qv[pk * 13 + tid] = qv[tid];
+    } else if (tid >= 64 && tid < 76) {
+      const int f = tid - 64;
+      zw[f] = gw.kind == GPMPC_SE_ISO ? qw[f] : qw[f] / gw.ls[f];
+      Qw[pk * 12 + f] = qw[f];
+    } else if (tid >= 128 && tid < 128 + 98) {  // A_k = I + A_c dt = -(the block's first 14 columns)
+      for (int e = tid - 128; e < R6_NX * R6_NX; e += 98) {
+        const int r = e / R6_NX, c = e - r * R6_NX;
+        A[pk * R6_NX * R6_NX + e] = -blk[r * R6_SZ + c];
+      }
+    }
+    __syncthreads();
+    double acc[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+    {
+      double z[13], zn = 0.0;
+#pragma unroll
+      for (int f = 0; f < 13; ++f) { z[f] = zv[f]; zn += z[f] * z[f]; }
+      for (int j = tid; j < gv.n; j += 256) {
+        double dot = 0.0;
+#pragma unroll
+        for (int f = 0; f < 13; ++f) dot = fma(z[f], gv.Xs[(int64_t)j * 13 + f], dot);
+        const double kv = kernel_epilogue(gv.kind, (zn + gv.Xn[j]) - 2.0 * dot, gv.sigma2, gv.iso_scale);
+#pragma unroll
+        for (int c = 0; c < 3; ++c) acc[c] = fma(kv, gv.alphaT[(int64_t)c * gv.n + j], acc[c]);
+      }
+    }
+    {
+      double z[12], zn = 0.0;
+#pragma unroll
+      for (int f = 0; f < 12; ++f) { z[f] = zw[f]; zn += z[f] * z[f]; }
+      for (int j = tid; j < gw.n; j += 256) {
+        double dot = 0.0;
+#pragma unroll
+        for (int f = 0; f < 12; ++f) dot = fma(z[f], gw.Xs[(int64_t)j * 12 + f], dot);
+        const double kv = kernel_epilogue(gw.kind, (zn + gw.Xn[j]) - 2.0 * dot, gw.sigma2, gw.iso_scale);
+#pragma unroll
+        for (int c = 0; c < 3; ++c) acc[3 + c] = fma(kv, gw.alphaT[(int64_t)c * gw.n + j], acc[3 + c]);
+      }
+    }
+#pragma unroll
+    for (int c = 0; c < 6; ++c)
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) acc[c] += __shfl_xor(acc[c], o);
+    if (lane == 0)
+      for (int c = 0; c < 6; ++c) red[wave][c] = acc[c];
+    __syncthreads();
+    if (tid == 0) {
+      double d[6];
+      for (int c = 0; c < 6; ++c) {
+        const double m = ((red[0][c] + red[1][c]) + red[2][c]) + red[3][c];
+        const GpView &g = c < 3 ? gv : gw;
+        d[c] = m * g.ystd[c % 3] + g.ymean[c % 3];
+      }
+      double xn[R6_NX];
+      r6_step(rk, sx, su, dt, xn);
+      for (int c = 0; c < 3; ++c) {
+        xn[4 + c] = xn[4 + c] + d[c] * dt;
+        xn[11 + c] = xn[11 + c] + d[3 + c] * dt;
+      }
+      for (int i = 0; i < R6_NX; ++i) {
+        sx[i] = xn[i];
+        means[((int64_t)b * (N + 1) + k + 1) * R6_NX + i] = xn[i];
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// q_k = var dt^2 on the velocity rows 4-6 (d_v) and the rate rows 11-13 (d_omega)
+__global__ void k_uprop6_q(int P, double dt2, const double *__restrict__ vv, const double *__restrict__ vw,
+                           double *__restrict__ q) {
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= P) return;
+  for (int i = 0; i < R6_NX; ++i) {
+    double v = 0.0;
+    if (i >= 4 && i < 7) v = vv[(int64_t)j * 3 + i - 4] * dt2;
+    if (i >= 11) v = vw[(int64_t)j * 3 + i - 11] * dt2;
+    q[(int64_t)j * R6_NX + i] = v;
+  }
+}
+
+extern "C" int gpmpc_uprop6_linear(gpmpc_ctx *ctx, void *gp_v, void *gp_w, int exact, const double *rocket,
+                                   int batch, int N, double dt, const double *x0, const double *U,
+                                   const double *S0, double s0_diag, double *means, double *covs) {
+  GPMPC_CHECK_ARG(ctx && gp_v && gp_w && rocket && x0 && U && means && covs && batch >= 0 && N >= 0);
+  const GpView gv = exact ? gp_view((gpmpc_gp *)gp_v) : fitc_view((gpmpc_fitc *)gp_v);
+  const GpView gw = exact ? gp_view((gpmpc_gp *)gp_w) : fitc_view((gpmpc_fitc *)gp_w);
+  if (gv.d != 13 || gw.d != 12 || gv.n_out != 3 || gw.n_out != 3 || gv.kind == GPMPC_KPROG ||
+      gw.kind == GPMPC_KPROG) {
+    gpmpc_set_error("uprop6_linear: needs the StructuredRocketGP pair (13 / 12 features, 3 outputs, leaf kernels)");
+    return -2;
+  }
+  // rocket: J_B (9, row-major), r_T_B (3), g_I (3), alpha, g0
+  R6Rocket rk{};
+  double Jd[3], Jf[9] = {}, Ji[9] = {};
+  bool joff = false;
+  const double jdiag[3] = {rocket[0], rocket[4], rocket[8]};
+  if (r6_inertia(rocket, jdiag, Jd, Jf, Ji, joff)) return -2;
+  for (int i = 0; i < 3; ++i) { rk.J[i] = Jd[i]; rk.rT[i] = rocket[9 + i]; rk.gI[i] = rocket[12 + i]; }
+  for (int i = 0; i < 9; ++i) { rk.Jf[i] = Jf[i]; rk.Ji[i] = Ji[i]; }
+  rk.full = joff;
+  rk.alpha = rocket[15];
+  rk.g0 = rocket[16];
+  if (batch == 0) return 0;
+  GPMPC_HIP(hipSetDevice(ctx->device));
+  hipStream_t s = ctx->stream;
+  const size_t B = batch, P = B * N;
+  DevBuf dQv, dQw, dA, dq, mv, vv, mw, vw;
+  GPMPC_HIP(dQv.alloc(s, sizeof(double) * (P * 13 + 1)));
+  GPMPC_HIP(dQw.alloc(s, sizeof(double) * (P * 12 + 1)));
+  GPMPC_HIP(dA.alloc(s, sizeof(double) * (P * R6_NX * R6_NX + 1)));
+  GPMPC_HIP(dq.alloc(s, sizeof(double) * (P * R6_NX + 1)));
+  // inputs in one pinned upload, means and covariances in one read-back
+  const size_t bytes = Stage::pad(8 * B * R6_NX) + Stage::pad(8 * P * R6_NU) +
+                       (S0 ? Stage::pad(8 * B * R6_NX * R6_NX) : 0) + Stage::pad(8 * B * (N + 1) * R6_NX) +
+                       Stage::pad(8 * B * (N + 1) * R6_NX * R6_NX);
+  Stage sg(s, bytes);
+  if (!sg.ok()) {
+    gpmpc_set_error("uprop6_linear: staging buffers: out of memory");
+    return -1;
+  }
+  const double *dx0 = sg.in(x0, B * R6_NX), *dU = sg.in(U, P * R6_NU);
+  const double *dS0 = S0 ? sg.in(S0, B * R6_NX * R6_NX) : nullptr;
+  double *dmeans = sg.out(means, B * (N + 1) * R6_NX), *dcov = sg.out(covs, B * (N + 1) * R6_NX * R6_NX);
+  GPMPC_HIP(sg.upload());
+  hipLaunchKernelGGL(k_uprop6_means, dim3(batch), dim3(256), 0, s, gv, gw, rk, N, dt, dx0, dU, dQv.as<double>(),
+                     dQw.as<double>(), dA.as<double>(), dmeans);
+  GPMPC_HIP(hipGetLastError());
+  if (P) {
+    for (DevBuf *d : {&mv, &vv, &mw, &vw}) GPMPC_HIP(d->alloc(s, sizeof(double) * P * 3));
+    int rc = exact ? gp_posterior_dev(ctx, (gpmpc_gp *)gp_v, dQv.as<double>(), (int)P, mv.as<double>(), vv.as<double>())
+                   : fitc_posterior_dev(ctx, (gpmpc_fitc *)gp_v, dQv.as<double>(), (int)P, mv.as<double>(),
+                                        vv.as<double>());
+    if (rc) return rc;
+    rc = exact ? gp_posterior_dev(ctx, (gpmpc_gp *)gp_w, dQw.as<double>(), (int)P, mw.as<double>(), vw.as<double>())
+               : fitc_posterior_dev(ctx, (gpmpc_fitc *)gp_w, dQw.as<double>(), (int)P, mw.as<double>(), vw.as<double>());
+    if (rc) return rc;
+    hipLaunchKernelGGL(k_uprop6_q, dim3((unsigned)((P + 255) / 256)), dim3(256), 0, s, (int)P, dt * dt,
+                       vv.as<double>(), vw.as<double>(), dq.as<double>());
+    GPMPC_HIP(hipGetLastError());
+  }
+  const int rc = gpmpc_cov_propagate_dev(ctx, batch, N, R6_NX, dA.as<double>(), dq.as<double>(), dS0, s0_diag, dcov);
+  if (rc) return rc;
+  GPMPC_HIP(sg.download());
   return 0;
 }

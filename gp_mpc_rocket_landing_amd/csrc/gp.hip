@@ -1149,18 +1149,13 @@ extern "C" int gpmpc_sparse_fit_prog(gpmpc_ctx *ctx, int method, const int *ops,
                     method == 0 ? lambda_diag : nullptr, method, &prog);
 }
 
-extern "C" int gpmpc_fitc_predict(gpmpc_ctx *ctx, gpmpc_fitc *gp, const double *Xq, int p,
-                                  double *mean, double *var) {
-  GPMPC_CHECK_ARG(ctx && gp && Xq && mean && var && p >= 0);
-  if (p == 0) return 0;
-  GPMPC_HIP(hipSetDevice(ctx->device));
+// the FITC posterior of p device-resident raw query rows (sparse_gp.py:255-305): mean / var (p x n_out)
+int fitc_posterior_dev(gpmpc_ctx *ctx, gpmpc_fitc *gp, const double *dq, int p, double *dmean, double *dvar) {
   hipStream_t s = ctx->stream;
   const GpCore &g = gp->core;
   const int m = gp->m;
-  DevBuf dq, Ks, pv, pw, meanT, dmean, dvar;
-  GPMPC_HIP(dq.alloc(s, sizeof(double) * p * g.d));
-  GPMPC_HIP(hipMemcpyAsync(dq.p, Xq, sizeof(double) * p * g.d, hipMemcpyHostToDevice, s));
-  int rc = core_cross(ctx, g, dq.as<double>(), p, Ks);  // K*u (p x m)
+  DevBuf Ks, pv, pw, meanT;
+  int rc = core_cross(ctx, g, dq, p, Ks);  // K*u (p x m)
   if (rc) return rc;
   const int nrv = gemm_row_tiles(m + g.n_out, p, m), nrw = gemm_row_tiles(m, p, m);
   GPMPC_HIP(pv.alloc(s, sizeof(double) * (size_t)nrv * p));
@@ -1171,16 +1166,31 @@ extern "C" int gpmpc_fitc_predict(gpmpc_ctx *ctx, gpmpc_fitc *gp, const double *
                                    pv.as<double>(), p, meanT.as<double>(), p));
   GPMPC_HIP(launch_gemm_nt(s, EPI_SUMSQ, m, p, m, gp->W2.as<double>(), m, Ks.as<double>(), m,
                            pw.as<double>(), p, 1.0, 0.0, 1, 0, 1, 0, 0, 0));
-  GPMPC_HIP(dmean.alloc(s, sizeof(double) * p * g.n_out));
-  GPMPC_HIP(dvar.alloc(s, sizeof(double) * p * g.n_out));
   hipLaunchKernelGGL(k_fitc_finish, dim3((p + 255) / 256), dim3(256), 0, s, p, g.n_out, nrv, nrw,
                      pv.as<double>(), pw.as<double>(), (int64_t)p, meanT.as<double>(), (int64_t)p,
-                     g.ymean.as<double>(), g.ystd.as<double>(), g.sigma2, dmean.as<double>(),
-                     dvar.as<double>());
+                     g.ymean.as<double>(), g.ystd.as<double>(), g.sigma2, dmean, dvar);
   GPMPC_HIP(hipGetLastError());
-  GPMPC_HIP(hipMemcpyAsync(mean, dmean.p, sizeof(double) * p * g.n_out, hipMemcpyDeviceToHost, s));
-  GPMPC_HIP(hipMemcpyAsync(var, dvar.p, sizeof(double) * p * g.n_out, hipMemcpyDeviceToHost, s));
-  GPMPC_HIP(hipStreamSynchronize(s));
+  return 0;
+}
+
+extern "C" int gpmpc_fitc_predict(gpmpc_ctx *ctx, gpmpc_fitc *gp, const double *Xq, int p,
+                                  double *mean, double *var) {
+  GPMPC_CHECK_ARG(ctx && gp && Xq && mean && var && p >= 0);
+  if (p == 0) return 0;
+  GPMPC_HIP(hipSetDevice(ctx->device));
+  const GpCore &g = gp->core;
+  // the queries in one pinned upload, mean and variance in one read-back
+  const size_t P = p, bo = Stage::pad(8 * P * g.n_out);
+  Stage sg(ctx->stream, Stage::pad(8 * P * g.d) + 2 * bo);
+  if (!sg.ok()) {
+    gpmpc_set_error("fitc_predict: staging buffers: out of memory");
+    return -1;
+  }
+  double *dq = sg.in(Xq, P * g.d), *dmean = sg.out(mean, P * g.n_out), *dvar = sg.out(var, P * g.n_out);
+  GPMPC_HIP(sg.upload());
+  const int rc = fitc_posterior_dev(ctx, gp, dq, p, dmean, dvar);
+  if (rc) return rc;
+  GPMPC_HIP(sg.download());
   return 0;
 }
 

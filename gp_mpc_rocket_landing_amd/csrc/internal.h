@@ -220,6 +220,8 @@ struct GpView {
 GpView gp_view(const gpmpc_gp *gp);
 // the exact GP's posterior of p device-resident raw query rows (gp.hip): mean / var (p x n_out)
 int gp_posterior_dev(gpmpc_ctx *ctx, gpmpc_gp *gp, const double *dq, int p, double *dmean, double *dvar);
+// the same for a FITC GP (gp.hip, the gpmpc_fitc_predict arithmetic)
+int fitc_posterior_dev(gpmpc_ctx *ctx, gpmpc_fitc *gp, const double *dq, int p, double *dmean, double *dvar);
 // the same view of a FITC GP: n = inducing points, Xs / Xn their scaled rows, alphaT
 GpView fitc_view(const gpmpc_fitc *gp);
 // its W2 = L_B^-1 L_uu^-1 (n x n lower): the predict's w = W2 k* (sparse_gp.py:293-296)

@@ -94,6 +94,35 @@ class UncertaintyPropagator:
     # host loop below become one kernel; the same recursion, rounding aside
     use_device = True
 
+    def _device_6dof(self, X0, U, Sigma_0, dt):
+        """gpmpc_uprop6_linear for Rocket6DoFDynamics over a fitted StructuredRocketGP at its
+        default feature set (the device features are features.py's at reference velocity
+        10 with altitude and density), its residual groups each one shared device GP."""
+        if not self.use_device or self.n_x != 14:
+            return None
+        from ..dynamics.rocket_6dof import Rocket6DoFDynamics
+        from ..gp.structured_gp import StructuredRocketGP
+        gp = self.gp
+        if type(self.dynamics) is not Rocket6DoFDynamics or type(gp) is not StructuredRocketGP:
+            return None
+        c = gp.config
+        if not (gp._is_fitted and c.reference_velocity == 10.0 and c.include_altitude and c.include_density):
+            return None
+        hv, hw = gp.gp_v.device_handle, gp.gp_omega.device_handle
+        if hv is None or hw is None:
+            return None
+        p = self.dynamics.params
+        rocket = np.concatenate([np.asarray(p.J_B, float).reshape(9), np.asarray(p.r_T_B, float).reshape(3),
+                                 np.asarray(p.g_I, float).reshape(3),
+                                 [float(p.alpha), float(p.g0)]])
+        S0 = None
+        if Sigma_0 is not None:
+            S0 = np.broadcast_to(np.asarray(Sigma_0, float), (X0.shape[0], 14, 14))
+        try:
+            return _lib.uprop6_linear(self.ctx, hv, hw, not c.use_sparse, rocket, X0, U, S0, dt)
+        except _lib.HIPError:
+            return None   # (a composite-kernel GP: the host loop)
+
     def _device_3dof(self, X0, U, Sigma_0, dt):
         if not self.use_device or self.n_x != 7:
             return None
@@ -142,6 +171,8 @@ class UncertaintyPropagator:
         if X0.shape != (B, nx):
             raise ValueError(f"X0 shape {X0.shape}, expected {(B, nx)}")
         dev = self._device_3dof(X0, U, Sigma_0, dt)
+        if dev is None:
+            dev = self._device_6dof(X0, U, Sigma_0, dt)
         if dev is not None:
             return dev
         rv, rw = self._rows()

@@ -349,6 +349,19 @@ int gpmpc_cov_propagate_dev(gpmpc_ctx *ctx, int batch, int N, int nx, const doub
 int gpmpc_uprop3_linear(gpmpc_ctx *ctx, gpmpc_gp *gp, int batch, int N, double dt, double alpha,
                         const double *g3, const double *x0, const double *U, const double *S0,
                         double s0_diag, double *means, double *covs);
+/* The same for the 14-state model (uncertainty_prop.py:117-177 as GPMPC.solve runs it for
+ * Rocket6DoFDynamics, gp_mpc.py:284-290): RK4 with quaternion normalisation
+ * (rocket_6dof.py step) plus dt times the StructuredRocketGP means on the velocity
+ * (rows 4-6, d_v) and rate rows (11-13, d_omega), A_k = I + dt J(x_k, u_k), q_k = dt^2 times
+ * the GP variances on those rows.  gp_v / gp_w: the pair's device GPs, gpmpc_gp * (exact = 1)
+ * or gpmpc_fitc * (exact = 0), 13 / 12 features and 3 outputs each, leaf kernels (else -2).
+ * rocket: J_B (9, row-major; invertible), r_T_B (3), g_I (3), alpha = 1 / (I_sp g0), g0.
+ * Host buffers: x0 (batch x 14), U (batch x N x 3), S0 (batch x 14 x 14) or NULL (s0_diag I)
+ * in; means (batch x (N+1) x 14), covs (batch x (N+1) x 14 x 14) out.  (Round 6, ABI 4: an
+ * added entry point.) */
+int gpmpc_uprop6_linear(gpmpc_ctx *ctx, void *gp_v, void *gp_w, int exact, const double *rocket,
+                        int batch, int N, double dt, const double *x0, const double *U,
+                        const double *S0, double s0_diag, double *means, double *covs);
 
 /* ---- BASELINE configs[4]: batched 6-DoF GP-MPC rollouts --------------------
  * gpmpc_rollout_batched of SURVEY 8b.  One step = for every running rollout:

@@ -207,3 +207,51 @@ def test_propagate_batch_3dof_device_training_sizes(gpu_ctx, n):
     mh, ch = p.propagate_batch(X0, Uh, None, 0.1)
     np.testing.assert_allclose(md, mh, rtol=1e-10, atol=1e-10)
     np.testing.assert_allclose(cd, ch, rtol=1e-7, atol=1e-15)
+
+
+@pytest.mark.parametrize("sparse,full_j,s0", [(True, False, False), (False, False, True), (True, True, False)])
+def test_propagate_batch_6dof_device_vs_host_loop(gpu_ctx, sparse, full_j, s0):
+    """gpmpc_uprop6_linear (the 14-state linear propagation in one device call) vs the
+    per-step host loop over the same StructuredRocketGP device pair: FITC (the reference
+    default) and exact, a diagonal and a full inertia tensor, with and without Sigma_0.
+    The device features and Jacobian are restated expressions of the host's (rounding
+    aside) and the GP means sum in another order, so the two agree to ~1e-12."""
+    _ctx_default(gpu_ctx)
+    from gp_mpc_rocket_landing_amd import _lib
+    from gp_mpc_rocket_landing_amd.dynamics import Rocket6DoFConfig, Rocket6DoFDynamics
+    from gp_mpc_rocket_landing_amd.mpc import UncertaintyPropagator
+    from gp_mpc_rocket_landing_amd.rollouts6 import fit_structured_gp, initial_conditions_6dof
+    gp = fit_structured_gp(300, 50, seed=0, use_sparse=sparse)
+    rc = Rocket6DoFConfig()
+    if full_j:
+        J = np.array(rc.J_B, float)
+        J = J + 0.05 * np.sqrt(np.outer(np.diag(J), np.diag(J))) * np.array([[0, 1, -1], [1, 0, 0.5], [-1, 0.5, 0]])
+        rc = Rocket6DoFConfig(J_B=J)
+    dyn = Rocket6DoFDynamics(rc)
+    B, N = 3, 12
+    X0 = initial_conditions_6dof(B)
+    X0[:, 11:14] = np.array([0.02, -0.01, 0.03])
+    rs = np.random.RandomState(7)
+    U = np.zeros((B, N, 3))
+    U[:, :, 2] = 0.9 * X0[:, 0:1] * rc.g0
+    U[:, :, :2] = 0.05 * rs.randn(B, N, 2)
+    S0 = None
+    if s0:
+        L = rs.randn(B, 14, 14) * 1e-3
+        S0 = np.einsum("bij,bkj->bik", L, L)
+    calls = []
+    real = _lib.uprop6_linear
+    monkeypatch = pytest.MonkeyPatch()
+    monkeypatch.setattr(_lib, "uprop6_linear", lambda *a, **k: calls.append(1) or real(*a, **k))
+    try:
+        p = UncertaintyPropagator(dyn, gp, ctx=gpu_ctx)
+        md, cd = p.propagate_batch(X0, U, S0, 0.1)
+        assert calls, "the device path was not taken"
+        p.use_device = False
+        mh, ch = p.propagate_batch(X0, U, S0, 0.1)
+    finally:
+        monkeypatch.undo()
+    assert md.shape == (B, N + 1, 14) and cd.shape == (B, N + 1, 14, 14)
+    np.testing.assert_array_equal(md[:, 0], X0)
+    np.testing.assert_allclose(md, mh, rtol=1e-10, atol=1e-11)
+    np.testing.assert_allclose(cd, ch, rtol=1e-7, atol=1e-15)
