@@ -468,23 +468,42 @@ __global__ __launch_bounds__(256) void k_uprop6_means(GpView gv, GpView gw, R6Ro
                                                       double *__restrict__ Qv, double *__restrict__ Qw,
                                                       double *__restrict__ A, double *__restrict__ means) {
   const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  __shared__ double sx[R6_NX], su[R6_NU], qv[13], qw[12], zv[13], zw[12], red[4][6];
+  __shared__ double sx[R6_NX], sxn[R6_NX], su[R6_NU], qv[13], qw[12], zv[13], zw[12], red[4][6];
   __shared__ double blk[R6_NX * R6_SZ];
+  // this thread's rows of each GP (row tid), held in registers for the N steps when both
+  // GPs have at most 256 rows (FITC inducing sets); else read per step
+  const bool reg = gv.n <= 256 && gw.n <= 256;
+  double xv[13], xw[12], nv = 0.0, nw = 0.0, av[3] = {0.0, 0.0, 0.0}, aw[3] = {0.0, 0.0, 0.0};
+  const bool okv = reg && tid < gv.n, okw = reg && tid < gw.n;
+#pragma unroll
+  for (int f = 0; f < 13; ++f) xv[f] = okv ? gv.Xs[(int64_t)tid * 13 + f] : 0.0;
+#pragma unroll
+  for (int f = 0; f < 12; ++f) xw[f] = okw ? gw.Xs[(int64_t)tid * 12 + f] : 0.0;
+  if (okv) {
+    nv = gv.Xn[tid];
+    for (int c = 0; c < 3; ++c) av[c] = gv.alphaT[(int64_t)c * gv.n + tid];
+  }
+  if (okw) {
+    nw = gw.Xn[tid];
+    for (int c = 0; c < 3; ++c) aw[c] = gw.alphaT[(int64_t)c * gw.n + tid];
+  }
   if (tid < R6_NX) {
     sx[tid] = x0[(int64_t)b * R6_NX + tid];
     means[(int64_t)b * (N + 1) * R6_NX + tid] = sx[tid];
   }
+  if (tid < R6_NU && N > 0) su[tid] = U[(int64_t)b * N * R6_NU + tid];
   __syncthreads();
   for (int k = 0; k < N; ++k) {
     const int64_t pk = (int64_t)b * N + k;
-    if (tid < R6_NU) su[tid] = U[pk * R6_NU + tid];
-    __syncthreads();
+    // the raw features (six roles, six lanes), -[A_d | B_d] and the nominal RK4 step, side by side
     if (tid < R6_FEAT_ROLES) {
       const double one[13] = {1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1};
       r6_features_role(tid, sx, su, one, one, qv, qw);
     } else if (tid == 64) {
       for (int e = 0; e < R6_NX * R6_SZ; ++e) blk[e] = 0.0;
       r6_neg_lin(rk, sx, su, dt, blk);
+    } else if (tid == 255) {
+      r6_step(rk, sx, su, dt, sxn);
     }
     __syncthreads();
     if (tid < 13) {
@@ -506,26 +525,48 @@ __global__ __launch_bounds__(256) void k_uprop6_means(GpView gv, GpView gw, R6Ro
       double z[13], zn = 0.0;
 #pragma unroll
       for (int f = 0; f < 13; ++f) { z[f] = zv[f]; zn += z[f] * z[f]; }
-      for (int j = tid; j < gv.n; j += 256) {
-        double dot = 0.0;
+      if (reg) {
+        if (okv) {
+          double dot = 0.0;
 #pragma unroll
-        for (int f = 0; f < 13; ++f) dot = fma(z[f], gv.Xs[(int64_t)j * 13 + f], dot);
-        const double kv = kernel_epilogue(gv.kind, (zn + gv.Xn[j]) - 2.0 * dot, gv.sigma2, gv.iso_scale);
+          for (int f = 0; f < 13; ++f) dot = fma(z[f], xv[f], dot);
+          const double kv = kernel_epilogue(gv.kind, (zn + nv) - 2.0 * dot, gv.sigma2, gv.iso_scale);
 #pragma unroll
-        for (int c = 0; c < 3; ++c) acc[c] = fma(kv, gv.alphaT[(int64_t)c * gv.n + j], acc[c]);
+          for (int c = 0; c < 3; ++c) acc[c] = fma(kv, av[c], acc[c]);
+        }
+      } else {
+        for (int j = tid; j < gv.n; j += 256) {
+          double dot = 0.0;
+#pragma unroll
+          for (int f = 0; f < 13; ++f) dot = fma(z[f], gv.Xs[(int64_t)j * 13 + f], dot);
+          const double kv = kernel_epilogue(gv.kind, (zn + gv.Xn[j]) - 2.0 * dot, gv.sigma2, gv.iso_scale);
+#pragma unroll
+          for (int c = 0; c < 3; ++c) acc[c] = fma(kv, gv.alphaT[(int64_t)c * gv.n + j], acc[c]);
+        }
       }
     }
     {
       double z[12], zn = 0.0;
 #pragma unroll
       for (int f = 0; f < 12; ++f) { z[f] = zw[f]; zn += z[f] * z[f]; }
-      for (int j = tid; j < gw.n; j += 256) {
-        double dot = 0.0;
+      if (reg) {
+        if (okw) {
+          double dot = 0.0;
 #pragma unroll
-        for (int f = 0; f < 12; ++f) dot = fma(z[f], gw.Xs[(int64_t)j * 12 + f], dot);
-        const double kv = kernel_epilogue(gw.kind, (zn + gw.Xn[j]) - 2.0 * dot, gw.sigma2, gw.iso_scale);
+          for (int f = 0; f < 12; ++f) dot = fma(z[f], xw[f], dot);
+          const double kv = kernel_epilogue(gw.kind, (zn + nw) - 2.0 * dot, gw.sigma2, gw.iso_scale);
 #pragma unroll
-        for (int c = 0; c < 3; ++c) acc[3 + c] = fma(kv, gw.alphaT[(int64_t)c * gw.n + j], acc[3 + c]);
+          for (int c = 0; c < 3; ++c) acc[3 + c] = fma(kv, aw[c], acc[3 + c]);
+        }
+      } else {
+        for (int j = tid; j < gw.n; j += 256) {
+          double dot = 0.0;
+#pragma unroll
+          for (int f = 0; f < 12; ++f) dot = fma(z[f], gw.Xs[(int64_t)j * 12 + f], dot);
+          const double kv = kernel_epilogue(gw.kind, (zn + gw.Xn[j]) - 2.0 * dot, gw.sigma2, gw.iso_scale);
+#pragma unroll
+          for (int c = 0; c < 3; ++c) acc[3 + c] = fma(kv, gw.alphaT[(int64_t)c * gw.n + j], acc[3 + c]);
+        }
       }
     }
 #pragma unroll
@@ -543,7 +584,7 @@ __global__ __launch_bounds__(256) void k_uprop6_means(GpView gv, GpView gw, R6Ro
         d[c] = m * g.ystd[c % 3] + g.ymean[c % 3];
       }
       double xn[R6_NX];
-      r6_step(rk, sx, su, dt, xn);
+      for (int i = 0; i < R6_NX; ++i) xn[i] = sxn[i];
       for (int c = 0; c < 3; ++c) {
         xn[4 + c] = xn[4 + c] + d[c] * dt;
         xn[11 + c] = xn[11 + c] + d[3 + c] * dt;
@@ -552,6 +593,8 @@ __global__ __launch_bounds__(256) void k_uprop6_means(GpView gv, GpView gw, R6Ro
         sx[i] = xn[i];
         means[((int64_t)b * (N + 1) + k + 1) * R6_NX + i] = xn[i];
       }
+    } else if (tid >= 1 && tid <= R6_NU && k + 1 < N) {
+      su[tid - 1] = U[(pk + 1) * R6_NU + tid - 1];  // the next step's controls
     }
     __syncthreads();
   }

@@ -7,59 +7,73 @@
 // and on the angular-rate block for 6-DoF), A_k the discrete Jacobian of the
 // nominal step.  The mean recursion does not depend on Sigma, so the host
 // (or the fleet) produces every A_k and q_k first and one launch runs all
-// trajectories.  One 64-lane wave per trajectory; n_x <= 16, so Sigma, A_k and
-// the product A_k Sigma_k live in LDS and each lane owns up to 4 of the n_x^2
-// entries.  HBM traffic per trajectory-step: read A_k (8 n_x^2 B) and q_k
-// (8 n_x B), write Sigma_{k+1} (8 n_x^2 B).
+// trajectories.  One workgroup per trajectory with one thread per entry of Sigma (n_x <=
+// 16: 64 threads at n_x = 7, 256 at 14), so a step is two n_x-term dot products per
+// thread and two barriers; the A_k and q_k of UP_CHUNK steps are staged into LDS in one
+// cooperative load, off the step chain (one global round trip per chunk, not per step).
+// HBM traffic per trajectory-step: read A_k (8 n_x^2 B) and q_k (8 n_x B), write
+// Sigma_{k+1} (8 n_x^2 B).
 #include "internal.h"
 
 #define UP_NXMAX 16
 
-__global__ __launch_bounds__(64) void k_cov_propagate(int N, int nx, const double *__restrict__ A,
-                                                      const double *__restrict__ q,
-                                                      const double *__restrict__ S0, double s0_diag,
-                                                      double *__restrict__ out) {
-  __shared__ double sA[UP_NXMAX][UP_NXMAX + 1];
+#define UP_CHUNK 16
+
+__global__ __launch_bounds__(256) void k_cov_propagate(int N, int nx, const double *__restrict__ A,
+                                                       const double *__restrict__ q,
+                                                       const double *__restrict__ S0, double s0_diag,
+                                                       double *__restrict__ out) {
+  __shared__ double sA[UP_CHUNK][UP_NXMAX][UP_NXMAX + 1];
+  __shared__ double sq[UP_CHUNK][UP_NXMAX];
   __shared__ double sS[UP_NXMAX][UP_NXMAX + 1];
   __shared__ double sT[UP_NXMAX][UP_NXMAX + 1];
-  const int b = blockIdx.x, lane = threadIdx.x, nn = nx * nx;
+  const int b = blockIdx.x, e = threadIdx.x, nt = blockDim.x, nn = nx * nx;
   const int64_t mat = (int64_t)nn;
+  const bool act = e < nn;
+  const int i = act ? e / nx : 0, j = act ? e - (e / nx) * nx : 0;
   double *ob = out + (int64_t)b * (N + 1) * mat;
-  for (int e = lane; e < nn; e += 64) {
-    const int i = e / nx, j = e % nx;
+  if (act) {
     const double v = S0 ? S0[(int64_t)b * mat + e] : (i == j ? s0_diag : 0.0);
     sS[i][j] = v;
     ob[e] = v;
   }
-  for (int k = 0; k < N; ++k) {
-    const double *Ak = A + ((int64_t)b * N + k) * mat;
-    const double *qk = q + ((int64_t)b * N + k) * nx;
-    for (int e = lane; e < nn; e += 64) sA[e / nx][e % nx] = Ak[e];
-    __syncthreads();
-    for (int e = lane; e < nn; e += 64) {  // T = A Sigma
-      const int i = e / nx, j = e % nx;
-      double t = 0.0;
-      for (int c = 0; c < nx; ++c) t = fma(sA[i][c], sS[c][j], t);
-      sT[i][j] = t;
+  for (int k0 = 0; k0 < N; k0 += UP_CHUNK) {
+    const int kc = min(UP_CHUNK, N - k0);
+    const double *Ac = A + ((int64_t)b * N + k0) * mat;
+    const double *qc = q + ((int64_t)b * N + k0) * nx;
+    for (int t = e; t < kc * nn; t += nt) {
+      const int kk = t / nn, r = t - kk * nn, ri = r / nx;
+      sA[kk][ri][r - ri * nx] = Ac[t];
+    }
+    for (int t = e; t < kc * nx; t += nt) {
+      const int kk = t / nx;
+      sq[kk][t - kk * nx] = qc[t];
     }
     __syncthreads();
-    double *ok = ob + (int64_t)(k + 1) * mat;
-    for (int e = lane; e < nn; e += 64) {  // Sigma' = T A^T + diag(q)
-      const int i = e / nx, j = e % nx;
-      double t = 0.0;
-      for (int c = 0; c < nx; ++c) t = fma(sT[i][c], sA[j][c], t);
-      if (i == j) t += qk[i];
-      ok[e] = t;
-      sS[i][j] = t;
+    for (int kk = 0; kk < kc; ++kk) {
+      if (act) {  // T = A Sigma
+        double t = 0.0;
+        for (int c = 0; c < nx; ++c) t = fma(sA[kk][i][c], sS[c][j], t);
+        sT[i][j] = t;
+      }
+      __syncthreads();
+      if (act) {  // Sigma' = T A^T + diag(q)
+        double t = 0.0;
+        for (int c = 0; c < nx; ++c) t = fma(sT[i][c], sA[kk][j][c], t);
+        if (i == j) t += sq[kk][i];
+        ob[(int64_t)(k0 + kk + 1) * mat + e] = t;
+        sS[i][j] = t;
+      }
+      __syncthreads();
     }
-    __syncthreads();
   }
 }
 
 static hipError_t launch_cov_propagate(hipStream_t s, int batch, int N, int nx, const double *A,
                                        const double *q, const double *S0, double s0_diag,
                                        double *out) {
-  hipLaunchKernelGGL(k_cov_propagate, dim3(batch), dim3(64), 0, s, N, nx, A, q, S0, s0_diag, out);
+  hipLaunchKernelGGL(k_cov_propagate, dim3(batch), dim3((nx * nx + 63) / 64 * 64), 0, s, N, nx, A, q, S0, s0_diag,
+                     out);
   return hipGetLastError();
 }
 
