@@ -139,3 +139,14 @@ def test_rollout6_default_config_is_the_reference_problem():
     assert list(c2.q_diag) == list(range(14)) and c2.qp.max_iter == 7
     with pytest.raises(ValueError):
         _lib.rollout6_default_config(r_diag=[1.0, 2.0])
+
+
+def test_cross3_is_np_cross_bitwise():
+    """rocket_6dof._cross3 (the dynamics' 3-vector cross product) forms np.cross's
+    products and differences in the same order: identical bits."""
+    from gp_mpc_rocket_landing_amd.dynamics.rocket_6dof import _cross3
+    rs = np.random.RandomState(0)
+    for _ in range(20000):
+        a = rs.randn(3) * 10 ** rs.uniform(-6, 6, 3)
+        b = rs.randn(3) * 10 ** rs.uniform(-6, 6, 3)
+        assert np.array_equal(np.cross(a, b), _cross3(a, b))
