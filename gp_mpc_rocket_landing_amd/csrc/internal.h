@@ -137,13 +137,15 @@ struct Stage {
   }
   void back(void *dst, size_t o, size_t b) {
     if (o < back_lo) back_lo = o;
-    backs[nback++] = Back{dst, o, b};
+    if (nback < (int)(sizeof(backs) / sizeof(backs[0]))) backs[nback] = Back{dst, o, b};
+    ++nback;  // (past the table: download() refuses)
   }
   hipError_t upload() {
     in_end = off;
     return off ? hipMemcpyAsync(d, h, off, hipMemcpyHostToDevice, s) : hipSuccess;
   }
   hipError_t download() {
+    if (nback > (int)(sizeof(backs) / sizeof(backs[0]))) return hipErrorInvalidValue;
     if (nback) {
       hipError_t e = hipMemcpyAsync(h + back_lo, d + back_lo, off - back_lo, hipMemcpyDeviceToHost, s);
       if (e != hipSuccess) return e;
