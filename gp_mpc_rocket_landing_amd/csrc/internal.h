@@ -106,18 +106,25 @@ struct Stage {
   struct Back { void *dst; size_t off, bytes; };
   hipStream_t s;
   char *h = nullptr, *d = nullptr;
-  size_t off = 0, in_end = 0, back_lo = (size_t)-1;
+  size_t off = 0, in_end = 0, back_lo = (size_t)-1, cap = 0;
+  bool bad = false;  // a buffer past the arena (the caller's byte count was short): upload() refuses
   Back backs[24];
   int nback = 0;
   static size_t pad(size_t b) { return (b + 255) & ~(size_t)255; }
   // bytes: the sum of pad(size) over every buffer the call stages
-  Stage(hipStream_t st, size_t bytes) : s(st) {
+  Stage(hipStream_t st, size_t bytes) : s(st), cap(bytes) {
     h = gpmpc_stage_host(s, bytes);
     d = (char *)gpmpc_scratch(s, 7, bytes);
+  }
+  bool fits(size_t b) {
+    if (off + pad(b) <= cap) return true;
+    bad = true;
+    return false;
   }
   bool ok() const { return h && d; }
   template <class T> T *in(const T *src, size_t n) {
     const size_t b = sizeof(T) * n;
+    if (!fits(b)) return (T *)d;
     if (b) memcpy(h + off, src, b);
     T *r = (T *)(d + off);
     off += pad(b);
@@ -126,11 +133,12 @@ struct Stage {
   template <class T> T *inout(T *src, size_t n) {
     const size_t o = off;
     T *r = in(src, n);
-    back(src, o, sizeof(T) * n);
+    if (!bad) back(src, o, sizeof(T) * n);
     return r;
   }
   template <class T> T *out(T *dst, size_t n) {
     const size_t o = off;
+    if (!fits(sizeof(T) * n)) return (T *)d;
     off += pad(sizeof(T) * n);
     back(dst, o, sizeof(T) * n);
     return (T *)(d + o);
@@ -141,11 +149,12 @@ struct Stage {
     ++nback;  // (past the table: download() refuses)
   }
   hipError_t upload() {
+    if (bad) return hipErrorInvalidValue;
     in_end = off;
     return off ? hipMemcpyAsync(d, h, off, hipMemcpyHostToDevice, s) : hipSuccess;
   }
   hipError_t download() {
-    if (nback > (int)(sizeof(backs) / sizeof(backs[0]))) return hipErrorInvalidValue;
+    if (bad || nback > (int)(sizeof(backs) / sizeof(backs[0]))) return hipErrorInvalidValue;
     if (nback) {
       hipError_t e = hipMemcpyAsync(h + back_lo, d + back_lo, off - back_lo, hipMemcpyDeviceToHost, s);
       if (e != hipSuccess) return e;
