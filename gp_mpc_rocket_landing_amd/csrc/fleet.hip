@@ -1563,6 +1563,7 @@ extern "C" int gpmpc_fleet_destroy(gpmpc_fleet *f) {
 // variances of all B N queries then come from the GP's own batched posterior, and one
 // launch propagates every covariance (k_cov_propagate).
 #define UP3_R 4  // training rows per thread held in registers (n <= 1024); larger n reads them per step
+#define UP_NCAP 256  // horizon steps whose controls the propagation kernels stage in LDS
 __global__ __launch_bounds__(256) void k_uprop3_means(GpView g, int N, double dt, double alpha, double g0,
                                                       double g1, double g2, const double *__restrict__ x0,
                                                       const double *__restrict__ U, double *__restrict__ Q,
@@ -1583,13 +1584,19 @@ __global__ __launch_bounds__(256) void k_uprop3_means(GpView g, int N, double dt
 #pragma unroll
     for (int c = 0; c < 3; ++c) ar[r][c] = ok ? g.alphaT[(int64_t)c * g.n + j] : 0.0;
   }
+  // the trajectory's controls staged in LDS once (up to UP_NCAP steps): no global
+  // round trip on the step chain
+  __shared__ double sU[UP_NCAP * NU];
+  const bool uc = N <= UP_NCAP;
+  for (int e = tid; uc && e < N * NU; e += 256) sU[e] = U[(int64_t)b * N * NU + e];
+  const double *Ub = uc ? sU : U + (int64_t)b * N * NU;
   if (tid < NX) {
     sx[tid] = x0[(int64_t)b * NX + tid];
     means[(int64_t)b * (N + 1) * NX + tid] = sx[tid];
   }
   __syncthreads();
   for (int k = 0; k < N; ++k) {
-    const double *u = U + ((int64_t)b * N + k) * NU;
+    const double *u = Ub + k * NU;
     if (tid == 0) {
       double z[NFEAT];
       features3(sx, u, z);

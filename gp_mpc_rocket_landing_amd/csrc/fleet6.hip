@@ -463,12 +463,13 @@ extern "C" int gpmpc_rollout6_destroy(gpmpc_rollout6 *r) {
 // normalisation (rocket_6dof.py step) plus dt d_v / dt d_w on the velocity / rate rows.
 // The variances of all B N queries then come from each GP's batched posterior, and one
 // launch propagates every covariance (k_cov_propagate).
+#define U6_NCAP 256  // horizon steps whose controls k_uprop6_means stages in LDS
 __global__ __launch_bounds__(256) void k_uprop6_means(GpView gv, GpView gw, R6Rocket rk, int N, double dt,
                                                       const double *__restrict__ x0, const double *__restrict__ U,
                                                       double *__restrict__ Qv, double *__restrict__ Qw,
                                                       double *__restrict__ A, double *__restrict__ means) {
   const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  __shared__ double sx[R6_NX], sxn[R6_NX], su[R6_NU], qv[13], qw[12], zv[13], zw[12], red[4][6];
+  __shared__ double sx[R6_NX], sxn[R6_NX], sug[R6_NU], qv[13], qw[12], zv[13], zw[12], red[4][6];
   __shared__ double blk[R6_NX * R6_SZ];
   // this thread's rows of each GP (row tid), held in registers for the N steps when both
   // GPs have at most 256 rows (FITC inducing sets); else read per step
@@ -487,14 +488,20 @@ __global__ __launch_bounds__(256) void k_uprop6_means(GpView gv, GpView gw, R6Ro
     nw = gw.Xn[tid];
     for (int c = 0; c < 3; ++c) aw[c] = gw.alphaT[(int64_t)c * gw.n + tid];
   }
+  // the trajectory's controls staged in LDS once (up to U6_NCAP steps): no global round
+  // trip on the step chain
+  __shared__ double sU[U6_NCAP * R6_NU];
+  const bool uc = N <= U6_NCAP;
+  for (int e = tid; uc && e < N * R6_NU; e += 256) sU[e] = U[(int64_t)b * N * R6_NU + e];
   if (tid < R6_NX) {
     sx[tid] = x0[(int64_t)b * R6_NX + tid];
     means[(int64_t)b * (N + 1) * R6_NX + tid] = sx[tid];
   }
-  if (tid < R6_NU && N > 0) su[tid] = U[(int64_t)b * N * R6_NU + tid];
+  if (!uc && tid < R6_NU && N > 0) sug[tid] = U[(int64_t)b * N * R6_NU + tid];
   __syncthreads();
   for (int k = 0; k < N; ++k) {
     const int64_t pk = (int64_t)b * N + k;
+    const double *su = uc ? sU + k * R6_NU : sug;
     // the raw features (six roles, six lanes), -[A_d | B_d] and the nominal RK4 step, side by side
     if (tid < R6_FEAT_ROLES) {
       const double one[13] = {1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1};
@@ -593,8 +600,8 @@ __global__ __launch_bounds__(256) void k_uprop6_means(GpView gv, GpView gw, R6Ro
         sx[i] = xn[i];
         means[((int64_t)b * (N + 1) + k + 1) * R6_NX + i] = xn[i];
       }
-    } else if (tid >= 1 && tid <= R6_NU && k + 1 < N) {
-      su[tid - 1] = U[(pk + 1) * R6_NU + tid - 1];  // the next step's controls
+    } else if (!uc && tid >= 1 && tid <= R6_NU && k + 1 < N) {
+      sug[tid - 1] = U[(pk + 1) * R6_NU + tid - 1];  // the next step's controls (long horizons)
     }
     __syncthreads();
   }

@@ -19,7 +19,10 @@
 
 #define UP_CHUNK 16
 
-__global__ __launch_bounds__(256) void k_cov_propagate(int N, int nx, const double *__restrict__ A,
+// NXC > 0: n_x known at compile time (7, 14): the dot products unrolled, their LDS reads in
+// flight together (same terms, same order: the same bits as the runtime-n_x form)
+template <int NXC>
+__global__ __launch_bounds__(256) void k_cov_propagate(int N, int nx_rt, const double *__restrict__ A,
                                                        const double *__restrict__ q,
                                                        const double *__restrict__ S0, double s0_diag,
                                                        double *__restrict__ out) {
@@ -27,6 +30,7 @@ __global__ __launch_bounds__(256) void k_cov_propagate(int N, int nx, const doub
   __shared__ double sq[UP_CHUNK][UP_NXMAX];
   __shared__ double sS[UP_NXMAX][UP_NXMAX + 1];
   __shared__ double sT[UP_NXMAX][UP_NXMAX + 1];
+  const int nx = NXC > 0 ? NXC : nx_rt;
   const int b = blockIdx.x, e = threadIdx.x, nt = blockDim.x, nn = nx * nx;
   const int64_t mat = (int64_t)nn;
   const bool act = e < nn;
@@ -53,13 +57,17 @@ __global__ __launch_bounds__(256) void k_cov_propagate(int N, int nx, const doub
     for (int kk = 0; kk < kc; ++kk) {
       if (act) {  // T = A Sigma
         double t = 0.0;
-        for (int c = 0; c < nx; ++c) t = fma(sA[kk][i][c], sS[c][j], t);
+#pragma unroll
+        for (int c = 0; c < (NXC > 0 ? NXC : UP_NXMAX); ++c)
+          if (NXC > 0 || c < nx) t = fma(sA[kk][i][c], sS[c][j], t);
         sT[i][j] = t;
       }
       __syncthreads();
       if (act) {  // Sigma' = T A^T + diag(q)
         double t = 0.0;
-        for (int c = 0; c < nx; ++c) t = fma(sT[i][c], sA[kk][j][c], t);
+#pragma unroll
+        for (int c = 0; c < (NXC > 0 ? NXC : UP_NXMAX); ++c)
+          if (NXC > 0 || c < nx) t = fma(sT[i][c], sA[kk][j][c], t);
         if (i == j) t += sq[kk][i];
         ob[(int64_t)(k0 + kk + 1) * mat + e] = t;
         sS[i][j] = t;
@@ -72,8 +80,10 @@ __global__ __launch_bounds__(256) void k_cov_propagate(int N, int nx, const doub
 static hipError_t launch_cov_propagate(hipStream_t s, int batch, int N, int nx, const double *A,
                                        const double *q, const double *S0, double s0_diag,
                                        double *out) {
-  hipLaunchKernelGGL(k_cov_propagate, dim3(batch), dim3((nx * nx + 63) / 64 * 64), 0, s, N, nx, A, q, S0, s0_diag,
-                     out);
+  const dim3 g(batch), t((nx * nx + 63) / 64 * 64);
+  if (nx == 7) hipLaunchKernelGGL(k_cov_propagate<7>, g, t, 0, s, N, nx, A, q, S0, s0_diag, out);
+  else if (nx == 14) hipLaunchKernelGGL(k_cov_propagate<14>, g, t, 0, s, N, nx, A, q, S0, s0_diag, out);
+  else hipLaunchKernelGGL(k_cov_propagate<0>, g, t, 0, s, N, nx, A, q, S0, s0_diag, out);
   return hipGetLastError();
 }
 
