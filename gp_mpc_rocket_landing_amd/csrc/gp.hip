@@ -696,8 +696,7 @@ static int core_posterior(gpmpc_ctx *ctx, const GpCore &g, const double *Ks, int
                      part.as<double>(), (int64_t)p, meanT.as<double>(), (int64_t)p,
                      g.ymean.as<double>(), g.ystd.as<double>(), g.sigma2, dmean, dvar);
   GPMPC_HIP(hipGetLastError());
-  GPMPC_HIP(hipStreamSynchronize(s));
-  return 0;
+  return 0;  // (stream-ordered: every caller reads the results after its own synchronisation)
 }
 
 // the posterior of p device-resident raw query rows (p x d): device mean / var (p x n_out)
