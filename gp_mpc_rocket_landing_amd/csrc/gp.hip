@@ -1148,11 +1148,78 @@ extern "C" int gpmpc_sparse_fit_prog(gpmpc_ctx *ctx, int method, const int *ops,
                     method == 0 ? lambda_diag : nullptr, method, &prog);
 }
 
+// FITC posterior for small inducing sets (m <= 256): one workgroup per query forms k*
+// (the k_scale_rows / k_gram arithmetic: same bits), v = L_uu^-1 k* over the lower triangle,
+// w = W2 k*, the mean alpha^T k* and the k_fitc_finish epilogue in one launch instead of five.
+// The sums |v|^2, |w|^2 and alpha^T k* run as a block reduction (another order than the
+// row-tile partials of the GEMM form: equal to ~1e-16 relative).
+#define FITC_SMALL_M 256
+#define FITC_SMALL_D 64
+#define FITC_SMALL_NO 8
+__global__ __launch_bounds__(256) void k_fitc_post_small(GpView g, int m, const double *__restrict__ W2,
+                                                         const double *__restrict__ Xq, double *__restrict__ mean,
+                                                         double *__restrict__ var) {
+  const int j = blockIdx.x, t = threadIdx.x, lane = t & 63, wave = t >> 6, d = g.d, no = g.n_out;
+  __shared__ double sz[FITC_SMALL_D], sk[FITC_SMALL_M], red[4][FITC_SMALL_NO + 2];
+  __shared__ double szn;
+  if (t < d) sz[t] = g.kind == GPMPC_SE_ISO ? Xq[(int64_t)j * d + t] : Xq[(int64_t)j * d + t] / g.ls[t];
+  __syncthreads();
+  if (t == 0) {
+    double q = 0.0;
+    for (int f = 0; f < d; ++f) q += sz[f] * sz[f];
+    szn = q;
+  }
+  __syncthreads();
+  if (t < m) {
+    double dot = 0.0;
+    for (int f = 0; f < d; ++f) dot = fma(sz[f], g.Xs[(int64_t)t * d + f], dot);
+    sk[t] = kernel_epilogue(g.kind, (szn + g.Xn[t]) - 2.0 * dot, g.sigma2, g.iso_scale);
+  }
+  __syncthreads();
+  double acc[FITC_SMALL_NO + 2];
+#pragma unroll
+  for (int c = 0; c < FITC_SMALL_NO + 2; ++c) acc[c] = 0.0;
+  if (t < m) {
+    const double *wr = g.W + (int64_t)t * m, *w2 = W2 + (int64_t)t * m;
+    double v = 0.0, w = 0.0;
+    for (int i = 0; i <= t; ++i) v = fma(wr[i], sk[i], v);
+    for (int i = 0; i < m; ++i) w = fma(w2[i], sk[i], w);
+    acc[0] = v * v;
+    acc[1] = w * w;
+    for (int c = 0; c < no; ++c) acc[2 + c] = g.alphaT[(int64_t)c * m + t] * sk[t];
+  }
+#pragma unroll
+  for (int c = 0; c < FITC_SMALL_NO + 2; ++c)
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) acc[c] += __shfl_xor(acc[c], o);
+  if (lane == 0)
+    for (int c = 0; c < FITC_SMALL_NO + 2; ++c) red[wave][c] = acc[c];
+  __syncthreads();
+  if (t < no) {
+    double r[2 + 1];
+    const int cs[3] = {0, 1, 2 + t};
+    for (int q = 0; q < 3; ++q) r[q] = ((red[0][cs[q]] + red[1][cs[q]]) + red[2][cs[q]]) + red[3][cs[q]];
+    double lat = g.sigma2 - r[0] + r[1];
+    lat = lat > 1e-10 ? lat : 1e-10;
+    mean[(int64_t)j * no + t] = r[2] * g.ystd[t] + g.ymean[t];
+    var[(int64_t)j * no + t] = lat * g.ystd[t] * g.ystd[t];
+  }
+}
+
 // the FITC posterior of p device-resident raw query rows (sparse_gp.py:255-305): mean / var (p x n_out)
 int fitc_posterior_dev(gpmpc_ctx *ctx, gpmpc_fitc *gp, const double *dq, int p, double *dmean, double *dvar) {
   hipStream_t s = ctx->stream;
   const GpCore &g = gp->core;
   const int m = gp->m;
+  // small inducing sets: one launch (GPMPC_FITC_SMALL=0: the GEMM form at every size)
+  const char *fs = getenv("GPMPC_FITC_SMALL");
+  if ((!fs || atoi(fs)) && m <= FITC_SMALL_M && g.d <= FITC_SMALL_D && g.n_out <= FITC_SMALL_NO &&
+      g.kind != GPMPC_KPROG) {
+    hipLaunchKernelGGL(k_fitc_post_small, dim3(p), dim3(256), 0, s, fitc_view(gp), m, gp->W2.as<double>(), dq,
+                       dmean, dvar);
+    GPMPC_HIP(hipGetLastError());
+    return 0;
+  }
   DevBuf Ks, pv, pw, meanT;
   int rc = core_cross(ctx, g, dq, p, Ks);  // K*u (p x m)
   if (rc) return rc;

@@ -421,3 +421,23 @@ def test_posterior_column_stationary_matches_oracle(gpu_ctx, monkeypatch, cs, n,
     for c in range(n_out):
         ok, w = close(m[:, c], mo[:, c], st["y_std"][c]); assert ok, ("mean", c, w)
         ok, w = close(v[:, c], vo[:, c], s2 * st["y_std"][c] ** 2); assert ok, ("var", c, w)
+
+
+@pytest.mark.parametrize("method,m", [("fitc", 50), ("vfe", 50), ("fitc", 256), ("fitc", 300)])
+def test_fitc_predict_small_inducing_set_one_launch(gpu_ctx, monkeypatch, method, m):
+    """The one-launch FITC / VFE posterior for m <= 256 inducing points (k_fitc_post_small)
+    against the five-launch GEMM form (GPMPC_FITC_SMALL=0) on the same handle: k* has the
+    same bits, the sums run in another order (1e-12 relative); m = 300 takes the GEMM form
+    either way."""
+    L = _lib()
+    rs = np.random.RandomState(m)
+    d, n = 11, 600
+    X = rs.randn(n, d); Y = np.stack([np.sin(X[:, 0]) + 0.1 * X[:, 1], np.cos(X[:, 2]), X[:, 3] * X[:, 4]], 1)
+    Z = X[rs.choice(n, m, replace=False)] + 1e-3 * rs.randn(m, d)
+    h = L.FITCHandle(gpu_ctx, Z, X, Y, np.linspace(0.8, 2.0, d), 1.3, 1e-3, method=method)
+    Xq = rs.randn(37, d)
+    mean1, var1 = h.predict(Xq)
+    monkeypatch.setenv("GPMPC_FITC_SMALL", "0")
+    mean0, var0 = h.predict(Xq)
+    np.testing.assert_allclose(mean1, mean0, rtol=1e-12, atol=1e-13)
+    np.testing.assert_allclose(var1, var0, rtol=1e-11, atol=1e-15)
