@@ -124,7 +124,24 @@ def launches(trace_csv, *keys):
             print(f"{n[:44]:44s} {grid:>16s} {_dur(r) / 1e3:10.1f} us")
 
 
-COMMANDS = dict(traffic=traffic, mfma=mfma, sum=sum_, top=top, kstats=kstats, timeline=timeline, launches=launches)
+def qpstamps(log):
+    """GPMPC_QP_STAMPS=1 stderr lines of k_qp_batched (problem 0's phase cycles), averaged."""
+    rows = [l.split() for l in open(log) if l.startswith("qp_stamps")]
+    it = [int(r[2].rstrip(":")) for r in rows]
+    v = [[int(x) for x in r[3:]] for r in rows]
+    n = len(rows)
+    m = [sum(c) / n for c in zip(*v)]
+    ni = sum(it) / n
+    print(f"{n} solves, iterations mean {ni:.2f} (min {min(it)}, max {max(it)})")
+    names = {1: "clip+scale", 2: "rho+factor", 3: "rhs", 8: "fwd chain (+diag if fused)", 9: "diag / fence",
+             10: "backward chain", 4: "post-solve barrier", 5: "z/y update", 6: "check/adapt", 7: "final"}
+    for k in [1, 2, 3, 8, 9, 10, 4, 5, 6, 7]:
+        print(f"{names[k]:28s} {m[k]:10.0f} cycles {m[k] / m[15] * 100:5.1f}%  per iteration {m[k] / ni:7.0f}")
+    print(f"total {m[15]:.0f} shader cycles, {m[14] / 100:.1f} us (100 MHz constant clock)")
+
+
+COMMANDS = dict(traffic=traffic, mfma=mfma, sum=sum_, top=top, kstats=kstats, timeline=timeline, launches=launches,
+                qpstamps=qpstamps)
 
 if __name__ == "__main__":
     if len(sys.argv) < 2 or sys.argv[1] not in COMMANDS:

@@ -17,6 +17,10 @@ through gpurun, alone or under scripts/profile.sh for a kernel trace / PMC pass)
   trsm                      trsm_lower / potrs at n = 128 and 1000, for a kernel trace
   rollouts6 [64,512]        bench.py's configs[4] rollouts leg (JSON)
   qp_sweep [B] [mi:eps,..]  configs[4] ADMM settings: status histogram and timing per setting
+  surface [reps] [prof]     bench.py's 3-DoF drop-in surface leg (JSON); prof: under cProfile
+  surface6 [reps] [prof]    bench.py's 14-state drop-in surface leg (JSON); prof: under cProfile
+                            (GPMPC_QP_STAMPS=1 beside either: k_qp_batched phase cycles on stderr,
+                            summarised by scripts/pmc.py qpstamps)
 """
 import json
 import os
@@ -418,9 +422,36 @@ def qp_sweep(B="64", settings="50:1e-4,100:1e-4,200:1e-4,400:1e-4,1000:1e-4,4000
                           "rollouts_per_s": round(B / el, 1), **st}), flush=True)
 
 
+def _surface(leg, reps, prof):
+    import bench
+    ctx = _lib.default_context()
+    fn = getattr(bench, leg)
+    if prof != "prof":
+        print(json.dumps(fn(ctx, reps=int(reps))), flush=True)
+        return
+    import cProfile
+    import pstats
+    fn(ctx, reps=1)  # warm
+    pr = cProfile.Profile()
+    pr.enable()
+    print(json.dumps(fn(ctx, reps=1)), flush=True)
+    pr.disable()
+    pstats.Stats(pr).sort_stats("tottime").print_stats(30)
+    pstats.Stats(pr).sort_stats("cumulative").print_stats(40)
+
+
+def surface(reps="2", prof=""):
+    _surface("surface_single_landing_bench", reps, prof)
+
+
+def surface6(reps="2", prof=""):
+    _surface("surface_gpmpc6_bench", reps, prof)
+
+
 COMMANDS = dict(single=single, step=step, stamps=stamps, placement=placement, streams=streams, fit=fit,
                 append=append, chol=chol, potrf=potrf, potrf_streams=potrf_streams, syrk_fitc=syrk_fitc,
-                gemm_loop=gemm_loop, trsm=trsm, rollouts6=rollouts6, qp_sweep=qp_sweep)
+                gemm_loop=gemm_loop, trsm=trsm, rollouts6=rollouts6, qp_sweep=qp_sweep, surface=surface,
+                surface6=surface6)
 
 if __name__ == "__main__":
     if len(sys.argv) < 2 or sys.argv[1] not in COMMANDS:

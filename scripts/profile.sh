@@ -4,6 +4,7 @@
 #   bash scripts/profile.sh TAG "PASSES" [-- command ...]
 # Passes (each under its own time limit; --pmc passes alone, counters per the guide's limits):
 #   tests      the GPU suite (PYTEST_ARGS: extra pytest arguments, e.g. -k EXPR or test files)
+#   surface    the two drop-in surface legs (probe.py surface / surface6) -> surface.json, surface6.json
 #   bench      the default bench line -> bench.json
 #   trace      --kernel-trace --stats of the bench's main workload (--no-chol)
 #   fulltrace  the same over the full bench (every leg)
@@ -34,6 +35,9 @@ for p in $PASSES; do
     tests) timeout -k 10 "${GT_TIMEOUT:-900}" python3 -u -m pytest -m gpu -x -v --timeout 300 \
              --timeout-method thread ${PYTEST_ARGS:-tests} > "$OUT/tests.log" 2>&1
            tail -3 "$OUT/tests.log" ;;
+    surface) timeout -k 10 300 python3 scripts/probe.py surface > "$OUT/surface.json" 2>"$OUT/surface.err"
+           timeout -k 10 300 python3 scripts/probe.py surface6 > "$OUT/surface6.json" 2>"$OUT/surface6.err"
+           cat "$OUT/surface.json" "$OUT/surface6.json" ;;
     bench) timeout -k 10 360 python3 bench.py > "$OUT/bench.log" 2>&1
            grep '^{' "$OUT/bench.log" | tail -1 > "$OUT/bench.json" ;;
     trace) prof 300 trace --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run -- \
